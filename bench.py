@@ -1,0 +1,229 @@
+"""Benchmark: HLL addAll of 16-byte keys (+ count) on MI355X, BASELINE configs[1].
+
+Step = RHyperLogLog.addAll(n synthetic 16-byte keys already resident in HBM)
+       + (N > 1) RCCL MAX all-reduce of the 16384 registers + count().
+The keys are the SURVEY.md 8d C2 stream (splitmix64, seed 0x5EED0002), each
+rank taking its own contiguous range (weak scaling: n keys per GPU).
+Secondary fields report the C3 Bloom filter (1B inserts at 1% FPP, EXTENDED
+mode, then 1B contains queries) on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--keys N_PER_GPU]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SEED_C2, SEED_C3, SEED_Q = 0x5EED0002, 0x5EED0003, 0x5EED0004
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(kernel: str, keys_per_launch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (null if absent)."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and k.get("keys_per_launch") == keys_per_launch and k.get("hbm_bytes_per_launch"):
+            best = k["hbm_bytes_per_launch"]
+    return best
+
+
+def cpu_baseline(sample_keys: int, passes: int):
+    """The oracle's restatement of Redis PFADD (hllPatLen + register max), one
+    core, over a pre-generated in-memory sample of the same C2 stream."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    keys = O.gen_keys16(SEED_C2, 0, sample_keys)
+    regs = np.zeros(O.REGISTERS, np.uint8)
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        O.hll_add(regs, keys, None, 16, sample_keys)
+    dt = time.perf_counter() - t0
+    return {"value": sample_keys * passes / dt, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": "%d passes over %d C2 16-byte keys (%.1f s, oracle/rsk_oracle.c orc_hll_add_raw, "
+                      "Redis 3.2.0 PFADD arithmetic, 1 thread)" % (passes, sample_keys, dt)}
+
+
+def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
+    import torch
+
+    from redisson_amd import KeyBatch, _lib
+
+    L = _lib.load()
+    size = ctypes.c_int64()
+    k = ctypes.c_int32()
+    _lib.check(L.rsk_bloom_params(n_ins, 0.01, _lib.RSK_BLOOM_EXTENDED, ctypes.byref(size), ctypes.byref(k)))
+    ins = torch.empty((n_ins, 16), dtype=torch.uint8, device="cuda")
+    qs = torch.empty((n_q, 16), dtype=torch.uint8, device="cuda")
+    _lib.check(L.rsk_gen_keys16(engine.ctx, SEED_C3, 0, n_ins, ins.data_ptr()))
+    _lib.check(L.rsk_gen_queries16(engine.ctx, SEED_Q, SEED_C3, n_ins, 0, n_q, qs.data_ptr()))
+    out = torch.empty(n_q, dtype=torch.uint8, device="cuda")
+    ki = KeyBatch.from_torch(ins).as_struct()
+    kq = KeyBatch.from_torch(qs).as_struct()
+    add_t, con_t = [], []
+    for r in range(reps + 1):
+        b = ctypes.c_void_p()
+        _lib.check(L.rsk_bloom_create(engine.ctx, size.value, k.value, ctypes.byref(b)))
+        engine.sync()
+        t0 = time.perf_counter()
+        _lib.check(L.rsk_bloom_add(b, ctypes.byref(ki), None))
+        engine.sync()
+        t1 = time.perf_counter()
+        _lib.check(L.rsk_bloom_contains(b, ctypes.byref(kq), out.data_ptr()))
+        engine.sync()
+        t2 = time.perf_counter()
+        if r:
+            add_t.append(t1 - t0)
+            con_t.append(t2 - t1)
+        if r == reps:
+            hits = int(out.sum().item())
+        L.rsk_bloom_destroy(b)
+    add_s, con_s = min(add_t), min(con_t)
+    return {"config": "C3: %d inserts @1%% FPP (size %d bits, k=%d, EXTENDED), %d contains (50%% inserted)"
+                      % (n_ins, size.value, k.value, n_q),
+            "insert_keys_per_s": n_ins / add_s, "contains_keys_per_s": n_q / con_s,
+            "insert_ms": add_s * 1e3, "contains_ms": con_s * 1e3, "contains_true": hits,
+            "insert_bit_rmw_per_s": n_ins * k.value / add_s, "contains_probe_gathers_per_s": n_q * (k.value - 1) / con_s}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--keys", type=int, default=1_000_000_000, help="16-byte keys per GPU")
+    ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
+    ap.add_argument("--no-bloom", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=128 << 20)
+    ap.add_argument("--cpu-passes", type=int, default=4)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from redisson_amd import Engine, KeyBatch, Redisson, _lib
+    from redisson_amd.client import Config
+
+    L = _lib.load()
+    client = Redisson.create(Config(device=local))
+    engine = client.engine
+    n = args.keys
+
+    # Inputs resident in HBM before the timed region (generation untimed).
+    keys = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    _lib.check(L.rsk_gen_keys16(engine.ctx, SEED_C2, rank * n, n, keys.data_ptr()))
+    kb = KeyBatch.from_torch(keys)
+    hll = client.getHyperLogLog("bench")
+    regs_t = torch.empty(16384, dtype=torch.uint8, device="cuda")
+
+    def step():
+        hll.addAll(kb)
+        if world > 1:
+            slot = client._hll_slot("bench", False)
+            _lib.check(L.rsk_hll_get_registers(slot.pool, slot.id, regs_t.data_ptr(), _lib.RSK_MEM_DEVICE))
+            dist.all_reduce(regs_t, op=dist.ReduceOp.MAX)  # RCCL over xGMI
+            torch.cuda.current_stream().synchronize()
+            _lib.check(L.rsk_hll_merge_raw(slot.pool, slot.id, regs_t.data_ptr(), _lib.RSK_MEM_DEVICE))
+        return hll.count()
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        engine.sync()
+
+    engine.prof_reset()
+    engine.prof_enable(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        card = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    engine.prof_enable(False)
+    add_ms, add_launches = engine.prof_read("hll_add16")
+    red_ms, red_launches = engine.prof_read("hll_reduce")
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_keys = n * world * args.steps
+    value = total_keys / elapsed
+    avg_launch_s = (add_ms / 1e3) / max(1, add_launches)
+    achieved = 16.0 * n / avg_launch_s / 1e9  # algorithmic bytes per launch / launch time
+    result = {
+        "metric": "HLL adds/s + Bloom lookups/s (node), % HBM roofline, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "keys/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (splitmix64 C2 stream generated on device, untimed)",
+        "config": {"workload": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
+                   "keys_per_gpu": n, "key_bytes": 16, "global_keys_per_step": n * world,
+                   "parallelism": "key-stream sharding, RCCL MAX all-reduce of 16 KiB registers" if world > 1
+                   else "single GPU", "redis_semantics": "3.2.0"},
+        "roofline": {"bound": "hbm", "kernel": "hll_add16_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic("hll_add16_kernel", n),
+                     "avg_launch_ms": avg_launch_s * 1e3, "launches": add_launches,
+                     "reduce_avg_ms": red_ms / max(1, red_launches),
+                     "algorithmic_bytes_per_launch": 16 * n},
+        "count": int(card),
+    }
+    if rank == 0 and world == 1 and not args.no_bloom:
+        bn = args.bloom_keys
+        del keys, kb
+        torch.cuda.empty_cache()
+        result["bloom"] = bloom_bench(engine, bn, bn, reps=2)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes)
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    client.shutdown()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

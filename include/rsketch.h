@@ -1,0 +1,201 @@
+/*
+ * rsketch.h -- C ABI of librsketch.so, the MI355X (gfx950) sketch engine
+ * behind Redisson's RHyperLogLog / RBloomFilter / RBitSet.
+ *
+ * The reference (alexs20/redisson, Redisson 2.2.17) has no native layer: its
+ * operator interface for this path is the Java object API, which today sends
+ * PFADD/PFCOUNT/PFMERGE/SETBIT/GETBIT/BITCOUNT to a Redis server.  Each entry
+ * point below replaces one of those Java methods (cited file:line, paths
+ * relative to src/main/java/org/redisson/) and is what a JNI shim binds
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every function returns an rsk_status; details via rsk_last_error()
+ *    (thread-local).  Status codes map 1:1 to the Java exceptions the
+ *    reference raises (see enum).  No C++ exception crosses this boundary.
+ *  - The caller owns all buffers passed in.  Key buffers live either in host
+ *    memory (RSK_MEM_HOST; copied over PCIe through a staging ring) or in
+ *    device memory of the context's GPU (RSK_MEM_DEVICE; read in place).
+ *  - The library owns device state behind opaque handles.  Calls on one
+ *    context are serialised on that context's HIP stream; results written to
+ *    host pointers are complete when the call returns.
+ *  - HLL semantics are Redis 3.2.0's (the version the reference CI pins,
+ *    .travis.yml:24): 16384 six-bit registers, MurmurHash64A seed
+ *    0xadc83b19, rank in [1,50], the 3.2.0 estimator.
+ */
+#ifndef RSKETCH_H
+#define RSKETCH_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSK_ABI_VERSION 1
+#define RSK_HLL_REGISTERS 16384
+#define RSK_HLL_DENSE_BYTES 12304 /* 16-byte "HYLL" header + 12288 register bytes */
+
+typedef enum rsk_status {
+  RSK_OK = 0,
+  RSK_ERR_INVALID_ARG = 1,     /* IllegalArgumentException (RedissonBloomFilter.java:175,227) */
+  RSK_ERR_NOT_INITIALIZED = 2, /* IllegalStateException "Bloom filter is not initialized!" (:217,:284) */
+  RSK_ERR_WRONGTYPE = 3,       /* RedisException -WRONGTYPE (CommandDecoder.java:239-243) */
+  RSK_ERR_INVALID_HLL = 4,     /* RedisException -INVALIDOBJ Corrupted HLL object */
+  RSK_ERR_DEVICE = 5,          /* HIP runtime / kernel failure */
+  RSK_ERR_OUT_OF_MEMORY = 6,   /* device allocation failed */
+  RSK_ERR_NO_DEVICE = 7        /* no gfx950 device visible */
+} rsk_status;
+
+typedef enum rsk_mem { RSK_MEM_HOST = 0, RSK_MEM_DEVICE = 1 } rsk_mem;
+
+typedef struct rsk_ctx rsk_ctx;
+typedef struct rsk_hll rsk_hll;
+typedef struct rsk_bloom rsk_bloom;
+
+typedef struct rsk_options {
+  int32_t device;         /* HIP device ordinal (one process per GPU) */
+  int32_t redis_version;  /* 320 = Redis 3.2.0 semantics (only supported value) */
+  uint64_t staging_bytes; /* host->device staging ring size; 0 = default (256 MiB) */
+} rsk_options;
+
+/* A batch of keys: fixed stride (offsets == NULL, each key fixed_len bytes)
+ * or a blob with n+1 byte offsets (key i = data[offsets[i] .. offsets[i+1])).
+ * data and offsets share one location.  These are the codec-encoded element
+ * bytes (CommandEncoder.java:77-79 / RedissonBloomFilter.java:170-178). */
+typedef struct rsk_keys {
+  const void *data;
+  const uint64_t *offsets;
+  uint64_t n;
+  uint32_t fixed_len;
+  uint32_t location; /* rsk_mem */
+} rsk_keys;
+
+/* ---------------------------------------------------------------- context */
+int rsk_init(const rsk_options *opts, rsk_ctx **out);
+int rsk_shutdown(rsk_ctx *ctx);
+const char *rsk_last_error(void);
+int rsk_abi_version(void);
+/* The HIP stream (hipStream_t) every call on this context is ordered on. */
+void *rsk_ctx_stream(rsk_ctx *ctx);
+int rsk_sync(rsk_ctx *ctx);
+/* Per-kernel device-time accounting with HIP events on the context stream
+ * (used by bench.py for the roofline; off by default). */
+int rsk_prof_enable(rsk_ctx *ctx, int on);
+int rsk_prof_reset(rsk_ctx *ctx);
+/* Accumulated milliseconds and launch count of kernel `name` since reset. */
+int rsk_prof_read(rsk_ctx *ctx, const char *name, double *ms, uint64_t *launches);
+
+/* ------------------------------------------------------------ HyperLogLog */
+/* A pool of n_sketches HLL keys (n_sketches = 1 for RHyperLogLog; 1e6 for
+ * the grouped COUNT DISTINCT config).  Sketches start absent (no key). */
+int rsk_hll_create(rsk_ctx *ctx, uint64_t n_sketches, rsk_hll **out);
+int rsk_hll_destroy(rsk_hll *h);
+uint64_t rsk_hll_size(const rsk_hll *h);
+/* 1 if the sketch exists (was created by add/merge/import), else 0. */
+int rsk_hll_exists(rsk_hll *h, uint64_t id, int *out);
+/* DEL: RedissonObject.deleteAsync (RedissonObject.java:117-119). */
+int rsk_hll_delete(rsk_hll *h, uint64_t id);
+
+/* PFADD id e1..en -- RedissonHyperLogLog.addAll/addAllAsync (:46-48,:70-76)
+ * with the INTENDED semantics (the fork's varargs bug is not reproduced, see
+ * DESIGN.md).  *changed_out (may be NULL) = 1 iff any register grew or the
+ * key was created: BooleanReplayConvertor (BooleanReplayConvertor.java:20-26). */
+int rsk_hll_add(rsk_hll *h, uint64_t id, const rsk_keys *keys, uint8_t *changed_out);
+
+/* One PFADD per element, in input order -- RedissonHyperLogLog.add (:40-43)
+ * issued n times (e.g. pipelined in an RBatch, RedissonBatch.java:76-83).
+ * out[i] = the reply of the i-th PFADD. */
+int rsk_hll_add_each(rsk_hll *h, uint64_t id, const rsk_keys *keys, uint8_t *out);
+
+/* Grouped PFADD: element i goes to sketch groups[i] (group ids in the same
+ * location as the keys).  Grouped COUNT DISTINCT (BASELINE config 5). */
+int rsk_hll_add_grouped(rsk_hll *h, const rsk_keys *keys, const uint32_t *groups);
+
+/* PFCOUNT id -- RedissonHyperLogLog.count/countAsync (:50-53,:78-81), for
+ * n ids at once; out is a host array of n uint64.  Honours and refreshes the
+ * per-key cardinality cache exactly like pfcountCommand. */
+int rsk_hll_count(rsk_hll *h, const uint64_t *ids, uint64_t n, uint64_t *out);
+
+/* PFCOUNT k1..kk (k >= 2 keys may repeat, pools may differ) --
+ * RedissonHyperLogLog.countWith/countWithAsync (:55-58,:83-89). */
+int rsk_hll_count_union(rsk_hll *const *hs, const uint64_t *ids, uint32_t k, uint64_t *out);
+/* Batched countWith: n unions of `arity` members each, all in pool h;
+ * member_ids is [n][arity] (host); out is [n]. */
+int rsk_hll_count_union_batch(rsk_hll *h, const uint64_t *member_ids, uint32_t arity, uint64_t n,
+                              uint64_t *out);
+
+/* PFMERGE dst src1..srck (dst included in the max) --
+ * RedissonHyperLogLog.mergeWith/mergeWithAsync (:60-63,:91-97). */
+int rsk_hll_merge(rsk_hll *dst, uint64_t dst_id, rsk_hll *const *srcs, const uint64_t *src_ids, uint32_t k);
+/* Batched mergeWith within one pool: for i < n, PFMERGE dst_ids[i] src_ids[i]. */
+int rsk_hll_merge_batch(rsk_hll *h, const uint64_t *dst_ids, const uint64_t *src_ids, uint64_t n);
+
+/* PFMERGE from raw registers (one byte per register, any location): the
+ * receive side of the multi-GPU RCCL MAX merge. */
+int rsk_hll_merge_raw(rsk_hll *h, uint64_t id, const uint8_t *regs, uint32_t location);
+/* Raw registers out (host or device destination, 16384 bytes). */
+int rsk_hll_get_registers(rsk_hll *h, uint64_t id, uint8_t *out, uint32_t location);
+/* Device pointer of the [n_sketches][16384] register array (for RCCL). */
+void *rsk_hll_device_registers(rsk_hll *h);
+
+/* GET of the key as a Redis dense "HYLL" string (12304 bytes; card bytes as
+ * Redis would hold them).  RBitSet.toByteArray-style export. */
+int rsk_hll_export_redis(rsk_hll *h, uint64_t id, uint8_t *buf, size_t cap, size_t *len);
+/* SET of a Redis HLL string (dense or sparse); validated like
+ * isHLLObjectOrReply / hllMerge.  Replaces the key. */
+int rsk_hll_import_redis(rsk_hll *h, uint64_t id, const uint8_t *buf, size_t len);
+
+/* ---------------------------------------------------------- Bloom filter */
+typedef enum rsk_bloom_mode {
+  RSK_BLOOM_COMPAT = 0,  /* size <= 2*Integer.MAX_VALUE (RedissonBloomFilter.java:52,226-227) */
+  RSK_BLOOM_EXTENDED = 1 /* larger filters (1B @ 1% = 9,585,058,377 bits) */
+} rsk_bloom_mode;
+
+/* tryInit sizing (optimalNumOfBits / optimalNumOfHashFunctions,
+ * RedissonBloomFilter.java:69-78,223-229) without allocating. */
+int rsk_bloom_params(int64_t expected_insertions, double false_probability, uint32_t mode,
+                     int64_t *size_out, int32_t *k_out);
+/* Allocate a zeroed filter of explicit size/k (the {name}__config values). */
+int rsk_bloom_create(rsk_ctx *ctx, int64_t size, int32_t k, rsk_bloom **out);
+/* tryInit(n, p): params + create. */
+int rsk_bloom_init(rsk_ctx *ctx, int64_t expected_insertions, double false_probability, uint32_t mode,
+                   rsk_bloom **out, int64_t *size_out, int32_t *k_out);
+int rsk_bloom_destroy(rsk_bloom *b);
+int rsk_bloom_info(const rsk_bloom *b, int64_t *size, int32_t *k);
+/* add(obj) for n objects in input order (RedissonBloomFilter.java:80-114).
+ * added_out (host, may be NULL) gets each add's reply: 1 iff one of the
+ * first k-1 SETBITs found its bit clear, exactly as if the adds ran one by
+ * one in input order. */
+int rsk_bloom_add(rsk_bloom *b, const rsk_keys *keys, uint8_t *added_out);
+/* contains(obj) for n objects (RedissonBloomFilter.java:133-168): 1 iff the
+ * first k-1 bits are all set.  out is a host array of n bytes. */
+int rsk_bloom_contains(rsk_bloom *b, const rsk_keys *keys, uint8_t *out);
+/* count() (RedissonBloomFilter.java:188-199) and the BITCOUNT it uses. */
+int rsk_bloom_count(rsk_bloom *b, int32_t *out);
+int rsk_bloom_bitcount(rsk_bloom *b, uint64_t *out);
+/* The bit string as Redis holds it (MSB-first, ceil(size/8) bytes). */
+int rsk_bloom_export_bits(rsk_bloom *b, uint8_t *buf, size_t cap, size_t *len);
+int rsk_bloom_import_bits(rsk_bloom *b, const uint8_t *buf, size_t len);
+/* OR raw bitset bytes (any location, ceil(size/8) bytes) into the filter:
+ * the receive side of the multi-GPU slice-OR merge. */
+int rsk_bloom_or_bits(rsk_bloom *b, const uint8_t *bits, size_t len, uint32_t location);
+void *rsk_bloom_device_bits(rsk_bloom *b);
+
+/* ----------------------------------------------- synthetic input streams */
+/* SURVEY 8d generators, run on the device into caller-provided device
+ * buffers (bench and parity tests; outside the timed region). */
+int rsk_gen_keys16(rsk_ctx *ctx, uint64_t seed, uint64_t start, uint64_t n, void *dev_out);
+int rsk_gen_grouped(rsk_ctx *ctx, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t *dev_groups,
+                    void *dev_keys);
+int rsk_gen_queries16(rsk_ctx *ctx, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
+                      void *dev_out);
+/* Variable-length keys: lengths first (dev_offsets gets n+1 offsets), then
+ * bytes into dev_blob (capacity blob_cap). */
+int rsk_gen_varlen(rsk_ctx *ctx, uint64_t seed, uint64_t start, uint64_t n, uint64_t *dev_offsets, void *dev_blob,
+                   uint64_t blob_cap, uint64_t *total_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSKETCH_H */

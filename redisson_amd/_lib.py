@@ -1,0 +1,202 @@
+"""ctypes binding of librsketch.so (include/rsketch.h).
+
+The HIP library is the only compute path: importing this module without the
+built library, or creating an Engine without a gfx950 device, raises.  There
+is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RSKETCH_LIB", os.path.join(HERE, "librsketch.so"))
+
+RSK_OK = 0
+RSK_ERR_INVALID_ARG = 1
+RSK_ERR_NOT_INITIALIZED = 2
+RSK_ERR_WRONGTYPE = 3
+RSK_ERR_INVALID_HLL = 4
+RSK_ERR_DEVICE = 5
+RSK_ERR_OUT_OF_MEMORY = 6
+RSK_ERR_NO_DEVICE = 7
+
+RSK_MEM_HOST = 0
+RSK_MEM_DEVICE = 1
+RSK_BLOOM_COMPAT = 0
+RSK_BLOOM_EXTENDED = 1
+HLL_REGISTERS = 16384
+HLL_DENSE_BYTES = 12304
+
+
+class RedissonError(Exception):
+    """Base of the errors surfaced by the engine."""
+
+
+class IllegalArgumentException(RedissonError, ValueError):
+    """java.lang.IllegalArgumentException (RedissonBloomFilter.java:175,227)."""
+
+
+class IllegalStateException(RedissonError, RuntimeError):
+    """java.lang.IllegalStateException (RedissonBloomFilter.java:217,284)."""
+
+
+class RedisException(RedissonError):
+    """org.redisson.client.RedisException (-WRONGTYPE / -INVALIDOBJ replies)."""
+
+
+class EngineError(RedissonError, RuntimeError):
+    """HIP runtime, device-memory or no-device failure."""
+
+
+_STATUS_EXC = {
+    RSK_ERR_INVALID_ARG: IllegalArgumentException,
+    RSK_ERR_NOT_INITIALIZED: IllegalStateException,
+    RSK_ERR_WRONGTYPE: RedisException,
+    RSK_ERR_INVALID_HLL: RedisException,
+    RSK_ERR_DEVICE: EngineError,
+    RSK_ERR_OUT_OF_MEMORY: EngineError,
+    RSK_ERR_NO_DEVICE: EngineError,
+}
+
+
+class rsk_options(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("redis_version", ctypes.c_int32), ("staging_bytes", ctypes.c_uint64)]
+
+
+class rsk_keys(ctypes.Structure):
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("offsets", ctypes.c_void_p),
+        ("n", ctypes.c_uint64),
+        ("fixed_len", ctypes.c_uint32),
+        ("location", ctypes.c_uint32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/rsketch.h.
+_vp, _u64, _u32, _i32, _i64, _sz = (ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32,
+                                    ctypes.c_int64, ctypes.c_size_t)
+_P = ctypes.POINTER
+SIGNATURES = {
+    "rsk_init": (ctypes.c_int, [_P(rsk_options), _P(_vp)]),
+    "rsk_shutdown": (ctypes.c_int, [_vp]),
+    "rsk_last_error": (ctypes.c_char_p, []),
+    "rsk_abi_version": (ctypes.c_int, []),
+    "rsk_ctx_stream": (_vp, [_vp]),
+    "rsk_sync": (ctypes.c_int, [_vp]),
+    "rsk_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rsk_prof_reset": (ctypes.c_int, [_vp]),
+    "rsk_prof_read": (ctypes.c_int, [_vp, ctypes.c_char_p, _P(ctypes.c_double), _P(_u64)]),
+    "rsk_hll_create": (ctypes.c_int, [_vp, _u64, _P(_vp)]),
+    "rsk_hll_destroy": (ctypes.c_int, [_vp]),
+    "rsk_hll_size": (_u64, [_vp]),
+    "rsk_hll_exists": (ctypes.c_int, [_vp, _u64, _P(ctypes.c_int)]),
+    "rsk_hll_delete": (ctypes.c_int, [_vp, _u64]),
+    "rsk_hll_add": (ctypes.c_int, [_vp, _u64, _P(rsk_keys), _vp]),
+    "rsk_hll_add_each": (ctypes.c_int, [_vp, _u64, _P(rsk_keys), _vp]),
+    "rsk_hll_add_grouped": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
+    "rsk_hll_count": (ctypes.c_int, [_vp, _vp, _u64, _vp]),
+    "rsk_hll_count_union": (ctypes.c_int, [_vp, _vp, _u32, _vp]),
+    "rsk_hll_count_union_batch": (ctypes.c_int, [_vp, _vp, _u32, _u64, _vp]),
+    "rsk_hll_merge": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u32]),
+    "rsk_hll_merge_batch": (ctypes.c_int, [_vp, _vp, _vp, _u64]),
+    "rsk_hll_merge_raw": (ctypes.c_int, [_vp, _u64, _vp, _u32]),
+    "rsk_hll_get_registers": (ctypes.c_int, [_vp, _u64, _vp, _u32]),
+    "rsk_hll_device_registers": (_vp, [_vp]),
+    "rsk_hll_export_redis": (ctypes.c_int, [_vp, _u64, _vp, _sz, _P(_sz)]),
+    "rsk_hll_import_redis": (ctypes.c_int, [_vp, _u64, _vp, _sz]),
+    "rsk_bloom_params": (ctypes.c_int, [_i64, ctypes.c_double, _u32, _P(_i64), _P(_i32)]),
+    "rsk_bloom_create": (ctypes.c_int, [_vp, _i64, _i32, _P(_vp)]),
+    "rsk_bloom_init": (ctypes.c_int, [_vp, _i64, ctypes.c_double, _u32, _P(_vp), _P(_i64), _P(_i32)]),
+    "rsk_bloom_destroy": (ctypes.c_int, [_vp]),
+    "rsk_bloom_info": (ctypes.c_int, [_vp, _P(_i64), _P(_i32)]),
+    "rsk_bloom_add": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
+    "rsk_bloom_contains": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
+    "rsk_bloom_count": (ctypes.c_int, [_vp, _P(_i32)]),
+    "rsk_bloom_bitcount": (ctypes.c_int, [_vp, _P(_u64)]),
+    "rsk_bloom_export_bits": (ctypes.c_int, [_vp, _vp, _sz, _P(_sz)]),
+    "rsk_bloom_import_bits": (ctypes.c_int, [_vp, _vp, _sz]),
+    "rsk_bloom_or_bits": (ctypes.c_int, [_vp, _vp, _sz, _u32]),
+    "rsk_bloom_device_bits": (_vp, [_vp]),
+    "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
+    "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
+    "rsk_gen_queries16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
+    "rsk_gen_varlen": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp, _vp, _u64, _P(_u64)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load librsketch.so; raises if it has not been built (no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    "librsketch.so not found at %s: build it with `make` (or __graft_entry__.build()). "
+                    "redisson_amd has no CPU fallback." % LIB_PATH)
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != RSK_OK:
+        msg = load().rsk_last_error().decode(errors="replace")
+        exc = _STATUS_EXC.get(rc, EngineError)
+        raise exc(msg if not what else "%s: %s" % (what, msg))
+
+
+class Engine:
+    """One rsk_ctx: a HIP stream and scratch on one GPU (one process per GPU)."""
+
+    _engines: dict = {}
+    _elock = threading.Lock()
+
+    def __init__(self, device: int = 0, staging_bytes: int = 0):
+        L = load()
+        opts = rsk_options(device, 320, staging_bytes)
+        h = ctypes.c_void_p()
+        check(L.rsk_init(ctypes.byref(opts), ctypes.byref(h)), "rsk_init")
+        self.ctx = h
+        self.device = device
+        self.lib = L
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Engine":
+        with cls._elock:
+            e = cls._engines.get(device)
+            if e is None:
+                e = cls._engines[device] = Engine(device)
+            return e
+
+    def stream(self) -> int:
+        return self.lib.rsk_ctx_stream(self.ctx)
+
+    def sync(self):
+        check(self.lib.rsk_sync(self.ctx))
+
+    def prof_enable(self, on=True):
+        check(self.lib.rsk_prof_enable(self.ctx, 1 if on else 0))
+
+    def prof_reset(self):
+        check(self.lib.rsk_prof_reset(self.ctx))
+
+    def prof_read(self, name: str):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        check(self.lib.rsk_prof_read(self.ctx, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def close(self):
+        if self.ctx:
+            self.lib.rsk_shutdown(self.ctx)
+            self.ctx = None

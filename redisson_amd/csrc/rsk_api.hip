@@ -1,0 +1,1033 @@
+// rsk_api.hip -- the C ABI of librsketch.so (include/rsketch.h).
+//
+// Host-side state machine of the Redis commands the reference issues for
+// this path (key existence, the HLL cardinality cache, Bloom sizing with
+// Java double semantics), plus staging of host key batches and error
+// mapping.  All arithmetic on keys runs in the HIP kernels of rsk_hll.hip /
+// rsk_bloom.hip; nothing here hashes a key.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+
+#include "rsk_internal.h"
+
+using rsk::DevKeys;
+using rsk::RskError;
+
+namespace rsk {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+template <class F>
+static int guarded(F&& fn) {
+  try {
+    fn();
+    g_last_error.clear();
+    return RSK_OK;
+  } catch (const RskError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return RSK_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return RSK_ERR_DEVICE;
+  }
+}
+
+[[noreturn]] static void fail(int code, const std::string& msg) { throw RskError{code, msg}; }
+
+void prof_begin(rsk_ctx* c, const char*, hipEvent_t* a, hipEvent_t* b) {
+  if (!c->prof.on) return;
+  for (hipEvent_t* e : {a, b}) {
+    if (!c->prof.free_events.empty()) {
+      *e = c->prof.free_events.back();
+      c->prof.free_events.pop_back();
+    } else if (hipEventCreate(e) != hipSuccess) {
+      *e = nullptr;
+    }
+  }
+  if (*a) (void)hipEventRecord(*a, c->stream);
+}
+
+void prof_end(rsk_ctx* c, const char* name, hipEvent_t a, hipEvent_t b) {
+  if (!c->prof.on || !a || !b) return;
+  (void)hipEventRecord(b, c->stream);
+  c->prof.pending.push_back({name, a, b});
+}
+
+static void prof_fold(rsk_ctx* c) {
+  for (auto& p : c->prof.pending) {
+    float ms = 0;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      auto& e = c->prof.totals[p.name];
+      e.ms += ms;
+      e.launches += 1;
+    }
+    c->prof.free_events.push_back(p.a);
+    c->prof.free_events.push_back(p.b);
+  }
+  c->prof.pending.clear();
+}
+
+}  // namespace rsk
+
+uint8_t* rsk_ctx::work(uint64_t bytes) {
+  if (bytes > work_bytes) {
+    if (d_work) {
+      RSK_HIP(hipStreamSynchronize(stream));
+      RSK_HIP(hipFree(d_work));
+      d_work = nullptr;
+      work_bytes = 0;
+    }
+    uint64_t sz = std::max<uint64_t>(bytes, 64ull << 20);
+    RSK_HIP(hipMalloc(&d_work, sz));
+    work_bytes = sz;
+  }
+  return d_work;
+}
+
+namespace {
+
+using namespace rsk;
+
+struct CtxLock {
+  std::lock_guard<std::recursive_mutex> g;
+  explicit CtxLock(rsk_ctx* c) : g(c->mu) {
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) fail(RSK_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+};
+
+void need(bool cond, const char* msg) {
+  if (!cond) fail(RSK_ERR_INVALID_ARG, msg);
+}
+
+// Device output scratch that is distinct from ctx->work (used inside
+// algorithms).  Kept per context, grown on demand.
+struct OutScratch {
+  uint8_t* p = nullptr;
+  uint64_t bytes = 0;
+};
+thread_local std::map<rsk_ctx*, OutScratch> g_out;
+
+uint8_t* out_scratch(rsk_ctx* c, uint64_t bytes) {
+  OutScratch& s = g_out[c];
+  if (bytes > s.bytes) {
+    if (s.p) {
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      RSK_HIP(hipFree(s.p));
+      s.p = nullptr;
+      s.bytes = 0;
+    }
+    uint64_t sz = std::max<uint64_t>(bytes, 16ull << 20);
+    RSK_HIP(hipMalloc(&s.p, sz));
+    s.bytes = sz;
+  }
+  return s.p;
+}
+
+void ensure_stage(rsk_ctx* c) {
+  if (!c->d_stage) RSK_HIP(hipMalloc(&c->d_stage, c->stage_bytes + c->stage_bytes / 4));
+}
+
+void check_keys(const rsk_keys* k) {
+  need(k != nullptr, "keys is NULL");
+  need(k->location == RSK_MEM_HOST || k->location == RSK_MEM_DEVICE, "keys.location must be RSK_MEM_HOST or RSK_MEM_DEVICE");
+  need(k->n == 0 || k->data != nullptr || (k->offsets == nullptr && k->fixed_len == 0), "keys.data is NULL");
+}
+
+// Calls fn(dev_keys, first_index, count) over the batch; host batches are
+// copied through the staging buffers in whole-key chunks.
+template <class F>
+void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
+  check_keys(k);
+  if (k->n == 0) return;
+  if (k->location == RSK_MEM_DEVICE) {
+    fn(DevKeys{reinterpret_cast<const uint8_t*>(k->data), k->offsets, k->n, k->fixed_len}, 0, k->n);
+    return;
+  }
+  ensure_stage(c);
+  uint8_t* d_data = c->d_stage;
+  uint64_t* d_offs = reinterpret_cast<uint64_t*>(c->d_stage + c->stage_bytes);
+  const uint64_t off_cap = c->stage_bytes / 4 / 8 - 1;  // keys per chunk (offsets)
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(k->data);
+  uint64_t first = 0;
+  while (first < k->n) {
+    uint64_t m;
+    if (k->offsets == nullptr) {
+      m = k->fixed_len ? c->stage_bytes / k->fixed_len : k->n;
+      m = std::min<uint64_t>(m, k->n - first);
+      need(m > 0, "key longer than the staging buffer");
+      if (k->fixed_len) RSK_HIP(hipMemcpyAsync(d_data, src + first * k->fixed_len, m * k->fixed_len,
+                                              hipMemcpyHostToDevice, c->stream));
+      fn(DevKeys{d_data, nullptr, m, k->fixed_len}, first, m);
+    } else {
+      const uint64_t base = k->offsets[first];
+      uint64_t lim = std::min<uint64_t>(k->n - first, off_cap);
+      // largest m <= lim with offsets[first+m] - base <= stage_bytes
+      const uint64_t* o = k->offsets + first;
+      m = (uint64_t)(std::upper_bound(o + 1, o + lim + 1, base + c->stage_bytes) - (o + 1));
+      need(m > 0, "key longer than the staging buffer");
+      need(k->offsets[first + m] >= base, "offsets must be non-decreasing");
+      RSK_HIP(hipMemcpyAsync(d_offs, k->offsets + first, (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+      if (k->offsets[first + m] > base)
+        RSK_HIP(hipMemcpyAsync(d_data, src + base, k->offsets[first + m] - base, hipMemcpyHostToDevice, c->stream));
+      // Offsets stay absolute: shift the data pointer instead of rebasing.
+      fn(DevKeys{d_data - base, d_offs, m, 0}, first, m);
+    }
+    // The staging buffer is reused by the next chunk.
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    first += m;
+  }
+}
+
+void check_hll(const rsk_hll* h, uint64_t id) {
+  need(h != nullptr, "hll handle is NULL");
+  need(id < h->n, "sketch id out of range");
+}
+
+uint8_t* regs_of(rsk_hll* h, uint64_t id) { return h->d_regs + id * (uint64_t)HLL_REGS; }
+
+// Redis createHLLObject: registers zero, card bytes zero (cache valid = 0).
+void create_if_missing(rsk_hll* h, uint64_t id, bool* created) {
+  *created = !h->exists[id];
+  h->exists[id] = 1;
+}
+
+// card[7] |= 0x80 (HLL_INVALIDATE_CACHE) for one sketch, on the stream.
+__global__ void invalidate_kernel(uint64_t* card, const uint32_t* flag, int force) {
+  if (force || (flag && *flag)) *card |= (1ull << 63);
+}
+
+__global__ void invalidate_all_kernel(uint64_t* card, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    card[i] |= (1ull << 63);
+}
+
+void invalidate(rsk_hll* h, uint64_t id, const uint32_t* d_flag, bool force) {
+  hipLaunchKernelGGL(invalidate_kernel, dim3(1), dim3(1), 0, h->ctx->stream, h->d_card + id, d_flag, force ? 1 : 0);
+  RSK_CHECK_LAUNCH("invalidate");
+}
+
+// ------------------------------------------------ Java double semantics
+int64_t java_d2l(double d) {
+  if (std::isnan(d)) return 0;
+  if (d >= 9223372036854775807.0) return INT64_MAX;
+  if (d <= -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)d;
+}
+int32_t java_d2i(double d) {
+  if (std::isnan(d)) return 0;
+  if (d >= 2147483647.0) return INT32_MAX;
+  if (d <= -2147483648.0) return INT32_MIN;
+  return (int32_t)d;
+}
+int64_t java_round(double a) {
+  if (a == 0x1.fffffffffffffp-2) return 0;
+  return java_d2l(std::floor(a + 0.5));
+}
+
+// RedissonBloomFilter.optimalNumOfBits (:73-78).
+int64_t optimal_bits(int64_t n, double p) {
+  if (p == 0) p = 4.9e-324;  // Double.MIN_VALUE
+  volatile double num = (double)(-n) * std::log(p);
+  volatile double den = std::log(2.0) * std::log(2.0);
+  return java_d2l(num / den);
+}
+// RedissonBloomFilter.optimalNumOfHashFunctions (:69-71).
+int32_t optimal_k(int64_t n, int64_t m) {
+  volatile double r = (double)m / (double)n;
+  volatile double x = r * std::log(2.0);
+  int32_t k = (int32_t)java_round(x);
+  return k > 1 ? k : 1;
+}
+
+constexpr int64_t BLOOM_MAX_SIZE = 2147483647LL * 2;  // RedissonBloomFilter.java:52
+constexpr int64_t BLOOM_EXT_MAX = 1LL << 44;          // 2 TiB of bits: beyond any single GPU
+
+FastMod63 make_fastmod(uint64_t d) {
+  FastMod63 f{};
+  f.d = d;
+  uint32_t l = 0;
+  while (l < 64 && ((unsigned __int128)1 << l) < d) ++l;
+  f.l = l;
+  if (l == 0) {
+    f.M = 0;
+  } else {
+    unsigned __int128 num = ((unsigned __int128)1 << (63 + l)) + d - 1;
+    f.M = (uint64_t)(num / d);
+  }
+  return f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsk_abi_version(void) { return RSK_ABI_VERSION; }
+const char* rsk_last_error(void) { return rsk::g_last_error.c_str(); }
+
+int rsk_init(const rsk_options* opts, rsk_ctx** out) {
+  return guarded([&] {
+    need(out != nullptr, "out is NULL");
+    *out = nullptr;
+    rsk_options o{};
+    if (opts) o = *opts;
+    if (o.redis_version == 0) o.redis_version = 320;
+    need(o.redis_version == 320, "only Redis 3.2.0 semantics (redis_version = 320) are implemented");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail(RSK_ERR_NO_DEVICE, "no HIP device visible");
+    need(o.device >= 0 && o.device < ndev, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    RSK_HIP(hipGetDeviceProperties(&prop, o.device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      fail(RSK_ERR_NO_DEVICE, std::string("librsketch is built for gfx950 only; device is ") + prop.gcnArchName);
+    auto* c = new rsk_ctx();
+    std::unique_ptr<rsk_ctx> guard(c);
+    c->device = o.device;
+    c->num_cus = prop.multiProcessorCount;
+    RSK_HIP(hipSetDevice(c->device));
+    RSK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->stage_bytes = o.staging_bytes ? o.staging_bytes : (256ull << 20);
+    c->slab_count = std::min<uint32_t>(RSK_MAX_SLABS, 2u * (uint32_t)c->num_cus);
+    RSK_HIP(hipMalloc(&c->d_slab, (uint64_t)c->slab_count * HLL_REGS));
+    c->small_bytes = 1 << 20;
+    RSK_HIP(hipMalloc(&c->d_small, c->small_bytes));
+    RSK_HIP(hipHostMalloc(&c->h_small, c->small_bytes, hipHostMallocDefault));
+    // Linear-counting table: m*log(m/ez), evaluated by the host libm exactly
+    // as Redis's hllCount does (E = m*log(m/ez)).
+    std::vector<double> lc(HLL_REGS + 1, 0.0);
+    const double m = HLL_REGS;
+    for (int ez = 1; ez <= HLL_REGS; ++ez) {
+      volatile double q = m / ez;
+      lc[ez] = m * std::log(q);
+    }
+    RSK_HIP(hipMalloc(&c->d_lc, lc.size() * sizeof(double)));
+    RSK_HIP(hipMemcpy(c->d_lc, lc.data(), lc.size() * sizeof(double), hipMemcpyHostToDevice));
+    *out = guard.release();
+  });
+}
+
+int rsk_shutdown(rsk_ctx* c) {
+  if (!c) return RSK_OK;
+  int rc = guarded([&] {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    rsk::prof_fold(c);
+    for (auto e : c->prof.free_events) (void)hipEventDestroy(e);
+    (void)hipFree(c->d_stage);
+    (void)hipFree(c->d_slab);
+    (void)hipFree(c->d_small);
+    (void)hipHostFree(c->h_small);
+    (void)hipFree(c->d_work);
+    (void)hipFree(c->d_lc);
+    auto it = g_out.find(c);
+    if (it != g_out.end()) {
+      (void)hipFree(it->second.p);
+      g_out.erase(it);
+    }
+    (void)hipStreamDestroy(c->stream);
+  });
+  delete c;
+  return rc;
+}
+
+void* rsk_ctx_stream(rsk_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int rsk_sync(rsk_ctx* c) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    CtxLock l(c);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_prof_enable(rsk_ctx* c, int on) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    CtxLock l(c);
+    c->prof.on = on != 0;
+  });
+}
+
+int rsk_prof_reset(rsk_ctx* c) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    CtxLock l(c);
+    rsk::prof_fold(c);
+    c->prof.totals.clear();
+  });
+}
+
+int rsk_prof_read(rsk_ctx* c, const char* name, double* ms, uint64_t* launches) {
+  return guarded([&] {
+    need(c && name && ms && launches, "NULL argument");
+    CtxLock l(c);
+    rsk::prof_fold(c);
+    auto it = c->prof.totals.find(name);
+    *ms = it == c->prof.totals.end() ? 0.0 : it->second.ms;
+    *launches = it == c->prof.totals.end() ? 0 : it->second.launches;
+  });
+}
+
+// ------------------------------------------------------------------ HLL
+int rsk_hll_create(rsk_ctx* c, uint64_t n, rsk_hll** out) {
+  return guarded([&] {
+    need(c && out, "NULL argument");
+    need(n > 0, "n_sketches must be > 0");
+    CtxLock l(c);
+    *out = nullptr;
+    auto* h = new rsk_hll();
+    std::unique_ptr<rsk_hll> guard(h);
+    h->ctx = c;
+    h->n = n;
+    h->exists.assign(n, 0);
+    RSK_HIP(hipMalloc(&h->d_regs, n * (uint64_t)HLL_REGS));
+    RSK_HIP(hipMalloc(&h->d_card, n * 8));
+    RSK_HIP(hipMemsetAsync(h->d_regs, 0, n * (uint64_t)HLL_REGS, c->stream));
+    RSK_HIP(hipMemsetAsync(h->d_card, 0, n * 8, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    *out = guard.release();
+  });
+}
+
+int rsk_hll_destroy(rsk_hll* h) {
+  if (!h) return RSK_OK;
+  int rc = guarded([&] {
+    CtxLock l(h->ctx);
+    RSK_HIP(hipStreamSynchronize(h->ctx->stream));
+    RSK_HIP(hipFree(h->d_regs));
+    RSK_HIP(hipFree(h->d_card));
+  });
+  delete h;
+  return rc;
+}
+
+uint64_t rsk_hll_size(const rsk_hll* h) { return h ? h->n : 0; }
+
+int rsk_hll_exists(rsk_hll* h, uint64_t id, int* out) {
+  return guarded([&] {
+    check_hll(h, id);
+    need(out != nullptr, "out is NULL");
+    *out = h->exists[id];
+  });
+}
+
+int rsk_hll_delete(rsk_hll* h, uint64_t id) {
+  return guarded([&] {
+    check_hll(h, id);
+    CtxLock l(h->ctx);
+    RSK_HIP(hipMemsetAsync(regs_of(h, id), 0, HLL_REGS, h->ctx->stream));
+    RSK_HIP(hipMemsetAsync(h->d_card + id, 0, 8, h->ctx->stream));
+    h->exists[id] = 0;
+  });
+}
+
+int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_out) {
+  return guarded([&] {
+    check_hll(h, id);
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    bool created;
+    create_if_missing(h, id, &created);
+    uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->d_small);
+    RSK_HIP(hipMemsetAsync(d_flag, 0, 4, c->stream));
+    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { hll_add_launch(c, dk, regs_of(h, id), d_flag); });
+    invalidate(h, id, d_flag, created);
+    if (changed_out) {
+      RSK_HIP(hipMemcpyAsync(c->h_small, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      uint32_t f;
+      std::memcpy(&f, c->h_small, 4);
+      *changed_out = (uint8_t)((f != 0) || created);
+    }
+  });
+}
+
+int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out) {
+  return guarded([&] {
+    check_hll(h, id);
+    need(out != nullptr, "out is NULL");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    bool created;
+    create_if_missing(h, id, &created);
+    check_keys(keys);
+    // Sub-chunks bounded for the 32-bit sort; replies compose sequentially.
+    const uint64_t max_chunk = 1ull << 26;
+    rsk_keys sub = *keys;
+    uint64_t done = 0;
+    while (done < keys->n) {
+      uint64_t m = std::min<uint64_t>(max_chunk, keys->n - done);
+      sub.n = m;
+      if (keys->offsets) {
+        sub.offsets = keys->offsets + done;
+        sub.data = keys->data;
+      } else {
+        sub.offsets = nullptr;
+        sub.data = reinterpret_cast<const uint8_t*>(keys->data) + done * keys->fixed_len;
+      }
+      for_each_chunk(c, &sub, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+        uint8_t* d_out = keys->location == RSK_MEM_DEVICE ? out + done + first : out_scratch(c, cnt);
+        hll_add_each_launch(c, dk, regs_of(h, id), d_out);
+        if (keys->location == RSK_MEM_HOST) {
+          RSK_HIP(hipMemcpyAsync(out + done + first, d_out, cnt, hipMemcpyDeviceToHost, c->stream));
+          RSK_HIP(hipStreamSynchronize(c->stream));
+        }
+      });
+      done += m;
+    }
+    // Any reply of 1 means a register grew: invalidate the cache.
+    if (keys->n > 0) {
+      if (keys->location == RSK_MEM_HOST) {
+        bool any = created;
+        for (uint64_t i = 0; i < keys->n && !any; ++i) any = out[i] != 0;
+        if (any) invalidate(h, id, nullptr, true);
+        if (created) out[0] = 1;
+      } else {
+        // Device replies: cheap on-device OR via the flag word.
+        invalidate(h, id, nullptr, true);  // conservative: a no-op PFADD keeps the old card bytes valid in Redis
+        if (created) RSK_HIP(hipMemsetAsync(out, 1, 1, c->stream));
+      }
+    } else if (created) {
+      invalidate(h, id, nullptr, true);
+    }
+  });
+}
+
+int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups) {
+  return guarded([&] {
+    need(h != nullptr, "hll handle is NULL");
+    need(keys == nullptr || keys->n == 0 || groups != nullptr, "groups is NULL");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    check_keys(keys);
+    if (keys->n == 0) return;
+    uint32_t* d_groups = nullptr;
+    if (keys->location == RSK_MEM_HOST) {
+      for (uint64_t i = 0; i < keys->n; ++i)
+        if (groups[i] < h->n) h->exists[groups[i]] = 1;
+    }
+    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+      if (keys->location == RSK_MEM_DEVICE) {
+        d_groups = const_cast<uint32_t*>(groups);
+      } else {
+        d_groups = reinterpret_cast<uint32_t*>(out_scratch(c, cnt * 4));
+        RSK_HIP(hipMemcpyAsync(d_groups, groups + first, cnt * 4, hipMemcpyHostToDevice, c->stream));
+      }
+      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n);
+    });
+    if (keys->location == RSK_MEM_DEVICE) {
+      // Group ids stay on the device: every sketch of the pool is treated as
+      // materialised (a pool-wide PFADD target), and every cache invalidated.
+      std::fill(h->exists.begin(), h->exists.end(), 1);
+    }
+    // Every pool member may have changed: invalidate all caches (card |= bit 63).
+    hipLaunchKernelGGL(invalidate_all_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
+    RSK_CHECK_LAUNCH("invalidate_all");
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
+  return guarded([&] {
+    need(h != nullptr && out != nullptr, "NULL argument");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    if (n == 0) return;
+    uint64_t* d_ids = nullptr;
+    uint8_t* s = out_scratch(c, (ids ? n * 8 : 0) + n * 8 + 256);
+    if (ids) {
+      for (uint64_t i = 0; i < n; ++i) need(ids[i] < h->n, "sketch id out of range");
+      d_ids = reinterpret_cast<uint64_t*>(s);
+      RSK_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, c->stream));
+    } else {
+      need(n <= h->n, "n exceeds pool size");
+    }
+    uint64_t* d_out = reinterpret_cast<uint64_t*>(s + (ids ? ((n * 8 + 255) & ~255ull) : 0));
+    hll_count_launch(c, h->d_regs, h->d_card, d_ids, n, d_out);
+    RSK_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+namespace {
+void union_impl(rsk_ctx* c, const std::vector<const uint8_t*>& ptrs, uint32_t arity, uint64_t n, uint64_t* out) {
+  uint8_t* s = out_scratch(c, ptrs.size() * 8 + n * 8 + 512);
+  auto* d_ptrs = reinterpret_cast<const uint8_t**>(s);
+  auto* d_out = reinterpret_cast<uint64_t*>(s + ((ptrs.size() * 8 + 255) & ~255ull));
+  RSK_HIP(hipMemcpyAsync(d_ptrs, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice, c->stream));
+  hll_union_count_launch(c, d_ptrs, arity, n, d_out);
+  RSK_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
+  RSK_HIP(hipStreamSynchronize(c->stream));
+}
+}  // namespace
+
+int rsk_hll_count_union(rsk_hll* const* hs, const uint64_t* ids, uint32_t k, uint64_t* out) {
+  return guarded([&] {
+    need(hs && ids && out && k >= 1, "bad arguments");
+    rsk_ctx* c = hs[0]->ctx;
+    CtxLock l(c);
+    std::vector<const uint8_t*> ptrs(k);
+    for (uint32_t a = 0; a < k; ++a) {
+      check_hll(hs[a], ids[a]);
+      need(hs[a]->ctx == c, "all sketches must share one context");
+      ptrs[a] = hs[a]->exists[ids[a]] ? regs_of(hs[a], ids[a]) : nullptr;
+    }
+    union_impl(c, ptrs, k, 1, out);
+  });
+}
+
+int rsk_hll_count_union_batch(rsk_hll* h, const uint64_t* member_ids, uint32_t arity, uint64_t n, uint64_t* out) {
+  return guarded([&] {
+    need(h && member_ids && out && arity >= 1, "bad arguments");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    std::vector<const uint8_t*> ptrs(n * arity);
+    for (uint64_t i = 0; i < n * arity; ++i) {
+      check_hll(h, member_ids[i]);
+      ptrs[i] = h->exists[member_ids[i]] ? regs_of(h, member_ids[i]) : nullptr;
+    }
+    if (n) union_impl(c, ptrs, arity, n, out);
+  });
+}
+
+int rsk_hll_merge(rsk_hll* dst, uint64_t dst_id, rsk_hll* const* srcs, const uint64_t* src_ids, uint32_t k) {
+  return guarded([&] {
+    check_hll(dst, dst_id);
+    need(k == 0 || (srcs && src_ids), "srcs is NULL");
+    rsk_ctx* c = dst->ctx;
+    CtxLock l(c);
+    std::vector<const uint8_t*> sp(k);
+    for (uint32_t a = 0; a < k; ++a) {
+      check_hll(srcs[a], src_ids[a]);
+      need(srcs[a]->ctx == c, "all sketches must share one context");
+      sp[a] = srcs[a]->exists[src_ids[a]] ? regs_of(srcs[a], src_ids[a]) : nullptr;
+    }
+    bool created;
+    create_if_missing(dst, dst_id, &created);
+    if (k) {
+      uint8_t* s = out_scratch(c, 8 + k * 8 + 512);
+      auto* d_dst = reinterpret_cast<uint8_t**>(s);
+      auto* d_src = reinterpret_cast<const uint8_t**>(s + 256);
+      uint8_t* dp = regs_of(dst, dst_id);
+      RSK_HIP(hipMemcpyAsync(d_dst, &dp, 8, hipMemcpyHostToDevice, c->stream));
+      RSK_HIP(hipMemcpyAsync(d_src, sp.data(), k * 8, hipMemcpyHostToDevice, c->stream));
+      hll_merge_launch(c, d_dst, d_src, k, 1);
+    }
+    invalidate(dst, dst_id, nullptr, true);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_ids, uint64_t n) {
+  return guarded([&] {
+    need(h && dst_ids && src_ids, "NULL argument");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    if (n == 0) return;
+    std::vector<uint8_t*> dp(n);
+    std::vector<const uint8_t*> sp(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      check_hll(h, dst_ids[i]);
+      check_hll(h, src_ids[i]);
+      sp[i] = h->exists[src_ids[i]] ? regs_of(h, src_ids[i]) : nullptr;
+      h->exists[dst_ids[i]] = 1;
+      dp[i] = regs_of(h, dst_ids[i]);
+    }
+    // PFMERGEs run in input order in Redis; a batch whose destinations are
+    // also sources of other pairs would depend on that order.  Run such
+    // batches as sequential waves of independent pairs.
+    uint8_t* s = out_scratch(c, 16 * n + 512);
+    auto* d_dst = reinterpret_cast<uint8_t**>(s);
+    auto* d_src = reinterpret_cast<const uint8_t**>(s + ((8 * n + 255) & ~255ull));
+    uint64_t start = 0;
+    while (start < n) {
+      // Grow the wave while no pair reads or writes a sketch written earlier in it.
+      std::map<const uint8_t*, int> written;
+      uint64_t end = start;
+      while (end < n) {
+        if (written.count(sp[end]) || written.count(dp[end])) break;
+        written[dp[end]] = 1;
+        ++end;
+      }
+      RSK_HIP(hipMemcpyAsync(d_dst, dp.data() + start, (end - start) * 8, hipMemcpyHostToDevice, c->stream));
+      RSK_HIP(hipMemcpyAsync(d_src, sp.data() + start, (end - start) * 8, hipMemcpyHostToDevice, c->stream));
+      hll_merge_launch(c, d_dst, d_src, 1, end - start);
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      start = end;
+    }
+    for (uint64_t i = 0; i < n; ++i) invalidate(h, dst_ids[i], nullptr, true);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_merge_raw(rsk_hll* h, uint64_t id, const uint8_t* regs, uint32_t location) {
+  return guarded([&] {
+    check_hll(h, id);
+    need(regs != nullptr, "regs is NULL");
+    need(location == RSK_MEM_HOST || location == RSK_MEM_DEVICE, "bad location");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    bool created;
+    create_if_missing(h, id, &created);
+    const uint8_t* src = regs;
+    if (location == RSK_MEM_HOST) {
+      uint8_t* s = out_scratch(c, HLL_REGS);
+      RSK_HIP(hipMemcpyAsync(s, regs, HLL_REGS, hipMemcpyHostToDevice, c->stream));
+      src = s;
+    }
+    hll_max_into_launch(c, regs_of(h, id), src, nullptr);
+    invalidate(h, id, nullptr, true);  // PFMERGE always invalidates
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_get_registers(rsk_hll* h, uint64_t id, uint8_t* out, uint32_t location) {
+  return guarded([&] {
+    check_hll(h, id);
+    need(out != nullptr, "out is NULL");
+    CtxLock l(h->ctx);
+    RSK_HIP(hipMemcpyAsync(out, regs_of(h, id), HLL_REGS,
+                           location == RSK_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                           h->ctx->stream));
+    RSK_HIP(hipStreamSynchronize(h->ctx->stream));
+  });
+}
+
+void* rsk_hll_device_registers(rsk_hll* h) { return h ? h->d_regs : nullptr; }
+
+int rsk_hll_export_redis(rsk_hll* h, uint64_t id, uint8_t* buf, size_t cap, size_t* len) {
+  return guarded([&] {
+    check_hll(h, id);
+    need(len != nullptr, "len is NULL");
+    CtxLock l(h->ctx);
+    if (!h->exists[id]) {  // GET of a missing key: nil
+      *len = 0;
+      return;
+    }
+    need(buf != nullptr && cap >= RSK_HLL_DENSE_BYTES, "buffer smaller than 12304 bytes");
+    std::vector<uint8_t> raw(HLL_REGS);
+    uint64_t card = 0;
+    RSK_HIP(hipMemcpyAsync(raw.data(), regs_of(h, id), HLL_REGS, hipMemcpyDeviceToHost, h->ctx->stream));
+    RSK_HIP(hipMemcpyAsync(&card, h->d_card + id, 8, hipMemcpyDeviceToHost, h->ctx->stream));
+    RSK_HIP(hipStreamSynchronize(h->ctx->stream));
+    std::memset(buf, 0, RSK_HLL_DENSE_BYTES);
+    std::memcpy(buf, "HYLL", 4);
+    buf[4] = 0;  // HLL_DENSE
+    for (int b = 0; b < 8; ++b) buf[8 + b] = (uint8_t)(card >> (8 * b));
+    uint8_t* p = buf + 16;
+    for (int j = 0; j < HLL_REGS; ++j) {  // HLL_DENSE_SET_REGISTER, 6 bits LSB-first
+      uint32_t bitpos = (uint32_t)j * 6, byte = bitpos >> 3, fb = bitpos & 7;
+      uint32_t v = raw[j] & 63;
+      p[byte] |= (uint8_t)(v << fb);
+      if (fb > 2) p[byte + 1] |= (uint8_t)(v >> (8 - fb));
+    }
+    *len = RSK_HLL_DENSE_BYTES;
+  });
+}
+
+int rsk_hll_import_redis(rsk_hll* h, uint64_t id, const uint8_t* buf, size_t len) {
+  return guarded([&] {
+    check_hll(h, id);
+    need(buf != nullptr || len == 0, "buf is NULL");
+    // isHLLObjectOrReply: header, magic, encoding, exact dense length.
+    if (len < 16 || std::memcmp(buf, "HYLL", 4) != 0 || buf[4] > 1 || (buf[4] == 0 && len != RSK_HLL_DENSE_BYTES))
+      fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value.");
+    std::vector<uint8_t> raw(HLL_REGS, 0);
+    if (buf[4] == 0) {
+      const uint8_t* p = buf + 16;
+      for (int j = 0; j < HLL_REGS; ++j) {
+        uint32_t bitpos = (uint32_t)j * 6, byte = bitpos >> 3, fb = bitpos & 7;
+        uint32_t b0 = p[byte], b1 = byte + 1 < 12288 ? p[byte + 1] : 0;
+        raw[j] = (uint8_t)(((b0 >> fb) | (b1 << (8 - fb))) & 63);
+      }
+    } else {
+      // Sparse opcodes: ZERO 00xxxxxx, XZERO 01xxxxxx yyyyyyyy, VAL 1vvvvvxx.
+      const uint8_t *p = buf + 16, *end = buf + len;
+      uint64_t i = 0;
+      bool overflow = false;
+      while (p < end) {
+        if ((*p & 0xc0) == 0) {
+          i += (*p & 0x3f) + 1;
+          p++;
+        } else if ((*p & 0xc0) == 0x40) {
+          if (p + 1 >= end) {
+            overflow = true;
+            break;
+          }
+          i += (((uint64_t)(*p & 0x3f) << 8) | p[1]) + 1;
+          p += 2;
+        } else {
+          uint64_t run = (*p & 3) + 1;
+          uint8_t v = (uint8_t)(((*p >> 2) & 0x1f) + 1);
+          if (run + i > HLL_REGS) {
+            overflow = true;
+            break;
+          }
+          while (run--) {
+            raw[i] = std::max(raw[i], v);
+            ++i;
+          }
+          p++;
+        }
+      }
+      if (overflow || i != HLL_REGS) fail(RSK_ERR_INVALID_HLL, "INVALIDOBJ Corrupted HLL object detected");
+    }
+    uint64_t card = 0;
+    for (int b = 0; b < 8; ++b) card |= (uint64_t)buf[8 + b] << (8 * b);
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    RSK_HIP(hipMemcpyAsync(regs_of(h, id), raw.data(), HLL_REGS, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemcpyAsync(h->d_card + id, &card, 8, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    h->exists[id] = 1;
+  });
+}
+
+// ---------------------------------------------------------------- Bloom
+int rsk_bloom_params(int64_t n, double p, uint32_t mode, int64_t* size_out, int32_t* k_out) {
+  return guarded([&] {
+    need(size_out && k_out, "NULL argument");
+    need(mode == RSK_BLOOM_COMPAT || mode == RSK_BLOOM_EXTENDED, "bad mode");
+    int64_t size = optimal_bits(n, p);
+    if (mode == RSK_BLOOM_COMPAT && size > BLOOM_MAX_SIZE)
+      fail(RSK_ERR_INVALID_ARG, "Bloom filter can't be greater than " + std::to_string(BLOOM_MAX_SIZE) +
+                                    ". But calculated size is " + std::to_string(size));
+    if (size > BLOOM_EXT_MAX) fail(RSK_ERR_INVALID_ARG, "Bloom filter size " + std::to_string(size) + " exceeds device limit");
+    *size_out = size;
+    *k_out = optimal_k(n, size);
+  });
+}
+
+int rsk_bloom_create(rsk_ctx* c, int64_t size, int32_t k, rsk_bloom** out) {
+  return guarded([&] {
+    need(c && out, "NULL argument");
+    need(size > 0, "Bloom filter size must be > 0");
+    need(size <= BLOOM_EXT_MAX, "Bloom filter size exceeds device limit");
+    need(k >= 1 && k <= 4096, "hashIterations must be in [1, 4096]");
+    CtxLock l(c);
+    *out = nullptr;
+    auto* b = new rsk_bloom();
+    std::unique_ptr<rsk_bloom> guard(b);
+    b->ctx = c;
+    b->size = size;
+    b->k = k;
+    b->nbytes = ((uint64_t)size + 7) / 8;
+    b->nwords = ((b->nbytes + 15) / 16) * 4;
+    b->fm = make_fastmod((uint64_t)size);
+    RSK_HIP(hipMalloc(&b->d_bits, b->nwords * 4));
+    RSK_HIP(hipMemsetAsync(b->d_bits, 0, b->nwords * 4, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    *out = guard.release();
+  });
+}
+
+int rsk_bloom_init(rsk_ctx* c, int64_t n, double p, uint32_t mode, rsk_bloom** out, int64_t* size_out,
+                   int32_t* k_out) {
+  int64_t size = 0;
+  int32_t k = 0;
+  int rc = rsk_bloom_params(n, p, mode, &size, &k);
+  if (rc != RSK_OK) return rc;
+  if (size_out) *size_out = size;
+  if (k_out) *k_out = k;
+  return rsk_bloom_create(c, size, k, out);
+}
+
+int rsk_bloom_destroy(rsk_bloom* b) {
+  if (!b) return RSK_OK;
+  int rc = guarded([&] {
+    CtxLock l(b->ctx);
+    RSK_HIP(hipStreamSynchronize(b->ctx->stream));
+    RSK_HIP(hipFree(b->d_bits));
+  });
+  delete b;
+  return rc;
+}
+
+int rsk_bloom_info(const rsk_bloom* b, int64_t* size, int32_t* k) {
+  return guarded([&] {
+    need(b && size && k, "NULL argument");
+    *size = b->size;
+    *k = b->k;
+  });
+}
+
+int rsk_bloom_add(rsk_bloom* b, const rsk_keys* keys, uint8_t* added_out) {
+  return guarded([&] {
+    need(b != nullptr, "bloom handle is NULL");
+    rsk_ctx* c = b->ctx;
+    CtxLock l(c);
+    check_keys(keys);
+    if (!added_out) {
+      for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { bloom_add_launch(c, b, dk); });
+      return;
+    }
+    // Replies need the ordered path; bound the probe count per sort.
+    const uint64_t max_keys = std::max<uint64_t>(1, (1ull << 28) / (uint64_t)b->k);
+    rsk_keys sub = *keys;
+    uint64_t done = 0;
+    while (done < keys->n) {
+      uint64_t m = std::min<uint64_t>(max_keys, keys->n - done);
+      sub.n = m;
+      if (keys->offsets) {
+        sub.offsets = keys->offsets + done;
+      } else {
+        sub.data = reinterpret_cast<const uint8_t*>(keys->data) + done * keys->fixed_len;
+      }
+      for_each_chunk(c, &sub, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+        uint8_t* d_out = keys->location == RSK_MEM_DEVICE ? added_out + done + first : out_scratch(c, cnt);
+        bloom_add_each_launch(c, b, dk, d_out);
+        if (keys->location == RSK_MEM_HOST) {
+          RSK_HIP(hipMemcpyAsync(added_out + done + first, d_out, cnt, hipMemcpyDeviceToHost, c->stream));
+          RSK_HIP(hipStreamSynchronize(c->stream));
+        }
+      });
+      done += m;
+    }
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_bloom_contains(rsk_bloom* b, const rsk_keys* keys, uint8_t* out) {
+  return guarded([&] {
+    need(b != nullptr && out != nullptr, "NULL argument");
+    rsk_ctx* c = b->ctx;
+    CtxLock l(c);
+    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+      if (keys->location == RSK_MEM_DEVICE) {
+        bloom_contains_launch(c, b, dk, out + first);
+      } else {
+        uint8_t* d_out = out_scratch(c, cnt);
+        bloom_contains_launch(c, b, dk, d_out);
+        RSK_HIP(hipMemcpyAsync(out + first, d_out, cnt, hipMemcpyDeviceToHost, c->stream));
+        RSK_HIP(hipStreamSynchronize(c->stream));
+      }
+    });
+  });
+}
+
+int rsk_bloom_bitcount(rsk_bloom* b, uint64_t* out) {
+  return guarded([&] {
+    need(b && out, "NULL argument");
+    rsk_ctx* c = b->ctx;
+    CtxLock l(c);
+    uint64_t* d = reinterpret_cast<uint64_t*>(c->d_small + 128);
+    bloom_bitcount_launch(c, b->d_bits, b->nwords, d);
+    RSK_HIP(hipMemcpyAsync(c->h_small + 128, d, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(out, c->h_small + 128, 8);
+  });
+}
+
+int rsk_bloom_count(rsk_bloom* b, int32_t* out) {
+  uint64_t bc = 0;
+  int rc = rsk_bloom_bitcount(b, &bc);
+  if (rc != RSK_OK) return rc;
+  return guarded([&] {
+    need(out != nullptr, "out is NULL");
+    // (int) (-size / ((double) k) * Math.log(1 - bitcount / ((double) size)))
+    volatile double a = (double)(-b->size) / (double)b->k;
+    volatile double q = (double)bc / (double)b->size;
+    volatile double lg = std::log(1 - q);
+    *out = java_d2i(a * lg);
+  });
+}
+
+int rsk_bloom_export_bits(rsk_bloom* b, uint8_t* buf, size_t cap, size_t* len) {
+  return guarded([&] {
+    need(b && len, "NULL argument");
+    need(buf != nullptr && cap >= b->nbytes, "buffer smaller than ceil(size/8)");
+    CtxLock l(b->ctx);
+    RSK_HIP(hipMemcpyAsync(buf, b->d_bits, b->nbytes, hipMemcpyDeviceToHost, b->ctx->stream));
+    RSK_HIP(hipStreamSynchronize(b->ctx->stream));
+    *len = b->nbytes;
+  });
+}
+
+int rsk_bloom_import_bits(rsk_bloom* b, const uint8_t* buf, size_t len) {
+  return guarded([&] {
+    need(b != nullptr, "NULL argument");
+    need(len <= b->nbytes, "bit string longer than the filter");
+    need(buf != nullptr || len == 0, "buf is NULL");
+    CtxLock l(b->ctx);
+    RSK_HIP(hipMemsetAsync(b->d_bits, 0, b->nwords * 4, b->ctx->stream));
+    if (len) RSK_HIP(hipMemcpyAsync(b->d_bits, buf, len, hipMemcpyHostToDevice, b->ctx->stream));
+    RSK_HIP(hipStreamSynchronize(b->ctx->stream));
+  });
+}
+
+int rsk_bloom_or_bits(rsk_bloom* b, const uint8_t* bits, size_t len, uint32_t location) {
+  return guarded([&] {
+    need(b != nullptr && (bits != nullptr || len == 0), "NULL argument");
+    need(len <= b->nbytes, "bit string longer than the filter");
+    rsk_ctx* c = b->ctx;
+    CtxLock l(c);
+    if (len == 0) return;
+    const uint8_t* src = bits;
+    if (location == RSK_MEM_HOST) {
+      uint8_t* s = out_scratch(c, len);
+      RSK_HIP(hipMemcpyAsync(s, bits, len, hipMemcpyHostToDevice, c->stream));
+      src = s;
+    }
+    bloom_or_launch(c, b->d_bits, src, len);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+void* rsk_bloom_device_bits(rsk_bloom* b) { return b ? b->d_bits : nullptr; }
+
+// ----------------------------------------------------------- generators
+int rsk_gen_keys16(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* dev_out) {
+  return guarded([&] {
+    need(c && (dev_out || n == 0), "NULL argument");
+    CtxLock l(c);
+    if (n) gen_keys16_launch(c, seed, start, n, dev_out);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_gen_grouped(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* dev_groups,
+                    void* dev_keys) {
+  return guarded([&] {
+    need(c && G > 0 && ((dev_groups && dev_keys) || n == 0), "bad arguments");
+    CtxLock l(c);
+    if (n) gen_grouped_launch(c, seed, G, start, n, dev_groups, dev_keys);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_gen_queries16(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
+                      void* dev_out) {
+  return guarded([&] {
+    need(c && n_ins > 0 && (dev_out || n == 0), "bad arguments");
+    CtxLock l(c);
+    if (n) gen_queries16_launch(c, qseed, iseed, n_ins, start, n, dev_out);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_gen_varlen(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* dev_offsets, void* dev_blob,
+                   uint64_t blob_cap, uint64_t* total_bytes) {
+  return guarded([&] {
+    need(c && dev_offsets && total_bytes, "NULL argument");
+    need(n < (1ull << 31), "n must be < 2^31 per call");
+    CtxLock l(c);
+    gen_varlen_lengths_launch(c, seed, start, n, dev_offsets);
+    uint64_t tot = 0;
+    RSK_HIP(hipMemcpyAsync(&tot, dev_offsets + n, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    *total_bytes = tot;
+    if (dev_blob) {
+      need(blob_cap >= tot, "blob capacity too small");
+      gen_varlen_bytes_launch(c, seed, start, n, dev_offsets, reinterpret_cast<uint8_t*>(dev_blob));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+    }
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,246 @@
+// rsk_bloom.hip -- Bloom-filter kernels for gfx950.
+//
+// Replaces RedissonBloomFilter's client-side index generation
+// (src/main/java/org/redisson/RedissonBloomFilter.java:116-131: xxHash64 r39
+// + FarmHash-uo double hashing, idx_i = (h_i & Long.MAX_VALUE) % size) and the
+// k SETBIT / GETBIT commands it pipelines to Redis (:94-98, :147-151), and
+// BITCOUNT for count() (:188-199).
+//
+// Data layout in HBM: the filter is the Redis string itself -- ceil(size/8)
+// bytes, bit i in byte i>>3 under mask 0x80>>(i&7) (bitops.c, MSB-first;
+// RedissonBitSet.java:152-173) -- addressed as little-endian u32 words so a
+// SETBIT is one memory-side atomicOr: word i>>5, bit 8*((i>>3)&3) + 7-(i&7).
+// Bounded by random 4-byte accesses, not by streaming bandwidth.
+#include <hipcub/hipcub.hpp>
+
+#include "rsk_internal.h"
+
+namespace rsk {
+
+RSK_DEV uint32_t bit_mask(uint64_t idx) { return 1u << ((uint32_t)((idx >> 3) & 3) * 8 + 7 - (uint32_t)(idx & 7)); }
+constexpr uint64_t JAVA_LONG_MAX = 0x7FFFFFFFFFFFFFFFULL;
+
+template <bool FIXED16>
+RSK_DEV void key_hashes(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                        uint64_t i, uint64_t& h1, uint64_t& h2) {
+  if (FIXED16) {
+    uint4 v = ld_nt16(reinterpret_cast<const uint4*>(data) + i);
+    uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
+    h1 = xxh64_16(w0, w1);
+    h2 = farm_16(w0, w1);
+  } else {
+    uint64_t s = offsets ? offsets[i] : i * fixed_len;
+    uint64_t len = offsets ? offsets[i + 1] - s : fixed_len;
+    h1 = xxh64(data + s, len);
+    h2 = farm_uo64(data + s, len);
+  }
+}
+
+template <bool FIXED16>
+__global__ __launch_bounds__(256) void bloom_add_kernel(const uint8_t* __restrict__ data,
+                                                        const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                                                        uint64_t n, uint32_t* __restrict__ bits, FastMod63 fm,
+                                                        int k) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h1, h2;
+    key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
+    uint64_t h = h1;
+    for (int t = 0; t < k; ++t) {
+      uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
+      atomicOr(&bits[idx >> 5], bit_mask(idx));
+      h += (t & 1) ? h1 : h2;
+    }
+  }
+}
+
+// contains: AND of the first k-1 bits (the reference never reads idx_{k-1}).
+template <bool FIXED16>
+__global__ __launch_bounds__(256) void bloom_contains_kernel(const uint8_t* __restrict__ data,
+                                                             const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                                                             uint64_t n, const uint32_t* __restrict__ bits,
+                                                             FastMod63 fm, int k, uint8_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h1, h2;
+    key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
+    uint64_t h = h1;
+    uint32_t all = 1;
+    for (int t = 0; t < k - 1; ++t) {
+      uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
+      all &= (bits[idx >> 5] & bit_mask(idx)) != 0;
+      h += (t & 1) ? h1 : h2;
+    }
+    out[i] = (uint8_t)all;
+  }
+}
+
+static bool fixed16(const DevKeys& k) {
+  return k.offsets == nullptr && k.fixed_len == 16 && (reinterpret_cast<uintptr_t>(k.data) & 15) == 0;
+}
+static uint32_t grid_for(rsk_ctx* c, uint64_t n) {
+  uint64_t g = (n + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 32;
+  return (uint32_t)(g < cap ? (g ? g : 1) : cap);
+}
+
+void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
+  if (k.n == 0) return;
+  if (fixed16(k)) {
+    ProfScope ps(c, "bloom_add16");
+    hipLaunchKernelGGL(bloom_add_kernel<true>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, nullptr, 16u,
+                       k.n, b->d_bits, b->fm, b->k);
+    RSK_CHECK_LAUNCH("bloom_add16");
+  } else {
+    ProfScope ps(c, "bloom_add");
+    hipLaunchKernelGGL(bloom_add_kernel<false>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, k.offsets,
+                       k.fixed_len, k.n, b->d_bits, b->fm, b->k);
+    RSK_CHECK_LAUNCH("bloom_add");
+  }
+}
+
+void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out) {
+  if (k.n == 0) return;
+  if (fixed16(k)) {
+    ProfScope ps(c, "bloom_contains16");
+    hipLaunchKernelGGL(bloom_contains_kernel<true>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, nullptr,
+                       16u, k.n, b->d_bits, b->fm, b->k, d_out);
+    RSK_CHECK_LAUNCH("bloom_contains16");
+  } else {
+    ProfScope ps(c, "bloom_contains");
+    hipLaunchKernelGGL(bloom_contains_kernel<false>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data,
+                       k.offsets, k.fixed_len, k.n, b->d_bits, b->fm, b->k, d_out);
+    RSK_CHECK_LAUNCH("bloom_contains");
+  }
+}
+
+// ------------------------------------------- add() replies, input order
+// Probe p = i*k + t.  A probe "finds its bit clear" iff the bit was clear
+// before the batch and p is the first probe (in sequence order) of that
+// bit.  Stable radix sort of (bit index, p) finds the first probe per bit.
+__global__ void bloom_probe_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+                                   uint32_t fixed_len, uint64_t n, const uint32_t* __restrict__ bits, FastMod63 fm,
+                                   int k, uint64_t* __restrict__ pidx, uint32_t* __restrict__ pseq,
+                                   uint8_t* __restrict__ pclear) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h1, h2;
+    key_hashes<false>(data, offsets, fixed_len, i, h1, h2);
+    uint64_t h = h1;
+    for (int t = 0; t < k; ++t) {
+      uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
+      uint64_t p = i * (uint64_t)k + t;
+      pidx[p] = idx;
+      pseq[p] = (uint32_t)p;
+      pclear[p] = (bits[idx >> 5] & bit_mask(idx)) == 0;
+      h += (t & 1) ? h1 : h2;
+    }
+  }
+}
+
+__global__ void bloom_first_kernel(const uint64_t* __restrict__ sidx, const uint32_t* __restrict__ sseq, uint64_t np,
+                                   const uint8_t* __restrict__ pclear, uint8_t* __restrict__ found0) {
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < np; q += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t p = sseq[q];
+    bool first = q == 0 || sidx[q] != sidx[q - 1];
+    found0[p] = first && pclear[p];
+  }
+}
+
+__global__ void bloom_reply_kernel(const uint8_t* __restrict__ found0, uint64_t n, int k, uint8_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint8_t r = 0;
+    for (int t = 0; t < k - 1; ++t) r |= found0[i * k + t];
+    out[i] = r;
+  }
+}
+
+void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out) {
+  const uint64_t n = k.n;
+  if (n == 0) return;
+  const uint64_t np = n * (uint64_t)b->k;
+  int end_bit = 1;
+  while (end_bit < 64 && ((uint64_t)(b->size - 1) >> end_bit) != 0) ++end_bit;
+  size_t tmp_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint32_t*)nullptr, (int)np, 0, end_bit, c->stream);
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  uint64_t need = 2 * al(np * 8) + 2 * al(np * 4) + 2 * al(np) + al(tmp_bytes);
+  uint8_t* w = c->work(need);
+  uint64_t* idx_in = reinterpret_cast<uint64_t*>(w);
+  uint64_t* idx_out = reinterpret_cast<uint64_t*>(w + al(np * 8));
+  uint32_t* seq_in = reinterpret_cast<uint32_t*>(w + 2 * al(np * 8));
+  uint32_t* seq_out = reinterpret_cast<uint32_t*>(w + 2 * al(np * 8) + al(np * 4));
+  uint8_t* pclear = w + 2 * al(np * 8) + 2 * al(np * 4);
+  uint8_t* found0 = pclear + al(np);
+  void* tmp = found0 + al(np);
+  ProfScope ps(c, "bloom_add_each");
+  hipLaunchKernelGGL(bloom_probe_kernel, dim3(grid_for(c, n)), dim3(256), 0, c->stream, k.data, k.offsets, k.fixed_len,
+                     n, b->d_bits, b->fm, b->k, idx_in, seq_in, pclear);
+  RSK_CHECK_LAUNCH("bloom_probe");
+  RSK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, idx_in, idx_out, seq_in, seq_out, (int)np, 0, end_bit,
+                                             c->stream));
+  hipLaunchKernelGGL(bloom_first_kernel, dim3(grid_for(c, np)), dim3(256), 0, c->stream, idx_out, seq_out, np, pclear,
+                     found0);
+  RSK_CHECK_LAUNCH("bloom_first");
+  hipLaunchKernelGGL(bloom_reply_kernel, dim3(grid_for(c, n)), dim3(256), 0, c->stream, found0, n, b->k, d_out);
+  RSK_CHECK_LAUNCH("bloom_reply");
+  bloom_add_launch(c, b, k);
+}
+
+// BITCOUNT over the filter words.
+__global__ __launch_bounds__(256) void popcount_kernel(const uint32_t* __restrict__ w, uint64_t nwords,
+                                                       unsigned long long* __restrict__ out) {
+  uint64_t acc = 0;
+  const uint64_t n4 = nwords / 4;
+  const uint4* w4 = reinterpret_cast<const uint4*>(w);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 v = ld_nt16(&w4[i]);
+    acc += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+  }
+  for (uint64_t i = n4 * 4 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    acc += __popc(w[i]);
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+  __shared__ uint64_t part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+}
+
+void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out) {
+  RSK_HIP(hipMemsetAsync(d_out, 0, 8, c->stream));
+  uint64_t g = (nwords / 4 + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 8;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  ProfScope ps(c, "bitcount");
+  hipLaunchKernelGGL(popcount_kernel, dim3((uint32_t)g), dim3(256), 0, c->stream, d_bits, nwords,
+                     reinterpret_cast<unsigned long long*>(d_out));
+  RSK_CHECK_LAUNCH("bitcount");
+}
+
+// bits |= src (byte string of nbytes), the receive side of a slice-OR merge.
+__global__ __launch_bounds__(256) void or_bytes_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                       uint64_t nbytes) {
+  const uint64_t n16 = nbytes / 16;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 a = reinterpret_cast<uint4*>(dst)[i];
+    uint4 b;
+    __builtin_memcpy(&b, src + 16 * i, 16);
+    reinterpret_cast<uint4*>(dst)[i] = make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+  }
+  for (uint64_t i = n16 * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] |= src[i];
+}
+
+void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes) {
+  uint64_t g = (nbytes / 16 + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 8;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  ProfScope ps(c, "bloom_or");
+  hipLaunchKernelGGL(or_bytes_kernel, dim3((uint32_t)g), dim3(256), 0, c->stream, reinterpret_cast<uint8_t*>(d_bits),
+                     d_src, nbytes);
+  RSK_CHECK_LAUNCH("bloom_or");
+}
+
+}  // namespace rsk

@@ -1,0 +1,115 @@
+// rsk_gen.hip -- on-device synthetic key streams, so that the
+// benchmark inputs are resident in HBM before the timed region.  The same
+// streams are restated on the CPU in oracle/rsk_oracle.c (orc_gen_*).
+#include <hipcub/hipcub.hpp>
+
+#include "rsk_internal.h"
+
+namespace rsk {
+
+// C2: key i = (splitmix64(s+2i), splitmix64(s+2i+1)) little-endian.
+__global__ void gen_keys16_kernel(uint64_t seed, uint64_t start, uint64_t n, uint4* __restrict__ out) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i = start + j;
+    uint64_t lo = splitmix64(seed + 2 * i), hi = splitmix64(seed + 2 * i + 1);
+    out[j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+}
+
+// C5: group = splitmix64(s+3i) mod G, key = (splitmix64(s+3i+1), splitmix64(s+3i+2)).
+__global__ void gen_grouped_kernel(uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* __restrict__ groups,
+                                   uint4* __restrict__ keys) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i = start + j;
+    groups[j] = (uint32_t)(splitmix64(seed + 3 * i) % G);
+    uint64_t lo = splitmix64(seed + 3 * i + 1), hi = splitmix64(seed + 3 * i + 2);
+    keys[j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+}
+
+// C3 queries: r = splitmix64(q+3j); r&1 -> inserted key (r>>1) mod n_ins,
+// else fresh (splitmix64(q+3j+1), splitmix64(q+3j+2)).
+__global__ void gen_queries16_kernel(uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
+                                     uint4* __restrict__ out) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t q = start + j;
+    uint64_t r = splitmix64(qseed + 3 * q);
+    uint64_t lo, hi;
+    if (r & 1) {
+      uint64_t i = (r >> 1) % n_ins;
+      lo = splitmix64(iseed + 2 * i);
+      hi = splitmix64(iseed + 2 * i + 1);
+    } else {
+      lo = splitmix64(qseed + 3 * q + 1);
+      hi = splitmix64(qseed + 3 * q + 2);
+    }
+    out[j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+}
+
+// C4: len_i = 8 + splitmix64(s ^ i) mod 57, bytes 0x21 + (b mod 94) with b
+// the bytes of splitmix64(s + 8i + w).  Lengths are written to offs[j+1];
+// the caller scans them into offsets.
+__global__ void gen_varlen_len_kernel(uint64_t seed, uint64_t start, uint64_t n, uint64_t* __restrict__ offs) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    offs[j + 1] = 8 + splitmix64(seed ^ (start + j)) % 57;
+  }
+}
+
+__global__ void gen_varlen_bytes_kernel(uint64_t seed, uint64_t start, uint64_t n, const uint64_t* __restrict__ offs,
+                                        uint8_t* __restrict__ blob) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i = start + j;
+    uint64_t s = offs[j], len = offs[j + 1] - s;
+    for (uint32_t w = 0; w * 8 < len; ++w) {
+      uint64_t r = splitmix64(seed + (i << 3) + w);
+      for (uint32_t b = 0; b < 8 && w * 8 + b < len; ++b)
+        blob[s + w * 8 + b] = (uint8_t)(0x21 + ((r >> (8 * b)) & 0xFF) % 94);
+    }
+  }
+}
+
+static uint32_t gen_grid(rsk_ctx* c, uint64_t n) {
+  uint64_t g = (n + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 16;
+  return (uint32_t)(g < cap ? (g ? g : 1) : cap);
+}
+
+void gen_keys16_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* out) {
+  hipLaunchKernelGGL(gen_keys16_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, seed, start, n,
+                     reinterpret_cast<uint4*>(out));
+  RSK_CHECK_LAUNCH("gen_keys16");
+}
+
+void gen_grouped_launch(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* g, void* keys) {
+  hipLaunchKernelGGL(gen_grouped_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, seed, G, start, n, g,
+                     reinterpret_cast<uint4*>(keys));
+  RSK_CHECK_LAUNCH("gen_grouped");
+}
+
+void gen_queries16_launch(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
+                          void* out) {
+  hipLaunchKernelGGL(gen_queries16_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, qseed, iseed, n_ins, start,
+                     n, reinterpret_cast<uint4*>(out));
+  RSK_CHECK_LAUNCH("gen_queries16");
+}
+
+void gen_varlen_lengths_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* offsets) {
+  RSK_HIP(hipMemsetAsync(offsets, 0, 8, c->stream));
+  hipLaunchKernelGGL(gen_varlen_len_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, seed, start, n, offsets);
+  RSK_CHECK_LAUNCH("gen_varlen_len");
+  // Inclusive scan of offsets[1..n] in place (offsets[0] = 0).
+  size_t tmp_bytes = 0;
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, offsets + 1, offsets + 1, (int)n, c->stream);
+  void* tmp = c->work(tmp_bytes + 256);
+  RSK_HIP(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, offsets + 1, offsets + 1, (int)n, c->stream));
+}
+
+void gen_varlen_bytes_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, const uint64_t* offsets,
+                             uint8_t* blob) {
+  hipLaunchKernelGGL(gen_varlen_bytes_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, seed, start, n, offsets,
+                     blob);
+  RSK_CHECK_LAUNCH("gen_varlen_bytes");
+}
+
+}  // namespace rsk

@@ -1,0 +1,595 @@
+// rsk_hll.hip -- HyperLogLog kernels for gfx950 (Redis 3.2.0 semantics).
+//
+// Replaces the PFADD / PFCOUNT / PFMERGE arithmetic that RedissonHyperLogLog
+// (src/main/java/org/redisson/RedissonHyperLogLog.java:65-97) delegates to the
+// Redis server (hyperloglog.c: hllAdd/hllPatLen, hllCount, pfmergeCommand).
+//
+// Data layout in HBM: a pool of sketches, [n][16384] raw registers, one byte
+// each (Redis's internal HLL_RAW form); the 6-bit dense packing only exists
+// at the Redis export/import boundary.  Each pool also keeps card[n], the
+// 8-byte cardinality cache of the Redis header.
+//
+// PFADD (streaming, HBM-bound): a persistent grid of 2 workgroups per CU.
+// Every workgroup owns a private 16384 x u32 register file in LDS (64 KiB,
+// so two fit in the CU's 160 KiB), streams a contiguous slice of the key
+// array with 16-byte loads, hashes each key and applies ds_max_u32.  At the
+// end it writes its file as 16 KiB of bytes (a "slab"); one reduce kernel
+// max-merges all slabs and the sketch's old registers (deterministic, no
+// global atomics), and raises a flag if any register grew.
+#include <hipcub/hipcub.hpp>
+
+#include "rsk_internal.h"
+
+namespace rsk {
+
+// Byte-wise max of four 7-bit lanes (registers are <= 63).
+RSK_DEV uint32_t bmax4(uint32_t a, uint32_t b) {
+  uint32_t d = (a | 0x80808080u) - b;
+  uint32_t m = ((d & 0x80808080u) >> 7) * 0xFFu;
+  return (a & m) | (b & ~m);
+}
+RSK_DEV uint4 bmax16(uint4 a, uint4 b) {
+  return make_uint4(bmax4(a.x, b.x), bmax4(a.y, b.y), bmax4(a.z, b.z), bmax4(a.w, b.w));
+}
+
+// ------------------------------------------------------------------ PFADD
+__device__ __forceinline__ void lds_zero(uint32_t* regs) {
+  uint4* r4 = reinterpret_cast<uint4*>(regs);
+  for (int j = threadIdx.x; j < HLL_REGS / 4; j += blockDim.x) r4[j] = make_uint4(0, 0, 0, 0);
+}
+
+// Pack the LDS file (u32 per register) into 16384 bytes of the slab.
+__device__ __forceinline__ void lds_to_slab(const uint32_t* regs, uint8_t* slab) {
+  const uint4* r4 = reinterpret_cast<const uint4*>(regs);
+  uint4* out = reinterpret_cast<uint4*>(slab);
+  for (int j = threadIdx.x; j < HLL_REGS / 16; j += blockDim.x) {
+    uint4 a = r4[4 * j], b = r4[4 * j + 1], c = r4[4 * j + 2], d = r4[4 * j + 3];
+    uint4 o;
+    o.x = a.x | (a.y << 8) | (a.z << 16) | (a.w << 24);
+    o.y = b.x | (b.y << 8) | (b.z << 16) | (b.w << 24);
+    o.z = c.x | (c.y << 8) | (c.z << 16) | (c.w << 24);
+    o.w = d.x | (d.y << 8) | (d.z << 16) | (d.w << 24);
+    out[j] = o;
+  }
+}
+
+RSK_DEV void hll_update(uint32_t* regs, uint64_t h) {
+  atomicMax(&regs[hll_index(h)], hll_rank(h));
+}
+
+// Fixed 16-byte keys: the C2 hot path.  U keys per lane in flight.
+template <int U>
+__global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add16_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                                       uint64_t per_block,
+                                                                       uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
+  lds_zero(regs);
+  __syncthreads();
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  constexpr int T = RSK_ADD_THREADS;
+  uint64_t i = begin + threadIdx.x;
+  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[i + (uint64_t)u * T]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x;
+      uint64_t w1 = ((uint64_t)v[u].w << 32) | v[u].z;
+      hll_update(regs, murmur64a_16(w0, w1));
+    }
+  }
+  for (; i < end; i += T) {
+    uint4 v = keys[i];
+    hll_update(regs, murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z));
+  }
+  __syncthreads();
+  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// Any fixed stride or blob+offsets: lane-per-key MurmurHash64A.
+template <bool VAR>
+__global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add_bytes_kernel(const uint8_t* __restrict__ data,
+                                                                           const uint64_t* __restrict__ offsets,
+                                                                           uint32_t fixed_len, uint64_t n,
+                                                                           uint64_t per_block,
+                                                                           uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
+  lds_zero(regs);
+  __syncthreads();
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  for (uint64_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+    uint64_t s, len;
+    if (VAR) {
+      s = offsets[i];
+      len = offsets[i + 1] - s;
+    } else {
+      s = i * fixed_len;
+      len = fixed_len;
+    }
+    hll_update(regs, murmur64a(data + s, len));
+  }
+  __syncthreads();
+  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// Max-merge `nslabs` slabs and the sketch's registers; 64 registers per
+// workgroup of 256 lanes (grid 256).  *flag |= 1 if any register grew.
+__global__ __launch_bounds__(256) void hll_reduce_kernel(const uint8_t* __restrict__ slabs, uint32_t nslabs,
+                                                         uint8_t* __restrict__ regs, uint32_t* __restrict__ flag) {
+  __shared__ uint4 part[4][256];
+  const int t = threadIdx.x;
+  const uint64_t col = (uint64_t)blockIdx.x * 64;  // first register of this block
+  uint4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = make_uint4(0, 0, 0, 0);
+  for (uint32_t s = t; s < nslabs; s += 256) {
+    const uint4* p = reinterpret_cast<const uint4*>(slabs + (uint64_t)s * HLL_REGS + col);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = bmax16(acc[q], p[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) part[q][t] = acc[q];
+  __syncthreads();
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (t < stride) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[q][t] = bmax16(part[q][t], part[q][t + stride]);
+    }
+    __syncthreads();
+  }
+  if (t < 4) {
+    uint4* r = reinterpret_cast<uint4*>(regs + col) + t;
+    uint4 old = *r;
+    uint4 nw = bmax16(old, part[t][0]);
+    if (nw.x != old.x || nw.y != old.y || nw.z != old.z || nw.w != old.w) {
+      *r = nw;
+      atomicOr(flag, 1u);
+    }
+  }
+}
+
+void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32_t* d_flag) {
+  if (k.n == 0) return;
+  constexpr uint64_t T = RSK_ADD_THREADS;
+  uint64_t max_blocks = c->slab_count;
+  // Enough keys per workgroup to amortise the 64 KiB LDS init + 16 KiB slab.
+  uint64_t blocks = (k.n + 4 * T - 1) / (4 * T);
+  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks == 0) blocks = 1;
+  uint64_t per_block = (k.n + blocks - 1) / blocks;
+  if (k.offsets == nullptr && k.fixed_len == 16 && (reinterpret_cast<uintptr_t>(k.data) & 15) == 0) {
+    // Round the slice up to whole tiles so every lane's loads stay coalesced.
+    const uint64_t tile = T * RSK_ADD_UNROLL;
+    per_block = (per_block + tile - 1) / tile * tile;
+    blocks = (k.n + per_block - 1) / per_block;
+    ProfScope ps(c, "hll_add16");
+    hipLaunchKernelGGL(hll_add16_kernel<RSK_ADD_UNROLL>, dim3((uint32_t)blocks), dim3(T), 0, c->stream,
+                       reinterpret_cast<const uint4*>(k.data), k.n, per_block, c->d_slab);
+    RSK_CHECK_LAUNCH("hll_add16");
+  } else if (k.offsets == nullptr) {
+    ProfScope ps(c, "hll_add_fixed");
+    hipLaunchKernelGGL(hll_add_bytes_kernel<false>, dim3((uint32_t)blocks), dim3(T), 0, c->stream, k.data, nullptr,
+                       k.fixed_len, k.n, per_block, c->d_slab);
+    RSK_CHECK_LAUNCH("hll_add_fixed");
+  } else {
+    ProfScope ps(c, "hll_add_var");
+    hipLaunchKernelGGL(hll_add_bytes_kernel<true>, dim3((uint32_t)blocks), dim3(T), 0, c->stream, k.data,
+                       k.offsets, 0u, k.n, per_block, c->d_slab);
+    RSK_CHECK_LAUNCH("hll_add_var");
+  }
+  ProfScope ps(c, "hll_reduce");
+  hipLaunchKernelGGL(hll_reduce_kernel, dim3(HLL_REGS / 64), dim3(256), 0, c->stream, c->d_slab, (uint32_t)blocks,
+                     d_regs_sketch, d_flag);
+  RSK_CHECK_LAUNCH("hll_reduce");
+}
+
+// dst = max(dst, src) for one sketch; flag if dst grew (PFMERGE from raw).
+__global__ __launch_bounds__(256) void hll_max_into_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                           uint32_t* __restrict__ flag) {
+  const int j = blockIdx.x * 256 + threadIdx.x;  // uint4 index, 1024 total
+  uint4* d = reinterpret_cast<uint4*>(dst) + j;
+  uint4 a = *d, b = reinterpret_cast<const uint4*>(src)[j];
+  uint4 m = bmax16(a, b);
+  if (m.x != a.x || m.y != a.y || m.z != a.z || m.w != a.w) {
+    *d = m;
+    if (flag) atomicOr(flag, 1u);
+  }
+}
+
+void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag) {
+  ProfScope ps(c, "hll_max_into");
+  hipLaunchKernelGGL(hll_max_into_kernel, dim3(HLL_REGS / 16 / 256), dim3(256), 0, c->stream, d_dst, d_src, d_flag);
+  RSK_CHECK_LAUNCH("hll_max_into");
+}
+
+// --------------------------------------------------------- grouped PFADD
+// Pair i -> sketch groups[i]; byte-max on the register's u32 word by CAS.
+__global__ __launch_bounds__(256) void hll_add_grouped16_kernel(const uint4* __restrict__ keys,
+                                                                const uint32_t* __restrict__ groups, uint64_t n,
+                                                                uint8_t* __restrict__ regs, uint64_t G) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 v = ld_nt16(&keys[i]);
+    uint32_t g = __builtin_nontemporal_load(&groups[i]);
+    if (g >= G) continue;
+    uint64_t h = murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
+    uint32_t idx = hll_index(h), rank = hll_rank(h);
+    uint32_t* word = reinterpret_cast<uint32_t*>(regs + (uint64_t)g * HLL_REGS + (idx & ~3u));
+    const uint32_t sh = (idx & 3u) * 8;
+    uint32_t old = *word;
+    while (((old >> sh) & 0xFF) < rank) {
+      uint32_t nw = (old & ~(0xFFu << sh)) | (rank << sh);
+      uint32_t prev = atomicCAS(word, old, nw);
+      if (prev == old) break;
+      old = prev;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void hll_add_grouped_bytes_kernel(const uint8_t* __restrict__ data,
+                                                                    const uint64_t* __restrict__ offsets,
+                                                                    uint32_t fixed_len,
+                                                                    const uint32_t* __restrict__ groups, uint64_t n,
+                                                                    uint8_t* __restrict__ regs, uint64_t G) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t g = groups[i];
+    if (g >= G) continue;
+    uint64_t s = offsets ? offsets[i] : i * fixed_len;
+    uint64_t len = offsets ? offsets[i + 1] - s : fixed_len;
+    uint64_t h = murmur64a(data + s, len);
+    uint32_t idx = hll_index(h), rank = hll_rank(h);
+    uint32_t* word = reinterpret_cast<uint32_t*>(regs + (uint64_t)g * HLL_REGS + (idx & ~3u));
+    const uint32_t sh = (idx & 3u) * 8;
+    uint32_t old = *word;
+    while (((old >> sh) & 0xFF) < rank) {
+      uint32_t nw = (old & ~(0xFFu << sh)) | (rank << sh);
+      uint32_t prev = atomicCAS(word, old, nw);
+      if (prev == old) break;
+      old = prev;
+    }
+  }
+}
+
+void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G) {
+  if (k.n == 0) return;
+  uint64_t blocks = (k.n + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 16;
+  if (blocks > cap) blocks = cap;
+  if (k.offsets == nullptr && k.fixed_len == 16 && (reinterpret_cast<uintptr_t>(k.data) & 15) == 0) {
+    ProfScope ps(c, "hll_add_grouped16");
+    hipLaunchKernelGGL(hll_add_grouped16_kernel, dim3((uint32_t)blocks), dim3(256), 0, c->stream,
+                       reinterpret_cast<const uint4*>(k.data), d_groups, k.n, d_regs, G);
+    RSK_CHECK_LAUNCH("hll_add_grouped16");
+  } else {
+    ProfScope ps(c, "hll_add_grouped");
+    hipLaunchKernelGGL(hll_add_grouped_bytes_kernel, dim3((uint32_t)blocks), dim3(256), 0, c->stream, k.data,
+                       k.offsets, k.fixed_len, d_groups, k.n, d_regs, G);
+    RSK_CHECK_LAUNCH("hll_add_grouped");
+  }
+}
+
+// ---------------------------------------------------------------- PFCOUNT
+RSK_DEV double pe(uint32_t r) {  // 2^-r, exact
+  return __longlong_as_double((long long)((uint64_t)(1023 - r) << 52));
+}
+
+// hllCount tail (Redis 3.2.0), FP64, compiled with -ffp-contract=off.
+// lc[ez] = m*log(m/ez) from the host libm.
+RSK_DEV uint64_t hll_estimate(double E, int ez, const double* __restrict__ lc) {
+  const double m = HLL_REGS;
+  double alpha = 0.7213 / (1 + 1.079 / m);
+  E = (1 / E) * alpha * m * m;
+  if (E < m * 2.5 && ez != 0) {
+    E = lc[ez];
+  } else if (E < 72000) {
+    double bias = 5.9119 * 1.0e-18 * (E * E * E * E) - 1.4253 * 1.0e-12 * (E * E * E) +
+                  1.2940 * 1.0e-7 * (E * E) - 5.2921 * 1.0e-3 * E + 83.3216;
+    E -= E * (bias / 100);
+  }
+  return (uint64_t)E;
+}
+
+// Redis sums 2^-reg in an encoding-specific order.  All orders agree when
+// every partial sum is exact, i.e. when the span from the smallest term
+// 2^-rmax to the top bit of the total fits 53 bits; the kernel checks this
+// on the exact fixed-point total and only otherwise replays Redis's order
+// (dense: groups of 16; raw: u64 words) serially.  Sparse keys always take
+// the exact path (registers <= 32).
+struct SumParts {
+  uint64_t inz;  // sum over nonzero registers of 2^(50-r)
+  uint32_t ez;
+  uint32_t rmax;
+};
+
+RSK_DEV void acc_word(SumParts& s, uint32_t w) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    uint32_t r = (w >> (8 * b)) & 0xFF;
+    if (r == 0) s.ez++;
+    else s.inz += 1ULL << (50 - r);
+    s.rmax = r > s.rmax ? r : s.rmax;
+  }
+}
+
+// Block reduction of SumParts over 256 lanes.
+__device__ __forceinline__ SumParts block_reduce(SumParts s) {
+  __shared__ uint64_t sh_inz[4];
+  __shared__ uint32_t sh_ez[4], sh_rmax[4];
+  for (int off = 32; off > 0; off >>= 1) {
+    s.inz += __shfl_down(s.inz, off, 64);
+    s.ez += __shfl_down(s.ez, off, 64);
+    uint32_t o = __shfl_down(s.rmax, off, 64);
+    s.rmax = o > s.rmax ? o : s.rmax;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh_inz[wv] = s.inz;
+    sh_ez[wv] = s.ez;
+    sh_rmax[wv] = s.rmax;
+  }
+  __syncthreads();
+  SumParts r{0, 0, 0};
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 4; ++q) {
+      r.inz += sh_inz[q];
+      r.ez += sh_ez[q];
+      r.rmax = sh_rmax[q] > r.rmax ? sh_rmax[q] : r.rmax;
+    }
+  }
+  return r;
+}
+
+// Exact E when every summation order is exact; returns false otherwise.
+RSK_DEV bool exact_sum(const SumParts& s, double* E) {
+  // V = ez*2^50 + inz, in units of 2^-50; up to 2^64 -> two limbs.
+  uint64_t lo = ((uint64_t)s.ez << 50) + s.inz;
+  uint64_t hi = ((uint64_t)s.ez >> 14) + (lo < s.inz ? 1 : 0);
+  int bl = hi ? 64 + (64 - __builtin_clzll(hi)) : (64 - __builtin_clzll(lo));
+  int low_unit = 50 - (int)s.rmax;  // smallest term is 2^(50-rmax) units
+  if (s.rmax == 0) low_unit = 50;
+  if (bl - low_unit > 53) return false;
+  *E = (double)lo * 0x1p-50 + (double)hi * 0x1p14;
+  return true;
+}
+
+RSK_DEV double dense_order_sum(const uint8_t* r, int* ezp) {
+  double E = 0;
+  int ez = 0;
+  for (int g = 0; g < HLL_REGS / 16; ++g) {
+    const uint8_t* q = r + 16 * g;
+    for (int t = 0; t < 16; ++t) ez += q[t] == 0;
+    E += (pe(q[0]) + pe(q[1])) + (pe(q[2]) + pe(q[3])) + (pe(q[4]) + pe(q[5])) + (pe(q[6]) + pe(q[7])) +
+         (pe(q[8]) + pe(q[9])) + (pe(q[10]) + pe(q[11])) + (pe(q[12]) + pe(q[13])) + (pe(q[14]) + pe(q[15]));
+  }
+  *ezp = ez;
+  return E;
+}
+
+__global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
+                                                        const uint64_t* __restrict__ ids, uint64_t n,
+                                                        const double* __restrict__ lc, uint64_t* __restrict__ out) {
+  for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const uint64_t id = ids ? ids[b] : b;
+    const uint64_t cached = card[id];
+    if ((cached >> 63) == 0) {  // HLL_VALID_CACHE
+      if (threadIdx.x == 0) out[b] = cached;
+      continue;
+    }
+    const uint8_t* r = regs + id * HLL_REGS;
+    SumParts s{0, 0, 0};
+    const uint4* r4 = reinterpret_cast<const uint4*>(r);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint4 v = r4[threadIdx.x + 256 * q];
+      acc_word(s, v.x);
+      acc_word(s, v.y);
+      acc_word(s, v.z);
+      acc_word(s, v.w);
+    }
+    s = block_reduce(s);
+    if (threadIdx.x == 0) {
+      double E;
+      int ez = (int)s.ez;
+      if (!exact_sum(s, &E)) E = dense_order_sum(r, &ez);
+      uint64_t v = hll_estimate(E, ez, lc);
+      out[b] = v;
+      card[id] = v;  // cache refreshed, valid
+    }
+    __syncthreads();
+  }
+}
+
+void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids, uint64_t n,
+                      uint64_t* d_out) {
+  if (n == 0) return;
+  uint64_t grid = n < (1u << 20) ? n : (1u << 20);
+  ProfScope ps(c, "hll_count");
+  hipLaunchKernelGGL(hll_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_regs, d_card, d_ids, n, c->d_lc,
+                     d_out);
+  RSK_CHECK_LAUNCH("hll_count");
+}
+
+RSK_DEV double raw_order_sum(const uint8_t* const* members, uint32_t arity, int* ezp) {
+  double E = 0;
+  int ez = 0;
+  for (int j = 0; j < HLL_REGS / 8; ++j) {
+    uint8_t b[8];
+    uint64_t word = 0;
+    for (int t = 0; t < 8; ++t) {
+      uint8_t m = 0;
+      for (uint32_t a = 0; a < arity; ++a) {
+        uint8_t x = members[a][8 * j + t];
+        m = x > m ? x : m;
+      }
+      b[t] = m;
+      word |= (uint64_t)m << (8 * t);
+    }
+    if (word == 0) {
+      ez += 8;
+    } else {
+      for (int t = 0; t < 8; ++t) {
+        if (b[t]) E += pe(b[t]);
+        else ez++;
+      }
+    }
+  }
+  E += ez;
+  *ezp = ez;
+  return E;
+}
+
+// Multi-key PFCOUNT: union of `arity` sketches into HLL_RAW, raw-order sum.
+__global__ __launch_bounds__(256) void hll_union_count_kernel(const uint8_t* const* __restrict__ member_ptrs,
+                                                              uint32_t arity, uint64_t n,
+                                                              const double* __restrict__ lc,
+                                                              uint64_t* __restrict__ out) {
+  for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const uint8_t* const* mem = member_ptrs + b * arity;
+    SumParts s{0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      for (uint32_t a = 0; a < arity; ++a) {
+        if (mem[a] == nullptr) continue;
+        v = bmax16(v, reinterpret_cast<const uint4*>(mem[a])[threadIdx.x + 256 * q]);
+      }
+      acc_word(s, v.x);
+      acc_word(s, v.y);
+      acc_word(s, v.z);
+      acc_word(s, v.w);
+    }
+    s = block_reduce(s);
+    if (threadIdx.x == 0) {
+      double E;
+      int ez = (int)s.ez;
+      if (!exact_sum(s, &E)) {
+        // Absent members contribute zeros: compact the pointer list.
+        const uint8_t* live[64];
+        uint32_t na = 0;
+        for (uint32_t a = 0; a < arity && na < 64; ++a)
+          if (mem[a]) live[na++] = mem[a];
+        E = raw_order_sum(live, na, &ez);
+      }
+      out[b] = hll_estimate(E, ez, lc);
+    }
+    __syncthreads();
+  }
+}
+
+void hll_union_count_launch(rsk_ctx* c, const uint8_t* const* d_member_ptrs, uint32_t arity, uint64_t n,
+                            uint64_t* d_out) {
+  if (n == 0) return;
+  uint64_t grid = n < (1u << 20) ? n : (1u << 20);
+  ProfScope ps(c, "hll_union_count");
+  hipLaunchKernelGGL(hll_union_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_member_ptrs, arity, n,
+                     c->d_lc, d_out);
+  RSK_CHECK_LAUNCH("hll_union_count");
+}
+
+// PFMERGE: dst[i] = max(dst[i], srcs[i][0..k)); null src = absent key.
+__global__ __launch_bounds__(256) void hll_merge_kernel(uint8_t* const* __restrict__ dst_ptrs,
+                                                        const uint8_t* const* __restrict__ src_ptrs, uint32_t k,
+                                                        uint64_t n) {
+  for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+    uint4* d = reinterpret_cast<uint4*>(dst_ptrs[b]);
+    const uint8_t* const* srcs = src_ptrs + b * k;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = threadIdx.x + 256 * q;
+      uint4 v = d[j];
+      for (uint32_t a = 0; a < k; ++a)
+        if (srcs[a]) v = bmax16(v, reinterpret_cast<const uint4*>(srcs[a])[j]);
+      d[j] = v;
+    }
+  }
+}
+
+void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* const* d_src_ptrs, uint32_t srcs_per_dst,
+                      uint64_t n) {
+  if (n == 0) return;
+  uint64_t grid = n < (1u << 20) ? n : (1u << 20);
+  ProfScope ps(c, "hll_merge");
+  hipLaunchKernelGGL(hll_merge_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_dst_ptrs, d_src_ptrs,
+                     srcs_per_dst, n);
+  RSK_CHECK_LAUNCH("hll_merge");
+}
+
+// ------------------------------------------- PFADD one element at a time
+// Element i replies 1 iff rank_i > max(reg0[idx_i], ranks of earlier
+// elements with the same index).  Elements are radix-sorted by register
+// index (stable, so input order survives inside a register), then one lane
+// per register walks its run.
+__global__ void hll_each_hash_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+                                     uint32_t fixed_len, uint64_t n, uint32_t* __restrict__ key_idx,
+                                     uint32_t* __restrict__ seq, uint8_t* __restrict__ rank) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t s = offsets ? offsets[i] : i * fixed_len;
+    uint64_t len = offsets ? offsets[i + 1] - s : fixed_len;
+    uint64_t h = murmur64a(data + s, len);
+    key_idx[i] = hll_index(h);
+    seq[i] = (uint32_t)i;
+    rank[i] = (uint8_t)hll_rank(h);
+  }
+}
+
+__global__ void hll_each_bounds_kernel(const uint32_t* __restrict__ sorted_idx, uint64_t n,
+                                       uint32_t* __restrict__ run_start) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
+    if (p == 0 || sorted_idx[p] != sorted_idx[p - 1]) run_start[sorted_idx[p]] = (uint32_t)p;
+  }
+}
+
+__global__ void hll_each_walk_kernel(const uint32_t* __restrict__ sorted_idx, const uint32_t* __restrict__ sorted_seq,
+                                     const uint8_t* __restrict__ rank, const uint32_t* __restrict__ run_start,
+                                     uint64_t n, uint8_t* __restrict__ regs, uint8_t* __restrict__ out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= HLL_REGS) return;
+  uint32_t p = run_start[r];
+  if (p == 0xFFFFFFFFu) return;
+  uint32_t running = regs[r];
+  for (; p < n && sorted_idx[p] == r; ++p) {
+    uint32_t i = sorted_seq[p];
+    uint32_t c = rank[i];
+    out[i] = c > running;
+    running = c > running ? c : running;
+  }
+  regs[r] = (uint8_t)running;
+}
+
+void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out) {
+  // d_regs_sketch is updated in place (const only for signature symmetry).
+  uint8_t* regs = const_cast<uint8_t*>(d_regs_sketch);
+  const uint64_t n = k.n;
+  if (n == 0) return;
+  size_t tmp_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint32_t*)nullptr, (int)n, 0, HLL_P, c->stream);
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  uint64_t need = 4 * al(n * 4) + al(n) + al(HLL_REGS * 4) + al(tmp_bytes);
+  uint8_t* w = c->work(need);
+  uint32_t* idx_in = reinterpret_cast<uint32_t*>(w);
+  uint32_t* idx_out = reinterpret_cast<uint32_t*>(w + al(n * 4));
+  uint32_t* seq_in = reinterpret_cast<uint32_t*>(w + 2 * al(n * 4));
+  uint32_t* seq_out = reinterpret_cast<uint32_t*>(w + 3 * al(n * 4));
+  uint8_t* rank = w + 4 * al(n * 4);
+  uint32_t* run_start = reinterpret_cast<uint32_t*>(w + 4 * al(n * 4) + al(n));
+  void* tmp = w + 4 * al(n * 4) + al(n) + al(HLL_REGS * 4);
+  uint64_t grid = (n + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  ProfScope ps(c, "hll_add_each");
+  hipLaunchKernelGGL(hll_each_hash_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, k.data, k.offsets,
+                     k.fixed_len, n, idx_in, seq_in, rank);
+  RSK_CHECK_LAUNCH("hll_each_hash");
+  RSK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, idx_in, idx_out, seq_in, seq_out, (int)n, 0, HLL_P,
+                                             c->stream));
+  RSK_HIP(hipMemsetAsync(run_start, 0xFF, HLL_REGS * 4, c->stream));
+  hipLaunchKernelGGL(hll_each_bounds_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, idx_out, n, run_start);
+  RSK_CHECK_LAUNCH("hll_each_bounds");
+  hipLaunchKernelGGL(hll_each_walk_kernel, dim3(HLL_REGS / 256), dim3(256), 0, c->stream, idx_out, seq_out, rank,
+                     run_start, n, regs, d_out);
+  RSK_CHECK_LAUNCH("hll_each_walk");
+}
+
+}  // namespace rsk

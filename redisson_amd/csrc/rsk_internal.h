@@ -1,0 +1,158 @@
+// rsk_internal.h -- host-side internals shared by the librsketch translation
+// units (context, handles, error plumbing, kernel launchers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsketch.h"
+#include "rsk_device.h"
+
+namespace rsk {
+
+void set_error(const std::string& msg);
+
+struct RskError {
+  int code;
+  std::string msg;
+};
+
+#define RSK_HIP(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess)                                                                       \
+      throw ::rsk::RskError{(_e == hipErrorOutOfMemory) ? RSK_ERR_OUT_OF_MEMORY : RSK_ERR_DEVICE, \
+                            std::string(#expr) + ": " + hipGetErrorString(_e)};                 \
+  } while (0)
+
+#define RSK_CHECK_LAUNCH(name)                                                              \
+  do {                                                                                      \
+    hipError_t _e = hipGetLastError();                                                      \
+    if (_e != hipSuccess)                                                                   \
+      throw ::rsk::RskError{RSK_ERR_DEVICE, std::string("launch ") + (name) + ": " + hipGetErrorString(_e)}; \
+  } while (0)
+
+struct ProfEntry {
+  double ms = 0;
+  uint64_t launches = 0;
+};
+
+// Kernel-time accounting: start/stop events around each launch on the
+// context stream, folded into per-kernel totals when read.
+struct Profiler {
+  bool on = false;
+  std::vector<hipEvent_t> free_events;
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::map<std::string, ProfEntry> totals;
+};
+
+}  // namespace rsk
+
+constexpr int RSK_ADD_THREADS = 512;     // HLL add workgroup (8 waves)
+constexpr int RSK_ADD_UNROLL = 4;        // 16-byte keys in flight per lane
+constexpr int RSK_MAX_SLABS = 4096;      // partial register files per launch
+
+struct rsk_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  std::recursive_mutex mu;
+  // host -> device staging for RSK_MEM_HOST key batches
+  uint8_t* d_stage = nullptr;
+  uint64_t stage_bytes = 0;
+  // per-workgroup partial register files [slabs][16384] u8
+  uint8_t* d_slab = nullptr;
+  uint32_t slab_count = 0;
+  // small scratch: flags / counters / ids (device) and pinned host mirror
+  uint8_t* d_small = nullptr;
+  uint8_t* h_small = nullptr;
+  uint64_t small_bytes = 0;
+  // grow-on-demand device scratch for batched calls
+  uint8_t* d_work = nullptr;
+  uint64_t work_bytes = 0;
+  // m*log(m/ez) for ez = 0..16384, computed with the host libm (Redis's log)
+  double* d_lc = nullptr;
+  rsk::Profiler prof;
+
+  uint8_t* work(uint64_t bytes);
+};
+
+struct rsk_hll {
+  rsk_ctx* ctx = nullptr;
+  uint64_t n = 0;
+  uint8_t* d_regs = nullptr;   // [n][16384] raw registers (one byte each)
+  uint64_t* d_card = nullptr;  // [n] Redis card[8] as LE u64 (bit 63 = cache invalid)
+  std::vector<uint8_t> exists; // host: key present
+};
+
+struct rsk_bloom {
+  rsk_ctx* ctx = nullptr;
+  int64_t size = 0;            // bits
+  int32_t k = 0;               // hashIterations
+  uint64_t nbytes = 0;         // ceil(size/8): the Redis string length
+  uint64_t nwords = 0;         // u32 words allocated (>= nbytes/4)
+  uint32_t* d_bits = nullptr;  // MSB-first bytes, addressed as LE u32 words
+  rsk::FastMod63 fm{};
+};
+
+namespace rsk {
+
+// ---- profiling helpers (rsk_api.hip)
+void prof_begin(rsk_ctx* c, const char* name, hipEvent_t* a, hipEvent_t* b);
+void prof_end(rsk_ctx* c, const char* name, hipEvent_t a, hipEvent_t b);
+
+struct ProfScope {
+  rsk_ctx* c;
+  const char* name;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(rsk_ctx* c_, const char* n) : c(c_), name(n) { prof_begin(c, name, &a, &b); }
+  ~ProfScope() { prof_end(c, name, a, b); }
+};
+
+// Resolved key batch on the device.
+struct DevKeys {
+  const uint8_t* data;
+  const uint64_t* offsets;  // nullptr for fixed stride
+  uint64_t n;
+  uint32_t fixed_len;
+};
+
+// ---- HLL launchers (rsk_hll.hip)
+// Adds keys into slabs and max-merges them into sketch `id`; sets *d_flag
+// (device u32) to 1 if any register grew.
+void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32_t* d_flag);
+void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G);
+void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids, uint64_t n,
+                      uint64_t* d_out);
+void hll_union_count_launch(rsk_ctx* c, const uint8_t* const* d_member_ptrs, uint32_t arity, uint64_t n,
+                            uint64_t* d_out);
+void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* const* d_src_ptrs, uint32_t srcs_per_dst,
+                      uint64_t n);
+void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out);
+void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag);
+
+// ---- Bloom launchers (rsk_bloom.hip)
+void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
+void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
+void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
+void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out);
+void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes);
+
+// ---- generators (rsk_gen.hip)
+void gen_keys16_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* out);
+void gen_grouped_launch(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* g, void* keys);
+void gen_queries16_launch(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
+                          void* out);
+void gen_varlen_lengths_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* offsets);
+void gen_varlen_bytes_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, const uint64_t* offsets,
+                             uint8_t* blob);
+
+}  // namespace rsk

@@ -1,0 +1,36 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 GPU and the built librsketch.so")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle import oracle as O
+
+    O.lib()
+    return O
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from redisson_amd import Engine
+
+    return Engine.get(0)
+
+
+@pytest.fixture()
+def client():
+    from redisson_amd import Redisson
+
+    c = Redisson.create()
+    yield c
+    c.shutdown()

@@ -1,0 +1,100 @@
+"""The C ABI library loads and exports every symbol include/rsketch.h declares;
+host-only entry points agree with the oracle (CPU only, no kernel launches)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rsketch.h")
+LIB = os.path.join(ROOT, "redisson_amd", "librsketch.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-s", "-C", ROOT, "redisson_amd/librsketch.so"], check=True)
+    from redisson_amd import _lib
+
+    return _lib.load()
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rsk_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_api():
+    names = declared_functions()
+    for must in ("rsk_init", "rsk_hll_add", "rsk_hll_count", "rsk_hll_count_union", "rsk_hll_merge",
+                 "rsk_hll_export_redis", "rsk_hll_import_redis", "rsk_bloom_init", "rsk_bloom_add",
+                 "rsk_bloom_contains", "rsk_bloom_count", "rsk_bloom_export_bits", "rsk_last_error"):
+        assert must in names
+
+
+def test_every_declared_symbol_is_exported(lib):
+    raw = ctypes.CDLL(LIB)
+    missing = [n for n in declared_functions() if not hasattr(raw, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header(lib):
+    from redisson_amd import _lib
+
+    assert set(declared_functions()) == set(_lib.SIGNATURES)
+
+
+def test_abi_version(lib):
+    assert lib.rsk_abi_version() == 1
+
+
+def test_init_without_gpu_fails_loudly(lib):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from redisson_amd import _lib
+
+    opts = _lib.rsk_options(0, 320, 0)
+    h = ctypes.c_void_p()
+    rc = lib.rsk_init(ctypes.byref(opts), ctypes.byref(h))
+    assert rc == _lib.RSK_ERR_NO_DEVICE
+    assert b"device" in lib.rsk_last_error()
+    with pytest.raises(_lib.EngineError):
+        _lib.Engine(0)
+
+
+def test_unsupported_redis_version(lib):
+    from redisson_amd import _lib
+
+    opts = _lib.rsk_options(0, 500, 0)
+    h = ctypes.c_void_p()
+    assert lib.rsk_init(ctypes.byref(opts), ctypes.byref(h)) == _lib.RSK_ERR_INVALID_ARG
+
+
+def test_bloom_params_match_oracle(lib, orc):
+    from redisson_amd.bloom import bloom_params
+
+    for n in (1, 3, 100, 1000, 12345, 55000000, 400000000, 550000000):
+        for p in (0.5, 0.3, 0.1, 0.03, 0.01, 0.001, 1e-5, 1e-9):
+            size = orc.bloom_optimal_bits(n, p)
+            if size > 2147483647 * 2:
+                with pytest.raises(ValueError):
+                    bloom_params(n, p)
+            else:
+                assert bloom_params(n, p) == (size, orc.bloom_optimal_k(n, size))
+            assert bloom_params(n, p, extended=True) == (size, orc.bloom_optimal_k(n, size))
+
+
+def test_bloom_params_reference_values(lib):
+    from redisson_amd import IllegalArgumentException
+    from redisson_amd.bloom import bloom_params
+
+    assert bloom_params(100, 0.03) == (729, 5)                   # RedissonBloomFilterTest.testConfig
+    assert bloom_params(550000000, 0.03) == (4014142460, 5)      # RedissonBloomFilterTest.test
+    with pytest.raises(IllegalArgumentException, match="can't be greater than 4294967294"):
+        bloom_params(10 ** 9, 0.01)                              # MAX_SIZE (RedissonBloomFilter.java:226)
+    assert bloom_params(10 ** 9, 0.01, extended=True) == (9585058377, 7)

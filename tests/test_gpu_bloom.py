@@ -1,0 +1,148 @@
+"""Bloom parity: gfx950 kernels against the CPU oracle (bit-exact bit strings,
+identical add/contains replies), through the C ABI."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from redisson_amd import _lib
+
+    return _lib.load()
+
+
+def _filter(L, engine, size, k):
+    from redisson_amd import _lib
+
+    b = ctypes.c_void_p()
+    _lib.check(L.rsk_bloom_create(engine.ctx, size, k, ctypes.byref(b)))
+    return b
+
+
+def _bits(L, b, size):
+    from redisson_amd import _lib
+
+    out = np.zeros((size + 7) // 8, np.uint8)
+    n = ctypes.c_size_t()
+    _lib.check(L.rsk_bloom_export_bits(b, out.ctypes.data, out.size, ctypes.byref(n)))
+    assert n.value == out.size
+    return out
+
+
+def _add(L, b, kb, replies=True):
+    from redisson_amd import _lib
+
+    out = np.zeros(max(1, kb.n), np.uint8)
+    ks = kb.as_struct()
+    _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), out.ctypes.data if replies else None))
+    return out[: kb.n]
+
+
+def _contains(L, b, kb):
+    from redisson_amd import _lib
+
+    out = np.zeros(max(1, kb.n), np.uint8)
+    ks = kb.as_struct()
+    _lib.check(L.rsk_bloom_contains(b, ctypes.byref(ks), out.ctypes.data))
+    return out[: kb.n]
+
+
+def test_golden_c3_insert(L, engine, orc):
+    from redisson_amd import KeyBatch
+
+    g = GOLDEN["bloom_c3_10000"]
+    keys = orc.gen_keys16(0x5EED0003, 0, 10000)
+    b = _filter(L, engine, g["size"], g["k"])
+    added = _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)))
+    bits = _bits(L, b, g["size"])
+    assert hashlib.sha256(bits.tobytes()).hexdigest() == g["bits_sha256"]
+    assert int(added.sum()) == g["added_true"]
+    ref_bits = np.zeros_like(bits)
+    ref_added = orc.bloom_add_batch(ref_bits, g["size"], g["k"], keys, None, 16, 10000)
+    assert np.array_equal(added, ref_added)
+    c = ctypes.c_int32()
+    assert L.rsk_bloom_count(b, ctypes.byref(c)) == 0 and c.value == g["count"]
+
+
+@pytest.mark.parametrize("size,k", [(729, 5), (95851, 7), (1000003, 33), (64, 3), (1, 2), (4014142460, 5)])
+def test_add_contains_varlen_parity(L, engine, orc, size, k):
+    from redisson_amd import KeyBatch
+
+    rng = np.random.default_rng(size % 1000 + k)
+    keys = [rng.integers(0, 256, int(rng.integers(0, 150)), dtype=np.uint8).tobytes() for _ in range(3000)]
+    keys += keys[:500] + [b"", b""]  # duplicates inside one batch
+    b = _filter(L, engine, size, k)
+    kb = KeyBatch.from_bytes_list(keys)
+    added = _add(L, b, kb)
+    blob, offs = orc.pack_keys(keys)
+    ref_bits = np.zeros((size + 7) // 8, np.uint8)
+    ref_added = orc.bloom_add_batch(ref_bits, size, k, blob, offs)
+    assert np.array_equal(added, ref_added)
+    if size < (1 << 28):
+        assert np.array_equal(_bits(L, b, size), ref_bits)
+    q = keys[:1000] + [rng.integers(0, 256, 20, dtype=np.uint8).tobytes() for _ in range(1000)]
+    qb, qo = orc.pack_keys(q)
+    if size < (1 << 28):
+        want = orc.bloom_contains_batch(ref_bits, size, k, qb, qo)
+    else:
+        want = None
+    got = _contains(L, b, KeyBatch.from_bytes_list(q))
+    assert got[:1000].all() or k == 1
+    if want is not None:
+        assert np.array_equal(got, want)
+
+
+def test_c3_stream_device_resident(L, engine, orc):
+    import torch
+    from redisson_amd import KeyBatch, _lib
+
+    n_ins, n_q = 2_000_000, 2_000_000
+    size = orc.bloom_optimal_bits(n_ins, 0.01)
+    k = orc.bloom_optimal_k(n_ins, size)
+    ins = torch.empty((n_ins, 16), dtype=torch.uint8, device="cuda")
+    qs = torch.empty((n_q, 16), dtype=torch.uint8, device="cuda")
+    _lib.check(L.rsk_gen_keys16(engine.ctx, 0x5EED0003, 0, n_ins, ins.data_ptr()))
+    _lib.check(L.rsk_gen_queries16(engine.ctx, 0x5EED0004, 0x5EED0003, n_ins, 0, n_q, qs.data_ptr()))
+    b = _filter(L, engine, size, k)
+    ks = KeyBatch.from_torch(ins).as_struct()
+    _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), None))
+    out = torch.zeros(n_q, dtype=torch.uint8, device="cuda")
+    qk = KeyBatch.from_torch(qs).as_struct()
+    _lib.check(L.rsk_bloom_contains(b, ctypes.byref(qk), out.data_ptr()))
+    engine.sync()
+    ref_bits = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(ref_bits, size, k, ins.cpu().numpy().reshape(-1), None, 16, n_ins, want=False)
+    assert np.array_equal(_bits(L, b, size), ref_bits)
+    qn = qs.cpu().numpy().reshape(-1)
+    assert np.array_equal(qn, orc.gen_queries16(0x5EED0004, 0x5EED0003, n_ins, 0, n_q))
+    want = orc.bloom_contains_batch(ref_bits, size, k, qn, None, 16, n_q)
+    got = out.cpu().numpy()
+    assert np.array_equal(got, want)
+    # every inserted key is found; the fresh half shows a ~1% false-positive rate
+    bc = ctypes.c_uint64()
+    assert L.rsk_bloom_bitcount(b, ctypes.byref(bc)) == 0 and bc.value == orc.bitcount(ref_bits)
+
+
+def test_or_bits_merge(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib
+
+    size, k = 100003, 5
+    keys = orc.gen_keys16(0x5EED0003, 0, 20000).reshape(-1, 16)
+    a = _filter(L, engine, size, k)
+    b = _filter(L, engine, size, k)
+    full = _filter(L, engine, size, k)
+    _add(L, a, KeyBatch.from_numpy(keys[:10000]), replies=False)
+    _add(L, b, KeyBatch.from_numpy(keys[10000:]), replies=False)
+    _add(L, full, KeyBatch.from_numpy(keys), replies=False)
+    bb = _bits(L, b, size)
+    _lib.check(L.rsk_bloom_or_bits(a, bb.ctypes.data, bb.size, _lib.RSK_MEM_HOST))
+    assert np.array_equal(_bits(L, a, size), _bits(L, full, size))

@@ -1,0 +1,262 @@
+"""HLL parity: the gfx950 kernels against the CPU oracle (bit-exact registers,
+exact PFCOUNT results), through the C ABI."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+SEED_C2 = 0x5EED0002
+SEED_C4 = 0x5EED0005
+
+
+@pytest.fixture(scope="module")
+def L():
+    from redisson_amd import _lib
+
+    return _lib.load()
+
+
+def _pool(L, engine, n=1):
+    from redisson_amd import _lib
+
+    h = ctypes.c_void_p()
+    _lib.check(L.rsk_hll_create(engine.ctx, n, ctypes.byref(h)))
+    return h
+
+
+def _regs(L, h, i=0):
+    from redisson_amd import _lib
+
+    out = np.zeros(16384, np.uint8)
+    _lib.check(L.rsk_hll_get_registers(h, i, out.ctypes.data, _lib.RSK_MEM_HOST))
+    return out
+
+
+def _add(L, h, kb, i=0):
+    from redisson_amd import _lib
+
+    ch = ctypes.c_uint8()
+    ks = kb.as_struct()
+    _lib.check(L.rsk_hll_add(h, i, ctypes.byref(ks), ctypes.byref(ch)))
+    return bool(ch.value)
+
+
+def _count(L, h, ids):
+    from redisson_amd import _lib
+
+    ids = np.asarray(ids, np.uint64)
+    out = np.zeros(ids.size, np.uint64)
+    _lib.check(L.rsk_hll_count(h, ids.ctypes.data, ids.size, out.ctypes.data))
+    return out
+
+
+def test_add16_matches_oracle(L, engine, orc):
+    from redisson_amd import KeyBatch
+
+    for n in (1, 7, 100, 1000, 20000, 200000, 1 << 20):
+        keys = orc.gen_keys16(SEED_C2, 0, n)
+        h = _pool(L, engine)
+        assert _add(L, h, KeyBatch.from_numpy(keys.reshape(n, 16)))
+        ref = np.zeros(16384, np.uint8)
+        orc.hll_add(ref, keys, None, 16, n)
+        got = _regs(L, h)
+        assert np.array_equal(got, ref), n
+        c = int(_count(L, h, [0])[0])
+        assert c == orc.hll_count_dense(ref) == orc.hll_count_raw(ref)
+        g = GOLDEN["hll"].get("c2_%d" % n)
+        if g:
+            assert hashlib.sha256(got.tobytes()).hexdigest() == g["registers_sha256"]
+            assert c == g["count_dense"]
+        L.rsk_hll_destroy(h)
+
+
+def test_add_device_resident_keys(L, engine, orc):
+    import torch
+    from redisson_amd import KeyBatch, _lib
+
+    n = 3_000_000
+    t = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    _lib.check(L.rsk_gen_keys16(engine.ctx, SEED_C2, 0, n, t.data_ptr()))
+    assert np.array_equal(t.cpu().numpy().reshape(-1), orc.gen_keys16(SEED_C2, 0, n))
+    h = _pool(L, engine)
+    _add(L, h, KeyBatch.from_torch(t))
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add_gen16(ref, SEED_C2, 0, n, 8)
+    assert np.array_equal(_regs(L, h), ref)
+    # idempotence: re-adding the same keys changes nothing -> PFADD replies 0
+    assert not _add(L, h, KeyBatch.from_torch(t))
+    # chunk-order independence: two halves into a fresh sketch
+    h2 = _pool(L, engine)
+    _add(L, h2, KeyBatch.from_torch(t[n // 2:]))
+    _add(L, h2, KeyBatch.from_torch(t[: n // 2]))
+    assert np.array_equal(_regs(L, h2), ref)
+
+
+@pytest.mark.parametrize("fixed_len", [1, 3, 7, 8, 9, 15, 17, 31, 33, 64, 65, 100])
+def test_add_fixed_lengths(L, engine, orc, fixed_len):
+    from redisson_amd import KeyBatch
+
+    rng = np.random.default_rng(fixed_len)
+    n = 50000
+    keys = rng.integers(0, 256, n * fixed_len, dtype=np.uint8)
+    h = _pool(L, engine)
+    _add(L, h, KeyBatch.from_numpy(keys.reshape(n, fixed_len)))
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, keys, None, fixed_len, n)
+    assert np.array_equal(_regs(L, h), ref)
+
+
+def test_add_variable_length_and_empty(L, engine, orc):
+    from redisson_amd import KeyBatch
+
+    rng = np.random.default_rng(7)
+    keys = [rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes() for _ in range(30000)]
+    keys += [b"", b"", b"x"]
+    h = _pool(L, engine)
+    _add(L, h, KeyBatch.from_bytes_list(keys))
+    blob, offs = orc.pack_keys(keys)
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, blob, offs)
+    assert np.array_equal(_regs(L, h), ref)
+
+
+def test_varlen_c4_stream(L, engine, orc):
+    import torch
+    from redisson_amd import KeyBatch, _lib
+
+    n = 200000
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    tot = ctypes.c_uint64()
+    _lib.check(L.rsk_gen_varlen(engine.ctx, SEED_C4, 0, n, offs.data_ptr(), None, 0, ctypes.byref(tot)))
+    blob = torch.empty(tot.value, dtype=torch.uint8, device="cuda")
+    _lib.check(L.rsk_gen_varlen(engine.ctx, SEED_C4, 0, n, offs.data_ptr(), blob.data_ptr(), tot.value,
+                                ctypes.byref(tot)))
+    rblob, roffs = orc.gen_varlen(SEED_C4, 0, n)
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), roffs)
+    assert np.array_equal(blob.cpu().numpy(), rblob[: int(roffs[-1])])
+    h = _pool(L, engine)
+    _add(L, h, KeyBatch.from_torch(blob, offs))
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, rblob, roffs)
+    assert np.array_equal(_regs(L, h), ref)
+
+
+def test_count_cache_and_union_and_merge(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib
+
+    h = _pool(L, engine, 4)
+    sets = []
+    for i, n in enumerate((10, 5000, 60000, 400000)):
+        keys = orc.gen_keys16(SEED_C2 + i, 0, n)
+        _add(L, h, KeyBatch.from_numpy(keys.reshape(n, 16)), i)
+        ref = np.zeros(16384, np.uint8)
+        orc.hll_add(ref, keys, None, 16, n)
+        sets.append(ref)
+    got = _count(L, h, [0, 1, 2, 3, 3, 0])
+    want = [orc.hll_count_dense(r) for r in sets]
+    assert list(got) == want + [want[3], want[0]]
+    # union (countWith): raw-order estimator on the max registers
+    for members in ([0, 1], [1, 2, 3], [3, 3], [0, 1, 2, 3]):
+        pools = (ctypes.c_void_p * len(members))(*([h.value] * len(members)))
+        ids = (ctypes.c_uint64 * len(members))(*members)
+        out = (ctypes.c_uint64 * 1)()
+        _lib.check(L.rsk_hll_count_union(pools, ids, len(members), out))
+        mx = np.maximum.reduce([sets[m] for m in members])
+        assert out[0] == orc.hll_count_raw(mx)
+    # merge (PFMERGE 0 <- 1,2): dest included
+    pools = (ctypes.c_void_p * 2)(h.value, h.value)
+    ids = (ctypes.c_uint64 * 2)(1, 2)
+    _lib.check(L.rsk_hll_merge(h, 0, pools, ids, 2))
+    mx = np.maximum.reduce([sets[0], sets[1], sets[2]])
+    assert np.array_equal(_regs(L, h, 0), mx)
+    assert int(_count(L, h, [0])[0]) == orc.hll_count_dense(mx)
+
+
+def test_count_inexact_fallback(L, engine, orc):
+    """Registers spanning > 53 bits force the ordered (dense) summation."""
+    from redisson_amd import _lib
+
+    rng = np.random.default_rng(3)
+    for trial in range(4):
+        regs = rng.integers(1, 4, 16384).astype(np.uint8)  # no zeros, small ranks
+        regs[rng.integers(0, 16384, 40)] = rng.integers(44, 51, 40).astype(np.uint8)
+        h = _pool(L, engine)
+        _lib.check(L.rsk_hll_merge_raw(h, 0, regs.ctypes.data, _lib.RSK_MEM_HOST))
+        assert int(_count(L, h, [0])[0]) == orc.hll_count_dense(regs)
+        pools = (ctypes.c_void_p * 1)(h.value)
+        ids = (ctypes.c_uint64 * 1)(0)
+        out = (ctypes.c_uint64 * 1)()
+        _lib.check(L.rsk_hll_count_union(pools, ids, 1, out))
+        assert out[0] == orc.hll_count_raw(regs)
+
+
+def test_export_import_redis_strings(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib
+
+    keys = orc.gen_keys16(SEED_C2, 0, 2000)
+    h = _pool(L, engine, 2)
+    _add(L, h, KeyBatch.from_numpy(keys.reshape(-1, 16)), 0)
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, keys, None, 16, 2000)
+    buf = (ctypes.c_uint8 * 12304)()
+    n = ctypes.c_size_t()
+    _lib.check(L.rsk_hll_export_redis(h, 0, buf, 12304, ctypes.byref(n)))
+    s = bytes(buf[: n.value])
+    assert n.value == 12304 and s[:5] == b"HYLL\x00"
+    rc, raw, enc = orc.hll_decode(s)
+    assert rc == 0 and enc == 0 and np.array_equal(raw, ref)
+    assert s[16:] == orc.hll_encode_dense(ref)[16:]
+    assert s[15] & 0x80  # cache invalid after PFADD
+    # import a sparse string produced by the oracle into slot 1
+    sp = orc.hll_encode_sparse(ref)
+    b = (ctypes.c_uint8 * len(sp)).from_buffer_copy(sp)
+    _lib.check(L.rsk_hll_import_redis(h, 1, b, len(sp)))
+    assert np.array_equal(_regs(L, h, 1), ref)
+    assert int(_count(L, h, [1])[0]) == orc.hll_count_string(sp)[1]
+    bad = (ctypes.c_uint8 * 20).from_buffer_copy(b"HYLL\x00" + b"\0" * 15)
+    assert L.rsk_hll_import_redis(h, 1, bad, 20) == _lib.RSK_ERR_WRONGTYPE
+
+
+def test_add_each_matches_sequential_pfadd(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib
+
+    rng = np.random.default_rng(11)
+    base = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(20000)]
+    keys = base + base[:5000] + [base[7]] * 3  # duplicates -> later replies 0
+    r = orc.RedisModel()
+    want = [r.pfadd("k", e) for e in keys]
+    h = _pool(L, engine)
+    out = np.zeros(len(keys), np.uint8)
+    ks = KeyBatch.from_bytes_list(keys).as_struct()
+    _lib.check(L.rsk_hll_add_each(h, 0, ctypes.byref(ks), out.ctypes.data))
+    assert out.tolist() == want
+    rc, raw, _ = orc.hll_decode(r.get("k"))
+    assert np.array_equal(_regs(L, h), raw)
+
+
+def test_grouped_add_matches_oracle(L, engine, orc):
+    import torch
+    from redisson_amd import KeyBatch, _lib
+
+    G, n = 1000, 2_000_000
+    g = torch.empty(n, dtype=torch.int32, device="cuda")
+    k = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    _lib.check(L.rsk_gen_grouped(engine.ctx, 0x5EED0006, G, 0, n, g.data_ptr(), k.data_ptr()))
+    h = _pool(L, engine, G)
+    ks = KeyBatch.from_torch(k).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.data_ptr()))
+    ref = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped(ref, G, 0x5EED0006, 0, n)
+    for gid in list(range(0, G, 37)) + [G - 1]:
+        assert np.array_equal(_regs(L, h, gid), ref[gid * 16384:(gid + 1) * 16384]), gid
+    ids = np.arange(G, dtype=np.uint64)
+    out = np.zeros(G, np.uint64)
+    _lib.check(L.rsk_hll_count(h, ids.ctypes.data, G, out.ctypes.data))
+    want = [orc.hll_count_dense(ref[i * 16384:(i + 1) * 16384]) for i in range(G)]
+    assert out.tolist() == want

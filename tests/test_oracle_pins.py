@@ -1,0 +1,162 @@
+"""Pin the CPU oracle before trusting it (CPU only).
+
+Every check here compares the oracle against something it was not derived
+from: published known answers for the hash functions, an independent XXH64
+implementation, and the expectations of the reference's own JUnit tests.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden.json")
+
+
+def test_murmur64a_smhasher_verification(orc):
+    # SMHasher VerificationTest: keys {0..i-1} hashed with seed 256-i, the
+    # concatenated hashes hashed with seed 0; "Murmur2B" = 0x1F0D3804.
+    L = orc.lib()
+    key = bytearray(256)
+    hashes = bytearray()
+    for i in range(256):
+        key[i] = i
+        hashes += struct.pack("<Q", L.orc_murmur64a(bytes(key[:i]), i, 256 - i))
+    final = L.orc_murmur64a(bytes(hashes), len(hashes), 0)
+    assert final & 0xFFFFFFFF == 0x1F0D3804
+
+
+def test_xxh64_matches_python_xxhash(orc):
+    xxhash = pytest.importorskip("xxhash")
+    rng = np.random.default_rng(1)
+    for n in list(range(0, 100)) + [127, 128, 129, 1000, 4096]:
+        for _ in range(3):
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            assert orc.xxh64(b) == xxhash.xxh64_intdigest(b, 0)
+    assert orc.xxh64(b"") == 0xEF46DB3751D8E999
+    assert orc.xxh64(b'"123"') == 0xAE40987216FED2E5
+
+
+def _s64(x):
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def test_farmhash_na_guava_known_answers(orc):
+    # Guava FarmHashFingerprint64Test.testReallySimpleFingerprints
+    # (Fingerprint64 == farmhashna::Hash64): lengths 4, 32 and 256.
+    assert _s64(orc.farmhash_na64(b"test")) == 8581389452482819506
+    assert _s64(orc.farmhash_na64(b"test" * 8)) == -4196240717365766262
+    assert _s64(orc.farmhash_na64(b"test" * 64)) == 3500507768004279527
+    assert orc.farmhash_na64(b"") == 0x9AE16A3B2F90404F  # k2
+
+
+def test_farmhash_uo_equals_na_up_to_64(orc):
+    for n in range(0, 65):
+        b = bytes((i * 7 + 3) & 0xFF for i in range(n))
+        assert orc.farmhash_uo64(b) == orc.farmhash_na64(b)
+
+
+def test_reference_hll_junit_add(orc):
+    # RedissonHyperLogLogTest.testAdd: JSON codec, Integer 1,2,3 -> b"1".. ; count()==3
+    r = orc.RedisModel()
+    for e in (b"1", b"2", b"3"):
+        r.pfadd("log", e)
+    assert r.pfcount("log") == 3
+
+
+def test_reference_hll_junit_merge(orc):
+    # RedissonHyperLogLogTest.testMerge
+    r = orc.RedisModel()
+    j = lambda s: ('"%s"' % s).encode()  # noqa: E731
+    assert [r.pfadd("hll1", j(s)) for s in ("foo", "bar", "zap", "a")] == [1, 1, 1, 1]
+    assert [r.pfadd("hll2", j(s)) for s in ("a", "b", "c", "foo", "c")] == [1, 1, 1, 1, 0]
+    r.pfmerge("hll3", "hll1", "hll2")
+    assert r.pfcount("hll3") == 6
+
+
+def test_reference_bloom_junit_config(orc):
+    # RedissonBloomFilterTest.testConfig: tryInit(100, 0.03) -> size 729, k 5
+    size = orc.bloom_optimal_bits(100, 0.03)
+    assert size == 729 and orc.bloom_optimal_k(100, size) == 5
+    # RedissonBloomFilterTest.test: tryInit(550000000, 0.03) fits under MAX_SIZE
+    size = orc.bloom_optimal_bits(550000000, 0.03)
+    assert size == 4014142460 and size <= 2147483647 * 2
+    assert orc.bloom_optimal_k(550000000, size) == 5
+
+
+def test_reference_bloom_junit_sequence(orc):
+    # RedissonBloomFilterTest.test, replayed through the oracle Redis model.
+    r = orc.RedisModel()
+    f = orc.OracleBloomFilter(r, "filter", lambda s: ('"%s"' % s).encode())
+    assert f.try_init(550000000, 0.03)
+    assert not f.contains("123")
+    assert f.add("123")
+    assert f.contains("123")
+    assert not f.add("123")
+    assert f.count() == 1
+    s = "hflgs;jl;ao1-32471320o31803-24"
+    assert not f.contains(s)
+    assert f.add(s)
+    assert f.contains(s)
+    assert f.count() == 2
+
+
+def test_reference_bloom_junit_init(orc):
+    r = orc.RedisModel()
+    f = orc.OracleBloomFilter(r, "filter", lambda s: s.encode())
+    assert f.try_init(55000000, 0.03)
+    assert not f.try_init(55000001, 0.03)
+    r.delete("filter", "{filter}__config")
+    assert f.try_init(55000001, 0.03)
+
+
+def test_bloom_max_size(orc):
+    # 1B @ 1% exceeds MAX_SIZE: the reference throws (RedissonBloomFilter.java:226-227)
+    assert orc.bloom_optimal_bits(10 ** 9, 0.01) == 9585058377
+    assert orc.bloom_optimal_bits(4 * 10 ** 8, 0.01) == 3834023350
+
+
+def test_bloom_k1_semantics(orc):
+    # k == 1: subList(1, size-1) is empty -> add() always False, contains() always True
+    bits = np.zeros(16, np.uint8)
+    keys = np.frombuffer(b"abcdefgh" * 4, np.uint8).copy()
+    added = orc.bloom_add_batch(bits, 100, 1, keys, None, 8, 4)
+    assert not added.any()
+    assert orc.bloom_contains_batch(np.zeros(16, np.uint8), 100, 1, keys, None, 8, 4).all()
+
+
+def test_hll_sparse_dense_roundtrip(orc):
+    regs = np.zeros(orc.REGISTERS, np.uint8)
+    orc.hll_add_gen16(regs, 0x5EED0002, 0, 3000)
+    sp = orc.hll_encode_sparse(regs)
+    de = orc.hll_encode_dense(regs)
+    assert len(de) == orc.DENSE_SIZE
+    for s in (sp, de):
+        rc, raw, enc = orc.hll_decode(s)
+        assert rc == 0 and np.array_equal(raw, regs)
+    # sparse and dense PFCOUNT agree (exact sums)
+    assert orc.hll_count_string(sp)[1] == orc.hll_count_string(de)[1] == orc.hll_count_raw(regs)
+
+
+def test_hll_decode_rejects(orc):
+    assert orc.hll_decode(b"HYLL")[0] == -1                         # short
+    assert orc.hll_decode(b"HYLX" + b"\0" * 12304)[0] == -1          # magic
+    assert orc.hll_decode(b"HYLL\x00" + b"\0" * 100)[0] == -1        # dense wrong length
+    assert orc.hll_decode(b"HYLL\x02" + b"\0" * 11)[0] == -1         # encoding > 1
+    bad = b"HYLL\x01" + b"\0" * 11 + bytes([0x7F, 0xFE])              # XZERO 16383, total != 16384
+    assert orc.hll_decode(bad)[0] == -2
+
+
+def test_golden_fixtures_reproduce(orc):
+    g = json.load(open(GOLDEN))
+    xs = [bytes.fromhex(h) for h in g["hash_inputs_hex"]]
+    assert ["%016x" % orc.murmur64a(x) for x in xs] == g["murmur64a_seed_adc83b19"]
+    assert ["%016x" % orc.xxh64(x) for x in xs] == g["xxh64_seed0"]
+    assert ["%016x" % orc.farmhash_uo64(x) for x in xs] == g["farmhash_uo64"]
+    for n, p, size, k in g["bloom_params"]:
+        assert orc.bloom_optimal_bits(n, p) == size and orc.bloom_optimal_k(n, size) == k
+    regs = np.zeros(orc.REGISTERS, np.uint8)
+    orc.hll_add_gen16(regs, 0x5EED0002, 0, 20000)
+    assert regs.tobytes().hex() == g["hll"]["c2_20000"]["registers_hex"]
+    assert orc.hll_count_dense(regs) == g["hll"]["c2_20000"]["count_dense"]
