@@ -17,7 +17,7 @@ build/%.o: redisson_amd/csrc/%.hip $(HDR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -s -C oracle

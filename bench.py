@@ -63,22 +63,21 @@ def cpu_baseline(sample_keys: int, passes: int):
 
 
 def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
-    import torch
-
-    from redisson_amd import KeyBatch, _lib
+    from redisson_amd import _lib, devmem
 
     L = _lib.load()
     size = ctypes.c_int64()
     k = ctypes.c_int32()
     _lib.check(L.rsk_bloom_params(n_ins, 0.01, _lib.RSK_BLOOM_EXTENDED, ctypes.byref(size), ctypes.byref(k)))
-    ins = torch.empty((n_ins, 16), dtype=torch.uint8, device="cuda")
-    qs = torch.empty((n_q, 16), dtype=torch.uint8, device="cuda")
-    _lib.check(L.rsk_gen_keys16(engine.ctx, SEED_C3, 0, n_ins, ins.data_ptr()))
-    _lib.check(L.rsk_gen_queries16(engine.ctx, SEED_Q, SEED_C3, n_ins, 0, n_q, qs.data_ptr()))
-    out = torch.empty(n_q, dtype=torch.uint8, device="cuda")
-    ki = KeyBatch.from_torch(ins).as_struct()
-    kq = KeyBatch.from_torch(qs).as_struct()
+    ins = devmem.gen_keys16(engine, SEED_C3, 0, n_ins)
+    qs = devmem.gen_queries16(engine, SEED_Q, SEED_C3, n_ins, 0, n_q)
+    out = devmem.DeviceBuffer(engine, n_q)
+    ki = ins.keys_fixed(n_ins, 16).as_struct()
+    kq = qs.keys_fixed(n_q, 16).as_struct()
     add_t, con_t = [], []
+    engine.prof_reset()
+    engine.prof_enable(True)
+    hits = 0
     for r in range(reps + 1):
         b = ctypes.c_void_p()
         _lib.check(L.rsk_bloom_create(engine.ctx, size.value, k.value, ctypes.byref(b)))
@@ -87,21 +86,28 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
         _lib.check(L.rsk_bloom_add(b, ctypes.byref(ki), None))
         engine.sync()
         t1 = time.perf_counter()
-        _lib.check(L.rsk_bloom_contains(b, ctypes.byref(kq), out.data_ptr()))
+        _lib.check(L.rsk_bloom_contains(b, ctypes.byref(kq), out.ptr))
         engine.sync()
         t2 = time.perf_counter()
         if r:
             add_t.append(t1 - t0)
             con_t.append(t2 - t1)
         if r == reps:
-            hits = int(out.sum().item())
+            hits = int(out.to_numpy().sum())
         L.rsk_bloom_destroy(b)
+    engine.prof_enable(False)
+    add_ms, add_n = engine.prof_read("bloom_add16")
+    con_ms, con_n = engine.prof_read("bloom_contains16")
     add_s, con_s = min(add_t), min(con_t)
+    for buf in (ins, qs, out):
+        buf.free()
     return {"config": "C3: %d inserts @1%% FPP (size %d bits, k=%d, EXTENDED), %d contains (50%% inserted)"
                       % (n_ins, size.value, k.value, n_q),
             "insert_keys_per_s": n_ins / add_s, "contains_keys_per_s": n_q / con_s,
             "insert_ms": add_s * 1e3, "contains_ms": con_s * 1e3, "contains_true": hits,
-            "insert_bit_rmw_per_s": n_ins * k.value / add_s, "contains_probe_gathers_per_s": n_q * (k.value - 1) / con_s}
+            "insert_kernel_avg_ms": add_ms / max(1, add_n), "contains_kernel_avg_ms": con_ms / max(1, con_n),
+            "insert_bit_rmw_per_s": n_ins * k.value / add_s,
+            "contains_probe_gathers_per_s": n_q * (k.value - 1) / con_s}
 
 
 def main():
@@ -114,7 +120,7 @@ def main():
     ap.add_argument("--no-bloom", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=128 << 20)
-    ap.add_argument("--cpu-passes", type=int, default=4)
+    ap.add_argument("--cpu-passes", type=int, default=8)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -123,46 +129,47 @@ def main():
     if world != args.gpus:
         log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
 
+    # librsketch (system ROCm runtime) is loaded before torch is imported, so
+    # the process has exactly one initialised HIP/HSA runtime.
+    from redisson_amd import _lib as _early
+
+    _early.load()
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # gloo only ships the RCCL id and the timings; the data path is RCCL.
+        dist.init_process_group("gloo")
 
-    from redisson_amd import Engine, KeyBatch, Redisson, _lib
-    from redisson_amd.client import Config
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.client import Config, Redisson
 
     L = _lib.load()
     client = Redisson.create(Config(device=local))
     engine = client.engine
+    if world > 1:
+        shard.init_comm(engine)
     n = args.keys
 
     # Inputs resident in HBM before the timed region (generation untimed).
-    keys = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
-    _lib.check(L.rsk_gen_keys16(engine.ctx, SEED_C2, rank * n, n, keys.data_ptr()))
-    kb = KeyBatch.from_torch(keys)
+    keys = devmem.gen_keys16(engine, SEED_C2, rank * n, n)
+    kb = keys.keys_fixed(n, 16)
     hll = client.getHyperLogLog("bench")
-    regs_t = torch.empty(16384, dtype=torch.uint8, device="cuda")
 
     def step():
         hll.addAll(kb)
         if world > 1:
             slot = client._hll_slot("bench", False)
-            _lib.check(L.rsk_hll_get_registers(slot.pool, slot.id, regs_t.data_ptr(), _lib.RSK_MEM_DEVICE))
-            dist.all_reduce(regs_t, op=dist.ReduceOp.MAX)  # RCCL over xGMI
-            torch.cuda.current_stream().synchronize()
-            _lib.check(L.rsk_hll_merge_raw(slot.pool, slot.id, regs_t.data_ptr(), _lib.RSK_MEM_DEVICE))
+            shard.hll_allreduce(slot.pool, slot.id)  # RCCL MAX over xGMI
         return hll.count()
 
     for _ in range(args.warmup):
         step()
 
     def barrier():
+        engine.sync()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
-        engine.sync()
 
     engine.prof_reset()
     engine.prof_enable(True)
@@ -176,7 +183,7 @@ def main():
     add_ms, add_launches = engine.prof_read("hll_add16")
     red_ms, red_launches = engine.prof_read("hll_reduce")
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -211,8 +218,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_bloom:
         bn = args.bloom_keys
-        del keys, kb
-        torch.cuda.empty_cache()
+        keys.free()
         result["bloom"] = bloom_bench(engine, bn, bn, reps=2)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes)

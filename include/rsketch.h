@@ -182,6 +182,35 @@ int rsk_bloom_import_bits(rsk_bloom *b, const uint8_t *buf, size_t len);
 int rsk_bloom_or_bits(rsk_bloom *b, const uint8_t *bits, size_t len, uint32_t location);
 void *rsk_bloom_device_bits(rsk_bloom *b);
 
+/* ------------------------------------------------------- device memory */
+/* HBM buffers for keys / replies that stay resident (JNI: wrap as direct
+ * buffers; Python: redisson_amd.devmem.DeviceBuffer). */
+typedef enum rsk_copy { RSK_H2D = 0, RSK_D2H = 1, RSK_D2D = 2 } rsk_copy;
+int rsk_dev_alloc(rsk_ctx *ctx, uint64_t bytes, void **out);
+int rsk_dev_free(rsk_ctx *ctx, void *p);
+/* Ordered on the context stream; returns when the copy is complete. */
+int rsk_memcpy(rsk_ctx *ctx, void *dst, const void *src, uint64_t bytes, uint32_t kind);
+int rsk_memset(rsk_ctx *ctx, void *p, int value, uint64_t bytes);
+
+/* ------------------------------------------- multi-GPU (RCCL over xGMI) */
+/* One process per GPU.  Rank 0 creates the id, the caller ships it to the
+ * other ranks (any out-of-band channel: torch.distributed gloo, MPI, a
+ * socket), every rank calls rsk_comm_init.  The key stream is sharded
+ * across ranks; the only exchange step is the sketch merge below. */
+#define RSK_COMM_ID_BYTES 128
+int rsk_comm_unique_id(uint8_t *id_out);
+int rsk_comm_init(rsk_ctx *ctx, int nranks, int rank, const uint8_t *id);
+int rsk_comm_destroy(rsk_ctx *ctx);
+/* Sketch id := register-wise MAX over all ranks (ncclAllReduce uint8 MAX,
+ * in place, 16 KiB).  Equals PFMERGE of the ranks' sketches; the cache is
+ * invalidated. */
+int rsk_hll_allreduce(rsk_hll *h, uint64_t id);
+/* The whole pool ([n][16384]) MAX over ranks. */
+int rsk_hll_allreduce_pool(rsk_hll *h);
+/* Bloom bit string := OR over all ranks.  RCCL has no bitwise-OR reduction:
+ * all-to-all of 1/N slices, local OR, all-gather. */
+int rsk_bloom_allreduce_or(rsk_bloom *b);
+
 /* ----------------------------------------------- synthetic input streams */
 /* SURVEY 8d generators, run on the device into caller-provided device
  * buffers (bench and parity tests; outside the timed region). */

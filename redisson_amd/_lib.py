@@ -120,6 +120,16 @@ SIGNATURES = {
     "rsk_bloom_import_bits": (ctypes.c_int, [_vp, _vp, _sz]),
     "rsk_bloom_or_bits": (ctypes.c_int, [_vp, _vp, _sz, _u32]),
     "rsk_bloom_device_bits": (_vp, [_vp]),
+    "rsk_dev_alloc": (ctypes.c_int, [_vp, _u64, _P(_vp)]),
+    "rsk_dev_free": (ctypes.c_int, [_vp, _vp]),
+    "rsk_memcpy": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32]),
+    "rsk_memset": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64]),
+    "rsk_comm_unique_id": (ctypes.c_int, [_vp]),
+    "rsk_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "rsk_comm_destroy": (ctypes.c_int, [_vp]),
+    "rsk_hll_allreduce": (ctypes.c_int, [_vp, _u64]),
+    "rsk_hll_allreduce_pool": (ctypes.c_int, [_vp]),
+    "rsk_bloom_allreduce_or": (ctypes.c_int, [_vp]),
     "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
     "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
     "rsk_gen_queries16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),

@@ -108,11 +108,10 @@ class RBloomFilter:
         if not replies:
             _lib.check(_lib.load().rsk_bloom_add(b, ctypes.byref(ks), None), "SETBIT")
             return None
-        buf, ptr = out_buffer(kb, kb.n)
+        buf, ptr = out_buffer(kb, kb.n, self._client.engine)
         _lib.check(_lib.load().rsk_bloom_add(b, ctypes.byref(ks), ptr), "SETBIT")
         if kb.on_device:
-            self._client.engine.sync()
-            return buf[: kb.n]
+            return buf  # replies stay in HBM (DeviceBuffer of n bytes)
         return [bool(x) for x in buf[: kb.n]]
 
     def contains(self, obj) -> bool:
@@ -121,12 +120,11 @@ class RBloomFilter:
     def containsAll(self, objects):
         kb = encode_all(self.codec, objects)
         b = self._filter()
-        buf, ptr = out_buffer(kb, kb.n)
+        buf, ptr = out_buffer(kb, kb.n, self._client.engine)
         ks = kb.as_struct()
         _lib.check(_lib.load().rsk_bloom_contains(b, ctypes.byref(ks), ptr), "GETBIT")
         if kb.on_device:
-            self._client.engine.sync()
-            return buf[: kb.n]
+            return buf  # replies stay in HBM (DeviceBuffer of n bytes)
         return [bool(x) for x in buf[: kb.n]]
 
     def count(self) -> int:

@@ -330,6 +330,7 @@ int rsk_shutdown(rsk_ctx* c) {
       (void)hipFree(it->second.p);
       g_out.erase(it);
     }
+    if (c->comm) (void)rsk_comm_destroy(c);
     (void)hipStreamDestroy(c->stream);
   });
   delete c;

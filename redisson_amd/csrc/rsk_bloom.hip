@@ -243,4 +243,28 @@ void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_
   RSK_CHECK_LAUNCH("bloom_or");
 }
 
+// dst = OR of rows[r][0..words) (the local step of the slice-OR merge).
+__global__ __launch_bounds__(256) void or_rows_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                      uint32_t rows, uint64_t words) {
+  const uint64_t w4 = words / 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w4; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint32_t r = 0; r < rows; ++r) {
+      uint4 v = reinterpret_cast<const uint4*>(src + (uint64_t)r * words)[i];
+      acc = make_uint4(acc.x | v.x, acc.y | v.y, acc.z | v.z, acc.w | v.w);
+    }
+    reinterpret_cast<uint4*>(dst)[i] = acc;
+  }
+}
+
+void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words) {
+  uint64_t g = (words / 4 + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 8;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  ProfScope ps(c, "bloom_or_rows");
+  hipLaunchKernelGGL(or_rows_kernel, dim3((uint32_t)g), dim3(256), 0, c->stream, d_dst, d_src, rows, words);
+  RSK_CHECK_LAUNCH("bloom_or_rows");
+}
+
 }  // namespace rsk

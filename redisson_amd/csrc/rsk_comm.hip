@@ -1,0 +1,224 @@
+// rsk_comm.hip -- device memory API and the RCCL merge layer.
+//
+// Multi-GPU layout: one process per GPU, the key stream split
+// into contiguous ranges, every GPU builds full sketches, and the only
+// exchange is the merge:
+//   HLL   : ncclAllReduce(uint8, ncclMax) over the 16 KiB register file
+//           (bit-exact: max is associative and commutative) -- latency-bound;
+//   pools : the same over [n][16384] (bandwidth-bound, ring over xGMI);
+//   Bloom : RCCL has no bitwise OR, so all-to-all of 1/N slices (grouped
+//           ncclSend/ncclRecv), a local OR, and ncclAllGather.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <vector>
+
+#include "rsk_internal.h"
+
+using rsk::RskError;
+
+namespace {
+
+#define RSK_NCCL(expr)                                                                                   \
+  do {                                                                                                   \
+    ncclResult_t _r = (expr);                                                                            \
+    if (_r != ncclSuccess)                                                                               \
+      throw RskError{RSK_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(_r)};                \
+  } while (0)
+
+template <class F>
+int guarded(F&& fn) {
+  try {
+    fn();
+    rsk::set_error("");
+    return RSK_OK;
+  } catch (const RskError& e) {
+    rsk::set_error(e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    rsk::set_error(e.what());
+    return RSK_ERR_DEVICE;
+  }
+}
+
+void need(bool cond, const char* msg) {
+  if (!cond) throw RskError{RSK_ERR_INVALID_ARG, msg};
+}
+
+struct Lock {
+  std::lock_guard<std::recursive_mutex> g;
+  explicit Lock(rsk_ctx* c) : g(c->mu) { RSK_HIP(hipSetDevice(c->device)); }
+};
+
+ncclComm_t comm_of(rsk_ctx* c) {
+  need(c->comm != nullptr, "no communicator: call rsk_comm_init first");
+  return reinterpret_cast<ncclComm_t>(c->comm);
+}
+
+__global__ void invalidate_card_kernel(uint64_t* card, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    card[i] |= (1ull << 63);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsk_dev_alloc(rsk_ctx* c, uint64_t bytes, void** out) {
+  return guarded([&] {
+    need(c && out, "NULL argument");
+    Lock l(c);
+    *out = nullptr;
+    RSK_HIP(hipMalloc(out, bytes ? bytes : 1));
+  });
+}
+
+int rsk_dev_free(rsk_ctx* c, void* p) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    Lock l(c);
+    if (p) {
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      RSK_HIP(hipFree(p));
+    }
+  });
+}
+
+int rsk_memcpy(rsk_ctx* c, void* dst, const void* src, uint64_t bytes, uint32_t kind) {
+  return guarded([&] {
+    need(c && (bytes == 0 || (dst && src)), "NULL argument");
+    need(kind <= RSK_D2D, "bad copy kind");
+    Lock l(c);
+    const hipMemcpyKind k = kind == RSK_H2D ? hipMemcpyHostToDevice
+                            : kind == RSK_D2H ? hipMemcpyDeviceToHost
+                                              : hipMemcpyDeviceToDevice;
+    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, k, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_memset(rsk_ctx* c, void* p, int value, uint64_t bytes) {
+  return guarded([&] {
+    need(c && (p || bytes == 0), "NULL argument");
+    Lock l(c);
+    if (bytes) RSK_HIP(hipMemsetAsync(p, value, bytes, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_comm_unique_id(uint8_t* id_out) {
+  return guarded([&] {
+    need(id_out != nullptr, "NULL argument");
+    ncclUniqueId id;
+    RSK_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(id_out, id.internal, RSK_COMM_ID_BYTES);
+  });
+}
+
+int rsk_comm_init(rsk_ctx* c, int nranks, int rank, const uint8_t* id) {
+  return guarded([&] {
+    need(c && id, "NULL argument");
+    need(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+    Lock l(c);
+    if (c->comm) {
+      (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(c->comm));
+      c->comm = nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, RSK_COMM_ID_BYTES);
+    ncclComm_t comm;
+    RSK_NCCL(ncclCommInitRank(&comm, nranks, uid, rank));
+    c->comm = comm;
+    c->nranks = nranks;
+    c->rank = rank;
+  });
+}
+
+int rsk_comm_destroy(rsk_ctx* c) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    Lock l(c);
+    if (c->comm) {
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      RSK_NCCL(ncclCommDestroy(reinterpret_cast<ncclComm_t>(c->comm)));
+      c->comm = nullptr;
+    }
+    c->nranks = 1;
+    c->rank = 0;
+  });
+}
+
+int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
+  return guarded([&] {
+    need(h && id < h->n, "bad sketch");
+    rsk_ctx* c = h->ctx;
+    Lock l(c);
+    ncclComm_t comm = comm_of(c);
+    uint8_t* regs = h->d_regs + id * (uint64_t)rsk::HLL_REGS;
+    {
+      rsk::ProfScope ps(c, "hll_allreduce");
+      RSK_NCCL(ncclAllReduce(regs, regs, rsk::HLL_REGS, ncclUint8, ncclMax, comm, c->stream));
+    }
+    hipLaunchKernelGGL(invalidate_card_kernel, dim3(1), dim3(64), 0, c->stream, h->d_card + id, (uint64_t)1);
+    RSK_CHECK_LAUNCH("invalidate");
+    h->exists[id] = 1;
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_allreduce_pool(rsk_hll* h) {
+  return guarded([&] {
+    need(h != nullptr, "bad pool");
+    rsk_ctx* c = h->ctx;
+    Lock l(c);
+    ncclComm_t comm = comm_of(c);
+    {
+      rsk::ProfScope ps(c, "hll_allreduce_pool");
+      RSK_NCCL(ncclAllReduce(h->d_regs, h->d_regs, h->n * (uint64_t)rsk::HLL_REGS, ncclUint8, ncclMax, comm,
+                             c->stream));
+    }
+    hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
+    RSK_CHECK_LAUNCH("invalidate");
+    std::fill(h->exists.begin(), h->exists.end(), 1);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_bloom_allreduce_or(rsk_bloom* b) {
+  return guarded([&] {
+    need(b != nullptr, "bad filter");
+    rsk_ctx* c = b->ctx;
+    Lock l(c);
+    ncclComm_t comm = comm_of(c);
+    const uint64_t N = (uint64_t)c->nranks;
+    if (N == 1) return;
+    // Slice of S words (multiple of 4 for 16-byte vector OR), N*S >= nwords.
+    uint64_t S = (b->nwords + N - 1) / N;
+    S = (S + 3) & ~uint64_t(3);
+    const uint64_t full = N * S;
+    uint32_t* send = reinterpret_cast<uint32_t*>(c->work(3 * full * 4 + 256));
+    uint32_t* recv = send + full;
+    uint32_t* gath = recv + full;
+    RSK_HIP(hipMemsetAsync(send, 0, full * 4, c->stream));
+    RSK_HIP(hipMemcpyAsync(send, b->d_bits, b->nwords * 4, hipMemcpyDeviceToDevice, c->stream));
+    {
+      rsk::ProfScope ps(c, "bloom_alltoall");
+      RSK_NCCL(ncclGroupStart());
+      for (uint64_t j = 0; j < N; ++j) {
+        RSK_NCCL(ncclSend(send + j * S, S * 4, ncclUint8, (int)j, comm, c->stream));
+        RSK_NCCL(ncclRecv(recv + j * S, S * 4, ncclUint8, (int)j, comm, c->stream));
+      }
+      RSK_NCCL(ncclGroupEnd());
+    }
+    uint32_t* mine = gath + (uint64_t)c->rank * S;
+    rsk::or_rows_launch(c, mine, recv, (uint32_t)N, S);
+    {
+      rsk::ProfScope ps(c, "bloom_allgather");
+      RSK_NCCL(ncclAllGather(mine, gath, S * 4, ncclUint8, comm, c->stream));
+    }
+    RSK_HIP(hipMemcpyAsync(b->d_bits, gath, b->nwords * 4, hipMemcpyDeviceToDevice, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+}  // extern "C"

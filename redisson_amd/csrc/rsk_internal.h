@@ -81,6 +81,10 @@ struct rsk_ctx {
   // m*log(m/ez) for ez = 0..16384, computed with the host libm (Redis's log)
   double* d_lc = nullptr;
   rsk::Profiler prof;
+  // RCCL communicator (multi-GPU merge layer), null when single-GPU
+  void* comm = nullptr;
+  int nranks = 1;
+  int rank = 0;
 
   uint8_t* work(uint64_t bytes);
 };
@@ -145,6 +149,8 @@ void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* 
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out);
 void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes);
+// dst[0..S) = OR over rows of src[rows][S] (u32 words).
+void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words);
 
 // ---- generators (rsk_gen.hip)
 void gen_keys16_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* out);

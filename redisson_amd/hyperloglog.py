@@ -65,12 +65,11 @@ class RHyperLogLog:
         the list of replies."""
         kb = encode_all(self.codec, objects)
         s = self._slot(True)
-        buf, ptr = out_buffer(kb, kb.n)
+        buf, ptr = out_buffer(kb, kb.n, self._client.engine)
         ks = kb.as_struct()
         _lib.check(_lib.load().rsk_hll_add_each(s.pool, s.id, ctypes.byref(ks), ptr), "PFADD")
         if kb.on_device:
-            self._client.engine.sync()
-            return buf[: kb.n]
+            return buf  # replies stay in HBM (DeviceBuffer of n bytes)
         return [bool(x) for x in buf[: kb.n]]
 
     # -- PFCOUNT
@@ -162,8 +161,12 @@ class GroupedHyperLogLog:
             self.pool = None
 
     def add(self, keys: KeyBatch, groups) -> None:
-        """groups: uint32 numpy array (host keys) or uint32/int32 CUDA tensor (device keys)."""
-        gp = groups.data_ptr() if hasattr(groups, "data_ptr") else np.ascontiguousarray(groups, np.uint32).ctypes.data
+        """groups: uint32 numpy array (host keys) or a DeviceBuffer of uint32 (device keys)."""
+        if hasattr(groups, "ptr"):
+            gp = groups.ptr
+        else:
+            groups = np.ascontiguousarray(groups, np.uint32)
+            gp = groups.ctypes.data
         ks = keys.as_struct()
         _lib.check(_lib.load().rsk_hll_add_grouped(self.pool, ctypes.byref(ks), gp))
 

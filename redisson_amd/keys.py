@@ -1,5 +1,5 @@
 """Key batches handed to the C ABI (rsk_keys): fixed stride or blob+offsets,
-in host memory or already resident in HBM (torch CUDA tensors)."""
+in host memory or already resident in HBM (redisson_amd.devmem.DeviceBuffer)."""
 from __future__ import annotations
 
 import ctypes
@@ -63,43 +63,22 @@ class KeyBatch:
             arr = np.zeros(1, np.uint8)
         return KeyBatch(arr.ctypes.data, offsets.ctypes.data, offsets.size - 1, 0, _lib.RSK_MEM_HOST, (arr, offsets))
 
-    @staticmethod
-    def from_torch(t, offsets=None) -> "KeyBatch":
-        """Keys already in HBM: uint8 CUDA tensor [n, L], or a 1-D blob with
-        an int64/uint64 CUDA offsets tensor of n+1 entries."""
-        if not t.is_cuda:
-            return KeyBatch.from_numpy(t.cpu().numpy(), None if offsets is None else offsets.cpu().numpy())
-        t = t.contiguous()
-        if offsets is None:
-            if t.dim() != 2:
-                raise ValueError("fixed-length keys must be a 2-D uint8 tensor [n, L]")
-            return KeyBatch(t.data_ptr(), None, t.shape[0], t.shape[1], _lib.RSK_MEM_DEVICE, (t,))
-        offsets = offsets.contiguous()
-        return KeyBatch(t.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, 0, _lib.RSK_MEM_DEVICE, (t, offsets))
-
 
 def encode_all(codec, objects) -> KeyBatch:
     if isinstance(objects, KeyBatch):
         return objects
     if isinstance(objects, np.ndarray):
         return KeyBatch.from_numpy(objects)
-    try:  # torch tensors without importing torch eagerly
-        import torch
-
-        if isinstance(objects, torch.Tensor):
-            return KeyBatch.from_torch(objects)
-    except ImportError:  # pragma: no cover
-        pass
     return KeyBatch.from_bytes_list([codec.encode(o) for o in objects])
 
 
-def out_buffer(kb: KeyBatch, n: int):
+def out_buffer(kb: KeyBatch, n: int, engine=None):
     """Per-key reply buffer in the keys' location (device replies stay in HBM)."""
     if kb.on_device:
-        import torch
+        from .devmem import DeviceBuffer
 
-        t = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
-        return t, t.data_ptr()
+        b = DeviceBuffer(engine, max(n, 1))
+        return b, b.ptr
     a = np.zeros(max(n, 1), dtype=np.uint8)
     return a, a.ctypes.data
 

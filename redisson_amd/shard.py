@@ -1,0 +1,103 @@
+"""Multi-GPU sharding: one process per GPU, the key stream split into
+contiguous ranges, full sketches per GPU, and one merge step through the
+RCCL layer of librsketch (rsk_comm.hip):
+
+  HLL   : rsk_hll_allreduce        ncclAllReduce(uint8, MAX), 16 KiB
+  pools : rsk_hll_allreduce_pool   the same over [n][16384]
+  Bloom : rsk_bloom_allreduce_or   all-to-all of 1/N slices, local OR, all-gather
+
+torch.distributed is used only as the out-of-band channel that ships the
+RCCL unique id (any backend; gloo keeps the GPU out of torch's hands).  The
+*_cpu functions restate the same exchange plans with torch.distributed on CPU
+tensors so that the N > 1 logic is testable without GPUs (tests/test_shard_gloo.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    """Contiguous range partition of n keys over world ranks (weak scaling
+    benches give every rank its own n instead)."""
+
+    n: int
+    world: int
+
+    def range(self, rank: int):
+        base, extra = divmod(self.n, self.world)
+        start = rank * base + min(rank, extra)
+        return start, start + base + (1 if rank < extra else 0)
+
+
+def slice_words(nwords: int, nranks: int) -> int:
+    """Words per rank in the Bloom slice-OR (a multiple of 4; N*S >= nwords).
+    Mirrors rsk_bloom_allreduce_or."""
+    s = (nwords + nranks - 1) // nranks
+    return (s + 3) & ~3
+
+
+def init_comm(engine, group=None) -> None:
+    """Create the RCCL communicator of this rank (torch.distributed must be
+    initialised; rank 0 creates the id, everyone else receives it)."""
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    if rank == 0:
+        _lib.check(L.rsk_comm_unique_id(uid))
+    box = [bytes(uid)]
+    dist.broadcast_object_list(box, src=0, group=group)
+    uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
+    _lib.check(L.rsk_comm_init(engine.ctx, world, rank, uid), "rsk_comm_init")
+
+
+def hll_allreduce(pool, sketch_id: int = 0) -> None:
+    _lib.check(_lib.load().rsk_hll_allreduce(pool, sketch_id), "rsk_hll_allreduce")
+
+
+def hll_allreduce_pool(pool) -> None:
+    _lib.check(_lib.load().rsk_hll_allreduce_pool(pool), "rsk_hll_allreduce_pool")
+
+
+def bloom_allreduce_or(bloom) -> None:
+    _lib.check(_lib.load().rsk_bloom_allreduce_or(bloom), "rsk_bloom_allreduce_or")
+
+
+# ------------------------------------------------------- CPU restatements
+def hll_allreduce_cpu(regs: np.ndarray, group=None) -> np.ndarray:
+    """The HLL exchange on CPU tensors: register-wise MAX over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(np.ascontiguousarray(regs, dtype=np.uint8).copy())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.numpy()
+
+
+def bloom_allreduce_or_cpu(bits: np.ndarray, group=None) -> np.ndarray:
+    """The Bloom slice-OR exchange on CPU tensors, same plan as the GPU path."""
+    import torch
+    import torch.distributed as dist
+
+    N, r = dist.get_world_size(group), dist.get_rank(group)
+    nbytes = bits.size
+    nwords = ((nbytes + 15) // 16) * 4
+    S = slice_words(nwords, N)
+    send = np.zeros(N * S * 4, np.uint8)
+    send[:nbytes] = bits
+    recv = torch.zeros(N * S * 4, dtype=torch.uint8)
+    dist.all_to_all_single(recv, torch.from_numpy(send), group=group)
+    rows = recv.numpy().reshape(N, S * 4)
+    mine = np.bitwise_or.reduce(rows, axis=0)
+    out = [torch.zeros(S * 4, dtype=torch.uint8) for _ in range(N)]
+    dist.all_gather(out, torch.from_numpy(mine.copy()), group=group)
+    full = np.concatenate([o.numpy() for o in out])
+    assert r >= 0
+    return full[:nbytes]

@@ -7,6 +7,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Load librsketch (system ROCm HIP/HSA) before any test module imports torch,
+# so the process never maps a second, torch-bundled HSA runtime first.
+if os.path.exists(os.path.join(ROOT, "redisson_amd", "librsketch.so")):
+    from redisson_amd import _lib as _rsk_lib
+
+    _rsk_lib.load()
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU and the built librsketch.so")

@@ -102,30 +102,27 @@ def test_add_contains_varlen_parity(L, engine, orc, size, k):
 
 
 def test_c3_stream_device_resident(L, engine, orc):
-    import torch
-    from redisson_amd import KeyBatch, _lib
+    from redisson_amd import _lib, devmem
 
     n_ins, n_q = 2_000_000, 2_000_000
     size = orc.bloom_optimal_bits(n_ins, 0.01)
     k = orc.bloom_optimal_k(n_ins, size)
-    ins = torch.empty((n_ins, 16), dtype=torch.uint8, device="cuda")
-    qs = torch.empty((n_q, 16), dtype=torch.uint8, device="cuda")
-    _lib.check(L.rsk_gen_keys16(engine.ctx, 0x5EED0003, 0, n_ins, ins.data_ptr()))
-    _lib.check(L.rsk_gen_queries16(engine.ctx, 0x5EED0004, 0x5EED0003, n_ins, 0, n_q, qs.data_ptr()))
+    ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n_ins)
+    qs = devmem.gen_queries16(engine, 0x5EED0004, 0x5EED0003, n_ins, 0, n_q)
     b = _filter(L, engine, size, k)
-    ks = KeyBatch.from_torch(ins).as_struct()
+    ks = ins.keys_fixed(n_ins, 16).as_struct()
     _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), None))
-    out = torch.zeros(n_q, dtype=torch.uint8, device="cuda")
-    qk = KeyBatch.from_torch(qs).as_struct()
-    _lib.check(L.rsk_bloom_contains(b, ctypes.byref(qk), out.data_ptr()))
+    out = devmem.DeviceBuffer(engine, n_q)
+    qk = qs.keys_fixed(n_q, 16).as_struct()
+    _lib.check(L.rsk_bloom_contains(b, ctypes.byref(qk), out.ptr))
     engine.sync()
     ref_bits = np.zeros((size + 7) // 8, np.uint8)
-    orc.bloom_add_batch(ref_bits, size, k, ins.cpu().numpy().reshape(-1), None, 16, n_ins, want=False)
+    orc.bloom_add_batch(ref_bits, size, k, ins.to_numpy(), None, 16, n_ins, want=False)
     assert np.array_equal(_bits(L, b, size), ref_bits)
-    qn = qs.cpu().numpy().reshape(-1)
+    qn = qs.to_numpy()
     assert np.array_equal(qn, orc.gen_queries16(0x5EED0004, 0x5EED0003, n_ins, 0, n_q))
     want = orc.bloom_contains_batch(ref_bits, size, k, qn, None, 16, n_q)
-    got = out.cpu().numpy()
+    got = out.to_numpy()
     assert np.array_equal(got, want)
     # every inserted key is found; the fresh half shows a ~1% false-positive rate
     bc = ctypes.c_uint64()

@@ -77,25 +77,31 @@ def test_add16_matches_oracle(L, engine, orc):
 
 
 def test_add_device_resident_keys(L, engine, orc):
-    import torch
-    from redisson_amd import KeyBatch, _lib
+    from redisson_amd import devmem
 
     n = 3_000_000
-    t = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
-    _lib.check(L.rsk_gen_keys16(engine.ctx, SEED_C2, 0, n, t.data_ptr()))
-    assert np.array_equal(t.cpu().numpy().reshape(-1), orc.gen_keys16(SEED_C2, 0, n))
+    t = devmem.gen_keys16(engine, SEED_C2, 0, n)
+    assert np.array_equal(t.to_numpy(), orc.gen_keys16(SEED_C2, 0, n))
+    kb = t.keys_fixed(n, 16)
     h = _pool(L, engine)
-    _add(L, h, KeyBatch.from_torch(t))
+    _add(L, h, kb)
     ref = np.zeros(16384, np.uint8)
     orc.hll_add_gen16(ref, SEED_C2, 0, n, 8)
     assert np.array_equal(_regs(L, h), ref)
     # idempotence: re-adding the same keys changes nothing -> PFADD replies 0
-    assert not _add(L, h, KeyBatch.from_torch(t))
+    assert not _add(L, h, kb)
     # chunk-order independence: two halves into a fresh sketch
     h2 = _pool(L, engine)
-    _add(L, h2, KeyBatch.from_torch(t[n // 2:]))
-    _add(L, h2, KeyBatch.from_torch(t[: n // 2]))
+    _add(L, h2, kb.slice(n // 2, n))
+    _add(L, h2, kb.slice(0, n // 2))
     assert np.array_equal(_regs(L, h2), ref)
+    # misaligned device keys take the generic path and agree
+    h3 = _pool(L, engine)
+    _add(L, h3, t.keys_fixed(n // 2 - 1, 16, offset=8))
+    ref3 = np.zeros(16384, np.uint8)
+    raw = orc.gen_keys16(SEED_C2, 0, n // 2)[8:8 + 16 * (n // 2 - 1)]
+    orc.hll_add(ref3, raw, None, 16, n // 2 - 1)
+    assert np.array_equal(_regs(L, h3), ref3)
 
 
 @pytest.mark.parametrize("fixed_len", [1, 3, 7, 8, 9, 15, 17, 31, 33, 64, 65, 100])
@@ -127,21 +133,15 @@ def test_add_variable_length_and_empty(L, engine, orc):
 
 
 def test_varlen_c4_stream(L, engine, orc):
-    import torch
-    from redisson_amd import KeyBatch, _lib
+    from redisson_amd import devmem
 
     n = 200000
-    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-    tot = ctypes.c_uint64()
-    _lib.check(L.rsk_gen_varlen(engine.ctx, SEED_C4, 0, n, offs.data_ptr(), None, 0, ctypes.byref(tot)))
-    blob = torch.empty(tot.value, dtype=torch.uint8, device="cuda")
-    _lib.check(L.rsk_gen_varlen(engine.ctx, SEED_C4, 0, n, offs.data_ptr(), blob.data_ptr(), tot.value,
-                                ctypes.byref(tot)))
+    blob, offs, tot = devmem.gen_varlen(engine, SEED_C4, 0, n)
     rblob, roffs = orc.gen_varlen(SEED_C4, 0, n)
-    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), roffs)
-    assert np.array_equal(blob.cpu().numpy(), rblob[: int(roffs[-1])])
+    assert np.array_equal(offs.to_numpy(np.uint64), roffs)
+    assert np.array_equal(blob.to_numpy(count=tot), rblob[: int(roffs[-1])])
     h = _pool(L, engine)
-    _add(L, h, KeyBatch.from_torch(blob, offs))
+    _add(L, h, blob.keys_var(offs, n))
     ref = np.zeros(16384, np.uint8)
     orc.hll_add(ref, rblob, roffs)
     assert np.array_equal(_regs(L, h), ref)
@@ -241,16 +241,15 @@ def test_add_each_matches_sequential_pfadd(L, engine, orc):
 
 
 def test_grouped_add_matches_oracle(L, engine, orc):
-    import torch
-    from redisson_amd import KeyBatch, _lib
+    from redisson_amd import _lib, devmem
 
     G, n = 1000, 2_000_000
-    g = torch.empty(n, dtype=torch.int32, device="cuda")
-    k = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
-    _lib.check(L.rsk_gen_grouped(engine.ctx, 0x5EED0006, G, 0, n, g.data_ptr(), k.data_ptr()))
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+    rg, rk = orc.gen_grouped(0x5EED0006, G, 0, n)
+    assert np.array_equal(g.to_numpy(np.uint32), rg) and np.array_equal(k.to_numpy(), rk)
     h = _pool(L, engine, G)
-    ks = KeyBatch.from_torch(k).as_struct()
-    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.data_ptr()))
+    ks = k.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
     ref = np.zeros(G * 16384, np.uint8)
     orc.hll_add_gen_grouped(ref, G, 0x5EED0006, 0, n)
     for gid in list(range(0, G, 37)) + [G - 1]:

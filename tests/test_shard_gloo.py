@@ -1,0 +1,82 @@
+"""N > 1 path on CPU: world_size-2 gloo processes run the same shard plan and
+exchange plans as the GPU path (RCCL MAX all-reduce; Bloom slice-OR) over
+oracle-built shards, and must reproduce the single-process sketch bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+SEED_C2 = 0x5EED0002
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from redisson_amd.shard import ShardPlan, bloom_allreduce_or_cpu, hll_allreduce_cpu
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = ShardPlan(n, world).range(rank)
+        regs = np.zeros(O.REGISTERS, np.uint8)
+        O.hll_add_gen16(regs, SEED_C2, lo, hi - lo)
+        merged = hll_allreduce_cpu(regs)
+        size = O.bloom_optimal_bits(n, 0.01)
+        k = O.bloom_optimal_k(n, size)
+        bits = np.zeros((size + 7) // 8, np.uint8)
+        keys = O.gen_keys16(0x5EED0003, lo, hi - lo)
+        O.bloom_add_batch(bits, size, k, keys, None, 16, hi - lo, want=False)
+        bmerged = bloom_allreduce_or_cpu(bits)
+        q.put((rank, merged.tobytes(), bmerged.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_merge_equals_single_process(world, orc):
+    n = 200_003
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = np.zeros(orc.REGISTERS, np.uint8)
+    orc.hll_add_gen16(ref, SEED_C2, 0, n)
+    size = orc.bloom_optimal_bits(n, 0.01)
+    k = orc.bloom_optimal_k(n, size)
+    bref = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(bref, size, k, orc.gen_keys16(0x5EED0003, 0, n), None, 16, n, want=False)
+    for rank, regs, bits in results:
+        assert regs == ref.tobytes(), rank
+        assert bits == bref.tobytes(), rank
+
+
+def test_shard_plan_covers_range():
+    from redisson_amd.shard import ShardPlan, slice_words
+
+    for n in (0, 1, 7, 1000, 10 ** 9 + 7):
+        for w in (1, 2, 3, 8):
+            p = ShardPlan(n, w)
+            rs = [p.range(r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+    for nw in (4, 8, 100, 299588432):
+        for N in (1, 2, 8):
+            s = slice_words(nw, N)
+            assert s % 4 == 0 and s * N >= nw
