@@ -1,0 +1,91 @@
+"""Summarise rocprofv3 output into profiles/*.json / *.md.
+
+usage: python scripts/pmc_summary.py STATS_DIR FETCH_DIR WRITE_DIR OUT_PREFIX KEYS_PER_LAUNCH
+
+* STATS_DIR: rocprofv3 --kernel-trace --stats --output-format csv run
+  (kernel_stats.csv: per-kernel calls / average duration).
+* FETCH_DIR / WRITE_DIR: separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes
+  (counter_collection.csv, one row per dispatch and counter).
+HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a wide (16 B/lane)
+coalesced streaming read, so the read side is doubled for the streaming
+hll_add16 kernel (the correction is recorded next to the raw value).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def find(d, pattern):
+    hits = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    return hits[0] if hits else None
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+
+
+def stats(d):
+    p = find(d, "*kernel_stats.csv")
+    out = {}
+    if not p:
+        return out, None
+    for row in csv.DictReader(open(p)):
+        out[short(row["Name"])] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                                   "total_ns": float(row["TotalDurationNs"]), "pct": float(row["Percentage"])}
+    return out, p
+
+
+def counters(d, counter):
+    p = find(d, "*counter_collection.csv")
+    vals = defaultdict(list)
+    if not p:
+        return {}, None
+    for row in csv.DictReader(open(p)):
+        if row.get("Counter_Name") != counter:
+            continue
+        vals[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, p
+
+
+def main():
+    sdir, fdir, wdir, prefix, keys = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
+    st, sp = stats(sdir)
+    fe, fp = counters(fdir, "FETCH_SIZE")
+    wr, wp = counters(wdir, "WRITE_SIZE")
+    kern = {}
+    for k in sorted(set(st) | set(fe) | set(wr)):
+        e = dict(st.get(k, {}))
+        if k in fe:
+            e["FETCH_SIZE_kib_raw"] = fe[k]
+        if k in wr:
+            e["WRITE_SIZE_kib"] = wr[k]
+        if k == "hll_add16_kernel":
+            e["keys_per_launch"] = keys
+            e["algorithmic_bytes_per_launch"] = 16 * keys
+            if k in fe:
+                e["fetch_bytes_per_launch"] = fe[k] * 1024 * 2  # gfx950 wide-stream correction
+            if k in fe and k in wr:
+                e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + wr[k] * 1024
+        kern[k] = e
+    doc = {"sources": {"stats": sp, "fetch": fp, "write": wp}, "kernels": kern,
+           "note": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch (mean over dispatches); fetch doubled for "
+                   "hll_add16_kernel per MI355X_MICROARCH.md HBM section"}
+    with open(prefix + ".json", "w") as f:
+        json.dump(doc, f, indent=1)
+    lines = ["| kernel | calls | avg us | % time | FETCH_SIZE KiB (raw) | WRITE_SIZE KiB |", "|---|---|---|---|---|---|"]
+    for k, e in sorted(kern.items(), key=lambda kv: -kv[1].get("pct", 0)):
+        lines.append("| %s | %s | %.1f | %.2f | %s | %s |" % (
+            k, e.get("calls", ""), e.get("avg_ns", 0) / 1e3, e.get("pct", 0),
+            "%.0f" % e["FETCH_SIZE_kib_raw"] if "FETCH_SIZE_kib_raw" in e else "",
+            "%.0f" % e["WRITE_SIZE_kib"] if "WRITE_SIZE_kib" in e else ""))
+    with open(prefix + ".md", "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
