@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-SEED_C2, SEED_C3, SEED_Q = 0x5EED0002, 0x5EED0003, 0x5EED0004
+SEED_C2, SEED_C3, SEED_Q, SEED_C4, SEED_C5 = 0x5EED0002, 0x5EED0003, 0x5EED0004, 0x5EED0005, 0x5EED0006
 
 
 def log(*a):
@@ -115,7 +115,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--keys", type=int, default=1_000_000_000, help="16-byte keys per GPU")
+    ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
+                    help="c2: 16-byte keys (headline); c4: variable-length keys; c5: grouped sketches")
+    ap.add_argument("--keys", type=int, default=1_000_000_000, help="keys (pairs for c5) per GPU")
+    ap.add_argument("--groups", type=int, default=1_000_000)
+    ap.add_argument("--batch-ops", type=int, default=100_000)
     ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
     ap.add_argument("--no-bloom", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -150,13 +154,46 @@ def main():
     if world > 1:
         shard.init_comm(engine)
     n = args.keys
-
-    # Inputs resident in HBM before the timed region (generation untimed).
-    keys = devmem.gen_keys16(engine, SEED_C2, rank * n, n)
-    kb = keys.keys_fixed(n, 16)
+    wl = args.workload
+    extra = {}
     hll = client.getHyperLogLog("bench")
 
+    # Inputs resident in HBM before the timed region (generation untimed).
+    if wl == "c2":
+        keys = devmem.gen_keys16(engine, SEED_C2, rank * n, n)
+        kb = keys.keys_fixed(n, 16)
+        kern, unit_bytes = "hll_add16", 16.0 * n
+        bufs = [keys]
+    elif wl == "c4":
+        blob, offs, tot = devmem.gen_varlen(engine, SEED_C4, rank * n, n)
+        kb = blob.keys_var(offs, n)
+        kern, unit_bytes = "hll_add_var", float(tot + 8 * n)
+        extra = {"key_bytes_total": tot, "mean_key_len": tot / n}
+        bufs = [blob, offs]
+    else:  # c5: grouped COUNT DISTINCT
+        from redisson_amd.hyperloglog import GroupedHyperLogLog
+        import numpy as np
+
+        G = args.groups
+        groups, gkeys = devmem.gen_grouped(engine, SEED_C5, G, rank * n, n)
+        kb = gkeys.keys_fixed(n, 16)
+        pool = GroupedHyperLogLog(engine, G)
+        rng = np.random.default_rng(5)
+        cw = rng.integers(0, G, size=(args.batch_ops, 2), dtype=np.uint64)
+        md = rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)
+        ms_ = rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)
+        kern, unit_bytes = "hll_add_grouped16", 20.0 * n
+        bufs = [groups, gkeys]
+
     def step():
+        if wl == "c5":
+            pool.add(kb, groups)
+            if world > 1:
+                shard.hll_allreduce_pool(pool.pool)
+            c = pool.count()
+            pool.countWith(cw)
+            pool.mergeWith(md, ms_)
+            return int(c[0])
         hll.addAll(kb)
         if world > 1:
             slot = client._hll_slot("bench", False)
@@ -180,8 +217,10 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     engine.prof_enable(False)
-    add_ms, add_launches = engine.prof_read("hll_add16")
+    add_ms, add_launches = engine.prof_read(kern)
     red_ms, red_launches = engine.prof_read("hll_reduce")
+    side = {name: engine.prof_read(name) for name in ("hll_count", "hll_union_count", "hll_merge",
+                                                       "hll_allreduce", "hll_allreduce_pool")}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -190,7 +229,13 @@ def main():
     total_keys = n * world * args.steps
     value = total_keys / elapsed
     avg_launch_s = (add_ms / 1e3) / max(1, add_launches)
-    achieved = 16.0 * n / avg_launch_s / 1e9  # algorithmic bytes per launch / launch time
+    achieved = unit_bytes / avg_launch_s / 1e9  # algorithmic bytes per launch / launch time
+    workloads = {
+        "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
+        "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
+        "c5": "Grouped HLL: %d sketches, grouped add + count(all) + %d countWith + %d mergeWith "
+              "(BASELINE configs[4])" % (args.groups, args.batch_ops, args.batch_ops),
+    }
     result = {
         "metric": "HLL adds/s + Bloom lookups/s (node), % HBM roofline, 1/2/4/8 MI355X",
         "value": value,
@@ -203,24 +248,28 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic (splitmix64 C2 stream generated on device, untimed)",
-        "config": {"workload": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
-                   "keys_per_gpu": n, "key_bytes": 16, "global_keys_per_step": n * world,
-                   "parallelism": "key-stream sharding, RCCL MAX all-reduce of 16 KiB registers" if world > 1
-                   else "single GPU", "redis_semantics": "3.2.0"},
-        "roofline": {"bound": "hbm", "kernel": "hll_add16_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "data": "synthetic (splitmix64 %s stream generated on device, untimed)" % wl.upper(),
+        "config": dict({"workload": workloads[wl],
+                        "keys_per_gpu": n, "global_keys_per_step": n * world,
+                        "parallelism": "key-stream sharding, RCCL MAX all-reduce of the registers" if world > 1
+                        else "single GPU", "redis_semantics": "3.2.0"}, **extra),
+        "roofline": {"bound": "hbm", "kernel": kern + "_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("hll_add16_kernel", n),
+                     "traffic": pmc_traffic(kern + "_kernel", n),
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": add_launches,
                      "reduce_avg_ms": red_ms / max(1, red_launches),
-                     "algorithmic_bytes_per_launch": 16 * n},
+                     "algorithmic_bytes_per_launch": unit_bytes},
+        "side_kernels_ms_per_launch": {k: (v[0] / v[1] if v[1] else None) for k, v in side.items()},
         "count": int(card),
     }
-    if rank == 0 and world == 1 and not args.no_bloom:
+    for b in bufs:
+        b.free()
+    if wl == "c5":
+        pool.close()
+    if rank == 0 and world == 1 and wl == "c2" and not args.no_bloom:
         bn = args.bloom_keys
-        keys.free()
         result["bloom"] = bloom_bench(engine, bn, bn, reps=2)
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes)
     else:
         result["cpu_baseline"] = None

@@ -211,6 +211,17 @@ int rsk_hll_allreduce_pool(rsk_hll *h);
  * all-to-all of 1/N slices, local OR, all-gather. */
 int rsk_bloom_allreduce_or(rsk_bloom *b);
 
+/* --------------------------------------------------------- diagnostics */
+/* Memory-system microbenchmark on a device buffer (roofline denominators):
+ * mode 0 stream read, 1 random 4 B gathers, 2 random 4 B atomicOr,
+ * 3 stream copy (buffer halves).  *ms = device time of the one launch. */
+int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
+/* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */
+int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint64_t n, double *ms);
+/* Time one launch of a tuning variant of the 16-byte Bloom contains kernel. */
+int rsk_diag_bloom_contains_variant(rsk_ctx *ctx, int variant, rsk_bloom *b, const void *dev_keys16, uint64_t n,
+                                    uint8_t *dev_out, double *ms);
+
 /* ----------------------------------------------- synthetic input streams */
 /* SURVEY 8d generators, run on the device into caller-provided device
  * buffers (bench and parity tests; outside the timed region). */

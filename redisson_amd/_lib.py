@@ -130,6 +130,10 @@ SIGNATURES = {
     "rsk_hll_allreduce": (ctypes.c_int, [_vp, _u64]),
     "rsk_hll_allreduce_pool": (ctypes.c_int, [_vp]),
     "rsk_bloom_allreduce_or": (ctypes.c_int, [_vp]),
+    "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
+    "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),
+    "rsk_diag_bloom_contains_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _u64, _vp,
+                                                       _P(ctypes.c_double)]),
     "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
     "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
     "rsk_gen_queries16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <new>
+#include <unordered_set>
 
 #include "rsk_internal.h"
 
@@ -203,6 +204,11 @@ __global__ void invalidate_kernel(uint64_t* card, const uint32_t* flag, int forc
   if (force || (flag && *flag)) *card |= (1ull << 63);
 }
 
+__global__ void invalidate_list_kernel(uint64_t* card, const uint64_t* ids, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    atomicOr(reinterpret_cast<unsigned long long*>(card + ids[i]), 1ull << 63);
+}
+
 __global__ void invalidate_all_kernel(uint64_t* card, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     card[i] |= (1ull << 63);
@@ -293,7 +299,7 @@ int rsk_init(const rsk_options* opts, rsk_ctx** out) {
     RSK_HIP(hipSetDevice(c->device));
     RSK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->stage_bytes = o.staging_bytes ? o.staging_bytes : (256ull << 20);
-    c->slab_count = std::min<uint32_t>(RSK_MAX_SLABS, 2u * (uint32_t)c->num_cus);
+    c->slab_count = std::min<uint32_t>(RSK_MAX_SLABS, 8u * (uint32_t)c->num_cus);
     RSK_HIP(hipMalloc(&c->d_slab, (uint64_t)c->slab_count * HLL_REGS));
     c->small_bytes = 1 << 20;
     RSK_HIP(hipMalloc(&c->d_small, c->small_bytes));
@@ -643,17 +649,23 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
     // PFMERGEs run in input order in Redis; a batch whose destinations are
     // also sources of other pairs would depend on that order.  Run such
     // batches as sequential waves of independent pairs.
-    uint8_t* s = out_scratch(c, 16 * n + 512);
+    const uint64_t seg = (8 * n + 255) & ~255ull;
+    uint8_t* s = out_scratch(c, 3 * seg + 512);
     auto* d_dst = reinterpret_cast<uint8_t**>(s);
-    auto* d_src = reinterpret_cast<const uint8_t**>(s + ((8 * n + 255) & ~255ull));
+    auto* d_src = reinterpret_cast<const uint8_t**>(s + seg);
+    auto* d_ids = reinterpret_cast<uint64_t*>(s + 2 * seg);
     uint64_t start = 0;
     while (start < n) {
-      // Grow the wave while no pair reads or writes a sketch written earlier in it.
-      std::map<const uint8_t*, int> written;
+      // Grow the wave while no pair touches a sketch another pair of the wave
+      // writes (RAW), or writes one another pair reads (WAR) or writes (WAW).
+      std::unordered_set<const uint8_t*> written, read;
       uint64_t end = start;
       while (end < n) {
-        if (written.count(sp[end]) || written.count(dp[end])) break;
-        written[dp[end]] = 1;
+        const uint8_t* d = dp[end];
+        const uint8_t* r = sp[end];
+        if (written.count(d) || read.count(d) || (r && written.count(r))) break;
+        written.insert(d);
+        if (r) read.insert(r);
         ++end;
       }
       RSK_HIP(hipMemcpyAsync(d_dst, dp.data() + start, (end - start) * 8, hipMemcpyHostToDevice, c->stream));
@@ -662,7 +674,11 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
       RSK_HIP(hipStreamSynchronize(c->stream));
       start = end;
     }
-    for (uint64_t i = 0; i < n; ++i) invalidate(h, dst_ids[i], nullptr, true);
+    // PFMERGE invalidates every destination's cache (one launch for the batch).
+    RSK_HIP(hipMemcpyAsync(d_ids, dst_ids, n * 8, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(invalidate_list_kernel, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0,
+                       c->stream, h->d_card, d_ids, n);
+    RSK_CHECK_LAUNCH("invalidate_list");
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }

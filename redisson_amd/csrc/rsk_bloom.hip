@@ -66,11 +66,94 @@ __global__ __launch_bounds__(256) void bloom_contains_kernel(const uint8_t* __re
     uint32_t all = 1;
     for (int t = 0; t < k - 1; ++t) {
       uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
-      all &= (bits[idx >> 5] & bit_mask(idx)) != 0;
+      if ((bits[idx >> 5] & bit_mask(idx)) == 0) {  // first clear bit decides (early exit)
+        all = 0;
+        break;
+      }
       h += (t & 1) ? h1 : h2;
     }
     out[i] = (uint8_t)all;
   }
+}
+
+static uint32_t grid_for(rsk_ctx* c, uint64_t n);
+
+// contains with early exit: a key stops probing at its first clear bit, so
+// a fresh key costs ~1/(1-fill) gathers instead of k-1 (fill ~0.52 at the
+// optimal size: ~2 instead of 6).  U keys per lane keep U dependent probe
+// chains in flight; the random 4-byte gather rate, not latency, is the bound.
+template <int U>
+__global__ __launch_bounds__(256) void bloom_contains16_ee_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                                  const uint32_t* __restrict__ bits, FastMod63 fm,
+                                                                  int k, uint8_t* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
+  for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x) * U + threadIdx.x; base < n; base += stride) {
+    uint64_t h[U], h1[U], h2[U];
+    bool alive[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)u * blockDim.x;
+      alive[u] = i < n;
+      if (alive[u]) {
+        uint4 v = ld_nt16(keys + i);
+        uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
+        h1[u] = xxh64_16(w0, w1);
+        h2[u] = farm_16(w0, w1);
+        h[u] = h1[u];
+      }
+    }
+    bool live_key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) live_key[u] = alive[u];
+    for (int t = 0; t < k - 1; ++t) {
+      uint32_t w[U];
+      uint64_t idx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        idx[u] = fastmod63(h[u] & JAVA_LONG_MAX, fm);
+        w[u] = alive[u] ? bits[idx[u] >> 5] : 0xFFFFFFFFu;
+      }
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        alive[u] = alive[u] && (w[u] & bit_mask(idx[u])) != 0;
+        h[u] += (t & 1) ? h1[u] : h2[u];
+        any |= alive[u];
+      }
+      if (!__any(any)) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)u * blockDim.x;
+      if (live_key[u]) out[i] = (uint8_t)alive[u];
+    }
+  }
+}
+
+template <int U>
+static void launch_contains_ee(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, uint32_t blocks_per_cu) {
+  uint64_t g = (k.n + 256 * U - 1) / (256 * U);
+  uint64_t cap = (uint64_t)c->num_cus * blocks_per_cu;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  hipLaunchKernelGGL(bloom_contains16_ee_kernel<U>, dim3((uint32_t)g), dim3(256), 0, c->stream,
+                     reinterpret_cast<const uint4*>(k.data), k.n, b->d_bits, b->fm, b->k, d_out);
+}
+
+void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant) {
+  switch (variant) {
+    case 0:
+      hipLaunchKernelGGL(bloom_contains_kernel<true>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data,
+                         nullptr, 16u, k.n, b->d_bits, b->fm, b->k, d_out);
+      break;
+    case 1: launch_contains_ee<1>(c, b, k, d_out, 32); break;
+    case 2: launch_contains_ee<2>(c, b, k, d_out, 32); break;
+    case 3: launch_contains_ee<4>(c, b, k, d_out, 32); break;
+    case 4: launch_contains_ee<1>(c, b, k, d_out, 8); break;
+    case 5: launch_contains_ee<2>(c, b, k, d_out, 8); break;
+    default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
+  }
+  RSK_CHECK_LAUNCH("bloom_contains_variant");
 }
 
 static bool fixed16(const DevKeys& k) {
@@ -101,8 +184,7 @@ void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* 
   if (k.n == 0) return;
   if (fixed16(k)) {
     ProfScope ps(c, "bloom_contains16");
-    hipLaunchKernelGGL(bloom_contains_kernel<true>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, nullptr,
-                       16u, k.n, b->d_bits, b->fm, b->k, d_out);
+    launch_contains_ee<2>(c, b, k, d_out, 32);
     RSK_CHECK_LAUNCH("bloom_contains16");
   } else {
     ProfScope ps(c, "bloom_contains");

@@ -104,6 +104,31 @@ RSK_DEV uint64_t murmur64a(const uint8_t* p, uint64_t len) {
   return mm_final(h);
 }
 
+// The same for keys of at most 64 bytes with every load issued up front (one
+// memory round trip per key instead of one per 8-byte block).  Words past
+// the key are not loaded (predicated) and the tail is read ending at the
+// key's last byte, so nothing beyond the key is touched.
+RSK_DEV uint64_t murmur64a_le64(const uint8_t* p, uint32_t len) {
+  uint64_t w[8];
+  const uint32_t nb = len >> 3, t = len & 7;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = (uint32_t)j < nb ? ld_u64(p + 8 * j) : 0;
+  const uint64_t tail = t ? ld_tail(p, len, t) : 0;
+  uint64_t h = (uint64_t)HLL_SEED ^ ((uint64_t)len * MM_M);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if ((uint32_t)j < nb) {
+      h ^= mm_mix(w[j]);
+      h *= MM_M;
+    }
+  }
+  if (t) {
+    h ^= tail;
+    h *= MM_M;
+  }
+  return mm_final(h);
+}
+
 // hllPatLen (Redis 3.2.0): rank = 1 + zeros from bit 14 up, bit 63 forced.
 RSK_DEV uint32_t hll_rank(uint64_t h) {
   uint64_t v = (h >> HLL_P) | (1ULL << (63 - HLL_P));

@@ -57,17 +57,16 @@ RSK_DEV void hll_update(uint32_t* regs, uint64_t h) {
   atomicMax(&regs[hll_index(h)], hll_rank(h));
 }
 
-// Fixed 16-byte keys: the C2 hot path.  U keys per lane in flight.
-template <int U>
-__global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add16_kernel(const uint4* __restrict__ keys, uint64_t n,
-                                                                       uint64_t per_block,
-                                                                       uint8_t* __restrict__ slabs) {
+// Fixed 16-byte keys: the C2 hot path.  U keys per lane in flight, T lanes
+// per workgroup (256 measured fastest: fewer waves contend for the LDS file).
+template <int U, int T>
+__global__ __launch_bounds__(T) void hll_add16_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                      uint64_t per_block, uint8_t* __restrict__ slabs) {
   __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
   lds_zero(regs);
   __syncthreads();
   const uint64_t begin = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  constexpr int T = RSK_ADD_THREADS;
   uint64_t i = begin + threadIdx.x;
   for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
     uint4 v[U];
@@ -86,6 +85,66 @@ __global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add16_kernel(const uin
   }
   __syncthreads();
   lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// Tuning variants of the 16-byte kernel (rsk_diag_hll_variant): keys in
+// flight per lane U, workgroup size T, nontemporal loads NT.
+template <int U, int T, bool NT>
+__global__ __launch_bounds__(T) void hll_add16_variant(const uint4* __restrict__ keys, uint64_t n, uint64_t per_block,
+                                                       uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
+  lds_zero(regs);
+  __syncthreads();
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  uint64_t i = begin + threadIdx.x;
+  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? ld_nt16(&keys[i + (uint64_t)u * T]) : keys[i + (uint64_t)u * T];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      hll_update(regs, murmur64a_16(((uint64_t)v[u].y << 32) | v[u].x, ((uint64_t)v[u].w << 32) | v[u].z));
+  }
+  for (; i < end; i += T) {
+    uint4 v = keys[i];
+    hll_update(regs, murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z));
+  }
+  __syncthreads();
+  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+template <int U, int T, bool NT>
+static void launch_variant(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu) {
+  uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * wg_per_cu, c->slab_count);
+  const uint64_t tile = (uint64_t)T * U;
+  uint64_t per_block = (n + blocks - 1) / blocks;
+  per_block = (per_block + tile - 1) / tile * tile;
+  blocks = (n + per_block - 1) / per_block;
+  hipLaunchKernelGGL((hll_add16_variant<U, T, NT>), dim3((uint32_t)blocks), dim3(T), 0, c->stream, keys, n, per_block,
+                     c->d_slab);
+}
+
+template <int U, int T>
+static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu);
+
+void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n) {
+  switch (variant) {
+    case 8: launch_b8<4, 512>(c, keys, n, 4); break;
+    case 9: launch_b8<4, 256>(c, keys, n, 8); break;
+    case 10: launch_b8<8, 512>(c, keys, n, 4); break;
+    case 11: launch_b8<4, 1024>(c, keys, n, 2); break;
+    case 0: launch_variant<4, 512, true>(c, keys, n, 2); break;
+    case 1: launch_variant<8, 512, true>(c, keys, n, 2); break;
+    case 2: launch_variant<2, 512, true>(c, keys, n, 2); break;
+    case 3: launch_variant<4, 512, false>(c, keys, n, 2); break;
+    case 4: launch_variant<4, 1024, true>(c, keys, n, 2); break;
+    case 5: launch_variant<4, 256, true>(c, keys, n, 2); break;
+    case 6: launch_variant<8, 1024, true>(c, keys, n, 2); break;
+    case 7: launch_variant<2, 1024, true>(c, keys, n, 2); break;
+    default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
+  }
+  RSK_CHECK_LAUNCH("hll_variant");
 }
 
 // Any fixed stride or blob+offsets: lane-per-key MurmurHash64A.
@@ -109,7 +168,265 @@ __global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add_bytes_kernel(const
       s = i * fixed_len;
       len = fixed_len;
     }
-    hll_update(regs, murmur64a(data + s, len));
+    hll_update(regs, len <= 64 ? murmur64a_le64(data + s, (uint32_t)len) : murmur64a(data + s, len));
+  }
+  __syncthreads();
+  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// ---- byte-register LDS file (16 KiB): check-then-CAS update.  After the
+// first few keys per register almost every key only reads its register
+// (a rank above the current value is rare), so the RMW is rarely taken and
+// the 4x smaller file leaves LDS for staging and for more workgroups.
+RSK_DEV void hll_update8(uint32_t* regs32, uint64_t h) {
+  const uint32_t idx = hll_index(h), rank = hll_rank(h);
+  uint32_t* w = regs32 + (idx >> 2);
+  const uint32_t sh = (idx & 3u) * 8;
+  uint32_t cur = *w;
+  while (((cur >> sh) & 0xFFu) < rank) {
+    const uint32_t nw = (cur & ~(0xFFu << sh)) | (rank << sh);
+    const uint32_t prev = atomicCAS(w, cur, nw);
+    if (prev == cur) break;
+    cur = prev;
+  }
+}
+
+__device__ __forceinline__ void lds8_zero(uint32_t* regs32) {
+  uint4* r4 = reinterpret_cast<uint4*>(regs32);
+  for (int j = threadIdx.x; j < HLL_REGS / 16; j += blockDim.x) r4[j] = make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void lds8_to_slab(const uint32_t* regs32, uint8_t* slab) {
+  const uint4* r4 = reinterpret_cast<const uint4*>(regs32);
+  uint4* out = reinterpret_cast<uint4*>(slab);
+  for (int j = threadIdx.x; j < HLL_REGS / 16; j += blockDim.x) out[j] = r4[j];
+}
+
+// 16-byte keys with the byte-register file (tuning variant).
+template <int U, int T>
+__global__ __launch_bounds__(T) void hll_add16_b8_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                         uint64_t per_block, uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
+  lds8_zero(regs32);
+  __syncthreads();
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  uint64_t i = begin + threadIdx.x;
+  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[i + (uint64_t)u * T]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      hll_update8(regs32, murmur64a_16(((uint64_t)v[u].y << 32) | v[u].x, ((uint64_t)v[u].w << 32) | v[u].z));
+  }
+  for (; i < end; i += T) {
+    uint4 v = keys[i];
+    hll_update8(regs32, murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z));
+  }
+  __syncthreads();
+  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+template <int U, int T>
+static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu) {
+  uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * wg_per_cu, c->slab_count);
+  const uint64_t tile = (uint64_t)T * U;
+  uint64_t per_block = (n + blocks - 1) / blocks;
+  per_block = (per_block + tile - 1) / tile * tile;
+  blocks = (n + per_block - 1) / per_block;
+  hipLaunchKernelGGL((hll_add16_b8_kernel<U, T>), dim3((uint32_t)blocks), dim3(T), 0, c->stream, keys, n, per_block,
+                     c->d_slab);
+}
+
+// Blob + offsets, LDS-staged (the C4 path).  A workgroup takes tiles of T
+// consecutive keys; their bytes are one contiguous blob range, loaded with
+// coalesced 16-byte loads into LDS, and each lane then hashes its key from
+// LDS with aligned 8-byte reads + funnel shifts.  A tile whose bytes exceed
+// the stage (keys longer than STAGE/T on average) is hashed from global.
+constexpr int VAR_T = 512;
+constexpr int VAR_STAGE = 32768;  // bytes per tile (64 B per key)
+
+RSK_DEV uint64_t lds_word(const uint64_t* st, uint32_t q, uint32_t sh) {
+  // 8 bytes starting at byte 8*q + sh (sh < 8) of the stage
+  const uint64_t lo = st[q];
+  return sh ? (lo >> (8 * sh)) | (st[q + 1] << (64 - 8 * sh)) : lo;
+}
+
+RSK_DEV uint64_t murmur64a_lds(const uint64_t* st, uint32_t off, uint32_t len) {
+  const uint32_t q = off >> 3, sh = off & 7;
+  const uint32_t nb = len >> 3, t = len & 7;
+  uint64_t h = (uint64_t)HLL_SEED ^ ((uint64_t)len * MM_M);
+  for (uint32_t j = 0; j < nb; ++j) {
+    h ^= mm_mix(lds_word(st, q + j, sh));
+    h *= MM_M;
+  }
+  if (t) {
+    // the tail's bytes start at off + 8*nb; bytes past the key are masked
+    h ^= lds_word(st, q + nb, sh) & ((1ULL << (8 * t)) - 1);
+    h *= MM_M;
+  }
+  return mm_final(h);
+}
+
+__global__ __launch_bounds__(VAR_T) void hll_add_var_staged_kernel(const uint8_t* __restrict__ data,
+                                                                   const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                   uint64_t per_block, uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
+  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
+  lds8_zero(regs32);
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  for (uint64_t base = begin; base < end; base += VAR_T) {
+    const uint64_t last = base + VAR_T < end ? base + VAR_T : end;
+    const uint64_t i = base + threadIdx.x;
+    const bool mine = i < last;
+    const uint64_t s = mine ? offsets[i] : 0;
+    const uint64_t e = mine ? offsets[i + 1] : 0;
+    const uint64_t lo = offsets[base], hi = offsets[last];
+    const uint64_t a0 = lo & ~uint64_t(15);
+    const bool staged = hi - a0 <= VAR_STAGE;
+    __syncthreads();  // previous tile's stage reads are done
+    if (staged) {
+      const uint32_t nchunk = (uint32_t)((hi - a0 + 15) >> 4);
+      const uint4* src = reinterpret_cast<const uint4*>(data + a0);
+      uint4* dst = reinterpret_cast<uint4*>(stage);
+      for (uint32_t c = threadIdx.x; c < nchunk; c += VAR_T) dst[c] = ld_nt16(src + c);
+    }
+    __syncthreads();
+    if (mine) {
+      const uint32_t len = (uint32_t)(e - s);
+      const uint64_t h = staged ? murmur64a_lds(stage, (uint32_t)(s - a0), len)
+                                : (len <= 64 ? murmur64a_le64(data + s, len) : murmur64a(data + s, len));
+      hll_update8(regs32, h);
+    }
+  }
+  __syncthreads();
+  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// Software-pipelined variant of the staged kernel: while a tile is hashed
+// from LDS, the next tile's bytes are already in flight into registers (16 B
+// per lane, coalesced) and the tile after that has its offsets in flight.
+// The stage is written from registers after a barrier (async-STAGE split).
+constexpr int VAR_CH = VAR_STAGE / 16 / VAR_T;  // 16-B chunks per lane (hi - a0 <= VAR_STAGE)
+
+struct VarTile {
+  uint64_t s, e, lo, hi;
+  bool mine, valid;
+};
+
+RSK_DEV VarTile var_desc(const uint64_t* __restrict__ offsets, uint64_t begin, uint64_t end, uint64_t t) {
+  VarTile d;
+  const uint64_t base = begin + t * VAR_T;
+  d.valid = base < end;
+  if (!d.valid) {
+    d.s = d.e = d.lo = d.hi = 0;
+    d.mine = false;
+    return d;
+  }
+  const uint64_t last = base + VAR_T < end ? base + VAR_T : end;
+  const uint64_t i = base + threadIdx.x;
+  d.mine = i < last;
+  d.s = d.mine ? offsets[i] : 0;
+  d.e = d.mine ? offsets[i + 1] : 0;
+  d.lo = offsets[base];
+  d.hi = offsets[last];
+  return d;
+}
+
+__global__ __launch_bounds__(VAR_T) void hll_add_var_pipe_kernel(const uint8_t* __restrict__ data,
+                                                                 const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                 uint64_t per_block, uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
+  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 8];
+  lds8_zero(regs32);
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  if (begin >= end) {
+    __syncthreads();
+    lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+    return;
+  }
+  const uint64_t ntile = (end - begin + VAR_T - 1) / VAR_T;
+  uint4 C[VAR_CH];
+  VarTile cur = var_desc(offsets, begin, end, 0);
+  VarTile nxt = var_desc(offsets, begin, end, 1);
+  uint64_t a0 = cur.lo & ~uint64_t(15);
+  bool staged = cur.hi - a0 <= VAR_STAGE;
+  uint32_t nch = staged ? (uint32_t)((cur.hi - a0 + 15) >> 4) : 0;
+#pragma unroll
+  for (int c = 0; c < VAR_CH; ++c) {
+    const uint32_t j = threadIdx.x + c * VAR_T;
+    if (j < nch) C[c] = ld_nt16(data + a0 + 16ull * j);
+  }
+  for (uint64_t t = 0; t < ntile; ++t) {
+    __syncthreads();  // every lane is done reading the previous tile
+    uint4* st4 = reinterpret_cast<uint4*>(stage);
+#pragma unroll
+    for (int c = 0; c < VAR_CH; ++c) {
+      const uint32_t j = threadIdx.x + c * VAR_T;
+      if (j < nch) st4[j] = C[c];
+    }
+    const uint64_t ca0 = a0;
+    const bool cstaged = staged;
+    const VarTile me = cur;
+    __syncthreads();
+    // Next tile: its bytes into registers, the one after: its offsets.
+    cur = nxt;
+    if (cur.valid) {
+      a0 = cur.lo & ~uint64_t(15);
+      staged = cur.hi - a0 <= VAR_STAGE;
+      nch = staged ? (uint32_t)((cur.hi - a0 + 15) >> 4) : 0;
+#pragma unroll
+      for (int c = 0; c < VAR_CH; ++c) {
+        const uint32_t j = threadIdx.x + c * VAR_T;
+        if (j < nch) C[c] = ld_nt16(data + a0 + 16ull * j);
+      }
+      nxt = var_desc(offsets, begin, end, t + 2);
+    } else {
+      nch = 0;
+    }
+    if (me.mine) {
+      const uint32_t len = (uint32_t)(me.e - me.s);
+      const uint64_t h = cstaged ? murmur64a_lds(stage, (uint32_t)(me.s - ca0), len)
+                                 : (len <= 64 ? murmur64a_le64(data + me.s, len) : murmur64a(data + me.s, len));
+      hll_update8(regs32, h);
+    }
+  }
+  __syncthreads();
+  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// Blob + offsets, the C4 path: U keys per lane per round, each key's bytes
+// fetched in one burst; longer keys fall back to the streaming loop.
+template <int U>
+__global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add_var_kernel(const uint8_t* __restrict__ data,
+                                                                         const uint64_t* __restrict__ offsets,
+                                                                         uint64_t n, uint64_t per_block,
+                                                                         uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
+  lds_zero(regs);
+  __syncthreads();
+  constexpr int T = RSK_ADD_THREADS;
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  for (uint64_t i = begin + threadIdx.x; i < end; i += (uint64_t)U * T) {
+    uint64_t s[U];
+    uint32_t len[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t j = i + (uint64_t)u * T;
+      ok[u] = j < end;
+      s[u] = ok[u] ? offsets[j] : 0;
+      len[u] = ok[u] ? (uint32_t)(offsets[j + 1] - s[u]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      uint64_t h = len[u] <= 64 ? murmur64a_le64(data + s[u], len[u]) : murmur64a(data + s[u], len[u]);
+      hll_update(regs, h);
+    }
   }
   __syncthreads();
   lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
@@ -154,19 +471,23 @@ __global__ __launch_bounds__(256) void hll_reduce_kernel(const uint8_t* __restri
 void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32_t* d_flag) {
   if (k.n == 0) return;
   constexpr uint64_t T = RSK_ADD_THREADS;
-  uint64_t max_blocks = c->slab_count;
-  // Enough keys per workgroup to amortise the 64 KiB LDS init + 16 KiB slab.
+  const uint64_t max_blocks = c->slab_count;
+  // Enough keys per workgroup to amortise the 64 KiB LDS init + 16 KiB slab;
+  // a persistent grid of the 2 workgroups per CU that the 64 KiB file allows.
   uint64_t blocks = (k.n + 4 * T - 1) / (4 * T);
-  if (blocks > max_blocks) blocks = max_blocks;
+  blocks = std::min<uint64_t>(blocks, std::min<uint64_t>(2ull * c->num_cus, max_blocks));
   if (blocks == 0) blocks = 1;
   uint64_t per_block = (k.n + blocks - 1) / blocks;
   if (k.offsets == nullptr && k.fixed_len == 16 && (reinterpret_cast<uintptr_t>(k.data) & 15) == 0) {
     // Round the slice up to whole tiles so every lane's loads stay coalesced.
-    const uint64_t tile = T * RSK_ADD_UNROLL;
+    constexpr uint64_t T16 = 256;
+    const uint64_t tile = T16 * RSK_ADD_UNROLL;
+    blocks = std::min<uint64_t>((k.n + tile - 1) / tile, std::min<uint64_t>(2ull * c->num_cus, max_blocks));
+    per_block = (k.n + blocks - 1) / blocks;
     per_block = (per_block + tile - 1) / tile * tile;
     blocks = (k.n + per_block - 1) / per_block;
     ProfScope ps(c, "hll_add16");
-    hipLaunchKernelGGL(hll_add16_kernel<RSK_ADD_UNROLL>, dim3((uint32_t)blocks), dim3(T), 0, c->stream,
+    hipLaunchKernelGGL((hll_add16_kernel<RSK_ADD_UNROLL, T16>), dim3((uint32_t)blocks), dim3(T16), 0, c->stream,
                        reinterpret_cast<const uint4*>(k.data), k.n, per_block, c->d_slab);
     RSK_CHECK_LAUNCH("hll_add16");
   } else if (k.offsets == nullptr) {
@@ -175,9 +496,14 @@ void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32
                        k.fixed_len, k.n, per_block, c->d_slab);
     RSK_CHECK_LAUNCH("hll_add_fixed");
   } else {
+    // LDS-staged tiles: 48 KiB of LDS per workgroup -> 3 workgroups per CU.
+    blocks = std::min<uint64_t>((k.n + VAR_T - 1) / VAR_T, std::min<uint64_t>(3ull * c->num_cus, max_blocks));
+    per_block = (k.n + blocks - 1) / blocks;
+    per_block = (per_block + VAR_T - 1) / VAR_T * VAR_T;
+    blocks = (k.n + per_block - 1) / per_block;
     ProfScope ps(c, "hll_add_var");
-    hipLaunchKernelGGL(hll_add_bytes_kernel<true>, dim3((uint32_t)blocks), dim3(T), 0, c->stream, k.data,
-                       k.offsets, 0u, k.n, per_block, c->d_slab);
+    hipLaunchKernelGGL(hll_add_var_pipe_kernel, dim3((uint32_t)blocks), dim3(VAR_T), 0, c->stream, k.data,
+                       k.offsets, k.n, per_block, c->d_slab);
     RSK_CHECK_LAUNCH("hll_add_var");
   }
   ProfScope ps(c, "hll_reduce");

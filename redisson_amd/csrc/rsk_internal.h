@@ -142,11 +142,13 @@ void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* con
                       uint64_t n);
 void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out);
 void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag);
+void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n);
 
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
+void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);
 void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out);
 void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes);
 // dst[0..S) = OR over rows of src[rows][S] (u32 words).

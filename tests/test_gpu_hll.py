@@ -259,3 +259,39 @@ def test_grouped_add_matches_oracle(L, engine, orc):
     _lib.check(L.rsk_hll_count(h, ids.ctypes.data, G, out.ctypes.data))
     want = [orc.hll_count_dense(ref[i * 16384:(i + 1) * 16384]) for i in range(G)]
     assert out.tolist() == want
+
+
+def test_batched_merge_and_union_follow_redis_order(L, engine, orc):
+    """rsk_hll_merge_batch == PFMERGE dst src issued in order (chains and
+    read-after-write inside one batch); rsk_hll_count_union_batch == PFCOUNT a b."""
+    from redisson_amd import KeyBatch, _lib
+
+    G = 64
+    rng = np.random.default_rng(21)
+    h = _pool(L, engine, G)
+    r = orc.RedisModel()
+    for g in range(0, G, 2):  # odd groups stay absent
+        keys = orc.gen_keys16(0x5EED0100 + g, 0, int(rng.integers(1, 3000)))
+        _add(L, h, KeyBatch.from_numpy(keys.reshape(-1, 16)), g)
+        r.pfadd(str(g), *[keys[16 * i:16 * i + 16].tobytes() for i in range(keys.size // 16)])
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, G, size=(300, 2))]
+    pairs += [(1, 2), (3, 1), (5, 3), (2, 5)]  # chains through destinations
+    d = np.array([p[0] for p in pairs], np.uint64)
+    s = np.array([p[1] for p in pairs], np.uint64)
+    _lib.check(L.rsk_hll_merge_batch(h, d.ctypes.data, s.ctypes.data, d.size))
+    for a, b in pairs:
+        r.pfmerge(str(a), str(b))
+    for g in range(G):
+        want = r.get(str(g))
+        got = _regs(L, h, g)
+        if want is None:
+            assert not got.any()
+        else:
+            assert np.array_equal(got, orc.hll_decode(want)[1]), g
+    members = rng.integers(0, G, size=(200, 3)).astype(np.uint64)
+    out = np.zeros(200, np.uint64)
+    _lib.check(L.rsk_hll_count_union_batch(h, members.ctypes.data, 3, 200, out.ctypes.data))
+    for i in range(200):
+        assert out[i] == r.pfcount(*[str(int(x)) for x in members[i]]), i
+    cnt = _count(L, h, list(range(G)))
+    assert [int(x) for x in cnt] == [r.pfcount(str(g)) for g in range(G)]
