@@ -182,6 +182,35 @@ int rsk_bloom_import_bits(rsk_bloom *b, const uint8_t *buf, size_t len);
 int rsk_bloom_or_bits(rsk_bloom *b, const uint8_t *bits, size_t len, uint32_t location);
 void *rsk_bloom_device_bits(rsk_bloom *b);
 
+/* --------------------------------------------------------------- RBitSet */
+/* A Redis string addressed as bits, MSB-first (bitops.c; the layout the
+ * Bloom filter uses).  Each call replaces the command RedissonBitSet sends
+ * (src/main/java/org/redisson/RedissonBitSet.java). */
+typedef struct rsk_bitset rsk_bitset;
+typedef enum rsk_bitop { RSK_BITOP_AND = 0, RSK_BITOP_OR = 1, RSK_BITOP_XOR = 2, RSK_BITOP_NOT = 3 } rsk_bitop;
+int rsk_bitset_create(rsk_ctx *ctx, rsk_bitset **out);  /* an absent key (empty string) */
+int rsk_bitset_destroy(rsk_bitset *b);
+/* STRLEN: size() = 8 * STRLEN (BitsSizeReplayConvertor.java:21-27). */
+int rsk_bitset_strlen(rsk_bitset *b, uint64_t *bytes);
+/* SETBIT off value for n offsets (set/clear(index) :70-80,:196-209); grows the
+ * string to (max offset >> 3) + 1 bytes like Redis.  offsets host or device. */
+int rsk_bitset_setbits(rsk_bitset *b, const uint64_t *offsets, uint64_t n, int value, uint32_t location);
+/* GETBIT for n offsets (get(index)); out in the offsets' location. */
+int rsk_bitset_getbits(rsk_bitset *b, const uint64_t *offsets, uint64_t n, uint32_t location, uint8_t *out);
+/* set(from, to) / clear(from, to) (:217-236): SETBIT i v for i in [from, to). */
+int rsk_bitset_set_range(rsk_bitset *b, uint64_t from, uint64_t to, int value);
+/* BITCOUNT (cardinality(), :240-243). */
+int rsk_bitset_bitcount(rsk_bitset *b, uint64_t *out);
+/* length(): index of the highest set bit + 1 (0 when none). */
+int rsk_bitset_length(rsk_bitset *b, uint64_t *out);
+/* BITOP op dst src1..srck (and/or/xor(names) apply it as BITOP op self self
+ * names, :125-145; not() as BITOP NOT self self).  dst may be a source. */
+int rsk_bitset_bitop(int op, rsk_bitset *dst, rsk_bitset *const *srcs, uint32_t k);
+/* GET (toByteArray(), :88-91) / SET (set(BitSet), :211-214) / DEL (clear()). */
+int rsk_bitset_get_bytes(rsk_bitset *b, uint8_t *buf, size_t cap, size_t *len);
+int rsk_bitset_set_bytes(rsk_bitset *b, const uint8_t *buf, size_t len);
+int rsk_bitset_clear(rsk_bitset *b);
+
 /* ------------------------------------------------------- device memory */
 /* HBM buffers for keys / replies that stay resident (JNI: wrap as direct
  * buffers; Python: redisson_amd.devmem.DeviceBuffer). */

@@ -120,6 +120,18 @@ SIGNATURES = {
     "rsk_bloom_import_bits": (ctypes.c_int, [_vp, _vp, _sz]),
     "rsk_bloom_or_bits": (ctypes.c_int, [_vp, _vp, _sz, _u32]),
     "rsk_bloom_device_bits": (_vp, [_vp]),
+    "rsk_bitset_create": (ctypes.c_int, [_vp, _P(_vp)]),
+    "rsk_bitset_destroy": (ctypes.c_int, [_vp]),
+    "rsk_bitset_strlen": (ctypes.c_int, [_vp, _P(_u64)]),
+    "rsk_bitset_setbits": (ctypes.c_int, [_vp, _vp, _u64, ctypes.c_int, _u32]),
+    "rsk_bitset_getbits": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp]),
+    "rsk_bitset_set_range": (ctypes.c_int, [_vp, _u64, _u64, ctypes.c_int]),
+    "rsk_bitset_bitcount": (ctypes.c_int, [_vp, _P(_u64)]),
+    "rsk_bitset_length": (ctypes.c_int, [_vp, _P(_u64)]),
+    "rsk_bitset_bitop": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _u32]),
+    "rsk_bitset_get_bytes": (ctypes.c_int, [_vp, _vp, _sz, _P(_sz)]),
+    "rsk_bitset_set_bytes": (ctypes.c_int, [_vp, _vp, _sz]),
+    "rsk_bitset_clear": (ctypes.c_int, [_vp]),
     "rsk_dev_alloc": (ctypes.c_int, [_vp, _u64, _P(_vp)]),
     "rsk_dev_free": (ctypes.c_int, [_vp, _vp]),
     "rsk_memcpy": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32]),

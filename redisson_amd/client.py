@@ -63,6 +63,11 @@ class Redisson:
     def getBloomFilter(self, name: str, codec=None) -> RBloomFilter:
         return RBloomFilter(self, name, codec)
 
+    def getBitSet(self, name: str):
+        from .bitset import RBitSet
+
+        return RBitSet(self, name)
+
     def createBatch(self):
         from .batch import RBatch
 
@@ -81,6 +86,8 @@ class Redisson:
             _lib.load().rsk_hll_destroy(obj.pool)
         elif kind == "bloom":
             _lib.load().rsk_bloom_destroy(obj)
+        elif kind == "bitset":
+            _lib.load().rsk_bitset_destroy(obj)
         return 1
 
     def delete(self, *names) -> int:
@@ -115,6 +122,20 @@ class Redisson:
             h = ctypes.c_void_p()
             _lib.check(_lib.load().rsk_bloom_create(self.engine.ctx, size, k, ctypes.byref(h)))
             self._db[name] = ("bloom", h)
+            return h
+
+    def _bitset_handle(self, name: str, create: bool):
+        with self._lock:
+            v = self._db.get(name)
+            if v is not None:
+                if v[0] != "bitset":
+                    self._wrongtype(name)
+                return v[1]
+            if not create:
+                return None
+            h = ctypes.c_void_p()
+            _lib.check(_lib.load().rsk_bitset_create(self.engine.ctx, ctypes.byref(h)))
+            self._db[name] = ("bitset", h)
             return h
 
     def _hash(self, name: str) -> dict:

@@ -10,7 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <new>
-#include <unordered_set>
+#include <unordered_map>
 
 #include "rsk_internal.h"
 
@@ -441,16 +441,26 @@ int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_
     CtxLock l(c);
     bool created;
     create_if_missing(h, id, &created);
+    // The reduce kernel raises the flag to this call's epoch when a register
+    // grows and invalidates the card cache itself: no memset, no extra launch.
     uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->d_small);
-    RSK_HIP(hipMemsetAsync(d_flag, 0, 4, c->stream));
-    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { hll_add_launch(c, dk, regs_of(h, id), d_flag); });
-    invalidate(h, id, d_flag, created);
+    if (++c->epoch == 0) {  // wrapped: restart the epoch sequence from a clean flag
+      RSK_HIP(hipMemsetAsync(d_flag, 0, 4, c->stream));
+      c->epoch = 1;
+    }
+    const uint32_t epoch = c->epoch;
+    bool any_chunk = false;
+    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) {
+      hll_add_launch(c, dk, regs_of(h, id), h->d_card + id, d_flag, epoch, created && !any_chunk);
+      any_chunk = true;
+    });
+    if (!any_chunk && created) invalidate(h, id, nullptr, true);  // PFADD key (no elements) creates it
     if (changed_out) {
       RSK_HIP(hipMemcpyAsync(c->h_small, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
       uint32_t f;
       std::memcpy(&f, c->h_small, 4);
-      *changed_out = (uint8_t)((f != 0) || created);
+      *changed_out = (uint8_t)((f == epoch) || created);
     }
   });
 }
@@ -547,18 +557,31 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
     CtxLock l(c);
     if (n == 0) return;
     uint64_t* d_ids = nullptr;
+    SmallIds small{};
+    const bool by_value = ids && n <= 8;
     uint8_t* s = out_scratch(c, (ids ? n * 8 : 0) + n * 8 + 256);
     if (ids) {
       for (uint64_t i = 0; i < n; ++i) need(ids[i] < h->n, "sketch id out of range");
-      d_ids = reinterpret_cast<uint64_t*>(s);
-      RSK_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, c->stream));
+      if (by_value) {
+        for (uint64_t i = 0; i < n; ++i) small.v[i] = ids[i];
+        small.n = (uint32_t)n;
+      } else {
+        d_ids = reinterpret_cast<uint64_t*>(s);
+        RSK_HIP(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, c->stream));
+      }
     } else {
       need(n <= h->n, "n exceeds pool size");
     }
     uint64_t* d_out = reinterpret_cast<uint64_t*>(s + (ids ? ((n * 8 + 255) & ~255ull) : 0));
-    hll_count_launch(c, h->d_regs, h->d_card, d_ids, n, d_out);
-    RSK_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
-    RSK_HIP(hipStreamSynchronize(c->stream));
+    hll_count_launch(c, h->d_regs, h->d_card, d_ids, small, n, d_out);
+    if (n * 8 <= 4096) {  // small results come back through the pinned buffer
+      RSK_HIP(hipMemcpyAsync(c->h_small + 4096, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      std::memcpy(out, c->h_small + 4096, n * 8);
+    } else {
+      RSK_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+    }
   });
 }
 
@@ -647,33 +670,49 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
       dp[i] = regs_of(h, dst_ids[i]);
     }
     // PFMERGEs run in input order in Redis; a batch whose destinations are
-    // also sources of other pairs would depend on that order.  Run such
-    // batches as sequential waves of independent pairs.
+    // also sources of other pairs depends on that order.  Level the pairs:
+    // a pair runs after the last writer of its source (RAW) and of its
+    // destination (WAW), and after the last reader of its destination (WAR).
+    // Pairs of one level are independent and run as one launch.
+    std::unordered_map<uint64_t, uint32_t> last_w, last_r;
+    std::vector<uint32_t> level(n);
+    uint32_t max_level = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      uint32_t lv = 0;
+      auto it = last_w.find(src_ids[i]);
+      if (it != last_w.end()) lv = std::max(lv, it->second);
+      it = last_w.find(dst_ids[i]);
+      if (it != last_w.end()) lv = std::max(lv, it->second);
+      it = last_r.find(dst_ids[i]);
+      if (it != last_r.end()) lv = std::max(lv, it->second);
+      level[i] = ++lv;
+      last_w[dst_ids[i]] = lv;
+      uint32_t& r = last_r[src_ids[i]];
+      r = std::max(r, lv);
+      max_level = std::max(max_level, lv);
+    }
+    std::vector<uint64_t> start(max_level + 2, 0);
+    for (uint64_t i = 0; i < n; ++i) start[level[i] + 1]++;
+    for (uint32_t l = 1; l <= max_level + 1; ++l) start[l] += start[l - 1];
+    std::vector<uint8_t*> dps(n);
+    std::vector<const uint8_t*> sps(n);
+    {
+      std::vector<uint64_t> fill(start.begin(), start.end());
+      for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t p = fill[level[i]]++;
+        dps[p] = dp[i];
+        sps[p] = sp[i];
+      }
+    }
     const uint64_t seg = (8 * n + 255) & ~255ull;
     uint8_t* s = out_scratch(c, 3 * seg + 512);
     auto* d_dst = reinterpret_cast<uint8_t**>(s);
     auto* d_src = reinterpret_cast<const uint8_t**>(s + seg);
     auto* d_ids = reinterpret_cast<uint64_t*>(s + 2 * seg);
-    uint64_t start = 0;
-    while (start < n) {
-      // Grow the wave while no pair touches a sketch another pair of the wave
-      // writes (RAW), or writes one another pair reads (WAR) or writes (WAW).
-      std::unordered_set<const uint8_t*> written, read;
-      uint64_t end = start;
-      while (end < n) {
-        const uint8_t* d = dp[end];
-        const uint8_t* r = sp[end];
-        if (written.count(d) || read.count(d) || (r && written.count(r))) break;
-        written.insert(d);
-        if (r) read.insert(r);
-        ++end;
-      }
-      RSK_HIP(hipMemcpyAsync(d_dst, dp.data() + start, (end - start) * 8, hipMemcpyHostToDevice, c->stream));
-      RSK_HIP(hipMemcpyAsync(d_src, sp.data() + start, (end - start) * 8, hipMemcpyHostToDevice, c->stream));
-      hll_merge_launch(c, d_dst, d_src, 1, end - start);
-      RSK_HIP(hipStreamSynchronize(c->stream));
-      start = end;
-    }
+    RSK_HIP(hipMemcpyAsync(d_dst, dps.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemcpyAsync(d_src, sps.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    for (uint32_t l = 1; l <= max_level; ++l)
+      hll_merge_launch(c, d_dst + start[l], d_src + start[l], 1, start[l + 1] - start[l]);
     // PFMERGE invalidates every destination's cache (one launch for the batch).
     RSK_HIP(hipMemcpyAsync(d_ids, dst_ids, n * 8, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(invalidate_list_kernel, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0,

@@ -304,138 +304,16 @@ __global__ __launch_bounds__(VAR_T) void hll_add_var_staged_kernel(const uint8_t
   lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
 }
 
-// Software-pipelined variant of the staged kernel: while a tile is hashed
-// from LDS, the next tile's bytes are already in flight into registers (16 B
-// per lane, coalesced) and the tile after that has its offsets in flight.
-// The stage is written from registers after a barrier (async-STAGE split).
-constexpr int VAR_CH = VAR_STAGE / 16 / VAR_T;  // 16-B chunks per lane (hi - a0 <= VAR_STAGE)
-
-struct VarTile {
-  uint64_t s, e, lo, hi;
-  bool mine, valid;
-};
-
-RSK_DEV VarTile var_desc(const uint64_t* __restrict__ offsets, uint64_t begin, uint64_t end, uint64_t t) {
-  VarTile d;
-  const uint64_t base = begin + t * VAR_T;
-  d.valid = base < end;
-  if (!d.valid) {
-    d.s = d.e = d.lo = d.hi = 0;
-    d.mine = false;
-    return d;
-  }
-  const uint64_t last = base + VAR_T < end ? base + VAR_T : end;
-  const uint64_t i = base + threadIdx.x;
-  d.mine = i < last;
-  d.s = d.mine ? offsets[i] : 0;
-  d.e = d.mine ? offsets[i + 1] : 0;
-  d.lo = offsets[base];
-  d.hi = offsets[last];
-  return d;
-}
-
-__global__ __launch_bounds__(VAR_T) void hll_add_var_pipe_kernel(const uint8_t* __restrict__ data,
-                                                                 const uint64_t* __restrict__ offsets, uint64_t n,
-                                                                 uint64_t per_block, uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
-  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 8];
-  lds8_zero(regs32);
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  if (begin >= end) {
-    __syncthreads();
-    lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-    return;
-  }
-  const uint64_t ntile = (end - begin + VAR_T - 1) / VAR_T;
-  uint4 C[VAR_CH];
-  VarTile cur = var_desc(offsets, begin, end, 0);
-  VarTile nxt = var_desc(offsets, begin, end, 1);
-  uint64_t a0 = cur.lo & ~uint64_t(15);
-  bool staged = cur.hi - a0 <= VAR_STAGE;
-  uint32_t nch = staged ? (uint32_t)((cur.hi - a0 + 15) >> 4) : 0;
-#pragma unroll
-  for (int c = 0; c < VAR_CH; ++c) {
-    const uint32_t j = threadIdx.x + c * VAR_T;
-    if (j < nch) C[c] = ld_nt16(data + a0 + 16ull * j);
-  }
-  for (uint64_t t = 0; t < ntile; ++t) {
-    __syncthreads();  // every lane is done reading the previous tile
-    uint4* st4 = reinterpret_cast<uint4*>(stage);
-#pragma unroll
-    for (int c = 0; c < VAR_CH; ++c) {
-      const uint32_t j = threadIdx.x + c * VAR_T;
-      if (j < nch) st4[j] = C[c];
-    }
-    const uint64_t ca0 = a0;
-    const bool cstaged = staged;
-    const VarTile me = cur;
-    __syncthreads();
-    // Next tile: its bytes into registers, the one after: its offsets.
-    cur = nxt;
-    if (cur.valid) {
-      a0 = cur.lo & ~uint64_t(15);
-      staged = cur.hi - a0 <= VAR_STAGE;
-      nch = staged ? (uint32_t)((cur.hi - a0 + 15) >> 4) : 0;
-#pragma unroll
-      for (int c = 0; c < VAR_CH; ++c) {
-        const uint32_t j = threadIdx.x + c * VAR_T;
-        if (j < nch) C[c] = ld_nt16(data + a0 + 16ull * j);
-      }
-      nxt = var_desc(offsets, begin, end, t + 2);
-    } else {
-      nch = 0;
-    }
-    if (me.mine) {
-      const uint32_t len = (uint32_t)(me.e - me.s);
-      const uint64_t h = cstaged ? murmur64a_lds(stage, (uint32_t)(me.s - ca0), len)
-                                 : (len <= 64 ? murmur64a_le64(data + me.s, len) : murmur64a(data + me.s, len));
-      hll_update8(regs32, h);
-    }
-  }
-  __syncthreads();
-  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-// Blob + offsets, the C4 path: U keys per lane per round, each key's bytes
-// fetched in one burst; longer keys fall back to the streaming loop.
-template <int U>
-__global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add_var_kernel(const uint8_t* __restrict__ data,
-                                                                         const uint64_t* __restrict__ offsets,
-                                                                         uint64_t n, uint64_t per_block,
-                                                                         uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
-  lds_zero(regs);
-  __syncthreads();
-  constexpr int T = RSK_ADD_THREADS;
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  for (uint64_t i = begin + threadIdx.x; i < end; i += (uint64_t)U * T) {
-    uint64_t s[U];
-    uint32_t len[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t j = i + (uint64_t)u * T;
-      ok[u] = j < end;
-      s[u] = ok[u] ? offsets[j] : 0;
-      len[u] = ok[u] ? (uint32_t)(offsets[j + 1] - s[u]) : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!ok[u]) continue;
-      uint64_t h = len[u] <= 64 ? murmur64a_le64(data + s[u], len[u]) : murmur64a(data + s[u], len[u]);
-      hll_update(regs, h);
-    }
-  }
-  __syncthreads();
-  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
 // Max-merge `nslabs` slabs and the sketch's registers; 64 registers per
-// workgroup of 256 lanes (grid 256).  *flag |= 1 if any register grew.
+// workgroup of 256 lanes (grid 256).  If any register grew: *flag =
+// max(*flag, epoch) (the caller's call number, so no reset is needed) and
+// the Redis card cache is invalidated (HLL_INVALIDATE_CACHE), as it is when
+// the key was just created.
 __global__ __launch_bounds__(256) void hll_reduce_kernel(const uint8_t* __restrict__ slabs, uint32_t nslabs,
-                                                         uint8_t* __restrict__ regs, uint32_t* __restrict__ flag) {
+                                                         uint8_t* __restrict__ regs, uint32_t* __restrict__ flag,
+                                                         uint32_t epoch, unsigned long long* __restrict__ card,
+                                                         int created) {
+  if (created && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(card, 1ull << 63);
   __shared__ uint4 part[4][256];
   const int t = threadIdx.x;
   const uint64_t col = (uint64_t)blockIdx.x * 64;  // first register of this block
@@ -463,12 +341,14 @@ __global__ __launch_bounds__(256) void hll_reduce_kernel(const uint8_t* __restri
     uint4 nw = bmax16(old, part[t][0]);
     if (nw.x != old.x || nw.y != old.y || nw.z != old.z || nw.w != old.w) {
       *r = nw;
-      atomicOr(flag, 1u);
+      atomicMax(flag, epoch);
+      atomicOr(card, 1ull << 63);
     }
   }
 }
 
-void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32_t* d_flag) {
+void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64_t* d_card, uint32_t* d_flag,
+                    uint32_t epoch, bool created) {
   if (k.n == 0) return;
   constexpr uint64_t T = RSK_ADD_THREADS;
   const uint64_t max_blocks = c->slab_count;
@@ -502,13 +382,13 @@ void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32
     per_block = (per_block + VAR_T - 1) / VAR_T * VAR_T;
     blocks = (k.n + per_block - 1) / per_block;
     ProfScope ps(c, "hll_add_var");
-    hipLaunchKernelGGL(hll_add_var_pipe_kernel, dim3((uint32_t)blocks), dim3(VAR_T), 0, c->stream, k.data,
+    hipLaunchKernelGGL(hll_add_var_staged_kernel, dim3((uint32_t)blocks), dim3(VAR_T), 0, c->stream, k.data,
                        k.offsets, k.n, per_block, c->d_slab);
     RSK_CHECK_LAUNCH("hll_add_var");
   }
   ProfScope ps(c, "hll_reduce");
   hipLaunchKernelGGL(hll_reduce_kernel, dim3(HLL_REGS / 64), dim3(256), 0, c->stream, c->d_slab, (uint32_t)blocks,
-                     d_regs_sketch, d_flag);
+                     d_regs_sketch, d_flag, epoch, reinterpret_cast<unsigned long long*>(d_card), created ? 1 : 0);
   RSK_CHECK_LAUNCH("hll_reduce");
 }
 
@@ -694,10 +574,10 @@ RSK_DEV double dense_order_sum(const uint8_t* r, int* ezp) {
 }
 
 __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
-                                                        const uint64_t* __restrict__ ids, uint64_t n,
+                                                        const uint64_t* __restrict__ ids, SmallIds small, uint64_t n,
                                                         const double* __restrict__ lc, uint64_t* __restrict__ out) {
   for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
-    const uint64_t id = ids ? ids[b] : b;
+    const uint64_t id = ids ? ids[b] : (small.n ? small.v[b] : b);
     const uint64_t cached = card[id];
     if ((cached >> 63) == 0) {  // HLL_VALID_CACHE
       if (threadIdx.x == 0) out[b] = cached;
@@ -727,13 +607,13 @@ __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restric
   }
 }
 
-void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids, uint64_t n,
-                      uint64_t* d_out) {
+void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
+                      const SmallIds& small, uint64_t n, uint64_t* d_out) {
   if (n == 0) return;
   uint64_t grid = n < (1u << 20) ? n : (1u << 20);
   ProfScope ps(c, "hll_count");
-  hipLaunchKernelGGL(hll_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_regs, d_card, d_ids, n, c->d_lc,
-                     d_out);
+  hipLaunchKernelGGL(hll_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_regs, d_card, d_ids, small, n,
+                     c->d_lc, d_out);
   RSK_CHECK_LAUNCH("hll_count");
 }
 

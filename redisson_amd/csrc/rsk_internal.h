@@ -85,6 +85,8 @@ struct rsk_ctx {
   void* comm = nullptr;
   int nranks = 1;
   int rank = 0;
+  // call number written by kernels that report "something changed" (no reset)
+  uint32_t epoch = 0;
 
   uint8_t* work(uint64_t bytes);
 };
@@ -132,10 +134,16 @@ struct DevKeys {
 // ---- HLL launchers (rsk_hll.hip)
 // Adds keys into slabs and max-merges them into sketch `id`; sets *d_flag
 // (device u32) to 1 if any register grew.
-void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint32_t* d_flag);
+void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64_t* d_card, uint32_t* d_flag,
+                    uint32_t epoch, bool created);
 void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G);
-void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids, uint64_t n,
-                      uint64_t* d_out);
+// Up to 8 sketch ids passed by value (saves a host->device copy per PFCOUNT).
+struct SmallIds {
+  uint64_t v[8];
+  uint32_t n;
+};
+void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
+                      const SmallIds& small, uint64_t n, uint64_t* d_out);
 void hll_union_count_launch(rsk_ctx* c, const uint8_t* const* d_member_ptrs, uint32_t arity, uint64_t n,
                             uint64_t* d_out);
 void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* const* d_src_ptrs, uint32_t srcs_per_dst,
