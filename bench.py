@@ -75,10 +75,11 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
     ki = ins.keys_fixed(n_ins, 16).as_struct()
     kq = qs.keys_fixed(n_q, 16).as_struct()
     add_t, con_t = [], []
-    engine.prof_reset()
-    engine.prof_enable(True)
     hits = 0
     for r in range(reps + 1):
+        if r == 1:  # rep 0 is warm-up (first-call scratch allocation); kernel times from rep 1
+            engine.prof_reset()
+            engine.prof_enable(True)
         b = ctypes.c_void_p()
         _lib.check(L.rsk_bloom_create(engine.ctx, size.value, k.value, ctypes.byref(b)))
         engine.sync()
@@ -98,6 +99,11 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
     engine.prof_enable(False)
     add_ms, add_n = engine.prof_read("bloom_add16")
     con_ms, con_n = engine.prof_read("bloom_contains16")
+    stages = {}
+    for name in ("bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply"):
+        ms, cnt = engine.prof_read(name)
+        if cnt:
+            stages[name] = ms / max(1, add_n)  # per insert batch (summed over its chunks)
     add_s, con_s = min(add_t), min(con_t)
     for buf in (ins, qs, out):
         buf.free()
@@ -106,6 +112,7 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
             "insert_keys_per_s": n_ins / add_s, "contains_keys_per_s": n_q / con_s,
             "insert_ms": add_s * 1e3, "contains_ms": con_s * 1e3, "contains_true": hits,
             "insert_kernel_avg_ms": add_ms / max(1, add_n), "contains_kernel_avg_ms": con_ms / max(1, con_n),
+            "insert_stage_ms": stages,
             "insert_bit_rmw_per_s": n_ins * k.value / add_s,
             "contains_probe_gathers_per_s": n_q * (k.value - 1) / con_s}
 

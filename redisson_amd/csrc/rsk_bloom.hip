@@ -17,23 +17,12 @@
 
 namespace rsk {
 
-RSK_DEV uint32_t bit_mask(uint64_t idx) { return 1u << ((uint32_t)((idx >> 3) & 3) * 8 + 7 - (uint32_t)(idx & 7)); }
-constexpr uint64_t JAVA_LONG_MAX = 0x7FFFFFFFFFFFFFFFULL;
+RSK_DEV uint32_t bit_mask(uint64_t idx) { return bloom_bit_mask(idx); }
 
 template <bool FIXED16>
 RSK_DEV void key_hashes(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len,
                         uint64_t i, uint64_t& h1, uint64_t& h2) {
-  if (FIXED16) {
-    uint4 v = ld_nt16(reinterpret_cast<const uint4*>(data) + i);
-    uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
-    h1 = xxh64_16(w0, w1);
-    h2 = farm_16(w0, w1);
-  } else {
-    uint64_t s = offsets ? offsets[i] : i * fixed_len;
-    uint64_t len = offsets ? offsets[i + 1] - s : fixed_len;
-    h1 = xxh64(data + s, len);
-    h2 = farm_uo64(data + s, len);
-  }
+  bloom_key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
 }
 
 template <bool FIXED16>
@@ -169,11 +158,13 @@ void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
   if (k.n == 0) return;
   if (fixed16(k)) {
     ProfScope ps(c, "bloom_add16");
+    if (bloom_add_partitioned(c, b, k)) return;  // large batches: LDS slices (rsk_bloom_part.hip)
     hipLaunchKernelGGL(bloom_add_kernel<true>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, nullptr, 16u,
                        k.n, b->d_bits, b->fm, b->k);
     RSK_CHECK_LAUNCH("bloom_add16");
   } else {
     ProfScope ps(c, "bloom_add");
+    if (bloom_add_partitioned(c, b, k)) return;
     hipLaunchKernelGGL(bloom_add_kernel<false>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, k.offsets,
                        k.fixed_len, k.n, b->d_bits, b->fm, b->k);
     RSK_CHECK_LAUNCH("bloom_add");

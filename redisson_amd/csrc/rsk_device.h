@@ -385,6 +385,34 @@ RSK_DEV uint64_t fastmod63(uint64_t x, const FastMod63& f) {
   return x - q * f.d;
 }
 
+// ------------------------------------------------------ Bloom probe indices
+// RedissonBloomFilter.hash (:116-131): h1 = xx_r39(bytes), h2 = farmUo(bytes),
+// idx_t = (h_t & Long.MAX_VALUE) % size with h_0 = h1, h_{t+1} = h_t + (t even ? h2 : h1).
+constexpr uint64_t JAVA_LONG_MAX = 0x7FFFFFFFFFFFFFFFULL;
+
+template <bool FIXED16>
+RSK_DEV void bloom_key_hashes(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+                              uint32_t fixed_len, uint64_t i, uint64_t& h1, uint64_t& h2) {
+  if (FIXED16) {
+    uint4 v = ld_nt16(reinterpret_cast<const uint4*>(data) + i);
+    uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
+    h1 = xxh64_16(w0, w1);
+    h2 = farm_16(w0, w1);
+  } else {
+    uint64_t s = offsets ? offsets[i] : i * fixed_len;
+    uint64_t len = offsets ? offsets[i + 1] - s : fixed_len;
+    h1 = xxh64(data + s, len);
+    h2 = farm_uo64(data + s, len);
+  }
+}
+
+// Bit i of the Redis string (byte i>>3, mask 0x80>>(i&7); bitops.c) inside
+// its little-endian u32 word i>>5.  Any base that is a multiple of 32 bits
+// keeps the mask, so slice-local indices use it too.
+RSK_DEV uint32_t bloom_bit_mask(uint64_t idx) {
+  return 1u << ((uint32_t)((idx >> 3) & 3) * 8 + 7 - (uint32_t)(idx & 7));
+}
+
 // ------------------------------------------------------- synthetic streams
 RSK_DEV uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ULL;

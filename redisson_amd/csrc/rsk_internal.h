@@ -154,6 +154,9 @@ void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n);
 
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
+// Slice-partitioned add (rsk_bloom_part.hip); false when the direct kernel is used
+// (small batch, k > 4096, filter > 2^34 bits, or RSK_BLOOM_PARTITION=0).
+bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);

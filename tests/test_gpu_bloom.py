@@ -129,6 +129,62 @@ def test_c3_stream_device_resident(L, engine, orc):
     assert L.rsk_bloom_bitcount(b, ctypes.byref(bc)) == 0 and bc.value == orc.bitcount(ref_bits)
 
 
+@pytest.mark.parametrize("size,k,n", [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 33, 20000),
+                                      (19170117, 7, 300000), (157298745, 7, 400000), (157298745, 3, 700000)])
+def test_partitioned_add_parity(L, engine, orc, monkeypatch, size, k, n):
+    """Slice-partitioned add (forced on) gives the oracle's bit string: one partition
+    level (<= 256 slices of 2^19 bits) and two levels (157M bits = 301 slices)."""
+    from redisson_amd import KeyBatch
+
+    monkeypatch.setenv("RSK_BLOOM_PARTITION", "1")
+    keys = orc.gen_keys16(0x5EED0003, 0, n)
+    b = _filter(L, engine, size, k)
+    _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)), replies=False)
+    ref = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(ref, size, k, keys, None, 16, n, want=False)
+    assert np.array_equal(_bits(L, b, size), ref)
+    # variable-length keys (blob + offsets) and duplicates through the same path
+    rng = np.random.default_rng(k)
+    vk = [rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes() for _ in range(4000)]
+    vk += vk[:1000] + [b""]
+    _add(L, b, KeyBatch.from_bytes_list(vk), replies=False)
+    blob, offs = orc.pack_keys(vk)
+    orc.bloom_add_batch(ref, size, k, blob, offs, want=False)
+    assert np.array_equal(_bits(L, b, size), ref)
+
+
+def test_partitioned_add_matches_direct_c3_size(L, engine, monkeypatch):
+    """At the C3 filter size (9,585,058,377 bits, 18,283 slices, two levels) the
+    partitioned add and the direct atomicOr kernel set identical bits."""
+    from redisson_amd import _lib, devmem
+
+    size, k, n = 9585058377, 7, 3_000_000
+    ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
+    ks = ins.keys_fixed(n, 16).as_struct()
+    filters = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RSK_BLOOM_PARTITION", mode)
+        f = _filter(L, engine, size, k)
+        _lib.check(L.rsk_bloom_add(f, ctypes.byref(ks), None))
+        filters[mode] = f
+    engine.sync()
+    counts = {}
+    for mode, f in filters.items():
+        bc = ctypes.c_uint64()
+        _lib.check(L.rsk_bloom_bitcount(f, ctypes.byref(bc)))
+        counts[mode] = bc.value
+    assert counts["1"] == counts["0"] > 0.99 * n * k
+    # partitioned |= direct leaves the count unchanged  =>  the bit strings are equal
+    nbytes = (size + 7) // 8
+    _lib.check(L.rsk_bloom_or_bits(filters["1"], L.rsk_bloom_device_bits(filters["0"]), nbytes, _lib.RSK_MEM_DEVICE))
+    bc = ctypes.c_uint64()
+    _lib.check(L.rsk_bloom_bitcount(filters["1"], ctypes.byref(bc)))
+    assert bc.value == counts["0"]
+    for f in filters.values():
+        L.rsk_bloom_destroy(f)
+    ins.free()
+
+
 def test_or_bits_merge(L, engine, orc):
     from redisson_amd import KeyBatch, _lib
 
