@@ -10,20 +10,28 @@
 // Bit setting is an OR, so the order of the probes does not matter.  For
 // batches of millions of keys the probes are instead partitioned by the
 // 64 KiB slice (2^19 bits) of the filter they land in, and each slice is
-// then updated in LDS with ds_or_b32 and written back once:
+// then updated in LDS with ds_or_b32 and written back once.  Every output
+// position is computed up front (no global atomics, deterministic layout):
 //
-//   hist   : hash the keys, count probes per slice (LDS histogram, <= 32768 slices)
-//   scan   : exclusive sum -> slice_start[]; cursors; part2 tile map
-//   part1  : hash again, counting-sort each 4096-probe tile in LDS by coarse
-//            bucket (<= 256), write the tile as contiguous runs (u32 payload:
-//            index inside the coarse bucket)
-//   part2  : (filters > 256 slices) the same by slice inside each coarse bucket
+//   hist   : G blocks, block b hashes its contiguous key range and writes
+//            cnt[s][b] = its probes in slice s (LDS histogram, <= 32768 slices)
+//   scan   : off2 = exclusive sum of cnt in slice-major order, so slice s's
+//            probes occupy [off2[s][0], off2[s+1][0]) and block b's share of
+//            them starts at off2[s][b]
+//   coarse : (filters > 256 slices) coarse bucket c = 2^f2 consecutive slices;
+//            off1[c][b] = where block b's coarse-c probes go in the part1 buffer
+//   part1  : block b hashes its keys again, counting-sorts each 4096-probe
+//            tile in LDS by coarse bucket and appends each bucket's run at its
+//            LDS cursor (initialised from off1 / off2)
+//   part2  : (two levels) unit (c, b) = block b's coarse-c run, re-sorted by
+//            slice and appended at off2[s][b]
 //   apply  : one workgroup per slice: load the 64 KiB slice into LDS, ds_or
 //            every probe, store the slice back
 //
 // HBM traffic per key (16-byte keys, k probes): 16 (hist) + 16 + 4k (part1)
 // + 8k (part2) + 4k (apply) bytes, plus 2 x the filter per chunk -- all
-// streaming, against k random memory-side atomics for the direct kernel.
+// streaming or run-coalesced, against k random memory-side atomics for the
+// direct kernel.
 #include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
@@ -37,8 +45,12 @@ constexpr uint32_t SLICE_WORDS = 1u << (SLICE_LOG - 5);  // 16384 u32 = 64 KiB o
 constexpr uint32_t MAX_SLICES = 32768;                   // filters up to 2^34 bits (2 GiB)
 constexpr int PT = 256;                                  // partition workgroup
 constexpr uint32_t TILE = 4096;                          // probes per partition tile
+constexpr int KT = 4;                                    // keys per lane per part1 tile
+constexpr int ET = TILE / PT;                            // elements per lane per part2 tile
 constexpr int HIST_T = 1024;
+constexpr int HIST_U = 4;  // 16-byte keys in flight per lane in hist
 constexpr int APPLY_T = 1024;
+constexpr int APPLY_U = 4;
 constexpr uint64_t PROBE_CAP = 1ull << 31;  // probes per chunk (u32 positions)
 
 // Exclusive scan of one value per lane over a 256-lane workgroup.
@@ -64,176 +76,309 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tot
   return pre + x - v;
 }
 
-// Per-slice probe counts for the whole batch.
+RSK_DEV void key_range(uint64_t n, uint64_t per, uint64_t* begin, uint64_t* end) {
+  *begin = (uint64_t)blockIdx.x * per;
+  if (*begin > n) *begin = n;
+  *end = *begin + per < n ? *begin + per : n;
+}
+
+template <typename F>
+RSK_DEV void for_probes(uint64_t h1, uint64_t h2, int k, const FastMod63& fm, F&& f) {
+  uint64_t x = h1;
+  for (int t = 0; t < k; ++t) {
+    f(t, fastmod63(x & JAVA_LONG_MAX, fm));
+    x += (t & 1) ? h1 : h2;
+  }
+}
+
+// hist: cnt[s * G + b] = probes of block b's keys that land in slice s.
 template <bool FIXED16>
 __global__ __launch_bounds__(HIST_T) void bloom_slice_hist_kernel(const uint8_t* __restrict__ data,
                                                                   const uint64_t* __restrict__ offsets,
-                                                                  uint32_t fixed_len, uint64_t n, FastMod63 fm, int k,
-                                                                  uint32_t nslices, uint32_t* __restrict__ hist) {
+                                                                  uint32_t fixed_len, uint64_t n, uint64_t per,
+                                                                  FastMod63 fm, int k, uint32_t nslices,
+                                                                  uint32_t* __restrict__ cnt) {
   __shared__ uint32_t h[MAX_SLICES];
   for (uint32_t s = threadIdx.x; s < nslices; s += HIST_T) h[s] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * HIST_T + threadIdx.x; i < n; i += (uint64_t)gridDim.x * HIST_T) {
-    uint64_t h1, h2;
-    bloom_key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
-    uint64_t x = h1;
-    for (int t = 0; t < k; ++t) {
-      const uint64_t idx = fastmod63(x & JAVA_LONG_MAX, fm);
-      atomicAdd(&h[(uint32_t)(idx >> SLICE_LOG)], 1u);
-      x += (t & 1) ? h1 : h2;
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  auto count = [&](int, uint64_t idx) { atomicAdd(&h[(uint32_t)(idx >> SLICE_LOG)], 1u); };
+  if (FIXED16) {
+    const uint4* keys = reinterpret_cast<const uint4*>(data);
+    for (uint64_t i = begin + threadIdx.x; i < end; i += (uint64_t)HIST_T * HIST_U) {
+      uint4 v[HIST_U];
+#pragma unroll
+      for (int u = 0; u < HIST_U; ++u) {
+        const uint64_t j = i + (uint64_t)u * HIST_T;
+        v[u] = j < end ? ld_nt16(keys + j) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < HIST_U; ++u) {
+        if (i + (uint64_t)u * HIST_T >= end) break;
+        const uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x, w1 = ((uint64_t)v[u].w << 32) | v[u].z;
+        for_probes(xxh64_16(w0, w1), farm_16(w0, w1), k, fm, count);
+      }
+    }
+  } else {
+    for (uint64_t i = begin + threadIdx.x; i < end; i += HIST_T) {
+      uint64_t h1, h2;
+      bloom_key_hashes<false>(data, offsets, fixed_len, i, h1, h2);
+      for_probes(h1, h2, k, fm, count);
     }
   }
   __syncthreads();
-  for (uint32_t s = threadIdx.x; s < nslices; s += HIST_T)
-    if (h[s]) atomicAdd(&hist[s], h[s]);
+  for (uint32_t s = threadIdx.x; s < nslices; s += HIST_T) cnt[(uint64_t)s * gridDim.x + blockIdx.x] = h[s];
 }
 
-// Cursors and the part2 tile map from slice_start[0..nslices] (one block).
-// Coarse bucket c covers slices [c << f2, (c+1) << f2).
-__global__ __launch_bounds__(PT) void bloom_part_init_kernel(const uint32_t* __restrict__ slice_start,
-                                                             uint32_t nslices, uint32_t f2, uint32_t nbins1,
-                                                             uint32_t* __restrict__ cursor1,
-                                                             uint32_t* __restrict__ cursor2,
-                                                             uint32_t* __restrict__ tiles_before) {
-  for (uint32_t s = threadIdx.x; s < nslices; s += PT) cursor2[s] = slice_start[s];
-  const uint32_t c = threadIdx.x;
-  uint32_t tiles = 0;
-  if (c < nbins1) {
-    const uint32_t lo = slice_start[c << f2];
-    const uint32_t hi = slice_start[min((c + 1) << f2, nslices)];
-    cursor1[c] = lo;
-    tiles = (hi - lo + TILE - 1) / TILE;
-  }
+// coarse: off1[c * G + b] for coarse bucket c = slices [c << f2, (c+1) << f2).
+// Bucket c's region of the part1 buffer starts where slice c << f2 starts
+// (off2[(c << f2) * G]) and holds block 0's run, block 1's run, ...
+__global__ __launch_bounds__(PT) void bloom_coarse_offsets_kernel(const uint32_t* __restrict__ cnt,
+                                                                  const uint32_t* __restrict__ off2, uint32_t G,
+                                                                  uint32_t f2, uint32_t nslices,
+                                                                  uint32_t* __restrict__ off1) {
+  const uint32_t c = blockIdx.x;
+  const uint32_t s0 = c << f2, s1 = min((c + 1) << f2, nslices);
+  const uint32_t per = (G + PT - 1) / PT;  // consecutive blocks per lane
+  const uint32_t b0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b0 + per && b < G; ++b)
+    for (uint32_t s = s0; s < s1; ++s) sum += cnt[(uint64_t)s * G + b];
   uint32_t total;
-  const uint32_t before = block_excl_scan256(tiles, &total);
-  if (c <= nbins1) tiles_before[c] = c < nbins1 ? before : total;
-  if (c == PT - 1 && nbins1 == PT) tiles_before[PT] = total;
+  uint32_t run = off2[(uint64_t)s0 * G] + block_excl_scan256(sum, &total);
+  for (uint32_t b = b0; b < b0 + per && b < G; ++b) {
+    off1[(uint64_t)c * G + b] = run;
+    for (uint32_t s = s0; s < s1; ++s) run += cnt[(uint64_t)s * G + b];
+  }
+  if (c == gridDim.x - 1 && threadIdx.x == 0) off1[(uint64_t)gridDim.x * G] = off2[(uint64_t)nslices * G];
 }
 
-// Scatter one LDS tile: probe p has payload pay[p] and tag[p] = bin << 16 |
-// rank inside its bin; the tile is counting-sorted by bin in LDS and each
-// bin's run is written contiguously at a slot claimed from cursor[bin].
-struct TileLds {
-  uint32_t hist[PT], lstart[PT], gbase[PT];
-  uint32_t pay[TILE], tag[TILE], srt[TILE];
+// LDS image of one partition tile: probe p has payload pay[p] and tag[p] =
+// bin << 16 | rank inside its bin; the tile is counting-sorted by bin into
+// srt/sbin and each bin's run is appended at cur[bin] (dlt[bin] = cur[bin] -
+// lstart[bin] maps a sorted position to its output position).
+struct SortLds {
+  uint32_t hist[PT], lstart[PT], cur[PT], dlt[PT];
+  uint32_t srt[TILE];
   uint8_t sbin[TILE];
 };
+struct TileLds : SortLds {  // + probes staged in LDS (part1: k probes per key, k is runtime)
+  uint32_t pay[TILE], tag[TILE];
+};
 
-__device__ __forceinline__ void tile_scatter(TileLds& L, uint32_t np, uint32_t* __restrict__ cursor,
-                                             uint32_t* __restrict__ out) {
+// After the ranking atomics: bin starts inside the tile.  Returns this lane's bin count.
+__device__ __forceinline__ uint32_t tile_bins(SortLds& L) {
   __syncthreads();
   const uint32_t cnt = L.hist[threadIdx.x];
   uint32_t total;
-  L.lstart[threadIdx.x] = block_excl_scan256(cnt, &total);
-  if (cnt) L.gbase[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt);
+  const uint32_t ls = block_excl_scan256(cnt, &total);
+  L.lstart[threadIdx.x] = ls;
+  L.dlt[threadIdx.x] = L.cur[threadIdx.x] - ls;
   __syncthreads();
-  for (uint32_t p = threadIdx.x; p < np; p += PT) {
-    const uint32_t tg = L.tag[p], b = tg >> 16;
-    const uint32_t pos = L.lstart[b] + (tg & 0xFFFFu);
-    L.srt[pos] = L.pay[p];
-    L.sbin[pos] = (uint8_t)b;
-  }
+  return cnt;
+}
+
+__device__ __forceinline__ void tile_place(SortLds& L, uint32_t tg, uint32_t pay) {
+  const uint32_t b = tg >> 16;
+  const uint32_t pos = L.lstart[b] + (tg & 0xFFFFu);
+  L.srt[pos] = pay;
+  L.sbin[pos] = (uint8_t)b;
+}
+
+// Sorted tile -> runs in global memory; advances the cursors.
+__device__ __forceinline__ void tile_write(SortLds& L, uint32_t np, uint32_t cnt, uint32_t* __restrict__ out) {
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < np; j += PT) {
-    const uint32_t b = L.sbin[j];
-    out[L.gbase[b] + (j - L.lstart[b])] = L.srt[j];
-  }
+  for (uint32_t j = threadIdx.x; j < np; j += PT) out[L.dlt[L.sbin[j]] + j] = L.srt[j];
   __syncthreads();
+  L.cur[threadIdx.x] += cnt;
   L.hist[threadIdx.x] = 0;
 }
 
-// part1: keys -> probes, partitioned by coarse bucket idx >> shift1 (< 256).
+__device__ __forceinline__ void tile_scatter(TileLds& L, uint32_t np, uint32_t* __restrict__ out) {
+  const uint32_t cnt = tile_bins(L);
+  for (uint32_t p = threadIdx.x; p < np; p += PT) tile_place(L, L.tag[p], L.pay[p]);
+  tile_write(L, np, cnt, out);
+}
+
+// part1: block b's keys -> probes, partitioned by bin = idx >> shift1 (< 256);
+// bin's run of block b starts at start[bin * G + b].
 template <bool FIXED16>
 __global__ __launch_bounds__(PT) void bloom_part1_kernel(const uint8_t* __restrict__ data,
                                                          const uint64_t* __restrict__ offsets, uint32_t fixed_len,
-                                                         uint64_t n, FastMod63 fm, int k, uint32_t shift1,
-                                                         uint32_t* __restrict__ cursor1, uint32_t* __restrict__ out) {
+                                                         uint64_t n, uint64_t per, FastMod63 fm, int k,
+                                                         uint32_t shift1, uint32_t nbins,
+                                                         const uint32_t* __restrict__ start,
+                                                         uint32_t* __restrict__ out) {
   __shared__ TileLds L;
-  const uint32_t kpt = TILE / (uint32_t)k;
-  const uint64_t ntiles = (n + kpt - 1) / kpt;
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  const uint32_t kpt = min((uint32_t)(PT * KT), TILE / (uint32_t)k);  // keys per tile
   const uint64_t low = (1ull << shift1) - 1;
   L.hist[threadIdx.x] = 0;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t k0 = tile * kpt;
-    const uint32_t nk = (uint32_t)(n - k0 < kpt ? n - k0 : kpt);
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < nk; q += PT) {
-      uint64_t h1, h2;
-      bloom_key_hashes<FIXED16>(data, offsets, fixed_len, k0 + q, h1, h2);
-      uint64_t x = h1;
-      for (int t = 0; t < k; ++t) {
-        const uint64_t idx = fastmod63(x & JAVA_LONG_MAX, fm);
-        const uint32_t b = (uint32_t)(idx >> shift1);
-        const uint32_t r = atomicAdd(&L.hist[b], 1u);
-        const uint32_t p = q * (uint32_t)k + (uint32_t)t;
-        L.pay[p] = (uint32_t)(idx & low);
-        L.tag[p] = (b << 16) | r;
-        x += (t & 1) ? h1 : h2;
+  if (threadIdx.x < nbins) L.cur[threadIdx.x] = start[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  auto hash_tile_key = [&](uint32_t q, uint64_t h1, uint64_t h2) {
+    for_probes(h1, h2, k, fm, [&](int t, uint64_t idx) {
+      const uint32_t b = (uint32_t)(idx >> shift1);
+      const uint32_t r = atomicAdd(&L.hist[b], 1u);
+      const uint32_t p = q * (uint32_t)k + (uint32_t)t;
+      L.pay[p] = (uint32_t)(idx & low);
+      L.tag[p] = (b << 16) | r;
+    });
+  };
+  if (FIXED16) {
+    const uint4* keys = reinterpret_cast<const uint4*>(data);
+    uint4 nxt[KT];
+    auto fetch = [&](uint64_t k0) {
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        const uint32_t q = threadIdx.x + u * PT;
+        nxt[u] = (q < kpt && k0 + q < end) ? ld_nt16(keys + k0 + q) : make_uint4(0, 0, 0, 0);
       }
+    };
+    fetch(begin);
+    for (uint64_t k0 = begin; k0 < end; k0 += kpt) {
+      const uint32_t nk = (uint32_t)(end - k0 < kpt ? end - k0 : kpt);
+      uint4 cur[KT];
+#pragma unroll
+      for (int u = 0; u < KT; ++u) cur[u] = nxt[u];
+      fetch(k0 + kpt);  // next tile's keys stream in while this one is sorted
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        const uint32_t q = threadIdx.x + u * PT;
+        if (q < nk) {
+          const uint64_t w0 = ((uint64_t)cur[u].y << 32) | cur[u].x, w1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+          hash_tile_key(q, xxh64_16(w0, w1), farm_16(w0, w1));
+        }
+      }
+      tile_scatter(L, nk * (uint32_t)k, out);
     }
-    tile_scatter(L, nk * (uint32_t)k, cursor1, out);
+  } else {
+    for (uint64_t k0 = begin; k0 < end; k0 += kpt) {
+      const uint32_t nk = (uint32_t)(end - k0 < kpt ? end - k0 : kpt);
+      __syncthreads();
+      for (uint32_t q = threadIdx.x; q < nk; q += PT) {
+        uint64_t h1, h2;
+        bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
+        hash_tile_key(q, h1, h2);
+      }
+      tile_scatter(L, nk * (uint32_t)k, out);
+    }
   }
 }
 
-// part2: each coarse bucket's probes, partitioned by slice (< 2^f2 per bucket).
-// Tiles never straddle a coarse bucket: tile t belongs to the bucket c with
-// tiles_before[c] <= t < tiles_before[c+1].
+// part2: units u = c * G + b in order (= the part1 buffer in order); unit u
+// is [off1[u], off1[u+1]).  Workgroup w takes the units whose start falls in
+// its equal share of the buffer, re-sorts each unit by slice (2^f2 bins) and
+// appends slice s's run at off2[s * G + b].
 __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restrict__ in,
-                                                         const uint32_t* __restrict__ slice_start,
-                                                         const uint32_t* __restrict__ tiles_before, uint32_t nbins1,
-                                                         uint32_t f2, uint32_t nslices,
-                                                         uint32_t* __restrict__ cursor2, uint32_t* __restrict__ out) {
-  __shared__ TileLds L;
-  __shared__ uint32_t tb[PT + 1];
-  for (uint32_t c = threadIdx.x; c <= nbins1; c += PT) tb[c] = tiles_before[c];
+                                                         const uint32_t* __restrict__ off1,
+                                                         const uint32_t* __restrict__ off2, uint32_t G,
+                                                         uint32_t nunits, uint32_t f2, uint32_t nslices,
+                                                         uint32_t* __restrict__ out) {
+  __shared__ SortLds L;
+  __shared__ uint32_t range[2];
+  const uint32_t total = off1[nunits];
+  if (threadIdx.x < 2) {  // first unit starting at or after a share boundary
+    const uint64_t edge = (uint64_t)total * (blockIdx.x + threadIdx.x) / gridDim.x;
+    uint32_t lo = 0, hi = nunits;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off1[mid] < edge) lo = mid + 1;
+      else hi = mid;
+    }
+    range[threadIdx.x] = (blockIdx.x + threadIdx.x == gridDim.x) ? nunits : lo;
+  }
   L.hist[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t total_tiles = tb[nbins1];
+  const uint32_t u_end = range[1];
   const uint32_t low = (1u << SLICE_LOG) - 1;
-  for (uint32_t tile = blockIdx.x; tile < total_tiles; tile += gridDim.x) {
-    uint32_t lo_c = 0, hi_c = nbins1;  // largest c with tb[c] <= tile
-    while (hi_c - lo_c > 1) {
-      const uint32_t mid = (lo_c + hi_c) >> 1;
-      if (tb[mid] <= tile) lo_c = mid;
-      else hi_c = mid;
+  const uint32_t nb = 1u << f2;
+  // tile cursor: unit u, element j (absolute); the next tile is prefetched
+  uint32_t u = range[0];
+  uint32_t j = u < u_end ? off1[u] : 0;
+  auto skip_empty = [&]() {
+    while (u < u_end && j >= off1[u + 1]) {
+      ++u;
+      if (u < u_end) j = off1[u];
     }
-    const uint32_t c = lo_c;
-    const uint32_t end = slice_start[min((c + 1) << f2, nslices)];
-    const uint32_t j0 = slice_start[c << f2] + (tile - tb[c]) * TILE;
-    const uint32_t np = end - j0 < TILE ? end - j0 : TILE;
+  };
+  skip_empty();
+  uint32_t nxt[ET];
+  auto fetch = [&](uint32_t fu, uint32_t fj) {
+    const uint32_t lim = fu < u_end ? off1[fu + 1] : 0;
+#pragma unroll
+    for (int e = 0; e < ET; ++e) {
+      const uint32_t p = fj + threadIdx.x + e * PT;
+      nxt[e] = (fu < u_end && p < lim && p < fj + TILE) ? __builtin_nontemporal_load(&in[p]) : 0;
+    }
+  };
+  fetch(u, j);
+  uint32_t loaded_unit = 0xFFFFFFFFu;
+  while (u < u_end) {
+    const uint32_t ue = off1[u + 1];
+    const uint32_t np = ue - j < TILE ? ue - j : TILE;
+    uint32_t vals[ET];
+#pragma unroll
+    for (int e = 0; e < ET; ++e) vals[e] = nxt[e];
+    const uint32_t cu = u;
+    // advance to the next tile and prefetch it
+    j += np;
+    skip_empty();
+    fetch(u, j);
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < np; p += PT) {
-      const uint32_t v = __builtin_nontemporal_load(&in[j0 + p]);
-      const uint32_t b = v >> SLICE_LOG;
-      const uint32_t r = atomicAdd(&L.hist[b], 1u);
-      L.pay[p] = v & low;
-      L.tag[p] = (b << 16) | r;
+    if (cu != loaded_unit) {  // new unit: its slice cursors
+      const uint32_t c = cu / G, b = cu - c * G;
+      const uint32_t s = (c << f2) + threadIdx.x;
+      if (threadIdx.x < nb && s < nslices) L.cur[threadIdx.x] = off2[(uint64_t)s * G + b];
+      loaded_unit = cu;
     }
-    tile_scatter(L, np, cursor2 + ((uint64_t)c << f2), out);
+    uint32_t tag[ET];  // payload and rank stay in registers
+#pragma unroll
+    for (int e = 0; e < ET; ++e) {
+      const uint32_t p = threadIdx.x + e * PT;
+      if (p < np) {
+        const uint32_t bin = vals[e] >> SLICE_LOG;
+        tag[e] = (bin << 16) | atomicAdd(&L.hist[bin], 1u);
+      }
+    }
+    const uint32_t cnt = tile_bins(L);
+#pragma unroll
+    for (int e = 0; e < ET; ++e)
+      if (threadIdx.x + e * PT < np) tile_place(L, tag[e], vals[e] & low);
+    tile_write(L, np, cnt, out);
   }
 }
 
-// apply: slice s = bits words [s*16384, (s+1)*16384) updated in LDS.
+// apply: slice s = bits words [s*16384, (s+1)*16384), probes [off2[s*G], off2[(s+1)*G]).
 __global__ __launch_bounds__(APPLY_T) void bloom_slice_apply_kernel(const uint32_t* __restrict__ probes,
-                                                                    const uint32_t* __restrict__ slice_start,
+                                                                    const uint32_t* __restrict__ off2, uint32_t G,
                                                                     uint32_t nslices, uint32_t* __restrict__ bits,
                                                                     uint64_t nwords) {
   __shared__ __attribute__((aligned(16))) uint32_t sl[SLICE_WORDS];
   for (uint32_t s = blockIdx.x; s < nslices; s += gridDim.x) {
-    const uint32_t a = slice_start[s], e = slice_start[s + 1];
+    const uint32_t a = off2[(uint64_t)s * G], e = off2[(uint64_t)(s + 1) * G];
     if (a == e) continue;  // uniform across the workgroup
     const uint64_t w0 = (uint64_t)s * SLICE_WORDS;
     const uint32_t nw4 = (uint32_t)((nwords - w0 < SLICE_WORDS ? nwords - w0 : SLICE_WORDS) / 4);
     uint4* g4 = reinterpret_cast<uint4*>(bits + w0);
     uint4* l4 = reinterpret_cast<uint4*>(sl);
-    for (uint32_t j = threadIdx.x; j < nw4; j += APPLY_T) l4[j] = g4[j];
+    for (uint32_t q = threadIdx.x; q < nw4; q += APPLY_T) l4[q] = g4[q];
     __syncthreads();
-    for (uint32_t j = a + threadIdx.x; j < e; j += APPLY_T) {
-      const uint32_t v = __builtin_nontemporal_load(&probes[j]);
-      atomicOr(&sl[v >> 5], bloom_bit_mask(v));
+    for (uint32_t q = a + threadIdx.x; q < e; q += APPLY_T * APPLY_U) {
+      uint32_t v[APPLY_U];
+#pragma unroll
+      for (int t = 0; t < APPLY_U; ++t) {
+        const uint32_t i = q + t * APPLY_T;
+        v[t] = i < e ? __builtin_nontemporal_load(&probes[i]) : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int t = 0; t < APPLY_U; ++t)
+        if (v[t] != 0xFFFFFFFFu) atomicOr(&sl[v[t] >> 5], bloom_bit_mask(v[t]));
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < nw4; j += APPLY_T) g4[j] = l4[j];
+    for (uint32_t q = threadIdx.x; q < nw4; q += APPLY_T) g4[q] = l4[q];
     __syncthreads();
   }
 }
@@ -242,6 +387,11 @@ static int part_mode() {
   const char* e = std::getenv("RSK_BLOOM_PARTITION");  // unset: auto; "0": never; "1": always
   if (!e || !*e) return -1;
   return e[0] == '0' ? 0 : 1;
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt) {  // tuning knobs (scripts/bloom_part_tune.py)
+  const char* e = std::getenv(name);
+  return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
 }
 
 static uint32_t bits_for(uint64_t v) {  // bits needed to hold v (0 -> 0)
@@ -266,69 +416,72 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t shift1 = SLICE_LOG + f2;
   const uint32_t nbins1 = (uint32_t)(((nslices - 1) >> f2) + 1);
   const uint32_t ns = (uint32_t)nslices;
+  const uint32_t cus = (uint32_t)c->num_cus;
+  const uint32_t G = std::max<uint32_t>(1, env_u32("RSK_BLOOM_G_PER_CU", 2)) * cus;  // hist / part1 blocks
+  const uint32_t p2_grid = std::max<uint32_t>(1, env_u32("RSK_BLOOM_P2_PER_CU", 4)) * cus;
 
   const uint64_t chunk = std::max<uint64_t>(1, PROBE_CAP / k);
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk) * k;
+  const uint64_t ncnt = (uint64_t)ns * G + 1;
+  const uint64_t noff1 = (uint64_t)nbins1 * G + 1;
   size_t scan_bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(ns + 1),
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt,
                                          c->stream);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  const uint64_t meta = 2 * al(4ull * (ns + 1)) + al(4 * PT) + al(4ull * ns) + al(4 * (PT + 1)) + al(scan_bytes);
+  const uint64_t meta = 2 * al(4 * ncnt) + al(4 * noff1) + al(scan_bytes);
   uint8_t* w = c->work(meta + (f2 ? 2 : 1) * al(4 * max_np));
-  uint32_t* hist = reinterpret_cast<uint32_t*>(w);
-  uint32_t* slice_start = reinterpret_cast<uint32_t*>(w + al(4ull * (ns + 1)));
-  uint32_t* cursor1 = reinterpret_cast<uint32_t*>(w + 2 * al(4ull * (ns + 1)));
-  uint32_t* cursor2 = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(cursor1) + al(4 * PT));
-  uint32_t* tiles_before = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(cursor2) + al(4ull * ns));
-  void* scan_tmp = reinterpret_cast<uint8_t*>(tiles_before) + al(4 * (PT + 1));
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(w);
+  uint32_t* off2 = reinterpret_cast<uint32_t*>(w + al(4 * ncnt));
+  uint32_t* off1 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt));
+  void* scan_tmp = w + 2 * al(4 * ncnt) + al(4 * noff1);
   uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta);
   uint32_t* buf_b = f2 ? reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np)) : buf_a;
 
-  const uint32_t cus = (uint32_t)c->num_cus;
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
+    const uint64_t per = (m + G - 1) / G;
     DevKeys dk = keys;
     dk.n = m;
     if (keys.offsets) dk.offsets = keys.offsets + first;
     else dk.data = keys.data + first * keys.fixed_len;
     {
       ProfScope ps(c, "bloom_part_hist");
-      RSK_HIP(hipMemsetAsync(hist, 0, 4ull * (ns + 1), c->stream));
-      const uint32_t g = (uint32_t)std::min<uint64_t>(cus, (m + HIST_T - 1) / HIST_T);
+      RSK_HIP(hipMemsetAsync(cnt + ncnt - 1, 0, 4, c->stream));
       if (f16)
-        hipLaunchKernelGGL(bloom_slice_hist_kernel<true>, dim3(g), dim3(HIST_T), 0, c->stream, dk.data, nullptr, 16u,
-                           m, b->fm, b->k, ns, hist);
+        hipLaunchKernelGGL(bloom_slice_hist_kernel<true>, dim3(G), dim3(HIST_T), 0, c->stream, dk.data, nullptr, 16u,
+                           m, per, b->fm, b->k, ns, cnt);
       else
-        hipLaunchKernelGGL(bloom_slice_hist_kernel<false>, dim3(g), dim3(HIST_T), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, ns, hist);
+        hipLaunchKernelGGL(bloom_slice_hist_kernel<false>, dim3(G), dim3(HIST_T), 0, c->stream, dk.data, dk.offsets,
+                           dk.fixed_len, m, per, b->fm, b->k, ns, cnt);
       RSK_CHECK_LAUNCH("bloom_slice_hist");
-      RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, hist, slice_start, (int)(ns + 1), c->stream));
-      hipLaunchKernelGGL(bloom_part_init_kernel, dim3(1), dim3(PT), 0, c->stream, slice_start, ns, f2, nbins1, cursor1,
-                         cursor2, tiles_before);
-      RSK_CHECK_LAUNCH("bloom_part_init");
+      RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, cnt, off2, (int)ncnt, c->stream));
+      if (f2) {
+        hipLaunchKernelGGL(bloom_coarse_offsets_kernel, dim3(nbins1), dim3(PT), 0, c->stream, cnt, off2, G, f2, ns,
+                           off1);
+        RSK_CHECK_LAUNCH("bloom_coarse_offsets");
+      }
     }
     {
       ProfScope ps(c, "bloom_part1");
-      const uint64_t kpt = TILE / k;
-      const uint32_t g = (uint32_t)std::min<uint64_t>(4ull * cus, (m + kpt - 1) / kpt);
+      const uint32_t* start = f2 ? off1 : off2;
       if (f16)
-        hipLaunchKernelGGL(bloom_part1_kernel<true>, dim3(g), dim3(PT), 0, c->stream, dk.data, nullptr, 16u, m, b->fm,
-                           b->k, shift1, cursor1, buf_a);
+        hipLaunchKernelGGL(bloom_part1_kernel<true>, dim3(G), dim3(PT), 0, c->stream, dk.data, nullptr, 16u, m, per,
+                           b->fm, b->k, shift1, nbins1, start, buf_a);
       else
-        hipLaunchKernelGGL(bloom_part1_kernel<false>, dim3(g), dim3(PT), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, shift1, cursor1, buf_a);
+        hipLaunchKernelGGL(bloom_part1_kernel<false>, dim3(G), dim3(PT), 0, c->stream, dk.data, dk.offsets,
+                           dk.fixed_len, m, per, b->fm, b->k, shift1, nbins1, start, buf_a);
       RSK_CHECK_LAUNCH("bloom_part1");
     }
     if (f2) {
       ProfScope ps(c, "bloom_part2");
-      hipLaunchKernelGGL(bloom_part2_kernel, dim3(4 * cus), dim3(PT), 0, c->stream, buf_a, slice_start, tiles_before,
-                         nbins1, f2, ns, cursor2, buf_b);
+      hipLaunchKernelGGL(bloom_part2_kernel, dim3(p2_grid), dim3(PT), 0, c->stream, buf_a, off1, off2, G,
+                         nbins1 * G, f2, ns, buf_b);
       RSK_CHECK_LAUNCH("bloom_part2");
     }
     {
       ProfScope ps(c, "bloom_slice_apply");
       hipLaunchKernelGGL(bloom_slice_apply_kernel, dim3(std::min<uint32_t>(ns, 2 * cus)), dim3(APPLY_T), 0, c->stream,
-                         buf_b, slice_start, ns, b->d_bits, b->nwords);
+                         buf_b, off2, G, ns, b->d_bits, b->nwords);
       RSK_CHECK_LAUNCH("bloom_slice_apply");
     }
   }
