@@ -44,9 +44,11 @@ def pmc_traffic(kernel: str, keys_per_launch: int):
     return best
 
 
-def cpu_baseline(sample_keys: int, passes: int):
-    """The oracle's restatement of Redis PFADD (hllPatLen + register max), one
-    core, over a pre-generated in-memory sample of the same C2 stream."""
+def cpu_baseline(sample_keys: int, passes: int, threads: int):
+    """The oracle's restatement of Redis PFADD (hllPatLen + register max) over
+    a pre-generated in-memory sample of the same C2 stream: one core (the
+    Redis-equivalent, Redis being single-threaded) as `value`, and all of the
+    host cores this job may use (OpenMP, private registers + max-merge)."""
     import numpy as np
 
     from oracle import oracle as O
@@ -57,9 +59,37 @@ def cpu_baseline(sample_keys: int, passes: int):
     for _ in range(passes):
         O.hll_add(regs, keys, None, 16, sample_keys)
     dt = time.perf_counter() - t0
+    mt = np.zeros(O.REGISTERS, np.uint8)
+    t1 = time.perf_counter()
+    for _ in range(passes):
+        O.hll_add_fixed_mt(mt, keys, 16, sample_keys, threads)
+    dt_mt = time.perf_counter() - t1
+    assert np.array_equal(mt, regs)
     return {"value": sample_keys * passes / dt, "unit": "keys/s", "cores": 1, "kind": "port",
             "sample": "%d passes over %d C2 16-byte keys (%.1f s, oracle/rsk_oracle.c orc_hll_add_raw, "
-                      "Redis 3.2.0 PFADD arithmetic, 1 thread)" % (passes, sample_keys, dt)}
+                      "Redis 3.2.0 PFADD arithmetic, 1 thread)" % (passes, sample_keys, dt),
+            "all_cores": {"value": sample_keys * passes / dt_mt, "unit": "keys/s", "cores": threads,
+                          "sample": "same sample, orc_hll_add_fixed_mt, %d OpenMP threads (%.1f s)"
+                                    % (threads, dt_mt)}}
+
+
+def random_access_peaks(engine, nbytes: int, reps: int = 3):
+    """Live random-access denominators over a buffer the size of the filter:
+    4-byte gathers and 4-byte atomicOr at uniformly random words (rsk_diag_membench)."""
+    from redisson_amd import _lib, devmem
+
+    L = _lib.load()
+    buf = devmem.DeviceBuffer(engine, nbytes)
+    buf.zero()
+    ops = 1 << 30
+    best = {}
+    for name, mode in (("gather4B", 1), ("atomicor4B", 2)):
+        for _ in range(reps):
+            ms = ctypes.c_double()
+            _lib.check(L.rsk_diag_membench(engine.ctx, mode, buf.ptr, nbytes, ops, ctypes.byref(ms)))
+            best[name] = max(best.get(name, 0.0), ops / (ms.value / 1e3))
+    buf.free()
+    return best
 
 
 def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
@@ -95,6 +125,13 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
             con_t.append(t2 - t1)
         if r == reps:
             hits = int(out.to_numpy().sum())
+            # untimed: the gathers the contains kernel issues for these queries
+            pr = ctypes.c_uint64()
+            _lib.check(L.rsk_diag_bloom_contains_probes(engine.ctx, b, qs.ptr, n_q, out.ptr, ctypes.byref(pr)))
+            probes = pr.value
+            bc = ctypes.c_uint64()
+            _lib.check(L.rsk_bloom_bitcount(b, ctypes.byref(bc)))
+            fill = bc.value / size.value
         L.rsk_bloom_destroy(b)
     engine.prof_enable(False)
     add_ms, add_n = engine.prof_read("bloom_add16")
@@ -107,14 +144,30 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
     add_s, con_s = min(add_t), min(con_t)
     for buf in (ins, qs, out):
         buf.free()
+    peaks = random_access_peaks(engine, (size.value + 7) // 8)
+    gathers_per_s = probes / con_s
+    sets_per_s = n_ins * k.value / add_s
     return {"config": "C3: %d inserts @1%% FPP (size %d bits, k=%d, EXTENDED), %d contains (50%% inserted)"
                       % (n_ins, size.value, k.value, n_q),
             "insert_keys_per_s": n_ins / add_s, "contains_keys_per_s": n_q / con_s,
             "insert_ms": add_s * 1e3, "contains_ms": con_s * 1e3, "contains_true": hits,
             "insert_kernel_avg_ms": add_ms / max(1, add_n), "contains_kernel_avg_ms": con_ms / max(1, con_n),
             "insert_stage_ms": stages,
-            "insert_bit_rmw_per_s": n_ins * k.value / add_s,
-            "contains_probe_gathers_per_s": n_q * (k.value - 1) / con_s}
+            "insert_bit_rmw_per_s": sets_per_s,
+            "contains_probe_gathers_per_s": gathers_per_s,
+            "random_access_roofline": {
+                "filter_fill": fill,
+                "contains": {"bound": "random 4 B gather", "gathers_issued": probes,
+                             "gathers_per_key": probes / n_q, "achieved": gathers_per_s,
+                             "peak": peaks["gather4B"], "unit": "gathers/s",
+                             "frac": gathers_per_s / peaks["gather4B"],
+                             "hbm_GBps_at_64B_per_gather": gathers_per_s * 64 / 1e9},
+                "insert": {"bound": "random 4 B atomicOr (direct kernel)", "achieved": sets_per_s,
+                           "peak": peaks["atomicor4B"], "unit": "bit-sets/s",
+                           "ratio": sets_per_s / peaks["atomicor4B"],
+                           "note": "slice-partitioned: probes sorted into 64 KiB LDS-resident filter slices, "
+                                   "so the insert is not bound by memory-side atomics"},
+                "peaks_measured_on": "a zeroed buffer of the filter's size, 2^30 uniformly random ops, best of 3"}}
 
 
 def main():
@@ -132,6 +185,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=128 << 20)
     ap.add_argument("--cpu-passes", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU figure (the GPU box's CPU share is 16)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -277,7 +331,8 @@ def main():
         bn = args.bloom_keys
         result["bloom"] = bloom_bench(engine, bn, bn, reps=2)
     if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes)
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes,
+                                              max(1, min(args.cpu_threads, os.cpu_count() or 1)))
     else:
         result["cpu_baseline"] = None
     if rank == 0:

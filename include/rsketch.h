@@ -250,6 +250,10 @@ int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint
 /* Time one launch of a tuning variant of the 16-byte Bloom contains kernel. */
 int rsk_diag_bloom_contains_variant(rsk_ctx *ctx, int variant, rsk_bloom *b, const void *dev_keys16, uint64_t n,
                                     uint8_t *dev_out, double *ms);
+/* Run the production 16-byte contains kernel's gather sequence with a tally:
+ * replies into dev_out, *probes = bit gathers issued (early exit included). */
+int rsk_diag_bloom_contains_probes(rsk_ctx *ctx, rsk_bloom *b, const void *dev_keys16, uint64_t n, uint8_t *dev_out,
+                                   uint64_t *probes);
 
 /* ----------------------------------------------- synthetic input streams */
 /* SURVEY 8d generators, run on the device into caller-provided device

@@ -104,6 +104,34 @@ uint64_t orc_hll_add_raw(uint8_t *regs, const uint8_t *data, const uint64_t *off
     return grown;
 }
 
+/* The same over fixed-length keys on nthreads host cores: OpenMP, private
+ * registers per thread, max-merged at the end (SURVEY 8d's "all host cores"
+ * CPU figure; registers equal orc_hll_add_raw's because max commutes). */
+void orc_hll_add_fixed_mt(uint8_t *regs, const uint8_t *data, uint32_t fixed_len, uint64_t n, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 1) {
+        uint8_t *priv = (uint8_t *)calloc((size_t)nthreads, ORC_HLL_REGISTERS);
+#pragma omp parallel num_threads(nthreads)
+        {
+            uint8_t *mine = priv + (size_t)omp_get_thread_num() * ORC_HLL_REGISTERS;
+#pragma omp for schedule(static)
+            for (uint64_t i = 0; i < n; i++) {
+                long idx;
+                int c = orc_hll_patlen(data + i * (uint64_t)fixed_len, fixed_len, &idx);
+                if (c > mine[idx]) mine[idx] = (uint8_t)c;
+            }
+        }
+        for (int t = 0; t < nthreads; t++)
+            for (int j = 0; j < ORC_HLL_REGISTERS; j++)
+                if (priv[(size_t)t * ORC_HLL_REGISTERS + j] > regs[j]) regs[j] = priv[(size_t)t * ORC_HLL_REGISTERS + j];
+        free(priv);
+        return;
+    }
+#endif
+    (void)nthreads;
+    orc_hll_add_raw(regs, data, NULL, fixed_len, n);
+}
+
 /* ===================================================================== */
 /* Synthetic inputs.  splitmix64 output for state x.          */
 /* ===================================================================== */

@@ -44,6 +44,8 @@ int orc_hll_patlen(const uint8_t *ele, size_t len, long *regp);
  * number of registers that grew. */
 uint64_t orc_hll_add_raw(uint8_t *regs, const uint8_t *data, const uint64_t *offsets,
                          uint32_t fixed_len, uint64_t n);
+/* Fixed-length keys on nthreads cores (OpenMP, private registers, max-merge). */
+void orc_hll_add_fixed_mt(uint8_t *regs, const uint8_t *data, uint32_t fixed_len, uint64_t n, int nthreads);
 /* Same, but the keys are the synthetic 16-byte stream of SURVEY 8d (C2),
  * generated on the fly; nthreads > 1 uses OpenMP with private registers. */
 void orc_hll_add_gen16(uint8_t *regs, uint64_t seed, uint64_t start, uint64_t n, int nthreads);

@@ -674,21 +674,36 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
     // a pair runs after the last writer of its source (RAW) and of its
     // destination (WAW), and after the last reader of its destination (WAR).
     // Pairs of one level are independent and run as one launch.
-    std::unordered_map<uint64_t, uint32_t> last_w, last_r;
+    // Per-sketch last writer / last reader levels live in flat per-pool
+    // arrays, reset lazily by an epoch stamp (no hashing, no clearing).
+    if (h->lv_stamp.size() != h->n) {
+      h->lv_stamp.assign(h->n, 0);
+      h->lv_w.assign(h->n, 0);
+      h->lv_r.assign(h->n, 0);
+      h->lv_epoch = 0;
+    }
+    if (++h->lv_epoch == 0) {
+      std::fill(h->lv_stamp.begin(), h->lv_stamp.end(), 0);
+      h->lv_epoch = 1;
+    }
+    const uint32_t ep = h->lv_epoch;
+    auto touch = [&](uint64_t id) {
+      if (h->lv_stamp[id] != ep) {
+        h->lv_stamp[id] = ep;
+        h->lv_w[id] = 0;
+        h->lv_r[id] = 0;
+      }
+    };
     std::vector<uint32_t> level(n);
     uint32_t max_level = 0;
     for (uint64_t i = 0; i < n; ++i) {
-      uint32_t lv = 0;
-      auto it = last_w.find(src_ids[i]);
-      if (it != last_w.end()) lv = std::max(lv, it->second);
-      it = last_w.find(dst_ids[i]);
-      if (it != last_w.end()) lv = std::max(lv, it->second);
-      it = last_r.find(dst_ids[i]);
-      if (it != last_r.end()) lv = std::max(lv, it->second);
-      level[i] = ++lv;
-      last_w[dst_ids[i]] = lv;
-      uint32_t& r = last_r[src_ids[i]];
-      r = std::max(r, lv);
+      const uint64_t s = src_ids[i], d = dst_ids[i];
+      touch(s);
+      touch(d);
+      const uint32_t lv = std::max(std::max(h->lv_w[s], h->lv_w[d]), h->lv_r[d]) + 1;
+      level[i] = lv;
+      h->lv_w[d] = lv;
+      h->lv_r[s] = std::max(h->lv_r[s], lv);
       max_level = std::max(max_level, lv);
     }
     std::vector<uint64_t> start(max_level + 2, 0);

@@ -5,6 +5,8 @@
 //   mode 2: random 4 B atomicOr over the buffer           -> atomics/s
 //   mode 3: streaming copy (read + write halves)          -> GB/s (read+write)
 // Indices come from splitmix64(i), as uniform as the Bloom probe stream.
+#include <cstring>
+
 #include "rsk_internal.h"
 
 namespace rsk {
@@ -134,6 +136,28 @@ extern "C" int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes
     *ms = f;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
+    rsk::set_error("");
+    return RSK_OK;
+  } catch (const rsk::RskError& e) {
+    rsk::set_error(e.msg);
+    return e.code;
+  }
+}
+
+extern "C" int rsk_diag_bloom_contains_probes(rsk_ctx* c, rsk_bloom* bf, const void* dev_keys16, uint64_t n,
+                                              uint8_t* dev_out, uint64_t* probes) {
+  try {
+    if (!c || !bf || !dev_keys16 || !dev_out || !probes || n == 0)
+      throw rsk::RskError{RSK_ERR_INVALID_ARG, "bad arguments"};
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RSK_HIP(hipSetDevice(c->device));
+    auto* d = reinterpret_cast<unsigned long long*>(c->d_small + 384);
+    RSK_HIP(hipMemsetAsync(d, 0, 8, c->stream));
+    rsk::bloom_contains_probe_count_launch(
+        c, bf, rsk::DevKeys{reinterpret_cast<const uint8_t*>(dev_keys16), nullptr, n, 16}, dev_out, d);
+    RSK_HIP(hipMemcpyAsync(c->h_small + 384, d, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(probes, c->h_small + 384, 8);
     rsk::set_error("");
     return RSK_OK;
   } catch (const rsk::RskError& e) {

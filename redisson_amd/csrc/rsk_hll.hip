@@ -239,66 +239,148 @@ static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per
 }
 
 // Blob + offsets, LDS-staged (the C4 path).  A workgroup takes tiles of T
-// consecutive keys; their bytes are one contiguous blob range, loaded with
-// coalesced 16-byte loads into LDS, and each lane then hashes its key from
-// LDS with aligned 8-byte reads + funnel shifts.  A tile whose bytes exceed
-// the stage (keys longer than STAGE/T on average) is hashed from global.
+// consecutive keys; their bytes are one contiguous blob range, copied into
+// LDS with coalesced 16-byte loads that are issued one tile ahead (register
+// prefetch; the tile's end offset is itself loaded a tile earlier, so the
+// stage loads never wait on an offset load).  MurmurHash64A is a serial
+// chain of ceil(len/8) steps, so a wave runs as long as its longest key: the
+// tile's keys are counting-sorted by step count in LDS (wave-aggregated LDS
+// atomics) and lane j hashes the j-th key of that order, which makes every
+// wave nearly uniform in length.  A tile whose bytes exceed the stage is
+// hashed from global memory, unsorted.
 constexpr int VAR_T = 512;
-constexpr int VAR_STAGE = 32768;  // bytes per tile (64 B per key)
+constexpr int VAR_STAGE = 32768;                // bytes per tile (64 B per key)
+constexpr int VAR_PF = VAR_STAGE / 16 / VAR_T;  // 16-byte chunks per lane
+constexpr uint32_t VAR_MAXCLS = 16;             // step classes 0..16 (16 = that long or longer)
+constexpr uint32_t VAR_NONE = VAR_MAXCLS + 1;   // lane past the end of the tile
+constexpr int VAR_NCLS = VAR_MAXCLS + 2;
 
-RSK_DEV uint64_t lds_word(const uint64_t* st, uint32_t q, uint32_t sh) {
-  // 8 bytes starting at byte 8*q + sh (sh < 8) of the stage
-  const uint64_t lo = st[q];
-  return sh ? (lo >> (8 * sh)) | (st[q + 1] << (64 - 8 * sh)) : lo;
-}
-
+// MurmurHash64A of `len` bytes at byte `off` of the stage: one 8-byte LDS
+// read per step, the unaligned word assembled by a funnel shift.
 RSK_DEV uint64_t murmur64a_lds(const uint64_t* st, uint32_t off, uint32_t len) {
-  const uint32_t q = off >> 3, sh = off & 7;
+  const uint32_t q = off >> 3, sh = (off & 7) * 8;
   const uint32_t nb = len >> 3, t = len & 7;
   uint64_t h = (uint64_t)HLL_SEED ^ ((uint64_t)len * MM_M);
+  uint64_t lo = st[q];
   for (uint32_t j = 0; j < nb; ++j) {
-    h ^= mm_mix(lds_word(st, q + j, sh));
+    const uint64_t hi = st[q + j + 1];
+    h ^= mm_mix(sh ? (lo >> sh) | (hi << (64 - sh)) : lo);
     h *= MM_M;
+    lo = hi;
   }
   if (t) {
     // the tail's bytes start at off + 8*nb; bytes past the key are masked
-    h ^= lds_word(st, q + nb, sh) & ((1ULL << (8 * t)) - 1);
+    const uint64_t hi = st[q + nb + 1];
+    h ^= (sh ? (lo >> sh) | (hi << (64 - sh)) : lo) & ((1ULL << (8 * t)) - 1);
     h *= MM_M;
   }
   return mm_final(h);
 }
 
-__global__ __launch_bounds__(VAR_T) void hll_add_var_staged_kernel(const uint8_t* __restrict__ data,
-                                                                   const uint64_t* __restrict__ offsets, uint64_t n,
-                                                                   uint64_t per_block, uint8_t* __restrict__ slabs) {
+// 3 workgroups per CU (LDS ~50 KiB each) = 6 waves per SIMD.
+__global__ __launch_bounds__(VAR_T, 6) void hll_add_var_staged_kernel(const uint8_t* __restrict__ data,
+                                                                      const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                      uint64_t per_block, uint8_t* __restrict__ slabs) {
   __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
   __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
+  __shared__ uint32_t perm[VAR_T];  // sorted keys: stage offset | len << 16
+  __shared__ uint32_t cnt[VAR_NCLS], cbase[VAR_NCLS];
+  const uint32_t tid = threadIdx.x;
   lds8_zero(regs32);
+  if (tid < VAR_NCLS) cnt[tid] = 0;
   const uint64_t begin = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  for (uint64_t base = begin; base < end; base += VAR_T) {
-    const uint64_t last = base + VAR_T < end ? base + VAR_T : end;
-    const uint64_t i = base + threadIdx.x;
-    const bool mine = i < last;
-    const uint64_t s = mine ? offsets[i] : 0;
-    const uint64_t e = mine ? offsets[i + 1] : 0;
-    const uint64_t lo = offsets[base], hi = offsets[last];
-    const uint64_t a0 = lo & ~uint64_t(15);
-    const bool staged = hi - a0 <= VAR_STAGE;
-    __syncthreads();  // previous tile's stage reads are done
+  const uintptr_t dbase = reinterpret_cast<uintptr_t>(data);
+
+  // Tile state, one tile ahead.  The stage window starts at the 16-byte-
+  // aligned ADDRESS at or below the tile's first byte, so no chunk load
+  // crosses into a page the blob does not touch.
+  uint64_t last = 0, s = 0, e = 0, hi_ahead = 0;
+  uintptr_t a0 = 0;
+  uint32_t nchunk = 0;
+  bool staged = false, mine = false;
+  uint4 pf[VAR_PF];
+  // Tile [b, last) with byte range [lo, hi): stage loads issue at once.
+  auto fetch = [&](uint64_t b, uint64_t lo, uint64_t hi) {
+    last = b + VAR_T < end ? b + VAR_T : end;
+    a0 = (dbase + lo) & ~uintptr_t(15);
+    const uint64_t span = dbase + hi - a0;
+    staged = span <= (uint64_t)VAR_STAGE;
+    nchunk = staged ? (uint32_t)((span + 15) >> 4) : 0;
+#pragma unroll
+    for (int u = 0; u < VAR_PF; ++u) {
+      const uint32_t c = tid + (uint32_t)u * VAR_T;
+      if (c < nchunk) pf[u] = ld_nt16(reinterpret_cast<const uint4*>(a0) + c);
+    }
+    const uint64_t i = b + tid;
+    mine = i < last;
+    s = mine ? offsets[i] : 0;
+    e = mine ? offsets[i + 1] : 0;
+    hi_ahead = offsets[last + VAR_T < end ? last + VAR_T : end];  // the following tile's end
+  };
+  uint64_t cur_hi = 0;
+  if (begin < end) {
+    cur_hi = offsets[begin + VAR_T < end ? begin + VAR_T : end];
+    fetch(begin, offsets[begin], cur_hi);
+  }
+
+  for (uint64_t base = begin; base < end;) {
+    __syncthreads();  // [A] previous tile's stage / perm / cbase reads are done
+    uint4* st16 = reinterpret_cast<uint4*>(stage);
+#pragma unroll
+    for (int u = 0; u < VAR_PF; ++u) {
+      const uint32_t c = tid + (uint32_t)u * VAR_T;
+      if (c < nchunk) st16[c] = pf[u];
+    }
+    const uint64_t len64 = e - s;
+    const uint64_t steps = (len64 + 7) >> 3;
+    const uint32_t cls = !mine ? VAR_NONE : (steps < VAR_MAXCLS ? (uint32_t)steps : VAR_MAXCLS);
+    uint32_t my_off = 0;
     if (staged) {
-      const uint32_t nchunk = (uint32_t)((hi - a0 + 15) >> 4);
-      const uint4* src = reinterpret_cast<const uint4*>(data + a0);
-      uint4* dst = reinterpret_cast<uint4*>(stage);
-      for (uint32_t c = threadIdx.x; c < nchunk; c += VAR_T) dst[c] = ld_nt16(src + c);
+      // Wave-aggregated count: one LDS atomic per (wave, class present).
+      uint64_t rem = __ballot(cls != VAR_NONE);
+      while (rem) {
+        const int leader = __builtin_ctzll(rem);
+        const uint32_t c = (uint32_t)__shfl((int)cls, leader);
+        const uint64_t m = __ballot(cls == c);
+        uint32_t old = 0;
+        if ((int)__lane_id() == leader) old = atomicAdd(&cnt[c], (uint32_t)__popcll(m));
+        old = (uint32_t)__shfl((int)old, leader);
+        if (cls == c)
+          my_off = old + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        rem &= ~m;
+      }
     }
-    __syncthreads();
-    if (mine) {
-      const uint32_t len = (uint32_t)(e - s);
-      const uint64_t h = staged ? murmur64a_lds(stage, (uint32_t)(s - a0), len)
-                                : (len <= 64 ? murmur64a_le64(data + s, len) : murmur64a(data + s, len));
-      hll_update8(regs32, h);
+    // Keep this tile's key, then issue the next tile's loads (they land
+    // while this tile hashes).
+    const bool cur_staged = staged, cur_mine = mine;
+    const uint64_t cur_s = s;
+    const uint32_t cur_off = (uint32_t)(dbase + s - a0);
+    const uint64_t next = last;
+    if (next < end) {
+      const uint64_t lo_n = cur_hi;
+      cur_hi = hi_ahead;
+      fetch(next, lo_n, cur_hi);
     }
+    __syncthreads();  // [B] stage written, counts final
+    if (cur_staged) {
+      if (tid < VAR_NCLS) {
+        uint32_t acc = 0;
+        for (uint32_t c = 0; c < tid; ++c) acc += cnt[c];
+        cbase[tid] = acc;
+      }
+      __syncthreads();  // [C]
+      if (cls != VAR_NONE) perm[cbase[cls] + my_off] = cur_off | ((uint32_t)len64 << 16);
+      __syncthreads();  // [D]
+      if (tid < VAR_NCLS) cnt[tid] = 0;
+      if (tid < cbase[VAR_NONE]) {
+        const uint32_t p = perm[tid];
+        hll_update8(regs32, murmur64a_lds(stage, p & 0xFFFFu, p >> 16));
+      }
+    } else if (cur_mine) {
+      hll_update8(regs32, len64 <= 64 ? murmur64a_le64(data + cur_s, (uint32_t)len64) : murmur64a(data + cur_s, len64));
+    }
+    base = next;
   }
   __syncthreads();
   lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
@@ -498,66 +580,56 @@ RSK_DEV uint64_t hll_estimate(double E, int ez, const double* __restrict__ lc) {
 }
 
 // Redis sums 2^-reg in an encoding-specific order.  All orders agree when
-// every partial sum is exact, i.e. when the span from the smallest term
-// 2^-rmax to the top bit of the total fits 53 bits; the kernel checks this
-// on the exact fixed-point total and only otherwise replays Redis's order
-// (dense: groups of 16; raw: u64 words) serially.  Sparse keys always take
-// the exact path (registers <= 32).
-struct SumParts {
-  uint64_t inz;  // sum over nonzero registers of 2^(50-r)
-  uint32_t ez;
-  uint32_t rmax;
+// every partial sum is exact: the terms are multiples of 2^-rmax, so every
+// partial sum below 2^(53-rmax) is an exact double.  The kernels therefore
+// sum in any order in FP64, each term built directly as the bits of 2^-r,
+// and compare the total with that bound.  Rounding is monotone and the
+// bound is representable, so the computed total reaches it iff the exact
+// total does; only then is Redis's order replayed serially (dense: groups
+// of 16; raw: u64 words).  Sparse keys always pass (registers <= 32).
+struct SumD {
+  double t;       // sum over all registers of 2^-r (a zero register adds 1)
+  uint32_t ez;    // zero registers
+  uint32_t rmax;  // largest register
 };
 
-RSK_DEV void acc_word(SumParts& s, uint32_t w) {
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    uint32_t r = (w >> (8 * b)) & 0xFF;
-    if (r == 0) s.ez++;
-    else s.inz += 1ULL << (50 - r);
-    s.rmax = r > s.rmax ? r : s.rmax;
-  }
+RSK_DEV void acc_word(SumD& s, uint32_t w) {
+  // bit 7 of a byte of z is set exactly where that byte of w is zero
+  const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+  s.ez += __popc(z);
+  const uint32_t r0 = w & 0xFFu, r1 = (w >> 8) & 0xFFu, r2 = (w >> 16) & 0xFFu, r3 = w >> 24;
+  const uint32_t m01 = r0 > r1 ? r0 : r1, m23 = r2 > r3 ? r2 : r3;
+  const uint32_t m = m01 > m23 ? m01 : m23;
+  s.rmax = m > s.rmax ? m : s.rmax;
+  s.t += (pe(r0) + pe(r1)) + (pe(r2) + pe(r3));
 }
 
-// Block reduction of SumParts over 256 lanes.
-__device__ __forceinline__ SumParts block_reduce(SumParts s) {
-  __shared__ uint64_t sh_inz[4];
-  __shared__ uint32_t sh_ez[4], sh_rmax[4];
+RSK_DEV SumD wave_reduce(SumD s) {
   for (int off = 32; off > 0; off >>= 1) {
-    s.inz += __shfl_down(s.inz, off, 64);
+    s.t += __shfl_down(s.t, off, 64);
     s.ez += __shfl_down(s.ez, off, 64);
-    uint32_t o = __shfl_down(s.rmax, off, 64);
+    const uint32_t o = __shfl_down(s.rmax, off, 64);
     s.rmax = o > s.rmax ? o : s.rmax;
   }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) {
-    sh_inz[wv] = s.inz;
-    sh_ez[wv] = s.ez;
-    sh_rmax[wv] = s.rmax;
-  }
-  __syncthreads();
-  SumParts r{0, 0, 0};
-  if (threadIdx.x == 0) {
-    for (int q = 0; q < 4; ++q) {
-      r.inz += sh_inz[q];
-      r.ez += sh_ez[q];
-      r.rmax = sh_rmax[q] > r.rmax ? sh_rmax[q] : r.rmax;
-    }
-  }
-  return r;
+  return s;
 }
 
-// Exact E when every summation order is exact; returns false otherwise.
-RSK_DEV bool exact_sum(const SumParts& s, double* E) {
-  // V = ez*2^50 + inz, in units of 2^-50; up to 2^64 -> two limbs.
-  uint64_t lo = ((uint64_t)s.ez << 50) + s.inz;
-  uint64_t hi = ((uint64_t)s.ez >> 14) + (lo < s.inz ? 1 : 0);
-  int bl = hi ? 64 + (64 - __builtin_clzll(hi)) : (64 - __builtin_clzll(lo));
-  int low_unit = 50 - (int)s.rmax;  // smallest term is 2^(50-rmax) units
-  if (s.rmax == 0) low_unit = 50;
-  if (bl - low_unit > 53) return false;
-  *E = (double)lo * 0x1p-50 + (double)hi * 0x1p14;
-  return true;
+// Every summation order gives s.t exactly (see above).
+RSK_DEV bool exact_total(const SumD& s) {
+  return s.t < __longlong_as_double((long long)((uint64_t)(1023 + 53 - s.rmax) << 52));  // 2^(53-rmax)
+}
+
+// One sketch's 16 KiB as 16 uint4 per lane of a wave.
+RSK_DEV SumD wave_sum(const uint4 (&v)[16]) {
+  SumD s{0.0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    acc_word(s, v[q].x);
+    acc_word(s, v[q].y);
+    acc_word(s, v[q].z);
+    acc_word(s, v[q].w);
+  }
+  return wave_reduce(s);
 }
 
 RSK_DEV double dense_order_sum(const uint8_t* r, int* ezp) {
@@ -573,44 +645,41 @@ RSK_DEV double dense_order_sum(const uint8_t* r, int* ezp) {
   return E;
 }
 
+// PFCOUNT, one wave per sketch: the 16 KiB are 16 uint4 loads per lane, all
+// in flight at once; no LDS and no barrier.
 __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
                                                         const uint64_t* __restrict__ ids, SmallIds small, uint64_t n,
                                                         const double* __restrict__ lc, uint64_t* __restrict__ out) {
-  for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; b < n; b += nwaves) {
     const uint64_t id = ids ? ids[b] : (small.n ? small.v[b] : b);
     const uint64_t cached = card[id];
     if ((cached >> 63) == 0) {  // HLL_VALID_CACHE
-      if (threadIdx.x == 0) out[b] = cached;
+      if (lane == 0) out[b] = cached;
       continue;
     }
     const uint8_t* r = regs + id * HLL_REGS;
-    SumParts s{0, 0, 0};
-    const uint4* r4 = reinterpret_cast<const uint4*>(r);
+    const uint4* r4 = reinterpret_cast<const uint4*>(r) + lane;
+    uint4 v[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint4 v = r4[threadIdx.x + 256 * q];
-      acc_word(s, v.x);
-      acc_word(s, v.y);
-      acc_word(s, v.z);
-      acc_word(s, v.w);
-    }
-    s = block_reduce(s);
-    if (threadIdx.x == 0) {
-      double E;
+    for (int q = 0; q < 16; ++q) v[q] = r4[64 * q];
+    const SumD s = wave_sum(v);
+    if (lane == 0) {
       int ez = (int)s.ez;
-      if (!exact_sum(s, &E)) E = dense_order_sum(r, &ez);
-      uint64_t v = hll_estimate(E, ez, lc);
-      out[b] = v;
-      card[id] = v;  // cache refreshed, valid
+      const double E = exact_total(s) ? s.t : dense_order_sum(r, &ez);
+      const uint64_t est = hll_estimate(E, ez, lc);
+      out[b] = est;
+      card[id] = est;  // cache refreshed, valid
     }
-    __syncthreads();
   }
 }
 
 void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
                       const SmallIds& small, uint64_t n, uint64_t* d_out) {
   if (n == 0) return;
-  uint64_t grid = n < (1u << 20) ? n : (1u << 20);
+  uint64_t grid = (n + 3) / 4;  // 4 waves (sketches) per workgroup
+  if (grid > (1u << 20)) grid = 1u << 20;
   ProfScope ps(c, "hll_count");
   hipLaunchKernelGGL(hll_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_regs, d_card, d_ids, small, n,
                      c->d_lc, d_out);
@@ -651,26 +720,24 @@ __global__ __launch_bounds__(256) void hll_union_count_kernel(const uint8_t* con
                                                               uint32_t arity, uint64_t n,
                                                               const double* __restrict__ lc,
                                                               uint64_t* __restrict__ out) {
-  for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; b < n; b += nwaves) {  // one wave per union
     const uint8_t* const* mem = member_ptrs + b * arity;
-    SumParts s{0, 0, 0};
+    uint4 v[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      for (uint32_t a = 0; a < arity; ++a) {
-        if (mem[a] == nullptr) continue;
-        v = bmax16(v, reinterpret_cast<const uint4*>(mem[a])[threadIdx.x + 256 * q]);
-      }
-      acc_word(s, v.x);
-      acc_word(s, v.y);
-      acc_word(s, v.z);
-      acc_word(s, v.w);
+    for (int q = 0; q < 16; ++q) v[q] = make_uint4(0, 0, 0, 0);
+    for (uint32_t a = 0; a < arity; ++a) {
+      if (mem[a] == nullptr) continue;
+      const uint4* p = reinterpret_cast<const uint4*>(mem[a]) + lane;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = bmax16(v[q], p[64 * q]);
     }
-    s = block_reduce(s);
-    if (threadIdx.x == 0) {
-      double E;
+    const SumD s = wave_sum(v);
+    if (lane == 0) {
       int ez = (int)s.ez;
-      if (!exact_sum(s, &E)) {
+      double E = s.t;
+      if (!exact_total(s)) {
         // Absent members contribute zeros: compact the pointer list.
         const uint8_t* live[64];
         uint32_t na = 0;
@@ -680,14 +747,14 @@ __global__ __launch_bounds__(256) void hll_union_count_kernel(const uint8_t* con
       }
       out[b] = hll_estimate(E, ez, lc);
     }
-    __syncthreads();
   }
 }
 
 void hll_union_count_launch(rsk_ctx* c, const uint8_t* const* d_member_ptrs, uint32_t arity, uint64_t n,
                             uint64_t* d_out) {
   if (n == 0) return;
-  uint64_t grid = n < (1u << 20) ? n : (1u << 20);
+  uint64_t grid = (n + 3) / 4;  // 4 waves (unions) per workgroup
+  if (grid > (1u << 20)) grid = 1u << 20;
   ProfScope ps(c, "hll_union_count");
   hipLaunchKernelGGL(hll_union_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_member_ptrs, arity, n,
                      c->d_lc, d_out);

@@ -97,6 +97,9 @@ struct rsk_hll {
   uint8_t* d_regs = nullptr;   // [n][16384] raw registers (one byte each)
   uint64_t* d_card = nullptr;  // [n] Redis card[8] as LE u64 (bit 63 = cache invalid)
   std::vector<uint8_t> exists; // host: key present
+  // rsk_hll_merge_batch leveling state per sketch id (valid while stamp == lv_epoch)
+  std::vector<uint32_t> lv_stamp, lv_w, lv_r;
+  uint32_t lv_epoch = 0;
 };
 
 struct rsk_bloom {
@@ -160,6 +163,8 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);
+void bloom_contains_probe_count_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out,
+                                       unsigned long long* d_probes);
 void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out);
 void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes);
 // dst[0..S) = OR over rows of src[rows][S] (u32 words).

@@ -14,7 +14,8 @@ sys.path.insert(0, ROOT)
 from redisson_amd import _lib, devmem  # noqa: E402
 
 NAMES = {0: "all_k-1_parallel", 1: "early_exit_U1_32wg", 2: "early_exit_U2_32wg", 3: "early_exit_U4_32wg",
-         4: "early_exit_U1_8wg", 5: "early_exit_U2_8wg"}
+         4: "early_exit_U1_8wg", 5: "early_exit_U2_8wg", 6: "phased_U2_P2", 7: "phased_U2_P3",
+         8: "phased_U1_P3", 9: "phased_U1_P6", 10: "phased_U4_P2", 11: "phased_U1_P2"}
 
 
 def main():

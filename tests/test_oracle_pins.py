@@ -160,3 +160,14 @@ def test_golden_fixtures_reproduce(orc):
     orc.hll_add_gen16(regs, 0x5EED0002, 0, 20000)
     assert regs.tobytes().hex() == g["hll"]["c2_20000"]["registers_hex"]
     assert orc.hll_count_dense(regs) == g["hll"]["c2_20000"]["count_dense"]
+
+
+def test_multithreaded_cpu_baseline_matches_sequential(orc):
+    # bench.py's all-cores CPU figure must compute the same registers as the 1-core port
+    keys = orc.gen_keys16(0x5EED0002, 0, 200_000)
+    seq = np.zeros(orc.REGISTERS, np.uint8)
+    orc.hll_add(seq, keys, None, 16, 200_000)
+    for threads in (1, 3, 8):
+        mt = np.zeros(orc.REGISTERS, np.uint8)
+        orc.hll_add_fixed_mt(mt, keys, 16, 200_000, threads)
+        assert np.array_equal(mt, seq), threads
