@@ -247,6 +247,11 @@ int rsk_bloom_allreduce_or(rsk_bloom *b);
 int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
 /* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */
 int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint64_t n, double *ms);
+/* Time one launch of a variant of the blob+offsets PFADD kernel (slabs only):
+ * 0 production (step-count sort, 1 key per lane), 1 sorted with 2 keys per lane,
+ * 2 round-1 form (no prefetch, no sort), 3 sorted with 4 keys per lane. */
+int rsk_diag_hll_var_variant(rsk_ctx *ctx, int variant, const void *dev_data, const uint64_t *dev_offsets, uint64_t n,
+                             double *ms);
 /* Time one launch of a tuning variant of the 16-byte Bloom contains kernel. */
 int rsk_diag_bloom_contains_variant(rsk_ctx *ctx, int variant, rsk_bloom *b, const void *dev_keys16, uint64_t n,
                                     uint8_t *dev_out, double *ms);

@@ -146,6 +146,7 @@ SIGNATURES = {
     "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),
     "rsk_diag_bloom_contains_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _u64, _vp,
                                                        _P(ctypes.c_double)]),
+    "rsk_diag_hll_var_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _u64, _P(ctypes.c_double)]),
     "rsk_diag_bloom_contains_probes": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _P(_u64)]),
     "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
     "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),

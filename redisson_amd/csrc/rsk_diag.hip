@@ -165,3 +165,29 @@ extern "C" int rsk_diag_bloom_contains_probes(rsk_ctx* c, rsk_bloom* bf, const v
     return e.code;
   }
 }
+
+extern "C" int rsk_diag_hll_var_variant(rsk_ctx* c, int variant, const void* dev_data, const uint64_t* dev_offsets,
+                                        uint64_t n, double* ms) {
+  try {
+    if (!c || !dev_data || !dev_offsets || !ms || n == 0) throw rsk::RskError{RSK_ERR_INVALID_ARG, "bad arguments"};
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    RSK_HIP(hipSetDevice(c->device));
+    hipEvent_t a, b;
+    RSK_HIP(hipEventCreate(&a));
+    RSK_HIP(hipEventCreate(&b));
+    RSK_HIP(hipEventRecord(a, c->stream));
+    rsk::hll_var_variant_launch(c, variant, reinterpret_cast<const uint8_t*>(dev_data), dev_offsets, n);
+    RSK_HIP(hipEventRecord(b, c->stream));
+    RSK_HIP(hipEventSynchronize(b));
+    float f = 0;
+    RSK_HIP(hipEventElapsedTime(&f, a, b));
+    *ms = f;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    rsk::set_error("");
+    return RSK_OK;
+  } catch (const rsk::RskError& e) {
+    rsk::set_error(e.msg);
+    return e.code;
+  }
+}

@@ -238,89 +238,137 @@ static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per
                      c->d_slab);
 }
 
-// Blob + offsets, LDS-staged (the C4 path).  A workgroup takes tiles of T
+// Blob + offsets, LDS-staged (the C4 path).  A workgroup takes tiles of 512
 // consecutive keys; their bytes are one contiguous blob range, copied into
 // LDS with coalesced 16-byte loads that are issued one tile ahead (register
 // prefetch; the tile's end offset is itself loaded a tile earlier, so the
 // stage loads never wait on an offset load).  MurmurHash64A is a serial
-// chain of ceil(len/8) steps, so a wave runs as long as its longest key: the
-// tile's keys are counting-sorted by step count in LDS (wave-aggregated LDS
-// atomics) and lane j hashes the j-th key of that order, which makes every
-// wave nearly uniform in length.  A tile whose bytes exceed the stage is
-// hashed from global memory, unsorted.
-constexpr int VAR_T = 512;
+// chain of ceil(len/8) multiply-bound steps and a wave runs as long as its
+// longest key, so the tile's keys are counting-sorted by step count in LDS
+// (one LDS atomic per key gives its rank in its class) and each lane then
+// hashes KPL adjacent keys of that order, so the lanes of a wave see nearly
+// equal lengths.  KPL = 1 in production (measured: KPL 2 and 4 interleave
+// independent chains but lose more to registers and selects than they win,
+// scripts/var_variants.py).  A tile whose bytes exceed the stage is hashed
+// from global memory, unsorted.
+constexpr int VAR_TILE = 512;                   // keys per tile
 constexpr int VAR_STAGE = 32768;                // bytes per tile (64 B per key)
-constexpr int VAR_PF = VAR_STAGE / 16 / VAR_T;  // 16-byte chunks per lane
 constexpr uint32_t VAR_MAXCLS = 16;             // step classes 0..16 (16 = that long or longer)
-constexpr uint32_t VAR_NONE = VAR_MAXCLS + 1;   // lane past the end of the tile
-constexpr int VAR_NCLS = VAR_MAXCLS + 2;
+constexpr uint32_t VAR_NONE = VAR_MAXCLS + 1;   // slot past the end of the tile
+constexpr int VAR_NCLS_PAD = 20;                // classes 0..17, padded
 
-// MurmurHash64A of `len` bytes at byte `off` of the stage: one 8-byte LDS
-// read per step, the unaligned word assembled by a funnel shift.
-RSK_DEV uint64_t murmur64a_lds(const uint64_t* st, uint32_t off, uint32_t len) {
-  const uint32_t q = off >> 3, sh = (off & 7) * 8;
+// One unaligned 8-byte LDS read (gfx950 LDS takes byte-aligned ds_read_b64;
+// hipcc emits it for the memcpy).
+RSK_DEV uint64_t lds_u64(const uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+
+// MurmurHash64A of KPL keys of the stage (bytes [off, off+len)), as KPL
+// interleaved chains over max(len/8) steps; a chain past its own blocks
+// keeps its value (its clamped read stays inside its key + 7 bytes).  The
+// tail read may run up to 7 bytes past a key, inside the stage's slack;
+// those bytes are masked off.
+RSK_DEV uint64_t murmur64a_lds(const uint8_t* p, uint32_t len) {
   const uint32_t nb = len >> 3, t = len & 7;
   uint64_t h = (uint64_t)HLL_SEED ^ ((uint64_t)len * MM_M);
-  uint64_t lo = st[q];
   for (uint32_t j = 0; j < nb; ++j) {
-    const uint64_t hi = st[q + j + 1];
-    h ^= mm_mix(sh ? (lo >> sh) | (hi << (64 - sh)) : lo);
+    h ^= mm_mix(lds_u64(p + 8 * j));
     h *= MM_M;
-    lo = hi;
   }
   if (t) {
-    // the tail's bytes start at off + 8*nb; bytes past the key are masked
-    const uint64_t hi = st[q + nb + 1];
-    h ^= (sh ? (lo >> sh) | (hi << (64 - sh)) : lo) & ((1ULL << (8 * t)) - 1);
+    h ^= lds_u64(p + 8 * nb) & ((1ULL << (8 * t)) - 1);
     h *= MM_M;
   }
   return mm_final(h);
 }
+template <int KPL>
+RSK_DEV void murmur64a_lds_multi(const uint8_t* st, const uint32_t (&off)[KPL], const uint32_t (&len)[KPL],
+                                 uint64_t (&h)[KPL]) {
+  if constexpr (KPL == 1) {
+    h[0] = murmur64a_lds(st + off[0], len[0]);
+    return;
+  }
+  uint32_t nb[KPL], nmax = 0;
+#pragma unroll
+  for (int q = 0; q < KPL; ++q) {
+    nb[q] = len[q] >> 3;
+    nmax = nb[q] > nmax ? nb[q] : nmax;
+    h[q] = (uint64_t)HLL_SEED ^ ((uint64_t)len[q] * MM_M);
+  }
+  for (uint32_t j = 0; j < nmax; ++j) {
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+      const uint32_t jj = j < nb[q] ? j : nb[q];
+      const uint64_t hn = (h[q] ^ mm_mix(lds_u64(st + off[q] + 8 * jj))) * MM_M;
+      h[q] = j < nb[q] ? hn : h[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < KPL; ++q) {
+    const uint32_t t = len[q] & 7;
+    if (t) h[q] = (h[q] ^ (lds_u64(st + off[q] + 8 * nb[q]) & ((1ULL << (8 * t)) - 1))) * MM_M;
+    h[q] = mm_final(h[q]);
+  }
+}
 
-// 3 workgroups per CU (LDS ~50 KiB each) = 6 waves per SIMD.
-__global__ __launch_bounds__(VAR_T, 6) void hll_add_var_staged_kernel(const uint8_t* __restrict__ data,
-                                                                      const uint64_t* __restrict__ offsets, uint64_t n,
-                                                                      uint64_t per_block, uint8_t* __restrict__ slabs) {
+// Bytes [off, off+len) of the stage, or of global memory for an unstaged tile.
+RSK_DEV uint64_t var_hash(bool staged, const uint64_t* st, uint32_t off, const uint8_t* g, uint64_t len) {
+  if (staged) return murmur64a_lds(reinterpret_cast<const uint8_t*>(st) + off, (uint32_t)len);
+  return len <= 64 ? murmur64a_le64(g, (uint32_t)len) : murmur64a(g, len);
+}
+
+// KPL keys per lane, 512 / KPL lanes; 3 workgroups per CU (LDS ~50 KiB each).
+template <int KPL>
+__global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_add_var_staged_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint64_t n, uint64_t per_block,
+    uint8_t* __restrict__ slabs) {
+  constexpr int T = VAR_TILE / KPL;
+  constexpr int PF = VAR_STAGE / 16 / T;  // 16-byte stage chunks per lane
   __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
   __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
-  __shared__ uint32_t perm[VAR_T];  // sorted keys: stage offset | len << 16
-  __shared__ uint32_t cnt[VAR_NCLS], cbase[VAR_NCLS];
+  __shared__ uint32_t perm[VAR_TILE];  // sorted keys: stage offset | len << 16
+  __shared__ uint32_t cnt[VAR_NCLS_PAD], cbase[VAR_NCLS_PAD];
   const uint32_t tid = threadIdx.x;
   lds8_zero(regs32);
-  if (tid < VAR_NCLS) cnt[tid] = 0;
+  if (tid < VAR_NCLS_PAD) cnt[tid] = 0;
   const uint64_t begin = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = begin + per_block < n ? begin + per_block : n;
   const uintptr_t dbase = reinterpret_cast<uintptr_t>(data);
+  const uint8_t* st8 = reinterpret_cast<const uint8_t*>(stage);
 
   // Tile state, one tile ahead.  The stage window starts at the 16-byte-
   // aligned ADDRESS at or below the tile's first byte, so no chunk load
-  // crosses into a page the blob does not touch.
-  uint64_t last = 0, s = 0, e = 0, hi_ahead = 0;
+  // crosses into a page the blob does not touch.  Lane key q is tile key
+  // tid + q*T (coalesced offset loads).
+  uint64_t last = 0, hi_ahead = 0, s[KPL], e[KPL];
   uintptr_t a0 = 0;
   uint32_t nchunk = 0;
-  bool staged = false, mine = false;
-  uint4 pf[VAR_PF];
-  // Tile [b, last) with byte range [lo, hi): stage loads issue at once.
+  bool staged = false;
+  uint4 pf[PF];
   auto fetch = [&](uint64_t b, uint64_t lo, uint64_t hi) {
-    last = b + VAR_T < end ? b + VAR_T : end;
+    last = b + VAR_TILE < end ? b + VAR_TILE : end;
     a0 = (dbase + lo) & ~uintptr_t(15);
     const uint64_t span = dbase + hi - a0;
     staged = span <= (uint64_t)VAR_STAGE;
     nchunk = staged ? (uint32_t)((span + 15) >> 4) : 0;
 #pragma unroll
-    for (int u = 0; u < VAR_PF; ++u) {
-      const uint32_t c = tid + (uint32_t)u * VAR_T;
+    for (int u = 0; u < PF; ++u) {
+      const uint32_t c = tid + (uint32_t)u * T;
       if (c < nchunk) pf[u] = ld_nt16(reinterpret_cast<const uint4*>(a0) + c);
     }
-    const uint64_t i = b + tid;
-    mine = i < last;
-    s = mine ? offsets[i] : 0;
-    e = mine ? offsets[i + 1] : 0;
-    hi_ahead = offsets[last + VAR_T < end ? last + VAR_T : end];  // the following tile's end
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+      const uint64_t i = b + tid + (uint64_t)q * T;
+      s[q] = i < last ? offsets[i] : 0;
+      e[q] = i < last ? offsets[i + 1] : 0;
+    }
+    hi_ahead = offsets[last + VAR_TILE < end ? last + VAR_TILE : end];  // the following tile's end
   };
   uint64_t cur_hi = 0;
   if (begin < end) {
-    cur_hi = offsets[begin + VAR_T < end ? begin + VAR_T : end];
+    cur_hi = offsets[begin + VAR_TILE < end ? begin + VAR_TILE : end];
     fetch(begin, offsets[begin], cur_hi);
   }
 
@@ -328,62 +376,132 @@ __global__ __launch_bounds__(VAR_T, 6) void hll_add_var_staged_kernel(const uint
     __syncthreads();  // [A] previous tile's stage / perm / cbase reads are done
     uint4* st16 = reinterpret_cast<uint4*>(stage);
 #pragma unroll
-    for (int u = 0; u < VAR_PF; ++u) {
-      const uint32_t c = tid + (uint32_t)u * VAR_T;
+    for (int u = 0; u < PF; ++u) {
+      const uint32_t c = tid + (uint32_t)u * T;
       if (c < nchunk) st16[c] = pf[u];
     }
-    const uint64_t len64 = e - s;
-    const uint64_t steps = (len64 + 7) >> 3;
-    const uint32_t cls = !mine ? VAR_NONE : (steps < VAR_MAXCLS ? (uint32_t)steps : VAR_MAXCLS);
-    uint32_t my_off = 0;
-    if (staged) {
-      // Wave-aggregated count: one LDS atomic per (wave, class present).
-      uint64_t rem = __ballot(cls != VAR_NONE);
-      while (rem) {
-        const int leader = __builtin_ctzll(rem);
-        const uint32_t c = (uint32_t)__shfl((int)cls, leader);
-        const uint64_t m = __ballot(cls == c);
-        uint32_t old = 0;
-        if ((int)__lane_id() == leader) old = atomicAdd(&cnt[c], (uint32_t)__popcll(m));
-        old = (uint32_t)__shfl((int)old, leader);
-        if (cls == c)
-          my_off = old + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        rem &= ~m;
-      }
+    const bool cur_staged = staged;  // workgroup-uniform
+    uint32_t cls[KPL], rk[KPL], coff[KPL];
+    uint64_t clen[KPL], cs[KPL];
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+      const bool mine = base + tid + (uint64_t)q * T < last;
+      clen[q] = e[q] - s[q];
+      cs[q] = s[q];
+      coff[q] = (uint32_t)(dbase + s[q] - a0);
+      const uint64_t steps = (clen[q] + 7) >> 3;
+      cls[q] = !mine ? VAR_NONE : (steps < VAR_MAXCLS ? (uint32_t)steps : VAR_MAXCLS);
+      rk[q] = (cur_staged && cls[q] != VAR_NONE) ? atomicAdd(&cnt[cls[q]], 1u) : 0u;  // rank inside the class
     }
-    // Keep this tile's key, then issue the next tile's loads (they land
-    // while this tile hashes).
-    const bool cur_staged = staged, cur_mine = mine;
-    const uint64_t cur_s = s;
-    const uint32_t cur_off = (uint32_t)(dbase + s - a0);
+    // Issue the next tile's loads (they land while this tile hashes).
     const uint64_t next = last;
     if (next < end) {
       const uint64_t lo_n = cur_hi;
       cur_hi = hi_ahead;
       fetch(next, lo_n, cur_hi);
     }
-    __syncthreads();  // [B] stage written, counts final
+    __syncthreads();  // [B] stage written, class counts final
     if (cur_staged) {
-      if (tid < VAR_NCLS) {
+      if (tid == 0) {  // class starts: one lane's exclusive prefix over the counts
         uint32_t acc = 0;
-        for (uint32_t c = 0; c < tid; ++c) acc += cnt[c];
-        cbase[tid] = acc;
+#pragma unroll
+        for (int c = 0; c < VAR_NCLS_PAD; ++c) {
+          const uint32_t v = cnt[c];
+          cbase[c] = acc;
+          acc += v;
+        }
       }
       __syncthreads();  // [C]
-      if (cls != VAR_NONE) perm[cbase[cls] + my_off] = cur_off | ((uint32_t)len64 << 16);
+#pragma unroll
+      for (int q = 0; q < KPL; ++q)
+        if (cls[q] != VAR_NONE) perm[cbase[cls[q]] + rk[q]] = coff[q] | ((uint32_t)clen[q] << 16);
       __syncthreads();  // [D]
-      if (tid < VAR_NCLS) cnt[tid] = 0;
-      if (tid < cbase[VAR_NONE]) {
-        const uint32_t p = perm[tid];
-        hll_update8(regs32, murmur64a_lds(stage, p & 0xFFFFu, p >> 16));
+      if (tid < VAR_NCLS_PAD) cnt[tid] = 0;
+      const uint32_t nvalid = cbase[VAR_NONE];
+      uint32_t o[KPL], l[KPL];
+#pragma unroll
+      for (int q = 0; q < KPL; ++q) {
+        const uint32_t pos = tid * KPL + q;  // adjacent sorted keys: one class per lane, nearly
+        const uint32_t p = pos < nvalid ? perm[pos] : 0u;
+        o[q] = p & 0xFFFFu;
+        l[q] = p >> 16;
       }
-    } else if (cur_mine) {
-      hll_update8(regs32, len64 <= 64 ? murmur64a_le64(data + cur_s, (uint32_t)len64) : murmur64a(data + cur_s, len64));
+      uint64_t h[KPL];
+      murmur64a_lds_multi<KPL>(st8, o, l, h);
+#pragma unroll
+      for (int q = 0; q < KPL; ++q)
+        if (tid * KPL + q < nvalid) hll_update8(regs32, h[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < KPL; ++q)
+        if (cls[q] != VAR_NONE) hll_update8(regs32, var_hash(false, stage, 0, data + cs[q], clen[q]));
     }
     base = next;
   }
   __syncthreads();
   lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+// The round-1 form (no prefetch, no sort): the A/B baseline of the diag.
+constexpr int VAR_T = 512;
+__global__ __launch_bounds__(VAR_T) void hll_add_var_simple_kernel(const uint8_t* __restrict__ data,
+                                                                   const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                   uint64_t per_block, uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
+  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
+  lds8_zero(regs32);
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  const uintptr_t dbase = reinterpret_cast<uintptr_t>(data);
+  for (uint64_t base = begin; base < end; base += VAR_T) {
+    const uint64_t last = base + VAR_T < end ? base + VAR_T : end;
+    const uint64_t i = base + threadIdx.x;
+    const bool mine = i < last;
+    const uint64_t s = mine ? offsets[i] : 0;
+    const uint64_t e = mine ? offsets[i + 1] : 0;
+    const uintptr_t a0 = (dbase + offsets[base]) & ~uintptr_t(15);
+    const uint64_t span = dbase + offsets[last] - a0;
+    const bool staged = span <= (uint64_t)VAR_STAGE;
+    __syncthreads();  // previous tile's stage reads are done
+    if (staged) {
+      const uint32_t nchunk = (uint32_t)((span + 15) >> 4);
+      const uint4* src = reinterpret_cast<const uint4*>(a0);
+      uint4* dst = reinterpret_cast<uint4*>(stage);
+      for (uint32_t c = threadIdx.x; c < nchunk; c += VAR_T) dst[c] = ld_nt16(src + c);
+    }
+    __syncthreads();
+    if (mine) hll_update8(regs32, var_hash(staged, stage, (uint32_t)(dbase + s - a0), data + s, e - s));
+  }
+  __syncthreads();
+  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+static void var_grid(rsk_ctx* c, uint64_t n, uint64_t* blocks, uint64_t* per_block) {
+  // LDS-staged tiles: ~50 KiB of LDS per workgroup -> 3 workgroups per CU.
+  uint64_t b = std::min<uint64_t>((n + VAR_TILE - 1) / VAR_TILE, std::min<uint64_t>(3ull * c->num_cus, c->slab_count));
+  if (b == 0) b = 1;
+  uint64_t pb = (n + b - 1) / b;
+  pb = (pb + VAR_TILE - 1) / VAR_TILE * VAR_TILE;
+  *per_block = pb;
+  *blocks = (n + pb - 1) / pb;
+}
+
+void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const uint64_t* offsets, uint64_t n) {
+  uint64_t blocks, per_block;
+  var_grid(c, n, &blocks, &per_block);
+  const dim3 g((uint32_t)blocks);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL(hll_add_var_staged_kernel<1>, g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
+                               per_block, c->d_slab); break;
+    case 1: hipLaunchKernelGGL(hll_add_var_staged_kernel<2>, g, dim3(VAR_TILE / 2), 0, c->stream, data, offsets, n,
+                               per_block, c->d_slab); break;
+    case 2: hipLaunchKernelGGL(hll_add_var_simple_kernel, g, dim3(VAR_T), 0, c->stream, data, offsets, n, per_block,
+                               c->d_slab); break;
+    case 3: hipLaunchKernelGGL(hll_add_var_staged_kernel<4>, g, dim3(VAR_TILE / 4), 0, c->stream, data, offsets, n,
+                               per_block, c->d_slab); break;
+    default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
+  }
+  RSK_CHECK_LAUNCH("hll_var_variant");
 }
 
 // Max-merge `nslabs` slabs and the sketch's registers; 64 registers per
@@ -458,13 +576,9 @@ void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64
                        k.fixed_len, k.n, per_block, c->d_slab);
     RSK_CHECK_LAUNCH("hll_add_fixed");
   } else {
-    // LDS-staged tiles: 48 KiB of LDS per workgroup -> 3 workgroups per CU.
-    blocks = std::min<uint64_t>((k.n + VAR_T - 1) / VAR_T, std::min<uint64_t>(3ull * c->num_cus, max_blocks));
-    per_block = (k.n + blocks - 1) / blocks;
-    per_block = (per_block + VAR_T - 1) / VAR_T * VAR_T;
-    blocks = (k.n + per_block - 1) / per_block;
+    var_grid(c, k.n, &blocks, &per_block);
     ProfScope ps(c, "hll_add_var");
-    hipLaunchKernelGGL(hll_add_var_staged_kernel, dim3((uint32_t)blocks), dim3(VAR_T), 0, c->stream, k.data,
+    hipLaunchKernelGGL(hll_add_var_staged_kernel<1>, dim3((uint32_t)blocks), dim3(VAR_TILE), 0, c->stream, k.data,
                        k.offsets, k.n, per_block, c->d_slab);
     RSK_CHECK_LAUNCH("hll_add_var");
   }

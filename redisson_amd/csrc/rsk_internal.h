@@ -154,6 +154,8 @@ void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* con
 void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out);
 void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag);
 void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n);
+// Blob+offsets PFADD variants (rsk_diag_hll_var_variant), slabs only.
+void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const uint64_t* offsets, uint64_t n);
 
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);

@@ -16,6 +16,7 @@ for w in "$@"; do
     c5) step bench_c5 600 python bench.py --workload c5 --keys 500000000 --steps 3 --warmup 1 || exit 1 ;;
     c5prof) step c5prof 600 python scripts/c5_profile.py || exit 1 ;;
     bloomvar) step bloomvar 600 python scripts/bloom_variants.py gpurun_out/bloom_variants.json || exit 1 ;;
+    varvar) step varvar 600 python scripts/var_variants.py gpurun_out/var_variants.json || exit 1 ;;
   esac
 done
 exit 0
