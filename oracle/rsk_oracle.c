@@ -186,8 +186,9 @@ void orc_gen_queries16(uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t 
             lo = orc_splitmix64(iseed + 2 * i);
             hi = orc_splitmix64(iseed + 2 * i + 1);
         } else {
-            lo = orc_splitmix64(qseed + 3 * q + 1);
-            hi = orc_splitmix64(qseed + 3 * q + 2);
+            /* bit 63 set: never a state of the insert stream (iseed + j, j < 2^62) */
+            lo = orc_splitmix64((qseed + 3 * q + 1) | 0x8000000000000000ULL);
+            hi = orc_splitmix64((qseed + 3 * q + 2) | 0x8000000000000000ULL);
         }
         memcpy(out + 16 * j, &lo, 8);
         memcpy(out + 16 * j + 8, &hi, 8);

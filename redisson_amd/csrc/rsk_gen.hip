@@ -29,6 +29,8 @@ __global__ void gen_grouped_kernel(uint64_t seed, uint64_t G, uint64_t start, ui
 
 // C3 queries: r = splitmix64(q+3j); r&1 -> inserted key (r>>1) mod n_ins,
 // else fresh (splitmix64(q+3j+1), splitmix64(q+3j+2)).
+constexpr uint64_t FRESH_TAG = 1ULL << 63;
+
 __global__ void gen_queries16_kernel(uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
                                      uint4* __restrict__ out) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
@@ -40,8 +42,10 @@ __global__ void gen_queries16_kernel(uint64_t qseed, uint64_t iseed, uint64_t n_
       lo = splitmix64(iseed + 2 * i);
       hi = splitmix64(iseed + 2 * i + 1);
     } else {
-      lo = splitmix64(qseed + 3 * q + 1);
-      hi = splitmix64(qseed + 3 * q + 2);
+      // bit 63 set: a state range the insert stream (iseed + j, j < 2^62)
+      // never reaches, so a fresh key is never an inserted one
+      lo = splitmix64((qseed + 3 * q + 1) | FRESH_TAG);
+      hi = splitmix64((qseed + 3 * q + 2) | FRESH_TAG);
     }
     out[j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
   }

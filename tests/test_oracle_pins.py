@@ -171,3 +171,19 @@ def test_multithreaded_cpu_baseline_matches_sequential(orc):
         mt = np.zeros(orc.REGISTERS, np.uint8)
         orc.hll_add_fixed_mt(mt, keys, 16, 200_000, threads)
         assert np.array_equal(mt, seq), threads
+
+
+def test_c3_query_stream_fresh_keys_are_fresh(orc):
+    # C3 queries: r&1 -> an inserted key, else a fresh key from a state range the
+    # insert stream never reaches; the fresh half shows the filter's ~1% FP rate.
+    n = 200_000
+    size = orc.bloom_optimal_bits(n, 0.01)
+    k = orc.bloom_optimal_k(n, size)
+    bits = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(bits, size, k, orc.gen_keys16(0x5EED0003, 0, n), None, 16, n, want=False)
+    q = orc.gen_queries16(0x5EED0004, 0x5EED0003, n, 0, n)
+    got = orc.bloom_contains_batch(bits, size, k, q, None, 16, n).astype(bool)
+    member = np.array([orc.splitmix64(0x5EED0004 + 3 * i) & 1 for i in range(n)], bool)
+    assert got[member].all()
+    assert 0.40 < member.mean() < 0.60
+    assert got[~member].mean() < 0.03
