@@ -111,35 +111,63 @@ __global__ void range_kernel(uint8_t* __restrict__ d, uint64_t from, uint64_t to
   }
 }
 
-// BITOP: out[i] = op over srcs (bytes past a source's length read as 0).
+// BITOP: out = op over srcs (bytes past a source's length read as 0), in
+// 16-byte chunks.  Every string buffer is zero past its length and padded to
+// 16 bytes, so a chunk that starts inside a source is read whole and a chunk
+// past its end reads as zero; only NOT needs the output's tail masked.
 struct SrcList {
   const uint8_t* p[16];
   uint64_t len[16];
   uint32_t k;
 };
 
-__global__ void bitop_kernel(uint8_t* __restrict__ out, uint64_t n, SrcList s, int op) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    uint8_t acc = i < s.len[0] ? s.p[0][i] : 0;
-    if (op == 3) {
-      acc = (uint8_t)~acc;  // NOT
+RSK_DEV uint4 op16(uint4 a, uint4 b, int op) {
+  if (op == RSK_BITOP_AND) return make_uint4(a.x & b.x, a.y & b.y, a.z & b.z, a.w & b.w);
+  if (op == RSK_BITOP_OR) return make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+
+__global__ void bitop_kernel(uint4* __restrict__ out, uint64_t n, SrcList s, int op) {
+  const uint64_t n16 = (n + 15) >> 4;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = c << 4;
+    uint4 acc = b < s.len[0] ? reinterpret_cast<const uint4*>(s.p[0])[c] : make_uint4(0, 0, 0, 0);
+    if (op == RSK_BITOP_NOT) {
+      uint32_t w[4] = {~acc.x, ~acc.y, ~acc.z, ~acc.w};
+      if (b + 16 > n) {  // bytes at or past n stay zero
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t keep = (int64_t)n - (int64_t)(b + 4 * q);  // bytes of word q below n
+          w[q] = keep >= 4 ? w[q] : keep <= 0 ? 0u : (w[q] & ((1u << (8 * keep)) - 1));
+        }
+      }
+      acc = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
       for (uint32_t j = 1; j < s.k; ++j) {
-        const uint8_t x = i < s.len[j] ? s.p[j][i] : 0;
-        acc = op == 0 ? (uint8_t)(acc & x) : op == 1 ? (uint8_t)(acc | x) : (uint8_t)(acc ^ x);
+        const uint4 x = b < s.len[j] ? reinterpret_cast<const uint4*>(s.p[j])[c] : make_uint4(0, 0, 0, 0);
+        acc = op16(acc, x, op);
       }
     }
-    out[i] = acc;
+    out[c] = acc;
   }
 }
 
-// Highest set bit index + 1 (0 if none): per byte, bit i = 8b + 7 - ctz(v).
-__global__ void length_kernel(const uint8_t* __restrict__ d, uint64_t len, unsigned long long* __restrict__ out) {
+// Highest set bit index + 1 (0 if none), 16 bytes per lane: the last nonzero
+// byte b of the chunk holds MSB-first bit 8b + 7 - ctz(byte).
+__global__ void length_kernel(const uint4* __restrict__ d, uint64_t len, unsigned long long* __restrict__ out) {
   unsigned long long best = 0;
-  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < len; b += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t v = d[b];
-    const unsigned long long cand = 8 * b + 7 - __builtin_ctz(v) + 1;
-    if (v && cand > best) best = cand;
+  const uint64_t n16 = (len + 15) >> 4;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 v = d[c];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (w[q]) {
+        const uint32_t byte = 3 - (__builtin_clz(w[q]) >> 3);  // highest nonzero byte of the LE word
+        const uint32_t bv = (w[q] >> (8 * byte)) & 0xFFu;
+        best = (c << 7) + 8ull * (4 * q + byte) + 8 - __builtin_ctz(bv);
+      }
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     const unsigned long long o = __shfl_down(best, off, 64);
@@ -254,8 +282,17 @@ int rsk_bitset_set_range(rsk_bitset* b, uint64_t from, uint64_t to, int value) {
     rsk_ctx* c = b->ctx;
     Lock l(c);
     grow(b, ((to - 1) >> 3) + 1);
-    const uint64_t nbytes = ((to - 1) >> 3) - (from >> 3) + 1;
-    hipLaunchKernelGGL(range_kernel, dim3(grid_of(c, nbytes)), dim3(256), 0, c->stream, b->d, from, to, value);
+    // Whole bytes by a memset; the partial first / last byte by the mask kernel.
+    const uint64_t full_lo = (from + 7) >> 3, full_hi = to >> 3;  // bytes [full_lo, full_hi) are covered whole
+    if (full_hi > full_lo) {
+      RSK_HIP(hipMemsetAsync(b->d + full_lo, value ? 0xFF : 0x00, full_hi - full_lo, c->stream));
+      if (from < full_lo * 8)
+        hipLaunchKernelGGL(range_kernel, dim3(1), dim3(64), 0, c->stream, b->d, from, full_lo * 8, value);
+      if (full_hi * 8 < to)
+        hipLaunchKernelGGL(range_kernel, dim3(1), dim3(64), 0, c->stream, b->d, full_hi * 8, to, value);
+    } else {
+      hipLaunchKernelGGL(range_kernel, dim3(1), dim3(64), 0, c->stream, b->d, from, to, value);
+    }
     RSK_CHECK_LAUNCH("bitset_range");
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
@@ -290,7 +327,8 @@ int rsk_bitset_length(rsk_bitset* b, uint64_t* out) {
     }
     auto* d = reinterpret_cast<unsigned long long*>(c->d_small + 320);
     RSK_HIP(hipMemsetAsync(d, 0, 8, c->stream));
-    hipLaunchKernelGGL(length_kernel, dim3(grid_of(c, b->len)), dim3(256), 0, c->stream, b->d, b->len, d);
+    hipLaunchKernelGGL(length_kernel, dim3(grid_of(c, (b->len + 15) / 16)), dim3(256), 0, c->stream,
+                       reinterpret_cast<const uint4*>(b->d), b->len, d);
     RSK_CHECK_LAUNCH("bitset_length");
     RSK_HIP(hipMemcpyAsync(c->h_small + 320, d, 8, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
@@ -325,7 +363,8 @@ int rsk_bitset_bitop(int op, rsk_bitset* dst, rsk_bitset* const* srcs, uint32_t 
     uint8_t* nd = nullptr;
     RSK_HIP(hipMalloc(&nd, cap));
     RSK_HIP(hipMemsetAsync(nd, 0, cap, c->stream));
-    hipLaunchKernelGGL(bitop_kernel, dim3(grid_of(c, maxlen)), dim3(256), 0, c->stream, nd, maxlen, s, op);
+    hipLaunchKernelGGL(bitop_kernel, dim3(grid_of(c, (maxlen + 15) / 16)), dim3(256), 0, c->stream,
+                       reinterpret_cast<uint4*>(nd), maxlen, s, op);
     RSK_CHECK_LAUNCH("bitset_bitop");
     RSK_HIP(hipStreamSynchronize(c->stream));
     if (dst->d) RSK_HIP(hipFree(dst->d));
