@@ -239,10 +239,14 @@ def main():
         groups, gkeys = devmem.gen_grouped(engine, SEED_C5, G, rank * n, n)
         kb = gkeys.keys_fixed(n, 16)
         pool = GroupedHyperLogLog(engine, G)
-        rng = np.random.default_rng(5)
-        cw = rng.integers(0, G, size=(args.batch_ops, 2), dtype=np.uint64)
-        md = rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)
-        ms_ = rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)
+        # N > 1: the pool is reduce-scattered, rank r owns a contiguous 1/N of
+        # the sketches and runs count / countWith / mergeWith on those.
+        own_first, own_count = shard.owned_range(G, world, rank)
+        own_ids = np.arange(own_first, own_first + own_count, dtype=np.uint64)
+        rng = np.random.default_rng(5 + rank)
+        cw = rng.integers(own_first, own_first + own_count, size=(args.batch_ops, 2), dtype=np.uint64)
+        md = rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64)
+        ms_ = rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64)
         kern, unit_bytes = "hll_add_grouped16", 20.0 * n
         bufs = [groups, gkeys]
 
@@ -250,8 +254,10 @@ def main():
         if wl == "c5":
             pool.add(kb, groups)
             if world > 1:
-                shard.hll_allreduce_pool(pool.pool)
-            c = pool.count()
+                assert shard.hll_reducescatter_pool(pool.pool) == (own_first, own_count)  # RCCL MAX
+                c = pool.count(own_ids)
+            else:
+                c = pool.count()
             pool.countWith(cw)
             pool.mergeWith(md, ms_)
             return int(c[0])
@@ -281,7 +287,8 @@ def main():
     add_ms, add_launches = engine.prof_read(kern)
     red_ms, red_launches = engine.prof_read("hll_reduce")
     side = {name: engine.prof_read(name) for name in ("hll_count", "hll_union_count", "hll_merge",
-                                                       "hll_allreduce", "hll_allreduce_pool")}
+                                                       "hll_allreduce", "hll_allreduce_pool",
+                                                       "hll_reducescatter_pool")}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -295,7 +302,8 @@ def main():
         "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
         "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
         "c5": "Grouped HLL: %d sketches, grouped add + count(all) + %d countWith + %d mergeWith "
-              "(BASELINE configs[4])" % (args.groups, args.batch_ops, args.batch_ops),
+              "(BASELINE configs[4]); N > 1: RCCL MAX reduce-scatter of the pool, each rank counting, "
+              "unioning and merging its own 1/N of the sketches" % (args.groups, args.batch_ops, args.batch_ops),
     }
     result = {
         "metric": "HLL adds/s + Bloom lookups/s (node), % HBM roofline, 1/2/4/8 MI355X",

@@ -236,6 +236,12 @@ int rsk_comm_destroy(rsk_ctx *ctx);
 int rsk_hll_allreduce(rsk_hll *h, uint64_t id);
 /* The whole pool ([n][16384]) MAX over ranks. */
 int rsk_hll_allreduce_pool(rsk_hll *h);
+/* Grouped pools (C5): ncclReduceScatter(uint8 MAX) in place.  Afterwards this
+ * rank's sketches [*first, *first + *count) hold the MAX over all ranks;
+ * rank r owns [r*q, (r+1)*q) with q = n / nranks, and the last rank also the
+ * n mod nranks tail (which is all-reduced on every rank).  Sketches outside
+ * the owned range keep this rank's partial registers.  Caches invalidated. */
+int rsk_hll_reducescatter_pool(rsk_hll *h, uint64_t *first, uint64_t *count);
 /* Bloom bit string := OR over all ranks.  RCCL has no bitwise-OR reduction:
  * all-to-all of 1/N slices, local OR, all-gather. */
 int rsk_bloom_allreduce_or(rsk_bloom *b);

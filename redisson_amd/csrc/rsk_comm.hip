@@ -5,7 +5,9 @@
 // exchange is the merge:
 //   HLL   : ncclAllReduce(uint8, ncclMax) over the 16 KiB register file
 //           (bit-exact: max is associative and commutative) -- latency-bound;
-//   pools : the same over [n][16384] (bandwidth-bound, ring over xGMI);
+//   pools : the same over [n][16384] (bandwidth-bound, ring over xGMI), or a
+//           reduce-scatter that leaves rank r owning a contiguous 1/N of the
+//           sketches (the C5 plan: half the traffic of the all-reduce);
 //   Bloom : RCCL has no bitwise OR, so all-to-all of 1/N slices (grouped
 //           ncclSend/ncclRecv), a local OR, and ncclAllGather.
 #include <rccl/rccl.h>
@@ -180,6 +182,31 @@ int rsk_hll_allreduce_pool(rsk_hll* h) {
     hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
     RSK_CHECK_LAUNCH("invalidate");
     std::fill(h->exists.begin(), h->exists.end(), 1);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_out) {
+  return guarded([&] {
+    need(h && first_out && count_out, "NULL argument");
+    rsk_ctx* c = h->ctx;
+    Lock l(c);
+    ncclComm_t comm = comm_of(c);
+    const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank, R = rsk::HLL_REGS;
+    const uint64_t q = h->n / N, tail = h->n - q * N;
+    {
+      rsk::ProfScope ps(c, "hll_reducescatter_pool");
+      // In place: rank r's slice of the send buffer is its receive buffer.
+      if (q) RSK_NCCL(ncclReduceScatter(h->d_regs, h->d_regs + r * q * R, q * R, ncclUint8, ncclMax, comm, c->stream));
+      // The last n mod N sketches are reduced on every rank (owned by the last).
+      if (tail) RSK_NCCL(ncclAllReduce(h->d_regs + q * N * R, h->d_regs + q * N * R, tail * R, ncclUint8, ncclMax, comm,
+                                       c->stream));
+    }
+    hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
+    RSK_CHECK_LAUNCH("invalidate");
+    std::fill(h->exists.begin(), h->exists.end(), 1);
+    *first_out = r * q;
+    *count_out = q + (r == N - 1 ? tail : 0);
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }

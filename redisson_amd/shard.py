@@ -4,6 +4,7 @@ RCCL layer of librsketch (rsk_comm.hip):
 
   HLL   : rsk_hll_allreduce        ncclAllReduce(uint8, MAX), 16 KiB
   pools : rsk_hll_allreduce_pool   the same over [n][16384]
+          rsk_hll_reducescatter_pool  MAX reduce-scatter: rank r owns 1/N of the sketches (C5)
   Bloom : rsk_bloom_allreduce_or   all-to-all of 1/N slices, local OR, all-gather
 
 torch.distributed is used only as the out-of-band channel that ships the
@@ -66,6 +67,22 @@ def hll_allreduce_pool(pool) -> None:
     _lib.check(_lib.load().rsk_hll_allreduce_pool(pool), "rsk_hll_allreduce_pool")
 
 
+def owned_range(n: int, world: int, rank: int):
+    """Sketches a rank owns after rsk_hll_reducescatter_pool: [r*q, (r+1)*q),
+    q = n // world, plus the n % world tail on the last rank."""
+    q = n // world
+    return rank * q, q + (n - q * world if rank == world - 1 else 0)
+
+
+def hll_reducescatter_pool(pool):
+    """RCCL reduce-scatter (MAX) of a grouped pool; returns (first, count) of
+    the sketches this rank now holds fully merged."""
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(_lib.load().rsk_hll_reducescatter_pool(pool, ctypes.byref(first), ctypes.byref(count)),
+               "rsk_hll_reducescatter_pool")
+    return first.value, count.value
+
+
 def bloom_allreduce_or(bloom) -> None:
     _lib.check(_lib.load().rsk_bloom_allreduce_or(bloom), "rsk_bloom_allreduce_or")
 
@@ -79,6 +96,33 @@ def hll_allreduce_cpu(regs: np.ndarray, group=None) -> np.ndarray:
     t = torch.from_numpy(np.ascontiguousarray(regs, dtype=np.uint8).copy())
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t.numpy()
+
+
+def hll_reducescatter_pool_cpu(regs: np.ndarray, group=None):
+    """The C5 exchange plan on CPU tensors: rank r receives the MAX over ranks
+    of its owned rows (owned_range); returns (first, count, owned rows).  The
+    tail rows go through an all-reduce, as in rsk_hll_reducescatter_pool."""
+    import torch
+    import torch.distributed as dist
+
+    N, r = dist.get_world_size(group), dist.get_rank(group)
+    G = regs.shape[0]
+    q = G // N
+    first, count = owned_range(G, N, r)
+    out = np.empty((count, regs.shape[1]), np.uint8)
+    if q:
+        # reduce-scatter restated as N reductions of one slice each (gloo has no uint8 reduce_scatter)
+        for j in range(N):
+            t = torch.from_numpy(np.ascontiguousarray(regs[j * q:(j + 1) * q]).copy())
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            if j == r:
+                out[:q] = t.numpy()
+    if G - q * N:
+        t = torch.from_numpy(np.ascontiguousarray(regs[q * N:]).copy())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        if r == N - 1:
+            out[q:] = t.numpy()
+    return first, count, out
 
 
 def bloom_allreduce_or_cpu(bits: np.ndarray, group=None) -> np.ndarray:

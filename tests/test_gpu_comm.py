@@ -26,6 +26,9 @@ def test_one_rank_communicator(engine, orc):
         orc.hll_add(ref, keys, None, 16, 50000)
         _lib.check(L.rsk_hll_allreduce(h, 1))
         _lib.check(L.rsk_hll_allreduce_pool(h))
+        first, count = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(L.rsk_hll_reducescatter_pool(h, ctypes.byref(first), ctypes.byref(count)))
+        assert (first.value, count.value) == (0, 3)  # one rank owns the whole pool
         out = np.zeros(16384, np.uint8)
         _lib.check(L.rsk_hll_get_registers(h, 1, out.ctypes.data, _lib.RSK_MEM_HOST))
         assert np.array_equal(out, ref)

@@ -80,3 +80,47 @@ def test_shard_plan_covers_range():
         for N in (1, 2, 8):
             s = slice_words(nw, N)
             assert s % 4 == 0 and s * N >= nw
+
+
+def _worker_grouped(rank, world, port, G, n, q):
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from redisson_amd.shard import ShardPlan, hll_reducescatter_pool_cpu
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = ShardPlan(n, world).range(rank)
+        regs = np.zeros((G, O.REGISTERS), np.uint8)
+        O.hll_add_gen_grouped(regs, G, 0x5EED0006, lo, hi - lo)
+        first, count, owned = hll_reducescatter_pool_cpu(regs)
+        q.put((rank, first, count, owned.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,G", [(2, 7), (3, 7), (3, 2)])
+def test_grouped_reducescatter_owned_slices(world, G, orc):
+    """C5 plan: pairs sharded over ranks, the pool reduce-scattered (MAX); every
+    rank's owned sketches equal the single-process sketches, and the owned
+    ranges tile [0, G)."""
+    n = 40_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_grouped, args=(r, world, port, G, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = np.zeros((G, orc.REGISTERS), np.uint8)
+    orc.hll_add_gen_grouped(ref, G, 0x5EED0006, 0, n)
+    covered = 0
+    for rank, first, count, owned in results:
+        assert first == covered
+        covered += count
+        assert owned == ref[first:first + count].tobytes(), rank
+    assert covered == G
