@@ -44,6 +44,22 @@ def pmc_traffic(kernel: str, keys_per_launch: int):
     return best
 
 
+def pcie_inclusive(client, keys_host):
+    """PFADD of host-resident keys (pageable numpy, the JNI direct-buffer case):
+    the staging copies over PCIe are inside the timed region.  Never `value`."""
+    from redisson_amd import KeyBatch
+
+    hll = client.getHyperLogLog("bench-pcie")
+    kb = KeyBatch.from_numpy(keys_host.reshape(-1, 16))
+    hll.addAll(kb)  # warm-up (staging buffer allocation)
+    t0 = time.perf_counter()
+    hll.addAll(kb)
+    dt = time.perf_counter() - t0
+    n = kb.n
+    return {"value": n / dt, "unit": "keys/s", "GBps_host_to_hbm": 16 * n / dt / 1e9,
+            "sample": "%d C2 16-byte keys in pageable host memory, one addAll (256 MiB staging chunks)" % n}
+
+
 def cpu_baseline(sample_keys: int, passes: int, threads: int):
     """The oracle's restatement of Redis PFADD (hllPatLen + register max) over
     a pre-generated in-memory sample of the same C2 stream: one core (the
@@ -341,6 +357,11 @@ def main():
     if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes,
                                               max(1, min(args.cpu_threads, os.cpu_count() or 1)))
+        kd = devmem.gen_keys16(engine, SEED_C2, 0, args.cpu_sample)  # the same C2 stream, copied to host
+        host_keys = kd.to_numpy()
+        kd.free()
+        result["pcie_inclusive"] = pcie_inclusive(client, host_keys)
+        del host_keys
     else:
         result["cpu_baseline"] = None
     if rank == 0:
