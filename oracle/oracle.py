@@ -51,6 +51,8 @@ def lib():
             "orc_hll_add_raw": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_uint32, ctypes.c_uint64]),
             "orc_hll_add_gen16": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+            "orc_hll_add_gen_varlen": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_int]),
             "orc_hll_add_fixed_mt": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
                                             ctypes.c_int]),
             "orc_hll_add_gen_grouped": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
@@ -177,6 +179,10 @@ def hll_add(regs: np.ndarray, data: np.ndarray, offsets=None, fixed_len: int = 0
 def hll_add_fixed_mt(regs: np.ndarray, data: np.ndarray, fixed_len: int, n: int, nthreads: int):
     assert regs.dtype == np.uint8 and regs.size == REGISTERS and data.size >= n * fixed_len
     lib().orc_hll_add_fixed_mt(_ptr(regs), _ptr(data), fixed_len, n, nthreads)
+
+
+def hll_add_gen_varlen(regs: np.ndarray, seed: int, start: int, n: int, nthreads: int = 1):
+    lib().orc_hll_add_gen_varlen(_ptr(regs), seed, start, n, nthreads)
 
 
 def hll_add_gen16(regs: np.ndarray, seed: int, start: int, n: int, nthreads: int = 1):

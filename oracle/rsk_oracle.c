@@ -164,6 +164,35 @@ void orc_gen_varlen_key(uint64_t seed, uint64_t i, uint8_t *out) {
     }
 }
 
+/* PFADD arithmetic over the C4 stream generated on the fly (keys start ..
+ * start+n-1); nthreads > 1 uses OpenMP with private registers + max-merge. */
+void orc_hll_add_gen_varlen(uint8_t *regs, uint64_t seed, uint64_t start, uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    uint8_t *priv = (uint8_t *)calloc((size_t)nthreads, ORC_HLL_REGISTERS);
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+#ifdef _OPENMP
+        uint8_t *mine = priv + (size_t)omp_get_thread_num() * ORC_HLL_REGISTERS;
+#pragma omp for schedule(static)
+#else
+        uint8_t *mine = priv;
+#endif
+        for (uint64_t j = 0; j < n; j++) {
+            uint8_t key[64];
+            orc_gen_varlen_key(seed, start + j, key);
+            long idx;
+            int c = orc_hll_patlen(key, orc_gen_varlen_len(seed, start + j), &idx);
+            if (c > mine[idx]) mine[idx] = (uint8_t)c;
+        }
+    }
+    for (int t = 0; t < nthreads; t++)
+        for (int j = 0; j < ORC_HLL_REGISTERS; j++)
+            if (priv[(size_t)t * ORC_HLL_REGISTERS + j] > regs[j]) regs[j] = priv[(size_t)t * ORC_HLL_REGISTERS + j];
+    free(priv);
+}
+
 void orc_gen_grouped(uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t *groups, uint8_t *keys) {
     for (uint64_t j = 0; j < n; j++) {
         uint64_t i = start + j;

@@ -49,6 +49,8 @@ void orc_hll_add_fixed_mt(uint8_t *regs, const uint8_t *data, uint32_t fixed_len
 /* Same, but the keys are the synthetic 16-byte stream of SURVEY 8d (C2),
  * generated on the fly; nthreads > 1 uses OpenMP with private registers. */
 void orc_hll_add_gen16(uint8_t *regs, uint64_t seed, uint64_t start, uint64_t n, int nthreads);
+/* The C4 variable-length stream (8-64 B keys), generated on the fly. */
+void orc_hll_add_gen_varlen(uint8_t *regs, uint64_t seed, uint64_t start, uint64_t n, int nthreads);
 /* Grouped variant (C5 stream): regs is [G][16384]. */
 void orc_hll_add_gen_grouped(uint8_t *regs, uint64_t G, uint64_t seed, uint64_t start, uint64_t n);
 

@@ -295,3 +295,39 @@ def test_batched_merge_and_union_follow_redis_order(L, engine, orc):
         assert out[i] == r.pfcount(*[str(int(x)) for x in members[i]]), i
     cnt = _count(L, h, list(range(G)))
     assert [int(x) for x in cnt] == [r.pfcount(str(g)) for g in range(G)]
+
+
+def test_c2_full_size_bit_exact(L, engine, orc):
+    """BASELINE configs[1] at its full size: 1B 16-byte keys (device-generated
+    C2 stream) give registers bit-identical to Redis PFADD arithmetic (the
+    oracle, OpenMP over the same stream), and the exact PFCOUNT."""
+    from redisson_amd import devmem
+
+    n = 1_000_000_000
+    t = devmem.gen_keys16(engine, SEED_C2, 0, n)
+    h = _pool(L, engine)
+    _add(L, h, t.keys_fixed(n, 16))
+    t.free()
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add_gen16(ref, SEED_C2, 0, n, max(1, min(16, os.cpu_count() or 1)))
+    got = _regs(L, h)
+    assert np.array_equal(got, ref)
+    assert int(_count(L, h, [0])[0]) == orc.hll_count_dense(ref)
+    L.rsk_hll_destroy(h)
+
+
+def test_c4_full_size_bit_exact(L, engine, orc):
+    """BASELINE configs[3] at its per-GPU shard size: 1B variable-length keys
+    (blob + offsets, 44 GB in HBM) through the LDS-staged kernel, bit-exact."""
+    from redisson_amd import devmem
+
+    n = 1_000_000_000
+    blob, offs, tot = devmem.gen_varlen(engine, SEED_C4, 0, n)
+    h = _pool(L, engine)
+    _add(L, h, blob.keys_var(offs, n))
+    blob.free()
+    offs.free()
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add_gen_varlen(ref, SEED_C4, 0, n, max(1, min(16, os.cpu_count() or 1)))
+    assert np.array_equal(_regs(L, h), ref)
+    L.rsk_hll_destroy(h)

@@ -187,3 +187,14 @@ def test_c3_query_stream_fresh_keys_are_fresh(orc):
     assert got[member].all()
     assert 0.40 < member.mean() < 0.60
     assert got[~member].mean() < 0.03
+
+
+def test_varlen_stream_oracle_forms_agree(orc):
+    # the on-the-fly C4 oracle (used for the full-size GPU check) equals the packed-blob one
+    blob, offs = orc.gen_varlen(0x5EED0005, 1000, 50_000)
+    a = np.zeros(orc.REGISTERS, np.uint8)
+    orc.hll_add(a, blob, offs)
+    for threads in (1, 4):
+        b = np.zeros(orc.REGISTERS, np.uint8)
+        orc.hll_add_gen_varlen(b, 0x5EED0005, 1000, 50_000, threads)
+        assert np.array_equal(a, b), threads
