@@ -76,6 +76,12 @@ def lib():
                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]),
             "orc_bloom_contains_batch": (None, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]),
+            "orc_bloom_add_gen16_mt": (None, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+            "orc_bloom_contains_gen_queries_mt": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                                                    ctypes.c_int]),
             "orc_setbit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]),
             "orc_getbit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
             "orc_bitcount": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -518,3 +524,13 @@ class OracleBloomFilter:
     def count(self) -> int:
         self._read_config()
         return bloom_count(self.size, self.k, self.r.bitcount(self.name))
+
+
+def bloom_add_gen16_mt(bits: np.ndarray, size: int, k: int, seed: int, start: int, n: int, nthreads: int):
+    lib().orc_bloom_add_gen16_mt(_ptr(bits), size, k, seed, start, n, nthreads)
+
+
+def bloom_contains_gen_queries_mt(bits: np.ndarray, size: int, k: int, qseed: int, iseed: int, n_ins: int,
+                                  start: int, n: int, out: np.ndarray | None, nthreads: int) -> int:
+    return int(lib().orc_bloom_contains_gen_queries_mt(_ptr(bits), size, k, qseed, iseed, n_ins, start, n,
+                                                       _ptr(out) if out is not None else None, nthreads))

@@ -905,6 +905,52 @@ void orc_bloom_add_batch(uint8_t *bits, int64_t size, int k, const uint8_t *data
     }
 }
 
+/* The C3 insert stream (gen_keys16 keys start..start+n-1) on nthreads cores:
+ * SETBIT of all k indices by relaxed atomic byte OR (bits are only set, so
+ * the final string is order-independent).  k <= 64. */
+void orc_bloom_add_gen16_mt(uint8_t *bits, int64_t size, int k, uint64_t seed, uint64_t start, uint64_t n,
+                            int nthreads) {
+    if (k > 64) return;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+#endif
+    for (uint64_t j = 0; j < n; j++) {
+        uint8_t key[16];
+        uint64_t i = start + j, lo = orc_splitmix64(seed + 2 * i), hi = orc_splitmix64(seed + 2 * i + 1);
+        memcpy(key, &lo, 8);
+        memcpy(key + 8, &hi, 8);
+        int64_t idx[64];
+        orc_bloom_indexes(key, 16, k, size, idx);
+        for (int t = 0; t < k; t++)
+            __atomic_fetch_or(&bits[(uint64_t)idx[t] >> 3], (uint8_t)(0x80u >> (idx[t] & 7)), __ATOMIC_RELAXED);
+    }
+    (void)nthreads;
+}
+
+/* contains() over the C3 query stream (orc_gen_queries16) on nthreads cores;
+ * replies into out (may be NULL), returns the number of true replies. */
+uint64_t orc_bloom_contains_gen_queries_mt(const uint8_t *bits, int64_t size, int k, uint64_t qseed, uint64_t iseed,
+                                           uint64_t n_ins, uint64_t start, uint64_t n, uint8_t *out, int nthreads) {
+    uint64_t trues = 0;
+    if (k > 64) return 0;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static) reduction(+ : trues)
+#endif
+    for (uint64_t j = 0; j < n; j++) {
+        uint8_t key[16];
+        orc_gen_queries16(qseed, iseed, n_ins, start + j, 1, key);
+        int64_t idx[64];
+        orc_bloom_indexes(key, 16, k, size, idx);
+        int r = 1;
+        for (int t = 0; t < k - 1; t++)
+            if (!orc_getbit(bits, (uint64_t)idx[t])) { r = 0; break; }
+        if (out) out[j] = (uint8_t)r;
+        trues += (uint64_t)r;
+    }
+    (void)nthreads;
+    return trues;
+}
+
 /* contains(), RedissonBloomFilter.java:133-168: AND over getbit_0..getbit_{k-2}. */
 void orc_bloom_contains_batch(const uint8_t *bits, int64_t size, int k, const uint8_t *data,
                               const uint64_t *offsets, uint32_t fixed_len, uint64_t n, uint8_t *out) {

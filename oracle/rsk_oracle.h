@@ -81,6 +81,12 @@ void orc_bloom_add_batch(uint8_t *bits, int64_t size, int k, const uint8_t *data
 void orc_bloom_contains_batch(const uint8_t *bits, int64_t size, int k, const uint8_t *data,
                               const uint64_t *offsets, uint32_t fixed_len, uint64_t n, uint8_t *out);
 
+/* The C3 streams on nthreads cores (full-size parity checks). */
+void orc_bloom_add_gen16_mt(uint8_t *bits, int64_t size, int k, uint64_t seed, uint64_t start, uint64_t n,
+                            int nthreads);
+uint64_t orc_bloom_contains_gen_queries_mt(const uint8_t *bits, int64_t size, int k, uint64_t qseed, uint64_t iseed,
+                                           uint64_t n_ins, uint64_t start, uint64_t n, uint8_t *out, int nthreads);
+
 /* ---- Redis bitops (MSB-first string) -------------------------------- */
 int orc_setbit(uint8_t *bits, uint64_t off, int v);
 int orc_getbit(const uint8_t *bits, uint64_t off);

@@ -199,3 +199,39 @@ def test_or_bits_merge(L, engine, orc):
     bb = _bits(L, b, size)
     _lib.check(L.rsk_bloom_or_bits(a, bb.ctypes.data, bb.size, _lib.RSK_MEM_HOST))
     assert np.array_equal(_bits(L, a, size), _bits(L, full, size))
+
+
+def test_c3_full_size_bit_exact(L, engine, orc):
+    """BASELINE configs[2] at full size: 1B inserts at 1% FPP (EXTENDED,
+    9,585,058,377 bits, k=7) through the slice-partitioned insert, then 1B
+    contains(); the bit string and every reply equal the oracle's (OpenMP
+    restatement of the same streams)."""
+    import os
+
+    from redisson_amd import _lib, devmem
+
+    n = 1_000_000_000
+    size, k = 9585058377, 7
+    threads = max(1, min(16, os.cpu_count() or 1))
+    ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
+    b = _filter(L, engine, size, k)
+    ks = ins.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), None))
+    ins.free()
+    qs = devmem.gen_queries16(engine, 0x5EED0004, 0x5EED0003, n, 0, n)
+    out = devmem.DeviceBuffer(engine, n)
+    qk = qs.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_bloom_contains(b, ctypes.byref(qk), out.ptr))
+    qs.free()
+    got_bits = _bits(L, b, size)
+    got = out.to_numpy()
+    out.free()
+    L.rsk_bloom_destroy(b)
+    ref_bits = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_gen16_mt(ref_bits, size, k, 0x5EED0003, 0, n, threads)
+    assert np.array_equal(got_bits, ref_bits)
+    del got_bits
+    want = np.zeros(n, np.uint8)
+    trues = orc.bloom_contains_gen_queries_mt(ref_bits, size, k, 0x5EED0004, 0x5EED0003, n, 0, n, want, threads)
+    assert np.array_equal(got, want)
+    assert 0.50 < trues / n < 0.52  # half members + ~1% false positives on the fresh half

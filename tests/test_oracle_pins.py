@@ -198,3 +198,19 @@ def test_varlen_stream_oracle_forms_agree(orc):
         b = np.zeros(orc.REGISTERS, np.uint8)
         orc.hll_add_gen_varlen(b, 0x5EED0005, 1000, 50_000, threads)
         assert np.array_equal(a, b), threads
+
+
+def test_bloom_stream_oracle_forms_agree(orc):
+    # the OpenMP C3 oracle twins (full-size GPU check) equal the sequential batch forms
+    n, size, k = 30_000, 287_552, 7
+    keys = orc.gen_keys16(0x5EED0003, 0, n)
+    a = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(a, size, k, keys, None, 16, n, want=False)
+    b = np.zeros_like(a)
+    orc.bloom_add_gen16_mt(b, size, k, 0x5EED0003, 0, n, 4)
+    assert np.array_equal(a, b)
+    q = orc.gen_queries16(0x5EED0004, 0x5EED0003, n, 0, n)
+    want = orc.bloom_contains_batch(a, size, k, q, None, 16, n)
+    got = np.zeros(n, np.uint8)
+    assert orc.bloom_contains_gen_queries_mt(a, size, k, 0x5EED0004, 0x5EED0003, n, 0, n, got, 4) == int(want.sum())
+    assert np.array_equal(got, want)
