@@ -57,6 +57,9 @@ def lib():
                                             ctypes.c_int]),
             "orc_hll_add_gen_grouped": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                ctypes.c_uint64, ctypes.c_uint64]),
+            "orc_hll_add_gen_grouped_subset": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                      ctypes.c_int]),
             "orc_hll_dense_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
             "orc_hll_raw_sum": (ctypes.c_double, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
             "orc_hll_dense_sum": (ctypes.c_double, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
@@ -534,3 +537,9 @@ def bloom_contains_gen_queries_mt(bits: np.ndarray, size: int, k: int, qseed: in
                                   start: int, n: int, out: np.ndarray | None, nthreads: int) -> int:
     return int(lib().orc_bloom_contains_gen_queries_mt(_ptr(bits), size, k, qseed, iseed, n_ins, start, n,
                                                        _ptr(out) if out is not None else None, nthreads))
+
+
+def hll_add_gen_grouped_subset(regs: np.ndarray, G: int, gsub: int, seed: int, start: int, n: int,
+                               nthreads: int = 1):
+    assert regs.dtype == np.uint8 and regs.size == gsub * REGISTERS
+    lib().orc_hll_add_gen_grouped_subset(_ptr(regs), G, gsub, seed, start, n, nthreads)

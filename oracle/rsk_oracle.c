@@ -276,6 +276,38 @@ void orc_hll_add_gen_grouped(uint8_t *regs, uint64_t G, uint64_t seed, uint64_t 
     }
 }
 
+/* The same restricted to groups [0, gsub): regs is [gsub][16384]; only the
+ * pairs of those groups are hashed (a full-size check of a group sample),
+ * on nthreads cores, each thread owning a contiguous range of the groups. */
+void orc_hll_add_gen_grouped_subset(uint8_t *regs, uint64_t G, uint64_t gsub, uint64_t seed, uint64_t start,
+                                    uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+#ifdef _OPENMP
+        const uint64_t t = (uint64_t)omp_get_thread_num(), nt = (uint64_t)omp_get_num_threads();
+#else
+        const uint64_t t = 0, nt = 1;
+#endif
+        const uint64_t g0 = gsub * t / nt, g1 = gsub * (t + 1) / nt;
+        for (uint64_t j = 0; j < n; j++) {
+            const uint64_t i = start + j;
+            const uint32_t g = (uint32_t)(orc_splitmix64(seed + 3 * i) % G);
+            if (g < g0 || g >= g1) continue;
+            uint8_t key[16];
+            uint64_t lo = orc_splitmix64(seed + 3 * i + 1), hi = orc_splitmix64(seed + 3 * i + 2);
+            memcpy(key, &lo, 8);
+            memcpy(key + 8, &hi, 8);
+            long idx;
+            int c = orc_hll_patlen(key, 16, &idx);
+            uint8_t *r = regs + (uint64_t)g * ORC_HLL_REGISTERS;
+            if (c > r[idx]) r[idx] = (uint8_t)c;
+        }
+    }
+}
+
 /* ===================================================================== */
 /* Redis 3.2.0 dense register access (HLL_DENSE_GET/SET_REGISTER).        */
 /* ===================================================================== */

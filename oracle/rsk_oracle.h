@@ -53,6 +53,9 @@ void orc_hll_add_gen16(uint8_t *regs, uint64_t seed, uint64_t start, uint64_t n,
 void orc_hll_add_gen_varlen(uint8_t *regs, uint64_t seed, uint64_t start, uint64_t n, int nthreads);
 /* Grouped variant (C5 stream): regs is [G][16384]. */
 void orc_hll_add_gen_grouped(uint8_t *regs, uint64_t G, uint64_t seed, uint64_t start, uint64_t n);
+/* Groups [0, gsub) only (regs is [gsub][16384]), on nthreads cores. */
+void orc_hll_add_gen_grouped_subset(uint8_t *regs, uint64_t G, uint64_t gsub, uint64_t seed, uint64_t start,
+                                    uint64_t n, int nthreads);
 
 int orc_hll_dense_get(const uint8_t *dense_regs, int j);
 void orc_hll_dense_set(uint8_t *dense_regs, int j, int v);

@@ -331,3 +331,27 @@ def test_c4_full_size_bit_exact(L, engine, orc):
     orc.hll_add_gen_varlen(ref, SEED_C4, 0, n, max(1, min(16, os.cpu_count() or 1)))
     assert np.array_equal(_regs(L, h), ref)
     L.rsk_hll_destroy(h)
+
+
+def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
+    """BASELINE configs[4] at its per-GPU size: 1M sketches, 500M (group, key)
+    pairs through the grouped PFADD; the first 2048 sketches are bit-exact
+    against the oracle over the whole pair stream, and PFCOUNT of the pool
+    matches the oracle's estimator on them."""
+    from redisson_amd import _lib, devmem
+
+    G, n, gs = 1_000_000, 500_000_000, 2048
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+    h = _pool(L, engine, G)
+    ks = k.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    g.free()
+    k.free()
+    ref = np.zeros((gs, 16384), np.uint8)
+    orc.hll_add_gen_grouped_subset(ref, G, gs, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
+    got = np.zeros((gs, 16384), np.uint8)
+    _lib.check(L.rsk_memcpy(engine.ctx, got.ctypes.data, L.rsk_hll_device_registers(h), got.nbytes, 1))
+    assert np.array_equal(got, ref)
+    cnt = _count(L, h, list(range(gs)))
+    assert [int(c) for c in cnt[:64]] == [orc.hll_count_dense(ref[i]) for i in range(64)]
+    L.rsk_hll_destroy(h)

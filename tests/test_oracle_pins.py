@@ -214,3 +214,13 @@ def test_bloom_stream_oracle_forms_agree(orc):
     got = np.zeros(n, np.uint8)
     assert orc.bloom_contains_gen_queries_mt(a, size, k, 0x5EED0004, 0x5EED0003, n, 0, n, got, 4) == int(want.sum())
     assert np.array_equal(got, want)
+
+
+def test_grouped_subset_oracle_matches_full(orc):
+    G, n = 50, 20_000
+    full = np.zeros((G, orc.REGISTERS), np.uint8)
+    orc.hll_add_gen_grouped(full, G, 0x5EED0006, 0, n)
+    for threads in (1, 3):
+        sub = np.zeros((7, orc.REGISTERS), np.uint8)
+        orc.hll_add_gen_grouped_subset(sub, G, 7, 0x5EED0006, 0, n, threads)
+        assert np.array_equal(sub, full[:7]), threads
