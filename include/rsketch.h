@@ -174,6 +174,12 @@ int rsk_bloom_contains(rsk_bloom *b, const rsk_keys *keys, uint8_t *out);
 /* count() (RedissonBloomFilter.java:188-199) and the BITCOUNT it uses. */
 int rsk_bloom_count(rsk_bloom *b, int32_t *out);
 int rsk_bloom_bitcount(rsk_bloom *b, uint64_t *out);
+
+/* Hash.hashToBase64 (src/main/java/org/redisson/misc/Hash.java:29-40) of each
+ * key: farmUo and xx_r39 as two big-endian longs, Base64, trailing "=="
+ * dropped -> 22 ASCII chars per key, key i at out + 22*i (no terminators).
+ * `out` is in the keys' location. */
+int rsk_hash_to_base64(rsk_ctx *ctx, const rsk_keys *keys, char *out);
 /* The bit string as Redis holds it (MSB-first, ceil(size/8) bytes). */
 int rsk_bloom_export_bits(rsk_bloom *b, uint8_t *buf, size_t cap, size_t *len);
 int rsk_bloom_import_bits(rsk_bloom *b, const uint8_t *buf, size_t len);

@@ -15,7 +15,7 @@ from .keys import KeyBatch  # noqa: F401
 __all__ = [
     "Redisson", "Config", "RHyperLogLog", "RBloomFilter", "GroupedHyperLogLog", "KeyBatch", "Engine",
     "JsonJacksonCodec", "StringCodec", "LongCodec", "ByteArrayCodec", "JavaLong", "JavaInteger",
-    "IllegalArgumentException", "IllegalStateException", "RedisException", "EngineError", "RedissonError",
+    "IllegalArgumentException", "IllegalStateException", "RedisException", "EngineError", "RedissonError", "Hash",
 ]
 
 
@@ -33,4 +33,8 @@ def __getattr__(name):
         from . import bloom
 
         return bloom.RBloomFilter
+    if name == "Hash":
+        from . import misc
+
+        return misc.Hash
     raise AttributeError(name)

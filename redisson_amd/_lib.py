@@ -116,6 +116,7 @@ SIGNATURES = {
     "rsk_bloom_contains": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
     "rsk_bloom_count": (ctypes.c_int, [_vp, _P(_i32)]),
     "rsk_bloom_bitcount": (ctypes.c_int, [_vp, _P(_u64)]),
+    "rsk_hash_to_base64": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
     "rsk_bloom_export_bits": (ctypes.c_int, [_vp, _vp, _sz, _P(_sz)]),
     "rsk_bloom_import_bits": (ctypes.c_int, [_vp, _vp, _sz]),
     "rsk_bloom_or_bits": (ctypes.c_int, [_vp, _vp, _sz, _u32]),

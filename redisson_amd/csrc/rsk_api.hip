@@ -982,6 +982,25 @@ int rsk_bloom_contains(rsk_bloom* b, const rsk_keys* keys, uint8_t* out) {
   });
 }
 
+int rsk_hash_to_base64(rsk_ctx* c, const rsk_keys* keys, char* out) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    check_keys(keys);
+    need(keys->n == 0 || out != nullptr, "out is NULL");
+    CtxLock l(c);
+    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+      if (keys->location == RSK_MEM_DEVICE) {
+        hash_b64_launch(c, dk, out + 22 * first);
+      } else {
+        char* d = reinterpret_cast<char*>(out_scratch(c, 22 * cnt));
+        hash_b64_launch(c, dk, d);
+        RSK_HIP(hipMemcpyAsync(out + 22 * first, d, 22 * cnt, hipMemcpyDeviceToHost, c->stream));
+      }
+    });
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
 int rsk_bloom_bitcount(rsk_bloom* b, uint64_t* out) {
   return guarded([&] {
     need(b && out, "NULL argument");

@@ -430,3 +430,48 @@ void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t
 }
 
 }  // namespace rsk
+
+namespace rsk {
+
+// ------------------------------------------------ misc/Hash.hashToBase64
+// src/main/java/org/redisson/misc/Hash.java:29-40: h1 = farmUo(bytes),
+// h2 = xx_r39(bytes), written as two big-endian longs (ByteBuf.writeLong),
+// standard Base64 with padding, the trailing "==" dropped: 22 characters per
+// key (RedissonMultimap.java:62 and RedissonCache.java:160 name keys by it).
+__global__ __launch_bounds__(256) void hash_b64_kernel(const uint8_t* __restrict__ data,
+                                                       const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                                                       uint64_t n, char* __restrict__ out) {
+  const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h1, h2;  // bloom_key_hashes gives (xx, farm); Hash.java writes farm first
+    bloom_key_hashes<false>(data, offsets, fixed_len, i, h2, h1);
+    uint8_t b[18];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      b[q] = (uint8_t)(h1 >> (56 - 8 * q));
+      b[8 + q] = (uint8_t)(h2 >> (56 - 8 * q));
+    }
+    b[16] = b[17] = 0;
+    char* o = out + 22 * i;
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {  // 6 groups of 3 bytes -> 24 chars; the last 2 ('=' padding) dropped
+      const uint32_t v = ((uint32_t)b[3 * g] << 16) | ((uint32_t)b[3 * g + 1] << 8) | b[3 * g + 2];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (4 * g + c < 22) o[4 * g + c] = A[(v >> (18 - 6 * c)) & 63];
+    }
+  }
+}
+
+void hash_b64_launch(rsk_ctx* c, const DevKeys& k, char* d_out) {
+  if (k.n == 0) return;
+  uint64_t g = (k.n + 255) / 256;
+  const uint64_t cap = (uint64_t)c->num_cus * 16;
+  if (g > cap) g = cap;
+  ProfScope ps(c, "hash_b64");
+  hipLaunchKernelGGL(hash_b64_kernel, dim3((uint32_t)g), dim3(256), 0, c->stream, k.data, k.offsets, k.fixed_len, k.n,
+                     d_out);
+  RSK_CHECK_LAUNCH("hash_b64");
+}
+
+}  // namespace rsk

@@ -168,6 +168,8 @@ void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, u
 void bloom_contains_probe_count_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out,
                                        unsigned long long* d_probes);
 void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out);
+// misc/Hash.hashToBase64 of every key: 22 chars per key into d_out.
+void hash_b64_launch(rsk_ctx* c, const DevKeys& k, char* d_out);
 void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes);
 // dst[0..S) = OR over rows of src[rows][S] (u32 words).
 void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words);

@@ -224,3 +224,14 @@ def test_grouped_subset_oracle_matches_full(orc):
         sub = np.zeros((7, orc.REGISTERS), np.uint8)
         orc.hll_add_gen_grouped_subset(sub, G, 7, 0x5EED0006, 0, n, threads)
         assert np.array_equal(sub, full[:7]), threads
+
+
+def test_hash_to_base64_cpu_form_shape(orc):
+    # the CPU form the GPU misc/Hash test compares with: 16 bytes -> 24 Base64 chars, "==" dropped
+    import base64
+    import struct
+
+    import xxhash
+
+    s = base64.b64encode(struct.pack(">QQ", orc.farmhash_uo64(b"test"), xxhash.xxh64_intdigest(b"test", 0))).decode()
+    assert len(s) == 24 and s.endswith("==")
