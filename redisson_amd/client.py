@@ -50,6 +50,13 @@ class Redisson:
     def create(config: Config | None = None) -> "Redisson":
         return Redisson(config)
 
+    @staticmethod
+    def createReactive(config: Config | None = None):
+        """Redisson.createReactive(config) -> RedissonReactiveClient analogue."""
+        from .reactive import RedissonReactive
+
+        return RedissonReactive(Redisson(config))
+
     def shutdown(self):
         self._pool.shutdown(wait=True)
         with self._lock:
