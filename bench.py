@@ -256,13 +256,17 @@ def main():
         kb = gkeys.keys_fixed(n, 16)
         pool = GroupedHyperLogLog(engine, G)
         # N > 1: the pool is reduce-scattered, rank r owns a contiguous 1/N of
-        # the sketches and runs count / countWith / mergeWith on those.
+        # the sketches and counts those; countWith(a, b) runs on a's owner and
+        # mergeWith(dst, src) on dst's owner, with b / src drawn from all G
+        # sketches and fetched from their owners (rsk_hll_fetch_rows, RCCL).
         own_first, own_count = shard.owned_range(G, world, rank)
         own_ids = np.arange(own_first, own_first + own_count, dtype=np.uint64)
         rng = np.random.default_rng(5 + rank)
-        cw = rng.integers(own_first, own_first + own_count, size=(args.batch_ops, 2), dtype=np.uint64)
+        cw = np.stack([rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64),
+                       rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)], 1)
         md = rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64)
-        ms_ = rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64)
+        ms_ = rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)
+        remote = np.concatenate([cw[:, 1], ms_])
         kern, unit_bytes = "hll_add_grouped16", 20.0 * n
         bufs = [groups, gkeys]
 
@@ -272,6 +276,7 @@ def main():
             if world > 1:
                 assert shard.hll_reducescatter_pool(pool.pool) == (own_first, own_count)  # RCCL MAX
                 c = pool.count(own_ids)
+                shard.hll_fetch_rows(pool.pool, remote)  # partner / source rows from their owners
             else:
                 c = pool.count()
             pool.countWith(cw)
@@ -304,7 +309,7 @@ def main():
     red_ms, red_launches = engine.prof_read("hll_reduce")
     side = {name: engine.prof_read(name) for name in ("hll_count", "hll_union_count", "hll_merge",
                                                        "hll_allreduce", "hll_allreduce_pool",
-                                                       "hll_reducescatter_pool")}
+                                                       "hll_reducescatter_pool", "hll_fetch_rows")}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -318,8 +323,9 @@ def main():
         "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
         "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
         "c5": "Grouped HLL: %d sketches, grouped add + count(all) + %d countWith + %d mergeWith "
-              "(BASELINE configs[4]); N > 1: RCCL MAX reduce-scatter of the pool, each rank counting, "
-              "unioning and merging its own 1/N of the sketches" % (args.groups, args.batch_ops, args.batch_ops),
+              "(BASELINE configs[4]); N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
+              "own 1/N of the sketches and running countWith/mergeWith led by them against partners from "
+              "all G, fetched from their owners over RCCL" % (args.groups, args.batch_ops, args.batch_ops),
     }
     result = {
         "metric": "HLL adds/s + Bloom lookups/s (node), % HBM roofline, 1/2/4/8 MI355X",

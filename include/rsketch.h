@@ -248,6 +248,16 @@ int rsk_hll_allreduce_pool(rsk_hll *h);
  * n mod nranks tail (which is all-reduced on every rank).  Sketches outside
  * the owned range keep this rank's partial registers.  Caches invalidated. */
 int rsk_hll_reducescatter_pool(rsk_hll *h, uint64_t *first, uint64_t *count);
+/* Collective (every rank calls it, n may be 0): after a reduce-scatter, make
+ * the local rows ids[0..n) equal to their owners' rows, so that
+ * rsk_hll_count_union_batch / rsk_hll_merge_batch can read sketches owned by
+ * other ranks (countWith/mergeWith across owners, RedissonHyperLogLog.java:
+ * 83-97).  Ownership as in rsk_hll_reducescatter_pool; ids this rank owns are
+ * skipped, duplicates fetched once.  Plan: counts then ids exchanged with
+ * grouped ncclSend/ncclRecv, owners gather the rows into one staging buffer,
+ * rows sent back and scattered into the pool.  The fetched rows are a
+ * snapshot (caches invalidated); writes to them stay local. */
+int rsk_hll_fetch_rows(rsk_hll *h, const uint64_t *ids, uint64_t n);
 /* Bloom bit string := OR over all ranks.  RCCL has no bitwise-OR reduction:
  * all-to-all of 1/N slices, local OR, all-gather. */
 int rsk_bloom_allreduce_or(rsk_bloom *b);

@@ -143,6 +143,7 @@ SIGNATURES = {
     "rsk_hll_allreduce": (ctypes.c_int, [_vp, _u64]),
     "rsk_hll_allreduce_pool": (ctypes.c_int, [_vp]),
     "rsk_hll_reducescatter_pool": (ctypes.c_int, [_vp, _P(_u64), _P(_u64)]),
+    "rsk_hll_fetch_rows": (ctypes.c_int, [_vp, _vp, _u64]),
     "rsk_bloom_allreduce_or": (ctypes.c_int, [_vp]),
     "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
     "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),

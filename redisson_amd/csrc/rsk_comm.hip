@@ -12,6 +12,7 @@
 //           ncclSend/ncclRecv), a local OR, and ncclAllGather.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -60,6 +61,31 @@ ncclComm_t comm_of(rsk_ctx* c) {
 __global__ void invalidate_card_kernel(uint64_t* card, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     card[i] |= (1ull << 63);
+}
+
+// Row exchange (rsk_hll_fetch_rows): 16 KiB sketch rows between the pool and
+// a contiguous staging buffer, one workgroup per row, 16-byte lanes.
+constexpr uint32_t ROW_U4 = rsk::HLL_REGS / 16;  // 1024 uint4 per sketch
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restrict__ pool, const uint64_t* __restrict__ ids,
+                                                          uint64_t n, uint4* __restrict__ out) {
+  for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint4* src = pool + ids[r] * ROW_U4;
+    uint4* dst = out + r * ROW_U4;
+    for (uint32_t q = threadIdx.x; q < ROW_U4; q += 256) dst[q] = src[q];
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_rows_kernel(uint4* __restrict__ pool, uint64_t* __restrict__ card,
+                                                           const uint64_t* __restrict__ ids, uint64_t n,
+                                                           const uint4* __restrict__ in) {
+  for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint64_t id = ids[r];
+    uint4* dst = pool + id * ROW_U4;
+    const uint4* src = in + r * ROW_U4;
+    for (uint32_t q = threadIdx.x; q < ROW_U4; q += 256) dst[q] = src[q];
+    if (threadIdx.x == 0) card[id] |= (1ull << 63);
+  }
 }
 
 }  // namespace
@@ -207,6 +233,81 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
     std::fill(h->exists.begin(), h->exists.end(), 1);
     *first_out = r * q;
     *count_out = q + (r == N - 1 ? tail : 0);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) {
+  return guarded([&] {
+    need(h && (ids || n == 0), "NULL argument");
+    rsk_ctx* c = h->ctx;
+    Lock l(c);
+    ncclComm_t comm = comm_of(c);
+    const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank, R = rsk::HLL_REGS;
+    const uint64_t q = h->n / N;
+    auto owner = [&](uint64_t id) { return q ? std::min<uint64_t>(id / q, N - 1) : N - 1; };
+    // Requests: distinct ids owned elsewhere, grouped by owner (ascending id).
+    std::vector<uint64_t> want(ids, ids + n);
+    for (uint64_t id : want) need(id < h->n, "sketch id out of range");
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    want.erase(std::remove_if(want.begin(), want.end(), [&](uint64_t id) { return owner(id) == r; }), want.end());
+    std::vector<uint64_t> cnt(2 * N, 0);  // [0, N): rows asked of rank j; [N, 2N): rows rank j asks of us
+    for (uint64_t id : want) ++cnt[owner(id)];
+    auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+    uint64_t* d_cnt = reinterpret_cast<uint64_t*>(c->work(al(16 * N)));
+    RSK_HIP(hipMemcpyAsync(d_cnt, cnt.data(), 8 * N, hipMemcpyHostToDevice, c->stream));
+    {
+      rsk::ProfScope ps(c, "hll_fetch_counts");
+      RSK_NCCL(ncclGroupStart());  // counts: one u64 each way per peer
+      for (uint64_t j = 0; j < N; ++j) {
+        RSK_NCCL(ncclSend(d_cnt + j, 1, ncclUint64, (int)j, comm, c->stream));
+        RSK_NCCL(ncclRecv(d_cnt + N + j, 1, ncclUint64, (int)j, comm, c->stream));
+      }
+      RSK_NCCL(ncclGroupEnd());
+    }
+    RSK_HIP(hipMemcpyAsync(cnt.data() + N, d_cnt + N, 8 * N, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    uint64_t n_in = 0;
+    for (uint64_t j = 0; j < N; ++j) {
+      need(cnt[N + j] <= q + h->n % N, "peer asked for more rows than a rank owns");
+      n_in += cnt[N + j];
+    }
+    const uint64_t n_out = want.size();
+    if (n_in == 0 && n_out == 0) return;
+    // work: [want ids | incoming ids | rows we send | rows we receive]
+    uint8_t* w = c->work(al(8 * n_out) + al(8 * n_in) + (n_in + n_out) * R);
+    uint64_t* d_want = reinterpret_cast<uint64_t*>(w);
+    uint64_t* d_in = reinterpret_cast<uint64_t*>(w + al(8 * n_out));
+    uint8_t* rows_send = w + al(8 * n_out) + al(8 * n_in);
+    uint8_t* rows_recv = rows_send + n_in * R;
+    if (n_out) RSK_HIP(hipMemcpyAsync(d_want, want.data(), 8 * n_out, hipMemcpyHostToDevice, c->stream));
+    rsk::ProfScope ps(c, "hll_fetch_rows");
+    RSK_NCCL(ncclGroupStart());  // the ids each owner must ship
+    for (uint64_t j = 0, so = 0, ro = 0; j < N; so += cnt[j], ro += cnt[N + j], ++j) {
+      if (cnt[j]) RSK_NCCL(ncclSend(d_want + so, cnt[j], ncclUint64, (int)j, comm, c->stream));
+      if (cnt[N + j]) RSK_NCCL(ncclRecv(d_in + ro, cnt[N + j], ncclUint64, (int)j, comm, c->stream));
+    }
+    RSK_NCCL(ncclGroupEnd());
+    if (n_in) {
+      hipLaunchKernelGGL(gather_rows_kernel, dim3((uint32_t)std::min<uint64_t>(n_in, 1u << 16)), dim3(256), 0,
+                         c->stream, reinterpret_cast<const uint4*>(h->d_regs), d_in, n_in,
+                         reinterpret_cast<uint4*>(rows_send));
+      RSK_CHECK_LAUNCH("gather_rows");
+    }
+    RSK_NCCL(ncclGroupStart());  // the rows, in request order
+    for (uint64_t j = 0, so = 0, ro = 0; j < N; so += cnt[N + j], ro += cnt[j], ++j) {
+      if (cnt[N + j]) RSK_NCCL(ncclSend(rows_send + so * R, cnt[N + j] * R, ncclUint8, (int)j, comm, c->stream));
+      if (cnt[j]) RSK_NCCL(ncclRecv(rows_recv + ro * R, cnt[j] * R, ncclUint8, (int)j, comm, c->stream));
+    }
+    RSK_NCCL(ncclGroupEnd());
+    if (n_out) {
+      hipLaunchKernelGGL(scatter_rows_kernel, dim3((uint32_t)std::min<uint64_t>(n_out, 1u << 16)), dim3(256), 0,
+                         c->stream, reinterpret_cast<uint4*>(h->d_regs), h->d_card, d_want, n_out,
+                         reinterpret_cast<const uint4*>(rows_recv));
+      RSK_CHECK_LAUNCH("scatter_rows");
+      for (uint64_t id : want) h->exists[id] = 1;
+    }
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }

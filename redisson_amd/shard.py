@@ -83,6 +83,24 @@ def hll_reducescatter_pool(pool):
     return first.value, count.value
 
 
+def owner_of(ids, n: int, world: int) -> np.ndarray:
+    """Rank owning each sketch id after the reduce-scatter (owned_range)."""
+    q = n // world
+    ids = np.asarray(ids, dtype=np.uint64)
+    if q == 0:
+        return np.full(ids.shape, world - 1, dtype=np.int64)
+    return np.minimum(ids // np.uint64(q), np.uint64(world - 1)).astype(np.int64)
+
+
+def hll_fetch_rows(pool, ids) -> None:
+    """Collective: make the local rows `ids` equal to their owners' rows
+    (rsk_hll_fetch_rows), so countWith/mergeWith can read sketches owned by
+    other ranks.  Every rank calls it, possibly with no ids."""
+    a = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).ravel())
+    _lib.check(_lib.load().rsk_hll_fetch_rows(pool, a.ctypes.data if a.size else None, a.size),
+               "rsk_hll_fetch_rows")
+
+
 def bloom_allreduce_or(bloom) -> None:
     _lib.check(_lib.load().rsk_bloom_allreduce_or(bloom), "rsk_bloom_allreduce_or")
 
@@ -123,6 +141,36 @@ def hll_reducescatter_pool_cpu(regs: np.ndarray, group=None):
         if r == N - 1:
             out[q:] = t.numpy()
     return first, count, out
+
+
+def hll_fetch_rows_cpu(regs: np.ndarray, ids, group=None) -> np.ndarray:
+    """rsk_hll_fetch_rows restated on CPU tensors with the same plan: distinct
+    non-owned ids grouped by owner in ascending order, counts then ids
+    exchanged all-to-all, owners gather the rows in request order, rows sent
+    back and written into the local pool `regs` ([G][16384], updated in place)."""
+    import torch
+    import torch.distributed as dist
+
+    N, r = dist.get_world_size(group), dist.get_rank(group)
+    G, R = regs.shape
+    want = np.unique(np.asarray(ids, dtype=np.uint64).ravel())
+    assert want.size == 0 or int(want[-1]) < G
+    want = want[owner_of(want, G, N) != r]  # sorted by id, hence grouped by owner
+    cnt_out = np.bincount(owner_of(want, G, N), minlength=N).astype(np.int64)
+    cnt_in = torch.zeros(N, dtype=torch.int64)
+    dist.all_to_all_single(cnt_in, torch.from_numpy(cnt_out.copy()), group=group)
+    cnt_in = cnt_in.numpy()
+    so, si = [int(x) for x in cnt_out], [int(x) for x in cnt_in]
+    asked = torch.zeros(int(cnt_in.sum()), dtype=torch.int64)
+    dist.all_to_all_single(asked, torch.from_numpy(want.astype(np.int64)), output_split_sizes=si,
+                           input_split_sizes=so, group=group)
+    rows_send = torch.from_numpy(np.ascontiguousarray(regs[asked.numpy().astype(np.uint64)]).reshape(-1))
+    rows_recv = torch.zeros(want.size * R, dtype=torch.uint8)
+    dist.all_to_all_single(rows_recv, rows_send, output_split_sizes=[x * R for x in so],
+                           input_split_sizes=[x * R for x in si], group=group)
+    if want.size:
+        regs[want] = rows_recv.numpy().reshape(want.size, R)
+    return regs
 
 
 def bloom_allreduce_or_cpu(bits: np.ndarray, group=None) -> np.ndarray:

@@ -29,6 +29,12 @@ def test_one_rank_communicator(engine, orc):
         first, count = ctypes.c_uint64(), ctypes.c_uint64()
         _lib.check(L.rsk_hll_reducescatter_pool(h, ctypes.byref(first), ctypes.byref(count)))
         assert (first.value, count.value) == (0, 3)  # one rank owns the whole pool
+        fetch = np.array([2, 1, 1, 0], np.uint64)  # all owned: only the count exchange runs
+        _lib.check(L.rsk_hll_fetch_rows(h, fetch.ctypes.data, fetch.size))
+        _lib.check(L.rsk_hll_fetch_rows(h, None, 0))
+        with pytest.raises(_lib.IllegalArgumentException):  # id beyond the pool
+            bad = np.array([3], np.uint64)
+            _lib.check(L.rsk_hll_fetch_rows(h, bad.ctypes.data, 1))
         out = np.zeros(16384, np.uint8)
         _lib.check(L.rsk_hll_get_registers(h, 1, out.ctypes.data, _lib.RSK_MEM_HOST))
         assert np.array_equal(out, ref)

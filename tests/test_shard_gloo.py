@@ -124,3 +124,68 @@ def test_grouped_reducescatter_owned_slices(world, G, orc):
         covered += count
         assert owned == ref[first:first + count].tobytes(), rank
     assert covered == G
+
+
+def _worker_fetch(rank, world, port, G, n, q):
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from redisson_amd.shard import ShardPlan, hll_fetch_rows_cpu, hll_reducescatter_pool_cpu, owner_of
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = ShardPlan(n, world).range(rank)
+        regs = np.zeros((G, O.REGISTERS), np.uint8)
+        O.hll_add_gen_grouped(regs, G, 0x5EED0006, lo, hi - lo)
+        first, count, owned = hll_reducescatter_pool_cpu(regs)
+        regs[first:first + count] = owned
+        # countWith pairs led by an owned sketch, partner anywhere (duplicates,
+        # owned partners and other ranks' rows mixed); rank 1 asks for nothing.
+        rng = np.random.default_rng(11 + rank)
+        pairs = np.stack([rng.integers(first, first + max(count, 1), 6), rng.integers(0, G, 6)], 1).astype(np.uint64)
+        if rank == 1 or count == 0:
+            pairs = pairs[:0]
+        hll_fetch_rows_cpu(regs, pairs[:, 1])
+        assert all(owner_of(pairs[:, 0], G, world) == rank)
+        unions = [O.hll_count_raw(np.maximum(regs[int(a)], regs[int(b)])) for a, b in pairs]
+        q.put((rank, pairs.tolist(), unions))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,G", [(3, 10), (3, 2)])
+def test_fetch_rows_cross_owner_countwith(world, G, orc):
+    """countWith across owners (rsk_hll_fetch_rows plan): after the
+    reduce-scatter each rank fetches the partner sketches it does not own,
+    and its union counts equal the single-process PFCOUNT a b."""
+    n = 30_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_fetch, args=(r, world, port, G, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = np.zeros((G, orc.REGISTERS), np.uint8)
+    orc.hll_add_gen_grouped(ref, G, 0x5EED0006, 0, n)
+    checked = 0
+    for rank, pairs, unions in results:
+        for (a, b), u in zip(pairs, unions):
+            assert u == orc.hll_count_raw(np.maximum(ref[a], ref[b])), (rank, a, b)
+            checked += 1
+    assert checked > 0
+
+
+def test_owner_of_matches_owned_range():
+    from redisson_amd.shard import owned_range, owner_of
+
+    for G in (1, 2, 7, 10, 1000):
+        for N in (1, 2, 3, 8):
+            own = owner_of(np.arange(G, dtype=np.uint64), G, N)
+            for r in range(N):
+                f, c = owned_range(G, N, r)
+                assert (own[f:f + c] == r).all() and (own == r).sum() == c
