@@ -15,6 +15,7 @@ import argparse
 import ctypes
 import glob
 import json
+import math
 import os
 import sys
 import time
@@ -193,7 +194,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
                     help="c2: 16-byte keys (headline); c4: variable-length keys; c5: grouped sketches")
-    ap.add_argument("--keys", type=int, default=1_000_000_000, help="keys (pairs for c5) per GPU")
+    ap.add_argument("--keys", type=int, default=None,
+                    help="keys (pairs for c5) per GPU; default 1e9 (c2, c4), 5e8 for c5 (4e9 pairs over 8 GPUs)")
     ap.add_argument("--groups", type=int, default=1_000_000)
     ap.add_argument("--batch-ops", type=int, default=100_000)
     ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
@@ -230,8 +232,8 @@ def main():
     engine = client.engine
     if world > 1:
         shard.init_comm(engine)
-    n = args.keys
     wl = args.workload
+    n = args.keys if args.keys is not None else (500_000_000 if wl == "c5" else 1_000_000_000)
     extra = {}
     hll = client.getHyperLogLog("bench")
 
@@ -353,6 +355,14 @@ def main():
         "side_kernels_ms_per_launch": {k: (v[0] / v[1] if v[1] else None) for k, v in side.items()},
         "count": int(card),
     }
+    if wl == "c5":
+        # The grouped add must also read and write every touched sketch once
+        # whatever the update order (16 KiB in + 16 KiB out per touched
+        # sketch; at 500 pairs/sketch all G are touched): the state-inclusive floor.
+        touched = args.groups * -math.expm1(-n / args.groups)  # expected sketches hit by n uniform pairs
+        state = 2.0 * touched * 16384
+        result["roofline"]["state_bytes_per_launch"] = state
+        result["roofline"]["frac_incl_state"] = (unit_bytes + state) / avg_launch_s / 1e9 / HBM_PEAK_GBS
     for b in bufs:
         b.free()
     if wl == "c5":

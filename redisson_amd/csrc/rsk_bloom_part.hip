@@ -51,7 +51,10 @@ constexpr int HIST_T = 1024;
 constexpr int HIST_U = 4;  // 16-byte keys in flight per lane in hist
 constexpr int APPLY_T = 1024;
 constexpr int APPLY_U = 4;
-constexpr uint64_t PROBE_CAP = 1ull << 31;  // probes per chunk (u32 positions)
+// Probes per chunk: positions and offsets are u32, and every loop bound in
+// part2/apply stays below 2^32 - 2^24 + TILE without wrapping.  1B keys at
+// k = 7 take 2 chunks, i.e. 2 read+write passes of the filter in apply.
+constexpr uint64_t PROBE_CAP = (1ull << 32) - (1ull << 24);
 
 // Exclusive scan of one value per lane over a 256-lane workgroup.
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* total) {
