@@ -267,6 +267,7 @@ FastMod63 make_fastmod(uint64_t d) {
     unsigned __int128 num = ((unsigned __int128)1 << (63 + l)) + d - 1;
     f.M = (uint64_t)(num / d);
   }
+  f.r63 = d ? (uint64_t)((1ULL << 63) % d) : 0;
   return f;
 }
 

@@ -33,11 +33,10 @@ __global__ __launch_bounds__(256) void bloom_add_kernel(const uint8_t* __restric
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h1, h2;
     key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
-    uint64_t h = h1;
+    ProbeSeq ps(h1, h2, fm);
     for (int t = 0; t < k; ++t) {
-      uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
-      atomicOr(&bits[idx >> 5], bit_mask(idx));
-      h += (t & 1) ? h1 : h2;
+      atomicOr(&bits[ps.idx >> 5], bit_mask(ps.idx));
+      if (t + 1 < k) ps.next(t, fm);
     }
   }
 }
@@ -51,15 +50,14 @@ __global__ __launch_bounds__(256) void bloom_contains_kernel(const uint8_t* __re
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h1, h2;
     key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
-    uint64_t h = h1;
+    ProbeSeq ps(h1, h2, fm);
     uint32_t all = 1;
     for (int t = 0; t < k - 1; ++t) {
-      uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
-      if ((bits[idx >> 5] & bit_mask(idx)) == 0) {  // first clear bit decides (early exit)
+      if ((bits[ps.idx >> 5] & bit_mask(ps.idx)) == 0) {  // first clear bit decides (early exit)
         all = 0;
         break;
       }
-      h += (t & 1) ? h1 : h2;
+      ps.next(t, fm);
     }
     out[i] = (uint8_t)all;
   }
@@ -77,7 +75,7 @@ __global__ __launch_bounds__(256) void bloom_contains16_ee_kernel(const uint4* _
                                                                   int k, uint8_t* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
   for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x) * U + threadIdx.x; base < n; base += stride) {
-    uint64_t h[U], h1[U], h2[U];
+    ProbeSeq ps[U];
     bool alive[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -86,9 +84,7 @@ __global__ __launch_bounds__(256) void bloom_contains16_ee_kernel(const uint4* _
       if (alive[u]) {
         uint4 v = ld_nt16(keys + i);
         uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
-        h1[u] = xxh64_16(w0, w1);
-        h2[u] = farm_16(w0, w1);
-        h[u] = h1[u];
+        ps[u] = ProbeSeq(xxh64_16(w0, w1), farm_16(w0, w1), fm);
       }
     }
     bool live_key[U];
@@ -99,14 +95,14 @@ __global__ __launch_bounds__(256) void bloom_contains16_ee_kernel(const uint4* _
       uint64_t idx[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        idx[u] = fastmod63(h[u] & JAVA_LONG_MAX, fm);
+        idx[u] = ps[u].idx;
         w[u] = alive[u] ? bits[idx[u] >> 5] : 0xFFFFFFFFu;
       }
       bool any = false;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         alive[u] = alive[u] && (w[u] & bit_mask(idx[u])) != 0;
-        h[u] += (t & 1) ? h1[u] : h2[u];
+        ps[u].next(t, fm);
         any |= alive[u];
       }
       if (!__any(any)) break;
@@ -131,20 +127,17 @@ __global__ __launch_bounds__(256) void bloom_contains16_ph_kernel(const uint4* _
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
   uint32_t issued = 0;
   for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x) * U + threadIdx.x; base < n; base += stride) {
-    uint64_t h[U], h1[U], h2[U];
+    ProbeSeq ps[U];
     bool alive[U], live_key[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + (uint64_t)u * blockDim.x;
       alive[u] = live_key[u] = i < n;
-      h1[u] = h2[u] = 0;
       if (alive[u]) {
         uint4 v = ld_nt16(keys + i);
         uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
-        h1[u] = xxh64_16(w0, w1);
-        h2[u] = farm_16(w0, w1);
+        ps[u] = ProbeSeq(xxh64_16(w0, w1), farm_16(w0, w1), fm);
       }
-      h[u] = h1[u];
     }
     const int kk = k - 1;
     for (int t = 0; t < kk; t += P) {
@@ -154,11 +147,11 @@ __global__ __launch_bounds__(256) void bloom_contains16_ph_kernel(const uint4* _
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const bool go = alive[u] && t + p < kk;
-          const uint64_t idx = fastmod63(h[u] & JAVA_LONG_MAX, fm);
+          const uint64_t idx = ps[u].idx;
           w[u][p] = go ? bits[idx >> 5] : 0xFFFFFFFFu;
           msk[u][p] = bit_mask(idx);
           if (COUNT) issued += go ? 1u : 0u;
-          h[u] += ((t + p) & 1) ? h1[u] : h2[u];
+          ps[u].next(t + p, fm);
         }
       }
       bool any = false;
@@ -285,14 +278,14 @@ __global__ void bloom_probe_kernel(const uint8_t* __restrict__ data, const uint6
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h1, h2;
     key_hashes<false>(data, offsets, fixed_len, i, h1, h2);
-    uint64_t h = h1;
+    ProbeSeq ps(h1, h2, fm);
     for (int t = 0; t < k; ++t) {
-      uint64_t idx = fastmod63(h & JAVA_LONG_MAX, fm);
+      const uint64_t idx = ps.idx;
+      if (t + 1 < k) ps.next(t, fm);
       uint64_t p = i * (uint64_t)k + t;
       pidx[p] = idx;
       pseq[p] = (uint32_t)p;
       pclear[p] = (bits[idx >> 5] & bit_mask(idx)) == 0;
-      h += (t & 1) ? h1 : h2;
     }
   }
 }

@@ -40,13 +40,23 @@
 
 namespace rsk {
 
+#ifndef RSK_BLOOM_TILE2
+#define RSK_BLOOM_TILE2 8192
+#endif
 constexpr int SLICE_LOG = 19;                            // bits per slice = 2^19
 constexpr uint32_t SLICE_WORDS = 1u << (SLICE_LOG - 5);  // 16384 u32 = 64 KiB of LDS
 constexpr uint32_t MAX_SLICES = 32768;                   // filters up to 2^34 bits (2 GiB)
 constexpr int PT = 256;                                  // partition workgroup
-constexpr uint32_t TILE = 4096;                          // probes per partition tile
-constexpr int KT = 4;                                    // keys per lane per part1 tile
-constexpr int ET = TILE / PT;                            // elements per lane per part2 tile
+#ifndef RSK_BLOOM_TILE1
+#define RSK_BLOOM_TILE1 4096
+#endif
+#ifndef RSK_BLOOM_KT
+#define RSK_BLOOM_KT 4
+#endif
+constexpr uint32_t TILE = RSK_BLOOM_TILE1;               // probes per part1 tile
+constexpr int KT = RSK_BLOOM_KT;                         // keys per lane per part1 tile
+constexpr uint32_t TILE2 = RSK_BLOOM_TILE2;              // probes per part2 tile (longer output runs)
+constexpr int ET = TILE2 / PT;                           // elements per lane per part2 tile
 constexpr int HIST_T = 1024;
 constexpr int HIST_U = 4;  // 16-byte keys in flight per lane in hist
 constexpr int APPLY_T = 1024;
@@ -87,10 +97,10 @@ RSK_DEV void key_range(uint64_t n, uint64_t per, uint64_t* begin, uint64_t* end)
 
 template <typename F>
 RSK_DEV void for_probes(uint64_t h1, uint64_t h2, int k, const FastMod63& fm, F&& f) {
-  uint64_t x = h1;
+  ProbeSeq ps(h1, h2, fm);
   for (int t = 0; t < k; ++t) {
-    f(t, fastmod63(x & JAVA_LONG_MAX, fm));
-    x += (t & 1) ? h1 : h2;
+    f(t, ps.idx);
+    if (t + 1 < k) ps.next(t, fm);
   }
 }
 
@@ -161,17 +171,19 @@ __global__ __launch_bounds__(PT) void bloom_coarse_offsets_kernel(const uint32_t
 // bin << 16 | rank inside its bin; the tile is counting-sorted by bin into
 // srt/sbin and each bin's run is appended at cur[bin] (dlt[bin] = cur[bin] -
 // lstart[bin] maps a sorted position to its output position).
+template <uint32_t TS>
 struct SortLds {
   uint32_t hist[PT], lstart[PT], cur[PT], dlt[PT];
-  uint32_t srt[TILE];
-  uint8_t sbin[TILE];
+  uint32_t srt[TS];
+  uint8_t sbin[TS];
 };
-struct TileLds : SortLds {  // + probes staged in LDS (part1: k probes per key, k is runtime)
+struct TileLds : SortLds<TILE> {  // + probes staged in LDS (part1: k probes per key, k is runtime)
   uint32_t pay[TILE], tag[TILE];
 };
 
 // After the ranking atomics: bin starts inside the tile.  Returns this lane's bin count.
-__device__ __forceinline__ uint32_t tile_bins(SortLds& L) {
+template <class S>
+__device__ __forceinline__ uint32_t tile_bins(S& L) {
   __syncthreads();
   const uint32_t cnt = L.hist[threadIdx.x];
   uint32_t total;
@@ -182,7 +194,8 @@ __device__ __forceinline__ uint32_t tile_bins(SortLds& L) {
   return cnt;
 }
 
-__device__ __forceinline__ void tile_place(SortLds& L, uint32_t tg, uint32_t pay) {
+template <class S>
+__device__ __forceinline__ void tile_place(S& L, uint32_t tg, uint32_t pay) {
   const uint32_t b = tg >> 16;
   const uint32_t pos = L.lstart[b] + (tg & 0xFFFFu);
   L.srt[pos] = pay;
@@ -190,7 +203,8 @@ __device__ __forceinline__ void tile_place(SortLds& L, uint32_t tg, uint32_t pay
 }
 
 // Sorted tile -> runs in global memory; advances the cursors.
-__device__ __forceinline__ void tile_write(SortLds& L, uint32_t np, uint32_t cnt, uint32_t* __restrict__ out) {
+template <class S>
+__device__ __forceinline__ void tile_write(S& L, uint32_t np, uint32_t cnt, uint32_t* __restrict__ out) {
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < np; j += PT) out[L.dlt[L.sbin[j]] + j] = L.srt[j];
   __syncthreads();
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
                                                          const uint32_t* __restrict__ off2, uint32_t G,
                                                          uint32_t nunits, uint32_t f2, uint32_t nslices,
                                                          uint32_t* __restrict__ out) {
-  __shared__ SortLds L;
+  __shared__ SortLds<TILE2> L;
   __shared__ uint32_t range[2];
   const uint32_t total = off1[nunits];
   if (threadIdx.x < 2) {  // first unit starting at or after a share boundary
@@ -314,14 +328,14 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
 #pragma unroll
     for (int e = 0; e < ET; ++e) {
       const uint32_t p = fj + threadIdx.x + e * PT;
-      nxt[e] = (fu < u_end && p < lim && p < fj + TILE) ? __builtin_nontemporal_load(&in[p]) : 0;
+      nxt[e] = (fu < u_end && p < lim && p < fj + TILE2) ? __builtin_nontemporal_load(&in[p]) : 0;
     }
   };
   fetch(u, j);
   uint32_t loaded_unit = 0xFFFFFFFFu;
   while (u < u_end) {
     const uint32_t ue = off1[u + 1];
-    const uint32_t np = ue - j < TILE ? ue - j : TILE;
+    const uint32_t np = ue - j < TILE2 ? ue - j : TILE2;
     uint32_t vals[ET];
 #pragma unroll
     for (int e = 0; e < ET; ++e) vals[e] = nxt[e];

@@ -376,6 +376,7 @@ RSK_DEV uint64_t farm_uo64(const uint8_t* s, uint64_t len) {
 struct FastMod63 {
   uint64_t d;
   uint64_t M;
+  uint64_t r63;  // 2^63 mod d (ProbeSeq)
   uint32_t l;
   uint32_t pad;
 };
@@ -384,6 +385,35 @@ RSK_DEV uint64_t fastmod63(uint64_t x, const FastMod63& f) {
   uint64_t q = __umul64hi(x, f.M) >> (f.l - 1);
   return x - q * f.d;
 }
+
+// Bloom probe indices idx_t = (h_t & Long.MAX_VALUE) % size, h_0 = h1,
+// h_{t+1} = h_t + (t even ? h2 : h1) mod 2^64 (RedissonBloomFilter.java:116-131),
+// with two divisions per key instead of k.  With v_t = h_t mod 2^63 and
+// b = (step addend) mod 2^63:  v_{t+1} = v_t + b - c*2^63, c = bit 63 of
+// v_t + b, so  idx_{t+1} = idx_t + (b mod size) - c*(2^63 mod size)  (mod size),
+// every term already reduced: one conditional subtract and one conditional add.
+struct ProbeSeq {
+  uint64_t v = 0, idx = 0, v1 = 0, v2 = 0, r1 = 0, r2 = 0;
+  ProbeSeq() = default;
+  RSK_DEV ProbeSeq(uint64_t h1, uint64_t h2, const FastMod63& f) {
+    v1 = h1 & 0x7FFFFFFFFFFFFFFFULL;
+    v2 = h2 & 0x7FFFFFFFFFFFFFFFULL;
+    r1 = fastmod63(v1, f);
+    r2 = fastmod63(v2, f);
+    v = v1;
+    idx = r1;
+  }
+  // idx_t -> idx_{t+1}
+  RSK_DEV void next(int t, const FastMod63& f) {
+    const uint64_t b = (t & 1) ? v1 : v2, rb = (t & 1) ? r1 : r2;
+    const uint64_t s = v + b;  // < 2^64
+    uint64_t x = idx + rb;     // < 2 * size
+    x = x >= f.d ? x - f.d : x;
+    if (s >> 63) x = x >= f.r63 ? x - f.r63 : x + (f.d - f.r63);
+    v = s & 0x7FFFFFFFFFFFFFFFULL;
+    idx = x;
+  }
+};
 
 // ------------------------------------------------------ Bloom probe indices
 // RedissonBloomFilter.hash (:116-131): h1 = xx_r39(bytes), h2 = farmUo(bytes),
