@@ -274,6 +274,7 @@ def main():
 
     def step():
         if wl == "c5":
+            pool.clear()  # every step builds the G sketches from empty (fresh PFADDs, not idempotent re-adds)
             pool.add(kb, groups)
             if world > 1:
                 assert shard.hll_reducescatter_pool(pool.pool) == (own_first, own_count)  # RCCL MAX
@@ -308,10 +309,21 @@ def main():
     elapsed = time.perf_counter() - t0
     engine.prof_enable(False)
     add_ms, add_launches = engine.prof_read(kern)
+    kern_label = kern + "_kernel"
+    stage_ms = None
+    if wl == "c5" and add_launches == 0:
+        # the partitioned grouped PFADD (rsk_bloom_part.hip): its stages together are the add
+        stages = ("hll_gpart_count", "hll_gpart1", "hll_gpart2", "hll_gapply")
+        reads = {st: engine.prof_read(st) for st in stages}
+        add_launches = reads["hll_gapply"][1]
+        add_ms = sum(v[0] for v in reads.values())
+        stage_ms = {st: v[0] / max(1, v[1]) for st, v in reads.items()}
+        kern_label = ("hll_add_grouped (partitioned: hll_gcount + scan, hll_gpart1, hll_gcount2 + scan + "
+                      "bloom_part2, hll_gapply)")
     red_ms, red_launches = engine.prof_read("hll_reduce")
     side = {name: engine.prof_read(name) for name in ("hll_count", "hll_union_count", "hll_merge",
                                                        "hll_allreduce", "hll_allreduce_pool",
-                                                       "hll_reducescatter_pool", "hll_fetch_rows")}
+                                                       "hll_reducescatter_pool", "hll_fetch_rows", "hll_clear")}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -324,7 +336,7 @@ def main():
     workloads = {
         "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
         "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
-        "c5": "Grouped HLL: %d sketches, grouped add + count(all) + %d countWith + %d mergeWith "
+        "c5": "Grouped HLL: %d sketches cleared each step, grouped add + count(all) + %d countWith + %d mergeWith "
               "(BASELINE configs[4]); N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
               "own 1/N of the sketches and running countWith/mergeWith led by them against partners from "
               "all G, fetched from their owners over RCCL" % (args.groups, args.batch_ops, args.batch_ops),
@@ -346,9 +358,9 @@ def main():
                         "keys_per_gpu": n, "global_keys_per_step": n * world,
                         "parallelism": "key-stream sharding, RCCL MAX all-reduce of the registers" if world > 1
                         else "single GPU", "redis_semantics": "3.2.0"}, **extra),
-        "roofline": {"bound": "hbm", "kernel": kern + "_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": kern_label, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic(kern + "_kernel", n),
+                     "traffic": pmc_traffic("hll_add_grouped_partitioned" if stage_ms else kern + "_kernel", n),
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": add_launches,
                      "reduce_avg_ms": red_ms / max(1, red_launches),
                      "algorithmic_bytes_per_launch": unit_bytes},
@@ -363,6 +375,8 @@ def main():
         state = 2.0 * touched * 16384
         result["roofline"]["state_bytes_per_launch"] = state
         result["roofline"]["frac_incl_state"] = (unit_bytes + state) / avg_launch_s / 1e9 / HBM_PEAK_GBS
+        if stage_ms:
+            result["roofline"]["stage_ms_per_launch"] = stage_ms
     for b in bufs:
         b.free()
     if wl == "c5":

@@ -96,6 +96,8 @@ uint64_t rsk_hll_size(const rsk_hll *h);
 int rsk_hll_exists(rsk_hll *h, uint64_t id, int *out);
 /* DEL: RedissonObject.deleteAsync (RedissonObject.java:117-119). */
 int rsk_hll_delete(rsk_hll *h, uint64_t id);
+/* DEL of every sketch in the pool (registers and caches zeroed). */
+int rsk_hll_clear(rsk_hll *h);
 
 /* PFADD id e1..en -- RedissonHyperLogLog.addAll/addAllAsync (:46-48,:70-76)
  * with the INTENDED semantics (the fork's varargs bug is not reproduced, see

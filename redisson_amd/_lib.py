@@ -94,6 +94,7 @@ SIGNATURES = {
     "rsk_hll_size": (_u64, [_vp]),
     "rsk_hll_exists": (ctypes.c_int, [_vp, _u64, _P(ctypes.c_int)]),
     "rsk_hll_delete": (ctypes.c_int, [_vp, _u64]),
+    "rsk_hll_clear": (ctypes.c_int, [_vp]),
     "rsk_hll_add": (ctypes.c_int, [_vp, _u64, _P(rsk_keys), _vp]),
     "rsk_hll_add_each": (ctypes.c_int, [_vp, _u64, _P(rsk_keys), _vp]),
     "rsk_hll_add_grouped": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),

@@ -435,6 +435,19 @@ int rsk_hll_delete(rsk_hll* h, uint64_t id) {
   });
 }
 
+int rsk_hll_clear(rsk_hll* h) {
+  return guarded([&] {
+    if (!h) throw RskError{RSK_ERR_INVALID_ARG, "NULL handle"};
+    CtxLock l(h->ctx);
+    {
+      ProfScope ps(h->ctx, "hll_clear");
+      RSK_HIP(hipMemsetAsync(h->d_regs, 0, h->n * (uint64_t)HLL_REGS, h->ctx->stream));
+      RSK_HIP(hipMemsetAsync(h->d_card, 0, h->n * 8, h->ctx->stream));
+    }
+    std::fill(h->exists.begin(), h->exists.end(), 0);
+  });
+}
+
 int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_out) {
   return guarded([&] {
     check_hll(h, id);

@@ -285,24 +285,31 @@ __global__ __launch_bounds__(PT) void bloom_part1_kernel(const uint8_t* __restri
   }
 }
 
-// part2: units u = c * G + b in order (= the part1 buffer in order); unit u
-// is [off1[u], off1[u+1]).  Workgroup w takes the units whose start falls in
-// its equal share of the buffer, re-sorts each unit by slice (2^f2 bins) and
-// appends slice s's run at off2[s * G + b].
+// part2: unit u = (c, blocks [bb*GU, (bb+1)*GU)), u = c * (G/GU) + bb, in order
+// (= the part1 buffer in order): bucket c's runs of GU consecutive part1 blocks
+// are contiguous in the input and so are their slice-s outputs (off2 is
+// slice-major), so one unit covers them with one cursor per slice.  bin =
+// value >> bin_shift < 2^f2; value & pay_mask is written (Bloom slice offsets,
+// or HLL records as they are).  Workgroup w takes the units whose start falls
+// in its equal share of the buffer, re-sorts each unit by slice (2^f2 bins)
+// and appends slice s's run at off2[s * G + b] (b = the unit's first block).
 __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restrict__ in,
                                                          const uint32_t* __restrict__ off1,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
-                                                         uint32_t nunits, uint32_t f2, uint32_t nslices,
+                                                         uint32_t GU, uint32_t nunits, uint32_t f2, uint32_t nslices,
+                                                         uint32_t bin_shift, uint32_t pay_mask,
                                                          uint32_t* __restrict__ out) {
   __shared__ SortLds<TILE2> L;
   __shared__ uint32_t range[2];
-  const uint32_t total = off1[nunits];
+  const uint32_t NB = G / GU;  // units per coarse bucket
+  auto ust = [&](uint32_t v) { return off1[(uint64_t)(v / NB) * G + (v % NB) * GU]; };  // v == nunits: sentinel
+  const uint32_t total = ust(nunits);
   if (threadIdx.x < 2) {  // first unit starting at or after a share boundary
     const uint64_t edge = (uint64_t)total * (blockIdx.x + threadIdx.x) / gridDim.x;
     uint32_t lo = 0, hi = nunits;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (off1[mid] < edge) lo = mid + 1;
+      if (ust(mid) < edge) lo = mid + 1;
       else hi = mid;
     }
     range[threadIdx.x] = (blockIdx.x + threadIdx.x == gridDim.x) ? nunits : lo;
@@ -310,21 +317,20 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
   L.hist[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t u_end = range[1];
-  const uint32_t low = (1u << SLICE_LOG) - 1;
   const uint32_t nb = 1u << f2;
   // tile cursor: unit u, element j (absolute); the next tile is prefetched
   uint32_t u = range[0];
-  uint32_t j = u < u_end ? off1[u] : 0;
+  uint32_t j = u < u_end ? ust(u) : 0;
   auto skip_empty = [&]() {
-    while (u < u_end && j >= off1[u + 1]) {
+    while (u < u_end && j >= ust(u + 1)) {
       ++u;
-      if (u < u_end) j = off1[u];
+      if (u < u_end) j = ust(u);
     }
   };
   skip_empty();
   uint32_t nxt[ET];
   auto fetch = [&](uint32_t fu, uint32_t fj) {
-    const uint32_t lim = fu < u_end ? off1[fu + 1] : 0;
+    const uint32_t lim = fu < u_end ? ust(fu + 1) : 0;
 #pragma unroll
     for (int e = 0; e < ET; ++e) {
       const uint32_t p = fj + threadIdx.x + e * PT;
@@ -334,7 +340,7 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
   fetch(u, j);
   uint32_t loaded_unit = 0xFFFFFFFFu;
   while (u < u_end) {
-    const uint32_t ue = off1[u + 1];
+    const uint32_t ue = ust(u + 1);
     const uint32_t np = ue - j < TILE2 ? ue - j : TILE2;
     uint32_t vals[ET];
 #pragma unroll
@@ -346,7 +352,7 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
     fetch(u, j);
     __syncthreads();
     if (cu != loaded_unit) {  // new unit: its slice cursors
-      const uint32_t c = cu / G, b = cu - c * G;
+      const uint32_t c = cu / NB, b = (cu - c * NB) * GU;
       const uint32_t s = (c << f2) + threadIdx.x;
       if (threadIdx.x < nb && s < nslices) L.cur[threadIdx.x] = off2[(uint64_t)s * G + b];
       loaded_unit = cu;
@@ -356,14 +362,14 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
     for (int e = 0; e < ET; ++e) {
       const uint32_t p = threadIdx.x + e * PT;
       if (p < np) {
-        const uint32_t bin = vals[e] >> SLICE_LOG;
+        const uint32_t bin = vals[e] >> bin_shift;
         tag[e] = (bin << 16) | atomicAdd(&L.hist[bin], 1u);
       }
     }
     const uint32_t cnt = tile_bins(L);
 #pragma unroll
     for (int e = 0; e < ET; ++e)
-      if (threadIdx.x + e * PT < np) tile_place(L, tag[e], vals[e] & low);
+      if (threadIdx.x + e * PT < np) tile_place(L, tag[e], vals[e] & pay_mask);
     tile_write(L, np, cnt, out);
   }
 }
@@ -492,7 +498,7 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
     if (f2) {
       ProfScope ps(c, "bloom_part2");
       hipLaunchKernelGGL(bloom_part2_kernel, dim3(p2_grid), dim3(PT), 0, c->stream, buf_a, off1, off2, G,
-                         nbins1 * G, f2, ns, buf_b);
+                         1u, nbins1 * G, f2, ns, (uint32_t)SLICE_LOG, (1u << SLICE_LOG) - 1, buf_b);
       RSK_CHECK_LAUNCH("bloom_part2");
     }
     {
@@ -500,6 +506,215 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
       hipLaunchKernelGGL(bloom_slice_apply_kernel, dim3(std::min<uint32_t>(ns, 2 * cus)), dim3(APPLY_T), 0, c->stream,
                          buf_b, off2, G, ns, b->d_bits, b->nwords);
       RSK_CHECK_LAUNCH("bloom_slice_apply");
+    }
+  }
+  return true;
+}
+
+
+// ===================================================== grouped PFADD (C5)
+// RHyperLogLog.add on many sketches (rsk_hll_add_grouped, C5): pair i adds
+// key i to sketch groups[i].  Issued directly every pair is a random 4 B
+// read plus a memory-side CAS into a 16 GiB pool (the CAS dominates when the
+// sketches are fresh).  For large batches the pairs are instead partitioned
+// by sketch and each 8-sketch group (128 KiB) is updated in LDS:
+//   gcount : cnt1[c][b] = pairs of block b in coarse bin c = g >> 12 (<= 256 bins)
+//   gpart1 : block b hashes its pairs into records rec = (g & 0xFFF) << 20 |
+//            idx << 6 | rank and counting-sorts them by coarse bin (exact offsets)
+//   gcount2: cnt2[c*256 + f][b] = records of unit (c, b) in fine bin f = rec >> 24
+//            (16 sketches)
+//   part2  : the Bloom part2 kernel re-sorts each unit by fine bin (records kept)
+//   gapply : one workgroup per (fine bin, half): 8 sketches' registers in LDS
+//            (byte max by LDS CAS), read and written back once
+// HBM per pair: 4 (gcount) + 20 + 4 (gpart1) + 4 (gcount2) + 8 (part2) + 8 (gapply,
+// two halves), plus 32 KiB per touched sketch -- against a random read + CAS.
+constexpr uint32_t GP_BIN_SHIFT = 12;  // sketches per coarse bin = 4096 (rec keeps 12 bits of g)
+#ifndef RSK_GP_SK
+#define RSK_GP_SK 8
+#endif
+constexpr uint32_t GP_SK = RSK_GP_SK;  // sketches per gapply workgroup (GP_SK x 16 KiB of LDS)
+constexpr uint32_t GP_NP = 16 / GP_SK; // gapply parts per fine bin (each reads the bin's records)
+constexpr uint32_t GP_T = 1024;        // gcount / gapply workgroup
+constexpr uint32_t GP_TILE = 4096;     // records per gpart1 tile
+constexpr int GP_E = GP_TILE / PT;
+constexpr uint32_t GP_GU = 8;          // gpart1 blocks per part2 unit (G1 is a multiple)
+
+__global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __restrict__ groups, uint64_t n,
+                                                          uint64_t per, uint64_t G, uint32_t nbins,
+                                                          uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[PT];
+  for (uint32_t s = threadIdx.x; s < PT; s += GP_T) h[s] = 0;
+  __syncthreads();
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  for (uint64_t i = begin + threadIdx.x; i < end; i += GP_T) {
+    const uint32_t g = __builtin_nontemporal_load(&groups[i]);
+    if (g < G) atomicAdd(&h[g >> GP_BIN_SHIFT], 1u);
+  }
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < nbins; s += GP_T) cnt[(uint64_t)s * gridDim.x + blockIdx.x] = h[s];
+}
+
+__global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict__ keys,
+                                                        const uint32_t* __restrict__ groups, uint64_t n, uint64_t per,
+                                                        uint64_t G, uint32_t nbins, const uint32_t* __restrict__ start,
+                                                        uint32_t* __restrict__ out) {
+  __shared__ SortLds<GP_TILE> L;
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  L.hist[threadIdx.x] = 0;
+  if (threadIdx.x < nbins) L.cur[threadIdx.x] = start[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  for (uint64_t k0 = begin; k0 < end; k0 += GP_TILE) {
+    uint4 v[GP_E];
+    uint32_t g[GP_E];
+#pragma unroll
+    for (int e = 0; e < GP_E; ++e) {
+      const uint64_t i = k0 + threadIdx.x + (uint64_t)e * PT;
+      const bool ok = i < end;
+      v[e] = ok ? ld_nt16(keys + i) : make_uint4(0, 0, 0, 0);
+      g[e] = ok ? __builtin_nontemporal_load(&groups[i]) : 0xFFFFFFFFu;
+    }
+    __syncthreads();  // the previous tile's hist reset is visible
+    uint32_t rec[GP_E], tag[GP_E];
+#pragma unroll
+    for (int e = 0; e < GP_E; ++e) {
+      tag[e] = 0xFFFFFFFFu;
+      if (g[e] < G) {
+        const uint64_t hsh = murmur64a_16(((uint64_t)v[e].y << 32) | v[e].x, ((uint64_t)v[e].w << 32) | v[e].z);
+        rec[e] = ((g[e] & ((1u << GP_BIN_SHIFT) - 1)) << 20) | (hll_index(hsh) << 6) | hll_rank(hsh);
+        const uint32_t b = g[e] >> GP_BIN_SHIFT;
+        tag[e] = (b << 16) | atomicAdd(&L.hist[b], 1u);
+      }
+    }
+    const uint32_t cnt = tile_bins(L);
+    const uint32_t np = L.lstart[PT - 1] + L.hist[PT - 1];  // records placed in this tile
+#pragma unroll
+    for (int e = 0; e < GP_E; ++e)
+      if (tag[e] != 0xFFFFFFFFu) tile_place(L, tag[e], rec[e]);
+    tile_write(L, np, cnt, out);
+  }
+}
+
+// unit u = c * G1 + b is [off1[u], off1[u+1]); cnt2[(c * 256 + f) * G1 + b].
+__global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restrict__ recs,
+                                                         const uint32_t* __restrict__ off1, uint32_t G1,
+                                                         uint32_t* __restrict__ cnt2) {
+  __shared__ uint32_t h[PT];
+  const uint32_t u = blockIdx.x;
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t a = off1[u], e = off1[u + 1];
+  for (uint32_t i = a + threadIdx.x; i < e; i += PT) atomicAdd(&h[__builtin_nontemporal_load(&recs[i]) >> 24], 1u);
+  __syncthreads();
+  const uint32_t c = u / G1, b = u - c * G1;
+  cnt2[((uint64_t)c * PT + threadIdx.x) * G1 + b] = h[threadIdx.x];
+}
+
+// work item w: fine bin s = w / GP_NP (16 sketches from c*4096 + f*16), part w % GP_NP.
+__global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
+                                                          const uint32_t* __restrict__ off2, uint32_t G1,
+                                                          uint32_t nfine, uint64_t G, uint8_t* __restrict__ regs) {
+  __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
+  for (uint32_t w = blockIdx.x; w < GP_NP * nfine; w += gridDim.x) {
+    const uint32_t s = w / GP_NP, half = w % GP_NP;
+    const uint32_t a = off2[(uint64_t)s * G1], e = off2[(uint64_t)(s + 1) * G1];
+    const uint64_t g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
+    if (a == e || g0 >= G) continue;  // uniform across the workgroup
+    const uint32_t nsk = (uint32_t)(G - g0 < GP_SK ? G - g0 : GP_SK);
+    const uint32_t n4 = nsk * (HLL_REGS / 16);
+    uint4* gp = reinterpret_cast<uint4*>(regs + g0 * HLL_REGS);
+    uint4* lp = reinterpret_cast<uint4*>(r32);
+    for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
+    __syncthreads();
+    for (uint32_t i = a + threadIdx.x; i < e; i += GP_T) {
+      const uint32_t r = __builtin_nontemporal_load(&recs[i]);
+      const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
+      if (sk / GP_SK != half) continue;
+      const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
+      const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
+      uint32_t* word = &r32[byte >> 2];
+      uint32_t old = *word;
+      while (((old >> sh) & 0xFFu) < rank) {
+        const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+        if (prev == old) break;
+        old = prev;
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < n4; q += GP_T) gp[q] = lp[q];
+    __syncthreads();
+  }
+}
+
+static int gpart_mode() {
+  const char* e = std::getenv("RSK_HLL_GPART");  // unset: auto; "0": never; "1": always
+  if (!e || !*e) return -1;
+  return e[0] == '0' ? 0 : 1;
+}
+
+bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
+                                 uint64_t G) {
+  const int mode = gpart_mode();
+  const bool f16 =
+      keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
+  if (mode == 0 || !f16 || keys.n == 0 || G == 0 || G > (1ull << (GP_BIN_SHIFT + 8))) return false;
+  // auto: large batches dense enough that reading + writing each touched sketch once pays
+  if (mode < 0 && (keys.n < (1ull << 22) || keys.n < 16 * G)) return false;
+  const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
+  const uint32_t nfine = nbins1 * PT;
+  const uint32_t cus = (uint32_t)c->num_cus;
+  const uint32_t G1 = 2 * GP_GU * ((cus + GP_GU - 1) / GP_GU);  // gcount / gpart1 blocks, multiple of GP_GU
+  const uint32_t p2_grid = 4 * cus;
+  const uint64_t chunk = PROBE_CAP;
+  const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
+  const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)nfine * G1 + 1;
+  size_t sb1 = 0, sb2 = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt1, c->stream);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt2, c->stream);
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2));
+  uint8_t* w = c->work(meta + 2 * al(4 * max_np));
+  uint32_t* cnt1 = reinterpret_cast<uint32_t*>(w);
+  uint32_t* off1 = reinterpret_cast<uint32_t*>(w + al(4 * ncnt1));
+  uint32_t* cnt2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1));
+  uint32_t* off2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1) + al(4 * ncnt2));
+  void* scan_tmp = w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2);
+  uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta);
+  uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np));
+  for (uint64_t first = 0; first < keys.n; first += chunk) {
+    const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
+    const uint64_t per = (m + G1 - 1) / G1;
+    const uint4* kd = reinterpret_cast<const uint4*>(keys.data) + first;
+    const uint32_t* gd = d_groups + first;
+    {
+      ProfScope ps(c, "hll_gpart_count");
+      RSK_HIP(hipMemsetAsync(cnt1 + ncnt1 - 1, 0, 4, c->stream));
+      hipLaunchKernelGGL(hll_gcount_kernel, dim3(G1), dim3(GP_T), 0, c->stream, gd, m, per, G, nbins1, cnt1);
+      RSK_CHECK_LAUNCH("hll_gcount");
+      RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb1, cnt1, off1, (int)ncnt1, c->stream));
+    }
+    {
+      ProfScope ps(c, "hll_gpart1");
+      hipLaunchKernelGGL(hll_gpart1_kernel, dim3(G1), dim3(PT), 0, c->stream, kd, gd, m, per, G, nbins1, off1, buf_a);
+      RSK_CHECK_LAUNCH("hll_gpart1");
+    }
+    {
+      ProfScope ps(c, "hll_gpart2");
+      RSK_HIP(hipMemsetAsync(cnt2 + ncnt2 - 1, 0, 4, c->stream));
+      hipLaunchKernelGGL(hll_gcount2_kernel, dim3(nbins1 * G1), dim3(PT), 0, c->stream, buf_a, off1, G1, cnt2);
+      RSK_CHECK_LAUNCH("hll_gcount2");
+      RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, off2, (int)ncnt2, c->stream));
+      hipLaunchKernelGGL(bloom_part2_kernel, dim3(p2_grid), dim3(PT), 0, c->stream, buf_a, off1, off2, G1, GP_GU,
+                         nbins1 * (G1 / GP_GU), 8u, nfine, 24u, 0xFFFFFFFFu, buf_b);
+      RSK_CHECK_LAUNCH("hll_gpart2");
+    }
+    {
+      ProfScope ps(c, "hll_gapply");
+      const uint32_t per_cu = (160u * 1024) / (GP_SK * HLL_REGS + 1024);  // workgroups resident per CU
+      hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, 2 * per_cu * cus)), dim3(GP_T), 0,
+                         c->stream,
+                         buf_b, off2, G1, nfine, G, d_regs);
+      RSK_CHECK_LAUNCH("hll_gapply");
     }
   }
   return true;

@@ -162,6 +162,9 @@ void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Slice-partitioned add (rsk_bloom_part.hip); false when the direct kernel is used
 // (small batch, k > 4096, filter > 2^34 bits, or RSK_BLOOM_PARTITION=0).
 bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
+// Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
+// batch is not worth it (or not 16-byte keys): use the direct kernel.
+bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);

@@ -160,6 +160,10 @@ class GroupedHyperLogLog:
             _lib.load().rsk_hll_destroy(self.pool)
             self.pool = None
 
+    def clear(self) -> None:
+        """DEL of every sketch in the pool (rsk_hll_clear)."""
+        _lib.check(_lib.load().rsk_hll_clear(self.pool))
+
     def add(self, keys: KeyBatch, groups) -> None:
         """groups: uint32 numpy array (host keys) or a DeviceBuffer of uint32 (device keys)."""
         if hasattr(groups, "ptr"):

@@ -70,7 +70,24 @@ def main():
                 e["fetch_bytes_per_launch"] = fe[k] * 1024 * 2  # gfx950 wide-stream correction
             if k in fe and k in wr:
                 e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + wr[k] * 1024
+        if k == "hll_add_grouped16_kernel" and k in fe and k in wr:
+            # mixed access (16 B key stream + 4 B group ids + random 4 B register
+            # words): no calibrated correction exists, so the raw counters are used
+            e["keys_per_launch"] = keys
+            e["algorithmic_bytes_per_launch"] = 20 * keys
+            e["hbm_bytes_per_launch"] = (fe[k] + wr[k]) * 1024
+            e["hbm_bytes_note"] = "raw FETCH_SIZE + WRITE_SIZE (uncalibrated for random 4 B access)"
         kern[k] = e
+    parts = ("hll_gcount_kernel", "hll_gpart1_kernel", "hll_gcount2_kernel", "bloom_part2_kernel", "hll_gapply_kernel")
+    if "hll_gapply_kernel" in kern and all(p in fe and p in wr for p in parts):
+        # the partitioned grouped PFADD as one unit (only in a C5-only run, where
+        # bloom_part2_kernel is its fine-bin pass): raw counters summed over its stages
+        kern["hll_add_grouped_partitioned"] = {
+            "keys_per_launch": keys, "algorithmic_bytes_per_launch": 20 * keys,
+            "hbm_bytes_per_launch": sum((fe[p] + wr[p]) * 1024 for p in parts),
+            "stages": list(parts),
+            "hbm_bytes_note": "raw FETCH_SIZE + WRITE_SIZE of the stages per call (16 B key stream, 4 B records, "
+                              "16 KiB sketch rows; not corrected)"}
     doc = {"sources": {"stats": sp, "fetch": fp, "write": wp}, "kernels": kern,
            "note": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch (mean over dispatches); fetch doubled for "
                    "hll_add16_kernel per MI355X_MICROARCH.md HBM section"}

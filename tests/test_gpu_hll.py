@@ -261,6 +261,65 @@ def test_grouped_add_matches_oracle(L, engine, orc):
     assert out.tolist() == want
 
 
+def _pool_regs(L, engine, h, G):
+    from redisson_amd import _lib
+
+    out = np.zeros(G * 16384, np.uint8)
+    _lib.check(L.rsk_memcpy(engine.ctx, out.ctypes.data, L.rsk_hll_device_registers(h), out.nbytes, 1))
+    return out
+
+
+@pytest.mark.parametrize("G,n", [(8205, 3_000_000), (1, 50_000), (4096 * 3, 2_000_001), (20, 4_500_003)])
+def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, monkeypatch, G, n):
+    """Grouped PFADD partitioned by sketch (coarse bins of 4096 sketches, fine
+    bins of 16, LDS halves of 8; G not a multiple of any of them) equals the
+    direct random-CAS kernel and the oracle over the whole pool."""
+    from redisson_amd import _lib, devmem
+
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+    ks = k.keys_fixed(n, 16).as_struct()
+    pools = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RSK_HLL_GPART", mode)
+        h = _pool(L, engine, G)
+        _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+        pools[mode] = h
+    g.free()
+    k.free()
+    part, direct = (_pool_regs(L, engine, pools[m], G) for m in ("1", "0"))
+    assert np.array_equal(part, direct)
+    ref = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped(ref, G, 0x5EED0006, 0, n)
+    assert np.array_equal(part, ref)
+    for h in pools.values():
+        L.rsk_hll_destroy(h)
+
+
+def test_grouped_partitioned_host_pairs_skip_out_of_range(L, engine, orc, monkeypatch):
+    """Host-resident pairs through the partitioned path: group ids >= G are
+    ignored (as by the direct kernel), every other pair lands in its sketch;
+    a second batch max-merges into the existing registers."""
+    from redisson_amd import KeyBatch, _lib
+
+    monkeypatch.setenv("RSK_HLL_GPART", "1")
+    G, n = 100, 300_000
+    rng = np.random.default_rng(7)
+    keys = orc.gen_keys16(0x5EED0107, 0, n).reshape(-1, 16)
+    groups = rng.integers(0, 130, n).astype(np.uint32)
+    h = _pool(L, engine, G)
+    for lo, hi in ((0, n // 3), (n // 3, n)):
+        ks = KeyBatch.from_numpy(np.ascontiguousarray(keys[lo:hi])).as_struct()
+        _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), np.ascontiguousarray(groups[lo:hi]).ctypes.data))
+    got = _pool_regs(L, engine, h, G).reshape(G, 16384)
+    for gid in range(G):
+        sel = np.ascontiguousarray(keys[groups == gid])
+        ref = np.zeros(16384, np.uint8)
+        if sel.shape[0]:
+            orc.hll_add(ref, sel.reshape(-1), None, 16, sel.shape[0])
+        assert np.array_equal(got[gid], ref), gid
+    L.rsk_hll_destroy(h)
+
+
 def test_batched_merge_and_union_follow_redis_order(L, engine, orc):
     """rsk_hll_merge_batch == PFMERGE dst src issued in order (chains and
     read-after-write inside one batch); rsk_hll_count_union_batch == PFCOUNT a b."""
