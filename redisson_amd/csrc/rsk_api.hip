@@ -189,6 +189,7 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
 void check_hll(const rsk_hll* h, uint64_t id) {
   need(h != nullptr, "hll handle is NULL");
   need(id < h->n, "sketch id out of range");
+  h->zero = false;  // conservatively: every caller may write registers
 }
 
 uint8_t* regs_of(rsk_hll* h, uint64_t id) { return h->d_regs + id * (uint64_t)HLL_REGS; }
@@ -399,6 +400,7 @@ int rsk_hll_create(rsk_ctx* c, uint64_t n, rsk_hll** out) {
     RSK_HIP(hipMemsetAsync(h->d_regs, 0, n * (uint64_t)HLL_REGS, c->stream));
     RSK_HIP(hipMemsetAsync(h->d_card, 0, n * 8, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
+    h->zero = true;
     *out = guard.release();
   });
 }
@@ -445,6 +447,7 @@ int rsk_hll_clear(rsk_hll* h) {
       RSK_HIP(hipMemsetAsync(h->d_card, 0, h->n * 8, h->ctx->stream));
     }
     std::fill(h->exists.begin(), h->exists.end(), 0);
+    h->zero = true;
   });
 }
 
@@ -536,6 +539,8 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     need(keys == nullptr || keys->n == 0 || groups != nullptr, "groups is NULL");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
+    const bool pool_zero = h->zero;
+    h->zero = false;
     check_keys(keys);
     if (keys->n == 0) return;
     uint32_t* d_groups = nullptr;
@@ -550,7 +555,7 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
         d_groups = reinterpret_cast<uint32_t*>(out_scratch(c, cnt * 4));
         RSK_HIP(hipMemcpyAsync(d_groups, groups + first, cnt * 4, hipMemcpyHostToDevice, c->stream));
       }
-      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n);
+      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0);
     });
     if (keys->location == RSK_MEM_DEVICE) {
       // Group ids stay on the device: every sketch of the pool is treated as
@@ -784,7 +789,11 @@ int rsk_hll_get_registers(rsk_hll* h, uint64_t id, uint8_t* out, uint32_t locati
   });
 }
 
-void* rsk_hll_device_registers(rsk_hll* h) { return h ? h->d_regs : nullptr; }
+void* rsk_hll_device_registers(rsk_hll* h) {  // the caller may write through it
+  if (!h) return nullptr;
+  h->zero = false;
+  return h->d_regs;
+}
 
 int rsk_hll_export_redis(rsk_hll* h, uint64_t id, uint8_t* buf, size_t cap, size_t* len) {
   return guarded([&] {

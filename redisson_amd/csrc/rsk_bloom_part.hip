@@ -534,6 +534,7 @@ constexpr uint32_t GP_BIN_SHIFT = 12;  // sketches per coarse bin = 4096 (rec ke
 #endif
 constexpr uint32_t GP_SK = RSK_GP_SK;  // sketches per gapply workgroup (GP_SK x 16 KiB of LDS)
 constexpr uint32_t GP_NP = 16 / GP_SK; // gapply parts per fine bin (each reads the bin's records)
+constexpr int GP_U = 4;                // record loads in flight per gapply lane
 constexpr uint32_t GP_T = 1024;        // gcount / gapply workgroup
 constexpr uint32_t GP_TILE = 4096;     // records per gpart1 tile
 constexpr int GP_E = GP_TILE / PT;
@@ -613,7 +614,8 @@ __global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restr
 // work item w: fine bin s = w / GP_NP (16 sketches from c*4096 + f*16), part w % GP_NP.
 __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
-                                                          uint32_t nfine, uint64_t G, uint8_t* __restrict__ regs) {
+                                                          uint32_t nfine, uint64_t G, int pool_zero,
+                                                          uint8_t* __restrict__ regs) {
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
   for (uint32_t w = blockIdx.x; w < GP_NP * nfine; w += gridDim.x) {
     const uint32_t s = w / GP_NP, half = w % GP_NP;
@@ -624,20 +626,32 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
     const uint32_t n4 = nsk * (HLL_REGS / 16);
     uint4* gp = reinterpret_cast<uint4*>(regs + g0 * HLL_REGS);
     uint4* lp = reinterpret_cast<uint4*>(r32);
-    for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
+    if (pool_zero)  // the pool is known to be all zero: nothing to read
+      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = make_uint4(0, 0, 0, 0);
+    else
+      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
     __syncthreads();
-    for (uint32_t i = a + threadIdx.x; i < e; i += GP_T) {
-      const uint32_t r = __builtin_nontemporal_load(&recs[i]);
-      const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
-      if (sk / GP_SK != half) continue;
-      const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
-      const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
-      uint32_t* word = &r32[byte >> 2];
-      uint32_t old = *word;
-      while (((old >> sh) & 0xFFu) < rank) {
-        const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
-        if (prev == old) break;
-        old = prev;
+    for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += GP_T * GP_U) {
+      uint32_t rv[GP_U];  // GP_U record loads in flight per lane
+#pragma unroll
+      for (int u = 0; u < GP_U; ++u) {
+        const uint32_t i = i0 + u * GP_T;
+        rv[u] = i < e ? __builtin_nontemporal_load(&recs[i]) : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int u = 0; u < GP_U; ++u) {
+        const uint32_t r = rv[u];
+        const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
+        if (r == 0xFFFFFFFFu || sk / GP_SK != half) continue;  // (rank 63 never occurs: no real record is all ones)
+        const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
+        const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
+        uint32_t* word = &r32[byte >> 2];
+        uint32_t old = *word;
+        while (((old >> sh) & 0xFFu) < rank) {
+          const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+          if (prev == old) break;
+          old = prev;
+        }
       }
     }
     __syncthreads();
@@ -653,7 +667,7 @@ static int gpart_mode() {
 }
 
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
-                                 uint64_t G) {
+                                 uint64_t G, bool pool_zero) {
   const int mode = gpart_mode();
   const bool f16 =
       keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
@@ -713,7 +727,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       const uint32_t per_cu = (160u * 1024) / (GP_SK * HLL_REGS + 1024);  // workgroups resident per CU
       hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, 2 * per_cu * cus)), dim3(GP_T), 0,
                          c->stream,
-                         buf_b, off2, G1, nfine, G, d_regs);
+                         buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0, d_regs);
       RSK_CHECK_LAUNCH("hll_gapply");
     }
   }

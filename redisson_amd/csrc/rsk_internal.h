@@ -97,6 +97,10 @@ struct rsk_hll {
   uint8_t* d_regs = nullptr;   // [n][16384] raw registers (one byte each)
   uint64_t* d_card = nullptr;  // [n] Redis card[8] as LE u64 (bit 63 = cache invalid)
   std::vector<uint8_t> exists; // host: key present
+  // Every register is known to be 0 (set by create/clear, dropped by every
+  // entry point that may write registers): the grouped add then skips
+  // reading the pool.
+  mutable bool zero = false;
   // rsk_hll_merge_batch leveling state per sketch id (valid while stamp == lv_epoch)
   std::vector<uint32_t> lv_stamp, lv_w, lv_r;
   uint32_t lv_epoch = 0;
@@ -139,7 +143,8 @@ struct DevKeys {
 // (device u32) to 1 if any register grew.
 void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64_t* d_card, uint32_t* d_flag,
                     uint32_t epoch, bool created);
-void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G);
+void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
+                            bool pool_zero = false);
 // Up to 8 sketch ids passed by value (saves a host->device copy per PFCOUNT).
 struct SmallIds {
   uint64_t v[8];
@@ -164,7 +169,8 @@ void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
 // batch is not worth it (or not 16-byte keys): use the direct kernel.
-bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G);
+bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
+                                 bool pool_zero);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);

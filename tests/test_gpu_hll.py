@@ -320,6 +320,35 @@ def test_grouped_partitioned_host_pairs_skip_out_of_range(L, engine, orc, monkey
     L.rsk_hll_destroy(h)
 
 
+def test_grouped_partitioned_pool_state_after_other_writers(L, engine, orc, monkeypatch):
+    """The partitioned add skips reading a pool known to be all zero (fresh or
+    cleared): a PFADD into one sketch beforehand, and a clear afterwards, must
+    both be honoured."""
+    from redisson_amd import KeyBatch, _lib, devmem
+
+    monkeypatch.setenv("RSK_HLL_GPART", "1")
+    G, n = 64, 200_000
+    h = _pool(L, engine, G)
+    ka = orc.gen_keys16(0x5EED0200, 0, 5000)
+    _add(L, h, KeyBatch.from_numpy(ka.reshape(-1, 16)), 5)
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+    ks = k.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    grouped = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped(grouped, G, 0x5EED0006, 0, n)
+    ref = grouped.copy()
+    orc.hll_add(ref[5 * 16384:6 * 16384], ka, None, 16, 5000)
+    assert np.array_equal(_pool_regs(L, engine, h, G), ref)
+    _lib.check(L.rsk_hll_clear(h))
+    assert not _pool_regs(L, engine, h, G).any()
+    assert int(_count(L, h, [5])[0]) == 0
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    assert np.array_equal(_pool_regs(L, engine, h, G), grouped)
+    g.free()
+    k.free()
+    L.rsk_hll_destroy(h)
+
+
 def test_batched_merge_and_union_follow_redis_order(L, engine, orc):
     """rsk_hll_merge_batch == PFMERGE dst src issued in order (chains and
     read-after-write inside one batch); rsk_hll_count_union_batch == PFCOUNT a b."""
