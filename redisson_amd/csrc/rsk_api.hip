@@ -189,7 +189,8 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
 void check_hll(const rsk_hll* h, uint64_t id) {
   need(h != nullptr, "hll handle is NULL");
   need(id < h->n, "sketch id out of range");
-  h->zero = false;  // conservatively: every caller may write registers
+  rsk::hll_materialize(h);  // every caller reads or writes registers
+  h->zero = false;          // conservatively: every caller may write them
 }
 
 uint8_t* regs_of(rsk_hll* h, uint64_t id) { return h->d_regs + id * (uint64_t)HLL_REGS; }
@@ -273,6 +274,16 @@ FastMod63 make_fastmod(uint64_t d) {
 }
 
 }  // namespace
+
+namespace rsk {
+void hll_materialize(const rsk_hll* h) {
+  if (!h->pending_clear) return;
+  CtxLock l(h->ctx);
+  ProfScope ps(h->ctx, "hll_clear");
+  RSK_HIP(hipMemsetAsync(h->d_regs, 0, h->n * (uint64_t)HLL_REGS, h->ctx->stream));
+  h->pending_clear = false;
+}
+}  // namespace rsk
 
 extern "C" {
 
@@ -443,10 +454,11 @@ int rsk_hll_clear(rsk_hll* h) {
     CtxLock l(h->ctx);
     {
       ProfScope ps(h->ctx, "hll_clear");
-      RSK_HIP(hipMemsetAsync(h->d_regs, 0, h->n * (uint64_t)HLL_REGS, h->ctx->stream));
+      // registers: lazily (hll_materialize, or rewritten whole by the next grouped add)
       RSK_HIP(hipMemsetAsync(h->d_card, 0, h->n * 8, h->ctx->stream));
     }
     std::fill(h->exists.begin(), h->exists.end(), 0);
+    h->pending_clear = true;
     h->zero = true;
   });
 }
@@ -539,10 +551,10 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     need(keys == nullptr || keys->n == 0 || groups != nullptr, "groups is NULL");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    const bool pool_zero = h->zero;
-    h->zero = false;
     check_keys(keys);
     if (keys->n == 0) return;
+    const bool pool_zero = h->zero;
+    h->zero = false;
     uint32_t* d_groups = nullptr;
     if (keys->location == RSK_MEM_HOST) {
       for (uint64_t i = 0; i < keys->n; ++i)
@@ -555,7 +567,12 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
         d_groups = reinterpret_cast<uint32_t*>(out_scratch(c, cnt * 4));
         RSK_HIP(hipMemcpyAsync(d_groups, groups + first, cnt * 4, hipMemcpyHostToDevice, c->stream));
       }
-      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0);
+      // A pending lazy clear is completed by the partitioned add's first
+      // launch (every row written); any other path zeroes the pool first.
+      const bool write_all = h->pending_clear && hll_grouped_partition_applies(dk, h->n);
+      if (!write_all) hll_materialize(h);
+      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0, write_all);
+      h->pending_clear = false;
     });
     if (keys->location == RSK_MEM_DEVICE) {
       // Group ids stay on the device: every sketch of the pool is treated as
@@ -574,6 +591,7 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
     need(h != nullptr && out != nullptr, "NULL argument");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
+    hll_materialize(h);
     if (n == 0) return;
     uint64_t* d_ids = nullptr;
     SmallIds small{};
@@ -789,8 +807,14 @@ int rsk_hll_get_registers(rsk_hll* h, uint64_t id, uint8_t* out, uint32_t locati
   });
 }
 
-void* rsk_hll_device_registers(rsk_hll* h) {  // the caller may write through it
+void* rsk_hll_device_registers(rsk_hll* h) {  // the caller may read or write through it
   if (!h) return nullptr;
+  try {
+    rsk::hll_materialize(h);
+    RSK_HIP(hipStreamSynchronize(h->ctx->stream));
+  } catch (const RskError&) {
+    return nullptr;
+  }
   h->zero = false;
   return h->d_regs;
 }

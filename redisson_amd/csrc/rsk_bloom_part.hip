@@ -615,13 +615,13 @@ __global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restr
 __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
                                                           uint32_t nfine, uint64_t G, int pool_zero,
-                                                          uint8_t* __restrict__ regs) {
+                                                          int write_all, uint8_t* __restrict__ regs) {
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
   for (uint32_t w = blockIdx.x; w < GP_NP * nfine; w += gridDim.x) {
     const uint32_t s = w / GP_NP, half = w % GP_NP;
     const uint32_t a = off2[(uint64_t)s * G1], e = off2[(uint64_t)(s + 1) * G1];
     const uint64_t g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
-    if (a == e || g0 >= G) continue;  // uniform across the workgroup
+    if ((a == e && !write_all) || g0 >= G) continue;  // uniform across the workgroup
     const uint32_t nsk = (uint32_t)(G - g0 < GP_SK ? G - g0 : GP_SK);
     const uint32_t n4 = nsk * (HLL_REGS / 16);
     uint4* gp = reinterpret_cast<uint4*>(regs + g0 * HLL_REGS);
@@ -666,14 +666,21 @@ static int gpart_mode() {
   return e[0] == '0' ? 0 : 1;
 }
 
-bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
-                                 uint64_t G, bool pool_zero) {
+bool hll_grouped_partition_applies(const DevKeys& keys, uint64_t G) {
   const int mode = gpart_mode();
   const bool f16 =
       keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
   if (mode == 0 || !f16 || keys.n == 0 || G == 0 || G > (1ull << (GP_BIN_SHIFT + 8))) return false;
   // auto: large batches dense enough that reading + writing each touched sketch once pays
   if (mode < 0 && (keys.n < (1ull << 22) || keys.n < 16 * G)) return false;
+  return true;
+}
+
+// write_all (a pending lazy clear, pool_zero too): hll_gapply writes every
+// row of the pool, zero rows for sketches without records.
+bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
+                                 uint64_t G, bool pool_zero, bool write_all) {
+  if (!hll_grouped_partition_applies(keys, G)) return false;
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
   const uint32_t cus = (uint32_t)c->num_cus;
@@ -727,7 +734,8 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       const uint32_t per_cu = (160u * 1024) / (GP_SK * HLL_REGS + 1024);  // workgroups resident per CU
       hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, 2 * per_cu * cus)), dim3(GP_T), 0,
                          c->stream,
-                         buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0, d_regs);
+                         buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0,
+                         (write_all && first == 0) ? 1 : 0, d_regs);
       RSK_CHECK_LAUNCH("hll_gapply");
     }
   }

@@ -179,6 +179,7 @@ int rsk_comm_destroy(rsk_ctx* c) {
 int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
   return guarded([&] {
     need(h && id < h->n, "bad sketch");
+    rsk::hll_materialize(h);
     h->zero = false;
     rsk_ctx* c = h->ctx;
     Lock l(c);
@@ -198,6 +199,7 @@ int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
 int rsk_hll_allreduce_pool(rsk_hll* h) {
   return guarded([&] {
     need(h != nullptr, "bad pool");
+    rsk::hll_materialize(h);
     h->zero = false;
     rsk_ctx* c = h->ctx;
     Lock l(c);
@@ -217,6 +219,7 @@ int rsk_hll_allreduce_pool(rsk_hll* h) {
 int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_out) {
   return guarded([&] {
     need(h && first_out && count_out, "NULL argument");
+    rsk::hll_materialize(h);
     h->zero = false;
     rsk_ctx* c = h->ctx;
     Lock l(c);
@@ -243,6 +246,7 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
 int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) {
   return guarded([&] {
     need(h && (ids || n == 0), "NULL argument");
+    rsk::hll_materialize(h);
     h->zero = false;
     rsk_ctx* c = h->ctx;
     Lock l(c);

@@ -655,9 +655,9 @@ __global__ __launch_bounds__(256) void hll_add_grouped_bytes_kernel(const uint8_
 }
 
 void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
-                            bool pool_zero) {
+                            bool pool_zero, bool write_all) {
   if (k.n == 0) return;
-  if (hll_add_grouped_partitioned(c, k, d_groups, d_regs, G, pool_zero)) return;  // large batches: per-sketch LDS updates
+  if (hll_add_grouped_partitioned(c, k, d_groups, d_regs, G, pool_zero, write_all)) return;  // large batches: per-sketch LDS updates
   uint64_t blocks = (k.n + 255) / 256;
   uint64_t cap = (uint64_t)c->num_cus * 16;
   if (blocks > cap) blocks = cap;

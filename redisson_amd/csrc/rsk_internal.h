@@ -101,6 +101,10 @@ struct rsk_hll {
   // entry point that may write registers): the grouped add then skips
   // reading the pool.
   mutable bool zero = false;
+  // rsk_hll_clear is lazy: the registers are zeroed by the next grouped add
+  // that rewrites every row anyway (hll_gapply with write_all), or by
+  // hll_materialize before any other access.
+  mutable bool pending_clear = false;
   // rsk_hll_merge_batch leveling state per sketch id (valid while stamp == lv_epoch)
   std::vector<uint32_t> lv_stamp, lv_w, lv_r;
   uint32_t lv_epoch = 0;
@@ -144,7 +148,7 @@ struct DevKeys {
 void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64_t* d_card, uint32_t* d_flag,
                     uint32_t epoch, bool created);
 void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
-                            bool pool_zero = false);
+                            bool pool_zero = false, bool write_all = false);
 // Up to 8 sketch ids passed by value (saves a host->device copy per PFCOUNT).
 struct SmallIds {
   uint64_t v[8];
@@ -169,8 +173,11 @@ void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
 // batch is not worth it (or not 16-byte keys): use the direct kernel.
+bool hll_grouped_partition_applies(const DevKeys& k, uint64_t G);
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
-                                 bool pool_zero);
+                                 bool pool_zero, bool write_all);
+// Performs a pending lazy clear (rsk_api.hip).
+void hll_materialize(const rsk_hll* h);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);

@@ -344,8 +344,19 @@ def test_grouped_partitioned_pool_state_after_other_writers(L, engine, orc, monk
     assert int(_count(L, h, [5])[0]) == 0
     _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
     assert np.array_equal(_pool_regs(L, engine, h, G), grouped)
-    g.free()
-    k.free()
+    # lazy clear completed by the grouped add itself: pairs only for sketches
+    # 0..19, so rows 20..63 (full before the clear) must come back zero
+    _lib.check(L.rsk_hll_clear(h))
+    g2, k2 = devmem.gen_grouped(engine, 0x5EED0206, 20, 0, 100_000)
+    ks2 = k2.keys_fixed(100_000, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks2), g2.ptr))
+    ref2 = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped(ref2[:20 * 16384], 20, 0x5EED0206, 0, 100_000)
+    assert np.array_equal(_pool_regs(L, engine, h, G), ref2)
+    cnt = _count(L, h, list(range(G)))
+    assert cnt[20:].tolist() == [0] * (G - 20) and all(int(x) > 0 for x in cnt[:20])
+    for b in (g, k, g2, k2):
+        b.free()
     L.rsk_hll_destroy(h)
 
 
