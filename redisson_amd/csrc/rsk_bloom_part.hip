@@ -536,7 +536,10 @@ constexpr uint32_t GP_SK = RSK_GP_SK;  // sketches per gapply workgroup (GP_SK x
 constexpr uint32_t GP_NP = 16 / GP_SK; // gapply parts per fine bin (each reads the bin's records)
 constexpr int GP_U = 4;                // record loads in flight per gapply lane
 constexpr uint32_t GP_T = 1024;        // gcount / gapply workgroup
-constexpr uint32_t GP_TILE = 4096;     // records per gpart1 tile
+#ifndef RSK_GP_TILE
+#define RSK_GP_TILE 8192
+#endif
+constexpr uint32_t GP_TILE = RSK_GP_TILE;  // records per gpart1 tile
 constexpr int GP_E = GP_TILE / PT;
 constexpr uint32_t GP_GU = 8;          // gpart1 blocks per part2 unit (G1 is a multiple)
 
@@ -684,8 +687,10 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t G1 = 2 * GP_GU * ((cus + GP_GU - 1) / GP_GU);  // gcount / gpart1 blocks, multiple of GP_GU
-  const uint32_t p2_grid = 4 * cus;
+  const uint32_t GU = std::max<uint32_t>(1, env_u32("RSK_HLL_GPART_GU", GP_GU));  // part1 blocks per part2 unit
+  const uint32_t gpc = std::max<uint32_t>(1, env_u32("RSK_HLL_GPART_G", 2));     // gcount / gpart1 blocks per CU
+  const uint32_t G1 = GU * ((gpc * cus + GU - 1) / GU);                          // a multiple of GU
+  const uint32_t p2_grid = std::max<uint32_t>(1, env_u32("RSK_HLL_GPART_P2", 4)) * cus;
   const uint64_t chunk = PROBE_CAP;
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
   const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)nfine * G1 + 1;
@@ -725,8 +730,8 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       hipLaunchKernelGGL(hll_gcount2_kernel, dim3(nbins1 * G1), dim3(PT), 0, c->stream, buf_a, off1, G1, cnt2);
       RSK_CHECK_LAUNCH("hll_gcount2");
       RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, off2, (int)ncnt2, c->stream));
-      hipLaunchKernelGGL(bloom_part2_kernel, dim3(p2_grid), dim3(PT), 0, c->stream, buf_a, off1, off2, G1, GP_GU,
-                         nbins1 * (G1 / GP_GU), 8u, nfine, 24u, 0xFFFFFFFFu, buf_b);
+      hipLaunchKernelGGL(bloom_part2_kernel, dim3(p2_grid), dim3(PT), 0, c->stream, buf_a, off1, off2, G1, GU,
+                         nbins1 * (G1 / GU), 8u, nfine, 24u, 0xFFFFFFFFu, buf_b);
       RSK_CHECK_LAUNCH("hll_gpart2");
     }
     {
