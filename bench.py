@@ -58,7 +58,7 @@ def pcie_inclusive(client, keys_host):
     dt = time.perf_counter() - t0
     n = kb.n
     return {"value": n / dt, "unit": "keys/s", "GBps_host_to_hbm": 16 * n / dt / 1e9,
-            "sample": "%d C2 16-byte keys in pageable host memory, one addAll (256 MiB staging chunks)" % n}
+            "sample": "%d C2 16-byte keys in pageable host memory, one addAll (256 MiB chunks through two pinned host stages)" % n}
 
 
 def cpu_baseline(sample_keys: int, passes: int, threads: int):

@@ -10,6 +10,9 @@
 #include <cstring>
 #include <memory>
 #include <new>
+#include <thread>
+#include <vector>
+#include <cstdlib>
 #include <unordered_map>
 
 #include "rsk_internal.h"
@@ -141,8 +144,64 @@ void check_keys(const rsk_keys* k) {
   need(k->n == 0 || k->data != nullptr || (k->offsets == nullptr && k->fixed_len == 0), "keys.data is NULL");
 }
 
+// Host batches go through two pinned host stages: host threads fill one
+// (par_copy) while the DMA of the other runs, so the pageable user buffer is
+// read at memcpy speed and the link carries pinned transfers.  Each stage has
+// its own device twin, so chunk i+1's DMA may queue behind chunk i's kernels
+// without a host wait.  RSK_STAGE_THREADS (default 8) sets the copy threads.
+unsigned stage_threads() {
+  static const unsigned n = [] {
+    const char* e = std::getenv("RSK_STAGE_THREADS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 8;
+    return (unsigned)std::max<long>(1, std::min<long>(v, 64));
+  }();
+  return n;
+}
+
+void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  const uint64_t min_piece = 8ull << 20;
+  const unsigned nt = (unsigned)std::min<uint64_t>(stage_threads(), n / min_piece);
+  if (nt <= 1) {
+    if (n) std::memcpy(dst, src, n);
+    return;
+  }
+  const uint64_t piece = ((n + nt - 1) / nt + 4095) & ~uint64_t(4095);
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (unsigned t = 1; t < nt; ++t) {
+    const uint64_t lo = std::min<uint64_t>(n, (uint64_t)t * piece), hi = std::min<uint64_t>(n, lo + piece);
+    if (hi > lo) th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
+  }
+  std::memcpy(dst, src, std::min<uint64_t>(n, piece));
+  for (auto& x : th) x.join();
+}
+
+// Allocates the pinned stages once per context; on failure the context
+// copies from the pageable source instead (pin_off).
+void ensure_pinned(rsk_ctx* c) {
+  if (c->pin_off || c->h_pin[0]) return;
+  const uint64_t bytes = c->stage_bytes + c->stage_bytes / 4;
+  bool ok = hipHostMalloc(&c->h_pin[0], bytes, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(&c->h_pin[1], bytes, hipHostMallocDefault) == hipSuccess &&
+            hipMalloc(&c->d_pin[1], bytes) == hipSuccess &&
+            hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    for (int b = 0; b < 2; ++b) {
+      if (c->h_pin[b]) (void)hipHostFree(c->h_pin[b]);
+      if (c->d_pin[b]) (void)hipFree(c->d_pin[b]);
+      if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
+      c->h_pin[b] = c->d_pin[b] = nullptr;
+      c->pin_ev[b] = nullptr;
+    }
+    c->pin_off = true;
+  }
+}
+
 // Calls fn(dev_keys, first_index, count) over the batch; host batches are
-// copied through the staging buffers in whole-key chunks.
+// copied through the staging buffers in whole-key chunks.  On return every
+// chunk's work has completed.
 template <class F>
 void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
   check_keys(k);
@@ -152,19 +211,38 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
     return;
   }
   ensure_stage(c);
-  uint8_t* d_data = c->d_stage;
-  uint64_t* d_offs = reinterpret_cast<uint64_t*>(c->d_stage + c->stage_bytes);
+  ensure_pinned(c);
+  const bool pinned = !c->pin_off;
+  uint8_t* const dbuf[2] = {c->d_stage, pinned ? c->d_pin[1] : c->d_stage};
   const uint64_t off_cap = c->stage_bytes / 4 / 8 - 1;  // keys per chunk (offsets)
   const uint8_t* src = reinterpret_cast<const uint8_t*>(k->data);
+  // One host->device copy of a chunk's bytes: through the free pinned stage,
+  // or straight from the source when the context has none.
+  auto h2d = [&](int slot, uint64_t at, const void* from, uint64_t bytes) {
+    if (!bytes) return;
+    if (pinned) {
+      par_copy(c->h_pin[slot] + at, reinterpret_cast<const uint8_t*>(from), bytes);
+      RSK_HIP(hipMemcpyAsync(dbuf[slot] + at, c->h_pin[slot] + at, bytes, hipMemcpyHostToDevice, c->stream));
+    } else {
+      RSK_HIP(hipMemcpyAsync(dbuf[slot] + at, from, bytes, hipMemcpyHostToDevice, c->stream));
+    }
+  };
   uint64_t first = 0;
+  int slot = 0;
+  bool recorded[2] = {false, false};  // earlier calls ended with a stream sync
   while (first < k->n) {
+    // The pinned stage is free once the DMA that last read it has finished.
+    if (pinned && recorded[slot]) RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));
+    uint8_t* d_data = dbuf[slot];
+    uint64_t* d_offs = reinterpret_cast<uint64_t*>(d_data + c->stage_bytes);
     uint64_t m;
     if (k->offsets == nullptr) {
       m = k->fixed_len ? c->stage_bytes / k->fixed_len : k->n;
       m = std::min<uint64_t>(m, k->n - first);
       need(m > 0, "key longer than the staging buffer");
-      if (k->fixed_len) RSK_HIP(hipMemcpyAsync(d_data, src + first * k->fixed_len, m * k->fixed_len,
-                                              hipMemcpyHostToDevice, c->stream));
+      if (k->fixed_len) h2d(slot, 0, src + first * k->fixed_len, m * k->fixed_len);
+      if (pinned) RSK_HIP(hipEventRecord(c->pin_ev[slot], c->stream));
+      recorded[slot] = pinned;
       fn(DevKeys{d_data, nullptr, m, k->fixed_len}, first, m);
     } else {
       const uint64_t base = k->offsets[first];
@@ -174,16 +252,20 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
       m = (uint64_t)(std::upper_bound(o + 1, o + lim + 1, base + c->stage_bytes) - (o + 1));
       need(m > 0, "key longer than the staging buffer");
       need(k->offsets[first + m] >= base, "offsets must be non-decreasing");
-      RSK_HIP(hipMemcpyAsync(d_offs, k->offsets + first, (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
-      if (k->offsets[first + m] > base)
-        RSK_HIP(hipMemcpyAsync(d_data, src + base, k->offsets[first + m] - base, hipMemcpyHostToDevice, c->stream));
+      h2d(slot, c->stage_bytes, k->offsets + first, (m + 1) * 8);
+      h2d(slot, 0, src + base, k->offsets[first + m] - base);
+      if (pinned) RSK_HIP(hipEventRecord(c->pin_ev[slot], c->stream));
+      recorded[slot] = pinned;
       // Offsets stay absolute: shift the data pointer instead of rebasing.
       fn(DevKeys{d_data - base, d_offs, m, 0}, first, m);
     }
-    // The staging buffer is reused by the next chunk.
-    RSK_HIP(hipStreamSynchronize(c->stream));
+    // Without pinned stages the single device stage is reused by the next
+    // chunk (and the pageable copy is host-synchronous anyway).
+    if (!pinned) RSK_HIP(hipStreamSynchronize(c->stream));
     first += m;
+    slot ^= 1;
   }
+  RSK_HIP(hipStreamSynchronize(c->stream));
 }
 
 void check_hll(const rsk_hll* h, uint64_t id) {
@@ -339,6 +421,11 @@ int rsk_shutdown(rsk_ctx* c) {
     rsk::prof_fold(c);
     for (auto e : c->prof.free_events) (void)hipEventDestroy(e);
     (void)hipFree(c->d_stage);
+    for (int b = 0; b < 2; ++b) {
+      (void)hipHostFree(c->h_pin[b]);
+      (void)hipFree(c->d_pin[b]);
+      if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
+    }
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_small);
     (void)hipHostFree(c->h_small);

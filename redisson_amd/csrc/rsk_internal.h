@@ -68,6 +68,13 @@ struct rsk_ctx {
   // host -> device staging for RSK_MEM_HOST key batches
   uint8_t* d_stage = nullptr;
   uint64_t stage_bytes = 0;
+  // double-buffered pinned host stages (filled by host threads while the
+  // previous chunk's DMA runs), their device twins and "DMA done" events;
+  // pin_off: pinned allocation failed, copy from the pageable source
+  uint8_t* h_pin[2] = {nullptr, nullptr};
+  uint8_t* d_pin[2] = {nullptr, nullptr};
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  bool pin_off = false;
   // per-workgroup partial register files [slabs][16384] u8
   uint8_t* d_slab = nullptr;
   uint32_t slab_count = 0;
