@@ -138,10 +138,33 @@ void ensure_stage(rsk_ctx* c) {
   if (!c->d_stage) RSK_HIP(hipMalloc(&c->d_stage, c->stage_bytes + c->stage_bytes / 4));
 }
 
+// A pointer a kernel will dereference must be one the GPU can reach (device,
+// managed or registered/pinned host memory); a pageable host pointer passed
+// as RSK_MEM_DEVICE is rejected here instead of faulting the device.
+void need_gpu_ptr(const void* p, const char* msg) {
+  if (!p) return;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    fail(RSK_ERR_INVALID_ARG, msg);
+  }
+  if (a.type == hipMemoryTypeUnregistered) fail(RSK_ERR_INVALID_ARG, msg);
+}
+
 void check_keys(const rsk_keys* k) {
   need(k != nullptr, "keys is NULL");
   need(k->location == RSK_MEM_HOST || k->location == RSK_MEM_DEVICE, "keys.location must be RSK_MEM_HOST or RSK_MEM_DEVICE");
   need(k->n == 0 || k->data != nullptr || (k->offsets == nullptr && k->fixed_len == 0), "keys.data is NULL");
+  if (k->location == RSK_MEM_DEVICE && k->n > 0) {
+    need_gpu_ptr(k->data, "keys.data is not GPU-accessible memory (location RSK_MEM_DEVICE)");
+    need_gpu_ptr(k->offsets, "keys.offsets is not GPU-accessible memory (location RSK_MEM_DEVICE)");
+  }
+}
+
+// Per-key outputs follow the keys' location.
+void check_out(const rsk_keys* k, const void* out) {
+  if (k->location == RSK_MEM_DEVICE && k->n > 0)
+    need_gpu_ptr(out, "output is not GPU-accessible memory (keys are RSK_MEM_DEVICE)");
 }
 
 // Host batches go through two pinned host stages: host threads fill one
@@ -588,8 +611,9 @@ int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     bool created;
-    create_if_missing(h, id, &created);
     check_keys(keys);
+    check_out(keys, out);
+    create_if_missing(h, id, &created);
     // Sub-chunks bounded for the 32-bit sort; replies compose sequentially.
     const uint64_t max_chunk = 1ull << 26;
     rsk_keys sub = *keys;
@@ -640,6 +664,7 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     CtxLock l(c);
     check_keys(keys);
     if (keys->n == 0) return;
+    check_out(keys, groups);
     const bool pool_zero = h->zero;
     h->zero = false;
     uint32_t* d_groups = nullptr;
@@ -1068,6 +1093,7 @@ int rsk_bloom_add(rsk_bloom* b, const rsk_keys* keys, uint8_t* added_out) {
     rsk_ctx* c = b->ctx;
     CtxLock l(c);
     check_keys(keys);
+    check_out(keys, added_out);
     if (!added_out) {
       for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { bloom_add_launch(c, b, dk); });
       return;
@@ -1103,6 +1129,8 @@ int rsk_bloom_contains(rsk_bloom* b, const rsk_keys* keys, uint8_t* out) {
     need(b != nullptr && out != nullptr, "NULL argument");
     rsk_ctx* c = b->ctx;
     CtxLock l(c);
+    check_keys(keys);
+    check_out(keys, out);
     for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
       if (keys->location == RSK_MEM_DEVICE) {
         bloom_contains_launch(c, b, dk, out + first);
@@ -1121,6 +1149,7 @@ int rsk_hash_to_base64(rsk_ctx* c, const rsk_keys* keys, char* out) {
     need(c != nullptr, "ctx is NULL");
     check_keys(keys);
     need(keys->n == 0 || out != nullptr, "out is NULL");
+    check_out(keys, out);
     CtxLock l(c);
     for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
       if (keys->location == RSK_MEM_DEVICE) {

@@ -908,8 +908,10 @@ void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* con
 // ------------------------------------------- PFADD one element at a time
 // Element i replies 1 iff rank_i > max(reg0[idx_i], ranks of earlier
 // elements with the same index).  Elements are radix-sorted by register
-// index (stable, so input order survives inside a register), then one lane
-// per register walks its run.
+// index (stable, so input order survives inside a register); the "earlier
+// ranks" term is then an exclusive segmented max-scan over the sorted ranks
+// (rocprim scan-by-key), so a register hit by many elements (a skewed or
+// duplicate-heavy batch) costs no more than one spread over all registers.
 __global__ void hll_each_hash_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
                                      uint32_t fixed_len, uint64_t n, uint32_t* __restrict__ key_idx,
                                      uint32_t* __restrict__ seq, uint8_t* __restrict__ rank) {
@@ -923,28 +925,31 @@ __global__ void hll_each_hash_kernel(const uint8_t* __restrict__ data, const uin
   }
 }
 
-__global__ void hll_each_bounds_kernel(const uint32_t* __restrict__ sorted_idx, uint64_t n,
-                                       uint32_t* __restrict__ run_start) {
+__global__ void hll_each_gather_kernel(const uint32_t* __restrict__ sorted_seq, const uint8_t* __restrict__ rank,
+                                       uint64_t n, uint32_t* __restrict__ sorted_rank) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x)
+    sorted_rank[p] = rank[sorted_seq[p]];
+}
+
+// Replies in input order; the last element of each run leaves the register's
+// new value in next_reg (regs itself is only read here).
+__global__ void hll_each_reply_kernel(const uint32_t* __restrict__ sorted_idx, const uint32_t* __restrict__ sorted_seq,
+                                      const uint32_t* __restrict__ sorted_rank, const uint32_t* __restrict__ prefix,
+                                      uint64_t n, const uint8_t* __restrict__ regs, uint8_t* __restrict__ out,
+                                      uint32_t* __restrict__ next_reg) {
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
-    if (p == 0 || sorted_idx[p] != sorted_idx[p - 1]) run_start[sorted_idx[p]] = (uint32_t)p;
+    const uint32_t r = sorted_idx[p];
+    const uint32_t base = regs[r];
+    const uint32_t pre = prefix[p] > base ? prefix[p] : base;
+    const uint32_t c = sorted_rank[p];
+    out[sorted_seq[p]] = c > pre;
+    if (p + 1 == n || sorted_idx[p + 1] != r) next_reg[r] = c > pre ? c : pre;
   }
 }
 
-__global__ void hll_each_walk_kernel(const uint32_t* __restrict__ sorted_idx, const uint32_t* __restrict__ sorted_seq,
-                                     const uint8_t* __restrict__ rank, const uint32_t* __restrict__ run_start,
-                                     uint64_t n, uint8_t* __restrict__ regs, uint8_t* __restrict__ out) {
+__global__ void hll_each_store_kernel(const uint32_t* __restrict__ next_reg, uint8_t* __restrict__ regs) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= HLL_REGS) return;
-  uint32_t p = run_start[r];
-  if (p == 0xFFFFFFFFu) return;
-  uint32_t running = regs[r];
-  for (; p < n && sorted_idx[p] == r; ++p) {
-    uint32_t i = sorted_seq[p];
-    uint32_t c = rank[i];
-    out[i] = c > running;
-    running = c > running ? c : running;
-  }
-  regs[r] = (uint8_t)running;
+  if (r < HLL_REGS && next_reg[r] != 0xFFFFFFFFu) regs[r] = (uint8_t)next_reg[r];
 }
 
 void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out) {
@@ -952,9 +957,13 @@ void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_ske
   uint8_t* regs = const_cast<uint8_t*>(d_regs_sketch);
   const uint64_t n = k.n;
   if (n == 0) return;
-  size_t tmp_bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (uint32_t*)nullptr, (int)n, 0, HLL_P, c->stream);
+  size_t sort_bytes = 0, scan_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, HLL_P, c->stream);
+  (void)hipcub::DeviceScan::ExclusiveScanByKey(nullptr, scan_bytes, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                               (uint32_t*)nullptr, hipcub::Max(), 0u, (uint32_t)n,
+                                               hipcub::Equality(), c->stream);
+  size_t tmp_bytes = std::max(sort_bytes, scan_bytes);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   uint64_t need = 4 * al(n * 4) + al(n) + al(HLL_REGS * 4) + al(tmp_bytes);
   uint8_t* w = c->work(need);
@@ -963,22 +972,32 @@ void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_ske
   uint32_t* seq_in = reinterpret_cast<uint32_t*>(w + 2 * al(n * 4));
   uint32_t* seq_out = reinterpret_cast<uint32_t*>(w + 3 * al(n * 4));
   uint8_t* rank = w + 4 * al(n * 4);
-  uint32_t* run_start = reinterpret_cast<uint32_t*>(w + 4 * al(n * 4) + al(n));
+  uint32_t* next_reg = reinterpret_cast<uint32_t*>(w + 4 * al(n * 4) + al(n));
   void* tmp = w + 4 * al(n * 4) + al(n) + al(HLL_REGS * 4);
+  // After the sort the unsorted key/seq arrays are free: sorted ranks and
+  // the scan's output reuse them.
+  uint32_t* sorted_rank = idx_in;
+  uint32_t* prefix = seq_in;
   uint64_t grid = (n + 255) / 256;
   if (grid > 4096) grid = 4096;
   ProfScope ps(c, "hll_add_each");
   hipLaunchKernelGGL(hll_each_hash_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, k.data, k.offsets,
                      k.fixed_len, n, idx_in, seq_in, rank);
   RSK_CHECK_LAUNCH("hll_each_hash");
-  RSK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, idx_in, idx_out, seq_in, seq_out, (int)n, 0, HLL_P,
+  RSK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, idx_in, idx_out, seq_in, seq_out, (int)n, 0, HLL_P,
                                              c->stream));
-  RSK_HIP(hipMemsetAsync(run_start, 0xFF, HLL_REGS * 4, c->stream));
-  hipLaunchKernelGGL(hll_each_bounds_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, idx_out, n, run_start);
-  RSK_CHECK_LAUNCH("hll_each_bounds");
-  hipLaunchKernelGGL(hll_each_walk_kernel, dim3(HLL_REGS / 256), dim3(256), 0, c->stream, idx_out, seq_out, rank,
-                     run_start, n, regs, d_out);
-  RSK_CHECK_LAUNCH("hll_each_walk");
+  hipLaunchKernelGGL(hll_each_gather_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, seq_out, rank, n,
+                     sorted_rank);
+  RSK_CHECK_LAUNCH("hll_each_gather");
+  RSK_HIP(hipcub::DeviceScan::ExclusiveScanByKey(tmp, scan_bytes, (const uint32_t*)idx_out,
+                                                 (const uint32_t*)sorted_rank, prefix, hipcub::Max(), 0u, (uint32_t)n,
+                                                 hipcub::Equality(), c->stream));
+  RSK_HIP(hipMemsetAsync(next_reg, 0xFF, HLL_REGS * 4, c->stream));
+  hipLaunchKernelGGL(hll_each_reply_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, idx_out, seq_out,
+                     sorted_rank, prefix, n, regs, d_out, next_reg);
+  RSK_CHECK_LAUNCH("hll_each_reply");
+  hipLaunchKernelGGL(hll_each_store_kernel, dim3(HLL_REGS / 256), dim3(256), 0, c->stream, next_reg, regs);
+  RSK_CHECK_LAUNCH("hll_each_store");
 }
 
 }  // namespace rsk

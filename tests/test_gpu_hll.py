@@ -454,3 +454,77 @@ def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
     cnt = _count(L, h, list(range(gs)))
     assert [int(c) for c in cnt[:64]] == [orc.hll_count_dense(ref[i]) for i in range(64)]
     L.rsk_hll_destroy(h)
+
+
+def _add_each(L, h, kb, i=0):
+    from redisson_amd import _lib
+
+    out = np.zeros(kb.n, np.uint8)
+    ks = kb.as_struct()
+    _lib.check(L.rsk_hll_add_each(h, i, ctypes.byref(ks), out.ctypes.data))
+    return out
+
+
+def test_add_each_skewed_runs(L, engine, orc):
+    """Duplicate-heavy batches: one register's run spans many scan tiles."""
+    from redisson_amd import KeyBatch
+
+    # sequential Redis model on a small skewed batch (4 hot keys, 80 % of it)
+    rng = np.random.default_rng(12)
+    hot = [rng.integers(0, 256, 9, dtype=np.uint8).tobytes() for _ in range(4)]
+    cold = [rng.integers(0, 256, 9, dtype=np.uint8).tobytes() for _ in range(6000)]
+    keys = [hot[j] for j in rng.integers(0, 4, 24000)] + cold
+    order = rng.permutation(len(keys))
+    keys = [keys[j] for j in order]
+    r = orc.RedisModel()
+    want = [r.pfadd("k", e) for e in keys]
+    h = _pool(L, engine)
+    assert _add_each(L, h, KeyBatch.from_bytes_list(keys)).tolist() == want
+    _, raw, _ = orc.hll_decode(r.get("k"))
+    assert np.array_equal(_regs(L, h), raw)
+    # 3M copies of one key: only the first can reply 1
+    one = np.tile(orc.gen_keys16(SEED_C2, 5, 1), 3_000_000)
+    h2 = _pool(L, engine)
+    out = _add_each(L, h2, KeyBatch.from_numpy(one.reshape(-1, 16)))
+    assert out[0] == 1 and int(out[1:].sum()) == 0
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, one[:16], None, 16, 1)
+    assert np.array_equal(_regs(L, h2), ref)
+    # 1M distinct keys four times over: passes 2-4 reply 0, pass 1 replies as a
+    # fresh sketch does, registers as the oracle's
+    n = 1 << 20
+    k1 = orc.gen_keys16(SEED_C2, 0, n)
+    h3, h4 = _pool(L, engine), _pool(L, engine)
+    first = _add_each(L, h3, KeyBatch.from_numpy(k1.reshape(n, 16)))
+    out4 = _add_each(L, h4, KeyBatch.from_numpy(np.tile(k1, 4).reshape(4 * n, 16)))
+    assert np.array_equal(out4[:n], first) and int(out4[n:].sum()) == 0
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, k1, None, 16, n)
+    assert np.array_equal(_regs(L, h4), ref) and np.array_equal(_regs(L, h3), ref)
+
+
+def test_device_batch_with_host_output_is_rejected(L, engine, orc):
+    """A pageable host pointer where the GPU would write (keys RSK_MEM_DEVICE)
+    is refused with RSK_ERR_INVALID_ARG before any kernel runs."""
+    from redisson_amd import _lib, devmem
+
+    n = 1000
+    t = devmem.gen_keys16(engine, SEED_C2, 0, n)
+    ks = t.keys_fixed(n, 16).as_struct()
+    host_out = np.zeros(n, np.uint8)
+    h = _pool(L, engine)
+    assert L.rsk_hll_add_each(h, 0, ctypes.byref(ks), host_out.ctypes.data) == _lib.RSK_ERR_INVALID_ARG
+    b = ctypes.c_void_p()
+    _lib.check(L.rsk_bloom_create(engine.ctx, 100000, 3, ctypes.byref(b)))
+    assert L.rsk_bloom_contains(b, ctypes.byref(ks), host_out.ctypes.data) == _lib.RSK_ERR_INVALID_ARG
+    assert L.rsk_bloom_add(b, ctypes.byref(ks), host_out.ctypes.data) == _lib.RSK_ERR_INVALID_ARG
+    # host keys flagged as device-resident are refused too
+    hk = orc.gen_keys16(SEED_C2, 0, n)
+    bad = _lib.rsk_keys()
+    bad.data, bad.offsets, bad.n, bad.fixed_len, bad.location = hk.ctypes.data, None, n, 16, _lib.RSK_MEM_DEVICE
+    assert L.rsk_hll_add(h, 0, ctypes.byref(bad), None) == _lib.RSK_ERR_INVALID_ARG
+    # and the context still works
+    dout = devmem.DeviceBuffer.from_numpy(engine, np.zeros(n, np.uint8))
+    _lib.check(L.rsk_bloom_contains(b, ctypes.byref(ks), dout.ptr))
+    L.rsk_bloom_destroy(b)
+    L.rsk_hll_destroy(h)
