@@ -14,8 +14,12 @@
  *    (thread-local).  Status codes map 1:1 to the Java exceptions the
  *    reference raises (see enum).  No C++ exception crosses this boundary.
  *  - The caller owns all buffers passed in.  Key buffers live either in host
- *    memory (RSK_MEM_HOST; copied over PCIe through a staging ring) or in
- *    device memory of the context's GPU (RSK_MEM_DEVICE; read in place).
+ *    memory (RSK_MEM_HOST; copied over PCIe through two pinned host stages,
+ *    filled by host threads -- RSK_STAGE_THREADS, default 8 -- while the
+ *    other stage's DMA runs) or in device memory of the context's GPU
+ *    (RSK_MEM_DEVICE; read in place).  Per-key outputs follow the keys'
+ *    location; a RSK_MEM_DEVICE key or output pointer the GPU cannot reach
+ *    (pageable host memory) is refused with RSK_ERR_INVALID_ARG.
  *  - The library owns device state behind opaque handles.  Calls on one
  *    context are serialised on that context's HIP stream; results written to
  *    host pointers are complete when the call returns.
@@ -56,7 +60,8 @@ typedef struct rsk_bloom rsk_bloom;
 typedef struct rsk_options {
   int32_t device;         /* HIP device ordinal (one process per GPU) */
   int32_t redis_version;  /* 320 = Redis 3.2.0 semantics (only supported value) */
-  uint64_t staging_bytes; /* host->device staging ring size; 0 = default (256 MiB) */
+  uint64_t staging_bytes; /* bytes per host->device chunk (each of the two pinned
+                             stages holds one chunk + its offsets); 0 = default (256 MiB) */
 } rsk_options;
 
 /* A batch of keys: fixed stride (offsets == NULL, each key fixed_len bytes)
