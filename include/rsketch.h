@@ -265,9 +265,34 @@ int rsk_hll_reducescatter_pool(rsk_hll *h, uint64_t *first, uint64_t *count);
  * rows sent back and scattered into the pool.  The fetched rows are a
  * snapshot (caches invalidated); writes to them stay local. */
 int rsk_hll_fetch_rows(rsk_hll *h, const uint64_t *ids, uint64_t n);
+/* rsk_hll_fetch_rows with flags.  RSK_FETCH_SELF also routes the ids this rank
+ * owns through the exchange (the rank gathers, sends to itself, receives and
+ * scatters them): a no-op on the data that runs every exchange kernel on one
+ * GPU (tests).  Argument errors on any rank (an id outside the pool) are
+ * agreed on by all ranks before any row moves: every rank returns
+ * RSK_ERR_INVALID_ARG and no rank is left waiting in a collective. */
+#define RSK_FETCH_SELF 1u
+int rsk_hll_fetch_rows_flags(rsk_hll *h, const uint64_t *ids, uint64_t n, uint32_t flags);
 /* Bloom bit string := OR over all ranks.  RCCL has no bitwise-OR reduction:
- * all-to-all of 1/N slices, local OR, all-gather. */
+ * all-to-all of 1/N slices, local OR, all-gather (also at N = 1, where the
+ * rank exchanges with itself). */
 int rsk_bloom_allreduce_or(rsk_bloom *b);
+
+/* ------------------------------------------------------- exchange plans */
+/* The host arithmetic the collectives above run (no GPU needed; exported so
+ * the N > 1 plans are testable on CPU against redisson_amd/shard.py). */
+/* Contiguous key-stream shard of rank `rank`: [*begin, *end). */
+int rsk_plan_shard_range(uint64_t n, int world, int rank, uint64_t *begin, uint64_t *end);
+/* Sketches owned after rsk_hll_reducescatter_pool. */
+int rsk_plan_owned_range(uint64_t n, int nranks, int rank, uint64_t *first, uint64_t *count);
+int rsk_plan_owner(uint64_t n, int nranks, uint64_t id, int *owner);
+/* Words per rank of the Bloom slice-OR. */
+int rsk_plan_bloom_slice_words(uint64_t nwords, int nranks, uint64_t *words);
+/* rsk_hll_fetch_rows request plan: want_out (capacity n_ids) gets the
+ * distinct requested ids ascending, counts_out[nranks] the rows asked of each
+ * owner.  RSK_ERR_INVALID_ARG if an id is >= n. */
+int rsk_plan_fetch(uint64_t n, int nranks, int rank, const uint64_t *ids, uint64_t n_ids, uint32_t flags,
+                   uint64_t *want_out, uint64_t *n_want, uint64_t *counts_out);
 
 /* --------------------------------------------------------- diagnostics */
 /* Memory-system microbenchmark on a device buffer (roofline denominators):

@@ -26,6 +26,7 @@ RSK_MEM_HOST = 0
 RSK_MEM_DEVICE = 1
 RSK_BLOOM_COMPAT = 0
 RSK_BLOOM_EXTENDED = 1
+RSK_FETCH_SELF = 1
 HLL_REGISTERS = 16384
 HLL_DENSE_BYTES = 12304
 
@@ -145,6 +146,12 @@ SIGNATURES = {
     "rsk_hll_allreduce_pool": (ctypes.c_int, [_vp]),
     "rsk_hll_reducescatter_pool": (ctypes.c_int, [_vp, _P(_u64), _P(_u64)]),
     "rsk_hll_fetch_rows": (ctypes.c_int, [_vp, _vp, _u64]),
+    "rsk_hll_fetch_rows_flags": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
+    "rsk_plan_shard_range": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _P(_u64), _P(_u64)]),
+    "rsk_plan_owned_range": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _P(_u64), _P(_u64)]),
+    "rsk_plan_owner": (ctypes.c_int, [_u64, ctypes.c_int, _u64, _P(ctypes.c_int)]),
+    "rsk_plan_bloom_slice_words": (ctypes.c_int, [_u64, ctypes.c_int, _P(_u64)]),
+    "rsk_plan_fetch": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _vp, _u64, _u32, _vp, _P(_u64), _vp]),
     "rsk_bloom_allreduce_or": (ctypes.c_int, [_vp]),
     "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
     "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),

@@ -141,7 +141,8 @@ void ensure_stage(rsk_ctx* c) {
 // A pointer a kernel will dereference must be one the GPU can reach (device,
 // managed or registered/pinned host memory); a pageable host pointer passed
 // as RSK_MEM_DEVICE is rejected here instead of faulting the device.
-void need_gpu_ptr(const void* p, const char* msg) {
+// Device memory must belong to the context's GPU (no peer access is enabled).
+void need_gpu_ptr(const rsk_ctx* c, const void* p, const char* msg) {
   if (!p) return;
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -149,22 +150,24 @@ void need_gpu_ptr(const void* p, const char* msg) {
     fail(RSK_ERR_INVALID_ARG, msg);
   }
   if (a.type == hipMemoryTypeUnregistered) fail(RSK_ERR_INVALID_ARG, msg);
+  if (a.type == hipMemoryTypeDevice && c && a.device != c->device)
+    fail(RSK_ERR_INVALID_ARG, std::string(msg) + " (device memory of another GPU)");
 }
 
-void check_keys(const rsk_keys* k) {
+void check_keys(const rsk_ctx* c, const rsk_keys* k) {
   need(k != nullptr, "keys is NULL");
   need(k->location == RSK_MEM_HOST || k->location == RSK_MEM_DEVICE, "keys.location must be RSK_MEM_HOST or RSK_MEM_DEVICE");
   need(k->n == 0 || k->data != nullptr || (k->offsets == nullptr && k->fixed_len == 0), "keys.data is NULL");
   if (k->location == RSK_MEM_DEVICE && k->n > 0) {
-    need_gpu_ptr(k->data, "keys.data is not GPU-accessible memory (location RSK_MEM_DEVICE)");
-    need_gpu_ptr(k->offsets, "keys.offsets is not GPU-accessible memory (location RSK_MEM_DEVICE)");
+    need_gpu_ptr(c, k->data, "keys.data is not GPU-accessible memory (location RSK_MEM_DEVICE)");
+    need_gpu_ptr(c, k->offsets, "keys.offsets is not GPU-accessible memory (location RSK_MEM_DEVICE)");
   }
 }
 
 // Per-key outputs follow the keys' location.
-void check_out(const rsk_keys* k, const void* out) {
+void check_out(const rsk_ctx* c, const rsk_keys* k, const void* out) {
   if (k->location == RSK_MEM_DEVICE && k->n > 0)
-    need_gpu_ptr(out, "output is not GPU-accessible memory (keys are RSK_MEM_DEVICE)");
+    need_gpu_ptr(c, out, "output is not GPU-accessible memory (keys are RSK_MEM_DEVICE)");
 }
 
 // Host batches go through two pinned host stages: host threads fill one
@@ -225,9 +228,20 @@ void ensure_pinned(rsk_ctx* c) {
 // Calls fn(dev_keys, first_index, count) over the batch; host batches are
 // copied through the staging buffers in whole-key chunks.  On return every
 // chunk's work has completed.
+// Leaves the context stream drained when a call exits by exception, so no
+// queued copy still reads a pinned stage the next call refills (and no queued
+// kernel consumes the next call's keys).
+struct DrainOnThrow {
+  rsk_ctx* c;
+  ~DrainOnThrow() {
+    if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(c->stream);
+  }
+};
+
 template <class F>
 void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
-  check_keys(k);
+  check_keys(c, k);
+  DrainOnThrow drain{c};
   if (k->n == 0) return;
   if (k->location == RSK_MEM_DEVICE) {
     fn(DevKeys{reinterpret_cast<const uint8_t*>(k->data), k->offsets, k->n, k->fixed_len}, 0, k->n);
@@ -403,6 +417,9 @@ int rsk_init(const rsk_options* opts, rsk_ctx** out) {
     if (opts) o = *opts;
     if (o.redis_version == 0) o.redis_version = 320;
     need(o.redis_version == 320, "only Redis 3.2.0 semantics (redis_version = 320) are implemented");
+    // Each stage holds stage_bytes of key bytes plus stage_bytes/4 of u64 offsets.
+    need(o.staging_bytes == 0 || (o.staging_bytes >= (1ull << 20) && o.staging_bytes % 256 == 0),
+         "staging_bytes must be 0 (default) or a multiple of 256 that is >= 1 MiB");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail(RSK_ERR_NO_DEVICE, "no HIP device visible");
     need(o.device >= 0 && o.device < ndev, "device ordinal out of range");
@@ -578,6 +595,7 @@ int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_
     check_hll(h, id);
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
+    check_keys(c, keys);  // before the key is created: a refused batch leaves it absent
     bool created;
     create_if_missing(h, id, &created);
     // The reduce kernel raises the flag to this call's epoch when a register
@@ -611,8 +629,8 @@ int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     bool created;
-    check_keys(keys);
-    check_out(keys, out);
+    check_keys(c, keys);
+    check_out(c, keys, out);
     create_if_missing(h, id, &created);
     // Sub-chunks bounded for the 32-bit sort; replies compose sequentially.
     const uint64_t max_chunk = 1ull << 26;
@@ -662,9 +680,9 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     need(keys == nullptr || keys->n == 0 || groups != nullptr, "groups is NULL");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    check_keys(keys);
+    check_keys(c, keys);
     if (keys->n == 0) return;
-    check_out(keys, groups);
+    check_out(c, keys, groups);
     const bool pool_zero = h->zero;
     h->zero = false;
     uint32_t* d_groups = nullptr;
@@ -1092,8 +1110,8 @@ int rsk_bloom_add(rsk_bloom* b, const rsk_keys* keys, uint8_t* added_out) {
     need(b != nullptr, "bloom handle is NULL");
     rsk_ctx* c = b->ctx;
     CtxLock l(c);
-    check_keys(keys);
-    check_out(keys, added_out);
+    check_keys(c, keys);
+    check_out(c, keys, added_out);
     if (!added_out) {
       for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { bloom_add_launch(c, b, dk); });
       return;
@@ -1129,8 +1147,8 @@ int rsk_bloom_contains(rsk_bloom* b, const rsk_keys* keys, uint8_t* out) {
     need(b != nullptr && out != nullptr, "NULL argument");
     rsk_ctx* c = b->ctx;
     CtxLock l(c);
-    check_keys(keys);
-    check_out(keys, out);
+    check_keys(c, keys);
+    check_out(c, keys, out);
     for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
       if (keys->location == RSK_MEM_DEVICE) {
         bloom_contains_launch(c, b, dk, out + first);
@@ -1147,9 +1165,9 @@ int rsk_bloom_contains(rsk_bloom* b, const rsk_keys* keys, uint8_t* out) {
 int rsk_hash_to_base64(rsk_ctx* c, const rsk_keys* keys, char* out) {
   return guarded([&] {
     need(c != nullptr, "ctx is NULL");
-    check_keys(keys);
+    check_keys(c, keys);
     need(keys->n == 0 || out != nullptr, "out is NULL");
-    check_out(keys, out);
+    check_out(c, keys, out);
     CtxLock l(c);
     for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
       if (keys->location == RSK_MEM_DEVICE) {

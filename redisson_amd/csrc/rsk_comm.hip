@@ -178,17 +178,26 @@ int rsk_comm_destroy(rsk_ctx* c) {
 
 int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
   return guarded([&] {
-    need(h && id < h->n, "bad sketch");
-    rsk::hll_materialize(h);
-    h->zero = false;
+    need(h != nullptr, "bad sketch");
     rsk_ctx* c = h->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
-    uint8_t* regs = h->d_regs + id * (uint64_t)rsk::HLL_REGS;
+    // A bad id on one rank must not strand the others in the collective: that
+    // rank reduces a scratch row and reports the error after it.
+    const bool ok = id < h->n;
+    uint8_t* regs = ok ? h->d_regs + id * (uint64_t)rsk::HLL_REGS : c->work(rsk::HLL_REGS);
+    if (ok) {
+      rsk::hll_materialize(h);
+      h->zero = false;
+    } else {
+      RSK_HIP(hipMemsetAsync(regs, 0, rsk::HLL_REGS, c->stream));
+    }
     {
       rsk::ProfScope ps(c, "hll_allreduce");
       RSK_NCCL(ncclAllReduce(regs, regs, rsk::HLL_REGS, ncclUint8, ncclMax, comm, c->stream));
     }
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    need(ok, "sketch id out of range");
     hipLaunchKernelGGL(invalidate_card_kernel, dim3(1), dim3(64), 0, c->stream, h->d_card + id, (uint64_t)1);
     RSK_CHECK_LAUNCH("invalidate");
     h->exists[id] = 1;
@@ -237,37 +246,51 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
     hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
     RSK_CHECK_LAUNCH("invalidate");
     std::fill(h->exists.begin(), h->exists.end(), 1);
-    *first_out = r * q;
-    *count_out = q + (r == N - 1 ? tail : 0);
+    rsk::plan_owned_range(h->n, N, r, first_out, count_out);
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }
 
-int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) {
+int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32_t flags) {
   return guarded([&] {
     need(h && (ids || n == 0), "NULL argument");
+    need((flags & ~RSK_FETCH_SELF) == 0, "unknown flags");
     rsk::hll_materialize(h);
     h->zero = false;
     rsk_ctx* c = h->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
     const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank, R = rsk::HLL_REGS;
-    const uint64_t q = h->n / N;
-    auto owner = [&](uint64_t id) { return q ? std::min<uint64_t>(id / q, N - 1) : N - 1; };
-    // Requests: distinct ids owned elsewhere, grouped by owner (ascending id).
-    std::vector<uint64_t> want(ids, ids + n);
-    for (uint64_t id : want) need(id < h->n, "sketch id out of range");
-    std::sort(want.begin(), want.end());
-    want.erase(std::unique(want.begin(), want.end()), want.end());
-    want.erase(std::remove_if(want.begin(), want.end(), [&](uint64_t id) { return owner(id) == r; }), want.end());
-    std::vector<uint64_t> cnt(2 * N, 0);  // [0, N): rows asked of rank j; [N, 2N): rows rank j asks of us
-    for (uint64_t id : want) ++cnt[owner(id)];
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-    uint64_t* d_cnt = reinterpret_cast<uint64_t*>(c->work(al(16 * N)));
+    // Plan (rsk_plan.hip): distinct requested ids ascending = grouped by owner.
+    std::vector<uint64_t> want, cnt_out;
+    const bool ok_local = rsk::plan_fetch(h->n, N, r, ids, n, flags, &want, &cnt_out);
+    // Every rank agrees on argument errors (and on the pool size, which fixes
+    // every rank's owner map) before any exchange: one MAX all-reduce of
+    // {bad, n, ~n}; max(~n) = ~min(n).
+    uint64_t* d_meta = reinterpret_cast<uint64_t*>(c->work(al(8 * 3) + al(16 * N)));
+    uint64_t* d_cnt = d_meta + al(8 * 3) / 8;
+    uint64_t* h_meta = reinterpret_cast<uint64_t*>(c->h_small + 8192);
+    h_meta[0] = ok_local ? 0 : 1;
+    h_meta[1] = h->n;
+    h_meta[2] = ~h->n;
+    RSK_HIP(hipMemcpyAsync(d_meta, h_meta, 24, hipMemcpyHostToDevice, c->stream));
+    {
+      rsk::ProfScope ps(c, "hll_fetch_agree");
+      RSK_NCCL(ncclAllReduce(d_meta, d_meta, 3, ncclUint64, ncclMax, comm, c->stream));
+    }
+    RSK_HIP(hipMemcpyAsync(h_meta, d_meta, 24, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    need(ok_local, "sketch id out of range");
+    need(h_meta[0] == 0, "rsk_hll_fetch_rows: another rank passed an invalid sketch id");
+    need(h_meta[1] == ~h_meta[2], "rsk_hll_fetch_rows: pool sizes differ across ranks");
+    // Counts: one u64 each way per peer ([0, N): rows asked of rank j; [N, 2N): rows rank j asks of us).
+    std::vector<uint64_t> cnt(2 * N, 0);
+    std::copy(cnt_out.begin(), cnt_out.end(), cnt.begin());
     RSK_HIP(hipMemcpyAsync(d_cnt, cnt.data(), 8 * N, hipMemcpyHostToDevice, c->stream));
     {
       rsk::ProfScope ps(c, "hll_fetch_counts");
-      RSK_NCCL(ncclGroupStart());  // counts: one u64 each way per peer
+      RSK_NCCL(ncclGroupStart());
       for (uint64_t j = 0; j < N; ++j) {
         RSK_NCCL(ncclSend(d_cnt + j, 1, ncclUint64, (int)j, comm, c->stream));
         RSK_NCCL(ncclRecv(d_cnt + N + j, 1, ncclUint64, (int)j, comm, c->stream));
@@ -276,13 +299,12 @@ int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) {
     }
     RSK_HIP(hipMemcpyAsync(cnt.data() + N, d_cnt + N, 8 * N, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
+    // With equal pools and the shared plan a peer only asks for rows this rank
+    // owns, so every incoming count is bounded by the owned range.
     uint64_t n_in = 0;
-    for (uint64_t j = 0; j < N; ++j) {
-      need(cnt[N + j] <= q + h->n % N, "peer asked for more rows than a rank owns");
-      n_in += cnt[N + j];
-    }
+    for (uint64_t j = 0; j < N; ++j) n_in += cnt[N + j];
     const uint64_t n_out = want.size();
-    if (n_in == 0 && n_out == 0) return;
+    if (n_in == 0 && n_out == 0) return;  // agreed by every peer through the counts
     // work: [want ids | incoming ids | rows we send | rows we receive]
     uint8_t* w = c->work(al(8 * n_out) + al(8 * n_in) + (n_in + n_out) * R);
     uint64_t* d_want = reinterpret_cast<uint64_t*>(w);
@@ -320,6 +342,8 @@ int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) {
   });
 }
 
+int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) { return rsk_hll_fetch_rows_flags(h, ids, n, 0); }
+
 int rsk_bloom_allreduce_or(rsk_bloom* b) {
   return guarded([&] {
     need(b != nullptr, "bad filter");
@@ -327,15 +351,14 @@ int rsk_bloom_allreduce_or(rsk_bloom* b) {
     Lock l(c);
     ncclComm_t comm = comm_of(c);
     const uint64_t N = (uint64_t)c->nranks;
-    if (N == 1) return;
     // Slice of S words (multiple of 4 for 16-byte vector OR), N*S >= nwords.
-    uint64_t S = (b->nwords + N - 1) / N;
-    S = (S + 3) & ~uint64_t(3);
+    // At N = 1 the plan still runs (send to self, OR of one row, all-gather of one).
+    const uint64_t S = rsk::plan_bloom_slice_words(b->nwords, N);
     const uint64_t full = N * S;
     uint32_t* send = reinterpret_cast<uint32_t*>(c->work(3 * full * 4 + 256));
     uint32_t* recv = send + full;
     uint32_t* gath = recv + full;
-    RSK_HIP(hipMemsetAsync(send, 0, full * 4, c->stream));
+    if (full > b->nwords) RSK_HIP(hipMemsetAsync(send + b->nwords, 0, (full - b->nwords) * 4, c->stream));
     RSK_HIP(hipMemcpyAsync(send, b->d_bits, b->nwords * 4, hipMemcpyDeviceToDevice, c->stream));
     {
       rsk::ProfScope ps(c, "bloom_alltoall");

@@ -197,6 +197,13 @@ void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_
 // dst[0..S) = OR over rows of src[rows][S] (u32 words).
 void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words);
 
+// ---- exchange plans (rsk_plan.hip, host only)
+void plan_owned_range(uint64_t n, uint64_t N, uint64_t r, uint64_t* first, uint64_t* count);
+uint64_t plan_owner(uint64_t n, uint64_t N, uint64_t id);
+uint64_t plan_bloom_slice_words(uint64_t nwords, uint64_t N);
+bool plan_fetch(uint64_t n, uint64_t N, uint64_t r, const uint64_t* ids, uint64_t n_ids, uint32_t flags,
+                std::vector<uint64_t>* want, std::vector<uint64_t>* counts);
+
 // ---- generators (rsk_gen.hip)
 void gen_keys16_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* out);
 void gen_grouped_launch(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* g, void* keys);

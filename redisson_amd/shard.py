@@ -92,13 +92,25 @@ def owner_of(ids, n: int, world: int) -> np.ndarray:
     return np.minimum(ids // np.uint64(q), np.uint64(world - 1)).astype(np.int64)
 
 
-def hll_fetch_rows(pool, ids) -> None:
+def hll_fetch_rows(pool, ids, flags: int = 0) -> None:
     """Collective: make the local rows `ids` equal to their owners' rows
     (rsk_hll_fetch_rows), so countWith/mergeWith can read sketches owned by
-    other ranks.  Every rank calls it, possibly with no ids."""
+    other ranks.  Every rank calls it, possibly with no ids.  flags =
+    _lib.RSK_FETCH_SELF also routes owned ids through the exchange (tests)."""
     a = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).ravel())
-    _lib.check(_lib.load().rsk_hll_fetch_rows(pool, a.ctypes.data if a.size else None, a.size),
+    _lib.check(_lib.load().rsk_hll_fetch_rows_flags(pool, a.ctypes.data if a.size else None, a.size, flags),
                "rsk_hll_fetch_rows")
+
+
+def fetch_plan(n: int, world: int, rank: int, ids, flags: int = 0):
+    """The request plan of rsk_hll_fetch_rows restated: (distinct ids asked of
+    other ranks ascending, rows asked of each rank).  The library's own C++
+    plan (rsk_plan_fetch) is checked against this in tests/test_plan.py."""
+    want = np.unique(np.asarray(ids, dtype=np.uint64).ravel())
+    assert want.size == 0 or int(want[-1]) < n
+    if not flags & _lib.RSK_FETCH_SELF:
+        want = want[owner_of(want, n, world) != rank]
+    return want, np.bincount(owner_of(want, n, world), minlength=world).astype(np.uint64)
 
 
 def bloom_allreduce_or(bloom) -> None:
@@ -153,10 +165,8 @@ def hll_fetch_rows_cpu(regs: np.ndarray, ids, group=None) -> np.ndarray:
 
     N, r = dist.get_world_size(group), dist.get_rank(group)
     G, R = regs.shape
-    want = np.unique(np.asarray(ids, dtype=np.uint64).ravel())
-    assert want.size == 0 or int(want[-1]) < G
-    want = want[owner_of(want, G, N) != r]  # sorted by id, hence grouped by owner
-    cnt_out = np.bincount(owner_of(want, G, N), minlength=N).astype(np.int64)
+    want, cnt_out = fetch_plan(G, N, r, ids)  # sorted by id, hence grouped by owner
+    cnt_out = cnt_out.astype(np.int64)
     cnt_in = torch.zeros(N, dtype=torch.int64)
     dist.all_to_all_single(cnt_in, torch.from_numpy(cnt_out.copy()), group=group)
     cnt_in = cnt_in.numpy()

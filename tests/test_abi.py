@@ -75,6 +75,18 @@ def test_unsupported_redis_version(lib):
     assert lib.rsk_init(ctypes.byref(opts), ctypes.byref(h)) == _lib.RSK_ERR_INVALID_ARG
 
 
+@pytest.mark.parametrize("staging", [1, 24, 31, (1 << 20) + 8, 1000])
+def test_bad_staging_bytes_rejected(lib, staging):
+    """staging_bytes below 1 MiB or not a multiple of 256 would overflow the
+    offsets region of a stage: refused before any device work."""
+    from redisson_amd import _lib
+
+    opts = _lib.rsk_options(0, 320, staging)
+    h = ctypes.c_void_p()
+    assert lib.rsk_init(ctypes.byref(opts), ctypes.byref(h)) == _lib.RSK_ERR_INVALID_ARG
+    assert b"staging_bytes" in lib.rsk_last_error()
+
+
 def test_bloom_params_match_oracle(lib, orc):
     from redisson_amd.bloom import bloom_params
 

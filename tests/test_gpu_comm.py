@@ -1,6 +1,11 @@
 """RCCL merge layer on one GPU (a 1-rank communicator): the all-reduce paths
-run through RCCL and leave single-rank sketches unchanged.  N > 1 exchange
-plans are covered bit-exactly on CPU by tests/test_shard_gloo.py."""
+run through RCCL and leave single-rank sketches unchanged, and every exchange
+kernel of rsk_comm.hip runs: the Bloom slice-OR exchanges with its own rank
+(send-to-self, or_rows_kernel, all-gather) and rsk_hll_fetch_rows with
+RSK_FETCH_SELF routes owned rows through gather_rows_kernel, a self
+send/recv and scatter_rows_kernel.  The N > 1 plan arithmetic is checked on
+CPU (tests/test_plan.py: the library's C++ plans = shard.py's) and the
+exchange plans bit-exactly with gloo at world 2 and 3 (tests/test_shard_gloo.py)."""
 import ctypes
 
 import numpy as np
@@ -53,6 +58,84 @@ def test_one_rank_communicator(engine, orc):
         orc.bloom_add_batch(rb, 100003, 5, keys, None, 16, 50000, want=False)
         assert np.array_equal(bits, rb)
     finally:
+        _lib.check(L.rsk_comm_destroy(engine.ctx))
+
+
+def _prof(engine, name):
+    return engine.prof_read(name)[1]
+
+
+def test_self_exchange_runs_every_kernel(engine, orc):
+    """Rows through gather -> send/recv to self -> scatter must come back
+    bit-identical (an index mix-up in either kernel moves a row of another
+    sketch), caches invalidated and keys created; the Bloom slice-OR of one
+    rank leaves the bit string unchanged."""
+    from redisson_amd import KeyBatch, _lib, shard
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    engine.prof_enable(True)
+    engine.prof_reset()
+    try:
+        G = 6
+        h = ctypes.c_void_p()
+        _lib.check(L.rsk_hll_create(engine.ctx, G, ctypes.byref(h)))
+        refs = []
+        for g in range(G):  # distinct contents per sketch (sketch 5 stays empty)
+            n = 3000 * (g + 1) if g < 5 else 0
+            keys = orc.gen_keys16(0x5EED0100 + g, 0, max(n, 1))[: 16 * n]
+            ref = np.zeros(16384, np.uint8)
+            if n:
+                ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+                _lib.check(L.rsk_hll_add(h, g, ctypes.byref(ks), None))
+                orc.hll_add(ref, keys, None, 16, n)
+            refs.append(ref)
+        cnt = np.zeros(G, np.uint64)
+        _lib.check(L.rsk_hll_count(h, None, G, cnt.ctypes.data))  # fills the caches of sketches 0..4
+        shard.hll_fetch_rows(h, [4, 1, 4, 0, 5], flags=_lib.RSK_FETCH_SELF)
+        assert _prof(engine, "hll_fetch_rows") == 1  # the row exchange ran (not the early exit)
+        for g in range(G):
+            out = np.zeros(16384, np.uint8)
+            _lib.check(L.rsk_hll_get_registers(h, g, out.ctypes.data, _lib.RSK_MEM_HOST))
+            assert np.array_equal(out, refs[g]), g
+        ex = ctypes.c_int()
+        _lib.check(L.rsk_hll_exists(h, 5, ctypes.byref(ex)))
+        assert ex.value == 1  # fetched rows exist (snapshot of the owner's key)
+        cnt2 = np.zeros(G, np.uint64)
+        _lib.check(L.rsk_hll_count(h, None, G, cnt2.ctypes.data))
+        assert [int(x) for x in cnt2] == [orc.hll_count_dense(r) for r in refs]
+        # Lockstep argument errors: the bad id is reported, the communicator stays usable.
+        with pytest.raises(_lib.IllegalArgumentException):
+            shard.hll_fetch_rows(h, [1, G], flags=_lib.RSK_FETCH_SELF)
+        shard.hll_fetch_rows(h, [2], flags=_lib.RSK_FETCH_SELF)
+        with pytest.raises(_lib.IllegalArgumentException):
+            _lib.check(L.rsk_hll_allreduce(h, G))
+        _lib.check(L.rsk_hll_allreduce(h, 2))
+        out = np.zeros(16384, np.uint8)
+        _lib.check(L.rsk_hll_get_registers(h, 2, out.ctypes.data, _lib.RSK_MEM_HOST))
+        assert np.array_equal(out, refs[2])
+        # Bloom: the full slice-OR plan at N = 1 (odd size: the last slice is padded).
+        size, k = 1_000_003, 7
+        keys = orc.gen_keys16(0x5EED0003, 0, 40000)
+        b = ctypes.c_void_p()
+        _lib.check(L.rsk_bloom_create(engine.ctx, size, k, ctypes.byref(b)))
+        ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+        _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), None))
+        _lib.check(L.rsk_bloom_allreduce_or(b))
+        assert _prof(engine, "bloom_alltoall") == 1 and _prof(engine, "bloom_or_rows") == 1
+        assert _prof(engine, "bloom_allgather") == 1
+        bits = np.zeros((size + 7) // 8, np.uint8)
+        n = ctypes.c_size_t()
+        _lib.check(L.rsk_bloom_export_bits(b, bits.ctypes.data, bits.size, ctypes.byref(n)))
+        rb = np.zeros_like(bits)
+        orc.bloom_add_batch(rb, size, k, keys, None, 16, 40000, want=False)
+        assert np.array_equal(bits, rb)
+        _lib.check(L.rsk_bloom_destroy(b))
+        _lib.check(L.rsk_hll_destroy(h))
+    finally:
+        engine.prof_enable(False)
         _lib.check(L.rsk_comm_destroy(engine.ctx))
 
 

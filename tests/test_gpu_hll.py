@@ -523,6 +523,14 @@ def test_device_batch_with_host_output_is_rejected(L, engine, orc):
     bad = _lib.rsk_keys()
     bad.data, bad.offsets, bad.n, bad.fixed_len, bad.location = hk.ctypes.data, None, n, 16, _lib.RSK_MEM_DEVICE
     assert L.rsk_hll_add(h, 0, ctypes.byref(bad), None) == _lib.RSK_ERR_INVALID_ARG
+    ex = ctypes.c_int(-1)
+    _lib.check(L.rsk_hll_exists(h, 0, ctypes.byref(ex)))
+    assert ex.value == 0  # a refused PFADD does not create the key
+    empty = _lib.rsk_keys()
+    empty.data, empty.offsets, empty.n, empty.fixed_len, empty.location = None, None, 0, 16, _lib.RSK_MEM_HOST
+    changed = ctypes.c_uint8(7)
+    _lib.check(L.rsk_hll_add(h, 0, ctypes.byref(empty), ctypes.byref(changed)))
+    assert changed.value == 1  # PFADD key (no elements) on a missing key creates it: reply 1
     # and the context still works
     dout = devmem.DeviceBuffer.from_numpy(engine, np.zeros(n, np.uint8))
     _lib.check(L.rsk_bloom_contains(b, ctypes.byref(ks), dout.ptr))
