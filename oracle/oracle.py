@@ -20,7 +20,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librsk_oracle.so")
+# RSK_ORACLE_LIB: an alternative build (the ASan/UBSan one, tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("RSK_ORACLE_LIB", os.path.join(HERE, "librsk_oracle.so"))
 REGISTERS = 16384
 DENSE_SIZE = 16 + 12288
 SPARSE_MAX_BYTES = 3000  # Redis hll-sparse-max-bytes default
@@ -439,7 +440,10 @@ class RedisModel:
 
     def bitcount(self, name) -> int:
         o = self._bits(name)
-        return sum(bin(b).count("1") for b in o)
+        if not o:
+            return 0
+        a = np.frombuffer(o, dtype=np.uint8)
+        return int(lib().orc_bitcount(_ptr(a), a.size))
 
     def strlen(self, name) -> int:
         return len(self._bits(name))

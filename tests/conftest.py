@@ -9,7 +9,9 @@ if ROOT not in sys.path:
 
 # Load librsketch (system ROCm HIP/HSA) before any test module imports torch,
 # so the process never maps a second, torch-bundled HSA runtime first.
-if os.path.exists(os.path.join(ROOT, "redisson_amd", "librsketch.so")):
+# (Not under the sanitizer run, tests/test_sanitizers.py: it loads only the
+# ASan/UBSan builds of the oracle and of the host plan code.)
+if os.path.exists(os.path.join(ROOT, "redisson_amd", "librsketch.so")) and not os.environ.get("RSK_SANITIZE"):
     from redisson_amd import _lib as _rsk_lib
 
     _rsk_lib.load()

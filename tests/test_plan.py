@@ -4,36 +4,72 @@ rsk_comm.hip) against redisson_amd/shard.py, whose restatement the gloo tests
 arithmetic: runs on CPU through the C ABI (no GPU call), at N = 1, 2, 3, 8 and
 beyond, with pools smaller than N and with tails."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
 
 from redisson_amd import _lib, shard
 
+
+class _PlanLib:
+    """librsketch's exported plan functions, or (RSK_PLAN_LIB) the same
+    source built alone under ASan/UBSan (oracle/Makefile `asan`)."""
+
+    def __init__(self):
+        path = os.environ.get("RSK_PLAN_LIB")
+        if not path:
+            self.L = _lib.load()
+            return
+        self.L = ctypes.CDLL(path)
+        for name, (res, args) in _lib.SIGNATURES.items():
+            if name.startswith("rsk_plan_"):
+                fn = getattr(self.L, name)
+                fn.restype, fn.argtypes = res, args
+
+    def __getattr__(self, name):
+        return getattr(self.L, name)
+
+
+_PL = None
+
+
+def plan_lib():
+    global _PL
+    if _PL is None:
+        _PL = _PlanLib()
+    return _PL
+
+
 WORLDS = [1, 2, 3, 5, 8, 16]
 POOLS = [1, 2, 3, 7, 8, 9, 20, 1000, 1000003]
 
 
+def _ck(rc):
+    if rc != _lib.RSK_OK:
+        raise _lib.IllegalArgumentException("rsk_plan_* returned %d" % rc)
+
+
 def _c_owned(n, N, r):
     f, c = ctypes.c_uint64(), ctypes.c_uint64()
-    _lib.check(_lib.load().rsk_plan_owned_range(n, N, r, ctypes.byref(f), ctypes.byref(c)))
+    _ck(plan_lib().rsk_plan_owned_range(n, N, r, ctypes.byref(f), ctypes.byref(c)))
     return f.value, c.value
 
 
 def _c_fetch(n, N, r, ids, flags=0):
-    L = _lib.load()
+    L = plan_lib()
     ids = np.ascontiguousarray(np.asarray(ids, np.uint64))
     want = np.zeros(max(1, ids.size), np.uint64)
     cnt = np.zeros(N, np.uint64)
     nw = ctypes.c_uint64()
-    _lib.check(L.rsk_plan_fetch(n, N, r, ids.ctypes.data if ids.size else None, ids.size, flags,
-                                want.ctypes.data, ctypes.byref(nw), cnt.ctypes.data))
+    _ck(L.rsk_plan_fetch(n, N, r, ids.ctypes.data if ids.size else None, ids.size, flags,
+                         want.ctypes.data, ctypes.byref(nw), cnt.ctypes.data))
     return want[:nw.value], cnt
 
 
 @pytest.mark.parametrize("N", WORLDS)
 def test_owned_ranges_match_shard_py_and_tile_the_pool(N):
-    L = _lib.load()
+    L = plan_lib()
     for n in POOLS:
         covered = 0
         for r in range(N):
@@ -46,7 +82,7 @@ def test_owned_ranges_match_shard_py_and_tile_the_pool(N):
         own_py = shard.owner_of(ids, n, N)
         for i, want in zip(ids, own_py):
             o = ctypes.c_int()
-            _lib.check(L.rsk_plan_owner(n, N, int(i), ctypes.byref(o)))
+            _ck(L.rsk_plan_owner(n, N, int(i), ctypes.byref(o)))
             assert o.value == int(want)
             f, c = _c_owned(n, N, o.value)
             assert f <= int(i) < f + c
@@ -54,12 +90,12 @@ def test_owned_ranges_match_shard_py_and_tile_the_pool(N):
 
 @pytest.mark.parametrize("N", WORLDS)
 def test_shard_ranges_match_shardplan(N):
-    L = _lib.load()
+    L = plan_lib()
     for n in [0, 1, 5, 8, 1000, 10**9 + 7, 8 * 10**9]:
         end_prev = 0
         for r in range(N):
             b, e = ctypes.c_uint64(), ctypes.c_uint64()
-            _lib.check(L.rsk_plan_shard_range(n, N, r, ctypes.byref(b), ctypes.byref(e)))
+            _ck(L.rsk_plan_shard_range(n, N, r, ctypes.byref(b), ctypes.byref(e)))
             assert (b.value, e.value) == shard.ShardPlan(n, N).range(r)
             assert b.value == end_prev
             end_prev = e.value
@@ -68,10 +104,10 @@ def test_shard_ranges_match_shardplan(N):
 
 @pytest.mark.parametrize("N", WORLDS)
 def test_bloom_slice_words_match(N):
-    L = _lib.load()
+    L = plan_lib()
     for nwords in [4, 8, 12, 1000, 299_533_076, 2**30 + 4]:
         s = ctypes.c_uint64()
-        _lib.check(L.rsk_plan_bloom_slice_words(nwords, N, ctypes.byref(s)))
+        _ck(L.rsk_plan_bloom_slice_words(nwords, N, ctypes.byref(s)))
         assert s.value == shard.slice_words(nwords, N)
         assert s.value % 4 == 0 and s.value * N >= nwords
 
@@ -105,7 +141,7 @@ def test_fetch_plan_rejects_out_of_range_ids():
 
 
 def test_plan_argument_checks():
-    L = _lib.load()
+    L = plan_lib()
     f, c = ctypes.c_uint64(), ctypes.c_uint64()
     assert L.rsk_plan_owned_range(10, 0, 0, ctypes.byref(f), ctypes.byref(c)) == _lib.RSK_ERR_INVALID_ARG
     assert L.rsk_plan_owned_range(10, 2, 2, ctypes.byref(f), ctypes.byref(c)) == _lib.RSK_ERR_INVALID_ARG
