@@ -154,7 +154,8 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
     add_ms, add_n = engine.prof_read("bloom_add16")
     con_ms, con_n = engine.prof_read("bloom_contains16")
     stages = {}
-    for name in ("bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply"):
+    for name in ("bloom_st1", "bloom_st_mid", "bloom_st2", "bloom_st_apply",
+                 "bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply"):
         ms, cnt = engine.prof_read(name)
         if cnt:
             stages[name] = ms / max(1, add_n)  # per insert batch (summed over its chunks)

@@ -236,21 +236,27 @@ static uint32_t grid_for(rsk_ctx* c, uint64_t n) {
   return (uint32_t)(g < cap ? (g ? g : 1) : cap);
 }
 
-void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
+// k random memory-side atomicOr per key (small batches).
+void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
   if (k.n == 0) return;
-  if (fixed16(k)) {
-    ProfScope ps(c, "bloom_add16");
-    if (bloom_add_partitioned(c, b, k)) return;  // large batches: LDS slices (rsk_bloom_part.hip)
+  if (fixed16(k))
     hipLaunchKernelGGL(bloom_add_kernel<true>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, nullptr, 16u,
                        k.n, b->d_bits, b->fm, b->k);
-    RSK_CHECK_LAUNCH("bloom_add16");
-  } else {
-    ProfScope ps(c, "bloom_add");
-    if (bloom_add_partitioned(c, b, k)) return;
+  else
     hipLaunchKernelGGL(bloom_add_kernel<false>, dim3(grid_for(c, k.n)), dim3(256), 0, c->stream, k.data, k.offsets,
                        k.fixed_len, k.n, b->d_bits, b->fm, b->k);
-    RSK_CHECK_LAUNCH("bloom_add");
-  }
+  RSK_CHECK_LAUNCH("bloom_add_direct");
+}
+
+// Large batches: probes routed to LDS-resident 64 KiB filter slices, by the
+// super-tile partition (rsk_bloom_st.hip; k <= 16) or the exact-offset
+// pipeline (rsk_bloom_part.hip); small ones: direct atomics.
+void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
+  if (k.n == 0) return;
+  ProfScope ps(c, fixed16(k) ? "bloom_add16" : "bloom_add");
+  if (bloom_add_supertile(c, b, k)) return;
+  if (bloom_add_partitioned(c, b, k)) return;
+  bloom_add_direct_launch(c, b, k);
 }
 
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out) {

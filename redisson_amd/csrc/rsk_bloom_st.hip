@@ -1,0 +1,643 @@
+// rsk_bloom_st.hip -- Bloom insert for large batches by super-tile partition (gfx950).
+//
+// RedissonBloomFilter.add (src/main/java/org/redisson/RedissonBloomFilter.java:80-114)
+// sets k bits per element (k SETBITs, :94-98) at idx_t = (h_t & Long.MAX_VALUE)
+// % size (:116-131).  Setting bits is an OR, so the probes may be applied in
+// any order; this path routes them to 64 KiB slices of the filter (2^19 bits)
+// and ORs each slice in LDS, without knowing any count in advance:
+//
+//   st1   : one pass over the keys.  A super-tile = 2048 keys (k <= 8) or 1024
+//           (k <= 16): each lane hashes its keys once (XXH64 + farmhash), keeps
+//           its <= 16 probes in registers, ranks them by coarse bin (idx >>
+//           (19 + f2), <= 256 bins) with one LDS atomic each, places them in
+//           LDS and writes the bin-sorted super-tile CONTIGUOUSLY at its own
+//           slot (probes 26 bits: the position inside the coarse bin) plus a
+//           u16 header of bin offsets.  No histogram pass, no global offsets.
+//   hdrT  : header transposed to [bin][super-tile] (coalesced reads below).
+//   size  : per (coarse bin c, part p): probes and a tile budget for st2.
+//   st2   : one workgroup per (c, p) reads segment c of the super-tiles of
+//           part p (16 waves, each its own interleaved segment list, R probe
+//           slots per lane filled by 64-lane loads), ranks by fine bin (the
+//           2^f2 slices of c), and writes bin-sorted tiles contiguously into
+//           the (c, p) region, with u16 headers (19-bit slice offsets).
+//   apply : one workgroup per slice: 64 KiB of filter in LDS, every segment
+//           of that slice in the tiles of its coarse bin ORed in with ds_or,
+//           the slice written back once.
+// Filters of <= 256 slices skip st2 (apply reads the st1 tiles directly).
+//
+// HBM per key at k probes: 16 B of key + 4k (st1 write) + 4k + 4k (st2) + 4k
+// (apply) + ~1 % headers, plus 2 x the filter per chunk; LDS per probe: rank
+// atomic + lstart read + place + read-out (st1, st2) + ds_or (apply).  The
+// earlier pipeline (rsk_bloom_part.hip: histogram pass over the keys, exact
+// global offsets, sbin/dlt scatter) remains for k > 16 and as the fallback.
+#include <cstdlib>
+#include <cstring>
+
+#include "rsk_internal.h"
+
+namespace rsk {
+
+namespace {
+
+constexpr int SL_LOG = 19;                             // bits per slice
+constexpr uint32_t SL_WORDS = 1u << (SL_LOG - 5);      // 16384 u32 = 64 KiB of LDS
+constexpr uint32_t SL_MAX = 32768;                     // slices (2^34 bits) handled here
+constexpr int T1_DEFAULT = 512;                        // st1 workgroup (RSK_BLOOM_ST_T1 = 512 | 1024)
+constexpr int T2 = 1024;                               // st2 workgroup (16 waves)
+constexpr int R2 = 14;                                 // st2 probe slots per lane
+constexpr int TA = 1024;                               // apply workgroup
+constexpr uint32_t INVALID = 0xFFFFFFFFu;              // no probe (payloads are < 2^26)
+constexpr uint64_t DEFAULT_PROBE_CHUNK = 1ull << 33;   // probes per chunk (2 x 32 GiB of scratch)
+
+RSK_DEV uint32_t rdl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+RSK_DEV uint64_t rdl64(uint64_t v, uint32_t l) {
+  return ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32) | rdl((uint32_t)v, l);
+}
+
+// Exclusive scan of one value per lane over a T-lane workgroup.
+template <int T>
+RSK_DEV uint32_t block_scan(uint32_t v, uint32_t* total, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < T / 64; ++q) {
+    const uint32_t s = wsum[q];
+    pre += q < w ? s : 0;
+    tot += s;
+  }
+  *total = tot;
+  __syncthreads();
+  return pre + x - v;
+}
+
+RSK_DEV void key_words(const uint4& v, uint64_t* w0, uint64_t* w1) {
+  *w0 = ((uint64_t)v.y << 32) | v.x;
+  *w1 = ((uint64_t)v.w << 32) | v.z;
+}
+
+// ------------------------------------------------------------------- st1
+// Super-tile st = keys [st*KST, st*KST + KST): bin-sorted probes at
+// out[st * KST * k ...], header hdr[st][0..nb1] (bin offsets, [nb1] = total).
+template <bool FIXED16, int KMAX, int T1>
+__global__ __launch_bounds__(T1) void bloom_st1_kernel(const uint8_t* __restrict__ data,
+                                                       const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                                                       uint64_t n, FastMod63 fm, int k, uint32_t shift1, uint32_t nb1,
+                                                       uint64_t nst, uint32_t* __restrict__ out,
+                                                       uint16_t* __restrict__ hdr) {
+  constexpr int KPL = 16 / KMAX;        // keys per lane
+  constexpr uint32_t KST = T1 * KPL;    // keys per super-tile
+  constexpr int NP = KPL * KMAX;        // probe slots per lane (16)
+  __shared__ __attribute__((aligned(16))) uint32_t srt[T1 * NP];
+  __shared__ uint32_t hist[256], lstart[256], wsum[T1 / 64];
+  const uint64_t low = (1ull << shift1) - 1;
+  const uint64_t stride = (uint64_t)KST * (uint64_t)k;
+  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+  const uint4* keys16 = reinterpret_cast<const uint4*>(data);
+  uint4 nxt[KPL];
+  auto fetch = [&](uint64_t st) {
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const uint64_t i = st * KST + threadIdx.x + (uint64_t)u * T1;
+      nxt[u] = (FIXED16 && st < nst && i < n) ? ld_nt16(keys16 + i) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (FIXED16) fetch(blockIdx.x);
+  for (uint64_t st = blockIdx.x; st < nst; st += gridDim.x) {
+    const uint64_t k0 = st * KST;
+    const uint32_t nk = (uint32_t)(n - k0 < KST ? n - k0 : KST);
+    uint4 cur[KPL];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) cur[u] = nxt[u];
+    if (FIXED16) fetch(st + gridDim.x);  // the next super-tile's keys stream in meanwhile
+    __syncthreads();  // srt free (previous write-out done), hist reset visible
+    uint32_t pay[NP], tag[NP];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const uint32_t q = threadIdx.x + u * T1;
+      const bool ok = q < nk;
+      uint64_t h1 = 0, h2 = 0;
+      if (ok) {
+        if (FIXED16) {
+          uint64_t w0, w1;
+          key_words(cur[u], &w0, &w1);
+          h1 = xxh64_16(w0, w1);
+          h2 = farm_16(w0, w1);
+        } else {
+          bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
+        }
+      }
+      ProbeSeq ps(h1, h2, fm);
+#pragma unroll
+      for (int t = 0; t < KMAX; ++t) {
+        const int s = u * KMAX + t;
+        tag[s] = INVALID;
+        pay[s] = 0;
+        if (ok && t < k) {
+          const uint64_t idx = ps.idx;
+          const uint32_t bin = (uint32_t)(idx >> shift1);
+          pay[s] = (uint32_t)(idx & low);
+          tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+          if (t + 1 < k) ps.next(t, fm);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t cnt = threadIdx.x < nb1 ? hist[threadIdx.x] : 0;
+    uint32_t total;
+    const uint32_t ex = block_scan<T1>(cnt, &total, wsum);
+    if (threadIdx.x < nb1) {
+      lstart[threadIdx.x] = ex;
+      hist[threadIdx.x] = 0;
+    }
+    if (threadIdx.x <= nb1) hdr[st * (nb1 + 1) + threadIdx.x] = (uint16_t)(threadIdx.x < nb1 ? ex : total);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NP; ++s)
+      if (tag[s] != INVALID) srt[lstart[tag[s] >> 16] + (tag[s] & 0xFFFFu)] = pay[s];
+    __syncthreads();
+    uint4* o4 = reinterpret_cast<uint4*>(out + st * stride);  // 16-byte aligned: stride = 1024*16/KMAX*k... * 4 B
+    const uint4* s4 = reinterpret_cast<const uint4*>(srt);
+    for (uint32_t j = threadIdx.x; j < total / 4; j += T1) {
+      const uint4 v = s4[j];
+      u32x4 x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(o4 + j));
+    }
+    for (uint32_t j = (total & ~3u) + threadIdx.x; j < total; j += T1) out[st * stride + j] = srt[j];
+  }
+}
+
+// ------------------------------------------------------ header transpose
+// in [rows][cols] -> out [cols][rows] (u16), 64 x 64 tiles through LDS.
+__global__ __launch_bounds__(256) void st_transpose_kernel(const uint16_t* __restrict__ in, uint64_t rows,
+                                                           uint32_t cols, uint16_t* __restrict__ out) {
+  __shared__ uint16_t t[64][66];
+  const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+  const uint32_t c0 = blockIdx.y * 64;
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += 256) {
+    const uint32_t rr = i >> 6, cc = i & 63;
+    const uint64_t r = r0 + rr;
+    const uint32_t c = c0 + cc;
+    t[rr][cc] = (r < rows && c < cols) ? in[r * cols + c] : 0;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += 256) {
+    const uint32_t cc = i >> 6, rr = i & 63;
+    const uint64_t r = r0 + rr;
+    const uint32_t c = c0 + cc;
+    if (r < rows && c < cols) out[(uint64_t)c * rows + r] = t[rr][cc];
+  }
+}
+
+// ---------------------------------------------------------------- sizing
+// (c, p) = blockIdx.x: probes of coarse bin c in st1 tiles [t0, t1) of part p,
+// and st2's tile budget (see bloom_add_supertile).
+RSK_DEV void part_range(uint64_t nst, uint32_t P, uint32_t p, uint64_t* t0, uint64_t* t1) {
+  *t0 = nst * p / P;
+  *t1 = nst * (p + 1) / P;
+}
+
+RSK_DEV uint32_t tile_budget(uint64_t probes, uint64_t segs) {
+  return (uint32_t)(2 * ((probes / 64 + segs) / (16 * R2)) + 4);
+}
+
+__global__ __launch_bounds__(256) void st_size_kernel(const uint16_t* __restrict__ h1t, uint64_t nst, uint32_t P,
+                                                      int tiny_budget, uint64_t* __restrict__ tot,
+                                                      uint32_t* __restrict__ bud) {
+  __shared__ uint64_t part[4];
+  const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
+  uint64_t t0, t1;
+  part_range(nst, P, p, &t0, &t1);
+  const uint16_t* a = h1t + (uint64_t)c * nst;
+  const uint16_t* b = a + nst;
+  uint64_t s = 0;
+  for (uint64_t t = t0 + threadIdx.x; t < t1; t += 256) s += (uint32_t)(b[t] - a[t]);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t total = part[0] + part[1] + part[2] + part[3];
+    tot[cp] = total;
+    bud[cp] = tiny_budget ? 1u : tile_budget(total, t1 - t0);  // tiny: tests of the overflow fallback
+  }
+}
+
+// One workgroup: exclusive prefix sums reg_off (u64) / tile_off (u32) over
+// ncp entries, with the totals at [ncp].
+__global__ __launch_bounds__(1024) void st_offsets_kernel(const uint64_t* __restrict__ tot,
+                                                          const uint32_t* __restrict__ bud, uint32_t ncp,
+                                                          uint64_t* __restrict__ reg_off,
+                                                          uint32_t* __restrict__ tile_off) {
+  __shared__ uint64_t s_tot[1024];
+  __shared__ uint32_t s_bud[1024];
+  const uint32_t per = (ncp + 1023) / 1024, b0 = threadIdx.x * per;
+  uint64_t a = 0;
+  uint32_t c = 0;
+  for (uint32_t i = b0; i < b0 + per && i < ncp; ++i) {
+    a += tot[i];
+    c += bud[i];
+  }
+  s_tot[threadIdx.x] = a;
+  s_bud[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 1024 partials, serial (tiny)
+    uint64_t ra = 0;
+    uint32_t rc = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const uint64_t x = s_tot[i];
+      const uint32_t y = s_bud[i];
+      s_tot[i] = ra;
+      s_bud[i] = rc;
+      ra += x;
+      rc += y;
+    }
+    reg_off[ncp] = ra;
+    tile_off[ncp] = rc;
+  }
+  __syncthreads();
+  a = s_tot[threadIdx.x];
+  c = s_bud[threadIdx.x];
+  for (uint32_t i = b0; i < b0 + per && i < ncp; ++i) {
+    reg_off[i] = a;
+    tile_off[i] = c;
+    a += tot[i];
+    c += bud[i];
+  }
+}
+
+// ------------------------------------------------------------------- st2
+// Workgroup (c, p): segment c of the st1 tiles of part p -- wave w takes the
+// groups of 64 consecutive tiles t0 + 64 (w + 16 i) + [0, 64) -- bin-sorted
+// by fine bin (pay >> 19) into tiles written contiguously at out + reg_off[cp];
+// tile j of (c, p) gets header h2[tile_off[cp] + j][0..nb2] and its start tb2.
+__global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restrict__ in,
+                                                       const uint16_t* __restrict__ h1t, uint64_t nst,
+                                                       uint64_t stride1, uint32_t P, uint32_t nb2,
+                                                       const uint64_t* __restrict__ reg_off,
+                                                       const uint32_t* __restrict__ tile_off,
+                                                       const uint32_t* __restrict__ bud, uint32_t* __restrict__ used,
+                                                       uint32_t* __restrict__ out, uint16_t* __restrict__ h2,
+                                                       uint64_t* __restrict__ tb2, uint32_t* __restrict__ overflow) {
+  __shared__ __attribute__((aligned(16))) uint32_t srt[T2 * R2];
+  __shared__ uint32_t hist[128], lstart[128], wsum[T2 / 64];
+  const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t t0, t1;
+  part_range(nst, P, p, &t0, &t1);
+  const uint16_t* ha = h1t + (uint64_t)c * nst;
+  const uint16_t* hb = ha + nst;
+  if (threadIdx.x < 128) hist[threadIdx.x] = 0;
+  // wave-uniform cursor over a cache of 64 segments (one per lane, coalesced header loads)
+  uint64_t gbase = t0 + 64ull * w, cpos = 0, cur_pos = 0;
+  uint32_t ci = 64, clen = 0, cur_len = 0, off = 0;
+  bool have = true;
+  auto next_seg = [&]() {
+    while (true) {
+      if (ci == 64) {
+        if (gbase >= t1) return false;
+        const uint64_t t = gbase + lane;
+        if (t < t1) {
+          const uint32_t a = ha[t];
+          clen = (uint32_t)hb[t] - a;
+          cpos = t * stride1 + a;
+        } else {
+          clen = 0;
+          cpos = 0;
+        }
+        ci = 0;
+        gbase += 64ull * (T2 / 64);
+      }
+      const uint32_t len = rdl(clen, ci);
+      const uint64_t pos = rdl64(cpos, ci);
+      ++ci;
+      if (len) {
+        cur_len = len;
+        cur_pos = pos;
+        off = 0;
+        return true;
+      }
+    }
+  };
+  have = next_seg();
+  const uint64_t base = reg_off[cp];
+  const uint32_t tbeg = tile_off[cp], tcap = bud[cp];
+  uint64_t written = 0;
+  uint32_t ntile = 0;
+  for (;;) {
+    uint32_t pay[R2], tag[R2];
+#pragma unroll
+    for (int r = 0; r < R2; ++r) {
+      if (have && off >= cur_len) have = next_seg();
+      pay[r] = INVALID;
+      if (have) {
+        const uint32_t j = off + lane;
+        if (j < cur_len) pay[r] = __builtin_nontemporal_load(&in[cur_pos + j]);
+        off += 64;
+      }
+    }
+    if (have && off >= cur_len) have = next_seg();  // "more input" must be exact for the loop exit
+    __syncthreads();  // srt free, hist reset visible
+#pragma unroll
+    for (int r = 0; r < R2; ++r) {
+      tag[r] = INVALID;
+      if (pay[r] != INVALID) {
+        const uint32_t bin = pay[r] >> SL_LOG;
+        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+      }
+    }
+    const int more = __syncthreads_or(have ? 1 : 0);
+    const uint32_t cnt = threadIdx.x < nb2 ? hist[threadIdx.x] : 0;
+    uint32_t total;
+    const uint32_t ex = block_scan<T2>(cnt, &total, wsum);
+    if (threadIdx.x < nb2) {
+      lstart[threadIdx.x] = ex;
+      hist[threadIdx.x] = 0;
+    }
+    if (total) {
+      if (ntile < tcap) {
+        if (threadIdx.x <= nb2)
+          h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = (uint16_t)(threadIdx.x < nb2 ? ex : total);
+        if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
+      } else if (threadIdx.x == 0) {
+        atomicOr(overflow, 1u);  // budget exceeded (adversarial input): the host redoes the chunk
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < R2; ++r)
+        if (tag[r] != INVALID) srt[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
+      __syncthreads();
+      uint32_t* o = out + base + written;
+      for (uint32_t j = threadIdx.x; j < total; j += T2) o[j] = srt[j];
+      written += total;
+      ++ntile;
+    }
+    if (!more) break;
+  }
+  if (threadIdx.x == 0) used[cp] = ntile < tcap ? ntile : tcap;
+}
+
+// ----------------------------------------------------------------- apply
+// Slice s: OR every probe of s into the 64 KiB slice held in LDS.  Two-level:
+// the tiles of coarse bin c = s >> f2 (per part p: [tile_off[cp], + used[cp])),
+// segment f = s & (2^f2 - 1), rows f / f+1 of the transposed st2 headers, tile
+// starts tb[tile].  One level (f2 = 0, tile_off == nullptr): the st1 tiles
+// [0, nst), rows s / s+1 of the transposed st1 headers, tile t at t * stride.
+__global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __restrict__ probes,
+                                                            const uint16_t* __restrict__ ht, uint64_t row_stride,
+                                                            uint32_t f2, const uint64_t* __restrict__ tb,
+                                                            uint64_t stride, uint64_t nst,
+                                                            const uint32_t* __restrict__ tile_off,
+                                                            const uint32_t* __restrict__ used, uint32_t P,
+                                                            uint32_t nslices, uint32_t* __restrict__ bits,
+                                                            uint64_t nwords) {
+  __shared__ __attribute__((aligned(16))) uint32_t sl[SL_WORDS];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr uint32_t NW = TA / 64;
+  for (uint32_t s = blockIdx.x; s < nslices; s += gridDim.x) {
+    const uint64_t w0 = (uint64_t)s * SL_WORDS;
+    const uint32_t nw4 = (uint32_t)((nwords - w0 < SL_WORDS ? nwords - w0 : SL_WORDS) / 4);
+    uint4* g4 = reinterpret_cast<uint4*>(bits + w0);
+    uint4* l4 = reinterpret_cast<uint4*>(sl);
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) l4[q] = g4[q];
+    __syncthreads();
+    const uint32_t c = s >> f2, f = tile_off ? (s & ((1u << f2) - 1)) : s;
+    const uint16_t* ra = ht + (uint64_t)f * row_stride;
+    const uint16_t* rb = ra + row_stride;
+    const uint32_t nranges = tile_off ? P : 1;
+    for (uint32_t pr = 0; pr < nranges; ++pr) {
+      uint64_t ta, te;
+      if (tile_off) {
+        ta = tile_off[(uint64_t)c * P + pr];
+        te = ta + used[(uint64_t)c * P + pr];
+      } else {
+        ta = 0;
+        te = nst;
+      }
+      // wave w: groups of 64 consecutive tiles ta + 64 (w + NW i), one coalesced header load each
+      for (uint64_t g = ta + 64ull * w; g < te; g += 64ull * NW) {
+        const uint64_t t = g + lane;
+        uint32_t beg = 0, len = 0;
+        uint64_t pos = 0;
+        if (t < te) {
+          beg = ra[t];
+          len = (uint32_t)rb[t] - beg;
+          pos = (tb ? tb[t] : t * stride) + beg;
+        }
+        const uint32_t ng = (uint32_t)(te - g < 64 ? te - g : 64);
+        for (uint32_t j = 0; j < ng; j += 4) {  // 4 segments' loads in flight per lane
+          uint32_t v[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t jj = j + q < ng ? j + q : ng - 1;
+            const uint32_t sl_len = (j + q < ng) ? rdl(len, jj) : 0;
+            const uint64_t sp = rdl64(pos, jj);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t o = lane + 64 * h;
+              v[2 * q + h] = o < sl_len ? __builtin_nontemporal_load(&probes[sp + o]) : INVALID;
+            }
+            for (uint32_t o = lane + 128; o < sl_len; o += 64) {  // long segments (rare)
+              const uint32_t x = probes[sp + o];
+              atomicOr(&sl[x >> 5], bloom_bit_mask(x));
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (v[q] != INVALID) atomicOr(&sl[v[q] >> 5], bloom_bit_mask(v[q]));
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) g4[q] = l4[q];
+    __syncthreads();
+  }
+}
+
+int st_mode() {
+  const char* e = std::getenv("RSK_BLOOM_ST");  // unset: auto; "0": never; "1": always (any batch size)
+  if (!e || !*e) return -1;
+  return e[0] == '0' ? 0 : 1;
+}
+
+uint64_t probe_chunk() {
+  const char* e = std::getenv("RSK_BLOOM_ST_CHUNK");  // probes per chunk (tests force small chunks)
+  const uint64_t v = (e && *e) ? std::strtoull(e, nullptr, 10) : 0;
+  return v ? v : DEFAULT_PROBE_CHUNK;
+}
+
+uint32_t env_u32(const char* name, uint32_t dflt) {  // tuning knobs
+  const char* e = std::getenv(name);
+  return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
+}
+
+// Persistent grid: as many workgroups as are resident at once (occupancy API),
+// never more than `units` -- a queued workgroup of a persistent loop would
+// only start once a resident one had finished all of its units.
+template <class F>
+void launch_persistent(const void* kernel, int threads, uint64_t units, rsk_ctx* c, F&& launch) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    per_cu = 1;
+  }
+  launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)per_cu * (uint64_t)c->num_cus)));
+}
+
+uint32_t nbits(uint64_t v) {  // bits needed to hold v (0 -> 0)
+  uint32_t b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b;
+}
+
+}  // namespace
+
+bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
+  const int mode = st_mode();
+  const uint64_t k = (uint64_t)b->k;
+  const uint64_t nslices = ((uint64_t)b->size + (1ull << SL_LOG) - 1) >> SL_LOG;
+  if (mode == 0 || k > 16 || nslices > SL_MAX || keys.n == 0) return false;
+  if (mode < 0 && keys.n * k < (1ull << 22)) return false;  // small batches: direct atomics
+  const bool f16 =
+      keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
+  const uint32_t kmax = k <= 8 ? 8 : 16;
+  const uint32_t t1 = env_u32("RSK_BLOOM_ST_T1", T1_DEFAULT) == 1024 ? 1024 : 512;
+  const uint64_t kst = (uint64_t)t1 * (16 / kmax);
+  const uint32_t sb = nbits(nslices - 1);
+  const uint32_t f2 = sb > 8 ? sb - 8 : 0;
+  const uint32_t shift1 = SL_LOG + f2;
+  const uint32_t nb1 = (uint32_t)(((nslices - 1) >> f2) + 1);
+  const uint32_t nb2 = 1u << f2;
+  const uint32_t ns = (uint32_t)nslices;
+  const uint32_t cus = (uint32_t)c->num_cus;
+  const uint32_t P = f2 ? std::max<uint32_t>(1, (4 * cus + nb1 - 1) / nb1) : 1;
+  const uint32_t ncp = nb1 * P;
+  uint64_t chunk = std::max<uint64_t>(1, probe_chunk() / k / kst) * kst;  // keys per chunk, whole super-tiles
+  chunk = std::min<uint64_t>(chunk, keys.n);
+  const uint64_t max_nst = (chunk + kst - 1) / kst;
+  const uint64_t max_np = max_nst * kst * k;
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  // tile-budget bound of the whole chunk (sum over (c, p) of tile_budget)
+  const uint64_t tt_max = 2 * ((max_np / 64 + (uint64_t)nb1 * max_nst) / (16 * R2)) + 4ull * ncp + 64;
+  const uint64_t h1_bytes = al(max_nst * (nb1 + 1) * 2);
+  const uint64_t h2_bytes = f2 ? al(tt_max * (nb2 + 1) * 2) : 0;
+  const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + 256;
+  const uint64_t bytes = al(4 * max_np) * (f2 ? 2 : 1) + 2 * h1_bytes + 2 * h2_bytes + (f2 ? al(8 * tt_max) : 0) + meta;
+  uint8_t* w = c->work(bytes);
+  uint8_t* q = w;
+  auto take = [&](uint64_t n) {
+    uint8_t* r = q;
+    q += n;
+    return r;
+  };
+  uint32_t* l1 = reinterpret_cast<uint32_t*>(take(al(4 * max_np)));
+  uint32_t* l2 = f2 ? reinterpret_cast<uint32_t*>(take(al(4 * max_np))) : nullptr;
+  uint16_t* h1 = reinterpret_cast<uint16_t*>(take(h1_bytes));
+  uint16_t* h1t = reinterpret_cast<uint16_t*>(take(h1_bytes));
+  uint16_t* h2 = reinterpret_cast<uint16_t*>(take(h2_bytes));
+  uint16_t* h2t = reinterpret_cast<uint16_t*>(take(h2_bytes));
+  uint64_t* tb2 = f2 ? reinterpret_cast<uint64_t*>(take(al(8 * tt_max))) : nullptr;
+  uint64_t* tot = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
+  uint64_t* reg_off = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
+  uint32_t* bud = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* tile_off = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* used = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* overflow = reinterpret_cast<uint32_t*>(take(256));
+
+  std::vector<DevKeys> redo;
+  for (uint64_t first = 0; first < keys.n; first += chunk) {
+    const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
+    const uint64_t nst = (m + kst - 1) / kst;
+    DevKeys dk = keys;
+    dk.n = m;
+    if (keys.offsets) dk.offsets = keys.offsets + first;
+    else dk.data = keys.data + first * keys.fixed_len;
+    {
+      ProfScope ps(c, "bloom_st1");
+#define RSK_ST1(F16, KM, TT)                                                                                   \
+  launch_persistent((const void*)bloom_st1_kernel<F16, KM, TT>, TT, nst, c, [&](uint32_t grid) {            \
+    hipLaunchKernelGGL((bloom_st1_kernel<F16, KM, TT>), dim3(grid), dim3(TT), 0, c->stream, dk.data,         \
+                       dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, l1, h1);                   \
+  })
+      if (t1 == 1024) {
+        if (f16 && kmax == 8) RSK_ST1(true, 8, 1024);
+        else if (f16) RSK_ST1(true, 16, 1024);
+        else if (kmax == 8) RSK_ST1(false, 8, 1024);
+        else RSK_ST1(false, 16, 1024);
+      } else {
+        if (f16 && kmax == 8) RSK_ST1(true, 8, 512);
+        else if (f16) RSK_ST1(true, 16, 512);
+        else if (kmax == 8) RSK_ST1(false, 8, 512);
+        else RSK_ST1(false, 16, 512);
+      }
+#undef RSK_ST1
+      RSK_CHECK_LAUNCH("bloom_st1");
+    }
+    {
+      ProfScope ps(c, "bloom_st_mid");
+      hipLaunchKernelGGL(st_transpose_kernel, dim3((uint32_t)((nst + 63) / 64), (nb1 + 1 + 63) / 64), dim3(256), 0,
+                         c->stream, h1, nst, nb1 + 1, h1t);
+      RSK_CHECK_LAUNCH("bloom_st_transpose1");
+      if (f2) {
+        hipLaunchKernelGGL(st_size_kernel, dim3(ncp), dim3(256), 0, c->stream, h1t, nst, P,
+                           env_u32("RSK_BLOOM_ST_TINY_BUDGET", 0) ? 1 : 0, tot, bud);
+        RSK_CHECK_LAUNCH("bloom_st_size");
+        hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot, bud, ncp, reg_off, tile_off);
+        RSK_CHECK_LAUNCH("bloom_st_offsets");
+        RSK_HIP(hipMemsetAsync(overflow, 0, 4, c->stream));
+      }
+    }
+    if (f2) {
+      {
+        ProfScope ps(c, "bloom_st2");
+        hipLaunchKernelGGL(bloom_st2_kernel, dim3(ncp), dim3(T2), 0, c->stream, l1, h1t, nst, kst * k, P, nb2,
+                           reg_off, tile_off, bud, used, l2, h2, tb2, overflow);
+        RSK_CHECK_LAUNCH("bloom_st2");
+      }
+      {
+        ProfScope ps(c, "bloom_st_mid");
+        hipLaunchKernelGGL(st_transpose_kernel, dim3((uint32_t)((tt_max + 63) / 64), (nb2 + 1 + 63) / 64), dim3(256),
+                           0, c->stream, h2, tt_max, nb2 + 1, h2t);
+        RSK_CHECK_LAUNCH("bloom_st_transpose2");
+      }
+    }
+    {
+      ProfScope ps(c, "bloom_st_apply");
+      launch_persistent((const void*)bloom_st_apply_kernel, TA, ns, c, [&](uint32_t grid) {
+        if (f2)
+          hipLaunchKernelGGL(bloom_st_apply_kernel, dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2, tb2,
+                             (uint64_t)0, (uint64_t)0, tile_off, used, P, ns, b->d_bits, b->nwords);
+        else
+          hipLaunchKernelGGL(bloom_st_apply_kernel, dim3(grid), dim3(TA), 0, c->stream, l1, h1t, nst, 0u,
+                             (const uint64_t*)nullptr, kst * k, nst, (const uint32_t*)nullptr,
+                             (const uint32_t*)nullptr, 1u, ns, b->d_bits, b->nwords);
+      });
+      RSK_CHECK_LAUNCH("bloom_st_apply");
+    }
+    if (f2) {
+      uint32_t ov = 0;
+      RSK_HIP(hipMemcpyAsync(c->h_small + 8448, overflow, 4, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      std::memcpy(&ov, c->h_small + 8448, 4);
+      if (ov) redo.push_back(dk);
+    }
+  }
+  // A (c, p) that ran out of tile budget (only adversarial inputs can) left
+  // some probes of its chunk unapplied.  ORing is idempotent, so such a chunk
+  // is simply redone by the exact-offset pipeline (after the loop: it may
+  // regrow the scratch the pointers above live in).
+  for (const DevKeys& dk : redo)
+    if (!bloom_add_partitioned(c, b, dk)) bloom_add_direct_launch(c, b, dk);
+  return true;
+}
+
+}  // namespace rsk

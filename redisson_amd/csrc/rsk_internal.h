@@ -178,6 +178,10 @@ void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Slice-partitioned add (rsk_bloom_part.hip); false when the direct kernel is used
 // (small batch, k > 4096, filter > 2^34 bits, or RSK_BLOOM_PARTITION=0).
 bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
+// Super-tile partition (rsk_bloom_st.hip); false when not applicable (small
+// batch, k > 16, filter > 2^34 bits, or RSK_BLOOM_ST=0).
+bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
+void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
 // batch is not worth it (or not 16-byte keys): use the direct kernel.
 bool hll_grouped_partition_applies(const DevKeys& k, uint64_t G);

@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
-STAGES = ("bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply", "bloom_add16")
+STAGES = ("bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply", "bloom_st1", "bloom_st_mid",
+          "bloom_st2", "bloom_st_apply", "bloom_add16")
 
 
 def main():

@@ -153,15 +153,108 @@ def test_partitioned_add_parity(L, engine, orc, monkeypatch, size, k, n):
     assert np.array_equal(_bits(L, b, size), ref)
 
 
-def test_partitioned_add_matches_direct_c3_size(L, engine, monkeypatch):
-    """At the C3 filter size (9,585,058,377 bits, 18,283 slices, two levels) the
-    partitioned add and the direct atomicOr kernel set identical bits."""
+ST_CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000), (19170117, 7, 300000),
+            (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000), (4014142460, 8, 600000)]
+
+
+@pytest.mark.parametrize("size,k,n", ST_CASES)
+@pytest.mark.parametrize("knobs", ["", "RSK_BLOOM_ST_T1=1024", "RSK_BLOOM_ST_CHUNK=300000",
+                                   "RSK_BLOOM_ST_TINY_BUDGET=1"])
+def test_supertile_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs):
+    """Super-tile partition (rsk_bloom_st.hip, forced on) gives the oracle's bit
+    string: one level (<= 256 slices), two levels (301 and 7,657 slices), k in
+    {1, 2, 5, 7, 8} (2048-key super-tiles) and {9, 16} (1024-key), 1024-lane
+    super-tiles, many chunks, and a tile budget of one tile per (bin, part),
+    which overflows and sends each chunk through the exact-offset fallback."""
+    from redisson_amd import KeyBatch
+
+    monkeypatch.setenv("RSK_BLOOM_ST", "1")
+    for kv in filter(None, knobs.split(",")):
+        key, val = kv.split("=")
+        monkeypatch.setenv(key, val)
+    keys = orc.gen_keys16(0x5EED0003, 0, n)
+    b = _filter(L, engine, size, k)
+    _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)), replies=False)
+    ref = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(ref, size, k, keys, None, 16, n, want=False)
+    assert np.array_equal(_bits(L, b, size), ref)
+    # variable-length keys (blob + offsets, the generic hashing branch) and duplicates
+    rng = np.random.default_rng(k + n)
+    vk = [rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes() for _ in range(4000)]
+    vk += vk[:1000] + [b""]
+    _add(L, b, KeyBatch.from_bytes_list(vk), replies=False)
+    blob, offs = orc.pack_keys(vk)
+    orc.bloom_add_batch(ref, size, k, blob, offs, want=False)
+    assert np.array_equal(_bits(L, b, size), ref)
+    L.rsk_bloom_destroy(b)
+
+
+@pytest.mark.parametrize("knobs", ["", "RSK_BLOOM_ST_TINY_BUDGET=1"])
+def test_supertile_skewed_keys(L, engine, orc, monkeypatch, knobs):
+    """One key repeated 300,000 times plus a few distinct ones: every probe of
+    the repeated key lands in the same k slices (one long segment per super-tile
+    and bin), so st2 tiles and apply segments are full-length runs."""
+    from redisson_amd import KeyBatch
+
+    monkeypatch.setenv("RSK_BLOOM_ST", "1")
+    for kv in filter(None, knobs.split(",")):
+        key, val = kv.split("=")
+        monkeypatch.setenv(key, val)
+    size, k = 157298745, 7
+    base = orc.gen_keys16(0x5EED0003, 0, 1000).reshape(-1, 16)
+    keys = np.concatenate([np.repeat(base[:1], 300000, axis=0), base[1:]]).reshape(-1)
+    b = _filter(L, engine, size, k)
+    _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)), replies=False)
+    ref = np.zeros((size + 7) // 8, np.uint8)
+    orc.bloom_add_batch(ref, size, k, keys, None, 16, keys.size // 16, want=False)
+    assert np.array_equal(_bits(L, b, size), ref)
+    L.rsk_bloom_destroy(b)
+
+
+def test_supertile_matches_direct_c3_size(L, engine, monkeypatch):
+    """At the C3 filter size (9,585,058,377 bits, 18,283 slices: 143 coarse bins
+    x 128 slices) the super-tile insert and the direct atomicOr kernel set
+    identical bits."""
     from redisson_amd import _lib, devmem
 
     size, k, n = 9585058377, 7, 3_000_000
     ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
     ks = ins.keys_fixed(n, 16).as_struct()
     filters = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RSK_BLOOM_ST", mode)
+        monkeypatch.setenv("RSK_BLOOM_PARTITION", "0")
+        f = _filter(L, engine, size, k)
+        _lib.check(L.rsk_bloom_add(f, ctypes.byref(ks), None))
+        filters[mode] = f
+    engine.sync()
+    counts = {}
+    for mode, f in filters.items():
+        bc = ctypes.c_uint64()
+        _lib.check(L.rsk_bloom_bitcount(f, ctypes.byref(bc)))
+        counts[mode] = bc.value
+    assert counts["1"] == counts["0"] > 0.99 * n * k
+    nbytes = (size + 7) // 8
+    _lib.check(L.rsk_bloom_or_bits(filters["1"], L.rsk_bloom_device_bits(filters["0"]), nbytes, _lib.RSK_MEM_DEVICE))
+    bc = ctypes.c_uint64()
+    _lib.check(L.rsk_bloom_bitcount(filters["1"], ctypes.byref(bc)))
+    assert bc.value == counts["0"]
+    for f in filters.values():
+        L.rsk_bloom_destroy(f)
+    ins.free()
+
+
+def test_partitioned_add_matches_direct_c3_size(L, engine, monkeypatch):
+    """At the C3 filter size (9,585,058,377 bits, 18,283 slices, two levels) the
+    exact-offset partitioned add (the k > 16 path and the super-tile fallback)
+    and the direct atomicOr kernel set identical bits."""
+    from redisson_amd import _lib, devmem
+
+    size, k, n = 9585058377, 7, 3_000_000
+    ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
+    ks = ins.keys_fixed(n, 16).as_struct()
+    filters = {}
+    monkeypatch.setenv("RSK_BLOOM_ST", "0")
     for mode in ("1", "0"):
         monkeypatch.setenv("RSK_BLOOM_PARTITION", mode)
         f = _filter(L, engine, size, k)
