@@ -43,9 +43,10 @@ constexpr int SL_LOG = 19;                             // bits per slice
 constexpr uint32_t SL_WORDS = 1u << (SL_LOG - 5);      // 16384 u32 = 64 KiB of LDS
 constexpr uint32_t SL_MAX = 32768;                     // slices (2^34 bits) handled here
 constexpr int T1_DEFAULT = 512;                        // st1 workgroup (RSK_BLOOM_ST_T1 = 512 | 1024)
-constexpr int T2 = 1024;                               // st2 workgroup (16 waves)
+constexpr int T2_DEFAULT = 1024;                       // st2 workgroup (RSK_BLOOM_ST_T2 = 512 | 1024)
 constexpr int R2 = 14;                                 // st2 probe slots per lane
 constexpr int TA = 1024;                               // apply workgroup
+constexpr int UA_DEFAULT = 8;                          // apply: segments loaded at once per wave (RSK_BLOOM_ST_UA = 4 | 8)
 constexpr uint32_t INVALID = 0xFFFFFFFFu;              // no probe (payloads are < 2^26)
 constexpr uint64_t DEFAULT_PROBE_CHUNK = 1ull << 33;   // probes per chunk (2 x 32 GiB of scratch)
 
@@ -84,8 +85,51 @@ RSK_DEV void key_words(const uint4& v, uint64_t* w0, uint64_t* w1) {
 }
 
 // ------------------------------------------------------------------- st1
+// Wave 0 turns the bin counts (<= 256, 4 per lane) into bin starts: lstart
+// (LDS), the super-tile header row (global, [nb] = total) and the total.
+RSK_DEV uint32_t wave_scan_incl(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x;
+}
+
+template <int NBMAX>
+RSK_DEV void wave0_bin_starts(uint32_t* hist, uint32_t* lstart, uint32_t nb, uint16_t* hdr_row, uint32_t* s_total) {
+  constexpr int PER = NBMAX / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    v[i] = b < nb ? hist[b] : 0;
+    if (b < nb) hist[b] = 0;  // reset for the next tile (visible after the next barrier)
+    sum += v[i];
+  }
+  const uint32_t incl = wave_scan_incl(sum, lane);
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    if (b < nb) {
+      lstart[b] = run;
+      hdr_row[b] = (uint16_t)run;
+    }
+    run += v[i];
+  }
+  const uint32_t total = rdl(incl, 63);
+  if (lane == 0) {
+    hdr_row[nb] = (uint16_t)total;
+    *s_total = total;
+  }
+}
+
 // Super-tile st = keys [st*KST, st*KST + KST): bin-sorted probes at
 // out[st * KST * k ...], header hdr[st][0..nb1] (bin offsets, [nb1] = total).
+// The sorted image is double-buffered in LDS, so a tile's write-out overlaps
+// the next tile's hashing: three barriers per super-tile.
 template <bool FIXED16, int KMAX, int T1>
 __global__ __launch_bounds__(T1) void bloom_st1_kernel(const uint8_t* __restrict__ data,
                                                        const uint64_t* __restrict__ offsets, uint32_t fixed_len,
@@ -95,8 +139,8 @@ __global__ __launch_bounds__(T1) void bloom_st1_kernel(const uint8_t* __restrict
   constexpr int KPL = 16 / KMAX;        // keys per lane
   constexpr uint32_t KST = T1 * KPL;    // keys per super-tile
   constexpr int NP = KPL * KMAX;        // probe slots per lane (16)
-  __shared__ __attribute__((aligned(16))) uint32_t srt[T1 * NP];
-  __shared__ uint32_t hist[256], lstart[256], wsum[T1 / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t srt[2][T1 * NP];
+  __shared__ uint32_t hist[256], lstart[256], s_total;
   const uint64_t low = (1ull << shift1) - 1;
   const uint64_t stride = (uint64_t)KST * (uint64_t)k;
   if (threadIdx.x < 256) hist[threadIdx.x] = 0;
@@ -110,14 +154,15 @@ __global__ __launch_bounds__(T1) void bloom_st1_kernel(const uint8_t* __restrict
     }
   };
   if (FIXED16) fetch(blockIdx.x);
-  for (uint64_t st = blockIdx.x; st < nst; st += gridDim.x) {
+  __syncthreads();  // hist zeroed
+  uint32_t buf = 0;
+  for (uint64_t st = blockIdx.x; st < nst; st += gridDim.x, buf ^= 1) {
     const uint64_t k0 = st * KST;
     const uint32_t nk = (uint32_t)(n - k0 < KST ? n - k0 : KST);
     uint4 cur[KPL];
 #pragma unroll
     for (int u = 0; u < KPL; ++u) cur[u] = nxt[u];
     if (FIXED16) fetch(st + gridDim.x);  // the next super-tile's keys stream in meanwhile
-    __syncthreads();  // srt free (previous write-out done), hist reset visible
     uint32_t pay[NP], tag[NP];
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
@@ -149,28 +194,23 @@ __global__ __launch_bounds__(T1) void bloom_st1_kernel(const uint8_t* __restrict
         }
       }
     }
-    __syncthreads();
-    const uint32_t cnt = threadIdx.x < nb1 ? hist[threadIdx.x] : 0;
-    uint32_t total;
-    const uint32_t ex = block_scan<T1>(cnt, &total, wsum);
-    if (threadIdx.x < nb1) {
-      lstart[threadIdx.x] = ex;
-      hist[threadIdx.x] = 0;
-    }
-    if (threadIdx.x <= nb1) hdr[st * (nb1 + 1) + threadIdx.x] = (uint16_t)(threadIdx.x < nb1 ? ex : total);
-    __syncthreads();
+    __syncthreads();  // (A) every rank taken
+    if (threadIdx.x < 64) wave0_bin_starts<256>(hist, lstart, nb1, hdr + st * (nb1 + 1), &s_total);
+    __syncthreads();  // (B) lstart / total ready, hist zeroed
+    uint32_t* img = srt[buf];  // last read by the write-out of st - 2 gridDim.x, before every wave reached (B)
 #pragma unroll
     for (int s = 0; s < NP; ++s)
-      if (tag[s] != INVALID) srt[lstart[tag[s] >> 16] + (tag[s] & 0xFFFFu)] = pay[s];
-    __syncthreads();
-    uint4* o4 = reinterpret_cast<uint4*>(out + st * stride);  // 16-byte aligned: stride = 1024*16/KMAX*k... * 4 B
-    const uint4* s4 = reinterpret_cast<const uint4*>(srt);
+      if (tag[s] != INVALID) img[lstart[tag[s] >> 16] + (tag[s] & 0xFFFFu)] = pay[s];
+    const uint32_t total = s_total;
+    __syncthreads();  // (C) image complete
+    uint4* o4 = reinterpret_cast<uint4*>(out + st * stride);  // 16-byte aligned (stride * 4 B = 16 KiB * k)
+    const uint4* s4 = reinterpret_cast<const uint4*>(img);
     for (uint32_t j = threadIdx.x; j < total / 4; j += T1) {
       const uint4 v = s4[j];
       u32x4 x = {v.x, v.y, v.z, v.w};
       __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(o4 + j));
     }
-    for (uint32_t j = (total & ~3u) + threadIdx.x; j < total; j += T1) out[st * stride + j] = srt[j];
+    for (uint32_t j = (total & ~3u) + threadIdx.x; j < total; j += T1) out[st * stride + j] = img[j];
   }
 }
 
@@ -204,12 +244,16 @@ RSK_DEV void part_range(uint64_t nst, uint32_t P, uint32_t p, uint64_t* t0, uint
   *t1 = nst * (p + 1) / P;
 }
 
-RSK_DEV uint32_t tile_budget(uint64_t probes, uint64_t segs) {
-  return (uint32_t)(2 * ((probes / 64 + segs) / (16 * R2)) + 4);
+// A st2 tile holds `slots` = waves x R2 slots of 64 probes; a slot is short
+// only when it ends a segment, so a (c, p) needs at most
+// (probes / 64 + segments) / slots tiles when its waves stay balanced; twice
+// that is budgeted (an overflow is caught and redone, see bloom_add_supertile).
+RSK_DEV uint32_t tile_budget(uint64_t probes, uint64_t segs, uint32_t slots) {
+  return (uint32_t)(2 * ((probes / 64 + segs) / slots) + 4);
 }
 
 __global__ __launch_bounds__(256) void st_size_kernel(const uint16_t* __restrict__ h1t, uint64_t nst, uint32_t P,
-                                                      int tiny_budget, uint64_t* __restrict__ tot,
+                                                      uint32_t slots, int tiny_budget, uint64_t* __restrict__ tot,
                                                       uint32_t* __restrict__ bud) {
   __shared__ uint64_t part[4];
   const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
@@ -225,7 +269,7 @@ __global__ __launch_bounds__(256) void st_size_kernel(const uint16_t* __restrict
   if (threadIdx.x == 0) {
     const uint64_t total = part[0] + part[1] + part[2] + part[3];
     tot[cp] = total;
-    bud[cp] = tiny_budget ? 1u : tile_budget(total, t1 - t0);  // tiny: tests of the overflow fallback
+    bud[cp] = tiny_budget ? 1u : tile_budget(total, t1 - t0, slots);  // tiny: tests of the overflow fallback
   }
 }
 
@@ -274,9 +318,13 @@ __global__ __launch_bounds__(1024) void st_offsets_kernel(const uint64_t* __rest
 
 // ------------------------------------------------------------------- st2
 // Workgroup (c, p): segment c of the st1 tiles of part p -- wave w takes the
-// groups of 64 consecutive tiles t0 + 64 (w + 16 i) + [0, 64) -- bin-sorted
-// by fine bin (pay >> 19) into tiles written contiguously at out + reg_off[cp];
-// tile j of (c, p) gets header h2[tile_off[cp] + j][0..nb2] and its start tb2.
+// groups of 64 consecutive tiles t0 + 64 (w + NW i) + [0, 64), one coalesced
+// header load per group (the next group prefetched) -- bin-sorted by fine bin
+// (pay >> 19) into tiles written contiguously at out + reg_off[cp]; tile j of
+// (c, p) gets header h2[tile_off[cp] + j][0..nb2] and its start tb2.
+// A wave's R2 slots per tile are chunks of 64 probes of its cached segments:
+// the chunk -> segment map is a ballot over the lanes' chunk prefix sums.
+template <int T2>
 __global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restrict__ in,
                                                        const uint16_t* __restrict__ h1t, uint64_t nst,
                                                        uint64_t stride1, uint32_t P, uint32_t nb2,
@@ -284,99 +332,111 @@ __global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restric
                                                        const uint32_t* __restrict__ tile_off,
                                                        const uint32_t* __restrict__ bud, uint32_t* __restrict__ used,
                                                        uint32_t* __restrict__ out, uint16_t* __restrict__ h2,
-                                                       uint64_t* __restrict__ tb2, uint32_t* __restrict__ overflow) {
-  __shared__ __attribute__((aligned(16))) uint32_t srt[T2 * R2];
-  __shared__ uint32_t hist[128], lstart[128], wsum[T2 / 64];
+                                                       uint64_t* __restrict__ tb2, uint32_t* __restrict__ overflow,
+                                                       uint32_t dbg) {
+  constexpr uint32_t NW = T2 / 64;
+  __shared__ __attribute__((aligned(16))) uint32_t srt[2][T2 * R2];
+  __shared__ uint32_t hist[128], lstart[128], s_total;
+  __shared__ uint16_t s_hdr[129];
   const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index as a scalar: every per-wave cursor below stays in SGPRs
+  const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint64_t t0, t1;
   part_range(nst, P, p, &t0, &t1);
   const uint16_t* ha = h1t + (uint64_t)c * nst;
   const uint16_t* hb = ha + nst;
   if (threadIdx.x < 128) hist[threadIdx.x] = 0;
-  // wave-uniform cursor over a cache of 64 segments (one per lane, coalesced header loads)
-  uint64_t gbase = t0 + 64ull * w, cpos = 0, cur_pos = 0;
-  uint32_t ci = 64, clen = 0, cur_len = 0, off = 0;
-  bool have = true;
-  auto next_seg = [&]() {
-    while (true) {
-      if (ci == 64) {
-        if (gbase >= t1) return false;
-        const uint64_t t = gbase + lane;
-        if (t < t1) {
-          const uint32_t a = ha[t];
-          clen = (uint32_t)hb[t] - a;
-          cpos = t * stride1 + a;
-        } else {
-          clen = 0;
-          cpos = 0;
-        }
-        ci = 0;
-        gbase += 64ull * (T2 / 64);
-      }
-      const uint32_t len = rdl(clen, ci);
-      const uint64_t pos = rdl64(cpos, ci);
-      ++ci;
-      if (len) {
-        cur_len = len;
-        cur_pos = pos;
-        off = 0;
-        return true;
-      }
+  // segment cache (lane l: segment of tile g + l) and the prefetched next group
+  uint64_t g_next = t0 + 64ull * w;
+  uint32_t plen = 0, clen = 0;
+  uint64_t ppos = 0, cpos = 0;
+  bool pvalid = false;
+  auto load_group = [&]() {
+    pvalid = g_next < t1;
+    const uint64_t t = g_next + lane;
+    plen = 0;
+    ppos = 0;
+    if (t < t1) {
+      const uint32_t a = ha[t];
+      plen = (uint32_t)hb[t] - a;
+      ppos = t * stride1 + a;
     }
+    g_next += 64ull * NW;
   };
-  have = next_seg();
+  uint32_t pref = 0, ct = 0, q = 0;  // inclusive chunk prefix (per lane), chunks in cache, next chunk
+  auto refill = [&]() {  // make q < ct; false when this wave's segments are exhausted
+    while (q >= ct) {
+      if (!pvalid) return false;
+      clen = plen;
+      cpos = ppos;
+      pref = wave_scan_incl((clen + 63) >> 6, lane);
+      ct = rdl(pref, 63);
+      q = 0;
+      load_group();
+    }
+    return true;
+  };
+  load_group();
+  bool have = refill();
   const uint64_t base = reg_off[cp];
   const uint32_t tbeg = tile_off[cp], tcap = bud[cp];
   uint64_t written = 0;
-  uint32_t ntile = 0;
+  uint32_t ntile = 0, buf = 0;
+  __syncthreads();  // hist zeroed
   for (;;) {
     uint32_t pay[R2], tag[R2];
 #pragma unroll
     for (int r = 0; r < R2; ++r) {
-      if (have && off >= cur_len) have = next_seg();
       pay[r] = INVALID;
       if (have) {
-        const uint32_t j = off + lane;
-        if (j < cur_len) pay[r] = __builtin_nontemporal_load(&in[cur_pos + j]);
-        off += 64;
+        const uint32_t sg = (uint32_t)__builtin_popcountll(__ballot(pref <= q));  // segment of chunk q
+        const uint32_t first = sg ? rdl(pref, sg - 1) : 0;
+        const uint32_t o = (q - first) * 64 + lane;
+        if (o < rdl(clen, sg)) pay[r] = __builtin_nontemporal_load(&in[rdl64(cpos, sg) + o]);
+        ++q;
+        if (q >= ct) have = refill();
       }
     }
-    if (have && off >= cur_len) have = next_seg();  // "more input" must be exact for the loop exit
-    __syncthreads();  // srt free, hist reset visible
 #pragma unroll
     for (int r = 0; r < R2; ++r) {
       tag[r] = INVALID;
       if (pay[r] != INVALID) {
         const uint32_t bin = pay[r] >> SL_LOG;
-        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+        tag[r] = (dbg & 1) ? (bin << 16) : (bin << 16) | atomicAdd(&hist[bin], 1u);
       }
     }
-    const int more = __syncthreads_or(have ? 1 : 0);
-    const uint32_t cnt = threadIdx.x < nb2 ? hist[threadIdx.x] : 0;
-    uint32_t total;
-    const uint32_t ex = block_scan<T2>(cnt, &total, wsum);
-    if (threadIdx.x < nb2) {
-      lstart[threadIdx.x] = ex;
-      hist[threadIdx.x] = 0;
+    if (dbg & 4) {  // timing-only (RSK_BLOOM_ST2_DBG): input side alone
+      uint32_t acc = 0;
+#pragma unroll
+      for (int r = 0; r < R2; ++r) acc ^= pay[r];
+      if (acc == 0x12345678u) overflow[1] = acc;
+      if (!__syncthreads_or(have ? 1 : 0)) break;
+      continue;
     }
+    const int more = __syncthreads_or(have ? 1 : 0);  // (A) every rank taken
+    if (threadIdx.x < 64) wave0_bin_starts<128>(hist, lstart, nb2, s_hdr, &s_total);
+    __syncthreads();  // (B)
+    const uint32_t total = s_total;
     if (total) {
       if (ntile < tcap) {
-        if (threadIdx.x <= nb2)
-          h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = (uint16_t)(threadIdx.x < nb2 ? ex : total);
+        if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
         if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
       } else if (threadIdx.x == 0) {
         atomicOr(overflow, 1u);  // budget exceeded (adversarial input): the host redoes the chunk
       }
-      __syncthreads();
+      uint32_t* img = srt[buf];
+      if (!(dbg & 1)) {
 #pragma unroll
-      for (int r = 0; r < R2; ++r)
-        if (tag[r] != INVALID) srt[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
-      __syncthreads();
+        for (int r = 0; r < R2; ++r)
+          if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
+      }
+      __syncthreads();  // (C) image complete
       uint32_t* o = out + base + written;
-      for (uint32_t j = threadIdx.x; j < total; j += T2) o[j] = srt[j];
+      if (!(dbg & 2))
+        for (uint32_t j = threadIdx.x; j < total; j += T2) o[j] = img[j];
       written += total;
       ++ntile;
+      buf ^= 1;
     }
     if (!more) break;
   }
@@ -389,6 +449,7 @@ __global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restric
 // segment f = s & (2^f2 - 1), rows f / f+1 of the transposed st2 headers, tile
 // starts tb[tile].  One level (f2 = 0, tile_off == nullptr): the st1 tiles
 // [0, nst), rows s / s+1 of the transposed st1 headers, tile t at t * stride.
+template <int UA>
 __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __restrict__ probes,
                                                             const uint16_t* __restrict__ ht, uint64_t row_stride,
                                                             uint32_t f2, const uint64_t* __restrict__ tb,
@@ -398,7 +459,8 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
                                                             uint32_t nslices, uint32_t* __restrict__ bits,
                                                             uint64_t nwords) {
   __shared__ __attribute__((aligned(16))) uint32_t sl[SL_WORDS];
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index as a scalar: every per-wave cursor below stays in SGPRs
+  const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   constexpr uint32_t NW = TA / 64;
   for (uint32_t s = blockIdx.x; s < nslices; s += gridDim.x) {
     const uint64_t w0 = (uint64_t)s * SL_WORDS;
@@ -420,21 +482,30 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
         ta = 0;
         te = nst;
       }
-      // wave w: groups of 64 consecutive tiles ta + 64 (w + NW i), one coalesced header load each
-      for (uint64_t g = ta + 64ull * w; g < te; g += 64ull * NW) {
-        const uint64_t t = g + lane;
-        uint32_t beg = 0, len = 0;
-        uint64_t pos = 0;
+      // wave w: groups of 64 consecutive tiles ta + 64 (w + NW i), one coalesced
+      // header load each, the next group's issued before this one is processed
+      uint32_t nlen = 0;
+      uint64_t npos = 0;
+      auto hload = [&](uint64_t gg) {
+        const uint64_t t = gg + lane;
+        nlen = 0;
+        npos = 0;
         if (t < te) {
-          beg = ra[t];
-          len = (uint32_t)rb[t] - beg;
-          pos = (tb ? tb[t] : t * stride) + beg;
+          const uint32_t beg = ra[t];
+          nlen = (uint32_t)rb[t] - beg;
+          npos = (tb ? tb[t] : t * stride) + beg;
         }
+      };
+      hload(ta + 64ull * w);
+      for (uint64_t g = ta + 64ull * w; g < te; g += 64ull * NW) {
+        const uint32_t len = nlen;
+        const uint64_t pos = npos;
+        hload(g + 64ull * NW);
         const uint32_t ng = (uint32_t)(te - g < 64 ? te - g : 64);
-        for (uint32_t j = 0; j < ng; j += 4) {  // 4 segments' loads in flight per lane
-          uint32_t v[8];
+        for (uint32_t j = 0; j < ng; j += UA) {  // UA segments' loads in flight per lane
+          uint32_t v[2 * UA];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < UA; ++q) {
             const uint32_t jj = j + q < ng ? j + q : ng - 1;
             const uint32_t sl_len = (j + q < ng) ? rdl(len, jj) : 0;
             const uint64_t sp = rdl64(pos, jj);
@@ -449,7 +520,7 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
             }
           }
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
+          for (int q = 0; q < 2 * UA; ++q)
             if (v[q] != INVALID) atomicOr(&sl[v[q] >> 5], bloom_bit_mask(v[q]));
         }
       }
@@ -512,6 +583,10 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t kmax = k <= 8 ? 8 : 16;
   const uint32_t t1 = env_u32("RSK_BLOOM_ST_T1", T1_DEFAULT) == 1024 ? 1024 : 512;
   const uint64_t kst = (uint64_t)t1 * (16 / kmax);
+  const uint32_t t2 = env_u32("RSK_BLOOM_ST_T2", T2_DEFAULT) == 512 ? 512 : 1024;
+  const uint32_t slots2 = (t2 / 64) * R2;  // probe slots of 64 per st2 tile
+  const uint32_t ua = env_u32("RSK_BLOOM_ST_UA", UA_DEFAULT) == 8 ? 8 : 4;
+  const uint32_t dbg2 = env_u32("RSK_BLOOM_ST2_DBG", 0);  // timing experiments only: results are wrong when set
   const uint32_t sb = nbits(nslices - 1);
   const uint32_t f2 = sb > 8 ? sb - 8 : 0;
   const uint32_t shift1 = SL_LOG + f2;
@@ -527,7 +602,7 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   // tile-budget bound of the whole chunk (sum over (c, p) of tile_budget)
-  const uint64_t tt_max = 2 * ((max_np / 64 + (uint64_t)nb1 * max_nst) / (16 * R2)) + 4ull * ncp + 64;
+  const uint64_t tt_max = 2 * ((max_np / 64 + (uint64_t)nb1 * max_nst) / slots2) + 4ull * ncp + 64;
   const uint64_t h1_bytes = al(max_nst * (nb1 + 1) * 2);
   const uint64_t h2_bytes = f2 ? al(tt_max * (nb2 + 1) * 2) : 0;
   const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + 256;
@@ -588,7 +663,7 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
                          c->stream, h1, nst, nb1 + 1, h1t);
       RSK_CHECK_LAUNCH("bloom_st_transpose1");
       if (f2) {
-        hipLaunchKernelGGL(st_size_kernel, dim3(ncp), dim3(256), 0, c->stream, h1t, nst, P,
+        hipLaunchKernelGGL(st_size_kernel, dim3(ncp), dim3(256), 0, c->stream, h1t, nst, P, slots2,
                            env_u32("RSK_BLOOM_ST_TINY_BUDGET", 0) ? 1 : 0, tot, bud);
         RSK_CHECK_LAUNCH("bloom_st_size");
         hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot, bud, ncp, reg_off, tile_off);
@@ -599,8 +674,12 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
     if (f2) {
       {
         ProfScope ps(c, "bloom_st2");
-        hipLaunchKernelGGL(bloom_st2_kernel, dim3(ncp), dim3(T2), 0, c->stream, l1, h1t, nst, kst * k, P, nb2,
-                           reg_off, tile_off, bud, used, l2, h2, tb2, overflow);
+        if (t2 == 512)
+          hipLaunchKernelGGL(bloom_st2_kernel<512>, dim3(ncp), dim3(512), 0, c->stream, l1, h1t, nst, kst * k, P,
+                             nb2, reg_off, tile_off, bud, used, l2, h2, tb2, overflow, dbg2);
+        else
+          hipLaunchKernelGGL(bloom_st2_kernel<1024>, dim3(ncp), dim3(1024), 0, c->stream, l1, h1t, nst, kst * k, P,
+                             nb2, reg_off, tile_off, bud, used, l2, h2, tb2, overflow, dbg2);
         RSK_CHECK_LAUNCH("bloom_st2");
       }
       {
@@ -612,15 +691,19 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
     }
     {
       ProfScope ps(c, "bloom_st_apply");
-      launch_persistent((const void*)bloom_st_apply_kernel, TA, ns, c, [&](uint32_t grid) {
-        if (f2)
-          hipLaunchKernelGGL(bloom_st_apply_kernel, dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2, tb2,
-                             (uint64_t)0, (uint64_t)0, tile_off, used, P, ns, b->d_bits, b->nwords);
-        else
-          hipLaunchKernelGGL(bloom_st_apply_kernel, dim3(grid), dim3(TA), 0, c->stream, l1, h1t, nst, 0u,
-                             (const uint64_t*)nullptr, kst * k, nst, (const uint32_t*)nullptr,
-                             (const uint32_t*)nullptr, 1u, ns, b->d_bits, b->nwords);
-      });
+#define RSK_APPLY(U)                                                                                            \
+  launch_persistent((const void*)bloom_st_apply_kernel<U>, TA, ns, c, [&](uint32_t grid) {                    \
+    if (f2)                                                                                                     \
+      hipLaunchKernelGGL((bloom_st_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2,    \
+                         tb2, (uint64_t)0, (uint64_t)0, tile_off, used, P, ns, b->d_bits, b->nwords);           \
+    else                                                                                                        \
+      hipLaunchKernelGGL((bloom_st_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l1, h1t, nst, 0u,       \
+                         (const uint64_t*)nullptr, kst * k, nst, (const uint32_t*)nullptr,                      \
+                         (const uint32_t*)nullptr, 1u, ns, b->d_bits, b->nwords);                               \
+  })
+      if (ua == 8) RSK_APPLY(8);
+      else RSK_APPLY(4);
+#undef RSK_APPLY
       RSK_CHECK_LAUNCH("bloom_st_apply");
     }
     if (f2) {

@@ -25,6 +25,7 @@ def find(d, pattern):
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
 
 

@@ -10,6 +10,7 @@ from collections import defaultdict
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
 
 
