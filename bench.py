@@ -154,7 +154,7 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
     add_ms, add_n = engine.prof_read("bloom_add16")
     con_ms, con_n = engine.prof_read("bloom_contains16")
     stages = {}
-    for name in ("bloom_pg1", "bloom_pg_mid", "bloom_pg2", "bloom_pg_apply", "bloom_st1", "bloom_st_mid", "bloom_st2", "bloom_st_apply",
+    for name in ("bloom_st1", "bloom_st_mid", "bloom_st2", "bloom_st_apply",
                  "bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply"):
         ms, cnt = engine.prof_read(name)
         if cnt:

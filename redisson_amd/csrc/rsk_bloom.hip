@@ -254,7 +254,6 @@ void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k) {
   if (k.n == 0) return;
   ProfScope ps(c, fixed16(k) ? "bloom_add16" : "bloom_add");
-  if (bloom_add_paged(c, b, k)) return;
   if (bloom_add_supertile(c, b, k)) return;
   if (bloom_add_partitioned(c, b, k)) return;
   bloom_add_direct_launch(c, b, k);

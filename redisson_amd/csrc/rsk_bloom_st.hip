@@ -6,23 +6,27 @@
 // any order; this path routes them to 64 KiB slices of the filter (2^19 bits)
 // and ORs each slice in LDS, without knowing any count in advance:
 //
-//   st1   : one pass over the keys.  A super-tile = 2048 keys (k <= 8) or 1024
-//           (k <= 16): each lane hashes its keys once (XXH64 + farmhash), keeps
-//           its <= 16 probes in registers, ranks them by coarse bin (idx >>
-//           (19 + f2), <= 256 bins) with one LDS atomic each, places them in
-//           LDS and writes the bin-sorted super-tile CONTIGUOUSLY at its own
-//           slot (probes 26 bits: the position inside the coarse bin) plus a
-//           u16 header of bin offsets.  No histogram pass, no global offsets.
+//   st1   : one pass over the keys.  A super-tile = 2 keys per lane (k <= 8) or
+//           1 (k <= 16) of a 512-lane workgroup: each lane hashes its keys once
+//           (XXH64 + farmhash), keeps its <= 16 probes in registers, ranks them
+//           by coarse bin (idx >> (19 + f2), <= 256 bins) with one LDS atomic
+//           each, places them in an LDS image (double-buffered: the write-out
+//           of one super-tile overlaps the hashing of the next) and writes the
+//           bin-sorted super-tile CONTIGUOUSLY at its own slot (probes 26 bits:
+//           the position inside the coarse bin) plus a u16 header of bin
+//           offsets.  No histogram pass, no global offsets.
 //   hdrT  : header transposed to [bin][super-tile] (coalesced reads below).
 //   size  : per (coarse bin c, part p): probes and a tile budget for st2.
 //   st2   : one workgroup per (c, p) reads segment c of the super-tiles of
-//           part p (16 waves, each its own interleaved segment list, R probe
-//           slots per lane filled by 64-lane loads), ranks by fine bin (the
-//           2^f2 slices of c), and writes bin-sorted tiles contiguously into
-//           the (c, p) region, with u16 headers (19-bit slice offsets).
+//           part p (16 waves, each its own groups of 64 consecutive
+//           super-tiles, R2 = 14 slots of 64 probes per lane, the chunk ->
+//           segment map a ballot over the lanes' chunk prefix sums), ranks by
+//           fine bin (the 2^f2 slices of c), and writes bin-sorted tiles
+//           contiguously into the (c, p) region, with u16 headers (19-bit
+//           slice offsets).
 //   apply : one workgroup per slice: 64 KiB of filter in LDS, every segment
-//           of that slice in the tiles of its coarse bin ORed in with ds_or,
-//           the slice written back once.
+//           of that slice in the tiles of its coarse bin ORed in with ds_or
+//           (UA segments' loads in flight per wave), the slice written back once.
 // Filters of <= 256 slices skip st2 (apply reads the st1 tiles directly).
 //
 // HBM per key at k probes: 16 B of key + 4k (st1 write) + 4k + 4k (st2) + 4k
@@ -30,6 +34,9 @@
 // atomic + lstart read + place + read-out (st1, st2) + ds_or (apply).  The
 // earlier pipeline (rsk_bloom_part.hip: histogram pass over the keys, exact
 // global offsets, sbin/dlt scatter) remains for k > 16 and as the fallback.
+// Measured variants: a paged layout (runs appended to 4 KiB
+// pages, whole-page reads) made apply faster but the scattered run writes cost
+// more than the segment reads they replaced.
 #include <cstdlib>
 #include <cstring>
 
@@ -332,8 +339,7 @@ __global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restric
                                                        const uint32_t* __restrict__ tile_off,
                                                        const uint32_t* __restrict__ bud, uint32_t* __restrict__ used,
                                                        uint32_t* __restrict__ out, uint16_t* __restrict__ h2,
-                                                       uint64_t* __restrict__ tb2, uint32_t* __restrict__ overflow,
-                                                       uint32_t dbg) {
+                                                       uint64_t* __restrict__ tb2, uint32_t* __restrict__ overflow) {
   constexpr uint32_t NW = T2 / 64;
   __shared__ __attribute__((aligned(16))) uint32_t srt[2][T2 * R2];
   __shared__ uint32_t hist[128], lstart[128], s_total;
@@ -402,16 +408,8 @@ __global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restric
       tag[r] = INVALID;
       if (pay[r] != INVALID) {
         const uint32_t bin = pay[r] >> SL_LOG;
-        tag[r] = (dbg & 1) ? (bin << 16) : (bin << 16) | atomicAdd(&hist[bin], 1u);
+        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
       }
-    }
-    if (dbg & 4) {  // timing-only (RSK_BLOOM_ST2_DBG): input side alone
-      uint32_t acc = 0;
-#pragma unroll
-      for (int r = 0; r < R2; ++r) acc ^= pay[r];
-      if (acc == 0x12345678u) overflow[1] = acc;
-      if (!__syncthreads_or(have ? 1 : 0)) break;
-      continue;
     }
     const int more = __syncthreads_or(have ? 1 : 0);  // (A) every rank taken
     if (threadIdx.x < 64) wave0_bin_starts<128>(hist, lstart, nb2, s_hdr, &s_total);
@@ -425,15 +423,12 @@ __global__ __launch_bounds__(T2) void bloom_st2_kernel(const uint32_t* __restric
         atomicOr(overflow, 1u);  // budget exceeded (adversarial input): the host redoes the chunk
       }
       uint32_t* img = srt[buf];
-      if (!(dbg & 1)) {
 #pragma unroll
-        for (int r = 0; r < R2; ++r)
-          if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
-      }
+      for (int r = 0; r < R2; ++r)
+        if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
       __syncthreads();  // (C) image complete
       uint32_t* o = out + base + written;
-      if (!(dbg & 2))
-        for (uint32_t j = threadIdx.x; j < total; j += T2) o[j] = img[j];
+      for (uint32_t j = threadIdx.x; j < total; j += T2) o[j] = img[j];
       written += total;
       ++ntile;
       buf ^= 1;
@@ -586,7 +581,6 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t t2 = env_u32("RSK_BLOOM_ST_T2", T2_DEFAULT) == 512 ? 512 : 1024;
   const uint32_t slots2 = (t2 / 64) * R2;  // probe slots of 64 per st2 tile
   const uint32_t ua = env_u32("RSK_BLOOM_ST_UA", UA_DEFAULT) == 8 ? 8 : 4;
-  const uint32_t dbg2 = env_u32("RSK_BLOOM_ST2_DBG", 0);  // timing experiments only: results are wrong when set
   const uint32_t sb = nbits(nslices - 1);
   const uint32_t f2 = sb > 8 ? sb - 8 : 0;
   const uint32_t shift1 = SL_LOG + f2;
@@ -676,10 +670,10 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
         ProfScope ps(c, "bloom_st2");
         if (t2 == 512)
           hipLaunchKernelGGL(bloom_st2_kernel<512>, dim3(ncp), dim3(512), 0, c->stream, l1, h1t, nst, kst * k, P,
-                             nb2, reg_off, tile_off, bud, used, l2, h2, tb2, overflow, dbg2);
+                             nb2, reg_off, tile_off, bud, used, l2, h2, tb2, overflow);
         else
           hipLaunchKernelGGL(bloom_st2_kernel<1024>, dim3(ncp), dim3(1024), 0, c->stream, l1, h1t, nst, kst * k, P,
-                             nb2, reg_off, tile_off, bud, used, l2, h2, tb2, overflow, dbg2);
+                             nb2, reg_off, tile_off, bud, used, l2, h2, tb2, overflow);
         RSK_CHECK_LAUNCH("bloom_st2");
       }
       {

@@ -181,8 +181,6 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Super-tile partition (rsk_bloom_st.hip); false when not applicable (small
 // batch, k > 16, filter > 2^34 bits, or RSK_BLOOM_ST=0).
 bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
-// Paged partition (rsk_bloom_pg.hip); same applicability (RSK_BLOOM_PG=0: off).
-bool bloom_add_paged(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
 // batch is not worth it (or not 16-byte keys): use the direct kernel.

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 from redisson_amd import _lib, devmem  # noqa: E402
 
 STAGES = ("bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply", "bloom_st1", "bloom_st_mid",
-          "bloom_st2", "bloom_st_apply", "bloom_pg1", "bloom_pg_mid", "bloom_pg2", "bloom_pg_apply", "bloom_add16")
+          "bloom_st2", "bloom_st_apply", "bloom_add16")
 
 
 def main():

@@ -137,7 +137,6 @@ def test_partitioned_add_parity(L, engine, orc, monkeypatch, size, k, n):
     from redisson_amd import KeyBatch
 
     monkeypatch.setenv("RSK_BLOOM_PARTITION", "1")
-    monkeypatch.setenv("RSK_BLOOM_PG", "0")
     monkeypatch.setenv("RSK_BLOOM_ST", "0")
     keys = orc.gen_keys16(0x5EED0003, 0, n)
     b = _filter(L, engine, size, k)
@@ -159,22 +158,19 @@ ST_CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000
             (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000), (4014142460, 8, 600000)]
 
 
-PG_KNOBS = ["RSK_BLOOM_PG=1", "RSK_BLOOM_PG=1,RSK_BLOOM_PG_T1=1024", "RSK_BLOOM_PG=1,RSK_BLOOM_PG_CHUNK=300000",
-            "RSK_BLOOM_PG=1,RSK_BLOOM_PG_T2=512", "RSK_BLOOM_PG=1,RSK_BLOOM_PG_UA=8"]
-ST_KNOBS = ["RSK_BLOOM_PG=0,RSK_BLOOM_ST=1", "RSK_BLOOM_PG=0,RSK_BLOOM_ST=1,RSK_BLOOM_ST_T1=1024",
-            "RSK_BLOOM_PG=0,RSK_BLOOM_ST=1,RSK_BLOOM_ST_CHUNK=300000",
-            "RSK_BLOOM_PG=0,RSK_BLOOM_ST=1,RSK_BLOOM_ST_TINY_BUDGET=1"]
+ST_KNOBS = ["RSK_BLOOM_ST=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T1=1024", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_CHUNK=300000",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_ST_TINY_BUDGET=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4"]
 
 
 @pytest.mark.parametrize("size,k,n", ST_CASES)
-@pytest.mark.parametrize("knobs", PG_KNOBS + ST_KNOBS)
+@pytest.mark.parametrize("knobs", ST_KNOBS)
 def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs):
-    """The slice-routed inserts, forced on, give the oracle's bit string: the
-    paged partition (rsk_bloom_pg.hip) and the super-tile one (rsk_bloom_st.hip),
-    one level (<= 256 slices) and two (301 and 7,657 slices), k in {1, 2, 5, 7,
-    8} (2048-key tiles) and {9, 16} (1024-key), 1024-lane tiles, many chunks,
-    512-lane second passes, 8-chunk page loads, and (super-tile) a tile budget
-    of one tile per (bin, part), which overflows into the exact-offset fallback."""
+    """The super-tile insert (rsk_bloom_st.hip), forced on, gives the oracle's
+    bit string: one level (<= 256 slices) and two (301 and 7,657 slices), k in
+    {1, 2, 5, 7, 8} (1024-key super-tiles) and {9, 16} (512-key), 1024-lane
+    super-tiles, many chunks, 512-lane st2 with 4 segments per apply step, and
+    a tile budget of one tile per (bin, part), which overflows into the
+    exact-offset fallback."""
     from redisson_amd import KeyBatch
 
     for kv in filter(None, knobs.split(",")):
@@ -197,11 +193,11 @@ def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs)
     L.rsk_bloom_destroy(b)
 
 
-@pytest.mark.parametrize("knobs", ["RSK_BLOOM_PG=1", "RSK_BLOOM_PG=1,RSK_BLOOM_PG_CHUNK=700000"] + ST_KNOBS)
+@pytest.mark.parametrize("knobs", ST_KNOBS)
 def test_slice_routed_skewed_keys(L, engine, orc, monkeypatch, knobs):
     """One key repeated 300,000 times plus a few distinct ones: every probe of
-    the repeated key lands in the same k slices, so one bin's run fills many
-    pages per tile (blocks of consecutive new pages) / long segments."""
+    the repeated key lands in the same k slices (one long segment per
+    super-tile and bin), so st2 tiles and apply segments are full-length runs."""
     from redisson_amd import KeyBatch
 
     for kv in filter(None, knobs.split(",")):
@@ -218,11 +214,11 @@ def test_slice_routed_skewed_keys(L, engine, orc, monkeypatch, knobs):
     L.rsk_bloom_destroy(b)
 
 
-@pytest.mark.parametrize("path", ["RSK_BLOOM_PG", "RSK_BLOOM_ST"])
+@pytest.mark.parametrize("path", ["RSK_BLOOM_ST"])
 def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, path):
     """At the C3 filter size (9,585,058,377 bits, 18,283 slices: 143 coarse bins
-    x 128 slices) the paged / super-tile insert and the direct atomicOr kernel
-    set identical bits."""
+    x 128 slices) the super-tile insert and the direct atomicOr kernel set
+    identical bits."""
     from redisson_amd import _lib, devmem
 
     size, k, n = 9585058377, 7, 3_000_000
@@ -230,8 +226,6 @@ def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, path):
     ks = ins.keys_fixed(n, 16).as_struct()
     filters = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RSK_BLOOM_PG", "0")
-        monkeypatch.setenv("RSK_BLOOM_ST", "0")
         monkeypatch.setenv(path, mode)
         monkeypatch.setenv("RSK_BLOOM_PARTITION", "0")
         f = _filter(L, engine, size, k)
@@ -265,7 +259,6 @@ def test_partitioned_add_matches_direct_c3_size(L, engine, monkeypatch):
     ks = ins.keys_fixed(n, 16).as_struct()
     filters = {}
     monkeypatch.setenv("RSK_BLOOM_ST", "0")
-    monkeypatch.setenv("RSK_BLOOM_PG", "0")
     for mode in ("1", "0"):
         monkeypatch.setenv("RSK_BLOOM_PARTITION", mode)
         f = _filter(L, engine, size, k)
