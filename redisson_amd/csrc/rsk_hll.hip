@@ -402,14 +402,15 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
     }
     __syncthreads();  // [B] stage written, class counts final
     if (cur_staged) {
-      if (tid == 0) {  // class starts: one lane's exclusive prefix over the counts
-        uint32_t acc = 0;
+      if (tid < 64) {  // class starts: wave 0's exclusive prefix over the counts (one LDS read per lane)
+        const uint32_t v = tid < VAR_NCLS_PAD ? cnt[tid] : 0;
+        uint32_t x = v;
 #pragma unroll
-        for (int c = 0; c < VAR_NCLS_PAD; ++c) {
-          const uint32_t v = cnt[c];
-          cbase[c] = acc;
-          acc += v;
+        for (int o = 1; o < 32; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if (tid >= (uint32_t)o) x += y;
         }
+        if (tid < VAR_NCLS_PAD) cbase[tid] = x - v;
       }
       __syncthreads();  // [C]
 #pragma unroll
