@@ -90,6 +90,33 @@ def cpu_baseline(sample_keys: int, passes: int, threads: int):
                                     % (threads, dt_mt)}}
 
 
+def bloom_cpu_baseline(n_ins: int, sample_1t: int, sample_mt: int, threads: int):
+    """BASELINE.md's Bloom CPU restatement: inserts into the filter sized for
+    n_ins @1% FPP (3,834,023,350 bits, k=7 at 4e8), the reference's own hash
+    scheme (xx_r39 + farmUo, u63 mod) and SETBIT addressing, from the oracle."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    size = O.bloom_optimal_bits(n_ins, 0.01)
+    k = O.bloom_optimal_k(n_ins, size)
+    bits = np.zeros((size + 7) // 8, np.uint8)
+    keys = O.gen_keys16(SEED_C3, 0, sample_1t)
+    t0 = time.perf_counter()
+    O.bloom_add_batch(bits, size, k, keys, None, 16, sample_1t, want=False)
+    dt = time.perf_counter() - t0
+    del keys
+    t1 = time.perf_counter()
+    O.bloom_add_gen16_mt(bits, size, k, SEED_C3, sample_1t, sample_mt, threads)
+    dt_mt = time.perf_counter() - t1
+    return {"value": sample_1t / dt, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": "%d C3 16-byte keys (pre-generated, %.1f s) inserted into a %d-bit filter (k=%d: %d inserts "
+                      "@1%% FPP, BASELINE.md), oracle orc_bloom_add_batch, 1 thread" % (sample_1t, dt, size, k, n_ins),
+            "all_cores": {"value": sample_mt / dt_mt, "unit": "keys/s", "cores": threads,
+                          "sample": "the next %d keys of the stream, orc_bloom_add_gen16_mt (keys generated inline), "
+                                    "%d OpenMP threads (%.1f s)" % (sample_mt, threads, dt_mt)}}
+
+
 def random_access_peaks(engine, nbytes: int, reps: int = 3):
     """Live random-access denominators over a buffer the size of the filter:
     4-byte gathers and 4-byte atomicOr at uniformly random words (rsk_diag_membench)."""
@@ -109,7 +136,7 @@ def random_access_peaks(engine, nbytes: int, reps: int = 3):
     return best
 
 
-def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
+def bloom_bench(engine, n_ins: int, n_q: int, reps: int, with_replies: bool = True):
     from redisson_amd import _lib, devmem
 
     L = _lib.load()
@@ -160,6 +187,23 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
         if cnt:
             stages[name] = ms / max(1, add_n)  # per insert batch (summed over its chunks)
     add_s, con_s = min(add_t), min(con_t)
+    replies = None
+    if with_replies:
+        # RBloomFilter.add's per-element reply (RedissonBloomFilter.java:100-107) for
+        # every key of the batch, in input order, into a fresh filter (one run).
+        rout = devmem.DeviceBuffer(engine, n_ins)
+        b = ctypes.c_void_p()
+        _lib.check(L.rsk_bloom_create(engine.ctx, size.value, k.value, ctypes.byref(b)))
+        engine.sync()
+        t0 = time.perf_counter()
+        _lib.check(L.rsk_bloom_add(b, ctypes.byref(ki), rout.ptr))
+        engine.sync()
+        dt = time.perf_counter() - t0
+        replies = {"keys": n_ins, "ms": dt * 1e3, "keys_per_s": n_ins / dt,
+                   "replies_true": int(rout.to_numpy().sum()),
+                   "note": "rsk_bloom_add with added_out (sequential SETBIT-reply semantics), fresh filter, one run"}
+        L.rsk_bloom_destroy(b)
+        rout.free()
     for buf in (ins, qs, out):
         buf.free()
     peaks = random_access_peaks(engine, (size.value + 7) // 8)
@@ -185,7 +229,24 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int):
                            "ratio": sets_per_s / peaks["atomicor4B"],
                            "note": "slice-partitioned: probes sorted into 64 KiB LDS-resident filter slices, "
                                    "so the insert is not bound by memory-side atomics"},
-                "peaks_measured_on": "a zeroed buffer of the filter's size, 2^30 uniformly random ops, best of 3"}}
+                "peaks_measured_on": "a zeroed buffer of the filter's size, 2^30 uniformly random ops, best of 3"},
+            "insert_roofline": insert_roofline(n_ins, k.value, size.value, add_s),
+            "insert_with_replies": replies}
+
+
+def insert_roofline(n: int, k: int, size: int, secs: float):
+    """HBM view of the C3 insert: the streaming floor (every key read once, the
+    filter read and written once) and the super-tile pipeline's own traffic model
+    (st1 writes 4k B/key of probe tags, st2 reads and rewrites them, apply reads
+    them again), both as bytes / measured insert time."""
+    filt = (size + 7) // 8
+    floor_b = 16.0 * n + 2.0 * filt
+    model_b = 16.0 * n + 16.0 * k * n + 2.0 * filt
+    return {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "algorithmic_bytes": floor_b, "achieved": floor_b / secs / 1e9,
+            "frac": floor_b / secs / 1e9 / HBM_PEAK_GBS,
+            "pipeline_model_bytes": model_b, "pipeline_model_GBps": model_b / secs / 1e9,
+            "pipeline_model_frac": model_b / secs / 1e9 / HBM_PEAK_GBS}
 
 
 def main():
@@ -201,6 +262,7 @@ def main():
     ap.add_argument("--batch-ops", type=int, default=100_000)
     ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
     ap.add_argument("--no-bloom", action="store_true")
+    ap.add_argument("--no-bloom-replies", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=128 << 20)
     ap.add_argument("--cpu-passes", type=int, default=8)
@@ -385,10 +447,12 @@ def main():
         pool.close()
     if rank == 0 and world == 1 and wl == "c2" and not args.no_bloom:
         bn = args.bloom_keys
-        result["bloom"] = bloom_bench(engine, bn, bn, reps=2)
+        result["bloom"] = bloom_bench(engine, bn, bn, reps=2, with_replies=not args.no_bloom_replies)
     if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes,
-                                              max(1, min(args.cpu_threads, os.cpu_count() or 1)))
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes, thr)
+        if not args.no_bloom:
+            result["cpu_baseline"]["bloom"] = bloom_cpu_baseline(400_000_000, 1 << 24, 1 << 27, thr)
         kd = devmem.gen_keys16(engine, SEED_C2, 0, args.cpu_sample)  # the same C2 stream, copied to host
         host_keys = kd.to_numpy()
         kd.free()
