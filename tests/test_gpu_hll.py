@@ -536,3 +536,28 @@ def test_device_batch_with_host_output_is_rejected(L, engine, orc):
     _lib.check(L.rsk_bloom_contains(b, ctypes.byref(ks), dout.ptr))
     L.rsk_bloom_destroy(b)
     L.rsk_hll_destroy(h)
+
+
+@pytest.mark.parametrize("n,branch", [(20_000, "linear"), (45_000, "bias"), (65_000, "bias"), (200_000, "raw")])
+def test_count_estimator_branches(L, engine, orc, n, branch):
+    # PFCOUNT on the GPU in each hllCount branch (linear counting, the 3.2.0
+    # bias polynomial, raw) against a Python restatement that shares no code
+    # with the oracle or the kernels (tests/redis_hllcount.py).
+    from redis_hllcount import redis32_hllcount_raw
+
+    from redisson_amd import KeyBatch
+
+    keys = orc.gen_keys16(SEED_C2, 0, n)
+    h = _pool(L, engine, 2)
+    _add(L, h, KeyBatch.from_numpy(keys.reshape(n, 16)), 0)
+    want, got_branch = redis32_hllcount_raw(_regs(L, h, 0))
+    assert got_branch == branch
+    assert int(_count(L, h, [0])[0]) == want  # single-key PFCOUNT (dense order)
+    pools = (ctypes.c_void_p * 2)(h.value, h.value)
+    ids = np.array([0, 1], np.uint64)  # sketch 1 empty: union == sketch 0 (raw order)
+    out = np.zeros(1, np.uint64)
+    from redisson_amd import _lib
+
+    _lib.check(L.rsk_hll_count_union(pools, ids.ctypes.data, 2, out.ctypes.data))
+    assert int(out[0]) == want
+    L.rsk_hll_destroy(h)
