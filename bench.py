@@ -31,17 +31,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel: str, keys_per_launch: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (null if absent)."""
+def pmc_traffic(kernel: str, config: dict):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary taken with
+    this same bench configuration (null if none matches)."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
+        if d.get("config") != config:
+            continue
         k = d.get("kernels", {}).get(kernel)
-        if k and k.get("keys_per_launch") == keys_per_launch and k.get("hbm_bytes_per_launch"):
-            best = k["hbm_bytes_per_launch"]
+        if k and k.get("hbm_bytes_per_launch"):
+            best = {"bytes": k["hbm_bytes_per_launch"], "source": os.path.relpath(p, ROOT)}
     return best
 
 
@@ -253,12 +256,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
                     help="c2: 16-byte keys (headline); c4: variable-length keys; c5: grouped sketches")
     ap.add_argument("--keys", type=int, default=None,
                     help="keys (pairs for c5) per GPU; default 1e9 (c2, c4), 5e8 for c5 (4e9 pairs over 8 GPUs)")
     ap.add_argument("--groups", type=int, default=1_000_000)
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="c5: draw groups Zipf(S) over the sketches (SURVEY 8d stress variant; 0 = uniform)")
     ap.add_argument("--batch-ops", type=int, default=100_000)
     ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
     ap.add_argument("--no-bloom", action="store_true")
@@ -317,7 +322,11 @@ def main():
         import numpy as np
 
         G = args.groups
-        groups, gkeys = devmem.gen_grouped(engine, SEED_C5, G, rank * n, n)
+        if args.zipf > 0:
+            groups, gkeys = devmem.gen_grouped_zipf(engine, SEED_C5, G, args.zipf, rank * n, n)
+            extra = {"group_distribution": "Zipf(%g) over the %d sketches (rank 1 = sketch 0)" % (args.zipf, G)}
+        else:
+            groups, gkeys = devmem.gen_grouped(engine, SEED_C5, G, rank * n, n)
         kb = gkeys.keys_fixed(n, 16)
         pool = GroupedHyperLogLog(engine, G)
         # N > 1: the pool is reduce-scattered, rank r owns a contiguous 1/N of
@@ -423,19 +432,30 @@ def main():
                         else "single GPU", "redis_semantics": "3.2.0"}, **extra),
         "roofline": {"bound": "hbm", "kernel": kern_label, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("hll_add_grouped_partitioned" if stage_ms else kern + "_kernel", n),
+                     "traffic": None,
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": add_launches,
                      "reduce_avg_ms": red_ms / max(1, red_launches),
                      "algorithmic_bytes_per_launch": unit_bytes},
         "side_kernels_ms_per_launch": {k: (v[0] / v[1] if v[1] else None) for k, v in side.items()},
         "count": int(card),
     }
+    pmc_cfg = {"workload": wl, "keys": n, "zipf": args.zipf,
+               "bloom_keys": args.bloom_keys if (wl == "c2" and not args.no_bloom) else 0}
+    tr = pmc_traffic("hll_add_grouped_partitioned" if stage_ms else kern + "_kernel", pmc_cfg)
+    if tr:
+        result["roofline"]["traffic"] = tr["bytes"]
+        result["roofline"]["traffic_source"] = tr["source"]
     if wl == "c5":
         # The grouped add must also write every touched sketch once whatever
         # the update order (16 KiB per touched sketch; at 500 pairs/sketch all
         # G are touched; the pool was just cleared, so nothing need be read):
         # the state-inclusive floor.
         touched = args.groups * -math.expm1(-n / args.groups)  # expected sketches hit by n uniform pairs
+        if args.zipf > 0:  # expected sketches hit by n Zipf pairs: sum over ranks of 1 - (1 - p_r)^n
+            import numpy as np
+
+            w = np.arange(1, args.groups + 1, dtype=np.float64) ** -args.zipf
+            touched = float(-np.expm1(n * np.log1p(-w / w.sum())).sum())
         state = 1.0 * touched * 16384  # written once; the cleared pool need not be read
         result["roofline"]["state_bytes_per_launch"] = state
         result["roofline"]["frac_incl_state"] = (unit_bytes + state) / avg_launch_s / 1e9 / HBM_PEAK_GBS
@@ -448,6 +468,12 @@ def main():
     if rank == 0 and world == 1 and wl == "c2" and not args.no_bloom:
         bn = args.bloom_keys
         result["bloom"] = bloom_bench(engine, bn, bn, reps=2, with_replies=not args.no_bloom_replies)
+        tr = pmc_traffic("bloom_insert_supertile", pmc_cfg)
+        if tr:
+            ir = result["bloom"]["insert_roofline"]
+            ir["traffic"] = tr["bytes"]
+            ir["traffic_source"] = tr["source"]
+            ir["traffic_GBps"] = tr["bytes"] / (ir["algorithmic_bytes"] / ir["achieved"]) / 1e9
     if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes, thr)

@@ -320,6 +320,11 @@ int rsk_diag_bloom_contains_probes(rsk_ctx *ctx, rsk_bloom *b, const void *dev_k
 int rsk_gen_keys16(rsk_ctx *ctx, uint64_t seed, uint64_t start, uint64_t n, void *dev_out);
 int rsk_gen_grouped(rsk_ctx *ctx, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t *dev_groups,
                     void *dev_keys);
+/* C5 Zipf(s) stress variant: group = Zipf(s) rank over [0, G) (rank 1 -> group 0)
+ * drawn from splitmix64(seed + 3i) >> 1 against a u63 cumulative-weight table;
+ * keys as rsk_gen_grouped (oracle: orc_gen_grouped_zipf). */
+int rsk_gen_grouped_zipf(rsk_ctx *ctx, uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n,
+                         uint32_t *dev_groups, void *dev_keys);
 int rsk_gen_queries16(rsk_ctx *ctx, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
                       void *dev_out);
 /* Variable-length keys: lengths first (dev_offsets gets n+1 offsets), then

@@ -92,6 +92,12 @@ def lib():
             "orc_gen_keys16": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
             "orc_gen_varlen_len": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint64]),
             "orc_gen_varlen_key": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+            "orc_zipf_cdf": (None, [ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p]),
+            "orc_gen_grouped_zipf": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+            "orc_hll_add_gen_grouped_zipf_subset": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                           ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64,
+                                                           ctypes.c_uint64, ctypes.c_int]),
             "orc_gen_grouped": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_void_p]),
             "orc_gen_queries16": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -197,6 +203,25 @@ def hll_add_gen_varlen(regs: np.ndarray, seed: int, start: int, n: int, nthreads
 
 def hll_add_gen16(regs: np.ndarray, seed: int, start: int, n: int, nthreads: int = 1):
     lib().orc_hll_add_gen16(_ptr(regs), seed, start, n, nthreads)
+
+
+def zipf_cdf(G: int, s: float) -> np.ndarray:
+    cdf = np.zeros(G, np.uint64)
+    lib().orc_zipf_cdf(G, s, _ptr(cdf))
+    return cdf
+
+
+def gen_grouped_zipf(seed: int, G: int, s: float, start: int, n: int):
+    groups = np.zeros(n, np.uint32)
+    keys = np.zeros(16 * n, np.uint8)
+    lib().orc_gen_grouped_zipf(seed, G, s, start, n, _ptr(groups), _ptr(keys))
+    return groups, keys
+
+
+def hll_add_gen_grouped_zipf_subset(regs: np.ndarray, G: int, gsub: int, s: float, seed: int, start: int, n: int,
+                                    nthreads: int = 1):
+    assert regs.dtype == np.uint8 and regs.size == gsub * REGISTERS
+    lib().orc_hll_add_gen_grouped_zipf_subset(_ptr(regs), G, gsub, s, seed, start, n, nthreads)
 
 
 def hll_add_gen_grouped(regs: np.ndarray, G: int, seed: int, start: int, n: int):

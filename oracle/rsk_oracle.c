@@ -203,6 +203,85 @@ void orc_gen_grouped(uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint
     }
 }
 
+/* C5 Zipf(s) stress variant (restates rsk_gen.hip zipf_cdf / gen_grouped_zipf_kernel):
+ * cdf[r] = floor(2^63 * sum_{q<=r+1} q^-s / sum_{q<=G} q^-s), cdf[G-1] = 2^63;
+ * group of pair i = first r with (splitmix64(seed+3i) >> 1) < cdf[r]. */
+void orc_zipf_cdf(uint64_t G, double s, uint64_t *cdf) {
+    double total = 0.0, cum = 0.0;
+    for (uint64_t r = 1; r <= G; r++) total += pow((double)r, -s);
+    for (uint64_t r = 1; r <= G; r++) {
+        cum += pow((double)r, -s);
+        cdf[r - 1] = (uint64_t)ldexp(cum / total, 63);
+    }
+    cdf[G - 1] = 1ULL << 63;
+}
+
+static uint32_t zipf_rank(const uint64_t *cdf, uint64_t G, uint64_t u) {
+    uint64_t lo = 0, hi = G - 1;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (u < cdf[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return (uint32_t)lo;
+}
+
+void orc_gen_grouped_zipf(uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n, uint32_t *groups,
+                          uint8_t *keys) {
+    uint64_t *cdf = malloc(8 * G);
+    orc_zipf_cdf(G, s, cdf);
+    for (uint64_t j = 0; j < n; j++) {
+        uint64_t i = start + j;
+        groups[j] = zipf_rank(cdf, G, orc_splitmix64(seed + 3 * i) >> 1);
+        uint64_t lo = orc_splitmix64(seed + 3 * i + 1), hi = orc_splitmix64(seed + 3 * i + 2);
+        memcpy(keys + 16 * j, &lo, 8);
+        memcpy(keys + 16 * j + 8, &hi, 8);
+    }
+    free(cdf);
+}
+
+/* Registers of the Zipf groups [0, gsub) (the hottest ones) over the whole
+ * pair stream: regs is [gsub][16384].  Each of nthreads threads takes a
+ * contiguous range of the pairs into private registers, max-merged at the end
+ * (the hot groups get most pairs, so splitting by group would serialise). */
+void orc_hll_add_gen_grouped_zipf_subset(uint8_t *regs, uint64_t G, uint64_t gsub, double s, uint64_t seed,
+                                         uint64_t start, uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    uint64_t *cdf = malloc(8 * G);
+    orc_zipf_cdf(G, s, cdf);
+    const size_t per = (size_t)gsub * ORC_HLL_REGISTERS;
+    uint8_t *priv = calloc((size_t)nthreads, per);
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+#ifdef _OPENMP
+        const uint64_t t = (uint64_t)omp_get_thread_num(), nt = (uint64_t)omp_get_num_threads();
+#else
+        const uint64_t t = 0, nt = 1;
+#endif
+        uint8_t *mine = priv + t * per;
+        for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
+            const uint64_t i = start + j;
+            const uint32_t g = zipf_rank(cdf, G, orc_splitmix64(seed + 3 * i) >> 1);
+            if (g >= gsub) continue;
+            uint8_t key[16];
+            uint64_t lo = orc_splitmix64(seed + 3 * i + 1), hi = orc_splitmix64(seed + 3 * i + 2);
+            memcpy(key, &lo, 8);
+            memcpy(key + 8, &hi, 8);
+            long idx;
+            int c = orc_hll_patlen(key, 16, &idx);
+            uint8_t *r = mine + (uint64_t)g * ORC_HLL_REGISTERS;
+            if (c > r[idx]) r[idx] = (uint8_t)c;
+        }
+    }
+    for (int t = 0; t < nthreads; t++)
+        for (size_t j = 0; j < per; j++)
+            if (priv[(size_t)t * per + j] > regs[j]) regs[j] = priv[(size_t)t * per + j];
+    free(priv);
+    free(cdf);
+}
+
 /* Bloom query stream (C3): query q is an inserted key (index r>>1 mod n_ins
  * of the insert stream iseed) when r&1, else a fresh key. */
 void orc_gen_queries16(uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n, uint8_t *out) {

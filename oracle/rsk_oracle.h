@@ -100,6 +100,11 @@ void orc_gen_keys16(uint64_t seed, uint64_t start, uint64_t n, uint8_t *out);
 uint32_t orc_gen_varlen_len(uint64_t seed, uint64_t i);
 void orc_gen_varlen_key(uint64_t seed, uint64_t i, uint8_t *out);
 void orc_gen_grouped(uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t *groups, uint8_t *keys);
+void orc_zipf_cdf(uint64_t G, double s, uint64_t *cdf);
+void orc_gen_grouped_zipf(uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n, uint32_t *groups,
+                          uint8_t *keys);
+void orc_hll_add_gen_grouped_zipf_subset(uint8_t *regs, uint64_t G, uint64_t gsub, double s, uint64_t seed,
+                                         uint64_t start, uint64_t n, int nthreads);
 void orc_gen_queries16(uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n, uint8_t *out);
 
 #ifdef __cplusplus

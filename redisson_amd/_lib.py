@@ -161,6 +161,7 @@ SIGNATURES = {
     "rsk_diag_bloom_contains_probes": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _P(_u64)]),
     "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
     "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
+    "rsk_gen_grouped_zipf": (ctypes.c_int, [_vp, _u64, _u64, ctypes.c_double, _u64, _u64, _vp, _vp]),
     "rsk_gen_queries16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
     "rsk_gen_varlen": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp, _vp, _u64, _P(_u64)]),
 }

@@ -1272,6 +1272,26 @@ int rsk_gen_grouped(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint6
   });
 }
 
+int rsk_gen_grouped_zipf(rsk_ctx* c, uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n,
+                         uint32_t* dev_groups, void* dev_keys) {
+  return guarded([&] {
+    need(c && G > 0 && G < (1ull << 32) && ((dev_groups && dev_keys) || n == 0), "bad arguments");
+    need(s > 0.0 && s < 16.0, "Zipf exponent must be in (0, 16)");
+    CtxLock l(c);
+    if (!n) return;
+    const std::vector<uint64_t> cdf = zipf_cdf((uint32_t)G, s);
+    uint64_t* d_cdf = nullptr;
+    RSK_HIP(hipMalloc(&d_cdf, 8 * G));
+    hipError_t e = hipMemcpyAsync(d_cdf, cdf.data(), 8 * G, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+      gen_grouped_zipf_launch(c, seed, d_cdf, (uint32_t)G, start, n, dev_groups, dev_keys);
+      e = hipStreamSynchronize(c->stream);
+    }
+    (void)hipFree(d_cdf);
+    RSK_HIP(e);
+  });
+}
+
 int rsk_gen_queries16(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
                       void* dev_out) {
   return guarded([&] {

@@ -614,6 +614,11 @@ __global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restr
   cnt2[((uint64_t)c * PT + threadIdx.x) * G1 + b] = h[threadIdx.x];
 }
 
+// A fine bin's records beyond its first GP_CH go to hll_gapply_extra (skewed
+// groups, e.g. the Zipf(1.1) C5 variant, put a third of all pairs into one
+// bin: one workgroup would otherwise walk them alone).
+constexpr uint32_t GP_CH = 1u << 20;
+
 // work item w: fine bin s = w / GP_NP (16 sketches from c*4096 + f*16), part w % GP_NP.
 __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
@@ -622,7 +627,8 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
   for (uint32_t w = blockIdx.x; w < GP_NP * nfine; w += gridDim.x) {
     const uint32_t s = w / GP_NP, half = w % GP_NP;
-    const uint32_t a = off2[(uint64_t)s * G1], e = off2[(uint64_t)(s + 1) * G1];
+    const uint32_t a = off2[(uint64_t)s * G1], e0 = off2[(uint64_t)(s + 1) * G1];
+    const uint32_t e = e0 - a > GP_CH ? a + GP_CH : e0;  // the rest: hll_gapply_extra
     const uint64_t g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
     if ((a == e && !write_all) || g0 >= G) continue;  // uniform across the workgroup
     const uint32_t nsk = (uint32_t)(G - g0 < GP_SK ? G - g0 : GP_SK);
@@ -663,6 +669,87 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
   }
 }
 
+// List the extra work items: entry (s << 13) | (part << 12) | j for chunk
+// j >= 1 of fine bin s, part `part` (records [a + j GP_CH, min(e, a + (j+1) GP_CH))).
+__global__ __launch_bounds__(256) void hll_gextra_list_kernel(const uint32_t* __restrict__ off2, uint32_t G1,
+                                                              uint32_t nfine, uint32_t cap,
+                                                              uint32_t* __restrict__ list, uint32_t* __restrict__ nlist) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nfine; s += gridDim.x * blockDim.x) {
+    const uint32_t n = off2[(uint64_t)(s + 1) * G1] - off2[(uint64_t)s * G1];
+    if (n <= GP_CH) continue;
+    const uint32_t extra = (n - 1) / GP_CH;
+    const uint32_t at = atomicAdd(nlist, extra * GP_NP);
+    for (uint32_t j = 1; j <= extra; ++j)
+      for (uint32_t h = 0; h < GP_NP; ++h) {
+        const uint32_t q = at + (j - 1) * GP_NP + h;
+        if (q < cap) list[q] = (s << 13) | (h << 12) | j;
+      }
+  }
+}
+
+// Extra chunks of heavy fine bins, after hll_gapply wrote every row: the
+// chunk's records are maxed into zeroed LDS registers, then each non-zero
+// word is folded into the pool row by a bytewise-max CAS (only the few
+// workgroups of one heavy bin contend for its words).
+__global__ __launch_bounds__(GP_T) void hll_gapply_extra_kernel(const uint32_t* __restrict__ recs,
+                                                                const uint32_t* __restrict__ off2, uint32_t G1,
+                                                                uint64_t G, const uint32_t* __restrict__ list,
+                                                                const uint32_t* __restrict__ nlist, uint32_t cap,
+                                                                uint8_t* __restrict__ regs) {
+  __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
+  const uint32_t nl = min(*nlist, cap);
+  for (uint32_t w = blockIdx.x; w < nl; w += gridDim.x) {
+    const uint32_t ent = list[w], s = ent >> 13, half = (ent >> 12) & 1u, j = ent & 4095u;
+    const uint32_t a0 = off2[(uint64_t)s * G1], e0 = off2[(uint64_t)(s + 1) * G1];
+    const uint32_t a = a0 + j * GP_CH, e = e0 - a > GP_CH ? a + GP_CH : e0;
+    const uint64_t g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
+    if (g0 >= G) continue;
+    const uint32_t nsk = (uint32_t)(G - g0 < GP_SK ? G - g0 : GP_SK);
+    for (uint32_t q = threadIdx.x; q < GP_SK * HLL_REGS / 4; q += GP_T) r32[q] = 0;
+    __syncthreads();
+    for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += GP_T * GP_U) {
+      uint32_t rv[GP_U];
+#pragma unroll
+      for (int u = 0; u < GP_U; ++u) {
+        const uint32_t i = i0 + u * GP_T;
+        rv[u] = i < e ? __builtin_nontemporal_load(&recs[i]) : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int u = 0; u < GP_U; ++u) {
+        const uint32_t r = rv[u];
+        const uint32_t sk = (r >> 20) & 15u;
+        if (r == 0xFFFFFFFFu || sk / GP_SK != half) continue;
+        const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
+        const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
+        uint32_t* word = &r32[byte >> 2];
+        uint32_t old = *word;
+        while (((old >> sh) & 0xFFu) < rank) {
+          const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+          if (prev == old) break;
+          old = prev;
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t* gw = reinterpret_cast<uint32_t*>(regs + g0 * HLL_REGS);
+    for (uint32_t q = threadIdx.x; q < nsk * (HLL_REGS / 4); q += GP_T) {
+      const uint32_t v = r32[q];
+      if (!v) continue;
+      uint32_t old = gw[q];
+      for (;;) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) m |= max((old >> (8 * b)) & 0xFFu, (v >> (8 * b)) & 0xFFu) << (8 * b);
+        if (m == old) break;
+        const uint32_t prev = atomicCAS(&gw[q], old, m);
+        if (prev == old) break;
+        old = prev;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 static int gpart_mode() {
   const char* e = std::getenv("RSK_HLL_GPART");  // unset: auto; "0": never; "1": always
   if (!e || !*e) return -1;
@@ -698,13 +785,16 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt1, c->stream);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt2, c->stream);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2));
+  const uint32_t xcap = (uint32_t)(GP_NP * (chunk / GP_CH + 1) + 16);  // extra work items per chunk, at most
+  const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1));
   uint8_t* w = c->work(meta + 2 * al(4 * max_np));
   uint32_t* cnt1 = reinterpret_cast<uint32_t*>(w);
   uint32_t* off1 = reinterpret_cast<uint32_t*>(w + al(4 * ncnt1));
   uint32_t* cnt2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1));
   uint32_t* off2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1) + al(4 * ncnt2));
   void* scan_tmp = w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2);
+  uint32_t* xlist = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)));
+  uint32_t* xcount = xlist + xcap;
   uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta);
   uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np));
   for (uint64_t first = 0; first < keys.n; first += chunk) {
@@ -742,6 +832,13 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
                          buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0,
                          (write_all && first == 0) ? 1 : 0, d_regs);
       RSK_CHECK_LAUNCH("hll_gapply");
+      RSK_HIP(hipMemsetAsync(xcount, 0, 4, c->stream));
+      hipLaunchKernelGGL(hll_gextra_list_kernel, dim3((nfine + 255) / 256), dim3(256), 0, c->stream, off2, G1, nfine,
+                         xcap, xlist, xcount);
+      RSK_CHECK_LAUNCH("hll_gextra_list");
+      hipLaunchKernelGGL(hll_gapply_extra_kernel, dim3(2 * cus), dim3(GP_T), 0, c->stream, buf_b, off2, G1, G, xlist,
+                         xcount, xcap, d_regs);
+      RSK_CHECK_LAUNCH("hll_gapply_extra");
     }
   }
   return true;

@@ -1,6 +1,9 @@
 // rsk_gen.hip -- on-device synthetic key streams, so that the
 // benchmark inputs are resident in HBM before the timed region.  The same
 // streams are restated on the CPU in oracle/rsk_oracle.c (orc_gen_*).
+#include <cmath>
+#include <vector>
+
 #include <hipcub/hipcub.hpp>
 
 #include "rsk_internal.h"
@@ -24,6 +27,27 @@ __global__ void gen_grouped_kernel(uint64_t seed, uint64_t G, uint64_t start, ui
     groups[j] = (uint32_t)(splitmix64(seed + 3 * i) % G);
     uint64_t lo = splitmix64(seed + 3 * i + 1), hi = splitmix64(seed + 3 * i + 2);
     keys[j] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+}
+
+// C5 Zipf(s) stress variant: as gen_grouped_kernel, but the
+// group is the Zipf rank of u = splitmix64(s+3i) >> 1: the first r with
+// u < cdf[r] (cdf: u63 fixed-point cumulative weights r^-s, built on the host
+// by zipf_cdf below and restated in oracle/rsk_oracle.c orc_zipf_cdf).
+__global__ void gen_grouped_zipf_kernel(uint64_t seed, const uint64_t* __restrict__ cdf, uint32_t G, uint64_t start,
+                                        uint64_t n, uint32_t* __restrict__ groups, uint4* __restrict__ keys) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i = start + j;
+    const uint64_t u = splitmix64(seed + 3 * i) >> 1;
+    uint32_t lo = 0, hi = G - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (u < cdf[mid]) hi = mid;
+      else lo = mid + 1;
+    }
+    groups[j] = lo;
+    uint64_t a = splitmix64(seed + 3 * i + 1), b = splitmix64(seed + 3 * i + 2);
+    keys[j] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
   }
 }
 
@@ -89,6 +113,28 @@ void gen_grouped_launch(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, u
   hipLaunchKernelGGL(gen_grouped_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, seed, G, start, n, g,
                      reinterpret_cast<uint4*>(keys));
   RSK_CHECK_LAUNCH("gen_grouped");
+}
+
+// cdf[r] = floor(2^63 * sum_{q<=r+1} q^-s / sum_{q<=G} q^-s), cdf[G-1] = 2^63
+// (every u < 2^63 lands): two sequential double passes, glibc pow.
+std::vector<uint64_t> zipf_cdf(uint32_t G, double s) {
+  double total = 0.0;
+  for (uint32_t r = 1; r <= G; ++r) total += std::pow((double)r, -s);
+  std::vector<uint64_t> cdf(G);
+  double cum = 0.0;
+  for (uint32_t r = 1; r <= G; ++r) {
+    cum += std::pow((double)r, -s);
+    cdf[r - 1] = (uint64_t)std::ldexp(cum / total, 63);
+  }
+  cdf[G - 1] = 1ull << 63;
+  return cdf;
+}
+
+void gen_grouped_zipf_launch(rsk_ctx* c, uint64_t seed, const uint64_t* d_cdf, uint32_t G, uint64_t start, uint64_t n,
+                             uint32_t* g, void* keys) {
+  hipLaunchKernelGGL(gen_grouped_zipf_kernel, dim3(gen_grid(c, n)), dim3(256), 0, c->stream, seed, d_cdf, G, start, n,
+                     g, reinterpret_cast<uint4*>(keys));
+  RSK_CHECK_LAUNCH("gen_grouped_zipf");
 }
 
 void gen_queries16_launch(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,

@@ -211,6 +211,9 @@ bool plan_fetch(uint64_t n, uint64_t N, uint64_t r, const uint64_t* ids, uint64_
 // ---- generators (rsk_gen.hip)
 void gen_keys16_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* out);
 void gen_grouped_launch(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* g, void* keys);
+std::vector<uint64_t> zipf_cdf(uint32_t G, double s);
+void gen_grouped_zipf_launch(rsk_ctx* c, uint64_t seed, const uint64_t* d_cdf, uint32_t G, uint64_t start, uint64_t n,
+                             uint32_t* g, void* keys);
 void gen_queries16_launch(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
                           void* out);
 void gen_varlen_lengths_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* offsets);

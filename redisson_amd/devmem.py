@@ -80,6 +80,13 @@ def gen_grouped(engine, seed: int, G: int, start: int, n: int):
     return g, k
 
 
+def gen_grouped_zipf(engine, seed: int, G: int, s: float, start: int, n: int):
+    g = DeviceBuffer(engine, 4 * n)
+    k = DeviceBuffer(engine, 16 * n)
+    _lib.check(_lib.load().rsk_gen_grouped_zipf(engine.ctx, seed, G, s, start, n, g.ptr, k.ptr))
+    return g, k
+
+
 def gen_varlen(engine, seed: int, start: int, n: int):
     offs = DeviceBuffer(engine, 8 * (n + 1))
     tot = ctypes.c_uint64()

@@ -1,6 +1,10 @@
 """Summarise rocprofv3 output into profiles/*.json / *.md.
 
-usage: python scripts/pmc_summary.py STATS_DIR FETCH_DIR WRITE_DIR OUT_PREFIX KEYS_PER_LAUNCH
+usage: python scripts/pmc_summary.py STATS_DIR FETCH_DIR WRITE_DIR OUT_PREFIX KEYS_PER_LAUNCH [CONFIG_JSON]
+
+CONFIG_JSON ({"workload": "c2", "keys": 1e9, "bloom_keys": ..., "zipf": 0}) is
+the bench configuration the three runs used; bench.py reads a summary's
+traffic only when its own configuration equals it.
 
 * STATS_DIR: rocprofv3 --kernel-trace --stats --output-format csv run
   (kernel_stats.csv: per-kernel calls / average duration).
@@ -54,6 +58,7 @@ def counters(d, counter):
 
 def main():
     sdir, fdir, wdir, prefix, keys = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
+    config = json.loads(sys.argv[6]) if len(sys.argv) > 6 else None
     st, sp = stats(sdir)
     fe, fp = counters(fdir, "FETCH_SIZE")
     wr, wp = counters(wdir, "WRITE_SIZE")
@@ -89,7 +94,19 @@ def main():
             "stages": list(parts),
             "hbm_bytes_note": "raw FETCH_SIZE + WRITE_SIZE of the stages per call (16 B key stream, 4 B records, "
                               "16 KiB sketch rows; not corrected)"}
-    doc = {"sources": {"stats": sp, "fetch": fp, "write": wp}, "kernels": kern,
+    st = ("bloom_st1_kernel", "st_transpose_kernel", "st_size_kernel", "st_offsets_kernel", "bloom_st2_kernel",
+          "bloom_st_apply_kernel")
+    if all(p in fe and p in wr for p in ("bloom_st1_kernel", "bloom_st2_kernel", "bloom_st_apply_kernel")):
+        # the super-tile Bloom insert (one chunk per insert at 1B keys, k = 7): per stage and summed.
+        # st1's key stream is a 16 B/lane read (FETCH doubled per the guide); the 4 B probe-tag
+        # reads of st2/apply are uncalibrated widths, reported raw.
+        stages = {p: {"fetch_kib_raw": fe.get(p, 0.0), "write_kib": wr.get(p, 0.0)} for p in st if p in fe}
+        tot = sum((fe.get(p, 0.0) + wr.get(p, 0.0)) * 1024 for p in st)
+        kern["bloom_insert_supertile"] = {
+            "stages": stages, "hbm_bytes_per_insert_raw": tot,
+            "hbm_bytes_per_launch": tot + fe["bloom_st1_kernel"] * 1024,
+            "note": "per insert call = one dispatch of each stage"}
+    doc = {"config": config, "sources": {"stats": sp, "fetch": fp, "write": wp}, "kernels": kern,
            "note": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch (mean over dispatches); fetch doubled for "
                    "hll_add16_kernel per MI355X_MICROARCH.md HBM section"}
     with open(prefix + ".json", "w") as f:

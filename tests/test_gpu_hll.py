@@ -453,6 +453,27 @@ def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
     assert np.array_equal(got, ref)
     cnt = _count(L, h, list(range(gs)))
     assert [int(c) for c in cnt[:64]] == [orc.hll_count_dense(ref[i]) for i in range(64)]
+    # the bench's batched countWith / mergeWith at full size: 10^5 ops over the
+    # 1M sketches in one call each; the first 256 ops use only sampled sketches
+    # (checked against the oracle), the rest draw from the other sketches.
+    rng = np.random.default_rng(9)
+    ops, chk = 100_000, 256
+    cw = rng.integers(gs, G, size=(ops, 2), dtype=np.uint64)
+    cw[:chk] = rng.integers(0, gs, size=(chk, 2), dtype=np.uint64)
+    out = np.zeros(ops, np.uint64)
+    _lib.check(L.rsk_hll_count_union_batch(h, cw.ctypes.data, 2, ops, out.ctypes.data))
+    for i in range(chk):
+        a, b = int(cw[i, 0]), int(cw[i, 1])
+        assert int(out[i]) == orc.hll_count_raw(np.maximum(ref[a], ref[b])), i
+    perm = rng.permutation(gs).astype(np.uint64)  # distinct sampled dst / src sketches
+    md = rng.integers(gs, G, size=ops, dtype=np.uint64)
+    ms = rng.integers(gs, G, size=ops, dtype=np.uint64)
+    md[:chk], ms[:chk] = perm[:chk], perm[chk:2 * chk]
+    _lib.check(L.rsk_hll_merge_batch(h, md.ctypes.data, ms.ctypes.data, ops))
+    for i in range(0, chk, 8):
+        d, sr = int(md[i]), int(ms[i])
+        assert np.array_equal(_regs(L, h, d), np.maximum(ref[d], ref[sr])), i
+        assert np.array_equal(_regs(L, h, sr), ref[sr]), i
     L.rsk_hll_destroy(h)
 
 
@@ -560,4 +581,57 @@ def test_count_estimator_branches(L, engine, orc, n, branch):
 
     _lib.check(L.rsk_hll_count_union(pools, ids.ctypes.data, 2, out.ctypes.data))
     assert int(out[0]) == want
+    L.rsk_hll_destroy(h)
+
+
+def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, monkeypatch):
+    """C5 Zipf(1.1) stress variant: the device generator equals the
+    oracle's pair stream; the partitioned grouped add over it (one coarse bin
+    holding most pairs, one fine bin a third of them) equals the direct kernel
+    and the oracle over the whole pool."""
+    from redisson_amd import _lib, devmem
+
+    G, n = 20_000, 3_000_000
+    g, k = devmem.gen_grouped_zipf(engine, 0x5EED0006, G, 1.1, 0, n)
+    rg, rk = orc.gen_grouped_zipf(0x5EED0006, G, 1.1, 0, n)
+    assert np.array_equal(g.to_numpy(np.uint32), rg) and np.array_equal(k.to_numpy(), rk)
+    assert (rg == 0).mean() > 0.05  # skewed: rank 1 alone draws > 5 % of the pairs
+    ks = k.keys_fixed(n, 16).as_struct()
+    pools = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RSK_HLL_GPART", mode)
+        h = _pool(L, engine, G)
+        _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+        pools[mode] = h
+    g.free()
+    k.free()
+    part, direct = (_pool_regs(L, engine, pools[m], G) for m in ("1", "0"))
+    assert np.array_equal(part, direct)
+    ref = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped_zipf_subset(ref, G, G, 1.1, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
+    assert np.array_equal(part, ref)
+    for h in pools.values():
+        L.rsk_hll_destroy(h)
+
+
+def test_c5_zipf_full_size_hot_groups_bit_exact(L, engine, orc):
+    """The Zipf(1.1) variant at the C5 per-GPU size (1M sketches, 500M pairs):
+    the 1024 hottest sketches (about 60 % of all pairs) bit-exact against the
+    oracle over the whole stream, and their PFCOUNTs."""
+    from redisson_amd import _lib, devmem
+
+    G, n, gs = 1_000_000, 500_000_000, 1024
+    g, k = devmem.gen_grouped_zipf(engine, 0x5EED0006, G, 1.1, 0, n)
+    h = _pool(L, engine, G)
+    ks = k.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    g.free()
+    k.free()
+    ref = np.zeros((gs, 16384), np.uint8)
+    orc.hll_add_gen_grouped_zipf_subset(ref, G, gs, 1.1, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
+    got = np.zeros((gs, 16384), np.uint8)
+    _lib.check(L.rsk_memcpy(engine.ctx, got.ctypes.data, L.rsk_hll_device_registers(h), got.nbytes, 1))
+    assert np.array_equal(got, ref)
+    cnt = _count(L, h, list(range(gs)))
+    assert [int(c) for c in cnt[:64]] == [orc.hll_count_dense(ref[i]) for i in range(64)]
     L.rsk_hll_destroy(h)

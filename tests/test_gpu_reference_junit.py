@@ -60,6 +60,47 @@ def test_hll_batch_pipelined_adds(client, orc):
     assert client.getHyperLogLog("pipe").count() == r.pfcount("pipe")
 
 
+def test_bitset_batch_pipelined_commands(client, orc):
+    # RBatch.getBitSet (RedissonBatch.java:191): SETBIT/GETBIT runs collapse into
+    # one launch each; every reply equals the in-order Redis model's.
+    batch = client.createBatch()
+    b = batch.getBitSet("bbits")
+    rng = np.random.default_rng(11)
+    offs = rng.integers(0, 5000, 300).tolist()
+    r = orc.RedisModel()
+    futs, want = [], []
+    for t, o in enumerate(offs):
+        if t % 7 == 3:
+            futs.append(b.clearAsync(o))
+            r.setbit("bbits", o, 0)
+            want.append(None)
+        elif t % 5 == 4:
+            futs.append(b.getAsync(o))
+            want.append(bool(r.getbit("bbits", o)))
+        else:
+            futs.append(b.setAsync(o))
+            r.setbit("bbits", o, 1)
+            want.append(None)
+    futs.append(b.cardinalityAsync())
+    want.append(r.bitcount("bbits"))
+    futs.append(b.setAsync(100, 200))
+    for o in range(100, 200):
+        r.setbit("bbits", o, 1)
+    want.append(None)
+    futs.append(b.clearAsync(150, 160))
+    for o in range(150, 160):
+        r.setbit("bbits", o, 0)
+    want.append(None)
+    futs.append(b.lengthAsync())
+    futs.append(b.toByteArrayAsync())
+    futs.append(b.getAsync(155))
+    res = batch.execute()
+    raw = r.get("bbits")
+    length = max((i for i in range(8 * len(raw)) if raw[i >> 3] & (0x80 >> (i & 7))), default=-1) + 1
+    want += [length, raw, False]
+    assert res == want and [f.result() for f in futs] == want
+
+
 def test_hll_redis_roundtrip(client, orc):
     h = client.getHyperLogLog("rt")
     h.addAll(list(range(5000)))

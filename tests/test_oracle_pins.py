@@ -296,3 +296,27 @@ def test_hll_estimator_branches_independent_restatement(orc, n, branch):
     want, got_branch = redis32_hllcount_raw(regs)
     assert got_branch == branch
     assert orc.hll_count_raw(regs) == want
+
+
+def test_zipf_stream_shape_and_subset_oracle(orc):
+    # the Zipf(1.1) table: monotone, ends at 2^63, rank frequencies follow r^-1.1
+    G, s = 10_000, 1.1
+    cdf = orc.zipf_cdf(G, s)
+    assert (np.diff(cdf.astype(np.float64)) >= 0).all() and int(cdf[-1]) == 1 << 63
+    w = np.arange(1, G + 1, dtype=np.float64) ** -s
+    assert abs(int(cdf[0]) / 2.0 ** 63 - w[0] / w.sum()) < 1e-12
+    n = 400_000
+    groups, keys = orc.gen_grouped_zipf(0x5EED0006, G, s, 0, n)
+    freq = np.bincount(groups, minlength=G) / n
+    assert abs(freq[0] - w[0] / w.sum()) < 0.01 and abs(freq[9] - w[9] / w.sum()) < 0.005
+    # the pair-parallel subset oracle equals a direct replay of the stream
+    gs = 64
+    ref = np.zeros(gs * orc.REGISTERS, np.uint8)
+    for j in np.nonzero(groups < gs)[0]:
+        idx, c = orc.patlen(keys[16 * j:16 * j + 16].tobytes())
+        o = int(groups[j]) * orc.REGISTERS + idx
+        ref[o] = max(ref[o], c)
+    for threads in (1, 3):
+        sub = np.zeros(gs * orc.REGISTERS, np.uint8)
+        orc.hll_add_gen_grouped_zipf_subset(sub, G, gs, s, 0x5EED0006, 0, n, threads)
+        assert np.array_equal(sub, ref), threads
