@@ -143,7 +143,9 @@ int rsk_hll_merge_batch(rsk_hll *h, const uint64_t *dst_ids, const uint64_t *src
 int rsk_hll_merge_raw(rsk_hll *h, uint64_t id, const uint8_t *regs, uint32_t location);
 /* Raw registers out (host or device destination, 16384 bytes). */
 int rsk_hll_get_registers(rsk_hll *h, uint64_t id, uint8_t *out, uint32_t location);
-/* Device pointer of the [n_sketches][16384] register array (for RCCL). */
+/* Device pointer of the [n_sketches][16384] register array (for RCCL).  A
+ * caller that writes registers through it must do so before its next call on
+ * this pool (each call re-derives the pool's cached state from that point). */
 void *rsk_hll_device_registers(rsk_hll *h);
 
 /* GET of the key as a Redis dense "HYLL" string (12304 bytes; card bytes as

@@ -309,7 +309,7 @@ void check_hll(const rsk_hll* h, uint64_t id) {
   need(h != nullptr, "hll handle is NULL");
   need(id < h->n, "sketch id out of range");
   rsk::hll_materialize(h);  // every caller reads or writes registers
-  h->zero = false;          // conservatively: every caller may write them
+  rsk::hll_touch(h);        // conservatively: every caller may write them
 }
 
 uint8_t* regs_of(rsk_hll* h, uint64_t id) { return h->d_regs + id * (uint64_t)HLL_REGS; }
@@ -401,6 +401,15 @@ void hll_materialize(const rsk_hll* h) {
   ProfScope ps(h->ctx, "hll_clear");
   RSK_HIP(hipMemsetAsync(h->d_regs, 0, h->n * (uint64_t)HLL_REGS, h->ctx->stream));
   h->pending_clear = false;
+  hll_touch(h);
+}
+
+void hll_touch(const rsk_hll* h) {
+  h->zero = false;
+  if (++h->pc_epoch == 0) {  // wrapped: clear every stamp so no stale one can match again
+    RSK_HIP(hipMemsetAsync(h->d_pepoch, 0, 4 * h->n, h->ctx->stream));
+    h->pc_epoch = 1;
+  }
 }
 }  // namespace rsk
 
@@ -535,6 +544,9 @@ int rsk_hll_create(rsk_ctx* c, uint64_t n, rsk_hll** out) {
     h->exists.assign(n, 0);
     RSK_HIP(hipMalloc(&h->d_regs, n * (uint64_t)HLL_REGS));
     RSK_HIP(hipMalloc(&h->d_card, n * 8));
+    RSK_HIP(hipMalloc(&h->d_pcount, n * 8));
+    RSK_HIP(hipMalloc(&h->d_pepoch, n * 4));
+    RSK_HIP(hipMemsetAsync(h->d_pepoch, 0, n * 4, c->stream));
     RSK_HIP(hipMemsetAsync(h->d_regs, 0, n * (uint64_t)HLL_REGS, c->stream));
     RSK_HIP(hipMemsetAsync(h->d_card, 0, n * 8, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
@@ -550,6 +562,8 @@ int rsk_hll_destroy(rsk_hll* h) {
     RSK_HIP(hipStreamSynchronize(h->ctx->stream));
     RSK_HIP(hipFree(h->d_regs));
     RSK_HIP(hipFree(h->d_card));
+    RSK_HIP(hipFree(h->d_pcount));
+    RSK_HIP(hipFree(h->d_pepoch));
   });
   delete h;
   return rc;
@@ -684,7 +698,7 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     if (keys->n == 0) return;
     check_out(c, keys, groups);
     const bool pool_zero = h->zero;
-    h->zero = false;
+    hll_touch(h);
     uint32_t* d_groups = nullptr;
     if (keys->location == RSK_MEM_HOST) {
       for (uint64_t i = 0; i < keys->n; ++i)
@@ -701,7 +715,11 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
       // launch (every row written); any other path zeroes the pool first.
       const bool write_all = h->pending_clear && hll_grouped_partition_applies(dk, h->n);
       if (!write_all) hll_materialize(h);
-      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0, write_all);
+      hll_touch(h);  // estimates of earlier chunks are stale once this one lands
+      const char* pe = std::getenv("RSK_HLL_PCOUNT");  // "0": no estimates from the grouped add (A/B)
+      const bool est = !(pe && pe[0] == '0');
+      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0, write_all,
+                             PCount{est ? h->d_pcount : nullptr, h->d_pepoch, h->pc_epoch});
       h->pending_clear = false;
     });
     if (keys->location == RSK_MEM_DEVICE) {
@@ -740,7 +758,7 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
       need(n <= h->n, "n exceeds pool size");
     }
     uint64_t* d_out = reinterpret_cast<uint64_t*>(s + (ids ? ((n * 8 + 255) & ~255ull) : 0));
-    hll_count_launch(c, h->d_regs, h->d_card, d_ids, small, n, d_out);
+    hll_count_launch(c, h->d_regs, h->d_card, d_ids, small, n, d_out, PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
     if (n * 8 <= 4096) {  // small results come back through the pinned buffer
       RSK_HIP(hipMemcpyAsync(c->h_small + 4096, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
@@ -941,11 +959,11 @@ void* rsk_hll_device_registers(rsk_hll* h) {  // the caller may read or write th
   if (!h) return nullptr;
   try {
     rsk::hll_materialize(h);
+    hll_touch(h);
     RSK_HIP(hipStreamSynchronize(h->ctx->stream));
   } catch (const RskError&) {
     return nullptr;
   }
-  h->zero = false;
   return h->d_regs;
 }
 

@@ -36,6 +36,7 @@
 
 #include <cstdlib>
 
+#include "rsk_hllcount.h"
 #include "rsk_internal.h"
 
 namespace rsk {
@@ -620,11 +621,17 @@ __global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restr
 constexpr uint32_t GP_CH = 1u << 20;
 
 // work item w: fine bin s = w / GP_NP (16 sketches from c*4096 + f*16), part w % GP_NP.
+// With pc.pcount: the PFCOUNT of every row written is estimated from LDS on
+// the way out (the write-back's uint4 i of each thread belongs to sketch i)
+// and left in pc (hll_count_kernel takes it instead of re-reading the row);
+// rows of split heavy bins and inexact sums are left for the count kernel.
 __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
                                                           uint32_t nfine, uint64_t G, int pool_zero,
-                                                          int write_all, uint8_t* __restrict__ regs) {
+                                                          int write_all, uint8_t* __restrict__ regs, PCount pc,
+                                                          const double* __restrict__ lc) {
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
+  __shared__ SumD part[GP_T / 64];
   for (uint32_t w = blockIdx.x; w < GP_NP * nfine; w += gridDim.x) {
     const uint32_t s = w / GP_NP, half = w % GP_NP;
     const uint32_t a = off2[(uint64_t)s * G1], e0 = off2[(uint64_t)(s + 1) * G1];
@@ -664,7 +671,43 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
       }
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < n4; q += GP_T) gp[q] = lp[q];
+    const bool est = pc.pcount && e0 - a <= GP_CH;  // (a split bin's extra chunks change the rows later)
+    if (!est) {
+      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) gp[q] = lp[q];
+      if (pc.pcount && threadIdx.x < nsk) pc.pepoch[g0 + threadIdx.x] = 0;  // no estimate for these rows
+    } else {
+      static_assert(GP_T / 64 == 2 * GP_SK, "two waves per sketch");
+      // wave w writes back (and sums) half w & 1 of sketch w >> 1: 8 uint4 per lane, one reduction per wave
+      const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = wv >> 1;
+      SumD sd{0.0, 0, 0};
+      if (i < nsk) {
+        const uint32_t q0 = i * (HLL_REGS / 16) + (wv & 1) * (HLL_REGS / 32);
+#pragma unroll
+        for (int u = 0; u < HLL_REGS / 32 / 64; ++u) {
+          const uint32_t q = q0 + u * 64 + lane;
+          const uint4 v = lp[q];
+          gp[q] = v;
+          acc_word(sd, v.x);
+          acc_word(sd, v.y);
+          acc_word(sd, v.z);
+          acc_word(sd, v.w);
+        }
+      }
+      sd = wave_reduce(sd);
+      if (lane == 0) part[wv] = sd;
+      __syncthreads();
+      if (threadIdx.x < nsk) {  // one lane per sketch: its two wave partials
+        const SumD p0 = part[2 * threadIdx.x], p1 = part[2 * threadIdx.x + 1];  // exact sums: any order
+        SumD t{p0.t + p1.t, p0.ez + p1.ez, p0.rmax > p1.rmax ? p0.rmax : p1.rmax};
+        const uint64_t g = g0 + threadIdx.x;
+        if (exact_total(t)) {
+          pc.pcount[g] = hll_estimate(t.t, (int)t.ez, lc);
+          pc.pepoch[g] = pc.epoch;
+        } else {
+          pc.pepoch[g] = 0;  // Redis's dense order: left to hll_count_kernel
+        }
+      }
+    }
     __syncthreads();
   }
 }
@@ -769,7 +812,7 @@ bool hll_grouped_partition_applies(const DevKeys& keys, uint64_t G) {
 // write_all (a pending lazy clear, pool_zero too): hll_gapply writes every
 // row of the pool, zero rows for sketches without records.
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
-                                 uint64_t G, bool pool_zero, bool write_all) {
+                                 uint64_t G, bool pool_zero, bool write_all, PCount pc) {
   if (!hll_grouped_partition_applies(keys, G)) return false;
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
@@ -830,7 +873,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, 2 * per_cu * cus)), dim3(GP_T), 0,
                          c->stream,
                          buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0,
-                         (write_all && first == 0) ? 1 : 0, d_regs);
+                         (write_all && first == 0) ? 1 : 0, d_regs, pc, c->d_lc);
       RSK_CHECK_LAUNCH("hll_gapply");
       RSK_HIP(hipMemsetAsync(xcount, 0, 4, c->stream));
       hipLaunchKernelGGL(hll_gextra_list_kernel, dim3((nfine + 255) / 256), dim3(256), 0, c->stream, off2, G1, nfine,

@@ -526,6 +526,263 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
   }
 }
 
+// ============================================ append variant (two-level filters)
+// sa1: the st1 super-tile (one hash pass, ranks by coarse bin, bin-sorted LDS
+// image), but each coarse bin's run is APPENDED to that bin's own region in
+// blocks of SA_B probes: a workgroup keeps one open block per bin and takes
+// new blocks from the bin's cursor with one atomicAdd for a whole run (issued
+// before the placement, consumed after it).  The region of bin c is then a
+// contiguous run of full blocks (plus one INVALID-padded tail block per
+// workgroup), so sa2 streams it with coalesced 16-byte loads -- no headers,
+// no segment planner, no transpose.
+// sa2: one workgroup per (c, p) streams blocks [nblk p / P, nblk (p+1) / P) of
+// bin c, ranks by fine bin and writes bin-sorted tiles exactly like st2, whose
+// output the apply kernel reads unchanged.  Tile count per (c, p) is exact:
+// ceil(probes / SA2_SLOTS).  A bin whose region overflows (only adversarial
+// inputs: 1.25x the expected share) sets `overflow`; the chunk is redone.
+constexpr uint32_t SA_B = 1024;     // probes per block
+constexpr int SA2_V = 3;            // sa2: uint4 loads (4 probes) per lane per tile (96 per fine bin: apply's 2 x 64 fast path)
+constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
+constexpr uint32_t SA2_SLOTS = SA2_T * SA2_V * 4;
+
+RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads instead of the LDS-only barrier
+  if (dbg) __syncthreads();
+  else lds_barrier();
+}
+
+template <bool FIXED16, int KMAX, int T1>
+__global__ __launch_bounds__(T1) void bloom_sa1_kernel(const uint8_t* __restrict__ data,
+                                                       const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                                                       uint64_t n, FastMod63 fm, int k, uint32_t shift1, uint32_t nb1,
+                                                       uint64_t nst, uint32_t* __restrict__ region,
+                                                       uint64_t cap_probes, uint32_t cap_blocks,
+                                                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ overflow,
+                                                       int dbg) {
+  constexpr int KPL = 16 / KMAX;
+  constexpr uint32_t KST = T1 * KPL;
+  constexpr int NP = KPL * KMAX;
+  constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
+  __shared__ __attribute__((aligned(16))) uint32_t img[T1 * NP];
+  __shared__ uint32_t hist[256], lstart[256], pos[256], room[256], p1[256], r1[256], p2[256];
+  __shared__ uint4 runs[256];  // per bin: image start, length, probes to the open block, its position
+  const uint64_t low = (1ull << shift1) - 1;
+  if (threadIdx.x < 256) {
+    hist[threadIdx.x] = 0;
+    pos[threadIdx.x] = 0;
+    room[threadIdx.x] = 0;  // no open block yet
+  }
+  const uint4* keys16 = reinterpret_cast<const uint4*>(data);
+  uint4 nxt[KPL];
+  auto fetch = [&](uint64_t st) {
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const uint64_t i = st * KST + threadIdx.x + (uint64_t)u * T1;
+      nxt[u] = (FIXED16 && st < nst && i < n) ? ld_nt16(keys16 + i) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (FIXED16) fetch(blockIdx.x);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t st = blockIdx.x; st < nst; st += gridDim.x) {
+    const uint64_t k0 = st * KST;
+    const uint32_t nk = (uint32_t)(n - k0 < KST ? n - k0 : KST);
+    uint4 cur[KPL];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) cur[u] = nxt[u];
+    if (FIXED16) fetch(st + gridDim.x);
+    uint32_t pay[NP], tag[NP];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const uint32_t q = threadIdx.x + u * T1;
+      const bool ok = q < nk;
+      uint64_t h1 = 0, h2 = 0;
+      if (ok) {
+        if (FIXED16) {
+          uint64_t w0, w1;
+          key_words(cur[u], &w0, &w1);
+          h1 = xxh64_16(w0, w1);
+          h2 = farm_16(w0, w1);
+        } else {
+          bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
+        }
+      }
+      ProbeSeq ps(h1, h2, fm);
+#pragma unroll
+      for (int t = 0; t < KMAX; ++t) {
+        const int s = u * KMAX + t;
+        tag[s] = INVALID;
+        pay[s] = 0;
+        if (ok && t < k) {
+          const uint64_t idx = ps.idx;
+          const uint32_t bin = (uint32_t)(idx >> shift1);
+          pay[s] = (uint32_t)(idx & low);
+          tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+          if (t + 1 < k) ps.next(t, fm);
+        }
+      }
+    }
+    sa_bar(dbg);  // (A) every rank taken
+    // wave 0: bin starts, and for each bin's run of L probes: the first
+    // min(L, room) go to the open block, the rest to ceil(rest / SA_B) new
+    // blocks taken with one atomicAdd (its result is used after the placement)
+    uint32_t nbk[PER], rest[PER], base[PER];
+    if (threadIdx.x < 64) {
+      uint32_t v[PER], sum = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        v[i] = b < nb1 ? hist[b] : 0;
+        if (b < nb1) hist[b] = 0;
+        sum += v[i];
+      }
+      const uint32_t incl = wave_scan_incl(sum, lane);
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        nbk[i] = 0;
+        rest[i] = 0;
+        base[i] = 0;
+        if (b < nb1) {
+          lstart[b] = run;
+          const uint32_t rm = room[b], a = v[i] < rm ? v[i] : rm;
+          p1[b] = pos[b];
+          r1[b] = a;
+          rest[i] = v[i] - a;
+          if (rest[i]) {
+            nbk[i] = (rest[i] + SA_B - 1) / SA_B;
+            base[i] = atomicAdd(&cursor[b], nbk[i]);
+          } else {
+            pos[b] += a;
+            room[b] = rm - a;
+          }
+        }
+        run += v[i];
+      }
+    }
+    sa_bar(dbg);  // (B) lstart / total ready (the cursor atomics stay in flight)
+#pragma unroll
+    for (int s = 0; s < NP; ++s)
+      if (tag[s] != INVALID) {
+        img[lstart[tag[s] >> 16] + (tag[s] & 0xFFFFu)] = pay[s];
+      }
+    if (threadIdx.x < 64) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        if (b < nb1 && rest[i]) {
+          if (base[i] + nbk[i] <= cap_blocks) {
+            p2[b] = base[i] * SA_B;
+            pos[b] = base[i] * SA_B + rest[i];
+            room[b] = nbk[i] * SA_B - rest[i];
+          } else {  // region full: drop the run (the host redoes the chunk)
+            atomicOr(overflow, 1u);
+            p2[b] = INVALID;
+            room[b] = 0;
+          }
+        }
+        if (b < nb1) runs[b] = make_uint4(lstart[b], r1[b] + rest[i], r1[b], p1[b]);
+      }
+    }
+    sa_bar(dbg);  // (C) image and run destinations complete
+    // bin-major write-out: wave w writes the runs of bins w, w + NW, ...; the
+    // per-bin values are LDS broadcasts, each lane moves one probe per step
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (uint32_t b = wv; b < nb1; b += T1 / 64) {
+      const uint4 r = runs[b];  // x: image start, y: length, z: to the open block, w: its position
+      if (!r.y) continue;
+      const uint32_t q = p2[b];
+      uint32_t* rb = region + (uint64_t)b * cap_probes;
+      for (uint32_t o = lane; o < r.y; o += 64) {
+        const uint32_t v = img[r.x + o];
+        if (o < r.z) rb[r.w + o] = v;
+        else if (q != INVALID) rb[q + (o - r.z)] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // pad every open block's tail with INVALID (sa2 streams whole blocks)
+  for (uint32_t b = 0; b < nb1; ++b) {
+    const uint32_t rm = room[b], ps = pos[b];
+    for (uint32_t q = threadIdx.x; q < rm; q += T1) region[(uint64_t)b * cap_probes + ps + q] = INVALID;
+  }
+}
+
+// tot[cp] = streamed probes of (c, p) (INVALID padding included), bud[cp] = its tiles
+__global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict__ cursor, uint32_t cap_blocks,
+                                                      uint32_t P, uint32_t ncp, uint64_t* __restrict__ tot,
+                                                      uint32_t* __restrict__ bud) {
+  const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cp >= ncp) return;
+  const uint32_t c = cp / P, p = cp - c * P;
+  const uint64_t nblk = min(cursor[c], cap_blocks);
+  const uint64_t probes = (nblk * (p + 1) / P - nblk * p / P) * SA_B;
+  tot[cp] = probes;
+  bud[cp] = (uint32_t)((probes + SA2_SLOTS - 1) / SA2_SLOTS);
+}
+
+__global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __restrict__ region, uint64_t cap_probes,
+                                                          const uint32_t* __restrict__ cursor, uint32_t cap_blocks,
+                                                          uint32_t P, uint32_t nb2,
+                                                          const uint64_t* __restrict__ reg_off,
+                                                          const uint32_t* __restrict__ tile_off,
+                                                          uint32_t* __restrict__ used, uint32_t* __restrict__ out,
+                                                          uint16_t* __restrict__ h2, uint64_t* __restrict__ tb2,
+                                                          int dbg) {
+  constexpr int NV = SA2_V * 4;
+  __shared__ __attribute__((aligned(16))) uint32_t srt[2][SA2_SLOTS];
+  __shared__ uint32_t hist[128], lstart[128], s_total;
+  __shared__ uint16_t s_hdr[129];
+  const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
+  const uint64_t nblk = min(cursor[c], cap_blocks);
+  const uint64_t b0 = nblk * p / P, b1 = nblk * (p + 1) / P;
+  const uint4* in = reinterpret_cast<const uint4*>(region + (uint64_t)c * cap_probes + b0 * SA_B);
+  const uint64_t n4 = (b1 - b0) * (SA_B / 4);  // uint4 of this (c, p)
+  if (threadIdx.x < 128) hist[threadIdx.x] = 0;
+  const uint64_t base = reg_off[cp];
+  const uint32_t tbeg = tile_off[cp];
+  uint64_t written = 0;
+  uint32_t ntile = 0, buf = 0;
+  __syncthreads();
+  for (uint64_t q0 = 0; q0 < n4; q0 += SA2_SLOTS / 4) {
+    uint32_t pay[NV], tag[NV];
+#pragma unroll
+    for (int v = 0; v < SA2_V; ++v) {
+      const uint64_t q = q0 + (uint64_t)v * SA2_T + threadIdx.x;
+      const uint4 x = q < n4 ? ld_nt16(in + q) : make_uint4(INVALID, INVALID, INVALID, INVALID);
+      pay[4 * v] = x.x;
+      pay[4 * v + 1] = x.y;
+      pay[4 * v + 2] = x.z;
+      pay[4 * v + 3] = x.w;
+    }
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      tag[r] = INVALID;
+      if (pay[r] != INVALID) {
+        const uint32_t bin = pay[r] >> SL_LOG;
+        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+      }
+    }
+    sa_bar(dbg);  // (A)
+    if (threadIdx.x < 64) wave0_bin_starts<128>(hist, lstart, nb2, s_hdr, &s_total);
+    sa_bar(dbg);  // (B)
+    const uint32_t total = s_total;
+    if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
+    if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
+    uint32_t* img = srt[buf];
+#pragma unroll
+    for (int r = 0; r < NV; ++r)
+      if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
+    sa_bar(dbg);  // (C)
+    uint32_t* o = out + base + written;
+    for (uint32_t j = threadIdx.x; j < total; j += SA2_T) o[j] = img[j];
+    written += total;
+    ++ntile;
+    buf ^= 1;
+  }
+  if (threadIdx.x == 0) used[cp] = ntile;
+}
+
 int st_mode() {
   const char* e = std::getenv("RSK_BLOOM_ST");  // unset: auto; "0": never; "1": always (any batch size)
   if (!e || !*e) return -1;
@@ -565,6 +822,143 @@ uint32_t nbits(uint64_t v) {  // bits needed to hold v (0 -> 0)
   return b;
 }
 
+// The append pipeline (sa1 -> sa2 -> apply) for filters of more than 256 slices.
+bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, uint32_t kmax, uint32_t t1,
+                      uint64_t kst, uint32_t f2, uint32_t shift1, uint32_t nb1, uint32_t P, uint64_t chunk) {
+  const uint64_t k = (uint64_t)b->k;
+  const uint32_t ns = (uint32_t)(((uint64_t)b->size + (1ull << SL_LOG) - 1) >> SL_LOG);
+  const uint32_t nb2 = 1u << f2;
+  const uint32_t ncp = nb1 * P;
+  const uint32_t cus = (uint32_t)c->num_cus;
+  const uint32_t ua = env_u32("RSK_BLOOM_ST_UA", UA_DEFAULT) == 8 ? 8 : 4;
+  const uint32_t dbg = env_u32("RSK_BLOOM_SA_DBG", 0);
+  const uint64_t max_nst = (chunk + kst - 1) / kst;
+  const uint64_t max_np = max_nst * kst * k;
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  // sa1 grid (persistent) and the per-bin region: 1.25x a full coarse bin's
+  // expected share of the probes, plus one open block per workgroup.
+  const void* k1 = t1 == 1024 ? (f16 ? (kmax == 8 ? (const void*)bloom_sa1_kernel<true, 8, 1024>
+                                                  : (const void*)bloom_sa1_kernel<true, 16, 1024>)
+                                     : (kmax == 8 ? (const void*)bloom_sa1_kernel<false, 8, 1024>
+                                                  : (const void*)bloom_sa1_kernel<false, 16, 1024>))
+                              : (f16 ? (kmax == 8 ? (const void*)bloom_sa1_kernel<true, 8, 512>
+                                                  : (const void*)bloom_sa1_kernel<true, 16, 512>)
+                                     : (kmax == 8 ? (const void*)bloom_sa1_kernel<false, 8, 512>
+                                                  : (const void*)bloom_sa1_kernel<false, 16, 512>));
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k1, (int)t1, 0) != hipSuccess || per_cu < 1) {
+    (void)hipGetLastError();
+    per_cu = 1;
+  }
+  const uint32_t grid1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_nst, (uint64_t)per_cu * cus));
+  const double share = (double)(1ull << shift1) / (double)(uint64_t)b->size;  // of one full coarse bin
+  const uint64_t slack = env_u32("RSK_BLOOM_SA_TINY", 0) ? 0 : 1;           // tests force the overflow fallback
+  const uint32_t cap_blocks =
+      (uint32_t)(slack * ((uint64_t)(1.25 * share * (double)max_np) / SA_B + 2ull * grid1 + 16) + (1 - slack) * 2);
+  const uint64_t cap_probes = (uint64_t)cap_blocks * SA_B;
+  if (cap_probes >= (1ull << 31)) return false;  // u32 run positions (INVALID = dropped) -> the exact-offset pipeline
+  const uint64_t region_probes = (uint64_t)nb1 * cap_probes;
+  const uint64_t tt_max = region_probes / SA2_SLOTS + ncp + 64;  // bound on sa2 tiles
+  const uint64_t h2_bytes = al(tt_max * (nb2 + 1) * 2);
+  const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4 * nb1) + 256;
+  const uint64_t bytes = 2 * al(4 * region_probes) + 2 * h2_bytes + al(8 * tt_max) + meta;
+  uint8_t* w = c->work(bytes);
+  uint8_t* q = w;
+  auto take = [&](uint64_t n) {
+    uint8_t* r = q;
+    q += n;
+    return r;
+  };
+  uint32_t* region = reinterpret_cast<uint32_t*>(take(al(4 * region_probes)));
+  uint32_t* l2 = reinterpret_cast<uint32_t*>(take(al(4 * region_probes)));
+  uint16_t* h2 = reinterpret_cast<uint16_t*>(take(h2_bytes));
+  uint16_t* h2t = reinterpret_cast<uint16_t*>(take(h2_bytes));
+  uint64_t* tb2 = reinterpret_cast<uint64_t*>(take(al(8 * tt_max)));
+  uint64_t* tot = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
+  uint64_t* reg_off = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
+  uint32_t* bud = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* tile_off = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* used = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(take(al(4 * nb1)));
+  uint32_t* overflow = reinterpret_cast<uint32_t*>(take(256));
+
+  std::vector<DevKeys> redo;
+  for (uint64_t first = 0; first < keys.n; first += chunk) {
+    const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
+    const uint64_t nst = (m + kst - 1) / kst;
+    DevKeys dk = keys;
+    dk.n = m;
+    if (keys.offsets) dk.offsets = keys.offsets + first;
+    else dk.data = keys.data + first * keys.fixed_len;
+    RSK_HIP(hipMemsetAsync(cursor, 0, 4 * nb1, c->stream));
+    RSK_HIP(hipMemsetAsync(overflow, 0, 4, c->stream));
+    {
+      ProfScope ps(c, "bloom_st1");
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(grid1, nst);
+#define RSK_SA1(F16, KM, TT)                                                                                   \
+  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, TT>), dim3(grid), dim3(TT), 0, c->stream, dk.data, dk.offsets, \
+                     dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, cap_probes, cap_blocks, cursor,    \
+                     overflow, (int)(dbg & 1))
+      if (t1 == 1024) {
+        if (f16 && kmax == 8) RSK_SA1(true, 8, 1024);
+        else if (f16) RSK_SA1(true, 16, 1024);
+        else if (kmax == 8) RSK_SA1(false, 8, 1024);
+        else RSK_SA1(false, 16, 1024);
+      } else {
+        if (f16 && kmax == 8) RSK_SA1(true, 8, 512);
+        else if (f16) RSK_SA1(true, 16, 512);
+        else if (kmax == 8) RSK_SA1(false, 8, 512);
+        else RSK_SA1(false, 16, 512);
+      }
+#undef RSK_SA1
+      RSK_CHECK_LAUNCH("bloom_sa1");
+    }
+    {
+      ProfScope ps(c, "bloom_st_mid");
+      hipLaunchKernelGGL(sa_size_kernel, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, cursor, cap_blocks, P, ncp,
+                         tot, bud);
+      RSK_CHECK_LAUNCH("bloom_sa_size");
+      hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot, bud, ncp, reg_off, tile_off);
+      RSK_CHECK_LAUNCH("bloom_st_offsets");
+    }
+    {
+      ProfScope ps(c, "bloom_st2");
+      hipLaunchKernelGGL(bloom_sa2_kernel, dim3(ncp), dim3(SA2_T), 0, c->stream, region, cap_probes, cursor,
+                         cap_blocks, P, nb2, reg_off, tile_off, used, l2, h2, tb2, (int)(dbg & 2));
+      RSK_CHECK_LAUNCH("bloom_sa2");
+    }
+    {
+      ProfScope ps(c, "bloom_st_mid");
+      hipLaunchKernelGGL(st_transpose_kernel, dim3((uint32_t)((tt_max + 63) / 64), (nb2 + 1 + 63) / 64), dim3(256), 0,
+                         c->stream, h2, tt_max, nb2 + 1, h2t);
+      RSK_CHECK_LAUNCH("bloom_st_transpose2");
+    }
+    {
+      ProfScope ps(c, "bloom_st_apply");
+#define RSK_APPLY(U)                                                                                          \
+  launch_persistent((const void*)bloom_st_apply_kernel<U>, TA, ns, c, [&](uint32_t grid) {                  \
+    hipLaunchKernelGGL((bloom_st_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2,  \
+                       tb2, (uint64_t)0, (uint64_t)0, tile_off, used, P, ns, b->d_bits, b->nwords);         \
+  })
+      if (ua == 8) RSK_APPLY(8);
+      else RSK_APPLY(4);
+#undef RSK_APPLY
+      RSK_CHECK_LAUNCH("bloom_st_apply");
+    }
+    uint32_t ov = 0;
+    RSK_HIP(hipMemcpyAsync(c->h_small + 8448, overflow, 4, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(&ov, c->h_small + 8448, 4);
+    if (ov) redo.push_back(dk);
+  }
+  // A coarse bin whose region filled up (only adversarial inputs can) lost
+  // some probes of its chunk; ORing is idempotent, so the chunk is redone by
+  // the exact-offset pipeline.
+  for (const DevKeys& dk : redo)
+    if (!bloom_add_partitioned(c, b, dk)) bloom_add_direct_launch(c, b, dk);
+  return true;
+}
+
 }  // namespace
 
 bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
@@ -592,6 +986,7 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t ncp = nb1 * P;
   uint64_t chunk = std::max<uint64_t>(1, probe_chunk() / k / kst) * kst;  // keys per chunk, whole super-tiles
   chunk = std::min<uint64_t>(chunk, keys.n);
+  if (f2 && env_u32("RSK_BLOOM_SA", 0)) return bloom_add_append(c, b, keys, f16, kmax, t1, kst, f2, shift1, nb1, P, chunk);
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };

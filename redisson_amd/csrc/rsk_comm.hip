@@ -188,7 +188,7 @@ int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
     uint8_t* regs = ok ? h->d_regs + id * (uint64_t)rsk::HLL_REGS : c->work(rsk::HLL_REGS);
     if (ok) {
       rsk::hll_materialize(h);
-      h->zero = false;
+      rsk::hll_touch(h);
     } else {
       RSK_HIP(hipMemsetAsync(regs, 0, rsk::HLL_REGS, c->stream));
     }
@@ -209,7 +209,7 @@ int rsk_hll_allreduce_pool(rsk_hll* h) {
   return guarded([&] {
     need(h != nullptr, "bad pool");
     rsk::hll_materialize(h);
-    h->zero = false;
+    rsk::hll_touch(h);
     rsk_ctx* c = h->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
@@ -229,7 +229,7 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
   return guarded([&] {
     need(h && first_out && count_out, "NULL argument");
     rsk::hll_materialize(h);
-    h->zero = false;
+    rsk::hll_touch(h);
     rsk_ctx* c = h->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
@@ -256,7 +256,7 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
     need(h && (ids || n == 0), "NULL argument");
     need((flags & ~RSK_FETCH_SELF) == 0, "unknown flags");
     rsk::hll_materialize(h);
-    h->zero = false;
+    rsk::hll_touch(h);
     rsk_ctx* c = h->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);

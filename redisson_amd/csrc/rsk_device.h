@@ -439,6 +439,13 @@ RSK_DEV void bloom_key_hashes(const uint8_t* __restrict__ data, const uint64_t* 
 // Bit i of the Redis string (byte i>>3, mask 0x80>>(i&7); bitops.c) inside
 // its little-endian u32 word i>>5.  Any base that is a multiple of 32 bits
 // keeps the mask, so slice-local indices use it too.
+// Workgroup barrier that orders LDS only: each wave waits for its own LDS
+// traffic (lgkmcnt) and meets the others, but its global loads, stores and
+// atomics stay in flight (__syncthreads' release fence would drain them:
+// s_waitcnt vmcnt(0) before every barrier).  For kernels whose global
+// writes are not read back by other waves of the same launch.
+RSK_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 RSK_DEV uint32_t bloom_bit_mask(uint64_t idx) {
   return 1u << ((uint32_t)((idx >> 3) & 3) * 8 + 7 - (uint32_t)(idx & 7));
 }

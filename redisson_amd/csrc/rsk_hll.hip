@@ -18,6 +18,7 @@
 // global atomics), and raises a flag if any register grew.
 #include <hipcub/hipcub.hpp>
 
+#include "rsk_hllcount.h"
 #include "rsk_internal.h"
 
 namespace rsk {
@@ -656,9 +657,9 @@ __global__ __launch_bounds__(256) void hll_add_grouped_bytes_kernel(const uint8_
 }
 
 void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
-                            bool pool_zero, bool write_all) {
+                            bool pool_zero, bool write_all, PCount pc) {
   if (k.n == 0) return;
-  if (hll_add_grouped_partitioned(c, k, d_groups, d_regs, G, pool_zero, write_all)) return;  // large batches: per-sketch LDS updates
+  if (hll_add_grouped_partitioned(c, k, d_groups, d_regs, G, pool_zero, write_all, pc)) return;  // large batches: per-sketch LDS updates
   uint64_t blocks = (k.n + 255) / 256;
   uint64_t cap = (uint64_t)c->num_cus * 16;
   if (blocks > cap) blocks = cap;
@@ -676,66 +677,6 @@ void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_grou
 }
 
 // ---------------------------------------------------------------- PFCOUNT
-RSK_DEV double pe(uint32_t r) {  // 2^-r, exact
-  return __longlong_as_double((long long)((uint64_t)(1023 - r) << 52));
-}
-
-// hllCount tail (Redis 3.2.0), FP64, compiled with -ffp-contract=off.
-// lc[ez] = m*log(m/ez) from the host libm.
-RSK_DEV uint64_t hll_estimate(double E, int ez, const double* __restrict__ lc) {
-  const double m = HLL_REGS;
-  double alpha = 0.7213 / (1 + 1.079 / m);
-  E = (1 / E) * alpha * m * m;
-  if (E < m * 2.5 && ez != 0) {
-    E = lc[ez];
-  } else if (E < 72000) {
-    double bias = 5.9119 * 1.0e-18 * (E * E * E * E) - 1.4253 * 1.0e-12 * (E * E * E) +
-                  1.2940 * 1.0e-7 * (E * E) - 5.2921 * 1.0e-3 * E + 83.3216;
-    E -= E * (bias / 100);
-  }
-  return (uint64_t)E;
-}
-
-// Redis sums 2^-reg in an encoding-specific order.  All orders agree when
-// every partial sum is exact: the terms are multiples of 2^-rmax, so every
-// partial sum below 2^(53-rmax) is an exact double.  The kernels therefore
-// sum in any order in FP64, each term built directly as the bits of 2^-r,
-// and compare the total with that bound.  Rounding is monotone and the
-// bound is representable, so the computed total reaches it iff the exact
-// total does; only then is Redis's order replayed serially (dense: groups
-// of 16; raw: u64 words).  Sparse keys always pass (registers <= 32).
-struct SumD {
-  double t;       // sum over all registers of 2^-r (a zero register adds 1)
-  uint32_t ez;    // zero registers
-  uint32_t rmax;  // largest register
-};
-
-RSK_DEV void acc_word(SumD& s, uint32_t w) {
-  // bit 7 of a byte of z is set exactly where that byte of w is zero
-  const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
-  s.ez += __popc(z);
-  const uint32_t r0 = w & 0xFFu, r1 = (w >> 8) & 0xFFu, r2 = (w >> 16) & 0xFFu, r3 = w >> 24;
-  const uint32_t m01 = r0 > r1 ? r0 : r1, m23 = r2 > r3 ? r2 : r3;
-  const uint32_t m = m01 > m23 ? m01 : m23;
-  s.rmax = m > s.rmax ? m : s.rmax;
-  s.t += (pe(r0) + pe(r1)) + (pe(r2) + pe(r3));
-}
-
-RSK_DEV SumD wave_reduce(SumD s) {
-  for (int off = 32; off > 0; off >>= 1) {
-    s.t += __shfl_down(s.t, off, 64);
-    s.ez += __shfl_down(s.ez, off, 64);
-    const uint32_t o = __shfl_down(s.rmax, off, 64);
-    s.rmax = o > s.rmax ? o : s.rmax;
-  }
-  return s;
-}
-
-// Every summation order gives s.t exactly (see above).
-RSK_DEV bool exact_total(const SumD& s) {
-  return s.t < __longlong_as_double((long long)((uint64_t)(1023 + 53 - s.rmax) << 52));  // 2^(53-rmax)
-}
-
 // One sketch's 16 KiB as 16 uint4 per lane of a wave.
 RSK_DEV SumD wave_sum(const uint4 (&v)[16]) {
   SumD s{0.0, 0, 0};
@@ -766,7 +707,8 @@ RSK_DEV double dense_order_sum(const uint8_t* r, int* ezp) {
 // in flight at once; no LDS and no barrier.
 __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
                                                         const uint64_t* __restrict__ ids, SmallIds small, uint64_t n,
-                                                        const double* __restrict__ lc, uint64_t* __restrict__ out) {
+                                                        const double* __restrict__ lc, uint64_t* __restrict__ out,
+                                                        PCount pc) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; b < n; b += nwaves) {
@@ -774,6 +716,14 @@ __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restric
     const uint64_t cached = card[id];
     if ((cached >> 63) == 0) {  // HLL_VALID_CACHE
       if (lane == 0) out[b] = cached;
+      continue;
+    }
+    if (pc.pcount && pc.pepoch[id] == pc.epoch) {  // estimated by the grouped add from these registers
+      if (lane == 0) {
+        const uint64_t est = pc.pcount[id];
+        out[b] = est;
+        card[id] = est;
+      }
       continue;
     }
     const uint8_t* r = regs + id * HLL_REGS;
@@ -793,13 +743,13 @@ __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restric
 }
 
 void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
-                      const SmallIds& small, uint64_t n, uint64_t* d_out) {
+                      const SmallIds& small, uint64_t n, uint64_t* d_out, PCount pc) {
   if (n == 0) return;
   uint64_t grid = (n + 3) / 4;  // 4 waves (sketches) per workgroup
   if (grid > (1u << 20)) grid = 1u << 20;
   ProfScope ps(c, "hll_count");
   hipLaunchKernelGGL(hll_count_kernel, dim3((uint32_t)grid), dim3(256), 0, c->stream, d_regs, d_card, d_ids, small, n,
-                     c->d_lc, d_out);
+                     c->d_lc, d_out, pc);
   RSK_CHECK_LAUNCH("hll_count");
 }
 

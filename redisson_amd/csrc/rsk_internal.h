@@ -112,6 +112,15 @@ struct rsk_hll {
   // that rewrites every row anyway (hll_gapply with write_all), or by
   // hll_materialize before any other access.
   mutable bool pending_clear = false;
+  // PFCOUNT precomputed by the partitioned grouped add (hll_gapply estimates
+  // every row it writes, from LDS): d_pcount[g] is valid while d_pepoch[g] ==
+  // pc_epoch.  Every entry point that may write registers bumps pc_epoch
+  // (hll_touch), so a stale estimate is never used; rsk_hll_count takes a
+  // valid one instead of re-reading the 16 KiB row, and refreshes the Redis
+  // card cache with it exactly as PFCOUNT would.
+  uint64_t* d_pcount = nullptr;
+  uint32_t* d_pepoch = nullptr;
+  mutable uint32_t pc_epoch = 1;
   // rsk_hll_merge_batch leveling state per sketch id (valid while stamp == lv_epoch)
   std::vector<uint32_t> lv_stamp, lv_w, lv_r;
   uint32_t lv_epoch = 0;
@@ -154,15 +163,22 @@ struct DevKeys {
 // (device u32) to 1 if any register grew.
 void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64_t* d_card, uint32_t* d_flag,
                     uint32_t epoch, bool created);
+// Registers of h may change: drop "known zero" and every precomputed PFCOUNT.
+void hll_touch(const rsk_hll* h);
+struct PCount {  // where hll_gapply leaves its estimates (none: pcount == nullptr)
+  uint64_t* pcount;
+  uint32_t* pepoch;
+  uint32_t epoch;
+};
 void hll_add_grouped_launch(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
-                            bool pool_zero = false, bool write_all = false);
+                            bool pool_zero = false, bool write_all = false, PCount pc = PCount{nullptr, nullptr, 0});
 // Up to 8 sketch ids passed by value (saves a host->device copy per PFCOUNT).
 struct SmallIds {
   uint64_t v[8];
   uint32_t n;
 };
 void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
-                      const SmallIds& small, uint64_t n, uint64_t* d_out);
+                      const SmallIds& small, uint64_t n, uint64_t* d_out, PCount pc = PCount{nullptr, nullptr, 0});
 void hll_union_count_launch(rsk_ctx* c, const uint8_t* const* d_member_ptrs, uint32_t arity, uint64_t n,
                             uint64_t* d_out);
 void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* const* d_src_ptrs, uint32_t srcs_per_dst,
@@ -186,7 +202,7 @@ void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // batch is not worth it (or not 16-byte keys): use the direct kernel.
 bool hll_grouped_partition_applies(const DevKeys& k, uint64_t G);
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
-                                 bool pool_zero, bool write_all);
+                                 bool pool_zero, bool write_all, PCount pc);
 // Performs a pending lazy clear (rsk_api.hip).
 void hll_materialize(const rsk_hll* h);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);

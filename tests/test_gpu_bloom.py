@@ -159,7 +159,9 @@ ST_CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000
 
 
 ST_KNOBS = ["RSK_BLOOM_ST=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T1=1024", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_CHUNK=300000",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_ST_TINY_BUDGET=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4"]
+            "RSK_BLOOM_ST=1,RSK_BLOOM_ST_TINY_BUDGET=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA=1,RSK_BLOOM_ST_CHUNK=300000",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=1,RSK_BLOOM_SA_TINY=1"]
 
 
 @pytest.mark.parametrize("size,k,n", ST_CASES)
@@ -168,9 +170,10 @@ def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs)
     """The super-tile insert (rsk_bloom_st.hip), forced on, gives the oracle's
     bit string: one level (<= 256 slices) and two (301 and 7,657 slices), k in
     {1, 2, 5, 7, 8} (1024-key super-tiles) and {9, 16} (512-key), 1024-lane
-    super-tiles, many chunks, 512-lane st2 with 4 segments per apply step, and
-    a tile budget of one tile per (bin, part), which overflows into the
-    exact-offset fallback."""
+    super-tiles, many chunks; two-level filters through the header pipeline
+    (st1/st2, default) with a one-tile budget (overflow) and 512-lane st2, and
+    through the append pipeline (sa1/sa2, RSK_BLOOM_SA=1) with many chunks and
+    with regions too small, which overflow into the exact-offset fallback."""
     from redisson_amd import KeyBatch
 
     for kv in filter(None, knobs.split(",")):
@@ -214,8 +217,8 @@ def test_slice_routed_skewed_keys(L, engine, orc, monkeypatch, knobs):
     L.rsk_bloom_destroy(b)
 
 
-@pytest.mark.parametrize("path", ["RSK_BLOOM_ST"])
-def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, path):
+@pytest.mark.parametrize("sa", ["1", "0"])
+def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, sa):
     """At the C3 filter size (9,585,058,377 bits, 18,283 slices: 143 coarse bins
     x 128 slices) the super-tile insert and the direct atomicOr kernel set
     identical bits."""
@@ -225,8 +228,9 @@ def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, path):
     ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
     ks = ins.keys_fixed(n, 16).as_struct()
     filters = {}
+    monkeypatch.setenv("RSK_BLOOM_SA", sa)
     for mode in ("1", "0"):
-        monkeypatch.setenv(path, mode)
+        monkeypatch.setenv("RSK_BLOOM_ST", mode)
         monkeypatch.setenv("RSK_BLOOM_PARTITION", "0")
         f = _filter(L, engine, size, k)
         _lib.check(L.rsk_bloom_add(f, ctypes.byref(ks), None))

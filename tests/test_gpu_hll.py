@@ -610,6 +610,9 @@ def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, monkeypa
     ref = np.zeros(G * 16384, np.uint8)
     orc.hll_add_gen_grouped_zipf_subset(ref, G, G, 1.1, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
     assert np.array_equal(part, ref)
+    # PFCOUNT of every sketch: estimated by the grouped add (split heavy bins excluded) or recomputed
+    want = [orc.hll_count_dense(ref[i * 16384:(i + 1) * 16384]) for i in range(G)]
+    assert _count(L, pools["1"], list(range(G))).tolist() == want
     for h in pools.values():
         L.rsk_hll_destroy(h)
 
@@ -634,4 +637,61 @@ def test_c5_zipf_full_size_hot_groups_bit_exact(L, engine, orc):
     assert np.array_equal(got, ref)
     cnt = _count(L, h, list(range(gs)))
     assert [int(c) for c in cnt[:64]] == [orc.hll_count_dense(ref[i]) for i in range(64)]
+    L.rsk_hll_destroy(h)
+
+
+def test_grouped_add_precomputed_counts_follow_later_writes(L, engine, orc, monkeypatch):
+    """The partitioned grouped add leaves every written row's PFCOUNT estimate
+    for rsk_hll_count (no 16 KiB re-read); any later write to the pool (PFADD,
+    PFMERGE, raw merge, import, clear, a second grouped add) must retire those
+    estimates, and every count must equal the oracle's on the current registers."""
+    from redisson_amd import KeyBatch, _lib, devmem
+
+    monkeypatch.setenv("RSK_HLL_GPART", "1")
+    G, n = 300, 600_000
+    h = _pool(L, engine, G)
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+    ks = k.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+
+    def check_all():
+        regs = _pool_regs(L, engine, h, G).reshape(G, 16384)
+        want = [orc.hll_count_dense(regs[i]) for i in range(G)]
+        assert _count(L, h, list(range(G))).tolist() == want
+        assert _count(L, h, list(range(G))).tolist() == want  # second call: from the card cache
+        return regs
+
+    check_all()
+    # each writer, then the counts of the whole pool again
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))  # idempotent re-add: fresh estimates
+    check_all()
+    ka = orc.gen_keys16(0x5EED0300, 0, 40_000)
+    _add(L, h, KeyBatch.from_numpy(ka.reshape(-1, 16)), 7)
+    regs = check_all()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    pools = (ctypes.c_void_p * 1)(h.value)
+    srcs = (ctypes.c_uint64 * 1)(7)
+    _lib.check(L.rsk_hll_merge(h, 11, pools, srcs, 1))
+    check_all()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    raw = np.full(16384, 9, np.uint8)
+    _lib.check(L.rsk_hll_merge_raw(h, 13, raw.ctypes.data, _lib.RSK_MEM_HOST))
+    check_all()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    sp = orc.hll_encode_sparse(regs[3])
+    b = (ctypes.c_uint8 * len(sp)).from_buffer_copy(sp)
+    _lib.check(L.rsk_hll_import_redis(h, 17, b, len(sp)))
+    check_all()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    _lib.check(L.rsk_hll_clear(h))
+    assert _count(L, h, list(range(G))).tolist() == [0] * G
+    # a second grouped add over a different stream after the clear
+    g2, k2 = devmem.gen_grouped(engine, 0x5EED0306, G, 0, n)
+    ks2 = k2.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks2), g2.ptr))
+    ref = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped(ref, G, 0x5EED0306, 0, n)
+    assert np.array_equal(check_all().reshape(-1), ref)
+    for x in (g, k, g2, k2):
+        x.free()
     L.rsk_hll_destroy(h)
