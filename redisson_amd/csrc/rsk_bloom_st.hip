@@ -528,19 +528,17 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
 
 // ============================================ append variant (two-level filters)
 // sa1: the st1 super-tile (one hash pass, ranks by coarse bin, bin-sorted LDS
-// image), but each coarse bin's run is APPENDED to that bin's own region in
-// blocks of SA_B probes: a workgroup keeps one open block per bin and takes
-// new blocks from the bin's cursor with one atomicAdd for a whole run (issued
-// before the placement, consumed after it).  The region of bin c is then a
-// contiguous run of full blocks (plus one INVALID-padded tail block per
-// workgroup), so sa2 streams it with coalesced 16-byte loads -- no headers,
-// no segment planner, no transpose.
-// sa2: one workgroup per (c, p) streams blocks [nblk p / P, nblk (p+1) / P) of
-// bin c, ranks by fine bin and writes bin-sorted tiles exactly like st2, whose
-// output the apply kernel reads unchanged.  Tile count per (c, p) is exact:
-// ceil(probes / SA2_SLOTS).  A bin whose region overflows (only adversarial
-// inputs: 1.25x the expected share) sets `overflow`; the chunk is redone.
-constexpr uint32_t SA_B = 1024;     // probes per block
+// image), but each coarse bin's run is APPENDED to this workgroup's private
+// sub-region for that bin: sub-region (w, c) = probes [(w nb1 + c) quota,
+// + quota), so a run's destination is known as soon as the tile's bin counts
+// are (no global atomics, no headers); the workgroup records how many probes
+// it appended per bin (used[w][c]).
+// sa2: one workgroup per (c, p) streams the sub-regions (w, c) of the
+// workgroups w of part p with coalesced 16-byte loads (a tile never spans two
+// sub-regions), ranks by fine bin and writes bin-sorted tiles exactly like
+// st2, whose output the apply kernel reads unchanged.  A sub-region that
+// overflows (only adversarial inputs: 1.25x the expected share per
+// workgroup) sets `overflow`; the chunk is redone.
 constexpr int SA2_V = 3;            // sa2: uint4 loads (4 probes) per lane per tile (96 per fine bin: apply's 2 x 64 fast path)
 constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
 constexpr uint32_t SA2_SLOTS = SA2_T * SA2_V * 4;
@@ -550,27 +548,30 @@ RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads in
   else lds_barrier();
 }
 
+// 512-lane workgroups: at most 80 VGPRs, so 3 workgroups (6 waves per SIMD) share a CU
 template <bool FIXED16, int KMAX, int T1>
-__global__ __launch_bounds__(T1) void bloom_sa1_kernel(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(T1, T1 == 512 ? 6 : 4) void bloom_sa1_kernel(const uint8_t* __restrict__ data,
                                                        const uint64_t* __restrict__ offsets, uint32_t fixed_len,
                                                        uint64_t n, FastMod63 fm, int k, uint32_t shift1, uint32_t nb1,
-                                                       uint64_t nst, uint32_t* __restrict__ region,
-                                                       uint64_t cap_probes, uint32_t cap_blocks,
-                                                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ overflow,
-                                                       int dbg) {
+                                                       uint64_t nst, uint32_t* __restrict__ region, uint32_t quota,
+                                                       uint32_t limit, uint32_t* __restrict__ used,
+                                                       uint32_t* __restrict__ overflow, int dbg) {
   constexpr int KPL = 16 / KMAX;
   constexpr uint32_t KST = T1 * KPL;
   constexpr int NP = KPL * KMAX;
   constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
-  __shared__ __attribute__((aligned(16))) uint32_t img[T1 * NP];
-  __shared__ uint32_t hist[256], lstart[256], pos[256], room[256], p1[256], r1[256], p2[256];
-  __shared__ uint4 runs[256];  // per bin: image start, length, probes to the open block, its position
+  // runs are padded to multiples of 4 probes (INVALID), so the write-out
+  // moves 16-byte groups of one bin to 16-byte aligned destinations
+  constexpr uint32_t IMG = T1 * NP + 4 * 256;
+  __shared__ __attribute__((aligned(16))) uint32_t img[IMG];
+  __shared__ uint8_t ibin[IMG / 4];
+  __shared__ uint32_t hist[256], lstart[256], pos[256], dst[256], s_total;
   const uint64_t low = (1ull << shift1) - 1;
   if (threadIdx.x < 256) {
     hist[threadIdx.x] = 0;
     pos[threadIdx.x] = 0;
-    room[threadIdx.x] = 0;  // no open block yet
   }
+  uint32_t* const mine = region + (uint64_t)blockIdx.x * nb1 * quota;  // sub-regions (blockIdx.x, 0..nb1)
   const uint4* keys16 = reinterpret_cast<const uint4*>(data);
   uint4 nxt[KPL];
   auto fetch = [&](uint64_t st) {
@@ -622,10 +623,9 @@ __global__ __launch_bounds__(T1) void bloom_sa1_kernel(const uint8_t* __restrict
       }
     }
     sa_bar(dbg);  // (A) every rank taken
-    // wave 0: bin starts, and for each bin's run of L probes: the first
-    // min(L, room) go to the open block, the rest to ceil(rest / SA_B) new
-    // blocks taken with one atomicAdd (its result is used after the placement)
-    uint32_t nbk[PER], rest[PER], base[PER];
+    // wave 0: bin starts and run destinations (runs of L probes take
+    // L4 = round_up(L, 4) slots, the tail INVALID): image position j of bin b
+    // goes to mine[j + dst[b]] (mod 2^32), dst[b] = b quota + pos[b] - lstart[b]
     if (threadIdx.x < 64) {
       uint32_t v[PER], sum = 0;
 #pragma unroll
@@ -633,154 +633,141 @@ __global__ __launch_bounds__(T1) void bloom_sa1_kernel(const uint8_t* __restrict
         const uint32_t b = lane * PER + i;
         v[i] = b < nb1 ? hist[b] : 0;
         if (b < nb1) hist[b] = 0;
-        sum += v[i];
+        sum += (v[i] + 3) & ~3u;
       }
       const uint32_t incl = wave_scan_incl(sum, lane);
-      uint32_t run = incl - sum;
+      uint32_t at = incl - sum;
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const uint32_t b = lane * PER + i;
-        nbk[i] = 0;
-        rest[i] = 0;
-        base[i] = 0;
+        const uint32_t l4 = (v[i] + 3) & ~3u;
         if (b < nb1) {
-          lstart[b] = run;
-          const uint32_t rm = room[b], a = v[i] < rm ? v[i] : rm;
-          p1[b] = pos[b];
-          r1[b] = a;
-          rest[i] = v[i] - a;
-          if (rest[i]) {
-            nbk[i] = (rest[i] + SA_B - 1) / SA_B;
-            base[i] = atomicAdd(&cursor[b], nbk[i]);
-          } else {
-            pos[b] += a;
-            room[b] = rm - a;
+          lstart[b] = at;
+          for (uint32_t j = at + v[i]; j < at + l4; ++j) img[j] = INVALID;
+          const uint32_t p = pos[b];
+          if (p + l4 <= limit) {  // limit = quota (< quota only in tests)
+            dst[b] = b * quota + p - at;
+            pos[b] = p + l4;
+          } else {  // sub-region full: drop the run (the host redoes the chunk)
+            if (v[i]) atomicOr(overflow, 1u);
+            dst[b] = INVALID;
           }
         }
-        run += v[i];
+        at += l4;
       }
+      if (lane == 63) s_total = incl;
     }
-    sa_bar(dbg);  // (B) lstart / total ready (the cursor atomics stay in flight)
+    sa_bar(dbg);  // (B) lstart / dst / total ready
 #pragma unroll
     for (int s = 0; s < NP; ++s)
       if (tag[s] != INVALID) {
-        img[lstart[tag[s] >> 16] + (tag[s] & 0xFFFFu)] = pay[s];
+        const uint32_t b = tag[s] >> 16, r = tag[s] & 0xFFFFu, j = lstart[b] + r;
+        img[j] = pay[s];
+        if ((r & 3) == 0) ibin[j >> 2] = (uint8_t)b;  // the group's first slot always holds a probe
       }
-    if (threadIdx.x < 64) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t b = lane * PER + i;
-        if (b < nb1 && rest[i]) {
-          if (base[i] + nbk[i] <= cap_blocks) {
-            p2[b] = base[i] * SA_B;
-            pos[b] = base[i] * SA_B + rest[i];
-            room[b] = nbk[i] * SA_B - rest[i];
-          } else {  // region full: drop the run (the host redoes the chunk)
-            atomicOr(overflow, 1u);
-            p2[b] = INVALID;
-            room[b] = 0;
-          }
-        }
-        if (b < nb1) runs[b] = make_uint4(lstart[b], r1[b] + rest[i], r1[b], p1[b]);
-      }
-    }
-    sa_bar(dbg);  // (C) image and run destinations complete
-    // bin-major write-out: wave w writes the runs of bins w, w + NW, ...; the
-    // per-bin values are LDS broadcasts, each lane moves one probe per step
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    for (uint32_t b = wv; b < nb1; b += T1 / 64) {
-      const uint4 r = runs[b];  // x: image start, y: length, z: to the open block, w: its position
-      if (!r.y) continue;
-      const uint32_t q = p2[b];
-      uint32_t* rb = region + (uint64_t)b * cap_probes;
-      for (uint32_t o = lane; o < r.y; o += 64) {
-        const uint32_t v = img[r.x + o];
-        if (o < r.z) rb[r.w + o] = v;
-        else if (q != INVALID) rb[q + (o - r.z)] = v;
+    const uint32_t total4 = s_total >> 2;
+    sa_bar(dbg);  // (C) image complete
+    const uint4* img4 = reinterpret_cast<const uint4*>(img);
+    for (uint32_t g = threadIdx.x; g < total4; g += T1) {
+      const uint32_t d = dst[ibin[g]];
+      if (d != INVALID) {
+        const uint4 v = img4[g];
+        u32x4 x = {v.x, v.y, v.z, v.w};
+        *reinterpret_cast<u32x4*>(mine + (4 * g + d)) = x;
       }
     }
   }
   __syncthreads();
-  // pad every open block's tail with INVALID (sa2 streams whole blocks)
-  for (uint32_t b = 0; b < nb1; ++b) {
-    const uint32_t rm = room[b], ps = pos[b];
-    for (uint32_t q = threadIdx.x; q < rm; q += T1) region[(uint64_t)b * cap_probes + ps + q] = INVALID;
-  }
+  if (threadIdx.x < nb1) used[(uint64_t)blockIdx.x * nb1 + threadIdx.x] = pos[threadIdx.x];
 }
 
-// tot[cp] = streamed probes of (c, p) (INVALID padding included), bud[cp] = its tiles
-__global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict__ cursor, uint32_t cap_blocks,
+// tot[cp] = probes of (c, p), bud[cp] = its sa2 tiles (one per SA2_SLOTS of each sub-region)
+__global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
                                                       uint32_t P, uint32_t ncp, uint64_t* __restrict__ tot,
                                                       uint32_t* __restrict__ bud) {
   const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
   if (cp >= ncp) return;
   const uint32_t c = cp / P, p = cp - c * P;
-  const uint64_t nblk = min(cursor[c], cap_blocks);
-  const uint64_t probes = (nblk * (p + 1) / P - nblk * p / P) * SA_B;
+  uint64_t probes = 0;
+  uint32_t tiles = 0;
+  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
+    const uint32_t u = used[(uint64_t)w * nb1 + c];
+    probes += u;
+    tiles += (u + SA2_SLOTS - 1) / SA2_SLOTS;
+  }
   tot[cp] = probes;
-  bud[cp] = (uint32_t)((probes + SA2_SLOTS - 1) / SA2_SLOTS);
+  bud[cp] = tiles;
 }
 
-__global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __restrict__ region, uint64_t cap_probes,
-                                                          const uint32_t* __restrict__ cursor, uint32_t cap_blocks,
+__global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __restrict__ region, uint32_t quota,
+                                                          const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
                                                           uint32_t P, uint32_t nb2,
                                                           const uint64_t* __restrict__ reg_off,
                                                           const uint32_t* __restrict__ tile_off,
-                                                          uint32_t* __restrict__ used, uint32_t* __restrict__ out,
+                                                          uint32_t* __restrict__ tiles_out, uint32_t* __restrict__ out,
                                                           uint16_t* __restrict__ h2, uint64_t* __restrict__ tb2,
                                                           int dbg) {
   constexpr int NV = SA2_V * 4;
-  __shared__ __attribute__((aligned(16))) uint32_t srt[2][SA2_SLOTS];
+  // one image buffer: with LDS-only barriers a wave's write-out of tile t is
+  // done before it reaches (A) of t+1, and the image is rewritten after (B)
+  __shared__ __attribute__((aligned(16))) uint32_t srt[1][SA2_SLOTS];
   __shared__ uint32_t hist[128], lstart[128], s_total;
   __shared__ uint16_t s_hdr[129];
   const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
-  const uint64_t nblk = min(cursor[c], cap_blocks);
-  const uint64_t b0 = nblk * p / P, b1 = nblk * (p + 1) / P;
-  const uint4* in = reinterpret_cast<const uint4*>(region + (uint64_t)c * cap_probes + b0 * SA_B);
-  const uint64_t n4 = (b1 - b0) * (SA_B / 4);  // uint4 of this (c, p)
   if (threadIdx.x < 128) hist[threadIdx.x] = 0;
   const uint64_t base = reg_off[cp];
   const uint32_t tbeg = tile_off[cp];
   uint64_t written = 0;
-  uint32_t ntile = 0, buf = 0;
+  uint32_t ntile = 0;
   __syncthreads();
-  for (uint64_t q0 = 0; q0 < n4; q0 += SA2_SLOTS / 4) {
-    uint32_t pay[NV], tag[NV];
+  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
+    const uint32_t nu = used[(uint64_t)w * nb1 + c];  // probes of sub-region (w, c)
+    const uint32_t* sub = region + ((uint64_t)w * nb1 + c) * quota;
+    const uint4* in = reinterpret_cast<const uint4*>(sub);  // quota is a multiple of 4: 16-byte aligned
+    for (uint32_t t0 = 0; t0 < nu; t0 += SA2_SLOTS) {
+      uint32_t pay[NV], tag[NV];
 #pragma unroll
-    for (int v = 0; v < SA2_V; ++v) {
-      const uint64_t q = q0 + (uint64_t)v * SA2_T + threadIdx.x;
-      const uint4 x = q < n4 ? ld_nt16(in + q) : make_uint4(INVALID, INVALID, INVALID, INVALID);
-      pay[4 * v] = x.x;
-      pay[4 * v + 1] = x.y;
-      pay[4 * v + 2] = x.z;
-      pay[4 * v + 3] = x.w;
-    }
-#pragma unroll
-    for (int r = 0; r < NV; ++r) {
-      tag[r] = INVALID;
-      if (pay[r] != INVALID) {
-        const uint32_t bin = pay[r] >> SL_LOG;
-        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+      for (int v = 0; v < SA2_V; ++v) {
+        const uint32_t q4 = t0 / 4 + v * SA2_T + threadIdx.x;  // uint4 index
+        uint4 x = make_uint4(INVALID, INVALID, INVALID, INVALID);
+        if (4 * q4 + 3 < nu) {
+          x = ld_nt16(in + q4);
+        } else if (4 * q4 < nu) {
+          x.x = sub[4 * q4];
+          if (4 * q4 + 1 < nu) x.y = sub[4 * q4 + 1];
+          if (4 * q4 + 2 < nu) x.z = sub[4 * q4 + 2];
+        }
+        pay[4 * v] = x.x;
+        pay[4 * v + 1] = x.y;
+        pay[4 * v + 2] = x.z;
+        pay[4 * v + 3] = x.w;
       }
-    }
-    sa_bar(dbg);  // (A)
-    if (threadIdx.x < 64) wave0_bin_starts<128>(hist, lstart, nb2, s_hdr, &s_total);
-    sa_bar(dbg);  // (B)
-    const uint32_t total = s_total;
-    if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
-    if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
-    uint32_t* img = srt[buf];
 #pragma unroll
-    for (int r = 0; r < NV; ++r)
-      if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
-    sa_bar(dbg);  // (C)
-    uint32_t* o = out + base + written;
-    for (uint32_t j = threadIdx.x; j < total; j += SA2_T) o[j] = img[j];
-    written += total;
-    ++ntile;
-    buf ^= 1;
+      for (int r = 0; r < NV; ++r) {
+        tag[r] = INVALID;
+        if (pay[r] != INVALID) {
+          const uint32_t bin = pay[r] >> SL_LOG;
+          tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+        }
+      }
+      sa_bar(dbg);  // (A)
+      if (threadIdx.x < 64) wave0_bin_starts<128>(hist, lstart, nb2, s_hdr, &s_total);
+      sa_bar(dbg);  // (B)
+      const uint32_t total = s_total;
+      if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
+      if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
+      uint32_t* img = srt[0];
+#pragma unroll
+      for (int r = 0; r < NV; ++r)
+        if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
+      sa_bar(dbg);  // (C)
+      uint32_t* o = out + base + written;
+      for (uint32_t j = threadIdx.x; j < total; j += SA2_T) o[j] = img[j];
+      written += total;
+      ++ntile;
+    }
   }
-  if (threadIdx.x == 0) used[cp] = ntile;
+  if (threadIdx.x == 0) tiles_out[cp] = ntile;
 }
 
 int st_mode() {
@@ -835,8 +822,6 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  // sa1 grid (persistent) and the per-bin region: 1.25x a full coarse bin's
-  // expected share of the probes, plus one open block per workgroup.
   const void* k1 = t1 == 1024 ? (f16 ? (kmax == 8 ? (const void*)bloom_sa1_kernel<true, 8, 1024>
                                                   : (const void*)bloom_sa1_kernel<true, 16, 1024>)
                                      : (kmax == 8 ? (const void*)bloom_sa1_kernel<false, 8, 1024>
@@ -850,18 +835,24 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     (void)hipGetLastError();
     per_cu = 1;
   }
-  const uint32_t grid1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_nst, (uint64_t)per_cu * cus));
-  const double share = (double)(1ull << shift1) / (double)(uint64_t)b->size;  // of one full coarse bin
-  const uint64_t slack = env_u32("RSK_BLOOM_SA_TINY", 0) ? 0 : 1;           // tests force the overflow fallback
-  const uint32_t cap_blocks =
-      (uint32_t)(slack * ((uint64_t)(1.25 * share * (double)max_np) / SA_B + 2ull * grid1 + 16) + (1 - slack) * 2);
-  const uint64_t cap_probes = (uint64_t)cap_blocks * SA_B;
-  if (cap_probes >= (1ull << 31)) return false;  // u32 run positions (INVALID = dropped) -> the exact-offset pipeline
-  const uint64_t region_probes = (uint64_t)nb1 * cap_probes;
-  const uint64_t tt_max = region_probes / SA2_SLOTS + ncp + 64;  // bound on sa2 tiles
+  // W persistent sa1 workgroups; each gets 1.25x its expected share of a full
+  // coarse bin per bin, plus one whole super-tile (a tile's run can be that
+  // long) and the <= 3 padding slots per run of each of its tiles.
+  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_nst, (uint64_t)per_cu * cus));
+  const double share = (double)(1ull << shift1) / (double)(uint64_t)b->size;
+  const bool tiny = env_u32("RSK_BLOOM_SA_TINY", 0) != 0;  // tests force the overflow fallback
+  // quota > one tile's probes: a valid run offset b quota + pos - lstart never equals INVALID
+  const uint64_t q64 = (uint64_t)(1.25 * share * (double)max_np / W) + kst * k + 3 * (max_nst / W + 1) + 64;
+  const uint32_t quota = (uint32_t)((q64 + 3) & ~uint64_t(3));
+  const uint32_t limit = tiny ? 32 : quota;
+  const uint64_t region_probes = (uint64_t)W * nb1 * quota;
+  if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;  // u32 offsets -> exact-offset pipeline
+  const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / SA2_SLOTS + (uint64_t)W * nb1 + 64;  // bound on sa2 tiles
   const uint64_t h2_bytes = al(tt_max * (nb2 + 1) * 2);
-  const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4 * nb1) + 256;
-  const uint64_t bytes = 2 * al(4 * region_probes) + 2 * h2_bytes + al(8 * tt_max) + meta;
+  const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256;
+  // sa2 places (c, p) at reg_off = prefix of its streamed probes, run padding included
+  const uint64_t l2_probes = max_np + 3ull * nb1 * max_nst;
+  const uint64_t bytes = al(4 * region_probes) + al(4 * l2_probes) + 2 * h2_bytes + al(8 * tt_max) + meta;
   uint8_t* w = c->work(bytes);
   uint8_t* q = w;
   auto take = [&](uint64_t n) {
@@ -870,7 +861,7 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     return r;
   };
   uint32_t* region = reinterpret_cast<uint32_t*>(take(al(4 * region_probes)));
-  uint32_t* l2 = reinterpret_cast<uint32_t*>(take(al(4 * region_probes)));
+  uint32_t* l2 = reinterpret_cast<uint32_t*>(take(al(4 * l2_probes)));
   uint16_t* h2 = reinterpret_cast<uint16_t*>(take(h2_bytes));
   uint16_t* h2t = reinterpret_cast<uint16_t*>(take(h2_bytes));
   uint64_t* tb2 = reinterpret_cast<uint64_t*>(take(al(8 * tt_max)));
@@ -878,27 +869,26 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   uint64_t* reg_off = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
   uint32_t* bud = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
   uint32_t* tile_off = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
-  uint32_t* used = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
-  uint32_t* cursor = reinterpret_cast<uint32_t*>(take(al(4 * nb1)));
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
+  uint32_t* used = reinterpret_cast<uint32_t*>(take(al(4ull * W * nb1)));
   uint32_t* overflow = reinterpret_cast<uint32_t*>(take(256));
 
   std::vector<DevKeys> redo;
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
     const uint64_t nst = (m + kst - 1) / kst;
+    const uint32_t Wc = (uint32_t)std::min<uint64_t>(W, nst);
     DevKeys dk = keys;
     dk.n = m;
     if (keys.offsets) dk.offsets = keys.offsets + first;
     else dk.data = keys.data + first * keys.fixed_len;
-    RSK_HIP(hipMemsetAsync(cursor, 0, 4 * nb1, c->stream));
     RSK_HIP(hipMemsetAsync(overflow, 0, 4, c->stream));
     {
       ProfScope ps(c, "bloom_st1");
-      const uint32_t grid = (uint32_t)std::min<uint64_t>(grid1, nst);
-#define RSK_SA1(F16, KM, TT)                                                                                   \
-  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, TT>), dim3(grid), dim3(TT), 0, c->stream, dk.data, dk.offsets, \
-                     dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, cap_probes, cap_blocks, cursor,    \
-                     overflow, (int)(dbg & 1))
+#define RSK_SA1(F16, KM, TT)                                                                                    \
+  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, TT>), dim3(Wc), dim3(TT), 0, c->stream, dk.data, dk.offsets,    \
+                     dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, overflow,    \
+                     (int)(dbg & 1))
       if (t1 == 1024) {
         if (f16 && kmax == 8) RSK_SA1(true, 8, 1024);
         else if (f16) RSK_SA1(true, 16, 1024);
@@ -915,16 +905,16 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     }
     {
       ProfScope ps(c, "bloom_st_mid");
-      hipLaunchKernelGGL(sa_size_kernel, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, cursor, cap_blocks, P, ncp,
-                         tot, bud);
+      hipLaunchKernelGGL(sa_size_kernel, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, used, Wc, nb1, P, ncp, tot,
+                         bud);
       RSK_CHECK_LAUNCH("bloom_sa_size");
       hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot, bud, ncp, reg_off, tile_off);
       RSK_CHECK_LAUNCH("bloom_st_offsets");
     }
     {
       ProfScope ps(c, "bloom_st2");
-      hipLaunchKernelGGL(bloom_sa2_kernel, dim3(ncp), dim3(SA2_T), 0, c->stream, region, cap_probes, cursor,
-                         cap_blocks, P, nb2, reg_off, tile_off, used, l2, h2, tb2, (int)(dbg & 2));
+      hipLaunchKernelGGL(bloom_sa2_kernel, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P, nb2,
+                         reg_off, tile_off, tiles, l2, h2, tb2, (int)(dbg & 2));
       RSK_CHECK_LAUNCH("bloom_sa2");
     }
     {
@@ -938,7 +928,7 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
 #define RSK_APPLY(U)                                                                                          \
   launch_persistent((const void*)bloom_st_apply_kernel<U>, TA, ns, c, [&](uint32_t grid) {                  \
     hipLaunchKernelGGL((bloom_st_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2,  \
-                       tb2, (uint64_t)0, (uint64_t)0, tile_off, used, P, ns, b->d_bits, b->nwords);         \
+                       tb2, (uint64_t)0, (uint64_t)0, tile_off, tiles, P, ns, b->d_bits, b->nwords);        \
   })
       if (ua == 8) RSK_APPLY(8);
       else RSK_APPLY(4);
@@ -951,9 +941,9 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     std::memcpy(&ov, c->h_small + 8448, 4);
     if (ov) redo.push_back(dk);
   }
-  // A coarse bin whose region filled up (only adversarial inputs can) lost
-  // some probes of its chunk; ORing is idempotent, so the chunk is redone by
-  // the exact-offset pipeline.
+  // A sub-region that filled up (only adversarial inputs can) lost some
+  // probes of its chunk; ORing is idempotent, so the chunk is redone by the
+  // exact-offset pipeline.
   for (const DevKeys& dk : redo)
     if (!bloom_add_partitioned(c, b, dk)) bloom_add_direct_launch(c, b, dk);
   return true;
@@ -986,7 +976,7 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t ncp = nb1 * P;
   uint64_t chunk = std::max<uint64_t>(1, probe_chunk() / k / kst) * kst;  // keys per chunk, whole super-tiles
   chunk = std::min<uint64_t>(chunk, keys.n);
-  if (f2 && env_u32("RSK_BLOOM_SA", 0)) return bloom_add_append(c, b, keys, f16, kmax, t1, kst, f2, shift1, nb1, P, chunk);
+  if (f2 && env_u32("RSK_BLOOM_SA", 1)) return bloom_add_append(c, b, keys, f16, kmax, t1, kst, f2, shift1, nb1, P, chunk);
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };

@@ -159,9 +159,10 @@ ST_CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000
 
 
 ST_KNOBS = ["RSK_BLOOM_ST=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T1=1024", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_CHUNK=300000",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_ST_TINY_BUDGET=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA=1,RSK_BLOOM_ST_CHUNK=300000",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=1,RSK_BLOOM_SA_TINY=1"]
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA_TINY=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA_DBG=3",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0", "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_TINY_BUDGET=1",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_CHUNK=300000"]
 
 
 @pytest.mark.parametrize("size,k,n", ST_CASES)
@@ -170,10 +171,11 @@ def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs)
     """The super-tile insert (rsk_bloom_st.hip), forced on, gives the oracle's
     bit string: one level (<= 256 slices) and two (301 and 7,657 slices), k in
     {1, 2, 5, 7, 8} (1024-key super-tiles) and {9, 16} (512-key), 1024-lane
-    super-tiles, many chunks; two-level filters through the header pipeline
-    (st1/st2, default) with a one-tile budget (overflow) and 512-lane st2, and
-    through the append pipeline (sa1/sa2, RSK_BLOOM_SA=1) with many chunks and
-    with regions too small, which overflow into the exact-offset fallback."""
+    super-tiles, many chunks; two-level filters through the append pipeline
+    (sa1/sa2, default; full barriers instead of LDS-only ones; sub-regions too
+    small, which overflow into the exact-offset fallback) and through the
+    header pipeline (st1/st2, RSK_BLOOM_SA=0) with a one-tile budget
+    (overflow), 512-lane st2 and many chunks."""
     from redisson_amd import KeyBatch
 
     for kv in filter(None, knobs.split(",")):
