@@ -133,6 +133,41 @@ RSK_DEV void wave0_bin_starts(uint32_t* hist, uint32_t* lstart, uint32_t nb, uin
   }
 }
 
+// wave0_bin_starts with every bin's run padded to a multiple of 4 slots
+// (INVALID in img), so runs start 16-byte aligned: starts and total padded.
+template <int NBMAX>
+RSK_DEV void wave0_bin_starts_pad4(uint32_t* hist, uint32_t* lstart, uint32_t nb, uint16_t* hdr_row,
+                                   uint32_t* s_total, uint32_t* img) {
+  constexpr int PER = NBMAX / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    v[i] = b < nb ? hist[b] : 0;
+    if (b < nb) hist[b] = 0;
+    sum += (v[i] + 3) & ~3u;
+  }
+  const uint32_t incl = wave_scan_incl(sum, lane);
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    const uint32_t l4 = (v[i] + 3) & ~3u;
+    if (b < nb) {
+      lstart[b] = run;
+      hdr_row[b] = (uint16_t)run;
+      for (uint32_t j = run + v[i]; j < run + l4; ++j) img[j] = INVALID;
+    }
+    run += l4;
+  }
+  const uint32_t total = rdl(incl, 63);
+  if (lane == 0) {
+    hdr_row[nb] = (uint16_t)total;
+    *s_total = total;
+  }
+}
+
 // Super-tile st = keys [st*KST, st*KST + KST): bin-sorted probes at
 // out[st * KST * k ...], header hdr[st][0..nb1] (bin offsets, [nb1] = total).
 // The sorted image is double-buffered in LDS, so a tile's write-out overlaps
@@ -542,6 +577,7 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
 constexpr int SA2_V = 3;            // sa2: uint4 loads (4 probes) per lane per tile (96 per fine bin: apply's 2 x 64 fast path)
 constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
 constexpr uint32_t SA2_SLOTS = SA2_T * SA2_V * 4;
+constexpr uint32_t SA2_PAD = 3 * 128;  // pad slots per sa2 tile, at most (<= 3 per fine bin)
 
 RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads instead of the LDS-only barrier
   if (dbg) __syncthreads();
@@ -695,7 +731,7 @@ __global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict
     probes += u;
     tiles += (u + SA2_SLOTS - 1) / SA2_SLOTS;
   }
-  tot[cp] = probes;
+  tot[cp] = ((probes + 3) & ~3ull) + (uint64_t)tiles * SA2_PAD;  // sa2 output bound: its tiles pad fine-bin runs
   bud[cp] = tiles;
 }
 
@@ -710,7 +746,7 @@ __global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __rest
   constexpr int NV = SA2_V * 4;
   // one image buffer: with LDS-only barriers a wave's write-out of tile t is
   // done before it reaches (A) of t+1, and the image is rewritten after (B)
-  __shared__ __attribute__((aligned(16))) uint32_t srt[1][SA2_SLOTS];
+  __shared__ __attribute__((aligned(16))) uint32_t srt[1][SA2_SLOTS + 4 * 128];  // + <= 3 pad slots per fine bin
   __shared__ uint32_t hist[128], lstart[128], s_total;
   __shared__ uint16_t s_hdr[129];
   const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
@@ -751,9 +787,9 @@ __global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __rest
         }
       }
       sa_bar(dbg);  // (A)
-      if (threadIdx.x < 64) wave0_bin_starts<128>(hist, lstart, nb2, s_hdr, &s_total);
+      if (threadIdx.x < 64) wave0_bin_starts_pad4<128>(hist, lstart, nb2, s_hdr, &s_total, srt[0]);
       sa_bar(dbg);  // (B)
-      const uint32_t total = s_total;
+      const uint32_t total = s_total;  // padded: a multiple of 4
       if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
       if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
       uint32_t* img = srt[0];
@@ -761,13 +797,102 @@ __global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __rest
       for (int r = 0; r < NV; ++r)
         if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = pay[r] & ((1u << SL_LOG) - 1);
       sa_bar(dbg);  // (C)
-      uint32_t* o = out + base + written;
-      for (uint32_t j = threadIdx.x; j < total; j += SA2_T) o[j] = img[j];
+      // 16-byte aligned: base and written are multiples of 4 slots
+      u32x4* o4 = reinterpret_cast<u32x4*>(out + base + written);
+      const uint4* i4 = reinterpret_cast<const uint4*>(img);
+      for (uint32_t j = threadIdx.x; j < total / 4; j += SA2_T) {
+        const uint4 v = i4[j];
+        u32x4 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, o4 + j);
+      }
       written += total;
       ++ntile;
     }
   }
   if (threadIdx.x == 0) tiles_out[cp] = ntile;
+}
+
+// Apply for the append pipeline's sa2 tiles: every fine-bin segment starts
+// 16-byte aligned and is padded to a multiple of 4 probes (INVALID), so a
+// half-wave loads one segment as up to 32 uint4 (128 probes) in one
+// instruction: UA segments per wave take UA/2 16-byte loads per lane.
+template <int UA>
+__global__ __launch_bounds__(TA) void bloom_sa_apply_kernel(const uint32_t* __restrict__ probes,
+                                                            const uint16_t* __restrict__ ht, uint64_t row_stride,
+                                                            uint32_t f2, const uint64_t* __restrict__ tb,
+                                                            const uint32_t* __restrict__ tile_off,
+                                                            const uint32_t* __restrict__ used, uint32_t P,
+                                                            uint32_t nslices, uint32_t* __restrict__ bits,
+                                                            uint64_t nwords) {
+  static_assert(UA % 2 == 0, "two segments per load instruction");
+  __shared__ __attribute__((aligned(16))) uint32_t sl[SL_WORDS];
+  const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t half = lane >> 5, l32 = lane & 31;
+  constexpr uint32_t NW = TA / 64;
+  const uint4* p4 = reinterpret_cast<const uint4*>(probes);
+  for (uint32_t s = blockIdx.x; s < nslices; s += gridDim.x) {
+    const uint64_t w0 = (uint64_t)s * SL_WORDS;
+    const uint32_t nw4 = (uint32_t)((nwords - w0 < SL_WORDS ? nwords - w0 : SL_WORDS) / 4);
+    uint4* g4 = reinterpret_cast<uint4*>(bits + w0);
+    uint4* l4 = reinterpret_cast<uint4*>(sl);
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) l4[q] = g4[q];
+    __syncthreads();
+    const uint32_t c = s >> f2, f = s & ((1u << f2) - 1);
+    const uint16_t* ra = ht + (uint64_t)f * row_stride;
+    const uint16_t* rb = ra + row_stride;
+    for (uint32_t pr = 0; pr < P; ++pr) {
+      const uint64_t ta = tile_off[(uint64_t)c * P + pr], te = ta + used[(uint64_t)c * P + pr];
+      uint32_t nlen = 0;
+      uint64_t npos = 0;
+      auto hload = [&](uint64_t gg) {
+        const uint64_t t = gg + lane;
+        nlen = 0;
+        npos = 0;
+        if (t < te) {
+          const uint32_t beg = ra[t];
+          nlen = (uint32_t)rb[t] - beg;  // a multiple of 4
+          npos = tb[t] + beg;            // a multiple of 4
+        }
+      };
+      hload(ta + 64ull * w);
+      for (uint64_t g = ta + 64ull * w; g < te; g += 64ull * NW) {
+        const uint32_t len = nlen;
+        const uint64_t pos = npos;
+        hload(g + 64ull * NW);
+        const uint32_t ng = (uint32_t)(te - g < 64 ? te - g : 64);
+        for (uint32_t j = 0; j < ng; j += UA) {
+          uint4 v[UA / 2];
+#pragma unroll
+          for (int q = 0; q < UA / 2; ++q) {
+            const uint32_t ja = j + 2 * q, jb = ja + 1;
+            const uint32_t la = ja < ng ? rdl(len, ja < 63 ? ja : 63) : 0;
+            const uint32_t lb = jb < ng ? rdl(len, jb < 63 ? jb : 63) : 0;
+            const uint64_t pa = rdl64(pos, ja < 63 ? ja : 63), pb = rdl64(pos, jb < 63 ? jb : 63);
+            const uint32_t my4 = (half ? lb : la) / 4;
+            const uint64_t mp4 = (half ? pb : pa) / 4;
+            v[q] = l32 < my4 ? ld_nt16(p4 + mp4 + l32) : make_uint4(INVALID, INVALID, INVALID, INVALID);
+            for (uint32_t o = l32 + 32; o < my4; o += 32) {  // segments longer than 128 probes (rare)
+              const uint4 x = p4[mp4 + o];
+              if (x.x != INVALID) atomicOr(&sl[x.x >> 5], bloom_bit_mask(x.x));
+              if (x.y != INVALID) atomicOr(&sl[x.y >> 5], bloom_bit_mask(x.y));
+              if (x.z != INVALID) atomicOr(&sl[x.z >> 5], bloom_bit_mask(x.z));
+              if (x.w != INVALID) atomicOr(&sl[x.w >> 5], bloom_bit_mask(x.w));
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < UA / 2; ++q) {
+            if (v[q].x != INVALID) atomicOr(&sl[v[q].x >> 5], bloom_bit_mask(v[q].x));
+            if (v[q].y != INVALID) atomicOr(&sl[v[q].y >> 5], bloom_bit_mask(v[q].y));
+            if (v[q].z != INVALID) atomicOr(&sl[v[q].z >> 5], bloom_bit_mask(v[q].z));
+            if (v[q].w != INVALID) atomicOr(&sl[v[q].w >> 5], bloom_bit_mask(v[q].w));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) g4[q] = l4[q];
+    __syncthreads();
+  }
 }
 
 int st_mode() {
@@ -848,10 +973,9 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   const uint64_t region_probes = (uint64_t)W * nb1 * quota;
   if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;  // u32 offsets -> exact-offset pipeline
   const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / SA2_SLOTS + (uint64_t)W * nb1 + 64;  // bound on sa2 tiles
+  const uint64_t l2_probes = max_np + 3ull * nb1 * max_nst + tt_max * SA2_PAD + 4ull * ncp;  // sa2 output, padded
   const uint64_t h2_bytes = al(tt_max * (nb2 + 1) * 2);
   const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256;
-  // sa2 places (c, p) at reg_off = prefix of its streamed probes, run padding included
-  const uint64_t l2_probes = max_np + 3ull * nb1 * max_nst;
   const uint64_t bytes = al(4 * region_probes) + al(4 * l2_probes) + 2 * h2_bytes + al(8 * tt_max) + meta;
   uint8_t* w = c->work(bytes);
   uint8_t* q = w;
@@ -926,9 +1050,9 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     {
       ProfScope ps(c, "bloom_st_apply");
 #define RSK_APPLY(U)                                                                                          \
-  launch_persistent((const void*)bloom_st_apply_kernel<U>, TA, ns, c, [&](uint32_t grid) {                  \
-    hipLaunchKernelGGL((bloom_st_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2,  \
-                       tb2, (uint64_t)0, (uint64_t)0, tile_off, tiles, P, ns, b->d_bits, b->nwords);        \
+  launch_persistent((const void*)bloom_sa_apply_kernel<U>, TA, ns, c, [&](uint32_t grid) {                  \
+    hipLaunchKernelGGL((bloom_sa_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2,  \
+                       tb2, tile_off, tiles, P, ns, b->d_bits, b->nwords);                                 \
   })
       if (ua == 8) RSK_APPLY(8);
       else RSK_APPLY(4);
