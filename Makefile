@@ -6,7 +6,7 @@ ARCH ?= gfx950
 # x86-64 gcc -O2 has none); integer paths are unaffected.
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-result
 SRC := $(wildcard redisson_amd/csrc/*.hip)
-HDR := $(wildcard redisson_amd/csrc/*.h) include/rsketch.h
+HDR := $(wildcard redisson_amd/csrc/*.h) $(wildcard include/*.h)
 OBJ := $(patsubst redisson_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := redisson_amd/librsketch.so
 

@@ -296,44 +296,6 @@ int rsk_plan_bloom_slice_words(uint64_t nwords, int nranks, uint64_t *words);
 int rsk_plan_fetch(uint64_t n, int nranks, int rank, const uint64_t *ids, uint64_t n_ids, uint32_t flags,
                    uint64_t *want_out, uint64_t *n_want, uint64_t *counts_out);
 
-/* --------------------------------------------------------- diagnostics */
-/* Memory-system microbenchmark on a device buffer (roofline denominators):
- * mode 0 stream read, 1 random 4 B gathers, 2 random 4 B atomicOr,
- * 3 stream copy (buffer halves).  *ms = device time of the one launch. */
-int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
-/* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */
-int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint64_t n, double *ms);
-/* Time one launch of a variant of the blob+offsets PFADD kernel (slabs only):
- * 0 production (step-count sort, 1 key per lane), 1 sorted with 2 keys per lane,
- * 2 round-1 form (no prefetch, no sort), 3 sorted with 4 keys per lane. */
-int rsk_diag_hll_var_variant(rsk_ctx *ctx, int variant, const void *dev_data, const uint64_t *dev_offsets, uint64_t n,
-                             double *ms);
-/* Time one launch of a tuning variant of the 16-byte Bloom contains kernel. */
-int rsk_diag_bloom_contains_variant(rsk_ctx *ctx, int variant, rsk_bloom *b, const void *dev_keys16, uint64_t n,
-                                    uint8_t *dev_out, double *ms);
-/* Run the production 16-byte contains kernel's gather sequence with a tally:
- * replies into dev_out, *probes = bit gathers issued (early exit included). */
-int rsk_diag_bloom_contains_probes(rsk_ctx *ctx, rsk_bloom *b, const void *dev_keys16, uint64_t n, uint8_t *dev_out,
-                                   uint64_t *probes);
-
-/* ----------------------------------------------- synthetic input streams */
-/* SURVEY 8d generators, run on the device into caller-provided device
- * buffers (bench and parity tests; outside the timed region). */
-int rsk_gen_keys16(rsk_ctx *ctx, uint64_t seed, uint64_t start, uint64_t n, void *dev_out);
-int rsk_gen_grouped(rsk_ctx *ctx, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t *dev_groups,
-                    void *dev_keys);
-/* C5 Zipf(s) stress variant: group = Zipf(s) rank over [0, G) (rank 1 -> group 0)
- * drawn from splitmix64(seed + 3i) >> 1 against a u63 cumulative-weight table;
- * keys as rsk_gen_grouped (oracle: orc_gen_grouped_zipf). */
-int rsk_gen_grouped_zipf(rsk_ctx *ctx, uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n,
-                         uint32_t *dev_groups, void *dev_keys);
-int rsk_gen_queries16(rsk_ctx *ctx, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
-                      void *dev_out);
-/* Variable-length keys: lengths first (dev_offsets gets n+1 offsets), then
- * bytes into dev_blob (capacity blob_cap). */
-int rsk_gen_varlen(rsk_ctx *ctx, uint64_t seed, uint64_t start, uint64_t n, uint64_t *dev_offsets, void *dev_blob,
-                   uint64_t blob_cap, uint64_t *total_bytes);
-
 #ifdef __cplusplus
 }
 #endif

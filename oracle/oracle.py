@@ -337,7 +337,7 @@ class _HLLKey:
                 self.dense = True
             else:
                 sp = hll_encode_sparse(self.regs)
-                if sp is None or len(sp) - 16 > SPARSE_MAX_BYTES:
+                if sp is None or len(sp) > SPARSE_MAX_BYTES:  # sdslen (header included), hllSparseSet
                     self.dense = True
 
     def to_string(self) -> bytes:

@@ -340,6 +340,41 @@ void invalidate(rsk_hll* h, uint64_t id, const uint32_t* d_flag, bool force) {
   RSK_CHECK_LAUNCH("invalidate");
 }
 
+// Redis sparse HLL payload (hyperloglog.c: ZERO 00xxxxxx run 1..64, XZERO
+// 01xxxxxx yyyyyyyy run 1..16384, VAL 1vvvvvxx value 1..32 run 1..4), the
+// canonical form: maximal runs, each cut into the longest opcodes.  Returns
+// the payload length, 0 if a register exceeds 32 or cap is too small.
+constexpr size_t HLL_SPARSE_MAX_BYTES = 3000;  // server.hll_sparse_max_bytes (whole string)
+size_t encode_sparse(const uint8_t* raw, uint8_t* out, size_t cap) {
+  size_t o = 0;
+  for (int j = 0; j < HLL_REGS;) {
+    const uint8_t v = raw[j];
+    int run = 1;
+    while (j + run < HLL_REGS && raw[j + run] == v) ++run;
+    j += run;
+    if (v > 32) return 0;
+    while (run > 0) {
+      if (v == 0 && run > 64) {
+        const int l = run < 16384 ? run : 16384;
+        if (o + 2 > cap) return 0;
+        out[o++] = (uint8_t)(0x40 | ((l - 1) >> 8));
+        out[o++] = (uint8_t)((l - 1) & 0xff);
+        run -= l;
+      } else if (v == 0) {
+        if (o + 1 > cap) return 0;
+        out[o++] = (uint8_t)(run - 1);
+        run = 0;
+      } else {
+        const int l = run < 4 ? run : 4;
+        if (o + 1 > cap) return 0;
+        out[o++] = (uint8_t)(0x80 | ((v - 1) << 2) | (l - 1));
+        run -= l;
+      }
+    }
+  }
+  return o;
+}
+
 // ------------------------------------------------ Java double semantics
 int64_t java_d2l(double d) {
   if (std::isnan(d)) return 0;
@@ -542,6 +577,7 @@ int rsk_hll_create(rsk_ctx* c, uint64_t n, rsk_hll** out) {
     h->ctx = c;
     h->n = n;
     h->exists.assign(n, 0);
+    h->dense.assign(n, 0);
     RSK_HIP(hipMalloc(&h->d_regs, n * (uint64_t)HLL_REGS));
     RSK_HIP(hipMalloc(&h->d_card, n * 8));
     RSK_HIP(hipMalloc(&h->d_pcount, n * 8));
@@ -586,6 +622,7 @@ int rsk_hll_delete(rsk_hll* h, uint64_t id) {
     RSK_HIP(hipMemsetAsync(regs_of(h, id), 0, HLL_REGS, h->ctx->stream));
     RSK_HIP(hipMemsetAsync(h->d_card + id, 0, 8, h->ctx->stream));
     h->exists[id] = 0;
+    h->dense[id] = 0;
   });
 }
 
@@ -599,6 +636,7 @@ int rsk_hll_clear(rsk_hll* h) {
       RSK_HIP(hipMemsetAsync(h->d_card, 0, h->n * 8, h->ctx->stream));
     }
     std::fill(h->exists.begin(), h->exists.end(), 0);
+    std::fill(h->dense.begin(), h->dense.end(), 0);
     h->pending_clear = true;
     h->zero = true;
   });
@@ -825,6 +863,7 @@ int rsk_hll_merge(rsk_hll* dst, uint64_t dst_id, rsk_hll* const* srcs, const uin
     }
     bool created;
     create_if_missing(dst, dst_id, &created);
+    dst->dense[dst_id] = 1;  // pfmergeCommand converts the destination to dense
     if (k) {
       uint8_t* s = out_scratch(c, 8 + k * 8 + 512);
       auto* d_dst = reinterpret_cast<uint8_t**>(s);
@@ -852,6 +891,7 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
       check_hll(h, src_ids[i]);
       sp[i] = h->exists[src_ids[i]] ? regs_of(h, src_ids[i]) : nullptr;
       h->exists[dst_ids[i]] = 1;
+      h->dense[dst_ids[i]] = 1;
       dp[i] = regs_of(h, dst_ids[i]);
     }
     // PFMERGEs run in input order in Redis; a batch whose destinations are
@@ -931,6 +971,7 @@ int rsk_hll_merge_raw(rsk_hll* h, uint64_t id, const uint8_t* regs, uint32_t loc
     CtxLock l(c);
     bool created;
     create_if_missing(h, id, &created);
+    h->dense[id] = 1;
     const uint8_t* src = regs;
     if (location == RSK_MEM_HOST) {
       uint8_t* s = out_scratch(c, HLL_REGS);
@@ -984,8 +1025,18 @@ int rsk_hll_export_redis(rsk_hll* h, uint64_t id, uint8_t* buf, size_t cap, size
     RSK_HIP(hipStreamSynchronize(h->ctx->stream));
     std::memset(buf, 0, RSK_HLL_DENSE_BYTES);
     std::memcpy(buf, "HYLL", 4);
-    buf[4] = 0;  // HLL_DENSE
     for (int b = 0; b < 8; ++b) buf[8 + b] = (uint8_t)(card >> (8 * b));
+    if (!h->dense[id]) {
+      const size_t n = encode_sparse(raw.data(), buf + 16, RSK_HLL_DENSE_BYTES - 16);
+      if (n && 16 + n <= HLL_SPARSE_MAX_BYTES) {
+        buf[4] = 1;  // HLL_SPARSE
+        *len = 16 + n;
+        return;
+      }
+      h->dense[id] = 1;  // promoted (hllSparseSet -> hllSparseToDense), for good
+      std::memset(buf + 16, 0, RSK_HLL_DENSE_BYTES - 16);
+    }
+    buf[4] = 0;  // HLL_DENSE
     uint8_t* p = buf + 16;
     for (int j = 0; j < HLL_REGS; ++j) {  // HLL_DENSE_SET_REGISTER, 6 bits LSB-first
       uint32_t bitpos = (uint32_t)j * 6, byte = bitpos >> 3, fb = bitpos & 7;
@@ -1052,6 +1103,7 @@ int rsk_hll_import_redis(rsk_hll* h, uint64_t id, const uint8_t* buf, size_t len
     RSK_HIP(hipMemcpyAsync(h->d_card + id, &card, 8, hipMemcpyHostToDevice, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
     h->exists[id] = 1;
+    h->dense[id] = buf[4] == 0;
   });
 }
 

@@ -201,6 +201,7 @@ int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
     hipLaunchKernelGGL(invalidate_card_kernel, dim3(1), dim3(64), 0, c->stream, h->d_card + id, (uint64_t)1);
     RSK_CHECK_LAUNCH("invalidate");
     h->exists[id] = 1;
+    h->dense[id] = 1;
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }
@@ -221,6 +222,7 @@ int rsk_hll_allreduce_pool(rsk_hll* h) {
     hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
     RSK_CHECK_LAUNCH("invalidate");
     std::fill(h->exists.begin(), h->exists.end(), 1);
+    std::fill(h->dense.begin(), h->dense.end(), 1);
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }
@@ -246,6 +248,7 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
     hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
     RSK_CHECK_LAUNCH("invalidate");
     std::fill(h->exists.begin(), h->exists.end(), 1);
+    std::fill(h->dense.begin(), h->dense.end(), 1);
     rsk::plan_owned_range(h->n, N, r, first_out, count_out);
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
@@ -336,7 +339,7 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
                          c->stream, reinterpret_cast<uint4*>(h->d_regs), h->d_card, d_want, n_out,
                          reinterpret_cast<const uint4*>(rows_recv));
       RSK_CHECK_LAUNCH("scatter_rows");
-      for (uint64_t id : want) h->exists[id] = 1;
+      for (uint64_t id : want) h->exists[id] = h->dense[id] = 1;
     }
     RSK_HIP(hipStreamSynchronize(c->stream));
   });

@@ -251,7 +251,9 @@ static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per
 // equal lengths.  KPL = 1 in production (measured: KPL 2 and 4 interleave
 // independent chains but lose more to registers and selects than they win,
 // scripts/var_variants.py).  A tile whose bytes exceed the stage is hashed
-// from global memory, unsorted.
+// from global memory, unsorted.  The tile's barriers order LDS only
+// (lds_barrier): __syncthreads' fence would wait for the next tile's stage
+// loads at the first barrier after they are issued, undoing the prefetch.
 constexpr int VAR_TILE = 512;                   // keys per tile
 constexpr int VAR_STAGE = 32768;                // bytes per tile (64 B per key)
 constexpr uint32_t VAR_MAXCLS = 16;             // step classes 0..16 (16 = that long or longer)
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
   }
 
   for (uint64_t base = begin; base < end;) {
-    __syncthreads();  // [A] previous tile's stage / perm / cbase reads are done
+    lds_barrier();  // [A] previous tile's stage / perm / cbase reads are done
     uint4* st16 = reinterpret_cast<uint4*>(stage);
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
       cur_hi = hi_ahead;
       fetch(next, lo_n, cur_hi);
     }
-    __syncthreads();  // [B] stage written, class counts final
+    lds_barrier();  // [B] stage written, class counts final
     if (cur_staged) {
       if (tid < 64) {  // class starts: wave 0's exclusive prefix over the counts (one LDS read per lane)
         const uint32_t v = tid < VAR_NCLS_PAD ? cnt[tid] : 0;
@@ -413,11 +415,11 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
         }
         if (tid < VAR_NCLS_PAD) cbase[tid] = x - v;
       }
-      __syncthreads();  // [C]
+      lds_barrier();  // [C]
 #pragma unroll
       for (int q = 0; q < KPL; ++q)
         if (cls[q] != VAR_NONE) perm[cbase[cls[q]] + rk[q]] = coff[q] | ((uint32_t)clen[q] << 16);
-      __syncthreads();  // [D]
+      lds_barrier();  // [D]
       if (tid < VAR_NCLS_PAD) cnt[tid] = 0;
       const uint32_t nvalid = cbase[VAR_NONE];
       uint32_t o[KPL], l[KPL];

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/rsketch.h"
+#include "../../include/rsketch_diag.h"
 #include "rsk_device.h"
 
 namespace rsk {
@@ -104,6 +105,12 @@ struct rsk_hll {
   uint8_t* d_regs = nullptr;   // [n][16384] raw registers (one byte each)
   uint64_t* d_card = nullptr;  // [n] Redis card[8] as LE u64 (bit 63 = cache invalid)
   std::vector<uint8_t> exists; // host: key present
+  // host: the key's Redis encoding is dense (HLL_DENSE).  Keys start sparse
+  // (createHLLObject); PFMERGE destinations, merged / fetched / all-reduced
+  // rows and SET of a dense string are dense; a sparse key is promoted for
+  // good once its registers no longer fit the sparse limits (value > 32 or
+  // more than hll-sparse-max-bytes = 3000 bytes), checked when it is read out.
+  std::vector<uint8_t> dense;
   // Every register is known to be 0 (set by create/clear, dropped by every
   // entry point that may write registers): the grouped add then skips
   // reading the pool.

@@ -1,4 +1,4 @@
-"""The C ABI library loads and exports every symbol include/rsketch.h declares;
+"""The C ABI library loads and exports every symbol include/*.h declares;
 host-only entry points agree with the oracle (CPU only, no kernel launches)."""
 import ctypes
 import os
@@ -9,6 +9,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "rsketch.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("rsketch.h", "rsketch_diag.h")]
 LIB = os.path.join(ROOT, "redisson_amd", "librsketch.so")
 
 
@@ -22,7 +23,7 @@ def lib():
 
 
 def declared_functions():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(rsk_[a-z0-9_]+)\s*\(", text)))
 

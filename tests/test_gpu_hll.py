@@ -695,3 +695,61 @@ def test_grouped_add_precomputed_counts_follow_later_writes(L, engine, orc, monk
     for x in (g, k, g2, k2):
         x.free()
     L.rsk_hll_destroy(h)
+
+
+def _export(L, h, i):
+    from redisson_amd import _lib
+
+    buf = (ctypes.c_uint8 * 12304)()
+    n = ctypes.c_size_t()
+    _lib.check(L.rsk_hll_export_redis(h, i, buf, 12304, ctypes.byref(n)))
+    return bytes(buf[: n.value])
+
+
+def test_export_follows_redis_encoding(L, engine, orc):
+    """GET of a key as Redis 3.2.0 would hold it: sparse while the registers fit
+    (values <= 32, <= 3000 bytes with the header), dense once promoted (for
+    good), after PFMERGE (destination converted) and after SET of a dense
+    string; byte-identical to the Redis model's canonical sparse form."""
+    from redisson_amd import KeyBatch, _lib
+
+    r = orc.RedisModel()
+    h = _pool(L, engine, 4)
+    keys = orc.gen_keys16(SEED_C2, 0, 4000).reshape(-1, 16)
+    empty = np.zeros((0, 16), np.uint8)
+    _add(L, h, KeyBatch.from_numpy(empty), 0)  # PFADD k (no elements): created, sparse XZERO
+    r.pfadd("k")
+    assert _export(L, h, 0) == r.get("k") and _export(L, h, 0)[4] == 1
+    done = 0
+    for upto in (1, 10, 100, 300, 600, 1200, 4000):
+        batch = keys[done:upto]
+        _add(L, h, KeyBatch.from_numpy(batch), 0)
+        r.pfadd("k", *[bytes(x) for x in batch])
+        done = upto
+        s = _export(L, h, 0)
+        assert s == r.get("k"), upto
+        if upto in (100, 300):
+            assert int(_count(L, h, [0])[0]) == r.pfcount("k")  # card cache refreshed, then read back out
+            assert _export(L, h, 0) == r.get("k")
+    assert _export(L, h, 0)[4] == 0  # 4000 keys: promoted to dense
+    # PFMERGE destination: dense even when small
+    _add(L, h, KeyBatch.from_numpy(keys[:5]), 1)
+    r.pfadd("a", *[bytes(x) for x in keys[:5]])
+    pools = (ctypes.c_void_p * 1)(h.value)
+    src = (ctypes.c_uint64 * 1)(1)
+    _lib.check(L.rsk_hll_merge(h, 2, pools, src, 1))
+    r.pfmerge("m", "a")
+    assert _export(L, h, 2) == r.get("m") and _export(L, h, 2)[4] == 0
+    # SET of a sparse string keeps it sparse; of a dense one, dense
+    sp = r.get("a")
+    b = (ctypes.c_uint8 * len(sp)).from_buffer_copy(sp)
+    _lib.check(L.rsk_hll_import_redis(h, 3, b, len(sp)))
+    assert _export(L, h, 3) == sp
+    dn = r.get("m")
+    b = (ctypes.c_uint8 * len(dn)).from_buffer_copy(dn)
+    _lib.check(L.rsk_hll_import_redis(h, 3, b, len(dn)))
+    assert _export(L, h, 3)[4] == 0
+    _lib.check(L.rsk_hll_delete(h, 3))  # DEL: a new key starts sparse again
+    _add(L, h, KeyBatch.from_numpy(keys[:3]), 3)
+    assert _export(L, h, 3)[4] == 1
+    L.rsk_hll_destroy(h)
