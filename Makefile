@@ -16,8 +16,13 @@ build/%.o: redisson_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# -z now: every HIP/RCCL symbol is bound when the library loads.  Lazily bound
+# calls made after `import torch` (which brings its own libamdhip64 into the
+# global symbol scope) would otherwise resolve to torch's HIP runtime, which
+# does not know these kernels (hipOccupancyMaxActiveBlocksPerMultiprocessor
+# answered 1 there: persistent grids a third of their size).
 $(LIB): $(OBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-z,now
 
 oracle:
 	$(MAKE) -s -C oracle

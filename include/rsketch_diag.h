@@ -17,6 +17,9 @@ extern "C" {
  * mode 0 stream read, 1 random 4 B gathers, 2 random 4 B atomicOr,
  * 3 stream copy (buffer halves).  *ms = device time of the one launch. */
 int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
+/* hipOccupancyMaxActiveBlocksPerMultiprocessor for a persistent Bloom kernel
+ * (which 0: sa1, 1: append apply): workgroups per CU and the HIP error code. */
+int rsk_diag_occupancy(int which, int *per_cu, int *hip_error);
 /* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */
 int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint64_t n, double *ms);
 /* Time one launch of a variant of the blob+offsets PFADD kernel (slabs only):

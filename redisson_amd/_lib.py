@@ -162,6 +162,7 @@ SIGNATURES = {
     "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
     "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
     "rsk_gen_grouped_zipf": (ctypes.c_int, [_vp, _u64, _u64, ctypes.c_double, _u64, _u64, _vp, _vp]),
+    "rsk_diag_occupancy": (ctypes.c_int, [ctypes.c_int, _vp, _vp]),
     "rsk_gen_queries16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
     "rsk_gen_varlen": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp, _vp, _u64, _P(_u64)]),
 }
@@ -180,6 +181,15 @@ def load():
                     "librsketch.so not found at %s: build it with `make` (or __graft_entry__.build()). "
                     "redisson_amd has no CPU fallback." % LIB_PATH)
             L = ctypes.CDLL(LIB_PATH)
+            # The HIP runtime dlopens libamd_comgr.so.3 by soname the first time it
+            # reads a code object's metadata (occupancy queries, hipcub grid
+            # sizing).  torch ships its own copy of that soname: imported first, it
+            # would satisfy that dlopen and the system runtime would misread our
+            # kernels (hipOccupancyMaxActiveBlocksPerMultiprocessor answered 1,
+            # scripts/occ_probe.py).  Binding the system copy now wins the soname.
+            comgr = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamd_comgr.so.3")
+            if os.path.exists(comgr):
+                ctypes.CDLL(comgr, mode=ctypes.RTLD_GLOBAL)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)
                 fn.restype = res

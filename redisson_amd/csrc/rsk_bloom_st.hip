@@ -817,7 +817,7 @@ __global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const uint32_t* __rest
 // half-wave loads one segment as up to 32 uint4 (128 probes) in one
 // instruction: UA segments per wave take UA/2 16-byte loads per lane.
 template <int UA>
-__global__ __launch_bounds__(TA) void bloom_sa_apply_kernel(const uint32_t* __restrict__ probes,
+__global__ __launch_bounds__(TA, 8) void bloom_sa_apply_kernel(const uint32_t* __restrict__ probes,
                                                             const uint16_t* __restrict__ ht, uint64_t row_stride,
                                                             uint32_t f2, const uint64_t* __restrict__ tb,
                                                             const uint32_t* __restrict__ tile_off,
@@ -955,11 +955,14 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
                                                   : (const void*)bloom_sa1_kernel<true, 16, 512>)
                                      : (kmax == 8 ? (const void*)bloom_sa1_kernel<false, 8, 512>
                                                   : (const void*)bloom_sa1_kernel<false, 16, 512>));
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k1, (int)t1, 0) != hipSuccess || per_cu < 1) {
-    (void)hipGetLastError();
-    per_cu = 1;
-  }
+  // Workgroups per CU from the kernels' own budgets, not from
+  // hipOccupancyMaxActiveBlocksPerMultiprocessor: in a process that has
+  // imported torch the runtime reads these code objects' metadata through
+  // torch's comgr and answers 1 (scripts/occ_probe.py), a third of the grid.
+  // sa1<512>: __launch_bounds__(512, 6) caps it at 80 VGPRs (6 waves per
+  // SIMD), 43 KiB of LDS -> 3; sa1<1024>: 78 KiB of LDS, 4 waves per SIMD -> 1.
+  (void)k1;
+  const int per_cu = t1 == 512 ? 3 : 1;
   // W persistent sa1 workgroups; each gets 1.25x its expected share of a full
   // coarse bin per bin, plus one whole super-tile (a tile's run can be that
   // long) and the <= 3 padding slots per run of each of its tiles.
@@ -1049,11 +1052,11 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     }
     {
       ProfScope ps(c, "bloom_st_apply");
+      // __launch_bounds__(TA, 8): <= 64 VGPRs, 64 KiB of LDS -> 2 workgroups per CU
+      const uint32_t ga = std::min<uint32_t>(ns, 2 * cus);
 #define RSK_APPLY(U)                                                                                          \
-  launch_persistent((const void*)bloom_sa_apply_kernel<U>, TA, ns, c, [&](uint32_t grid) {                  \
-    hipLaunchKernelGGL((bloom_sa_apply_kernel<U>), dim3(grid), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2,  \
-                       tb2, tile_off, tiles, P, ns, b->d_bits, b->nwords);                                 \
-  })
+  hipLaunchKernelGGL((bloom_sa_apply_kernel<U>), dim3(ga), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2, tb2,   \
+                     tile_off, tiles, P, ns, b->d_bits, b->nwords)
       if (ua == 8) RSK_APPLY(8);
       else RSK_APPLY(4);
 #undef RSK_APPLY
@@ -1074,6 +1077,17 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
 }
 
 }  // namespace
+
+// Occupancy of the two persistent Bloom kernels as this process sees it
+// (diagnostic: the grids are sized from it).
+int bloom_occupancy_probe(int which, int* per_cu) {
+  const void* k = which == 0 ? (const void*)bloom_sa1_kernel<true, 8, 512> : (const void*)bloom_sa_apply_kernel<8>;
+  const int threads = which == 0 ? 512 : TA;
+  *per_cu = -1;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k, threads, 0);
+  if (e != hipSuccess) (void)hipGetLastError();
+  return (int)e;
+}
 
 bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const int mode = st_mode();

@@ -97,6 +97,16 @@ extern "C" int rsk_diag_bloom_contains_variant(rsk_ctx* c, int variant, rsk_bloo
   }
 }
 
+namespace rsk {
+int bloom_occupancy_probe(int which, int* per_cu);
+}
+// Occupancy query result (hipError, per-CU workgroups) for the persistent
+// Bloom kernels: which 0 = sa1 (512 lanes), 1 = the append apply.
+extern "C" int rsk_diag_occupancy(int which, int* per_cu, int* hip_error) {
+  *hip_error = rsk::bloom_occupancy_probe(which, per_cu);
+  return RSK_OK;
+}
+
 extern "C" int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t nops, double* ms) {
   try {
     if (!c || !buf || !ms || bytes < 64 || mode < 0 || mode > 3) throw rsk::RskError{RSK_ERR_INVALID_ARG, "bad arguments"};

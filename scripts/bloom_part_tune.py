@@ -15,6 +15,10 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
+if os.environ.get("RSK_TUNE_TORCH"):  # A/B: the bench process also imports torch
+    _lib.load()
+    import torch  # noqa: F401
+
 STAGES = ("bloom_part_hist", "bloom_part1", "bloom_part2", "bloom_slice_apply", "bloom_st1", "bloom_st_mid",
           "bloom_st2", "bloom_st_apply", "bloom_add16")
 
@@ -29,6 +33,9 @@ def main():
     k = ctypes.c_int32()
     _lib.check(L.rsk_bloom_params(n, 0.01, _lib.RSK_BLOOM_EXTENDED, ctypes.byref(size), ctypes.byref(k)))
     ins = devmem.gen_keys16(eng, 0x5EED0003, 0, n)
+    extra = []
+    if os.environ.get("RSK_TUNE_QBUF"):  # A/B: the bench also holds the 1B query keys
+        extra.append(devmem.gen_keys16(eng, 0x5EED0004, 0, n))
     ks = ins.keys_fixed(n, 16).as_struct()
     res = {"n": n, "size": size.value, "k": k.value, "configs": {}}
     for cfg in configs:
