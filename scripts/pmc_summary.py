@@ -96,18 +96,27 @@ def main():
             "stages": list(parts),
             "hbm_bytes_note": "raw FETCH_SIZE + WRITE_SIZE of the stages per call (16 B key stream, 4 B records, "
                               "16 KiB sketch rows; not corrected)"}
-    st = ("bloom_st1_kernel", "st_transpose_kernel", "st_size_kernel", "st_offsets_kernel", "bloom_st2_kernel",
-          "bloom_st_apply_kernel")
-    if all(p in fe and p in wr for p in ("bloom_st1_kernel", "bloom_st2_kernel", "bloom_st_apply_kernel")):
-        # the super-tile Bloom insert (one chunk per insert at 1B keys, k = 7): per stage and summed.
-        # st1's key stream is a 16 B/lane read (FETCH doubled per the guide); the 4 B probe-tag
-        # reads of st2/apply are uncalibrated widths, reported raw.
-        stages = {p: {"fetch_kib_raw": fe.get(p, 0.0), "write_kib": wr.get(p, 0.0)} for p in st if p in fe}
-        tot = sum((fe.get(p, 0.0) + wr.get(p, 0.0)) * 1024 for p in st)
-        kern["bloom_insert_supertile"] = {
-            "stages": stages, "hbm_bytes_per_insert_raw": tot,
-            "hbm_bytes_per_launch": tot + fe["bloom_st1_kernel"] * 1024,
-            "note": "per insert call = one dispatch of each stage"}
+    # The Bloom insert at 1B keys, k = 7 (one chunk: one dispatch of each stage per insert call),
+    # per stage and summed.  Append pipeline (default): sa1 reads the keys, sa2 its sub-regions and
+    # apply its tiles with 16 B/lane loads, so FETCH is doubled per the guide; the header pipeline
+    # (st1/st2/st_apply, RSK_BLOOM_SA=0) reads probe tags with 4 B loads (uncalibrated: raw).
+    for name, st, wide in (("bloom_insert_supertile",
+                            ("bloom_sa1_kernel", "sa_size_kernel", "st_offsets_kernel", "bloom_sa2_kernel",
+                             "st_transpose_kernel", "bloom_sa_apply_kernel"),
+                            ("bloom_sa1_kernel", "bloom_sa2_kernel", "bloom_sa_apply_kernel")),
+                           ("bloom_insert_header_pipeline",
+                            ("bloom_st1_kernel", "st_transpose_kernel", "st_size_kernel", "st_offsets_kernel",
+                             "bloom_st2_kernel", "bloom_st_apply_kernel"), ("bloom_st1_kernel",))):
+        main = [x for x in st if x.startswith("bloom_")]
+        if not all(x in fe and x in wr for x in main):
+            continue
+        stages = {x: {"fetch_kib_raw": fe.get(x, 0.0), "write_kib": wr.get(x, 0.0),
+                      "avg_ns": kern.get(x, {}).get("avg_ns")} for x in st if x in fe}
+        raw = sum((fe.get(x, 0.0) + wr.get(x, 0.0)) * 1024 for x in st)
+        kern[name] = {"stages": stages, "hbm_bytes_per_insert_raw": raw,
+                      "hbm_bytes_per_launch": raw + sum(fe[x] * 1024 for x in wide if x in fe),
+                      "wide_read_stages_doubled": list(wide),
+                      "note": "per insert call = one dispatch of each stage"}
     doc = {"config": config, "sources": {"stats": sp, "fetch": fp, "write": wp}, "kernels": kern,
            "note": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch (mean over dispatches); fetch doubled for "
                    "hll_add16_kernel per MI355X_MICROARCH.md HBM section"}
