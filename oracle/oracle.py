@@ -86,6 +86,9 @@ def lib():
                                                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                                                     ctypes.c_int]),
+            "orc_bloom_add_replies_sample_gen16_mt": (None, [ctypes.c_int64, ctypes.c_int, ctypes.c_uint64,
+                                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                                             ctypes.c_void_p, ctypes.c_int]),
             "orc_setbit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]),
             "orc_getbit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
             "orc_bitcount": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -566,6 +569,16 @@ def bloom_contains_gen_queries_mt(bits: np.ndarray, size: int, k: int, qseed: in
                                   start: int, n: int, out: np.ndarray | None, nthreads: int) -> int:
     return int(lib().orc_bloom_contains_gen_queries_mt(_ptr(bits), size, k, qseed, iseed, n_ins, start, n,
                                                        _ptr(out) if out is not None else None, nthreads))
+
+
+def bloom_add_replies_sample_gen16_mt(size: int, k: int, seed: int, n: int, sample: np.ndarray,
+                                      nthreads: int) -> np.ndarray:
+    """add() replies of keys `sample` (ascending) when C3 stream keys 0..n-1 are
+    added in one batch to an empty filter (rsk_oracle.c)."""
+    sample = np.ascontiguousarray(sample, dtype=np.uint64)
+    out = np.zeros(sample.size, np.uint8)
+    lib().orc_bloom_add_replies_sample_gen16_mt(size, k, seed, n, _ptr(sample), sample.size, _ptr(out), nthreads)
+    return out
 
 
 def hll_add_gen_grouped_subset(regs: np.ndarray, G: int, gsub: int, seed: int, start: int, n: int,

@@ -1062,6 +1062,78 @@ uint64_t orc_bloom_contains_gen_queries_mt(const uint8_t *bits, int64_t size, in
     return trues;
 }
 
+/* add() replies of sampled keys of the C3 insert stream (gen_keys16 keys
+ * 0..n-1 added in ONE batch to an empty filter), on nthreads cores.  Key i
+ * answers true iff one of its probes t < k-1 is the first SETBIT of its bit in
+ * sequence order p = i k + t (the bit was clear before the batch), so only the
+ * minimum p over the probes of the sample's bits is needed: those bits go in
+ * a hash table (min p, atomically lowered by every probe of the stream that
+ * hits one; a small bitmap screens the rest).  sample[] ascending, k <= 64. */
+void orc_bloom_add_replies_sample_gen16_mt(int64_t size, int k, uint64_t seed, uint64_t n, const uint64_t *sample,
+                                           uint64_t ns, uint8_t *out, int nthreads) {
+    if (k > 64 || k < 1) return;
+    const uint64_t EMPTY = ~0ull;
+    uint64_t want = 4 * ns * (uint64_t)(k > 1 ? k - 1 : 1) + 16, cap = 16;
+    int lg = 4;
+    while (cap < want) { cap <<= 1; lg++; }
+    uint64_t *tbit = (uint64_t *)malloc(cap * 8), *tmin = (uint64_t *)malloc(cap * 8);
+    const int SCR = 27;
+    uint64_t *scr = (uint64_t *)calloc((1ull << SCR) / 64, 8);
+    for (uint64_t e = 0; e < cap; e++) { tbit[e] = EMPTY; tmin[e] = EMPTY; }
+    int64_t *sidx = (int64_t *)malloc(ns * 64 * 8);
+    for (uint64_t j = 0; j < ns; j++) {
+        uint8_t key[16];
+        orc_gen_keys16(seed, sample[j], 1, key);
+        orc_bloom_indexes(key, 16, k, size, sidx + j * 64);
+        for (int t = 0; t < k - 1; t++) {
+            const uint64_t b = (uint64_t)sidx[j * 64 + t];
+            uint64_t e = (b * 0x9E3779B97F4A7C15ull) >> (64 - lg);
+            while (tbit[e] != EMPTY && tbit[e] != b) e = (e + 1) & (cap - 1);
+            tbit[e] = b;
+            const uint64_t h = (b * 0xD6E8FEB86659FD93ull) >> (64 - SCR);
+            scr[h >> 6] |= 1ull << (h & 63);
+        }
+    }
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+#endif
+    for (uint64_t i = 0; i < n; i++) {
+        uint8_t key[16];
+        uint64_t lo = orc_splitmix64(seed + 2 * i), hi = orc_splitmix64(seed + 2 * i + 1);
+        memcpy(key, &lo, 8);
+        memcpy(key + 8, &hi, 8);
+        int64_t idx[64];
+        orc_bloom_indexes(key, 16, k, size, idx);
+        for (int t = 0; t < k; t++) {
+            const uint64_t b = (uint64_t)idx[t];
+            const uint64_t h = (b * 0xD6E8FEB86659FD93ull) >> (64 - SCR);
+            if (!((scr[h >> 6] >> (h & 63)) & 1)) continue;
+            uint64_t e = (b * 0x9E3779B97F4A7C15ull) >> (64 - lg);
+            while (tbit[e] != EMPTY && tbit[e] != b) e = (e + 1) & (cap - 1);
+            if (tbit[e] != b) continue;
+            const uint64_t p = i * (uint64_t)k + (uint64_t)t;
+            uint64_t cur = __atomic_load_n(&tmin[e], __ATOMIC_RELAXED);
+            while (p < cur && !__atomic_compare_exchange_n(&tmin[e], &cur, p, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+            }
+        }
+    }
+    for (uint64_t j = 0; j < ns; j++) {
+        int r = 0;
+        for (int t = 0; t < k - 1 && !r; t++) {
+            const uint64_t b = (uint64_t)sidx[j * 64 + t];
+            uint64_t e = (b * 0x9E3779B97F4A7C15ull) >> (64 - lg);
+            while (tbit[e] != b) e = (e + 1) & (cap - 1);
+            r = tmin[e] == sample[j] * (uint64_t)k + (uint64_t)t;
+        }
+        out[j] = (uint8_t)r;
+    }
+    free(tbit);
+    free(tmin);
+    free(scr);
+    free(sidx);
+    (void)nthreads;
+}
+
 /* contains(), RedissonBloomFilter.java:133-168: AND over getbit_0..getbit_{k-2}. */
 void orc_bloom_contains_batch(const uint8_t *bits, int64_t size, int k, const uint8_t *data,
                               const uint64_t *offsets, uint32_t fixed_len, uint64_t n, uint8_t *out) {

@@ -89,6 +89,10 @@ void orc_bloom_add_gen16_mt(uint8_t *bits, int64_t size, int k, uint64_t seed, u
                             int nthreads);
 uint64_t orc_bloom_contains_gen_queries_mt(const uint8_t *bits, int64_t size, int k, uint64_t qseed, uint64_t iseed,
                                            uint64_t n_ins, uint64_t start, uint64_t n, uint8_t *out, int nthreads);
+/* add() replies of the sampled keys sample[0..ns) when keys 0..n-1 of the C3
+ * stream are added in one batch to an empty filter. */
+void orc_bloom_add_replies_sample_gen16_mt(int64_t size, int k, uint64_t seed, uint64_t n, const uint64_t *sample,
+                                           uint64_t ns, uint8_t *out, int nthreads);
 
 /* ---- Redis bitops (MSB-first string) -------------------------------- */
 int orc_setbit(uint8_t *bits, uint64_t off, int v);

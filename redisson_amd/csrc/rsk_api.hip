@@ -1186,28 +1186,14 @@ int rsk_bloom_add(rsk_bloom* b, const rsk_keys* keys, uint8_t* added_out) {
       for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { bloom_add_launch(c, b, dk); });
       return;
     }
-    // Replies need the ordered path; bound the probe count per sort.
-    const uint64_t max_keys = std::max<uint64_t>(1, (1ull << 28) / (uint64_t)b->k);
-    rsk_keys sub = *keys;
-    uint64_t done = 0;
-    while (done < keys->n) {
-      uint64_t m = std::min<uint64_t>(max_keys, keys->n - done);
-      sub.n = m;
-      if (keys->offsets) {
-        sub.offsets = keys->offsets + done;
-      } else {
-        sub.data = reinterpret_cast<const uint8_t*>(keys->data) + done * keys->fixed_len;
+    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+      uint8_t* d_out = keys->location == RSK_MEM_DEVICE ? added_out + first : out_scratch(c, cnt);
+      bloom_add_replies_launch(c, b, dk, d_out);
+      if (keys->location == RSK_MEM_HOST) {
+        RSK_HIP(hipMemcpyAsync(added_out + first, d_out, cnt, hipMemcpyDeviceToHost, c->stream));
+        RSK_HIP(hipStreamSynchronize(c->stream));
       }
-      for_each_chunk(c, &sub, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
-        uint8_t* d_out = keys->location == RSK_MEM_DEVICE ? added_out + done + first : out_scratch(c, cnt);
-        bloom_add_each_launch(c, b, dk, d_out);
-        if (keys->location == RSK_MEM_HOST) {
-          RSK_HIP(hipMemcpyAsync(added_out + done + first, d_out, cnt, hipMemcpyDeviceToHost, c->stream));
-          RSK_HIP(hipStreamSynchronize(c->stream));
-        }
-      });
-      done += m;
-    }
+    });
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }

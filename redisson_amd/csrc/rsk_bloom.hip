@@ -346,6 +346,25 @@ void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* 
   bloom_add_launch(c, b, k);
 }
 
+// The sort path bounded for its 32-bit sort: sub-batches of <= 2^28 probes,
+// each answered against the filter the previous ones left.
+void bloom_add_replies_sorted(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out) {
+  const uint64_t max_keys = std::max<uint64_t>(1, (1ull << 28) / (uint64_t)b->k);
+  for (uint64_t done = 0; done < k.n; done += max_keys) {
+    DevKeys sub = k;
+    sub.n = std::min<uint64_t>(max_keys, k.n - done);
+    if (k.offsets) sub.offsets = k.offsets + done;
+    else sub.data = k.data + done * k.fixed_len;
+    bloom_add_each_launch(c, b, sub, d_out + done);
+  }
+}
+
+void bloom_add_replies_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out) {
+  if (k.n == 0) return;
+  if (bloom_add_replies_append(c, b, k, d_out)) return;
+  bloom_add_replies_sorted(c, b, k, d_out);
+}
+
 // BITCOUNT over the filter words.
 __global__ __launch_bounds__(256) void popcount_kernel(const uint32_t* __restrict__ w, uint64_t nwords,
                                                        unsigned long long* __restrict__ out) {

@@ -1,0 +1,487 @@
+// rsk_bloom_sa.h -- the append partition's first two stages (gfx950), shared
+// by the Bloom insert (rsk_bloom_st.hip, 4-byte probe records) and the
+// add()-with-replies pipeline (rsk_bloom_reply.hip, 8-byte records that also
+// carry the probe's sequence number).  Everything lives in an anonymous
+// namespace: each translation unit instantiates its own kernels.  See
+// rsk_bloom_st.hip for the pipeline.
+#pragma once
+#include "rsk_internal.h"
+
+namespace rsk {
+namespace {
+constexpr int SL_LOG = 19;                             // bits per slice
+constexpr uint32_t SL_WORDS = 1u << (SL_LOG - 5);      // 16384 u32 = 64 KiB of LDS
+constexpr uint32_t SL_MAX = 32768;                     // slices (2^34 bits) handled here
+constexpr uint32_t INVALID = 0xFFFFFFFFu;              // no probe (payloads are < 2^26)
+
+RSK_DEV uint32_t rdl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+RSK_DEV uint64_t rdl64(uint64_t v, uint32_t l) {
+  return ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32) | rdl((uint32_t)v, l);
+}
+
+// Exclusive scan of one value per lane over a T-lane workgroup.
+template <int T>
+RSK_DEV uint32_t block_scan(uint32_t v, uint32_t* total, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < T / 64; ++q) {
+    const uint32_t s = wsum[q];
+    pre += q < w ? s : 0;
+    tot += s;
+  }
+  *total = tot;
+  __syncthreads();
+  return pre + x - v;
+}
+
+RSK_DEV void key_words(const uint4& v, uint64_t* w0, uint64_t* w1) {
+  *w0 = ((uint64_t)v.y << 32) | v.x;
+  *w1 = ((uint64_t)v.w << 32) | v.z;
+}
+
+// ------------------------------------------------------------------- st1
+// Wave 0 turns the bin counts (<= 256, 4 per lane) into bin starts: lstart
+// (LDS), the super-tile header row (global, [nb] = total) and the total.
+RSK_DEV uint32_t wave_scan_incl(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x;
+}
+
+template <int NBMAX>
+RSK_DEV void wave0_bin_starts(uint32_t* hist, uint32_t* lstart, uint32_t nb, uint16_t* hdr_row, uint32_t* s_total) {
+  constexpr int PER = NBMAX / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    v[i] = b < nb ? hist[b] : 0;
+    if (b < nb) hist[b] = 0;  // reset for the next tile (visible after the next barrier)
+    sum += v[i];
+  }
+  const uint32_t incl = wave_scan_incl(sum, lane);
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    if (b < nb) {
+      lstart[b] = run;
+      hdr_row[b] = (uint16_t)run;
+    }
+    run += v[i];
+  }
+  const uint32_t total = rdl(incl, 63);
+  if (lane == 0) {
+    hdr_row[nb] = (uint16_t)total;
+    *s_total = total;
+  }
+}
+
+// Probe records of the append partition.  u32: the probe's bit offset inside
+// its bin (the insert); u64: (sequence << 32) | offset, the add()-with-replies
+// pipeline, whose last stage needs each probe's place in the batch.  Offsets
+// are < 2^26, so a record whose low word is INVALID is padding.
+template <class R>
+RSK_DEV uint32_t rec_off(R r) { return (uint32_t)r; }
+template <class R>
+RSK_DEV R rec_make(uint32_t off, uint32_t seq) {
+  if constexpr (sizeof(R) == 8) return ((uint64_t)seq << 32) | off;
+  else return off;
+}
+template <class R>
+RSK_DEV R rec_with_off(R r, uint32_t off) {  // same record, offset replaced
+  if constexpr (sizeof(R) == 8) return (r & ~0xFFFFFFFFull) | off;
+  else return off;
+}
+template <class R>
+constexpr R rec_pad() { return (R)~(R)0; }
+template <class R>
+RSK_DEV void unpack16(const uint4& x, R* out) {  // one 16-byte group -> 16 / sizeof(R) records
+  if constexpr (sizeof(R) == 8) {
+    out[0] = ((uint64_t)x.y << 32) | x.x;
+    out[1] = ((uint64_t)x.w << 32) | x.z;
+  } else {
+    out[0] = x.x;
+    out[1] = x.y;
+    out[2] = x.z;
+    out[3] = x.w;
+  }
+}
+
+// wave0_bin_starts with every bin's run padded to a whole 16-byte group of
+// records (rec_pad in img), so runs start 16-byte aligned: starts and total padded.
+template <int NBMAX, class R>
+RSK_DEV void wave0_bin_starts_pad(uint32_t* hist, uint32_t* lstart, uint32_t nb, uint16_t* hdr_row,
+                                  uint32_t* s_total, R* img) {
+  constexpr uint32_t RG = 16 / sizeof(R);
+  constexpr int PER = NBMAX / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    v[i] = b < nb ? hist[b] : 0;
+    if (b < nb) hist[b] = 0;
+    sum += (v[i] + RG - 1) & ~(RG - 1);
+  }
+  const uint32_t incl = wave_scan_incl(sum, lane);
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t b = lane * PER + i;
+    const uint32_t l4 = (v[i] + RG - 1) & ~(RG - 1);
+    if (b < nb) {
+      lstart[b] = run;
+      hdr_row[b] = (uint16_t)run;
+      for (uint32_t j = run + v[i]; j < run + l4; ++j) img[j] = rec_pad<R>();
+    }
+    run += l4;
+  }
+  const uint32_t total = rdl(incl, 63);
+  if (lane == 0) {
+    hdr_row[nb] = (uint16_t)total;
+    *s_total = total;
+  }
+}
+
+// ------------------------------------------------------ header transpose
+// in [rows][cols] -> out [cols][rows] (u16), 64 x 64 tiles through LDS.
+__global__ __launch_bounds__(256) void st_transpose_kernel(const uint16_t* __restrict__ in, uint64_t rows,
+                                                           uint32_t cols, uint16_t* __restrict__ out) {
+  __shared__ uint16_t t[64][66];
+  const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+  const uint32_t c0 = blockIdx.y * 64;
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += 256) {
+    const uint32_t rr = i >> 6, cc = i & 63;
+    const uint64_t r = r0 + rr;
+    const uint32_t c = c0 + cc;
+    t[rr][cc] = (r < rows && c < cols) ? in[r * cols + c] : 0;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += 256) {
+    const uint32_t cc = i >> 6, rr = i & 63;
+    const uint64_t r = r0 + rr;
+    const uint32_t c = c0 + cc;
+    if (r < rows && c < cols) out[(uint64_t)c * rows + r] = t[rr][cc];
+  }
+}
+
+// One workgroup: exclusive prefix sums reg_off (u64) / tile_off (u32) over
+// ncp entries, with the totals at [ncp].
+__global__ __launch_bounds__(1024) void st_offsets_kernel(const uint64_t* __restrict__ tot,
+                                                          const uint32_t* __restrict__ bud, uint32_t ncp,
+                                                          uint64_t* __restrict__ reg_off,
+                                                          uint32_t* __restrict__ tile_off) {
+  __shared__ uint64_t s_tot[1024];
+  __shared__ uint32_t s_bud[1024];
+  const uint32_t per = (ncp + 1023) / 1024, b0 = threadIdx.x * per;
+  uint64_t a = 0;
+  uint32_t c = 0;
+  for (uint32_t i = b0; i < b0 + per && i < ncp; ++i) {
+    a += tot[i];
+    c += bud[i];
+  }
+  s_tot[threadIdx.x] = a;
+  s_bud[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 1024 partials, serial (tiny)
+    uint64_t ra = 0;
+    uint32_t rc = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const uint64_t x = s_tot[i];
+      const uint32_t y = s_bud[i];
+      s_tot[i] = ra;
+      s_bud[i] = rc;
+      ra += x;
+      rc += y;
+    }
+    reg_off[ncp] = ra;
+    tile_off[ncp] = rc;
+  }
+  __syncthreads();
+  a = s_tot[threadIdx.x];
+  c = s_bud[threadIdx.x];
+  for (uint32_t i = b0; i < b0 + per && i < ncp; ++i) {
+    reg_off[i] = a;
+    tile_off[i] = c;
+    a += tot[i];
+    c += bud[i];
+  }
+}
+
+// ============================================ append variant (two-level filters)
+// sa1: the st1 super-tile (one hash pass, ranks by coarse bin, bin-sorted LDS
+// image), but each coarse bin's run is APPENDED to this workgroup's private
+// sub-region for that bin: sub-region (w, c) = probes [(w nb1 + c) quota,
+// + quota), so a run's destination is known as soon as the tile's bin counts
+// are (no global atomics, no headers); the workgroup records how many probes
+// it appended per bin (used[w][c]).
+// sa2: one workgroup per (c, p) streams the sub-regions (w, c) of the
+// workgroups w of part p with coalesced 16-byte loads (a tile never spans two
+// sub-regions), ranks by fine bin and writes bin-sorted tiles exactly like
+// st2, whose output the apply kernel reads unchanged.  A sub-region that
+// overflows (only adversarial inputs: 1.25x the expected share per
+// workgroup) sets `overflow`; the chunk is redone.
+constexpr int SA2_V = 3;            // sa2: uint4 loads per lane per tile (u32: 96 probes per fine bin: apply's 2 x 64 fast path)
+constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
+template <class R>
+constexpr uint32_t sa2_slots() { return SA2_T * SA2_V * (16 / sizeof(R)); }
+template <class R>
+constexpr uint32_t sa2_pad() { return (16 / sizeof(R) - 1) * 128; }  // pad slots per sa2 tile, at most (per fine bin)
+constexpr uint32_t SA2_SLOTS = sa2_slots<uint32_t>();
+constexpr uint32_t SA2_PAD = sa2_pad<uint32_t>();
+
+RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads instead of the LDS-only barrier
+  if (dbg) __syncthreads();
+  else lds_barrier();
+}
+
+// 512-lane workgroups: at most 80 VGPRs with 4-byte records, so 3 workgroups
+// (6 waves per SIMD) share a CU; 8-byte records: 2 workgroups (73 KiB of LDS).
+// seq0 of key q of the chunk = q k (u64 records carry seq0 + t; the host keeps
+// a chunk below 2^32 probes).
+template <bool FIXED16, int KMAX, int T1, class R>
+__global__ __launch_bounds__(T1, sizeof(R) == 8 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
+    FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
+    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow, int dbg) {
+  constexpr int KPL = 16 / KMAX;
+  constexpr uint32_t KST = T1 * KPL;
+  constexpr int NP = KPL * KMAX;
+  constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
+  constexpr uint32_t RG = 16 / sizeof(R);  // records per 16-byte group
+  // runs are padded to whole 16-byte groups (rec_pad), so the write-out
+  // moves 16-byte groups of one bin to 16-byte aligned destinations
+  constexpr uint32_t IMG = T1 * NP + RG * 256;
+  __shared__ __attribute__((aligned(16))) R img[IMG];
+  __shared__ uint8_t ibin[IMG / RG];
+  __shared__ uint32_t hist[256], lstart[256], pos[256], dst[256], s_total;
+  const uint64_t low = (1ull << shift1) - 1;
+  if (threadIdx.x < 256) {
+    hist[threadIdx.x] = 0;
+    pos[threadIdx.x] = 0;
+  }
+  R* const mine = region + (uint64_t)blockIdx.x * nb1 * quota;  // sub-regions (blockIdx.x, 0..nb1)
+  const uint4* keys16 = reinterpret_cast<const uint4*>(data);
+  uint4 nxt[KPL];
+  auto fetch = [&](uint64_t st) {
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const uint64_t i = st * KST + threadIdx.x + (uint64_t)u * T1;
+      nxt[u] = (FIXED16 && st < nst && i < n) ? ld_nt16(keys16 + i) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (FIXED16) fetch(blockIdx.x);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t st = blockIdx.x; st < nst; st += gridDim.x) {
+    const uint64_t k0 = st * KST;
+    const uint32_t nk = (uint32_t)(n - k0 < KST ? n - k0 : KST);
+    uint4 cur[KPL];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) cur[u] = nxt[u];
+    if (FIXED16) fetch(st + gridDim.x);
+    R pay[NP];
+    uint32_t tag[NP];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const uint32_t q = threadIdx.x + u * T1;
+      const bool ok = q < nk;
+      const uint32_t seq0 = sizeof(R) == 8 ? (uint32_t)((k0 + q) * (uint64_t)k) : 0u;
+      uint64_t h1 = 0, h2 = 0;
+      if (ok) {
+        if (FIXED16) {
+          uint64_t w0, w1;
+          key_words(cur[u], &w0, &w1);
+          h1 = xxh64_16(w0, w1);
+          h2 = farm_16(w0, w1);
+        } else {
+          bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
+        }
+      }
+      ProbeSeq ps(h1, h2, fm);
+#pragma unroll
+      for (int t = 0; t < KMAX; ++t) {
+        const int s = u * KMAX + t;
+        tag[s] = INVALID;
+        pay[s] = 0;
+        if (ok && t < k) {
+          const uint64_t idx = ps.idx;
+          const uint32_t bin = (uint32_t)(idx >> shift1);
+          pay[s] = rec_make<R>((uint32_t)(idx & low), seq0 + (uint32_t)t);
+          tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+          if (t + 1 < k) ps.next(t, fm);
+        }
+      }
+    }
+    sa_bar(dbg);  // (A) every rank taken
+    // wave 0: bin starts and run destinations (runs of L probes take
+    // L4 = round_up(L, RG) slots, the tail rec_pad): image position j of bin b
+    // goes to mine[j + dst[b]] (mod 2^32), dst[b] = b quota + pos[b] - lstart[b]
+    if (threadIdx.x < 64) {
+      uint32_t v[PER], sum = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        v[i] = b < nb1 ? hist[b] : 0;
+        if (b < nb1) hist[b] = 0;
+        sum += (v[i] + RG - 1) & ~(RG - 1);
+      }
+      const uint32_t incl = wave_scan_incl(sum, lane);
+      uint32_t at = incl - sum;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        const uint32_t l4 = (v[i] + RG - 1) & ~(RG - 1);
+        if (b < nb1) {
+          lstart[b] = at;
+          for (uint32_t j = at + v[i]; j < at + l4; ++j) img[j] = rec_pad<R>();
+          const uint32_t p = pos[b];
+          if (p + l4 <= limit) {  // limit = quota (< quota only in tests)
+            dst[b] = b * quota + p - at;
+            pos[b] = p + l4;
+          } else {  // sub-region full: drop the run (the host redoes the chunk)
+            if (v[i]) atomicOr(overflow, 1u);
+            dst[b] = INVALID;
+          }
+        }
+        at += l4;
+      }
+      if (lane == 63) s_total = incl;
+    }
+    sa_bar(dbg);  // (B) lstart / dst / total ready
+#pragma unroll
+    for (int s = 0; s < NP; ++s)
+      if (tag[s] != INVALID) {
+        const uint32_t b = tag[s] >> 16, r = tag[s] & 0xFFFFu, j = lstart[b] + r;
+        img[j] = pay[s];
+        if ((r & (RG - 1)) == 0) ibin[j / RG] = (uint8_t)b;  // the group's first slot always holds a probe
+      }
+    const uint32_t total4 = s_total / RG;
+    sa_bar(dbg);  // (C) image complete
+    const uint4* img4 = reinterpret_cast<const uint4*>(img);
+    for (uint32_t g = threadIdx.x; g < total4; g += T1) {
+      const uint32_t d = dst[ibin[g]];
+      if (d != INVALID) {
+        const uint4 v = img4[g];
+        u32x4 x = {v.x, v.y, v.z, v.w};
+        *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nb1) used[(uint64_t)blockIdx.x * nb1 + threadIdx.x] = pos[threadIdx.x];
+}
+
+// tot[cp] = records of (c, p), bud[cp] = its sa2 tiles (one per sa2_slots<R> of each sub-region)
+template <class R>
+__global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
+                                                      uint32_t P, uint32_t ncp, uint64_t* __restrict__ tot,
+                                                      uint32_t* __restrict__ bud) {
+  constexpr uint64_t RG = 16 / sizeof(R);
+  const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cp >= ncp) return;
+  const uint32_t c = cp / P, p = cp - c * P;
+  uint64_t probes = 0;
+  uint32_t tiles = 0;
+  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
+    const uint32_t u = used[(uint64_t)w * nb1 + c];
+    probes += u;
+    tiles += (u + sa2_slots<R>() - 1) / sa2_slots<R>();
+  }
+  // sa2 output bound: its tiles pad fine-bin runs
+  tot[cp] = ((probes + RG - 1) & ~(RG - 1)) + (uint64_t)tiles * sa2_pad<R>();
+  bud[cp] = tiles;
+}
+
+template <class R>
+__global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const R* __restrict__ region, uint32_t quota,
+                                                          const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
+                                                          uint32_t P, uint32_t nb2,
+                                                          const uint64_t* __restrict__ reg_off,
+                                                          const uint32_t* __restrict__ tile_off,
+                                                          uint32_t* __restrict__ tiles_out, R* __restrict__ out,
+                                                          uint16_t* __restrict__ h2, uint64_t* __restrict__ tb2,
+                                                          int dbg) {
+  constexpr uint32_t RG = 16 / sizeof(R);
+  constexpr int NV = SA2_V * RG;
+  constexpr uint32_t SLOTS = sa2_slots<R>();
+  // one image buffer: with LDS-only barriers a wave's write-out of tile t is
+  // done before it reaches (A) of t+1, and the image is rewritten after (B)
+  __shared__ __attribute__((aligned(16))) R srt[1][SLOTS + RG * 128];  // + pad slots per fine bin
+  __shared__ uint32_t hist[128], lstart[128], s_total;
+  __shared__ uint16_t s_hdr[129];
+  const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
+  if (threadIdx.x < 128) hist[threadIdx.x] = 0;
+  const uint64_t base = reg_off[cp];
+  const uint32_t tbeg = tile_off[cp];
+  uint64_t written = 0;
+  uint32_t ntile = 0;
+  __syncthreads();
+  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
+    const uint32_t nu = used[(uint64_t)w * nb1 + c];  // records of sub-region (w, c)
+    const R* sub = region + ((uint64_t)w * nb1 + c) * quota;
+    const uint4* in = reinterpret_cast<const uint4*>(sub);  // quota is a multiple of 4: 16-byte aligned
+    for (uint32_t t0 = 0; t0 < nu; t0 += SLOTS) {
+      R pay[NV];
+      uint32_t tag[NV];
+#pragma unroll
+      for (int v = 0; v < SA2_V; ++v) {
+        const uint32_t q4 = t0 / RG + v * SA2_T + threadIdx.x;  // uint4 index
+        if (RG * q4 + RG - 1 < nu) {
+          unpack16<R>(ld_nt16(in + q4), pay + RG * v);
+        } else {
+#pragma unroll
+          for (uint32_t e = 0; e < RG; ++e) pay[RG * v + e] = RG * q4 + e < nu ? sub[RG * q4 + e] : rec_pad<R>();
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        tag[r] = INVALID;
+        if (rec_off(pay[r]) != INVALID) {
+          const uint32_t bin = rec_off(pay[r]) >> SL_LOG;
+          tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+        }
+      }
+      sa_bar(dbg);  // (A)
+      if (threadIdx.x < 64) wave0_bin_starts_pad<128, R>(hist, lstart, nb2, s_hdr, &s_total, srt[0]);
+      sa_bar(dbg);  // (B)
+      const uint32_t total = s_total;  // padded: a multiple of RG
+      if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
+      if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
+      R* img = srt[0];
+#pragma unroll
+      for (int r = 0; r < NV; ++r)
+        if (tag[r] != INVALID)
+          img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = rec_with_off(pay[r], rec_off(pay[r]) & ((1u << SL_LOG) - 1));
+      sa_bar(dbg);  // (C)
+      // 16-byte aligned: base and written are multiples of RG slots
+      u32x4* o4 = reinterpret_cast<u32x4*>(out + base + written);
+      const uint4* i4 = reinterpret_cast<const uint4*>(img);
+      for (uint32_t j = threadIdx.x; j < total / RG; j += SA2_T) {
+        const uint4 v = i4[j];
+        u32x4 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, o4 + j);
+      }
+      written += total;
+      ++ntile;
+    }
+  }
+  if (threadIdx.x == 0) tiles_out[cp] = ntile;
+}
+
+}  // namespace
+}  // namespace rsk

@@ -213,6 +213,12 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d
 // Performs a pending lazy clear (rsk_api.hip).
 void hll_materialize(const rsk_hll* h);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
+// add() replies (RedissonBloomFilter.java:100-107) + the insert, any batch size:
+// the partitioned first-probe pipeline (rsk_bloom_reply.hip) when it applies,
+// else the sort path in sub-batches of 2^28 probes.
+void bloom_add_replies_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
+void bloom_add_replies_sorted(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
+bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);
 void bloom_contains_probe_count_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out,
