@@ -214,7 +214,7 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, with_replies: bool = Tr
             ms, cnt = engine.prof_read(name)
             if cnt:
                 rstages[name] = ms
-        chunks = -(-n_ins * k.value // 0xFFFFFFFF)
+        chunks = -(-n_ins * k.value // (1 << 33))  # rsk_bloom_reply.hip: chunks of <= 2^33 probes
         # per probe: 8 B record written by rp1, read + written by rp2 and rp3, read by
         # rp_apply; per chunk: the first-probe table (4 B per filter bit) written,
         # the filter read and written; keys read by rp1 and by the reply pass

@@ -4,27 +4,32 @@
 // sends the k SETBITs of an element in one pipeline and answers true iff one
 // of the FIRST k-1 replies was 0 (:100-107).  Over a batch the SETBITs run in
 // sequence order p = i k + t, so probe p finds its bit clear iff the bit was
-// clear before the batch and no probe q < p hit the same bit: the minimum
-// sequence number over the probes of a bit decides.  Instead of sorting all
-// k n (bit, p) pairs, this path partitions 8-byte records (p << 32 | offset)
-// down to 4 KiB blocks of the filter and takes the minimum per bit in LDS:
+// clear before the batch and no probe q < p hit the same bit.  For the reply
+// of key i only the smallest KEY over the probes of a bit matters: if
+// minkey[b_t] == i for some t < k-1, the first of key i's own probes on that
+// bit (t* <= t < k-1) found it clear; otherwise every one of them followed an
+// earlier key's probe (or the bit was set before the batch).  Instead of
+// sorting all k n (bit, p) pairs, this path partitions 8-byte records
+// (key << 32 | offset) down to 2 KiB blocks of the filter and takes the
+// minimum key per bit in LDS:
 //
 //   rp1, rp2 : the append partition's sa1 / sa2 (rsk_bloom_sa.h) with 8-byte
 //              records: coarse bins, then 64 KiB slices of the filter.
 //   rp3      : one workgroup per slice re-sorts its records into the slice's
-//              16 blocks of 2^15 bits through LDS (tiles of RP3_TILE records,
-//              a 17-entry u16 header per tile), written contiguously.
-//   rp_apply : one workgroup per block: minseq[32768] in LDS (128 KiB),
-//              atomicMin of every record's p; then the block's first-probe
-//              table fp[bit] = minseq (NONE where the bit was already set: no
-//              probe can find it clear) and the block ORed into the filter.
+//              32 blocks of 2^14 bits through LDS (tiles of RP3_TILE records,
+//              a 33-entry u16 header per tile), written contiguously.
+//   rp_apply : one workgroup per block: minkey[16384] in LDS (64 KiB),
+//              atomicMin of every record's key; then the block's first-key
+//              table fk[bit] = minkey (NONE where the bit was already set: no
+//              probe finds it clear) and the block ORed into the filter.
 //   rp_reply : per key, its first k-1 probe indices again; true at the first
-//              t with fp[idx_t] == i k + t (early exit, ~1.4 gathers per key
-//              at the C3 fill).
-// Chunks of < 2^32 probes run one after the other (p is 32 bits): each sees
-// the filter the previous chunks left, exactly like the sequential SETBITs.
+//              t with fk[idx_t] == i (early exit, ~1.4 gathers per key at the
+//              C3 fill).
+// Chunks (< 2^32 - 1 keys, and a bound on the probes for scratch) run one
+// after the other, each seeing the filter the previous ones left, exactly
+// like the sequential SETBITs; C3 (1B keys, k = 7) is one chunk.
 // HBM per probe: 8 B (rp1 write) + 16 (rp2) + 16 (rp3) + 8 (rp_apply), plus
-// 4 B per filter bit (fp) and 2 x the filter per chunk, plus the reply pass.
+// 4 B per filter bit (fk) and 2 x the filter per chunk, plus the reply pass.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -35,17 +40,19 @@ namespace rsk {
 
 namespace {
 
-constexpr int RB_LOG = 15;                            // bits per block
-constexpr uint32_t RB_BITS = 1u << RB_LOG;            // 32768: minseq in LDS = 128 KiB
-constexpr uint32_t RB_WORDS = RB_BITS / 32;           // 1024 filter words per block
-constexpr uint32_t RB_PER_SL = 1u << (SL_LOG - RB_LOG);  // 16 blocks per slice
-constexpr uint32_t NONE = 0xFFFFFFFFu;                // fp: no probe finds this bit clear
+constexpr int RB_LOG = 14;                            // bits per block
+constexpr uint32_t RB_BITS = 1u << RB_LOG;            // 16384: minkey in LDS = 64 KiB (2 workgroups per CU)
+constexpr uint32_t RB_WORDS = RB_BITS / 32;           // 512 filter words per block
+constexpr uint32_t RB_PER_SL = 1u << (SL_LOG - RB_LOG);  // 32 blocks per slice
+constexpr uint32_t RP3_CHUNKS = 128;                  // rp3: 64-record chunks per round
+constexpr uint32_t NONE = 0xFFFFFFFFu;                // fk: no probe finds this bit clear (never a key index)
 constexpr uint32_t RP3_T = 1024;                      // rp3 workgroup
 constexpr uint32_t RP3_PER = 8;                       // records per lane per rp3 round
 constexpr uint32_t RP3_TILE = RP3_T * RP3_PER;        // 8192 records per rp3 tile
 constexpr uint32_t RP3_GROUP = RP3_T;                 // sa2 tiles per rp3 group (one header per lane)
 constexpr uint32_t RA_T = 1024;                       // rp_apply workgroup
-constexpr uint64_t MAX_CHUNK_PROBES = 0xFFFFFFFFull;  // p < 2^32 - 1 (NONE is never a p)
+constexpr uint64_t MAX_CHUNK_KEYS = 0xFFFFFFFEull;    // key indices < NONE
+constexpr uint64_t DEFAULT_CHUNK_PROBES = 1ull << 33;  // scratch bound: ~2.3 x 8 B per probe
 
 // ------------------------------------------------------------------ sizing
 // Slice s = blockIdx.x: its records in the sa2 tiles of coarse bin s >> f2
@@ -80,10 +87,11 @@ __global__ __launch_bounds__(256) void rp_size_kernel(const uint16_t* __restrict
 // Workgroup = slice s.  Its input is one segment (the slice's fine bin) of
 // every sa2 tile of coarse bin c: taken a group of <= 1024 tiles at a time
 // (lane j: tile j's segment; a block scan gives the concatenation), in rounds
-// of RP3_TILE records: record i of the round is found by binary search over
-// the group's starts, ranked by block with an LDS atomic, placed in an LDS
+// of RP3_TILE records: record i of the round is found from a table of the
+// segment holding each 64-record chunk start (then a short forward walk over
+// the group's starts), ranked by block with an LDS atomic, placed in an LDS
 // image and written contiguously at the slice's region with a header
-// h3[tile][0..16] (block starts) and its position tb3[tile].  Padding records
+// h3[tile][0..32] (block starts) and its position tb3[tile].  Padding records
 // (low word INVALID) are dropped.
 __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__ in, const uint16_t* __restrict__ h2t,
                                                     uint64_t row_stride, uint32_t f2, const uint64_t* __restrict__ tb2,
@@ -95,7 +103,8 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ tb3, uint32_t* __restrict__ ntile3) {
   __shared__ __attribute__((aligned(16))) uint64_t img[RP3_TILE];
   __shared__ uint64_t s_pos[RP3_GROUP];
-  __shared__ uint32_t s_pre[RP3_GROUP];
+  __shared__ uint32_t s_pre[RP3_GROUP + 1];
+  __shared__ uint16_t tbl[RP3_CHUNKS];
   __shared__ uint32_t wsum[RP3_T / 64];
   __shared__ uint32_t hist[RB_PER_SL + 1], lstart[RB_PER_SL + 1];
   const uint32_t s = blockIdx.x, c = s >> f2, f = s & ((1u << f2) - 1);
@@ -120,8 +129,18 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
       uint32_t total;
       const uint32_t pre = block_scan<RP3_T>(len, &total, wsum);  // (barriers inside)
       if (threadIdx.x < ng) s_pre[threadIdx.x] = pre;
+      s_pre[ng] = total;  // (sentinel; written by every lane, same value)
       __syncthreads();
       for (uint32_t r0 = 0; r0 < total; r0 += RP3_TILE) {
+        // chunk table: tbl[c] = the segment holding record r0 + 64 c (each
+        // non-empty segment claims the chunk starts that fall inside it)
+        if (threadIdx.x < ng && len) {
+          const uint32_t a = pre, e = pre + len;
+          const uint32_t c0 = a > r0 ? (a - r0 + 63) >> 6 : 0;
+          const uint32_t c1 = e > r0 ? min(RP3_CHUNKS, (e - r0 + 63) >> 6) : 0;
+          for (uint32_t cc = c0; cc < c1; ++cc) tbl[cc] = (uint16_t)threadIdx.x;
+        }
+        __syncthreads();
         uint64_t rec[RP3_PER];
         uint32_t tag[RP3_PER];
 #pragma unroll
@@ -129,13 +148,9 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
           const uint32_t i = r0 + m * RP3_T + threadIdx.x;
           rec[m] = rec_pad<uint64_t>();
           if (i < total) {
-            uint32_t lo = 0, hi = ng;  // last segment j with s_pre[j] <= i
-            while (hi - lo > 1) {
-              const uint32_t mid = (lo + hi) >> 1;
-              if (s_pre[mid] <= i) lo = mid;
-              else hi = mid;
-            }
-            rec[m] = __builtin_nontemporal_load(in + s_pos[lo] + (i - s_pre[lo]));
+            uint32_t j = tbl[(i - r0) >> 6];  // then forward over the (few) segments of the chunk
+            while (s_pre[j + 1] <= i) ++j;
+            rec[m] = __builtin_nontemporal_load(in + s_pos[j] + (i - s_pre[j]));
           }
         }
 #pragma unroll
@@ -184,7 +199,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
 // ---------------------------------------------------------------- rp_apply
 // Workgroup = block b (bits [b 2^15, (b + 1) 2^15)): every segment of it in
 // its slice's rp3 tiles (wave w takes tiles w, w + 16, ...; 4 records per lane
-// in flight), atomicMin of p into minseq; then fp[bit] and the filter words,
+// in flight), atomicMin of the key into minkey; then fk[bit] and the filter words,
 // 64 bits per wave step (a ballot of "touched" is the MSB-first word pair).
 __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restrict__ in,
                                                         const uint16_t* __restrict__ h3,
@@ -192,7 +207,7 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
                                                         const uint32_t* __restrict__ tile3_off,
                                                         const uint32_t* __restrict__ ntile3, uint64_t nblocks,
                                                         uint32_t* __restrict__ bits, uint64_t nwords,
-                                                        uint32_t* __restrict__ fp) {
+                                                        uint32_t* __restrict__ fk) {
   __shared__ __attribute__((aligned(16))) uint32_t ms[RB_BITS];
   __shared__ uint32_t f0[RB_WORDS];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -222,11 +237,11 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
       }
     }
     __syncthreads();
-    uint32_t* fpb = fp + b * RB_BITS;
+    uint32_t* fkb = fk + b * RB_BITS;
     for (uint32_t o = threadIdx.x; o < RB_BITS; o += RA_T) {  // a wave covers 64 bits = words o/32, o/32 + 1
       const uint32_t v = ms[o];
       const uint32_t was = f0[o >> 5] & bloom_bit_mask(o);
-      fpb[o] = was ? NONE : v;
+      fkb[o] = was ? NONE : v;
       const uint64_t hit = __ballot(v != NONE);
       if (lane == 0 || lane == 32) {
         const uint32_t lo = (uint32_t)(lane == 0 ? hit : hit >> 32);
@@ -240,25 +255,23 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
 }
 
 // ---------------------------------------------------------------- rp_reply
-// Key i of the chunk: true iff fp[idx_t] == i k + t for some t < k - 1.  U
+// Key i of the chunk: true iff fk[idx_t] == i for some t < k - 1.  U
 // keys per lane keep U gather chains in flight; a wave stops when every key
 // is decided.
 template <bool FIXED16, int U>
 __global__ __launch_bounds__(256) void rp_reply_kernel(const uint8_t* __restrict__ data,
                                                        const uint64_t* __restrict__ offsets, uint32_t fixed_len,
                                                        uint64_t n, FastMod63 fm, int k,
-                                                       const uint32_t* __restrict__ fp, uint8_t* __restrict__ out) {
+                                                       const uint32_t* __restrict__ fk, uint8_t* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < n; base += stride) {
     ProbeSeq ps[U];
     bool live[U], yes[U];
-    uint32_t seq[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + (uint64_t)u * blockDim.x;
       live[u] = i < n;
       yes[u] = false;
-      seq[u] = (uint32_t)(i * (uint64_t)k);
       if (live[u]) {
         uint64_t h1, h2;
         bloom_key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
@@ -271,11 +284,11 @@ __global__ __launch_bounds__(256) void rp_reply_kernel(const uint8_t* __restrict
     for (int t = 0; t < k - 1; ++t) {
       uint32_t v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = open[u] ? fp[ps[u].idx] : NONE;
+      for (int u = 0; u < U; ++u) v[u] = open[u] ? fk[ps[u].idx] : NONE;
       bool any = false;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (open[u] && v[u] == seq[u] + (uint32_t)t) {
+        if (open[u] && v[u] == (uint32_t)(base + (uint64_t)u * blockDim.x)) {
           yes[u] = true;
           open[u] = false;
         }
@@ -327,9 +340,9 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint32_t cus = (uint32_t)c->num_cus;
   const uint32_t P = std::max<uint32_t>(1, (4 * cus + nb1 - 1) / nb1);
   const uint32_t ncp = nb1 * P;
-  const uint64_t probe_cap = std::min<uint64_t>(MAX_CHUNK_PROBES, env_knob("RSK_BLOOM_REPLY_CHUNK", 0) ? env_knob("RSK_BLOOM_REPLY_CHUNK", 0) : MAX_CHUNK_PROBES);
+  const uint64_t probe_cap = env_knob("RSK_BLOOM_REPLY_CHUNK", 0) ? env_knob("RSK_BLOOM_REPLY_CHUNK", 0) : DEFAULT_CHUNK_PROBES;
   uint64_t chunk = std::max<uint64_t>(1, probe_cap / k / kst) * kst;  // keys per chunk, whole super-tiles
-  if (chunk * k > MAX_CHUNK_PROBES) chunk -= kst;
+  if (chunk > MAX_CHUNK_KEYS) chunk = MAX_CHUNK_KEYS / kst * kst;
   chunk = std::min<uint64_t>(chunk, keys.n);
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
@@ -368,7 +381,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     uint64_t* tb2 = reinterpret_cast<uint64_t*>(take(al(8 * tt_max)));
     uint16_t* h3 = reinterpret_cast<uint16_t*>(take(al(tt3_max * (RB_PER_SL + 1) * 2)));
     uint64_t* tb3 = reinterpret_cast<uint64_t*>(take(al(8 * tt3_max)));
-    uint32_t* fp = reinterpret_cast<uint32_t*>(take(al(4 * nblocks * RB_BITS)));
+    uint32_t* fk = reinterpret_cast<uint32_t*>(take(al(4 * nblocks * RB_BITS)));
     uint64_t* tot = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
     uint64_t* reg_off = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
     uint32_t* bud = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
@@ -444,10 +457,10 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp_apply");
-      // 132 KiB of LDS: one workgroup per CU, each looping over its blocks
-      const uint32_t ga = (uint32_t)std::min<uint64_t>(nblocks, cus);
+      // 66 KiB of LDS: two workgroups per CU, each looping over its blocks
+      const uint32_t ga = (uint32_t)std::min<uint64_t>(nblocks, 2ull * cus);
       hipLaunchKernelGGL(rp_apply_kernel, dim3(ga), dim3(RA_T), 0, c->stream, region, h3, tb3, tile3_off, ntile3,
-                         nblocks, b->d_bits, b->nwords, fp);
+                         nblocks, b->d_bits, b->nwords, fk);
       RSK_CHECK_LAUNCH("bloom_rp_apply");
     }
     {
@@ -457,10 +470,10 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
       if (f16)
         hipLaunchKernelGGL((rp_reply_kernel<true, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, fp, d_out + first);
+                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
       else
         hipLaunchKernelGGL((rp_reply_kernel<false, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, fp, d_out + first);
+                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
       RSK_CHECK_LAUNCH("bloom_rp_reply");
     }
   }

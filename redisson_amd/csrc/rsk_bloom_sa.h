@@ -91,14 +91,14 @@ RSK_DEV void wave0_bin_starts(uint32_t* hist, uint32_t* lstart, uint32_t nb, uin
 }
 
 // Probe records of the append partition.  u32: the probe's bit offset inside
-// its bin (the insert); u64: (sequence << 32) | offset, the add()-with-replies
-// pipeline, whose last stage needs each probe's place in the batch.  Offsets
+// its bin (the insert); u64: (key index << 32) | offset, the add()-with-replies
+// pipeline, whose last stage needs the key each probe belongs to.  Offsets
 // are < 2^26, so a record whose low word is INVALID is padding.
 template <class R>
 RSK_DEV uint32_t rec_off(R r) { return (uint32_t)r; }
 template <class R>
-RSK_DEV R rec_make(uint32_t off, uint32_t seq) {
-  if constexpr (sizeof(R) == 8) return ((uint64_t)seq << 32) | off;
+RSK_DEV R rec_make(uint32_t off, uint32_t key) {
+  if constexpr (sizeof(R) == 8) return ((uint64_t)key << 32) | off;
   else return off;
 }
 template <class R>
@@ -251,8 +251,8 @@ RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads in
 
 // 512-lane workgroups: at most 80 VGPRs with 4-byte records, so 3 workgroups
 // (6 waves per SIMD) share a CU; 8-byte records: 2 workgroups (73 KiB of LDS).
-// seq0 of key q of the chunk = q k (u64 records carry seq0 + t; the host keeps
-// a chunk below 2^32 probes).
+// u64 records carry the key's index in the chunk (the host keeps a chunk
+// below 2^32 - 1 keys).
 template <bool FIXED16, int KMAX, int T1, class R>
 __global__ __launch_bounds__(T1, sizeof(R) == 8 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(T1, sizeof(R) == 8 ? 4 : (T1 == 512 ? 6 : 4)) void 
     for (int u = 0; u < KPL; ++u) {
       const uint32_t q = threadIdx.x + u * T1;
       const bool ok = q < nk;
-      const uint32_t seq0 = sizeof(R) == 8 ? (uint32_t)((k0 + q) * (uint64_t)k) : 0u;
+      const uint32_t key = sizeof(R) == 8 ? (uint32_t)(k0 + q) : 0u;
       uint64_t h1 = 0, h2 = 0;
       if (ok) {
         if (FIXED16) {
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(T1, sizeof(R) == 8 ? 4 : (T1 == 512 ? 6 : 4)) void 
         if (ok && t < k) {
           const uint64_t idx = ps.idx;
           const uint32_t bin = (uint32_t)(idx >> shift1);
-          pay[s] = rec_make<R>((uint32_t)(idx & low), seq0 + (uint32_t)t);
+          pay[s] = rec_make<R>((uint32_t)(idx & low), key);
           tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
           if (t + 1 < k) ps.next(t, fm);
         }

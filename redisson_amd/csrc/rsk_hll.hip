@@ -273,16 +273,22 @@ RSK_DEV uint64_t lds_u64(const uint8_t* p) {
 // keeps its value (its clamped read stays inside its key + 7 bytes).  The
 // tail read may run up to 7 bytes past a key, inside the stage's slack;
 // those bytes are masked off.
+// The loop runs ceil(len/8) - 1 full blocks and the last step is a select
+// (the tail masked, or the last full block mixed): every key of one step
+// class takes the same trip count, so a class-sorted wave does not pay the
+// full loop + odd remainder + tail of its mixed nb = len >> 3 (measured form
+// before: 5.8 step-times per wave on the C4 lengths 8..64 instead of 4.9).
 RSK_DEV uint64_t murmur64a_lds(const uint8_t* p, uint32_t len) {
-  const uint32_t nb = len >> 3, t = len & 7;
+  const uint32_t steps = (len + 7) >> 3, t = len & 7;
   uint64_t h = (uint64_t)HLL_SEED ^ ((uint64_t)len * MM_M);
-  for (uint32_t j = 0; j < nb; ++j) {
-    h ^= mm_mix(lds_u64(p + 8 * j));
-    h *= MM_M;
-  }
-  if (t) {
-    h ^= lds_u64(p + 8 * nb) & ((1ULL << (8 * t)) - 1);
-    h *= MM_M;
+  if (steps) {
+    for (uint32_t j = 0; j + 1 < steps; ++j) {
+      h ^= mm_mix(lds_u64(p + 8 * j));
+      h *= MM_M;
+    }
+    const uint64_t v = lds_u64(p + 8 * (steps - 1));
+    const uint64_t x = t ? (v & ((1ULL << (8 * t)) - 1)) : mm_mix(v);
+    h = (h ^ x) * MM_M;
   }
   return mm_final(h);
 }

@@ -137,10 +137,9 @@ def test_replies_match_sort_path_c3_filter(L, engine, monkeypatch):
 @pytest.mark.gpu
 def test_c3_full_size_replies(L, engine, orc):
     """BASELINE configs[2] with the reference's add() semantics at full size:
-    1B keys in one add() call into the 9,585,058,377-bit filter (k = 7, two
-    chunks of < 2^32 probes); 200,000 sampled replies equal the oracle's
-    (exact minimum sequence number over the whole stream for the sample's
-    bits), and the bit string equals the reply-less insert's."""
+    1B keys in one add() call into the 9,585,058,377-bit filter (k = 7, one
+    chunk); 200,000 sampled replies equal the oracle's (exact minimum
+    sequence number over the whole stream for the sample's bits), and the bit string equals the reply-less insert's."""
     import os
 
     from redisson_amd import _lib, devmem
