@@ -92,7 +92,9 @@ __global__ __launch_bounds__(256) void rp_size_kernel(const uint16_t* __restrict
 // the group's starts), ranked by block with an LDS atomic, placed in an LDS
 // image and written contiguously at the slice's region with a header
 // h3[tile][0..32] (block starts) and its position tb3[tile].  Padding records
-// (low word INVALID) are dropped.
+// (low word INVALID) are dropped.  The round's barriers order LDS only
+// (lds_barrier): a wave's record loads and tile stores stay in flight across
+// them (no global data is shared inside the workgroup).
 __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__ in, const uint16_t* __restrict__ h2t,
                                                     uint64_t row_stride, uint32_t f2, const uint64_t* __restrict__ tb2,
                                                     const uint32_t* __restrict__ tile_off,
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
           const uint32_t c1 = e > r0 ? min(RP3_CHUNKS, (e - r0 + 63) >> 6) : 0;
           for (uint32_t cc = c0; cc < c1; ++cc) tbl[cc] = (uint16_t)threadIdx.x;
         }
-        __syncthreads();
+        lds_barrier();
         uint64_t rec[RP3_PER];
         uint32_t tag[RP3_PER];
 #pragma unroll
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
             tag[m] = (blk << 16) | atomicAdd(&hist[blk], 1u);
           }
         }
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x < 64) {
           const uint32_t lane = threadIdx.x;
           const uint32_t v = lane < RB_PER_SL ? hist[lane] : 0;
@@ -179,17 +181,17 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
             lstart[RB_PER_SL] = tot;
           }
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (uint32_t m = 0; m < RP3_PER; ++m)
           if (tag[m] != INVALID) img[lstart[tag[m] >> 16] + (tag[m] & 0xFFFFu)] = rec[m];
         const uint32_t kept = lstart[RB_PER_SL];
-        __syncthreads();
+        lds_barrier();
         uint64_t* o = out + base + written;
         for (uint32_t j = threadIdx.x; j < kept; j += RP3_T) __builtin_nontemporal_store(img[j], o + j);
         written += kept;
         ++nt3;
-        __syncthreads();  // img and lstart are rewritten by the next round
+        lds_barrier();  // img and lstart are rewritten by the next round
       }
     }
   }
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
     uint4* m4 = reinterpret_cast<uint4*>(ms);
     for (uint32_t q = threadIdx.x; q < RB_BITS / 4; q += RA_T) m4[q] = make_uint4(NONE, NONE, NONE, NONE);
     for (uint32_t q = threadIdx.x; q < RB_WORDS; q += RA_T) f0[q] = wbase + q < nwords ? bits[wbase + q] : 0u;
-    __syncthreads();
+    lds_barrier();
     const uint32_t s = (uint32_t)(b / RB_PER_SL), sub = (uint32_t)(b % RB_PER_SL);
     const uint32_t t0 = tile3_off[s], nt = ntile3[s];
     for (uint32_t j = w; j < nt; j += NW) {
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
           if (rec_off(r[u]) != INVALID) atomicMin(&ms[rec_off(r[u]) & (RB_BITS - 1)], (uint32_t)(r[u] >> 32));
       }
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t* fkb = fk + b * RB_BITS;
     for (uint32_t o = threadIdx.x; o < RB_BITS; o += RA_T) {  // a wave covers 64 bits = words o/32, o/32 + 1
       const uint32_t v = ms[o];
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
         if (wbase + word < nwords) bits[wbase + word] = f0[word] | msk;
       }
     }
-    __syncthreads();  // ms / f0 are reset for the next block
+    lds_barrier();  // ms / f0 are reset for the next block
   }
 }
 

@@ -408,7 +408,7 @@ __global__ __launch_bounds__(TA, 8) void bloom_sa_apply_kernel(const uint32_t* _
     uint4* g4 = reinterpret_cast<uint4*>(bits + w0);
     uint4* l4 = reinterpret_cast<uint4*>(sl);
     for (uint32_t q = threadIdx.x; q < nw4; q += TA) l4[q] = g4[q];
-    __syncthreads();
+    lds_barrier();  // LDS only: the previous slice's write-back stays in flight
     const uint32_t c = s >> f2, f = s & ((1u << f2) - 1);
     const uint16_t* ra = ht + (uint64_t)f * row_stride;
     const uint16_t* rb = ra + row_stride;
@@ -461,9 +461,9 @@ __global__ __launch_bounds__(TA, 8) void bloom_sa_apply_kernel(const uint32_t* _
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t q = threadIdx.x; q < nw4; q += TA) g4[q] = l4[q];
-    __syncthreads();
+    lds_barrier();
   }
 }
 
