@@ -329,7 +329,10 @@ RSK_DEV uint64_t var_hash(bool staged, const uint64_t* st, uint32_t off, const u
 }
 
 // KPL keys per lane, 512 / KPL lanes; 3 workgroups per CU (LDS ~50 KiB each).
-template <int KPL>
+// DIAG (rsk_diag_hll_var_variant only): bit 0 replaces MurmurHash64A by one
+// 8-byte read of the key, bit 1 skips the register update (XOR-folded into a
+// slab byte instead): the cost of the rest of the kernel without them.
+template <int KPL, int DIAG = 0>
 __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_add_var_staged_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint64_t n, uint64_t per_block,
     uint8_t* __restrict__ slabs) {
@@ -346,6 +349,7 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
   const uint64_t end = begin + per_block < n ? begin + per_block : n;
   const uintptr_t dbase = reinterpret_cast<uintptr_t>(data);
   const uint8_t* st8 = reinterpret_cast<const uint8_t*>(stage);
+  uint64_t diag_acc = 0;
 
   // Tile state, one tile ahead.  The stage window starts at the 16-byte-
   // aligned ADDRESS at or below the tile's first byte, so no chunk load
@@ -365,7 +369,11 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const uint32_t c = tid + (uint32_t)u * T;
-      if (c < nchunk) pf[u] = ld_nt16(reinterpret_cast<const uint4*>(a0) + c);
+      // addressed from `data` (a global kernel argument), not from the integer
+      // a0: a pointer rebuilt from an integer is generic, and its flat loads
+      // count in lgkmcnt, so every LDS-only barrier of the tile would wait
+      // for this prefetch
+      if (c < nchunk) pf[u] = ld_nt16(reinterpret_cast<const uint4*>(data + (a0 - dbase)) + c);
     }
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
@@ -428,19 +436,37 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
       lds_barrier();  // [D]
       if (tid < VAR_NCLS_PAD) cnt[tid] = 0;
       const uint32_t nvalid = cbase[VAR_NONE];
-      uint32_t o[KPL], l[KPL];
+      uint32_t o[KPL], l[KPL], pos[KPL];
 #pragma unroll
       for (int q = 0; q < KPL; ++q) {
-        const uint32_t pos = tid * KPL + q;  // adjacent sorted keys: one class per lane, nearly
-        const uint32_t p = pos < nvalid ? perm[pos] : 0u;
+        // adjacent sorted keys: one class per lane, nearly.  With one key per
+        // lane, wave w takes sorted chunk w (w < 4) or 11 - w, so the two waves
+        // a SIMD holds (w, w + 4) get a short and a long chunk: the SIMDs
+        // finish a tile together instead of the one with the longest keys
+        // holding the workgroup at the next barrier.
+        if constexpr (KPL == 1 && T == 512) {
+          const uint32_t w = tid >> 6;
+          pos[q] = (w < 4 ? w : 11 - w) * 64 + (tid & 63);
+        } else {
+          pos[q] = tid * KPL + q;
+        }
+        const uint32_t p = pos[q] < nvalid ? perm[pos[q]] : 0u;
         o[q] = p & 0xFFFFu;
         l[q] = p >> 16;
       }
       uint64_t h[KPL];
-      murmur64a_lds_multi<KPL>(st8, o, l, h);
+      if constexpr (DIAG & 1) {
+#pragma unroll
+        for (int q = 0; q < KPL; ++q) h[q] = lds_u64(st8 + o[q]) ^ l[q];
+      } else {
+        murmur64a_lds_multi<KPL>(st8, o, l, h);
+      }
 #pragma unroll
       for (int q = 0; q < KPL; ++q)
-        if (tid * KPL + q < nvalid) hll_update8(regs32, h[q]);
+        if (pos[q] < nvalid) {
+          if constexpr (DIAG & 2) diag_acc ^= h[q];
+          else hll_update8(regs32, h[q]);
+        }
     } else {
 #pragma unroll
       for (int q = 0; q < KPL; ++q)
@@ -450,6 +476,7 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
   }
   __syncthreads();
   lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+  if constexpr ((DIAG & 2) != 0) slabs[(uint64_t)blockIdx.x * HLL_REGS + tid] = (uint8_t)(diag_acc % 51);
 }
 
 // The round-1 form (no prefetch, no sort): the A/B baseline of the diag.
@@ -475,7 +502,7 @@ __global__ __launch_bounds__(VAR_T) void hll_add_var_simple_kernel(const uint8_t
     __syncthreads();  // previous tile's stage reads are done
     if (staged) {
       const uint32_t nchunk = (uint32_t)((span + 15) >> 4);
-      const uint4* src = reinterpret_cast<const uint4*>(a0);
+      const uint4* src = reinterpret_cast<const uint4*>(data + (a0 - dbase));
       uint4* dst = reinterpret_cast<uint4*>(stage);
       for (uint32_t c = threadIdx.x; c < nchunk; c += VAR_T) dst[c] = ld_nt16(src + c);
     }
@@ -508,6 +535,12 @@ void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const 
     case 2: hipLaunchKernelGGL(hll_add_var_simple_kernel, g, dim3(VAR_T), 0, c->stream, data, offsets, n, per_block,
                                c->d_slab); break;
     case 3: hipLaunchKernelGGL(hll_add_var_staged_kernel<4>, g, dim3(VAR_TILE / 4), 0, c->stream, data, offsets, n,
+                               per_block, c->d_slab); break;
+    case 4: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 1>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
+                               per_block, c->d_slab); break;
+    case 5: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 2>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
+                               per_block, c->d_slab); break;
+    case 6: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 3>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
                                per_block, c->d_slab); break;
     default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
   }

@@ -1,6 +1,7 @@
 """C4 (blob+offsets) PFADD kernel variants on the C4 stream, interleaved
 rounds in one process: 0 production (step-count sort, 1 key per lane),
-1 sorted, 2 keys per lane, 2 round-1 form, 3 sorted, 4 keys per lane.   python scripts/var_variants.py OUT.json [n]"""
+1 sorted, 2 keys per lane, 2 round-1 form, 3 sorted, 4 keys per lane; diagnostics of
+the production kernel: 4 without MurmurHash64A, 5 without the register update, 6 without either.   python scripts/var_variants.py OUT.json [n]"""
 import ctypes
 import json
 import os
@@ -12,7 +13,8 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
-NAMES = {0: "sorted_1_per_lane", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane"}
+NAMES = {0: "sorted_1_per_lane", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane",
+         4: "diag_trivial_hash", 5: "diag_no_update", 6: "diag_trivial_hash_no_update"}
 
 
 def main():
