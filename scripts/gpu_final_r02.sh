@@ -2,7 +2,8 @@
 # Round-2 end-of-round GPU session on the final tree: parity suite, smoke, the
 # bench workloads, rocprofv3 kernel trace of the headline bench (agreement of
 # the trace with the bench's own HIP-event roofline), and separate PMC passes
-# (FETCH_SIZE, WRITE_SIZE) at the bench's own configuration.  Each GPU step has
+# (FETCH_SIZE, WRITE_SIZE) at the bench's own configuration; the same for the
+# Bloom add()-with-replies pipeline alone (PART=replies).  Each GPU step has
 # its own limit; the first failure ends the script.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -36,5 +37,18 @@ if [ "$PART" = all ] || [ "$PART" = prof ]; then
     '{"workload": "c5", "keys": 500000000, "zipf": 0.0, "bloom_keys": 0}'
   find gpurun_out/prof_stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_kernel_stats.csv \;
   find gpurun_out/prof5_stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_c5_kernel_stats.csv \;
+fi
+if [ "$PART" = all ] || [ "$PART" = prof ] || [ "$PART" = replies ]; then
+  # add() with replies alone in its process (its sa1/sa2 instances share the
+  # insert's kernel names)
+  R="python3 scripts/reply_profile.py 1000000000 2"
+  rm -rf gpurun_out/profr_stats gpurun_out/pmcr_fetch gpurun_out/pmcr_write
+  step reply_bench 200 $R || exit 1
+  step profr 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profr_stats -o run -- $R || exit 1
+  step pmcr_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcr_fetch -o run -- $R || exit 1
+  step pmcr_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcr_write -o run -- $R || exit 1
+  python3 scripts/pmc_summary.py gpurun_out/profr_stats gpurun_out/pmcr_fetch gpurun_out/pmcr_write gpurun_out/${TAG}_pmc_replies 1000000000 \
+    '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}'
+  find gpurun_out/profr_stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_replies_kernel_stats.csv \;
 fi
 exit 0
