@@ -145,14 +145,17 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
         lds_barrier();
         uint64_t rec[RP3_PER];
         uint32_t tag[RP3_PER];
+        // two records per lane and load: segments start at even records of
+        // 16-byte aligned tiles and have even lengths (sa2 pads runs), so a
+        // pair never straddles two segments
 #pragma unroll
-        for (uint32_t m = 0; m < RP3_PER; ++m) {
-          const uint32_t i = r0 + m * RP3_T + threadIdx.x;
-          rec[m] = rec_pad<uint64_t>();
+        for (uint32_t m = 0; m < RP3_PER / 2; ++m) {
+          const uint32_t i = r0 + 2 * (m * RP3_T + threadIdx.x);
+          rec[2 * m] = rec[2 * m + 1] = rec_pad<uint64_t>();
           if (i < total) {
             uint32_t j = tbl[(i - r0) >> 6];  // then forward over the (few) segments of the chunk
             while (s_pre[j + 1] <= i) ++j;
-            rec[m] = __builtin_nontemporal_load(in + s_pos[j] + (i - s_pre[j]));
+            unpack16<uint64_t>(ld_nt16(in + s_pos[j] + (i - s_pre[j])), rec + 2 * m);
           }
         }
 #pragma unroll
