@@ -219,16 +219,26 @@ __global__ __launch_bounds__(PT) void bloom_part1_kernel(const uint8_t* __restri
 // or HLL records as they are).  Workgroup w takes the units whose start falls
 // in its equal share of the buffer, re-sorts each unit by slice (2^f2 bins)
 // and appends slice s's run at off2[s * G + b] (b = the unit's first block).
+// With a unit table (ustart != nullptr, the grouped PFADD): unit v starts at
+// part1 block ustart[v] (linear c * G + b, ascending, [nunits] = the end) and
+// nunits is read from d_nunits -- units of one part1 block in buckets whose
+// runs would otherwise make units far above a workgroup's share (skewed groups).
 __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restrict__ in,
                                                          const uint32_t* __restrict__ off1,
                                                          const uint32_t* __restrict__ off2, uint32_t G,
-                                                         uint32_t GU, uint32_t nunits, uint32_t f2, uint32_t nslices,
-                                                         uint32_t bin_shift, uint32_t pay_mask,
+                                                         uint32_t GU, uint32_t nunits_arg, uint32_t f2,
+                                                         uint32_t nslices, uint32_t bin_shift, uint32_t pay_mask,
+                                                         const uint32_t* __restrict__ ustart,
+                                                         const uint32_t* __restrict__ d_nunits,
                                                          uint32_t* __restrict__ out) {
   __shared__ SortLds<TILE2> L;
   __shared__ uint32_t range[2];
-  const uint32_t NB = G / GU;  // units per coarse bucket
-  auto ust = [&](uint32_t v) { return off1[(uint64_t)(v / NB) * G + (v % NB) * GU]; };  // v == nunits: sentinel
+  const uint32_t NB = G / GU;  // units per coarse bucket (no unit table)
+  const uint32_t nunits = ustart ? *d_nunits : nunits_arg;
+  auto ublock = [&](uint32_t v) -> uint64_t {  // linear first part1 block of unit v (v == nunits: the end)
+    return ustart ? (uint64_t)ustart[v] : (uint64_t)(v / NB) * G + (v % NB) * GU;
+  };
+  auto ust = [&](uint32_t v) { return off1[ublock(v)]; };
   const uint32_t total = ust(nunits);
   if (threadIdx.x < 2) {  // first unit starting at or after a share boundary
     const uint64_t edge = (uint64_t)total * (blockIdx.x + threadIdx.x) / gridDim.x;
@@ -278,7 +288,8 @@ __global__ __launch_bounds__(PT) void bloom_part2_kernel(const uint32_t* __restr
     fetch(u, j);
     __syncthreads();
     if (cu != loaded_unit) {  // new unit: its slice cursors
-      const uint32_t c = cu / NB, b = (cu - c * NB) * GU;
+      const uint64_t lb = ublock(cu);
+      const uint32_t c = (uint32_t)(lb / G), b = (uint32_t)(lb - (uint64_t)c * G);
       const uint32_t s = (c << f2) + threadIdx.x;
       if (threadIdx.x < nb && s < nslices) L.cur[threadIdx.x] = off2[(uint64_t)s * G + b];
       loaded_unit = cu;
@@ -424,7 +435,8 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
     if (f2) {
       ProfScope ps(c, "bloom_part2");
       hipLaunchKernelGGL(bloom_part2_kernel, dim3(p2_grid), dim3(PT), 0, c->stream, buf_a, off1, off2, G,
-                         1u, nbins1 * G, f2, ns, (uint32_t)SLICE_LOG, (1u << SLICE_LOG) - 1, buf_b);
+                         1u, nbins1 * G, f2, ns, (uint32_t)SLICE_LOG, (1u << SLICE_LOG) - 1,
+                         (const uint32_t*)nullptr, (const uint32_t*)nullptr, buf_b);
       RSK_CHECK_LAUNCH("bloom_part2");
     }
     {
@@ -441,9 +453,9 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
 // part2 for other callers (the grouped PFADD, rsk_hll_group.hip).
 void part2_launch(rsk_ctx* c, uint32_t grid, const uint32_t* in, const uint32_t* off1, const uint32_t* off2,
                   uint32_t G, uint32_t GU, uint32_t nunits, uint32_t f2, uint32_t nslices, uint32_t bin_shift,
-                  uint32_t pay_mask, uint32_t* out) {
+                  uint32_t pay_mask, const uint32_t* ustart, const uint32_t* d_nunits, uint32_t* out) {
   hipLaunchKernelGGL(bloom_part2_kernel, dim3(grid), dim3(PT), 0, c->stream, in, off1, off2, G, GU, nunits, f2,
-                     nslices, bin_shift, pay_mask, out);
+                     nslices, bin_shift, pay_mask, ustart, d_nunits, out);
 }
 
 }  // namespace rsk

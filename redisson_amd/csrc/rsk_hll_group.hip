@@ -118,6 +118,38 @@ __global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restr
   cnt2[((uint64_t)c * PT + threadIdx.x) * G1 + b] = h[threadIdx.x];
 }
 
+// part2 units: GU part1 blocks each, or one block each in a coarse bin whose
+// GU-block units would be above a quarter of a part2 workgroup's share of the
+// records (skewed groups: Zipf(1.1) puts ~60 % of all pairs into bin 0, whose
+// GU-block units were ten shares each).  One workgroup; lane c = bin c.
+__global__ __launch_bounds__(PT) void hll_gunits_kernel(const uint32_t* __restrict__ off1, uint32_t G1, uint32_t GU,
+                                                        uint32_t nbins1, uint32_t p2_grid,
+                                                        uint32_t* __restrict__ ustart, uint32_t* __restrict__ d_nunits) {
+  __shared__ uint32_t cnt[PT];
+  const uint32_t c = threadIdx.x;
+  const uint64_t total = off1[(uint64_t)nbins1 * G1];
+  uint32_t gu = GU, n = 0;
+  if (c < nbins1) {
+    const uint64_t r = off1[(uint64_t)(c + 1) * G1] - off1[(uint64_t)c * G1];
+    if (r * GU > (uint64_t)G1 * (total / (4ull * p2_grid) + 1)) gu = 1;
+    n = G1 / gu;
+  }
+  cnt[c] = n;
+  __syncthreads();
+  if (c == 0) {  // exclusive prefix over <= 256 bins
+    uint32_t run = 0;
+    for (uint32_t i = 0; i < PT; ++i) {
+      const uint32_t v = cnt[i];
+      cnt[i] = run;
+      run += v;
+    }
+    ustart[run] = nbins1 * G1;
+    *d_nunits = run;
+  }
+  __syncthreads();
+  for (uint32_t q = 0; q < n; ++q) ustart[cnt[c] + q] = c * G1 + q * gu;
+}
+
 // A fine bin's records beyond its first GP_CH go to hll_gapply_extra (skewed
 // groups, e.g. the Zipf(1.1) C5 variant, put a third of all pairs into one
 // bin: one workgroup would otherwise walk them alone).
@@ -332,7 +364,8 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt2, c->stream);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   const uint32_t xcap = (uint32_t)(GP_NP * (chunk / GP_CH + 1) + 16);  // extra work items per chunk, at most
-  const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1));
+  const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1)) +
+                        al(4 * (ncnt1 + 1));
   uint8_t* w = c->work(meta + 2 * al(4 * max_np));
   uint32_t* cnt1 = reinterpret_cast<uint32_t*>(w);
   uint32_t* off1 = reinterpret_cast<uint32_t*>(w + al(4 * ncnt1));
@@ -341,6 +374,8 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   void* scan_tmp = w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2);
   uint32_t* xlist = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)));
   uint32_t* xcount = xlist + xcap;
+  uint32_t* ustart = reinterpret_cast<uint32_t*>(w + meta - al(4 * (ncnt1 + 1)));  // part2 units + [ncnt1]: count
+  uint32_t* d_nunits = ustart + ncnt1;
   uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta);
   uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np));
   for (uint64_t first = 0; first < keys.n; first += chunk) {
@@ -366,7 +401,11 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       hipLaunchKernelGGL(hll_gcount2_kernel, dim3(nbins1 * G1), dim3(PT), 0, c->stream, buf_a, off1, G1, cnt2);
       RSK_CHECK_LAUNCH("hll_gcount2");
       RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, off2, (int)ncnt2, c->stream));
-      part2_launch(c, p2_grid, buf_a, off1, off2, G1, GU, nbins1 * (G1 / GU), 8u, nfine, 24u, 0xFFFFFFFFu, buf_b);
+      hipLaunchKernelGGL(hll_gunits_kernel, dim3(1), dim3(PT), 0, c->stream, off1, G1, GU, nbins1, p2_grid, ustart,
+                         d_nunits);
+      RSK_CHECK_LAUNCH("hll_gunits");
+      part2_launch(c, p2_grid, buf_a, off1, off2, G1, GU, nbins1 * (G1 / GU), 8u, nfine, 24u, 0xFFFFFFFFu, ustart,
+                   d_nunits, buf_b);
       RSK_CHECK_LAUNCH("hll_gpart2");
     }
     {
