@@ -235,7 +235,10 @@ __global__ __launch_bounds__(1024) void st_offsets_kernel(const uint64_t* __rest
 // st2, whose output the apply kernel reads unchanged.  A sub-region that
 // overflows (only adversarial inputs: 1.25x the expected share per
 // workgroup) sets `overflow`; the chunk is redone.
-constexpr int SA2_V = 3;            // sa2: uint4 loads per lane per tile (u32: 96 probes per fine bin: apply's 2 x 64 fast path)
+#ifndef RSK_SA2_V
+#define RSK_SA2_V 3
+#endif
+constexpr int SA2_V = RSK_SA2_V;    // sa2: uint4 loads per lane per tile (u32: 96 probes per fine bin: apply's 2 x 64 fast path)
 constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
 template <class R>
 constexpr uint32_t sa2_slots() { return SA2_T * SA2_V * (16 / sizeof(R)); }
