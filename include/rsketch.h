@@ -173,9 +173,11 @@ int rsk_bloom_init(rsk_ctx *ctx, int64_t expected_insertions, double false_proba
 int rsk_bloom_destroy(rsk_bloom *b);
 int rsk_bloom_info(const rsk_bloom *b, int64_t *size, int32_t *k);
 /* add(obj) for n objects in input order (RedissonBloomFilter.java:80-114).
- * added_out (host, may be NULL) gets each add's reply: 1 iff one of the
- * first k-1 SETBITs found its bit clear, exactly as if the adds ran one by
- * one in input order. */
+ * added_out (may be NULL; host memory for RSK_MEM_HOST batches, device memory
+ * for RSK_MEM_DEVICE ones) gets each add's reply: 1 iff one of the first k-1
+ * SETBITs found its bit clear, exactly as if the adds ran one by one in input
+ * order.  Large batches answer through the first-key partition pipeline
+ * (DESIGN.md section 3), small ones through a sort of (bit, sequence). */
 int rsk_bloom_add(rsk_bloom *b, const rsk_keys *keys, uint8_t *added_out);
 /* contains(obj) for n objects (RedissonBloomFilter.java:133-168): 1 iff the
  * first k-1 bits are all set.  out is a host array of n bytes. */
