@@ -493,7 +493,7 @@ def main():
             ir = result["bloom"]["insert_roofline"]
             ir["traffic"] = tr["bytes"]
             ir["traffic_source"] = tr["source"]
-            ir["traffic_GBps"] = tr["bytes"] / (ir["algorithmic_bytes"] / ir["achieved"]) / 1e9
+            ir["traffic_GBps"] = tr["bytes"] * ir["achieved"] / ir["algorithmic_bytes"]  # traffic / insert time
     if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes, thr)
