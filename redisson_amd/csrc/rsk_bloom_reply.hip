@@ -53,6 +53,9 @@ constexpr uint32_t RP3_GROUP = RP3_T;                 // sa2 tiles per rp3 group
 constexpr uint32_t RA_T = 1024;                       // rp_apply workgroup
 constexpr uint64_t MAX_CHUNK_KEYS = 0xFFFFFFFEull;    // key indices < NONE
 constexpr uint64_t DEFAULT_CHUNK_PROBES = 1ull << 33;  // scratch bound: ~2.3 x 8 B per probe
+#ifndef RSK_RP_U
+#define RSK_RP_U 2  // rp_reply: keys (gather chains) per lane
+#endif
 
 // ------------------------------------------------------------------ sizing
 // Slice s = blockIdx.x: its records in the sa2 tiles of coarse bin s >> f2
@@ -470,7 +473,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp_reply");
-      constexpr int U = 2;
+      constexpr int U = RSK_RP_U;
       const uint64_t g = (m + 256 * U - 1) / (256 * U);
       const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
       if (f16)
