@@ -135,7 +135,11 @@ int rsk_hll_count_union_batch(rsk_hll *h, const uint64_t *member_ids, uint32_t a
 /* PFMERGE dst src1..srck (dst included in the max) --
  * RedissonHyperLogLog.mergeWith/mergeWithAsync (:60-63,:91-97). */
 int rsk_hll_merge(rsk_hll *dst, uint64_t dst_id, rsk_hll *const *srcs, const uint64_t *src_ids, uint32_t k);
-/* Batched mergeWith within one pool: for i < n, PFMERGE dst_ids[i] src_ids[i]. */
+/* Batched mergeWith within one pool: for i < n, PFMERGE dst_ids[i] src_ids[i],
+ * in input order.  PFMERGE has no reply, so the call returns once the merges
+ * are queued on the context's stream (mergeWithAsync): every later call is
+ * ordered after them, and a device fault would surface at the next call that
+ * waits for the device. */
 int rsk_hll_merge_batch(rsk_hll *h, const uint64_t *dst_ids, const uint64_t *src_ids, uint64_t n);
 
 /* PFMERGE from raw registers (one byte per register, any location): the

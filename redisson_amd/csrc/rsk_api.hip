@@ -94,6 +94,25 @@ uint8_t* rsk_ctx::work(uint64_t bytes) {
   return d_work;
 }
 
+uint8_t* rsk_ctx::pinned(uint64_t bytes) {
+  if (batch_pending) {  // an earlier call's DMA may still read the buffer
+    RSK_HIP(hipEventSynchronize(batch_ev));
+    batch_pending = false;
+  }
+  if (bytes > h_batch_bytes) {
+    if (h_batch) {
+      RSK_HIP(hipStreamSynchronize(stream));
+      RSK_HIP(hipHostFree(h_batch));
+      h_batch = nullptr;
+      h_batch_bytes = 0;
+    }
+    const uint64_t sz = std::max<uint64_t>(bytes, 4ull << 20);
+    RSK_HIP(hipHostMalloc(&h_batch, sz, hipHostMallocDefault));
+    h_batch_bytes = sz;
+  }
+  return h_batch;
+}
+
 namespace {
 
 using namespace rsk;
@@ -513,6 +532,8 @@ int rsk_shutdown(rsk_ctx* c) {
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_small);
     (void)hipHostFree(c->h_small);
+    if (c->h_batch) (void)hipHostFree(c->h_batch);
+    if (c->batch_ev) (void)hipEventDestroy(c->batch_ev);
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_lc);
     auto it = g_out.find(c);
@@ -809,14 +830,19 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
 }
 
 namespace {
-void union_impl(rsk_ctx* c, const std::vector<const uint8_t*>& ptrs, uint32_t arity, uint64_t n, uint64_t* out) {
-  uint8_t* s = out_scratch(c, ptrs.size() * 8 + n * 8 + 512);
+// ptrs: n * arity member pointers, in pinned host memory (rsk_ctx::pinned)
+// with n * 8 bytes after them for the results.
+void union_impl(rsk_ctx* c, const uint8_t* const* ptrs, uint32_t arity, uint64_t n, uint64_t* out) {
+  const uint64_t np = n * arity;
+  uint8_t* s = out_scratch(c, np * 8 + n * 8 + 512);
   auto* d_ptrs = reinterpret_cast<const uint8_t**>(s);
-  auto* d_out = reinterpret_cast<uint64_t*>(s + ((ptrs.size() * 8 + 255) & ~255ull));
-  RSK_HIP(hipMemcpyAsync(d_ptrs, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice, c->stream));
+  auto* d_out = reinterpret_cast<uint64_t*>(s + ((np * 8 + 255) & ~255ull));
+  uint64_t* h_out = const_cast<uint64_t*>(reinterpret_cast<const uint64_t*>(ptrs + np));
+  RSK_HIP(hipMemcpyAsync(d_ptrs, ptrs, np * 8, hipMemcpyHostToDevice, c->stream));
   hll_union_count_launch(c, d_ptrs, arity, n, d_out);
-  RSK_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
+  RSK_HIP(hipMemcpyAsync(h_out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
   RSK_HIP(hipStreamSynchronize(c->stream));
+  std::memcpy(out, h_out, n * 8);
 }
 }  // namespace
 
@@ -825,7 +851,7 @@ int rsk_hll_count_union(rsk_hll* const* hs, const uint64_t* ids, uint32_t k, uin
     need(hs && ids && out && k >= 1, "bad arguments");
     rsk_ctx* c = hs[0]->ctx;
     CtxLock l(c);
-    std::vector<const uint8_t*> ptrs(k);
+    auto* ptrs = reinterpret_cast<const uint8_t**>(c->pinned(8ull * k + 8));
     for (uint32_t a = 0; a < k; ++a) {
       check_hll(hs[a], ids[a]);
       need(hs[a]->ctx == c, "all sketches must share one context");
@@ -840,12 +866,13 @@ int rsk_hll_count_union_batch(rsk_hll* h, const uint64_t* member_ids, uint32_t a
     need(h && member_ids && out && arity >= 1, "bad arguments");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    std::vector<const uint8_t*> ptrs(n * arity);
+    if (n == 0) return;
+    auto* ptrs = reinterpret_cast<const uint8_t**>(c->pinned(8ull * n * arity + 8ull * n));
     for (uint64_t i = 0; i < n * arity; ++i) {
       check_hll(h, member_ids[i]);
       ptrs[i] = h->exists[member_ids[i]] ? regs_of(h, member_ids[i]) : nullptr;
     }
-    if (n) union_impl(c, ptrs, arity, n, out);
+    union_impl(c, ptrs, arity, n, out);
   });
 }
 
@@ -884,81 +911,82 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     if (n == 0) return;
-    std::vector<uint8_t*> dp(n);
-    std::vector<const uint8_t*> sp(n);
     for (uint64_t i = 0; i < n; ++i) {
       check_hll(h, dst_ids[i]);
       check_hll(h, src_ids[i]);
-      sp[i] = h->exists[src_ids[i]] ? regs_of(h, src_ids[i]) : nullptr;
-      h->exists[dst_ids[i]] = 1;
-      h->dense[dst_ids[i]] = 1;
-      dp[i] = regs_of(h, dst_ids[i]);
     }
     // PFMERGEs run in input order in Redis; a batch whose destinations are
     // also sources of other pairs depends on that order.  Level the pairs:
     // a pair runs after the last writer of its source (RAW) and of its
     // destination (WAW), and after the last reader of its destination (WAR).
     // Pairs of one level are independent and run as one launch.
-    // Per-sketch last writer / last reader levels live in flat per-pool
-    // arrays, reset lazily by an epoch stamp (no hashing, no clearing).
-    if (h->lv_stamp.size() != h->n) {
-      h->lv_stamp.assign(h->n, 0);
-      h->lv_w.assign(h->n, 0);
-      h->lv_r.assign(h->n, 0);
+    // Per-sketch last writer / last reader levels live in one flat per-pool
+    // array, reset lazily by an epoch stamp (no hashing, no clearing).
+    if (h->lv.size() != h->n) {
+      h->lv.assign(h->n, rsk_hll::Level{0, 0, 0});
       h->lv_epoch = 0;
     }
     if (++h->lv_epoch == 0) {
-      std::fill(h->lv_stamp.begin(), h->lv_stamp.end(), 0);
+      for (auto& e : h->lv) e.stamp = 0;
       h->lv_epoch = 1;
     }
     const uint32_t ep = h->lv_epoch;
-    auto touch = [&](uint64_t id) {
-      if (h->lv_stamp[id] != ep) {
-        h->lv_stamp[id] = ep;
-        h->lv_w[id] = 0;
-        h->lv_r[id] = 0;
-      }
+    auto touch = [&](uint64_t id) -> rsk_hll::Level& {
+      rsk_hll::Level& e = h->lv[id];
+      if (e.stamp != ep) e = rsk_hll::Level{ep, 0, 0};
+      return e;
     };
-    std::vector<uint32_t> level(n);
+    // pinned: [dst pointers n][src pointers n][dst ids n][level n (u32)]
+    const uint64_t seg = (8 * n + 255) & ~255ull;
+    uint8_t* hb = c->pinned(3 * seg + 4 * n + 256);
+    auto* dps = reinterpret_cast<uint8_t**>(hb);
+    auto* sps = reinterpret_cast<const uint8_t**>(hb + seg);
+    auto* ids = reinterpret_cast<uint64_t*>(hb + 2 * seg);
+    auto* level = reinterpret_cast<uint32_t*>(hb + 3 * seg);
     uint32_t max_level = 0;
+    std::vector<uint8_t> src_exists(n);  // as of the pair's turn in input order
     for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t s = src_ids[i], d = dst_ids[i];
-      touch(s);
-      touch(d);
-      const uint32_t lv = std::max(std::max(h->lv_w[s], h->lv_w[d]), h->lv_r[d]) + 1;
+      const uint64_t s_ = src_ids[i], d = dst_ids[i];
+      src_exists[i] = h->exists[s_];
+      h->exists[d] = 1;
+      h->dense[d] = 1;
+      rsk_hll::Level& ls = touch(s_);
+      rsk_hll::Level& ld = touch(d);
+      const uint32_t lv = std::max(std::max(ls.w, ld.w), ld.r) + 1;
       level[i] = lv;
-      h->lv_w[d] = lv;
-      h->lv_r[s] = std::max(h->lv_r[s], lv);
+      ld.w = lv;
+      ls.r = std::max(ls.r, lv);
       max_level = std::max(max_level, lv);
     }
     std::vector<uint64_t> start(max_level + 2, 0);
     for (uint64_t i = 0; i < n; ++i) start[level[i] + 1]++;
     for (uint32_t l = 1; l <= max_level + 1; ++l) start[l] += start[l - 1];
-    std::vector<uint8_t*> dps(n);
-    std::vector<const uint8_t*> sps(n);
     {
       std::vector<uint64_t> fill(start.begin(), start.end());
       for (uint64_t i = 0; i < n; ++i) {
         const uint64_t p = fill[level[i]]++;
-        dps[p] = dp[i];
-        sps[p] = sp[i];
+        sps[p] = src_exists[i] ? regs_of(h, src_ids[i]) : nullptr;
+        dps[p] = regs_of(h, dst_ids[i]);
       }
     }
-    const uint64_t seg = (8 * n + 255) & ~255ull;
+    std::memcpy(ids, dst_ids, n * 8);
     uint8_t* s = out_scratch(c, 3 * seg + 512);
     auto* d_dst = reinterpret_cast<uint8_t**>(s);
     auto* d_src = reinterpret_cast<const uint8_t**>(s + seg);
     auto* d_ids = reinterpret_cast<uint64_t*>(s + 2 * seg);
-    RSK_HIP(hipMemcpyAsync(d_dst, dps.data(), n * 8, hipMemcpyHostToDevice, c->stream));
-    RSK_HIP(hipMemcpyAsync(d_src, sps.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemcpyAsync(d_dst, dps, 3 * seg, hipMemcpyHostToDevice, c->stream));  // pointers and ids, one DMA
+    if (!c->batch_ev) RSK_HIP(hipEventCreateWithFlags(&c->batch_ev, hipEventDisableTiming));
+    RSK_HIP(hipEventRecord(c->batch_ev, c->stream));
+    c->batch_pending = true;
     for (uint32_t l = 1; l <= max_level; ++l)
       hll_merge_launch(c, d_dst + start[l], d_src + start[l], 1, start[l + 1] - start[l]);
     // PFMERGE invalidates every destination's cache (one launch for the batch).
-    RSK_HIP(hipMemcpyAsync(d_ids, dst_ids, n * 8, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(invalidate_list_kernel, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0,
                        c->stream, h->d_card, d_ids, n);
     RSK_CHECK_LAUNCH("invalidate_list");
-    RSK_HIP(hipStreamSynchronize(c->stream));
+    // No reply (PFMERGE answers OK): the call returns with the merges queued
+    // on the context stream, which orders every later call behind them
+    // (mergeWithAsync's future completes on the next synchronising call).
   });
 }
 

@@ -86,6 +86,15 @@ struct rsk_ctx {
   // grow-on-demand device scratch for batched calls
   uint8_t* d_work = nullptr;
   uint64_t work_bytes = 0;
+  // grow-on-demand pinned host scratch: per-op arrays of batched calls
+  // (countWith / mergeWith sketch pointers) built in place and copied with
+  // one asynchronous DMA; a call that returns before its DMA has run (the
+  // reply-less rsk_hll_merge_batch) records batch_ev, and pinned() waits for
+  // it before the buffer is written again
+  uint8_t* h_batch = nullptr;
+  uint64_t h_batch_bytes = 0;
+  hipEvent_t batch_ev = nullptr;
+  bool batch_pending = false;
   // m*log(m/ez) for ez = 0..16384, computed with the host libm (Redis's log)
   double* d_lc = nullptr;
   rsk::Profiler prof;
@@ -97,6 +106,7 @@ struct rsk_ctx {
   uint32_t epoch = 0;
 
   uint8_t* work(uint64_t bytes);
+  uint8_t* pinned(uint64_t bytes);
 };
 
 struct rsk_hll {
@@ -128,8 +138,13 @@ struct rsk_hll {
   uint64_t* d_pcount = nullptr;
   uint32_t* d_pepoch = nullptr;
   mutable uint32_t pc_epoch = 1;
-  // rsk_hll_merge_batch leveling state per sketch id (valid while stamp == lv_epoch)
-  std::vector<uint32_t> lv_stamp, lv_w, lv_r;
+  // rsk_hll_merge_batch leveling state per sketch id (valid while stamp ==
+  // lv_epoch): one 12-byte record per sketch, so a pair's lookups touch one
+  // cache line per sketch instead of three
+  struct Level {
+    uint32_t stamp, w, r;
+  };
+  std::vector<Level> lv;
   uint32_t lv_epoch = 0;
 };
 
