@@ -256,12 +256,16 @@ RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads in
 // (6 waves per SIMD) share a CU; 8-byte records: 2 workgroups (73 KiB of LDS).
 // u64 records carry the key's index in the chunk (the host keeps a chunk
 // below 2^32 - 1 keys).
-template <bool FIXED16, int KMAX, int T1, class R>
-__global__ __launch_bounds__(T1, sizeof(R) == 8 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
+// DIAG (timing diagnostics only, RSK_BLOOM_SA1_DIAG; results are not a
+// filter): 1 = the key words instead of XXH64 / farmhash, 2 = also probe
+// indices by one multiply-high instead of the exact u63 remainders.
+// KPL: keys per lane (default 16 / KMAX); more keys per super-tile make every
+// bin's run longer.
+template <bool FIXED16, int KMAX, int T1, class R, int DIAG = 0, int KPL = 16 / KMAX>
+__global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
     FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
     uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow, int dbg) {
-  constexpr int KPL = 16 / KMAX;
   constexpr uint32_t KST = T1 * KPL;
   constexpr int NP = KPL * KMAX;
   constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
@@ -309,24 +313,30 @@ __global__ __launch_bounds__(T1, sizeof(R) == 8 ? 4 : (T1 == 512 ? 6 : 4)) void 
         if (FIXED16) {
           uint64_t w0, w1;
           key_words(cur[u], &w0, &w1);
-          h1 = xxh64_16(w0, w1);
-          h2 = farm_16(w0, w1);
+          if constexpr (DIAG >= 1) {
+            h1 = w0;
+            h2 = w1;
+          } else {
+            h1 = xxh64_16(w0, w1);
+            h2 = farm_16(w0, w1);
+          }
         } else {
           bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
         }
       }
-      ProbeSeq ps(h1, h2, fm);
+      ProbeSeq ps;
+      if constexpr (DIAG < 2) ps = ProbeSeq(h1, h2, fm);
 #pragma unroll
       for (int t = 0; t < KMAX; ++t) {
         const int s = u * KMAX + t;
         tag[s] = INVALID;
         pay[s] = 0;
         if (ok && t < k) {
-          const uint64_t idx = ps.idx;
+          const uint64_t idx = DIAG >= 2 ? __umul64hi(h1 + (uint64_t)t * h2, fm.d) : ps.idx;
           const uint32_t bin = (uint32_t)(idx >> shift1);
           pay[s] = rec_make<R>((uint32_t)(idx & low), key);
           tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
-          if (t + 1 < k) ps.next(t, fm);
+          if (DIAG < 2 && t + 1 < k) ps.next(t, fm);
         }
       }
     }

@@ -508,7 +508,8 @@ uint32_t nbits(uint64_t v) {  // bits needed to hold v (0 -> 0)
 
 // The append pipeline (sa1 -> sa2 -> apply) for filters of more than 256 slices.
 bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, uint32_t kmax, uint32_t t1,
-                      uint64_t kst, uint32_t f2, uint32_t shift1, uint32_t nb1, uint32_t P, uint64_t chunk) {
+                      uint64_t kst, uint32_t f2, uint32_t shift1, uint32_t nb1, uint32_t P, uint64_t chunk,
+                      bool kpl4) {
   const uint64_t k = (uint64_t)b->k;
   const uint32_t ns = (uint32_t)(((uint64_t)b->size + (1ull << SL_LOG) - 1) >> SL_LOG);
   const uint32_t nb2 = 1u << f2;
@@ -525,7 +526,7 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   // torch's comgr and answers 1 (scripts/occ_probe.py), a third of the grid.
   // sa1<512>: __launch_bounds__(512, 6) caps it at 80 VGPRs (6 waves per
   // SIMD), 43 KiB of LDS -> 3; sa1<1024>: 78 KiB of LDS, 4 waves per SIMD -> 1.
-  const int per_cu = t1 == 512 ? 3 : 1;
+  const int per_cu = kpl4 ? 2 : (t1 == 512 ? 3 : 1);  // KPL 4: 73 KiB of LDS
   // W persistent sa1 workgroups; each gets 1.25x its expected share of a full
   // coarse bin per bin, plus one whole super-tile (a tile's run can be that
   // long) and the <= 3 padding slots per run of each of its tiles.
@@ -575,11 +576,17 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     RSK_HIP(hipMemsetAsync(overflow, 0, 4, c->stream));
     {
       ProfScope ps(c, "bloom_st1");
-#define RSK_SA1(F16, KM, TT)                                                                                    \
-  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, TT, uint32_t>), dim3(Wc), dim3(TT), 0, c->stream, dk.data, dk.offsets,    \
+#define RSK_SA1(F16, KM, TT, ...)                                                                               \
+  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, TT, uint32_t, ##__VA_ARGS__>), dim3(Wc), dim3(TT), 0, c->stream, dk.data, dk.offsets,    \
                      dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, overflow,    \
                      (int)(dbg & 1))
-      if (t1 == 1024) {
+      const uint32_t diag = env_u32("RSK_BLOOM_SA1_DIAG", 0);  // timing diagnostics (not a filter)
+      if (kpl4) {
+        RSK_SA1(true, 8, 512, 0, 4);
+      } else if (diag && f16 && kmax == 8 && t1 == 512) {
+        if (diag == 1) RSK_SA1(true, 8, 512, 1);
+        else RSK_SA1(true, 8, 512, 2);
+      } else if (t1 == 1024) {
         if (f16 && kmax == 8) RSK_SA1(true, 8, 1024);
         else if (f16) RSK_SA1(true, 16, 1024);
         else if (kmax == 8) RSK_SA1(false, 8, 1024);
@@ -677,7 +684,15 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t ncp = nb1 * P;
   uint64_t chunk = std::max<uint64_t>(1, probe_chunk() / k / kst) * kst;  // keys per chunk, whole super-tiles
   chunk = std::min<uint64_t>(chunk, keys.n);
-  if (f2 && env_u32("RSK_BLOOM_SA", 1)) return bloom_add_append(c, b, keys, f16, kmax, t1, kst, f2, shift1, nb1, P, chunk);
+  if (f2 && env_u32("RSK_BLOOM_SA", 1)) {
+    // 16-byte keys, k <= 8: 4 keys per lane (2048-key super-tiles, bin runs
+    // twice as long; 2 workgroups per CU): insert 36.0 -> 35.3 ms at C3, sa2
+    // and apply gaining from the longer runs (RSK_BLOOM_SA1_KPL=2: 2 per lane)
+    const bool kpl4 = f16 && kmax == 8 && t1 == 512 && env_u32("RSK_BLOOM_SA1_KPL", 4) == 4;
+    const uint64_t kst_a = kpl4 ? 2048 : kst;
+    const uint64_t chunk_a = std::min<uint64_t>(std::max<uint64_t>(1, probe_chunk() / k / kst_a) * kst_a, keys.n);
+    return bloom_add_append(c, b, keys, f16, kmax, t1, kst_a, f2, shift1, nb1, P, chunk_a, kpl4);
+  }
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
