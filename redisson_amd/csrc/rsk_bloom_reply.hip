@@ -81,8 +81,9 @@ __global__ __launch_bounds__(256) void rp_size_kernel(const uint16_t* __restrict
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t total = part[0] + part[1] + part[2] + part[3];
-    tot[s] = total;
-    bud[s] = (uint32_t)((total + RP3_TILE - 1) / RP3_TILE) + groups;
+    const uint32_t rounds = (uint32_t)((total + RP3_TILE - 1) / RP3_TILE) + groups;
+    tot[s] = (total + rounds + 1) & ~1ull;  // records + one pad per odd round, even (16-byte aligned slices)
+    bud[s] = rounds;
   }
 }
 
@@ -192,10 +193,19 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
         for (uint32_t m = 0; m < RP3_PER; ++m)
           if (tag[m] != INVALID) img[lstart[tag[m] >> 16] + (tag[m] & 0xFFFFu)] = rec[m];
         const uint32_t kept = lstart[RB_PER_SL];
+        // an odd round is padded by one record (after every block's segment)
+        // so that tiles stay 16-byte aligned and are written by 16-byte stores
+        if (threadIdx.x == 0 && (kept & 1)) img[kept] = rec_pad<uint64_t>();
+        const uint32_t kept2 = (kept + 1) & ~1u;
         lds_barrier();
-        uint64_t* o = out + base + written;
-        for (uint32_t j = threadIdx.x; j < kept; j += RP3_T) __builtin_nontemporal_store(img[j], o + j);
-        written += kept;
+        u32x4* o4 = reinterpret_cast<u32x4*>(out + base + written);
+        const uint4* i4 = reinterpret_cast<const uint4*>(img);
+        for (uint32_t j = threadIdx.x; j < kept2 / 2; j += RP3_T) {
+          const uint4 v = i4[j];
+          u32x4 x = {v.x, v.y, v.z, v.w};
+          __builtin_nontemporal_store(x, o4 + j);
+        }
+        written += kept2;
         ++nt3;
         lds_barrier();  // img and lstart are rewritten by the next round
       }
@@ -367,7 +377,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint64_t tt_max = (max_np + (uint64_t)nb1 * max_nst) / slots + (uint64_t)W * nb1 + 64;  // sa2 tiles
   const uint64_t l2_probes = max_np + (uint64_t)nb1 * max_nst + tt_max * sa2_pad<uint64_t>() + 2ull * ncp;
   const uint64_t tt3_max = l2_probes / RP3_TILE + (uint64_t)ns * (1 + P) + (uint64_t)nb2 * (tt_max / RP3_GROUP + 1) + 64;
-  const uint64_t reg_probes = std::max(region_probes, l2_probes);  // rp3 writes into the sa1 region
+  const uint64_t reg_probes = std::max(region_probes, l2_probes + tt3_max + ns);  // rp3 writes into the sa1 region
   const uint64_t h2_bytes = al(tt_max * (nb2 + 1) * 2);
   const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256 +
                         al(8 * (ns + 1)) * 2 + al(4 * (ns + 1)) * 3;
