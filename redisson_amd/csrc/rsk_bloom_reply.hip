@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void rp_size_kernel(const uint16_t* __restrict
   if (threadIdx.x == 0) {
     const uint64_t total = part[0] + part[1] + part[2] + part[3];
     const uint32_t rounds = (uint32_t)((total + RP3_TILE - 1) / RP3_TILE) + groups;
-    tot[s] = (total + rounds + 1) & ~1ull;  // records + one pad per odd round, even (16-byte aligned slices)
+    tot[s] = total + (uint64_t)RB_PER_SL * rounds;  // records + a pad per odd block segment; even (16-byte aligned)
     bud[s] = rounds;
   }
 }
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
                                                     const uint32_t* __restrict__ tile3_off,
                                                     uint64_t* __restrict__ out, uint16_t* __restrict__ h3,
                                                     uint64_t* __restrict__ tb3, uint32_t* __restrict__ ntile3) {
-  __shared__ __attribute__((aligned(16))) uint64_t img[RP3_TILE];
+  __shared__ __attribute__((aligned(16))) uint64_t img[RP3_TILE + RB_PER_SL];  // + one pad per odd block segment
   __shared__ uint64_t s_pos[RP3_GROUP];
   __shared__ uint32_t s_pre[RP3_GROUP + 1];
   __shared__ uint16_t tbl[RP3_CHUNKS];
@@ -172,14 +172,15 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
           }
         }
         lds_barrier();
-        if (threadIdx.x < 64) {
+        if (threadIdx.x < 64) {  // block segments padded to even lengths: 16-byte aligned record pairs
           const uint32_t lane = threadIdx.x;
-          const uint32_t v = lane < RB_PER_SL ? hist[lane] : 0;
-          const uint32_t incl = wave_scan_incl(v, lane);
+          const uint32_t v = lane < RB_PER_SL ? hist[lane] : 0, v2 = (v + 1) & ~1u;
+          const uint32_t incl = wave_scan_incl(v2, lane);
           if (lane < RB_PER_SL) {
-            lstart[lane] = incl - v;
+            lstart[lane] = incl - v2;
             hist[lane] = 0;
-            h3[(uint64_t)(tbeg + nt3) * (RB_PER_SL + 1) + lane] = (uint16_t)(incl - v);
+            if (v & 1) img[incl - 1] = rec_pad<uint64_t>();
+            h3[(uint64_t)(tbeg + nt3) * (RB_PER_SL + 1) + lane] = (uint16_t)(incl - v2);
           }
           const uint32_t tot = rdl(incl, RB_PER_SL - 1);
           if (lane == 0) {
@@ -192,11 +193,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
 #pragma unroll
         for (uint32_t m = 0; m < RP3_PER; ++m)
           if (tag[m] != INVALID) img[lstart[tag[m] >> 16] + (tag[m] & 0xFFFFu)] = rec[m];
-        const uint32_t kept = lstart[RB_PER_SL];
-        // an odd round is padded by one record (after every block's segment)
-        // so that tiles stay 16-byte aligned and are written by 16-byte stores
-        if (threadIdx.x == 0 && (kept & 1)) img[kept] = rec_pad<uint64_t>();
-        const uint32_t kept2 = (kept + 1) & ~1u;
+        const uint32_t kept2 = lstart[RB_PER_SL];  // even: every segment is
         lds_barrier();
         u32x4* o4 = reinterpret_cast<u32x4*>(out + base + written);
         const uint4* i4 = reinterpret_cast<const uint4*>(img);
@@ -241,13 +238,15 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
     for (uint32_t j = w; j < nt; j += NW) {
       const uint16_t* hr = h3 + (uint64_t)(t0 + j) * (RB_PER_SL + 1);
       const uint32_t beg = hr[sub], end = hr[sub + 1];
-      const uint64_t* seg = in + tb3[t0 + j];
-      for (uint32_t o = beg + lane; o < end; o += 4 * 64) {
+      // segments are even and 16-byte aligned: record pairs, 2 loads in flight per lane
+      const uint4* seg = reinterpret_cast<const uint4*>(in + tb3[t0 + j]);
+      for (uint32_t o = beg / 2 + lane; o < end / 2; o += 2 * 64) {
         uint64_t r[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 2; ++u) {
           const uint32_t x = o + 64 * u;
-          r[u] = x < end ? __builtin_nontemporal_load(seg + x) : rec_pad<uint64_t>();
+          if (x < end / 2) unpack16<uint64_t>(ld_nt16(seg + x), r + 2 * u);
+          else r[2 * u] = r[2 * u + 1] = rec_pad<uint64_t>();
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -377,7 +376,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint64_t tt_max = (max_np + (uint64_t)nb1 * max_nst) / slots + (uint64_t)W * nb1 + 64;  // sa2 tiles
   const uint64_t l2_probes = max_np + (uint64_t)nb1 * max_nst + tt_max * sa2_pad<uint64_t>() + 2ull * ncp;
   const uint64_t tt3_max = l2_probes / RP3_TILE + (uint64_t)ns * (1 + P) + (uint64_t)nb2 * (tt_max / RP3_GROUP + 1) + 64;
-  const uint64_t reg_probes = std::max(region_probes, l2_probes + tt3_max + ns);  // rp3 writes into the sa1 region
+  const uint64_t reg_probes = std::max(region_probes, l2_probes + RB_PER_SL * tt3_max);  // rp3 writes into the sa1 region
   const uint64_t h2_bytes = al(tt_max * (nb2 + 1) * 2);
   const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256 +
                         al(8 * (ns + 1)) * 2 + al(4 * (ns + 1)) * 3;
