@@ -515,7 +515,8 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   const uint32_t nb2 = 1u << f2;
   const uint32_t ncp = nb1 * P;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t ua = env_u32("RSK_BLOOM_ST_UA", UA_DEFAULT) == 8 ? 8 : 4;
+  const uint32_t ua_env = env_u32("RSK_BLOOM_ST_UA", UA_DEFAULT);
+  const uint32_t ua = ua_env == 16 ? 16 : ua_env == 8 ? 8 : 4;
   const uint32_t dbg = env_u32("RSK_BLOOM_SA_DBG", 0);
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
@@ -627,7 +628,8 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
 #define RSK_APPLY(U)                                                                                          \
   hipLaunchKernelGGL((bloom_sa_apply_kernel<U>), dim3(ga), dim3(TA), 0, c->stream, l2, h2t, tt_max, f2, tb2,   \
                      tile_off, tiles, P, ns, b->d_bits, b->nwords)
-      if (ua == 8) RSK_APPLY(8);
+      if (ua == 16) RSK_APPLY(16);
+      else if (ua == 8) RSK_APPLY(8);
       else RSK_APPLY(4);
 #undef RSK_APPLY
       RSK_CHECK_LAUNCH("bloom_st_apply");
@@ -680,7 +682,8 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t nb2 = 1u << f2;
   const uint32_t ns = (uint32_t)nslices;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t P = f2 ? std::max<uint32_t>(1, (4 * cus + nb1 - 1) / nb1) : 1;
+  // parts per coarse bin (sa2 workgroups per bin); RSK_BLOOM_SA_P overrides (tuning)
+  const uint32_t P = f2 ? std::max<uint32_t>(1, env_u32("RSK_BLOOM_SA_P", (4 * cus + nb1 - 1) / nb1)) : 1;
   const uint32_t ncp = nb1 * P;
   uint64_t chunk = std::max<uint64_t>(1, probe_chunk() / k / kst) * kst;  // keys per chunk, whole super-tiles
   chunk = std::min<uint64_t>(chunk, keys.n);
