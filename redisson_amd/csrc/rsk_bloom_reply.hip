@@ -121,6 +121,20 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
   if (threadIdx.x <= RB_PER_SL) hist[threadIdx.x] = 0;
   uint64_t written = 0;
   uint32_t nt3 = 0;
+  // a round's image is written out during the next round, after its record
+  // loads and ranks (one vmcnt counts loads and stores: the stores then have
+  // the scan and the scatter to drain before the next loads are waited for)
+  uint32_t pend = 0;
+  uint64_t pend_at = 0;
+  auto write_out = [&]() {
+    u32x4* o4 = reinterpret_cast<u32x4*>(out + base + pend_at);
+    const uint4* i4 = reinterpret_cast<const uint4*>(img);
+    for (uint32_t j = threadIdx.x; j < pend / 2; j += RP3_T) {
+      const uint4 v = i4[j];
+      u32x4 x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, o4 + j);
+    }
+  };
   for (uint32_t pr = 0; pr < P; ++pr) {
     const uint64_t t0 = tile_off[(uint64_t)c * P + pr], nt = ntile[(uint64_t)c * P + pr];
     for (uint64_t g0 = 0; g0 < nt; g0 += RP3_GROUP) {
@@ -171,6 +185,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
             tag[m] = (blk << 16) | atomicAdd(&hist[blk], 1u);
           }
         }
+        write_out();  // the previous round
         lds_barrier();
         if (threadIdx.x < 64) {  // block segments padded to even lengths: 16-byte aligned record pairs
           const uint32_t lane = threadIdx.x;
@@ -193,21 +208,16 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
 #pragma unroll
         for (uint32_t m = 0; m < RP3_PER; ++m)
           if (tag[m] != INVALID) img[lstart[tag[m] >> 16] + (tag[m] & 0xFFFFu)] = rec[m];
-        const uint32_t kept2 = lstart[RB_PER_SL];  // even: every segment is
-        lds_barrier();
-        u32x4* o4 = reinterpret_cast<u32x4*>(out + base + written);
-        const uint4* i4 = reinterpret_cast<const uint4*>(img);
-        for (uint32_t j = threadIdx.x; j < kept2 / 2; j += RP3_T) {
-          const uint4 v = i4[j];
-          u32x4 x = {v.x, v.y, v.z, v.w};
-          __builtin_nontemporal_store(x, o4 + j);
-        }
-        written += kept2;
+        pend = lstart[RB_PER_SL];  // even: every segment is
+        pend_at = written;
+        written += pend;
         ++nt3;
-        lds_barrier();  // img and lstart are rewritten by the next round
+        // the next round's first barrier orders this image before its write-out
       }
     }
   }
+  lds_barrier();
+  write_out();
   if (threadIdx.x == 0) ntile3[s] = nt3;
 }
 
@@ -365,7 +375,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   // sa1<u64>: 73 KiB of LDS and <= 128 VGPRs -> 2 workgroups per CU
-  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_nst, 2ull * cus));
+  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({max_nst, 2ull * cus, SA2_WMAX}));
   const double share = std::min(1.0, (double)(1ull << shift1) / (double)(uint64_t)b->size);  // of a coarse bin
   const uint64_t q64 = (uint64_t)(1.25 * share * (double)max_np / W) + kst * k + (max_nst / W + 1) + 64;
   const uint32_t quota = (uint32_t)((q64 + 3) & ~uint64_t(3));
@@ -451,8 +461,9 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp2");
-      hipLaunchKernelGGL(bloom_sa2_kernel<uint64_t>, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc,
-                         nb1, P, nb2, reg_off, tile_off, tiles, l2, h2, tb2, 0);
+      auto k2 = env_knob("RSK_BLOOM_SA2_PF", 0) ? bloom_sa2_kernel<uint64_t, true> : bloom_sa2_kernel<uint64_t, false>;
+      hipLaunchKernelGGL(k2, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P, nb2, reg_off,
+                         tile_off, tiles, l2, h2, tb2, 0);
       RSK_CHECK_LAUNCH("bloom_rp2");
     }
     {

@@ -240,6 +240,7 @@ __global__ __launch_bounds__(1024) void st_offsets_kernel(const uint64_t* __rest
 #endif
 constexpr int SA2_V = RSK_SA2_V;    // sa2: uint4 loads per lane per tile (u32: 96 probes per fine bin: apply's 2 x 64 fast path)
 constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
+constexpr uint32_t SA2_WMAX = 1024;  // sa1 workgroups per sa2 part, at most (the host keeps W <= this)
 template <class R>
 constexpr uint32_t sa2_slots() { return SA2_T * SA2_V * (16 / sizeof(R)); }
 template <class R>
@@ -291,6 +292,25 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
       nxt[u] = (FIXED16 && st < nst && i < n) ? ld_nt16(keys16 + i) : make_uint4(0, 0, 0, 0);
     }
   };
+  // The image of tile t is written out during tile t + 1, after its hashes
+  // and ranks (`pend4` 16-byte groups still in img; dst / ibin stay valid
+  // until barrier (A)).  gfx9 counts loads and stores in one vmcnt, so a wait
+  // for the keys is a wait for every store issued before it: the order
+  // [wait keys t] [hash t] [loads t+1] [stores t-1] [scan, scatter t] leaves
+  // the scan and scatter between the stores and the next wait, and the loads
+  // of t + 1 are never in the wait that precedes their own issue.
+  auto write_out = [&](uint32_t total4) {
+    const uint4* img4 = reinterpret_cast<const uint4*>(img);
+    for (uint32_t g = threadIdx.x; g < total4; g += T1) {
+      const uint32_t d = dst[ibin[g]];
+      if (d != INVALID) {
+        const uint4 v = img4[g];
+        u32x4 x = {v.x, v.y, v.z, v.w};
+        *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
+      }
+    }
+  };
+  uint32_t pend4 = 0;
   if (FIXED16) fetch(blockIdx.x);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
@@ -300,7 +320,7 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
     uint4 cur[KPL];
 #pragma unroll
     for (int u = 0; u < KPL; ++u) cur[u] = nxt[u];
-    if (FIXED16) fetch(st + gridDim.x);
+    if (FIXED16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keys t here, before the loads of t + 1 issue
     R pay[NP];
     uint32_t tag[NP];
 #pragma unroll
@@ -340,7 +360,9 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
         }
       }
     }
-    sa_bar(dbg);  // (A) every rank taken
+    if (FIXED16) fetch(st + gridDim.x);
+    write_out(pend4);  // tile t - 1
+    sa_bar(dbg);  // (A) every rank taken, the previous image written out
     // wave 0: bin starts and run destinations (runs of L probes take
     // L4 = round_up(L, RG) slots, the tail rec_pad): image position j of bin b
     // goes to mine[j + dst[b]] (mod 2^32), dst[b] = b quota + pos[b] - lstart[b]
@@ -383,18 +405,10 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
         img[j] = pay[s];
         if ((r & (RG - 1)) == 0) ibin[j / RG] = (uint8_t)b;  // the group's first slot always holds a probe
       }
-    const uint32_t total4 = s_total / RG;
+    pend4 = s_total / RG;
     sa_bar(dbg);  // (C) image complete
-    const uint4* img4 = reinterpret_cast<const uint4*>(img);
-    for (uint32_t g = threadIdx.x; g < total4; g += T1) {
-      const uint32_t d = dst[ibin[g]];
-      if (d != INVALID) {
-        const uint4 v = img4[g];
-        u32x4 x = {v.x, v.y, v.z, v.w};
-        *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
-      }
-    }
   }
+  write_out(pend4);  // the last tile
   __syncthreads();
   if (threadIdx.x < nb1) used[(uint64_t)blockIdx.x * nb1 + threadIdx.x] = pos[threadIdx.x];
 }
@@ -420,8 +434,12 @@ __global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict
   bud[cp] = tiles;
 }
 
-template <class R>
-__global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const R* __restrict__ region, uint32_t quota,
+// PF: tile t + 1's loads issue after tile t's ranks (otherwise at the top of
+// tile t + 1, as the other loads' latency is covered by the second
+// workgroup of the CU).  __launch_bounds__(1024, 8): at most 64 VGPRs, so two
+// workgroups share a CU.
+template <class R, bool PF = false>
+__global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict__ region, uint32_t quota,
                                                           const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
                                                           uint32_t P, uint32_t nb2,
                                                           const uint64_t* __restrict__ reg_off,
@@ -432,67 +450,105 @@ __global__ __launch_bounds__(SA2_T) void bloom_sa2_kernel(const R* __restrict__ 
   constexpr uint32_t RG = 16 / sizeof(R);
   constexpr int NV = SA2_V * RG;
   constexpr uint32_t SLOTS = sa2_slots<R>();
-  // one image buffer: with LDS-only barriers a wave's write-out of tile t is
-  // done before it reaches (A) of t+1, and the image is rewritten after (B)
+  // one image buffer: tile t's write-out is done before (A) of t + 1, and
+  // the image is rewritten after (B)
   __shared__ __attribute__((aligned(16))) R srt[1][SLOTS + RG * 128];  // + pad slots per fine bin
   __shared__ uint32_t hist[128], lstart[128], s_total;
   __shared__ uint16_t s_hdr[129];
+  __shared__ uint32_t s_used[SA2_WMAX];  // used[w][c] of this part's sub-regions
   const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
   if (threadIdx.x < 128) hist[threadIdx.x] = 0;
   const uint64_t base = reg_off[cp];
   const uint32_t tbeg = tile_off[cp];
   uint64_t written = 0;
   uint32_t ntile = 0;
+  // Tiles run over the sub-regions (w, c) of this part in order.  As in sa1,
+  // the loads of tile t + 1 issue after tile t's ranks and the image of tile
+  // t is written out during tile t + 1 (one vmcnt for loads and stores: see
+  // bloom_sa1_kernel).  A uint4 is loaded when its first record is below
+  // `used` (quota is a multiple of RG, so it lies inside the sub-region); the
+  // records past `used` are replaced by rec_pad.
+  const uint32_t wbeg = W * p / P, wend = W * (p + 1) / P;
+  for (uint32_t i = threadIdx.x; i < wend - wbeg; i += SA2_T) s_used[i] = used[(uint64_t)(wbeg + i) * nb1 + c];
   __syncthreads();
-  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
-    const uint32_t nu = used[(uint64_t)w * nb1 + c];  // records of sub-region (w, c)
-    const R* sub = region + ((uint64_t)w * nb1 + c) * quota;
-    const uint4* in = reinterpret_cast<const uint4*>(sub);  // quota is a multiple of 4: 16-byte aligned
-    for (uint32_t t0 = 0; t0 < nu; t0 += SLOTS) {
-      R pay[NV];
-      uint32_t tag[NV];
+  uint32_t w = wbeg, t0 = 0, nu = 0;
+  while (w < wend && (nu = s_used[w - wbeg]) == 0) ++w;
+  uint4 nxt[SA2_V];
+  auto fetch = [&](uint32_t w_, uint32_t t0_, uint32_t nu_) {
+    const uint4* in = reinterpret_cast<const uint4*>(region + ((uint64_t)w_ * nb1 + c) * quota);
 #pragma unroll
-      for (int v = 0; v < SA2_V; ++v) {
-        const uint32_t q4 = t0 / RG + v * SA2_T + threadIdx.x;  // uint4 index
-        if (RG * q4 + RG - 1 < nu) {
-          unpack16<R>(ld_nt16(in + q4), pay + RG * v);
-        } else {
-#pragma unroll
-          for (uint32_t e = 0; e < RG; ++e) pay[RG * v + e] = RG * q4 + e < nu ? sub[RG * q4 + e] : rec_pad<R>();
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < NV; ++r) {
-        tag[r] = INVALID;
-        if (rec_off(pay[r]) != INVALID) {
-          const uint32_t bin = rec_off(pay[r]) >> SL_LOG;
-          tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
-        }
-      }
-      sa_bar(dbg);  // (A)
-      if (threadIdx.x < 64) wave0_bin_starts_pad<128, R>(hist, lstart, nb2, s_hdr, &s_total, srt[0]);
-      sa_bar(dbg);  // (B)
-      const uint32_t total = s_total;  // padded: a multiple of RG
-      if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
-      if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
-      R* img = srt[0];
-#pragma unroll
-      for (int r = 0; r < NV; ++r)
-        if (tag[r] != INVALID)
-          img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = rec_with_off(pay[r], rec_off(pay[r]) & ((1u << SL_LOG) - 1));
-      sa_bar(dbg);  // (C)
-      // 16-byte aligned: base and written are multiples of RG slots
-      u32x4* o4 = reinterpret_cast<u32x4*>(out + base + written);
-      const uint4* i4 = reinterpret_cast<const uint4*>(img);
-      for (uint32_t j = threadIdx.x; j < total / RG; j += SA2_T) {
-        const uint4 v = i4[j];
-        u32x4 x = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(x, o4 + j);
-      }
-      written += total;
-      ++ntile;
+    for (int v = 0; v < SA2_V; ++v) {
+      const uint32_t q4 = t0_ / RG + v * SA2_T + threadIdx.x;
+      nxt[v] = RG * q4 < nu_ ? ld_nt16(in + q4) : make_uint4(0, 0, 0, 0);
     }
+  };
+  auto write_out = [&](uint32_t total, uint64_t at) {
+    // 16-byte aligned: base and at are multiples of RG slots
+    u32x4* o4 = reinterpret_cast<u32x4*>(out + base + at);
+    const uint4* i4 = reinterpret_cast<const uint4*>(srt[0]);
+    for (uint32_t j = threadIdx.x; j < total / RG; j += SA2_T) {
+      const uint4 v = i4[j];
+      u32x4 x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, o4 + j);
+    }
+  };
+  bool have = w < wend;
+  if (PF && have) fetch(w, 0, nu);
+  uint32_t pend = 0;  // records of the previous tile still in the image
+  uint64_t pend_at = 0;
+  __syncthreads();
+  while (have) {
+    if (!PF) fetch(w, t0, nu);
+    uint4 cur[SA2_V];
+#pragma unroll
+    for (int v = 0; v < SA2_V; ++v) cur[v] = nxt[v];
+    if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t's records, before tile t + 1's loads issue
+    const uint32_t ct0 = t0, cnu = nu;
+    t0 += SLOTS;
+    if (t0 >= nu) {
+      t0 = 0;
+      do ++w;
+      while (w < wend && (nu = s_used[w - wbeg]) == 0);
+    }
+    have = w < wend;
+    R pay[NV];
+    uint32_t tag[NV];
+#pragma unroll
+    for (int v = 0; v < SA2_V; ++v) {
+      const uint32_t q4 = ct0 / RG + v * SA2_T + threadIdx.x;
+      R x[RG];
+      unpack16<R>(cur[v], x);
+#pragma unroll
+      for (uint32_t e = 0; e < RG; ++e) pay[RG * v + e] = RG * q4 + e < cnu ? x[e] : rec_pad<R>();
+    }
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      tag[r] = INVALID;
+      if (rec_off(pay[r]) != INVALID) {
+        const uint32_t bin = rec_off(pay[r]) >> SL_LOG;
+        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+      }
+    }
+    if (PF && have) fetch(w, t0, nu);
+    write_out(pend, pend_at);  // tile t - 1
+    sa_bar(dbg);  // (A) ranks taken, the previous image written out
+    if (threadIdx.x < 64) wave0_bin_starts_pad<128, R>(hist, lstart, nb2, s_hdr, &s_total, srt[0]);
+    sa_bar(dbg);  // (B)
+    const uint32_t total = s_total;  // padded: a multiple of RG
+    if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
+    if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
+    R* img = srt[0];
+#pragma unroll
+    for (int r = 0; r < NV; ++r)
+      if (tag[r] != INVALID)
+        img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = rec_with_off(pay[r], rec_off(pay[r]) & ((1u << SL_LOG) - 1));
+    pend = total;
+    pend_at = written;
+    written += total;
+    ++ntile;
+    sa_bar(dbg);  // (C)
   }
+  write_out(pend, pend_at);
   if (threadIdx.x == 0) tiles_out[cp] = ntile;
 }
 

@@ -531,7 +531,7 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   // W persistent sa1 workgroups; each gets 1.25x its expected share of a full
   // coarse bin per bin, plus one whole super-tile (a tile's run can be that
   // long) and the <= 3 padding slots per run of each of its tiles.
-  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_nst, (uint64_t)per_cu * cus));
+  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({max_nst, (uint64_t)per_cu * cus, SA2_WMAX}));
   const double share = (double)(1ull << shift1) / (double)(uint64_t)b->size;
   const bool tiny = env_u32("RSK_BLOOM_SA_TINY", 0) != 0;  // tests force the overflow fallback
   // quota > one tile's probes: a valid run offset b quota + pos - lstart never equals INVALID
@@ -611,7 +611,8 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     }
     {
       ProfScope ps(c, "bloom_st2");
-      hipLaunchKernelGGL(bloom_sa2_kernel<uint32_t>, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P, nb2,
+      auto k2 = env_u32("RSK_BLOOM_SA2_PF", 0) ? bloom_sa2_kernel<uint32_t, true> : bloom_sa2_kernel<uint32_t, false>;
+      hipLaunchKernelGGL(k2, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P, nb2,
                          reg_off, tile_off, tiles, l2, h2, tb2, (int)(dbg & 2));
       RSK_CHECK_LAUNCH("bloom_sa2");
     }
