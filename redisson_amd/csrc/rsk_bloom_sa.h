@@ -259,7 +259,8 @@ RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads in
 // below 2^32 - 1 keys).
 // DIAG (timing diagnostics only, RSK_BLOOM_SA1_DIAG; results are not a
 // filter): 1 = the key words instead of XXH64 / farmhash, 2 = also probe
-// indices by one multiply-high instead of the exact u63 remainders.
+// indices by one multiply-high instead of the exact u63 remainders, 3 = as 2
+// and no write-out (which leaves the image, so the scatter, dead as well).
 // KPL: keys per lane (default 16 / KMAX); more keys per super-tile make every
 // bin's run longer.
 template <bool FIXED16, int KMAX, int T1, class R, int DIAG = 0, int KPL = 16 / KMAX>
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
     const uint4* img4 = reinterpret_cast<const uint4*>(img);
     for (uint32_t g = threadIdx.x; g < total4; g += T1) {
       const uint32_t d = dst[ibin[g]];
-      if (d != INVALID) {
+      if (DIAG != 3 && d != INVALID) {
         const uint4 v = img4[g];
         u32x4 x = {v.x, v.y, v.z, v.w};
         *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;

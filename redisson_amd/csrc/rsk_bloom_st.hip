@@ -583,7 +583,10 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
                      (int)(dbg & 1))
       const uint32_t diag = env_u32("RSK_BLOOM_SA1_DIAG", 0);  // timing diagnostics (not a filter)
       if (kpl4) {
-        RSK_SA1(true, 8, 512, 0, 4);
+        if (diag == 1) RSK_SA1(true, 8, 512, 1, 4);
+        else if (diag == 2) RSK_SA1(true, 8, 512, 2, 4);
+        else if (diag == 3) RSK_SA1(true, 8, 512, 3, 4);
+        else RSK_SA1(true, 8, 512, 0, 4);
       } else if (diag && f16 && kmax == 8 && t1 == 512) {
         if (diag == 1) RSK_SA1(true, 8, 512, 1);
         else RSK_SA1(true, 8, 512, 2);
