@@ -365,7 +365,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint32_t ns = (uint32_t)nslices;
   const uint64_t nblocks = ((uint64_t)b->size + RB_BITS - 1) / RB_BITS;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t P = std::max<uint32_t>(1, (4 * cus + nb1 - 1) / nb1);
+  const uint32_t P = std::max<uint32_t>(1, env_knob("RSK_BLOOM_SA_P", 4 * cus / nb1));  // as the insert's sa2
   const uint32_t ncp = nb1 * P;
   const uint64_t probe_cap = env_knob("RSK_BLOOM_REPLY_CHUNK", 0) ? env_knob("RSK_BLOOM_REPLY_CHUNK", 0) : DEFAULT_CHUNK_PROBES;
   uint64_t chunk = std::max<uint64_t>(1, probe_cap / k / kst) * kst;  // keys per chunk, whole super-tiles

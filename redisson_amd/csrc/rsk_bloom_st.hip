@@ -696,9 +696,13 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
     // twice as long; 2 workgroups per CU): insert 36.0 -> 35.3 ms at C3, sa2
     // and apply gaining from the longer runs (RSK_BLOOM_SA1_KPL=2: 2 per lane)
     const bool kpl4 = f16 && kmax == 8 && t1 == 512 && env_u32("RSK_BLOOM_SA1_KPL", 4) == 4;
+    // sa2 parts per coarse bin: at most two rounds of the two resident
+    // 1024-lane workgroups per CU (C3: 143 bins x 7 = 1001 <= 1024 workgroups;
+    // 8 parts left a third round 12 % full: sa2 10.9 -> 10.1 ms)
+    const uint32_t Psa = std::max<uint32_t>(1, env_u32("RSK_BLOOM_SA_P", 4 * cus / nb1));
     const uint64_t kst_a = kpl4 ? 2048 : kst;
     const uint64_t chunk_a = std::min<uint64_t>(std::max<uint64_t>(1, probe_chunk() / k / kst_a) * kst_a, keys.n);
-    return bloom_add_append(c, b, keys, f16, kmax, t1, kst_a, f2, shift1, nb1, P, chunk_a, kpl4);
+    return bloom_add_append(c, b, keys, f16, kmax, t1, kst_a, f2, shift1, nb1, Psa, chunk_a, kpl4);
   }
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
