@@ -493,15 +493,22 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp_reply");
-      constexpr int U = RSK_RP_U;
-      const uint64_t g = (m + 256 * U - 1) / (256 * U);
-      const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
-      if (f16)
-        hipLaunchKernelGGL((rp_reply_kernel<true, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
-      else
-        hipLaunchKernelGGL((rp_reply_kernel<false, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
+      // keys per lane: RSK_RP_U at build time, RSK_BLOOM_RP_U=1|2|4 at run time (tuning)
+      const uint32_t u = env_knob("RSK_BLOOM_RP_U", RSK_RP_U);
+      auto launch = [&](auto U_) {
+        constexpr int U = decltype(U_)::value;
+        const uint64_t g = (m + 256 * U - 1) / (256 * U);
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
+        if (f16)
+          hipLaunchKernelGGL((rp_reply_kernel<true, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
+                             dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
+        else
+          hipLaunchKernelGGL((rp_reply_kernel<false, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
+                             dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
+      };
+      if (u == 4) launch(std::integral_constant<int, 4>());
+      else if (u == 1) launch(std::integral_constant<int, 1>());
+      else launch(std::integral_constant<int, 2>());
       RSK_CHECK_LAUNCH("bloom_rp_reply");
     }
   }
