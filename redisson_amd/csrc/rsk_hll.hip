@@ -126,6 +126,54 @@ static void launch_variant(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t w
                      c->d_slab);
 }
 
+// Software-pipelined variant: the next U keys per lane load while the
+// current U are hashed (no stores in the loop, so the in-order vmcnt lets
+// the wait cover only the older loads).
+template <int U, int T>
+__global__ __launch_bounds__(T) void hll_add16_pf(const uint4* __restrict__ keys, uint64_t n, uint64_t per_block,
+                                                  uint8_t* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
+  lds_zero(regs);
+  __syncthreads();
+  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = begin + per_block < n ? begin + per_block : n;
+  uint64_t i = begin + threadIdx.x;
+  uint4 v[U];
+  if (i + (uint64_t)(U - 1) * T < end) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[i + (uint64_t)u * T]);
+  }
+  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
+    uint4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = v[u];
+    const uint64_t j = i + (uint64_t)U * T;
+    if (j + (uint64_t)(U - 1) * T < end) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[j + (uint64_t)u * T]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      hll_update(regs, murmur64a_16(((uint64_t)cur[u].y << 32) | cur[u].x, ((uint64_t)cur[u].w << 32) | cur[u].z));
+  }
+  for (; i < end; i += T) {
+    uint4 x = keys[i];
+    hll_update(regs, murmur64a_16(((uint64_t)x.y << 32) | x.x, ((uint64_t)x.w << 32) | x.z));
+  }
+  __syncthreads();
+  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
+}
+
+template <int U, int T>
+static void launch_pf(rsk_ctx* c, const uint4* keys, uint64_t n) {
+  uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * 2, c->slab_count);
+  const uint64_t tile = (uint64_t)T * U;
+  uint64_t per_block = (n + blocks - 1) / blocks;
+  per_block = (per_block + tile - 1) / tile * tile;
+  blocks = (n + per_block - 1) / per_block;
+  hipLaunchKernelGGL((hll_add16_pf<U, T>), dim3((uint32_t)blocks), dim3(T), 0, c->stream, keys, n, per_block, c->d_slab);
+}
+
 template <int U, int T>
 static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu);
 
@@ -135,6 +183,9 @@ void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n) 
     case 9: launch_b8<4, 256>(c, keys, n, 8); break;
     case 10: launch_b8<8, 512>(c, keys, n, 4); break;
     case 11: launch_b8<4, 1024>(c, keys, n, 2); break;
+    case 12: launch_pf<4, 256>(c, keys, n); break;
+    case 13: launch_pf<2, 256>(c, keys, n); break;
+    case 14: launch_pf<8, 256>(c, keys, n); break;
     case 0: launch_variant<4, 512, true>(c, keys, n, 2); break;
     case 1: launch_variant<8, 512, true>(c, keys, n, 2); break;
     case 2: launch_variant<2, 512, true>(c, keys, n, 2); break;

@@ -56,7 +56,10 @@ def main():
     keys = devmem.gen_keys16(eng, 0x5EED0002, 0, n)
     names = {0: "U4_T512_nt", 1: "U8_T512_nt", 2: "U2_T512_nt", 3: "U4_T512_plain", 4: "U4_T1024_nt",
              5: "U4_T256_nt", 6: "U8_T1024_nt", 7: "U2_T1024_nt", 8: "b8_U4_T512_4wg", 9: "b8_U4_T256_8wg",
-             10: "b8_U8_T512_4wg", 11: "b8_U4_T1024_2wg"}
+             10: "b8_U8_T512_4wg", 11: "b8_U4_T1024_2wg", 12: "pf_U4_T256", 13: "pf_U2_T256", 14: "pf_U8_T256"}
+    if os.environ.get("MEMBENCH_VARIANTS"):  # e.g. "5,12,13,14"
+        keep = {int(x) for x in os.environ["MEMBENCH_VARIANTS"].split(",")}
+        names = {v: nm for v, nm in names.items() if v in keep}
     vs = {v: [] for v in names}
     for _ in range(rounds):
         for v in names:
