@@ -275,8 +275,10 @@ def insert_roofline(n: int, k: int, size: int, secs: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults: the kernel trace shows the first ~12 launches on a box running
+    # slower while the clock settles (profiles/r02_roofline_check.json)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
                     help="c2: 16-byte keys (headline); c4: variable-length keys; c5: grouped sketches")
     ap.add_argument("--keys", type=int, default=None,
