@@ -162,7 +162,9 @@ ST_KNOBS = ["RSK_BLOOM_ST=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T1=1024", "RSK_BLOOM_
             "RSK_BLOOM_ST=1,RSK_BLOOM_SA_TINY=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA_DBG=3",
             "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0", "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_TINY_BUDGET=1",
             "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_CHUNK=300000"]
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_CHUNK=300000",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA_P=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA_P=13,RSK_BLOOM_SA2_PF=1",
+            "RSK_BLOOM_ST=1,RSK_BLOOM_SA1_KPL=2"]
 
 
 @pytest.mark.parametrize("size,k,n", ST_CASES)
@@ -175,7 +177,10 @@ def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs)
     (sa1/sa2, default; full barriers instead of LDS-only ones; sub-regions too
     small, which overflow into the exact-offset fallback) and through the
     header pipeline (st1/st2, RSK_BLOOM_SA=0) with a one-tile budget
-    (overflow), 512-lane st2 and many chunks."""
+    (overflow), 512-lane st2 and many chunks; sa2 with one part per coarse bin
+    (every workgroup walks all sub-regions) and with 13 (parts without any
+    sub-region when the batch has few super-tiles) plus its register
+    prefetch; sa1 with 2 keys per lane."""
     from redisson_amd import KeyBatch
 
     for kv in filter(None, knobs.split(",")):

@@ -38,7 +38,8 @@ def test_sampled_reply_oracle_matches_sequential(orc):
 CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000), (1000003, 3, 200000), (1000003, 33, 20000),
          (19170117, 7, 300000), (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000),
          (4014142460, 8, 600000)]
-KNOBS = ["RSK_BLOOM_REPLY=1", "RSK_BLOOM_REPLY=1,RSK_BLOOM_REPLY_CHUNK=300000", "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_TINY=1"]
+KNOBS = ["RSK_BLOOM_REPLY=1", "RSK_BLOOM_REPLY=1,RSK_BLOOM_REPLY_CHUNK=300000", "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_TINY=1",
+         "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_P=13,RSK_BLOOM_RP_U=4", "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_P=1,RSK_BLOOM_RP_U=1"]
 
 
 @pytest.mark.gpu
@@ -48,7 +49,8 @@ def test_replies_parity(L, engine, orc, monkeypatch, size, k, n, knobs):
     """Forced on at every size: one partition level (<= 256 slices) and two
     (301 and 7,657 slices), k in {1, 2, 3, 5, 7, 8, 9, 16} (33: the sort path); many chunks (each
     answered against the filter the earlier ones left); sub-regions too small
-    (the chunk falls back to the sort path).  A second batch of variable-length
+    (the chunk falls back to the sort path); rp2 with 13 parts per coarse bin
+    and with one, rp_reply with 4 and 1 keys per lane.  A second batch of variable-length
     keys repeats keys of the first and of itself (bits already set before the
     batch, first probes inside it)."""
     from redisson_amd import KeyBatch
