@@ -4,8 +4,9 @@ Step = RHyperLogLog.addAll(n synthetic 16-byte keys already resident in HBM)
        + (N > 1) RCCL MAX all-reduce of the 16384 registers + count().
 The keys are the SURVEY.md 8d C2 stream (splitmix64, seed 0x5EED0002), each
 rank taking its own contiguous range (weak scaling: n keys per GPU).
-Secondary fields report the C3 Bloom filter (1B inserts at 1% FPP, EXTENDED
-mode, then 1B contains queries) on rank 0.
+Secondary fields (`bloom`) report the C3 Bloom filter per node (1B inserts at
+1% FPP, EXTENDED mode, sharded over the ranks and merged with the RCCL
+slice-OR, then 1B contains queries sharded over the replicated filter).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--keys N_PER_GPU]
 """
@@ -139,48 +140,93 @@ def random_access_peaks(engine, nbytes: int, reps: int = 3):
     return best
 
 
-def bloom_bench(engine, n_ins: int, n_q: int, reps: int, with_replies: bool = True):
-    from redisson_amd import _lib, devmem
+def bloom_bench(engine, n_ins: int, n_q: int, reps: int, rank: int = 0, world: int = 1, with_replies: bool = True,
+                keep_bits: bool = False):
+    """Node-level Bloom (BASELINE configs[2]; north_star "Bloom lookups/s (node)",
+    SURVEY 8e): the C3 stream's n_ins inserts are sharded over the ranks, each
+    rank inserts its shard into its own filter of the full size, the partial bit
+    strings are merged by rsk_bloom_allreduce_or (slices to their owners, OR,
+    merged slices back over RCCL; at N = 1 the same call moves nothing), and
+    each rank answers its 1/N of the n_q queries against the replicated filter.
+    Phase times are the max over ranks; a phase ends on every rank's device."""
+    import numpy as np
+
+    from redisson_amd import _lib, devmem, shard
 
     L = _lib.load()
     size = ctypes.c_int64()
     k = ctypes.c_int32()
     _lib.check(L.rsk_bloom_params(n_ins, 0.01, _lib.RSK_BLOOM_EXTENDED, ctypes.byref(size), ctypes.byref(k)))
-    ins = devmem.gen_keys16(engine, SEED_C3, 0, n_ins)
-    qs = devmem.gen_queries16(engine, SEED_Q, SEED_C3, n_ins, 0, n_q)
-    out = devmem.DeviceBuffer(engine, n_q)
-    ki = ins.keys_fixed(n_ins, 16).as_struct()
-    kq = qs.keys_fixed(n_q, 16).as_struct()
-    add_t, con_t = [], []
-    hits = 0
+    ilo, ihi = shard.ShardPlan(n_ins, world).range(rank)
+    qlo, qhi = shard.ShardPlan(n_q, world).range(rank)
+    m_ins, m_q = ihi - ilo, qhi - qlo
+    ins = devmem.gen_keys16(engine, SEED_C3, ilo, m_ins)
+    qs = devmem.gen_queries16(engine, SEED_Q, SEED_C3, n_ins, qlo, m_q)
+    out = devmem.DeviceBuffer(engine, max(1, m_q))
+    ki = ins.keys_fixed(m_ins, 16).as_struct()
+    kq = qs.keys_fixed(m_q, 16).as_struct()
+
+    def node_max(vals, op="max"):
+        if world == 1:
+            return list(vals)
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor(list(vals), dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return t.tolist()
+
+    def barrier():
+        engine.sync()
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    phases = []
+    hits = probes = 0
+    bits = None
     for r in range(reps + 1):
         if r == 1:  # rep 0 is warm-up (first-call scratch allocation); kernel times from rep 1
             engine.prof_reset()
             engine.prof_enable(True)
         b = ctypes.c_void_p()
         _lib.check(L.rsk_bloom_create(engine.ctx, size.value, k.value, ctypes.byref(b)))
-        engine.sync()
+        barrier()
         t0 = time.perf_counter()
         _lib.check(L.rsk_bloom_add(b, ctypes.byref(ki), None))
         engine.sync()
         t1 = time.perf_counter()
+        shard.bloom_allreduce_or(b)  # returns once this rank's filter is the node's
+        t2 = time.perf_counter()
         _lib.check(L.rsk_bloom_contains(b, ctypes.byref(kq), out.ptr))
         engine.sync()
-        t2 = time.perf_counter()
+        t3 = time.perf_counter()
         if r:
-            add_t.append(t1 - t0)
-            con_t.append(t2 - t1)
+            phases.append((t1 - t0, t2 - t1, t2 - t0, t3 - t2))
         if r == reps:
-            hits = int(out.to_numpy().sum())
+            hits = int(out.to_numpy()[:m_q].sum())
             # untimed: the gathers the contains kernel issues for these queries
             pr = ctypes.c_uint64()
-            _lib.check(L.rsk_diag_bloom_contains_probes(engine.ctx, b, qs.ptr, n_q, out.ptr, ctypes.byref(pr)))
+            _lib.check(L.rsk_diag_bloom_contains_probes(engine.ctx, b, qs.ptr, m_q, out.ptr, ctypes.byref(pr)))
             probes = pr.value
             bc = ctypes.c_uint64()
             _lib.check(L.rsk_bloom_bitcount(b, ctypes.byref(bc)))
             fill = bc.value / size.value
+            if keep_bits:
+                bits = np.zeros((size.value + 7) // 8, np.uint8)
+                n_ = ctypes.c_size_t()
+                _lib.check(L.rsk_bloom_export_bits(b, bits.ctypes.data, bits.size, ctypes.byref(n_)))
         L.rsk_bloom_destroy(b)
+        barrier()
     engine.prof_enable(False)
+    # per rep: the slowest rank's phase; then the best rep
+    per_rep = [node_max(p) for p in phases]
+    ins_local_s = min(p[0] for p in per_rep)
+    merge_s = min(p[1] for p in per_rep)
+    add_s = min(p[2] for p in per_rep)
+    con_s = min(p[3] for p in per_rep)
+    hits, probes = (int(v) for v in node_max([hits, probes], "sum"))
     add_ms, add_n = engine.prof_read("bloom_add16")
     con_ms, con_n = engine.prof_read("bloom_contains16")
     stages = {}
@@ -189,9 +235,8 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, with_replies: bool = Tr
         ms, cnt = engine.prof_read(name)
         if cnt:
             stages[name] = ms / max(1, add_n)  # per insert batch (summed over its chunks)
-    add_s, con_s = min(add_t), min(con_t)
     replies = None
-    if with_replies:
+    if with_replies and world == 1:
         # RBloomFilter.add's per-element reply (RedissonBloomFilter.java:100-107) for
         # every key of the batch, in input order, into a fresh filter: run 0 warms
         # up (the pipeline's scratch is allocated), run 1 is timed.
@@ -232,10 +277,13 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, with_replies: bool = Tr
     peaks = random_access_peaks(engine, (size.value + 7) // 8)
     gathers_per_s = probes / con_s
     sets_per_s = n_ins * k.value / add_s
-    return {"config": "C3: %d inserts @1%% FPP (size %d bits, k=%d, EXTENDED), %d contains (50%% inserted)"
-                      % (n_ins, size.value, k.value, n_q),
+    res = {"config": "C3: %d inserts @1%% FPP (size %d bits, k=%d, EXTENDED), %d contains (50%% inserted); "
+                     "%d rank(s): inserts and queries sharded, filters merged by rsk_bloom_allreduce_or"
+                     % (n_ins, size.value, k.value, n_q, world),
+            "n_gpus": world, "path": "node: sharded insert + rsk_bloom_allreduce_or + sharded contains",
             "insert_keys_per_s": n_ins / add_s, "contains_keys_per_s": n_q / con_s,
-            "insert_ms": add_s * 1e3, "contains_ms": con_s * 1e3, "contains_true": hits,
+            "insert_ms": add_s * 1e3, "insert_local_ms": ins_local_s * 1e3, "merge_ms": merge_s * 1e3,
+            "contains_ms": con_s * 1e3, "contains_true": hits,
             "insert_kernel_avg_ms": add_ms / max(1, add_n), "contains_kernel_avg_ms": con_ms / max(1, con_n),
             "insert_stage_ms": stages,
             "insert_bit_rmw_per_s": sets_per_s,
@@ -253,8 +301,11 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, with_replies: bool = Tr
                            "note": "slice-partitioned: probes sorted into 64 KiB LDS-resident filter slices, "
                                    "so the insert is not bound by memory-side atomics"},
                 "peaks_measured_on": "a zeroed buffer of the filter's size, 2^30 uniformly random ops, best of 3"},
-            "insert_roofline": insert_roofline(n_ins, k.value, size.value, add_s),
+            "insert_roofline": insert_roofline(n_ins // world, k.value, size.value, ins_local_s),
             "insert_with_replies": replies}
+    if keep_bits:
+        res["bits"] = bits
+    return res
 
 
 def insert_roofline(n: int, k: int, size: int, secs: float):
@@ -322,6 +373,8 @@ def main():
     engine = client.engine
     if world > 1:
         shard.init_comm(engine)
+    elif not args.no_bloom and args.workload == "c2":
+        shard.init_comm_single(engine)  # the node-level Bloom merge runs through the same call at N = 1
     wl = args.workload
     n = args.keys if args.keys is not None else (500_000_000 if wl == "c5" else 1_000_000_000)
     extra = {}
@@ -487,10 +540,11 @@ def main():
         b.free()
     if wl == "c5":
         pool.close()
-    if rank == 0 and world == 1 and wl == "c2" and not args.no_bloom:
+    if wl == "c2" and not args.no_bloom:  # every rank: the node-level Bloom is collective
         bn = args.bloom_keys
-        result["bloom"] = bloom_bench(engine, bn, bn, reps=2, with_replies=not args.no_bloom_replies)
-        tr = pmc_traffic("bloom_insert_supertile", pmc_cfg)
+        result["bloom"] = bloom_bench(engine, bn, bn, reps=2, rank=rank, world=world,
+                                      with_replies=not args.no_bloom_replies)
+        tr = pmc_traffic("bloom_insert_supertile", pmc_cfg) if world == 1 else None
         if tr:
             ir = result["bloom"]["insert_roofline"]
             ir["traffic"] = tr["bytes"]

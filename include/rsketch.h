@@ -281,10 +281,16 @@ int rsk_hll_fetch_rows(rsk_hll *h, const uint64_t *ids, uint64_t n);
  * RSK_ERR_INVALID_ARG and no rank is left waiting in a collective. */
 #define RSK_FETCH_SELF 1u
 int rsk_hll_fetch_rows_flags(rsk_hll *h, const uint64_t *ids, uint64_t n, uint32_t flags);
-/* Bloom bit string := OR over all ranks.  RCCL has no bitwise-OR reduction:
- * all-to-all of 1/N slices, local OR, all-gather (also at N = 1, where the
- * rank exchanges with itself). */
+/* Bloom bit string := OR over all ranks (the node-level insert of sharded
+ * keys, RedissonBloomFilter.java:80-114, before the replicated contains()).
+ * RCCL has no bitwise-OR reduction: rank j owns a 1/N slice of the words;
+ * grouped ncclSend/ncclRecv bring every rank's copy of slice j to rank j,
+ * which ORs them into its filter, and send the merged slice back to every
+ * rank -- straight out of and into the filter, one transfer per peer.  At
+ * N = 1 nothing moves.  With RSK_FETCH_SELF the rank also exchanges its own
+ * slice with itself (every step runs on one GPU; tests). */
 int rsk_bloom_allreduce_or(rsk_bloom *b);
+int rsk_bloom_allreduce_or_flags(rsk_bloom *b, uint32_t flags);
 
 /* ------------------------------------------------------- exchange plans */
 /* The host arithmetic the collectives above run (no GPU needed; exported so

@@ -423,27 +423,36 @@ void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_
   RSK_CHECK_LAUNCH("bloom_or");
 }
 
-// dst = OR of rows[r][0..words) (the local step of the slice-OR merge).
-__global__ __launch_bounds__(256) void or_rows_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
-                                                      uint32_t rows, uint64_t words) {
+// dst |= OR of the rows (the local step of the slice-OR merge): 16-byte
+// lanes over the aligned body, one word per lane over the tail.
+__global__ __launch_bounds__(256) void or_rows_into_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                           uint32_t rows, uint64_t words, uint64_t stride) {
   const uint64_t w4 = words / 4;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w4; i += (uint64_t)gridDim.x * blockDim.x) {
-    uint4 acc = make_uint4(0, 0, 0, 0);
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = t0; i < w4; i += step) {
+    uint4 acc = reinterpret_cast<const uint4*>(dst)[i];
     for (uint32_t r = 0; r < rows; ++r) {
-      uint4 v = reinterpret_cast<const uint4*>(src + (uint64_t)r * words)[i];
+      const uint4 v = reinterpret_cast<const uint4*>(src + (uint64_t)r * stride)[i];
       acc = make_uint4(acc.x | v.x, acc.y | v.y, acc.z | v.z, acc.w | v.w);
     }
     reinterpret_cast<uint4*>(dst)[i] = acc;
   }
+  for (uint64_t i = 4 * w4 + t0; i < words; i += step) {
+    uint32_t acc = dst[i];
+    for (uint32_t r = 0; r < rows; ++r) acc |= src[(uint64_t)r * stride + i];
+    dst[i] = acc;
+  }
 }
 
-void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words) {
+void or_rows_into_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words,
+                         uint64_t stride) {
   uint64_t g = (words / 4 + 255) / 256;
-  uint64_t cap = (uint64_t)c->num_cus * 8;
+  const uint64_t cap = (uint64_t)c->num_cus * 8;
   if (g > cap) g = cap;
   if (g == 0) g = 1;
   ProfScope ps(c, "bloom_or_rows");
-  hipLaunchKernelGGL(or_rows_kernel, dim3((uint32_t)g), dim3(256), 0, c->stream, d_dst, d_src, rows, words);
+  hipLaunchKernelGGL(or_rows_into_kernel, dim3((uint32_t)g), dim3(256), 0, c->stream, d_dst, d_src, rows, words,
+                     stride);
   RSK_CHECK_LAUNCH("bloom_or_rows");
 }
 

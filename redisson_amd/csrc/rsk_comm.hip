@@ -8,8 +8,9 @@
 //   pools : the same over [n][16384] (bandwidth-bound, ring over xGMI), or a
 //           reduce-scatter that leaves rank r owning a contiguous 1/N of the
 //           sketches (the C5 plan: half the traffic of the all-reduce);
-//   Bloom : RCCL has no bitwise OR, so all-to-all of 1/N slices (grouped
-//           ncclSend/ncclRecv), a local OR, and ncclAllGather.
+//   Bloom : RCCL has no bitwise OR, so all-to-all of 1/N slices and, after a
+//           local OR, all-to-all of the merged slices back (grouped
+//           ncclSend/ncclRecv straight out of / into the filter).
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -347,38 +348,58 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
 
 int rsk_hll_fetch_rows(rsk_hll* h, const uint64_t* ids, uint64_t n) { return rsk_hll_fetch_rows_flags(h, ids, n, 0); }
 
-int rsk_bloom_allreduce_or(rsk_bloom* b) {
+int rsk_bloom_allreduce_or(rsk_bloom* b) { return rsk_bloom_allreduce_or_flags(b, 0); }
+
+int rsk_bloom_allreduce_or_flags(rsk_bloom* b, uint32_t flags) {
   return guarded([&] {
+    need((flags & ~RSK_FETCH_SELF) == 0, "unknown flags");
     need(b != nullptr, "bad filter");
     rsk_ctx* c = b->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
-    const uint64_t N = (uint64_t)c->nranks;
-    // Slice of S words (multiple of 4 for 16-byte vector OR), N*S >= nwords.
-    // At N = 1 the plan still runs (send to self, OR of one row, all-gather of one).
+    const uint64_t N = (uint64_t)c->nranks, me = (uint64_t)c->rank;
+    // Rank j owns words [j*S, j*S + sz(j)) of the filter: S is a multiple of 4
+    // (16-byte vector OR) with N*S >= nwords, so the last slices may be short
+    // or empty.  Slices travel straight out of and back into the filter (no
+    // staging copies); both phases are grouped point-to-point transfers, one
+    // per peer, which on a fully connected xGMI node use every link at once.
+    // At N = 1 the rank owns the whole filter and nothing moves.
     const uint64_t S = rsk::plan_bloom_slice_words(b->nwords, N);
-    const uint64_t full = N * S;
-    uint32_t* send = reinterpret_cast<uint32_t*>(c->work(3 * full * 4 + 256));
-    uint32_t* recv = send + full;
-    uint32_t* gath = recv + full;
-    if (full > b->nwords) RSK_HIP(hipMemsetAsync(send + b->nwords, 0, (full - b->nwords) * 4, c->stream));
-    RSK_HIP(hipMemcpyAsync(send, b->d_bits, b->nwords * 4, hipMemcpyDeviceToDevice, c->stream));
-    {
-      rsk::ProfScope ps(c, "bloom_alltoall");
-      RSK_NCCL(ncclGroupStart());
-      for (uint64_t j = 0; j < N; ++j) {
-        RSK_NCCL(ncclSend(send + j * S, S * 4, ncclUint8, (int)j, comm, c->stream));
-        RSK_NCCL(ncclRecv(recv + j * S, S * 4, ncclUint8, (int)j, comm, c->stream));
+    auto sz = [&](uint64_t j) {
+      const uint64_t lo = std::min(j * S, b->nwords);
+      return std::min(lo + S, b->nwords) - lo;
+    };
+    const uint64_t mine = sz(me), row = (mine + 3) & ~3ull;  // recv rows 16-byte aligned
+    // Peers: every other rank; with RSK_FETCH_SELF also this rank itself (its
+    // slice makes the round trip through RCCL, so the exchange runs on one GPU).
+    std::vector<uint64_t> peers;
+    for (uint64_t j = 0; j < N; ++j)
+      if (j != me || (flags & RSK_FETCH_SELF)) peers.push_back(j);
+    if (!peers.empty() && b->nwords > 0) {
+      uint32_t* recv = reinterpret_cast<uint32_t*>(c->work(peers.size() * row * 4 + 256));
+      {  // phase 1: every peer's copy of my slice
+        rsk::ProfScope ps(c, "bloom_alltoall");
+        RSK_NCCL(ncclGroupStart());
+        for (size_t r = 0; r < peers.size(); ++r) {
+          const uint64_t j = peers[r];
+          if (sz(j)) RSK_NCCL(ncclSend(b->d_bits + j * S, sz(j) * 4, ncclUint8, (int)j, comm, c->stream));
+          if (mine) RSK_NCCL(ncclRecv(recv + r * row, mine * 4, ncclUint8, (int)j, comm, c->stream));
+        }
+        RSK_NCCL(ncclGroupEnd());
       }
-      RSK_NCCL(ncclGroupEnd());
+      if (mine) rsk::or_rows_into_launch(c, b->d_bits + me * S, recv, (uint32_t)peers.size(), mine, row);
+      {  // phase 2: my merged slice to every peer, theirs into my filter
+        rsk::ProfScope ps(c, "bloom_allgather");
+        RSK_NCCL(ncclGroupStart());
+        for (uint64_t j : peers) {
+          // my own slice coming back (self exchange) lands in the consumed recv rows
+          uint32_t* into = j == me ? recv : b->d_bits + j * S;
+          if (mine) RSK_NCCL(ncclSend(b->d_bits + me * S, mine * 4, ncclUint8, (int)j, comm, c->stream));
+          if (sz(j)) RSK_NCCL(ncclRecv(into, sz(j) * 4, ncclUint8, (int)j, comm, c->stream));
+        }
+        RSK_NCCL(ncclGroupEnd());
+      }
     }
-    uint32_t* mine = gath + (uint64_t)c->rank * S;
-    rsk::or_rows_launch(c, mine, recv, (uint32_t)N, S);
-    {
-      rsk::ProfScope ps(c, "bloom_allgather");
-      RSK_NCCL(ncclAllGather(mine, gath, S * 4, ncclUint8, comm, c->stream));
-    }
-    RSK_HIP(hipMemcpyAsync(b->d_bits, gath, b->nwords * 4, hipMemcpyDeviceToDevice, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }

@@ -242,8 +242,10 @@ void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, 
 // misc/Hash.hashToBase64 of every key: 22 chars per key into d_out.
 void hash_b64_launch(rsk_ctx* c, const DevKeys& k, char* d_out);
 void bloom_or_launch(rsk_ctx* c, uint32_t* d_bits, const uint8_t* d_src, uint64_t nbytes);
-// dst[0..S) = OR over rows of src[rows][S] (u32 words).
-void or_rows_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words);
+// dst[0..words) |= OR over rows of src (row r at src + r*stride words; stride
+// and dst 16-byte aligned, words any count).
+void or_rows_into_launch(rsk_ctx* c, uint32_t* d_dst, const uint32_t* d_src, uint32_t rows, uint64_t words,
+                         uint64_t stride);
 
 // ---- exchange plans (rsk_plan.hip, host only)
 void plan_owned_range(uint64_t n, uint64_t N, uint64_t r, uint64_t* first, uint64_t* count);

@@ -5,7 +5,7 @@ RCCL layer of librsketch (rsk_comm.hip):
   HLL   : rsk_hll_allreduce        ncclAllReduce(uint8, MAX), 16 KiB
   pools : rsk_hll_allreduce_pool   the same over [n][16384]
           rsk_hll_reducescatter_pool  MAX reduce-scatter: rank r owns 1/N of the sketches (C5)
-  Bloom : rsk_bloom_allreduce_or   all-to-all of 1/N slices, local OR, all-gather
+  Bloom : rsk_bloom_allreduce_or   slices to their owners, local OR, merged slices back
 
 torch.distributed is used only as the out-of-band channel that ships the
 RCCL unique id (any backend; gloo keeps the GPU out of torch's hands).  The
@@ -113,8 +113,19 @@ def fetch_plan(n: int, world: int, rank: int, ids, flags: int = 0):
     return want, np.bincount(owner_of(want, n, world), minlength=world).astype(np.uint64)
 
 
-def bloom_allreduce_or(bloom) -> None:
-    _lib.check(_lib.load().rsk_bloom_allreduce_or(bloom), "rsk_bloom_allreduce_or")
+def bloom_allreduce_or(bloom, flags: int = 0) -> None:
+    """Collective: the filter := OR over ranks (flags = _lib.RSK_FETCH_SELF also
+    sends this rank's own slice through RCCL, so every step runs at N = 1)."""
+    _lib.check(_lib.load().rsk_bloom_allreduce_or_flags(bloom, flags), "rsk_bloom_allreduce_or")
+
+
+def init_comm_single(engine) -> None:
+    """A 1-rank RCCL communicator without torch.distributed (N = 1 runs of the
+    multi-GPU code path)."""
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid), "rsk_comm_init")
 
 
 # ------------------------------------------------------- CPU restatements
@@ -183,23 +194,38 @@ def hll_fetch_rows_cpu(regs: np.ndarray, ids, group=None) -> np.ndarray:
     return regs
 
 
+def bloom_slice_bounds(nwords: int, world: int, rank: int):
+    """Words [lo, hi) of the filter rank `rank` merges (rsk_bloom_allreduce_or:
+    slices of slice_words() words, the last ones short or empty)."""
+    S = slice_words(nwords, world)
+    lo = min(rank * S, nwords)
+    return lo, min(lo + S, nwords)
+
+
 def bloom_allreduce_or_cpu(bits: np.ndarray, group=None) -> np.ndarray:
-    """The Bloom slice-OR exchange on CPU tensors, same plan as the GPU path."""
+    """The Bloom slice-OR exchange on CPU tensors, same plan as the GPU path:
+    phase 1 sends slice j of every rank to rank j (ragged slices, nothing
+    padded), rank j ORs them into its own slice, phase 2 sends the merged
+    slice back to every rank."""
     import torch
     import torch.distributed as dist
 
     N, r = dist.get_world_size(group), dist.get_rank(group)
     nbytes = bits.size
     nwords = ((nbytes + 15) // 16) * 4
-    S = slice_words(nwords, N)
-    send = np.zeros(N * S * 4, np.uint8)
-    send[:nbytes] = bits
-    recv = torch.zeros(N * S * 4, dtype=torch.uint8)
-    dist.all_to_all_single(recv, torch.from_numpy(send), group=group)
-    rows = recv.numpy().reshape(N, S * 4)
-    mine = np.bitwise_or.reduce(rows, axis=0)
-    out = [torch.zeros(S * 4, dtype=torch.uint8) for _ in range(N)]
-    dist.all_gather(out, torch.from_numpy(mine.copy()), group=group)
-    full = np.concatenate([o.numpy() for o in out])
-    assert r >= 0
-    return full[:nbytes]
+    words = np.zeros(nwords * 4, np.uint8)
+    words[:nbytes] = bits
+    words = words.view(np.uint32)
+    bounds = [bloom_slice_bounds(nwords, N, j) for j in range(N)]
+    sizes = [hi - lo for lo, hi in bounds]
+    lo, hi = bounds[r]
+    recv = torch.zeros(N * sizes[r], dtype=torch.int32)
+    dist.all_to_all_single(recv, torch.from_numpy(words.view(np.int32).copy()),
+                           output_split_sizes=[sizes[r]] * N, input_split_sizes=sizes, group=group)
+    rows = recv.numpy().view(np.uint32).reshape(N, sizes[r])
+    merged = words.copy()
+    merged[lo:hi] = np.bitwise_or.reduce(rows, axis=0) if sizes[r] else merged[lo:hi]
+    back = torch.zeros(nwords, dtype=torch.int32)
+    dist.all_to_all_single(back, torch.from_numpy(np.tile(merged[lo:hi].view(np.int32), N)),
+                           output_split_sizes=sizes, input_split_sizes=[sizes[r]] * N, group=group)
+    return back.numpy().view(np.uint8)[:nbytes].copy()

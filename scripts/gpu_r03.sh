@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-3 GPU sessions.  Each GPU step runs under its own time limit and the
+# first failure ends the script (no retries).
+#   scripts/gpu_r03.sh PART [pytest selection...]
+#     tests  : the -m gpu suite (or the given test paths), then smoke
+#     sel    : only the given test paths / -k expression
+#     bench  : bench.py (C2 headline + node Bloom + CPU baselines)
+#     c4|c5|c5z : the other workloads
+#     prof   : rocprofv3 kernel trace of the headline bench + PMC passes
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+PART=${1:-tests}
+shift || true
+step() { local name=$1 lim=$2; shift 2; echo "== $name"; timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "rc=$rc" >> "gpurun_out/$name.log"; tail -3 "gpurun_out/$name.log" | cut -c1-400; return $rc; }
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+for p in ${PART//,/ }; do
+  case $p in
+    tests)
+      step pytest_gpu 900 $PYT -m gpu ${@:-tests} || exit 1
+      step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    sel)
+      step pytest_sel 600 $PYT -m gpu "$@" || exit 1 ;;
+    bench)
+      step bench 400 python bench.py || exit 1 ;;
+    benchq)
+      step benchq 300 python bench.py --no-cpu || exit 1 ;;
+    c4)
+      step bench_c4 200 python bench.py --workload c4 || exit 1 ;;
+    c5)
+      step bench_c5 200 python bench.py --workload c5 || exit 1 ;;
+    c5z)
+      step bench_c5_zipf 200 python bench.py --workload c5 --zipf 1.1 || exit 1 ;;
+    prof)
+      B="python3 bench.py --no-cpu --no-bloom-replies"
+      rm -rf gpurun_out/prof_stats
+      step prof_bench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats -o run -- $B || exit 1 ;;
+    *) echo "unknown part $p"; exit 2 ;;
+  esac
+done
+exit 0

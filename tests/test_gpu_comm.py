@@ -1,7 +1,7 @@
 """RCCL merge layer on one GPU (a 1-rank communicator): the all-reduce paths
 run through RCCL and leave single-rank sketches unchanged, and every exchange
 kernel of rsk_comm.hip runs: the Bloom slice-OR exchanges with its own rank
-(send-to-self, or_rows_kernel, all-gather) and rsk_hll_fetch_rows with
+(RSK_FETCH_SELF: its slice to itself, or_rows_into_kernel, the slice back) and rsk_hll_fetch_rows with
 RSK_FETCH_SELF routes owned rows through gather_rows_kernel, a self
 send/recv and scatter_rows_kernel.  The N > 1 plan arithmetic is checked on
 CPU (tests/test_plan.py: the library's C++ plans = shard.py's) and the
@@ -116,14 +116,17 @@ def test_self_exchange_runs_every_kernel(engine, orc):
         out = np.zeros(16384, np.uint8)
         _lib.check(L.rsk_hll_get_registers(h, 2, out.ctypes.data, _lib.RSK_MEM_HOST))
         assert np.array_equal(out, refs[2])
-        # Bloom: the full slice-OR plan at N = 1 (odd size: the last slice is padded).
+        # Bloom: the full slice-OR plan at N = 1 with the rank as its own peer
+        # (odd size: the last slice is ragged).
         size, k = 1_000_003, 7
         keys = orc.gen_keys16(0x5EED0003, 0, 40000)
         b = ctypes.c_void_p()
         _lib.check(L.rsk_bloom_create(engine.ctx, size, k, ctypes.byref(b)))
         ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
         _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), None))
-        _lib.check(L.rsk_bloom_allreduce_or(b))
+        _lib.check(L.rsk_bloom_allreduce_or(b))  # N = 1: nothing moves
+        assert _prof(engine, "bloom_alltoall") == 0
+        shard.bloom_allreduce_or(b, flags=_lib.RSK_FETCH_SELF)
         assert _prof(engine, "bloom_alltoall") == 1 and _prof(engine, "bloom_or_rows") == 1
         assert _prof(engine, "bloom_allgather") == 1
         bits = np.zeros((size + 7) // 8, np.uint8)

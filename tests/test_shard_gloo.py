@@ -43,9 +43,10 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_merge_equals_single_process(world, orc):
-    n = 200_003
+@pytest.mark.parametrize("world,n", [(2, 200_003), (3, 200_003), (3, 10)])
+def test_sharded_merge_equals_single_process(world, n, orc):
+    """n = 10: a 96-bit filter of 4 words -- rank 0 merges them all, ranks 1
+    and 2 own empty slices (the plan's ragged tail)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
