@@ -9,12 +9,28 @@ SRC := $(wildcard redisson_amd/csrc/*.hip)
 HDR := $(wildcard redisson_amd/csrc/*.h) $(wildcard include/*.h)
 OBJ := $(patsubst redisson_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := redisson_amd/librsketch.so
+# The test / bench support library (include/rsketch_diag.h): generators,
+# microbenchmarks, tuning variants, route overrides.  Not linked to the
+# product library; it shares only the internal headers.
+DSRC := $(wildcard redisson_amd/csrc/diag/*.hip)
+DHDR := $(HDR) $(wildcard redisson_amd/csrc/diag/*.h)
+DOBJ := $(patsubst redisson_amd/csrc/diag/%.hip,build/diag/%.o,$(DSRC))
+DLIB := redisson_amd/librsketch_diag.so
 
-all: $(LIB) oracle
+all: $(LIB) $(DLIB) oracle
 
+# Product objects: hidden visibility, so the library exports exactly the C ABI
+# of include/rsketch.h (its declarations carry default visibility).
 build/%.o: redisson_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -fvisibility-inlines-hidden -c $< -o $@
+
+build/diag/%.o: redisson_amd/csrc/diag/%.hip $(DHDR)
+	@mkdir -p build/diag
+	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -fvisibility-inlines-hidden -c $< -o $@
+
+$(DLIB): $(DOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DOBJ) -Wl,-rpath,/opt/rocm/lib -Wl,-z,now
 
 # -z now: every HIP/RCCL symbol is bound when the library loads.  Lazily bound
 # calls made after `import torch` (which brings its own libamdhip64 into the
@@ -29,10 +45,10 @@ oracle:
 
 asm: $(SRC)
 	@mkdir -p build/asm
-	for f in $(SRC); do $(HIPCC) $(HIPFLAGS) -S --cuda-device-only -o build/asm/$$(basename $$f .hip).s $$f; done
+	for f in $(SRC) $(DSRC); do $(HIPCC) $(HIPFLAGS) -S --cuda-device-only -o build/asm/$$(basename $$f .hip).s $$f; done
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(DLIB)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean asm

@@ -126,7 +126,7 @@ def random_access_peaks(engine, nbytes: int, reps: int = 3):
     4-byte gathers and 4-byte atomicOr at uniformly random words (rsk_diag_membench)."""
     from redisson_amd import _lib, devmem
 
-    L = _lib.load()
+    D = _lib.diag()
     buf = devmem.DeviceBuffer(engine, nbytes)
     buf.zero()
     ops = 1 << 30
@@ -134,7 +134,7 @@ def random_access_peaks(engine, nbytes: int, reps: int = 3):
     for name, mode in (("gather4B", 1), ("atomicor4B", 2)):
         for _ in range(reps):
             ms = ctypes.c_double()
-            _lib.check(L.rsk_diag_membench(engine.ctx, mode, buf.ptr, nbytes, ops, ctypes.byref(ms)))
+            _lib.check_diag(D.rsk_diag_membench(engine.ctx, mode, buf.ptr, nbytes, ops, ctypes.byref(ms)))
             best[name] = max(best.get(name, 0.0), ops / (ms.value / 1e3))
     buf.free()
     return best
@@ -208,7 +208,8 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, rank: int = 0, world: i
             hits = int(out.to_numpy()[:m_q].sum())
             # untimed: the gathers the contains kernel issues for these queries
             pr = ctypes.c_uint64()
-            _lib.check(L.rsk_diag_bloom_contains_probes(engine.ctx, b, qs.ptr, m_q, out.ptr, ctypes.byref(pr)))
+            _lib.check_diag(_lib.diag().rsk_diag_bloom_contains_probes(engine.ctx, b, qs.ptr, m_q, out.ptr,
+                                                                       ctypes.byref(pr)))
             probes = pr.value
             bc = ctypes.c_uint64()
             _lib.check(L.rsk_bloom_bitcount(b, ctypes.byref(bc)))

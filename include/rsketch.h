@@ -15,8 +15,8 @@
  *    reference raises (see enum).  No C++ exception crosses this boundary.
  *  - The caller owns all buffers passed in.  Key buffers live either in host
  *    memory (RSK_MEM_HOST; copied over PCIe through two pinned host stages,
- *    filled by host threads -- RSK_STAGE_THREADS, default 8 -- while the
- *    other stage's DMA runs) or in device memory of the context's GPU
+ *    filled by host threads -- rsk_options.stage_threads, default 8 -- while
+ *    the other stage's DMA runs) or in device memory of the context's GPU
  *    (RSK_MEM_DEVICE; read in place).  Per-key outputs follow the keys'
  *    location; a RSK_MEM_DEVICE key or output pointer the GPU cannot reach
  *    (pageable host memory) is refused with RSK_ERR_INVALID_ARG.
@@ -34,6 +34,12 @@
 
 #ifdef __cplusplus
 extern "C" {
+#endif
+
+/* librsketch.so is built with hidden visibility: exactly the functions
+ * declared here are exported. */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
 #endif
 
 #define RSK_ABI_VERSION 1
@@ -62,6 +68,8 @@ typedef struct rsk_options {
   int32_t redis_version;  /* 320 = Redis 3.2.0 semantics (only supported value) */
   uint64_t staging_bytes; /* bytes per host->device chunk (each of the two pinned
                              stages holds one chunk + its offsets); 0 = default (256 MiB) */
+  uint32_t stage_threads; /* host threads filling a pinned stage; 0 = default (8) */
+  uint32_t reserved;      /* must be 0 */
 } rsk_options;
 
 /* A batch of keys: fixed stride (offsets == NULL, each key fixed_len bytes)
@@ -76,6 +84,15 @@ typedef struct rsk_keys {
   uint32_t location; /* rsk_mem */
 } rsk_keys;
 
+/* Completion callback of the asynchronous entry points (rsk_*_async), the
+ * C side of RHyperLogLogAsync / RBloomFilter futures (RHyperLogLogAsync.java:
+ * 22-33; CommandAsyncService.java:86-105 completes a Netty promise the same
+ * way).  status: RSK_OK (the call's device work finished); value: the reply
+ * -- PFADD's changed flag (0/1), PFCOUNT's count, the number of keys of a
+ * Bloom add/contains whose per-key outputs are in place.  It runs on a
+ * runtime thread, once per accepted call, and must not call librsketch. */
+typedef void (*rsk_done_fn)(void *user, int status, uint64_t value);
+
 /* ---------------------------------------------------------------- context */
 int rsk_init(const rsk_options *opts, rsk_ctx **out);
 int rsk_shutdown(rsk_ctx *ctx);
@@ -84,6 +101,11 @@ int rsk_abi_version(void);
 /* The HIP stream (hipStream_t) every call on this context is ordered on. */
 void *rsk_ctx_stream(rsk_ctx *ctx);
 int rsk_sync(rsk_ctx *ctx);
+/* Release the context's grow-on-demand scratch (device work and output
+ * buffers, pinned per-op buffer).  Large batches grow it (the add()-with-
+ * replies pipeline up to ~165 GB at 1B keys); it is kept for the next call
+ * otherwise.  Waits for the context's queued work. */
+int rsk_trim(rsk_ctx *ctx);
 /* Per-kernel device-time accounting with HIP events on the context stream
  * (used by bench.py for the roofline; off by default). */
 int rsk_prof_enable(rsk_ctx *ctx, int on);
@@ -136,11 +158,26 @@ int rsk_hll_count_union_batch(rsk_hll *h, const uint64_t *member_ids, uint32_t a
  * RedissonHyperLogLog.mergeWith/mergeWithAsync (:60-63,:91-97). */
 int rsk_hll_merge(rsk_hll *dst, uint64_t dst_id, rsk_hll *const *srcs, const uint64_t *src_ids, uint32_t k);
 /* Batched mergeWith within one pool: for i < n, PFMERGE dst_ids[i] src_ids[i],
- * in input order.  PFMERGE has no reply, so the call returns once the merges
- * are queued on the context's stream (mergeWithAsync): every later call is
- * ordered after them, and a device fault would surface at the next call that
- * waits for the device. */
+ * in input order.  Returns when the merges are done (rsk_hll_merge_batch_async
+ * returns once they are queued). */
 int rsk_hll_merge_batch(rsk_hll *h, const uint64_t *dst_ids, const uint64_t *src_ids, uint64_t n);
+
+/* Asynchronous twins (RHyperLogLogAsync: addAllAsync, countAsync,
+ * countWithAsync, mergeWithAsync; RedissonHyperLogLog.java:65-97).  Arguments
+ * are validated and the work enqueued on the context stream before the call
+ * returns (RSK_OK: cb fires exactly once later; any other status: it never
+ * fires).  Host key batches are copied into the call's own pinned buffer, so
+ * the caller may reuse them at once; batches above 256 MiB run before the
+ * call returns and cb fires on the calling thread.  Calls on different
+ * handles may be issued from any threads concurrently; every call is ordered
+ * on its context's stream like the synchronous ones. */
+int rsk_hll_add_async(rsk_hll *h, uint64_t id, const rsk_keys *keys, rsk_done_fn cb, void *user);
+int rsk_hll_count_async(rsk_hll *h, uint64_t id, rsk_done_fn cb, void *user);
+int rsk_hll_count_union_async(rsk_hll *const *hs, const uint64_t *ids, uint32_t k, rsk_done_fn cb, void *user);
+int rsk_hll_merge_async(rsk_hll *dst, uint64_t dst_id, rsk_hll *const *srcs, const uint64_t *src_ids, uint32_t k,
+                        rsk_done_fn cb, void *user);
+int rsk_hll_merge_batch_async(rsk_hll *h, const uint64_t *dst_ids, const uint64_t *src_ids, uint64_t n,
+                              rsk_done_fn cb, void *user);
 
 /* PFMERGE from raw registers (one byte per register, any location): the
  * receive side of the multi-GPU RCCL MAX merge. */
@@ -189,6 +226,12 @@ int rsk_bloom_contains(rsk_bloom *b, const rsk_keys *keys, uint8_t *out);
 /* count() (RedissonBloomFilter.java:188-199) and the BITCOUNT it uses. */
 int rsk_bloom_count(rsk_bloom *b, int32_t *out);
 int rsk_bloom_bitcount(rsk_bloom *b, uint64_t *out);
+
+/* Asynchronous add / contains (the futures of RBloomFilter's batch calls):
+ * conventions as for rsk_hll_add_async; per-key outputs are in place when cb
+ * fires (host outputs must stay valid until then). */
+int rsk_bloom_add_async(rsk_bloom *b, const rsk_keys *keys, uint8_t *added_out, rsk_done_fn cb, void *user);
+int rsk_bloom_contains_async(rsk_bloom *b, const rsk_keys *keys, uint8_t *out, rsk_done_fn cb, void *user);
 
 /* Hash.hashToBase64 (src/main/java/org/redisson/misc/Hash.java:29-40) of each
  * key: farmUo and xx_r39 as two big-endian longs, Base64, trailing "=="
@@ -307,6 +350,10 @@ int rsk_plan_bloom_slice_words(uint64_t nwords, int nranks, uint64_t *words);
  * owner.  RSK_ERR_INVALID_ARG if an id is >= n. */
 int rsk_plan_fetch(uint64_t n, int nranks, int rank, const uint64_t *ids, uint64_t n_ids, uint32_t flags,
                    uint64_t *want_out, uint64_t *n_want, uint64_t *counts_out);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,10 @@
 /*
- * rsketch_diag.h -- benchmark and test support exported by librsketch.so:
- * memory-system microbenchmarks, kernel tuning variants and the synthetic
- * input streams of SURVEY.md 8d generated on the device.  Not part of the
- * product ABI (include/rsketch.h); bench.py, scripts/ and tests/ use it.
+ * rsketch_diag.h -- benchmark and test support, exported by a library of its
+ * own, librsketch_diag.so (the product library librsketch.so exports only
+ * include/rsketch.h): memory-system microbenchmarks, kernel tuning variants,
+ * the synthetic input streams of SURVEY.md 8d generated on the device, and
+ * the route overrides tests use to force every pipeline of the library.
+ * bench.py, scripts/ and tests/ use it.  Errors: rsk_diag_last_error().
  */
 #ifndef RSKETCH_DIAG_H
 #define RSKETCH_DIAG_H
@@ -12,14 +14,30 @@
 extern "C" {
 #endif
 
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
+const char *rsk_diag_last_error(void);
+
+/* Route override of a context (the product library has no other knob):
+ *   bloom_stream  slice-routed insert: 0 auto, 1 at any batch size, -1 never
+ *   bloom_part    exact-offset insert: 0 auto, 1 at any batch size, -1 never
+ *   bloom_chunk   probes per chunk of the slice-routed insert (0 = default)
+ *   sa_tiny       1: sub-regions of 32 probes (forces the overflow fallbacks)
+ *   sa_parts      sa2 / rp2 parts per coarse bin (0 = default)
+ *   reply         add() replies: 0 auto, 1 first-key pipeline at any size, -1 sort path
+ *   reply_chunk   probes per chunk of the first-key pipeline (0 = default)
+ *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
+ *   reset         every route back to automatic
+ * Every route gives bit-identical results; they differ in speed only. */
+int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
+
 /* --------------------------------------------------------- diagnostics */
 /* Memory-system microbenchmark on a device buffer (roofline denominators):
  * mode 0 stream read, 1 random 4 B gathers, 2 random 4 B atomicOr,
  * 3 stream copy (buffer halves).  *ms = device time of the one launch. */
 int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
-/* hipOccupancyMaxActiveBlocksPerMultiprocessor for a persistent Bloom kernel
- * (which 0: sa1, 1: append apply): workgroups per CU and the HIP error code. */
-int rsk_diag_occupancy(int which, int *per_cu, int *hip_error);
 /* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */
 int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint64_t n, double *ms);
 /* Time one launch of a variant of the blob+offsets PFADD kernel (slabs only):
@@ -52,6 +70,10 @@ int rsk_gen_queries16(rsk_ctx *ctx, uint64_t qseed, uint64_t iseed, uint64_t n_i
  * bytes into dev_blob (capacity blob_cap). */
 int rsk_gen_varlen(rsk_ctx *ctx, uint64_t seed, uint64_t start, uint64_t n, uint64_t *dev_offsets, void *dev_blob,
                    uint64_t blob_cap, uint64_t *total_bytes);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
 
 #ifdef __cplusplus
 }

@@ -3,19 +3,29 @@
  * returns when GPU sketches are enabled.  The executor arrives through the
  * constructor as for every Redisson object (RedissonObject.java:34-48); the
  * public interface is unchanged.  add/addAll/count/countWith/mergeWith and their
- * async twins (RedissonHyperLogLog.java:40-97) run on librsketch; expire/rename
- * and the other RExpirable calls stay with the Redis executor.
+ * async twins (RedissonHyperLogLog.java:40-97) run on librsketch, addressed by
+ * name in the context's keyspace (two instances of one name are one sketch;
+ * count of a name nobody wrote is 0 and creates nothing, as PFCOUNT).
  *
  * addAll implements the INTENDED "PFADD key e1..en": the fork passes the name
  * twice through varargs (RedissonHyperLogLog.java:70-76) and so adds one element.
+ *
+ * The key lives in GPU memory, not in Redis: delete / isExists / rename /
+ * renamenx act on the GPU keyspace; a TTL cannot be honoured, so expire /
+ * expireAt fail (UnsupportedOperationException) instead of being silently
+ * dropped, clearExpire answers false and remainTimeToLive -1 (no TTL, as
+ * PERSIST / PTTL answer for a key without one); move / migrate (other Redis
+ * databases or hosts) fail likewise.
  */
 package org.redisson.gpu;
 
-import java.util.Arrays;
 import java.util.Collection;
-import java.util.concurrent.Callable;
+import java.util.Collections;
+import java.util.Date;
+import java.util.concurrent.TimeUnit;
 
 import io.netty.util.concurrent.Future;
+import io.netty.util.concurrent.Promise;
 
 import org.redisson.RedissonHyperLogLog;
 import org.redisson.client.codec.Codec;
@@ -36,103 +46,174 @@ public class GpuHyperLogLog<V> extends RedissonHyperLogLog<V> {
         this(commandExecutor.getConnectionManager().getCodec(), commandExecutor, name, gpu);
     }
 
-    private Callable<Boolean> addTask(final Collection<V> objects) {
-        return new Callable<Boolean>() {
-            public Boolean call() {
-                KeyBuffer kb = KeyBuffer.encode(valueCodec, objects);
-                return RSketchNative.hllAdd(gpu.hll(getName()), 0, kb.bytes, kb.offsets, kb.n);
-            }
-        };
-    }
-
-    private Callable<Long> countTask(final String... others) {
-        return new Callable<Long>() {
-            public Long call() {
-                if (others.length == 0) {
-                    return RSketchNative.hllCount(gpu.hll(getName()), 0);
-                }
-                long[] hs = new long[others.length + 1];
-                long[] ids = new long[others.length + 1];
-                hs[0] = gpu.hll(getName());
-                for (int i = 0; i < others.length; i++) {
-                    hs[i + 1] = gpu.hll(others[i]);
-                }
-                return RSketchNative.hllCountUnion(hs, ids);
-            }
-        };
-    }
-
-    private Callable<Void> mergeTask(final String... others) {
-        return new Callable<Void>() {
-            public Void call() {
-                long[] hs = new long[others.length];
-                long[] ids = new long[others.length];
-                for (int i = 0; i < others.length; i++) {
-                    hs[i] = gpu.hll(others[i]);
-                }
-                RSketchNative.hllMerge(gpu.hll(getName()), 0, hs, ids);
-                return null;
-            }
-        };
+    private String[] withSelf(String... others) {
+        String[] names = new String[others.length + 1];
+        names[0] = getName();
+        System.arraycopy(others, 0, names, 1, others.length);
+        return names;
     }
 
     @Override
     public boolean add(V obj) {
-        return gpu.call(addTask(Arrays.asList(obj)));
+        KeyBuffer kb = KeyBuffer.encodeOne(valueCodec, obj);
+        return RSketchNative.hllAdd(gpu.space, getName(), kb.bytes, kb.offsets, 1);
     }
 
     @Override
     public boolean addAll(Collection<V> objects) {
-        return gpu.call(addTask(objects));
+        KeyBuffer kb = KeyBuffer.encode(valueCodec, objects);
+        return RSketchNative.hllAdd(gpu.space, getName(), kb.bytes, kb.offsets, kb.n);
+    }
+
+    /* n x PFADD in input order (the RBatch form): one reply per element. */
+    public boolean[] addEach(Collection<V> objects) {
+        KeyBuffer kb = KeyBuffer.encode(valueCodec, objects);
+        return RSketchNative.hllAddEach(gpu.space, getName(), kb.bytes, kb.offsets, kb.n);
     }
 
     @Override
     public long count() {
-        return gpu.call(countTask());
+        return RSketchNative.hllCount(gpu.space, getName());
     }
 
     @Override
     public long countWith(String... otherLogNames) {
-        return gpu.call(countTask(otherLogNames));
+        return RSketchNative.hllCountWith(gpu.space, withSelf(otherLogNames));
     }
 
     @Override
     public void mergeWith(String... otherLogNames) {
-        gpu.call(mergeTask(otherLogNames));
+        RSketchNative.hllMergeWith(gpu.space, getName(), otherLogNames);
     }
 
     @Override
     public Future<Boolean> addAsync(V obj) {
-        return gpu.callAsync(addTask(Arrays.asList(obj)));
+        return addAllAsync(Collections.singletonList(obj));
     }
 
     @Override
     public Future<Boolean> addAllAsync(Collection<V> objects) {
-        return gpu.callAsync(addTask(objects));
+        Promise<Boolean> p = gpu.newPromise();
+        try {
+            KeyBuffer kb = KeyBuffer.encode(valueCodec, objects);
+            RSketchNative.hllAddAsync(gpu.space, getName(), kb.bytes, kb.offsets, kb.n, p);
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
     }
 
     @Override
     public Future<Long> countAsync() {
-        return gpu.callAsync(countTask());
+        Promise<Long> p = gpu.newPromise();
+        try {
+            RSketchNative.hllCountAsync(gpu.space, getName(), p);
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
     }
 
     @Override
     public Future<Long> countWithAsync(String... otherLogNames) {
-        return gpu.callAsync(countTask(otherLogNames));
+        Promise<Long> p = gpu.newPromise();
+        try {
+            RSketchNative.hllCountWithAsync(gpu.space, withSelf(otherLogNames), p);
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
     }
 
     @Override
     public Future<Void> mergeWithAsync(String... otherLogNames) {
-        return gpu.callAsync(mergeTask(otherLogNames));
+        Promise<Void> p = gpu.newPromise();
+        try {
+            RSketchNative.hllMergeWithAsync(gpu.space, getName(), otherLogNames, p);
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
+    }
+
+    // ---------------------------------------------------------------- keyspace
+    @Override
+    public Future<Boolean> deleteAsync() {
+        Promise<Boolean> p = gpu.newPromise();
+        try {
+            p.setSuccess(gpu.delete(getName()));
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
     }
 
     @Override
-    public boolean delete() {
-        return gpu.call(new Callable<Boolean>() {
-            public Boolean call() {
-                RSketchNative.hllDelete(gpu.hll(getName()), 0);
-                return true;
-            }
-        });
+    public Future<Boolean> isExistsAsync() {
+        Promise<Boolean> p = gpu.newPromise();
+        p.setSuccess(gpu.type(getName()) != RSketchNative.NONE);
+        return p;
+    }
+
+    @Override
+    public Future<Void> renameAsync(String newName) {
+        Promise<Void> p = gpu.newPromise();
+        try {
+            GpuKeyspace.rename(gpu, getName(), newName, false);
+            p.setSuccess(null);
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
+    }
+
+    @Override
+    public Future<Boolean> renamenxAsync(String newName) {
+        Promise<Boolean> p = gpu.newPromise();
+        try {
+            p.setSuccess(GpuKeyspace.rename(gpu, getName(), newName, true));
+        } catch (RuntimeException e) {
+            p.tryFailure(e);
+        }
+        return p;
+    }
+
+    @Override
+    public Future<Boolean> expireAsync(long timeToLive, TimeUnit timeUnit) {
+        return gpu.failed(GpuKeyspace.noTtl());
+    }
+
+    @Override
+    public Future<Boolean> expireAtAsync(long timestamp) {
+        return gpu.failed(GpuKeyspace.noTtl());
+    }
+
+    @Override
+    public Future<Boolean> expireAtAsync(Date timestamp) {
+        return gpu.failed(GpuKeyspace.noTtl());
+    }
+
+    @Override
+    public Future<Boolean> clearExpireAsync() {
+        Promise<Boolean> p = gpu.newPromise();
+        p.setSuccess(Boolean.FALSE);
+        return p;
+    }
+
+    @Override
+    public Future<Long> remainTimeToLiveAsync() {
+        Promise<Long> p = gpu.newPromise();
+        p.setSuccess(Long.valueOf(-1));
+        return p;
+    }
+
+    @Override
+    public Future<Boolean> moveAsync(int database) {
+        return gpu.failed(GpuKeyspace.notOnGpu("move"));
+    }
+
+    @Override
+    public Future<Void> migrateAsync(String host, int port, int database) {
+        return gpu.failed(GpuKeyspace.notOnGpu("migrate"));
     }
 }

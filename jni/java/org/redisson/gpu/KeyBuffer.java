@@ -27,17 +27,28 @@ final class KeyBuffer {
         this.n = n;
     }
 
+    /* One element's codec bytes (IllegalArgumentException on a codec failure, :170-178). */
+    static byte[] encodeElement(Codec codec, Object o) {
+        try {
+            return codec.getValueEncoder().encode(o);
+        } catch (IOException e) {
+            throw new IllegalArgumentException(e);
+        }
+    }
+
     static KeyBuffer encode(Codec codec, Collection<?> objects) {
         List<byte[]> enc = new ArrayList<byte[]>(objects.size());
-        long total = 0;
         for (Object o : objects) {
-            try {
-                byte[] b = codec.getValueEncoder().encode(o);
-                enc.add(b);
-                total += b.length;
-            } catch (IOException e) {
-                throw new IllegalArgumentException(e);
-            }
+            enc.add(encodeElement(codec, o));
+        }
+        return ofEncoded(enc);
+    }
+
+    /* Elements already encoded (a batch queued element by element). */
+    static KeyBuffer ofEncoded(List<byte[]> enc) {
+        long total = 0;
+        for (byte[] b : enc) {
+            total += b.length;
         }
         if (total > Integer.MAX_VALUE) {
             throw new IllegalArgumentException("batch larger than 2 GiB: split it");

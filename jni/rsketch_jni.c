@@ -4,15 +4,30 @@
  *
  * Needs a JDK's jni.h, which this image lacks: it is source here and is built
  * where JAVA_HOME exists (make -C jni jni).  Every method follows one pattern:
- * fetch direct-buffer addresses and capacities, call the shim, throw
+ * fetch names / direct-buffer addresses and capacities, call the shim, throw
  * rsk_shim_exception_class(rc) with rsk_shim_last_error() on failure.  The
- * shim (all checks, all conversions) is what tests/c/shim_caller.c runs on
- * the GPU.
+ * shim (all checks, the name -> object keyspace, the config guard) is what
+ * tests/c/shim_caller.c runs on the GPU.
+ *
+ * Async methods take the Netty Promise the Java object returns; the shim's
+ * completion callback (a HIP runtime thread) attaches to the JVM and calls
+ * RSketchNative.complete(promise, kind, value, replies), which completes it --
+ * the listeners then run on the promise's executor (the Netty event loop), as
+ * for a Redis reply (CommandAsyncService.java:86-105).
  */
 #include <jni.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "rsketch_shim.h"
+
+static JavaVM *g_vm;
+
+JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM *vm, void *reserved) {
+  (void)reserved;
+  g_vm = vm;
+  return JNI_VERSION_1_6;
+}
 
 static rsk_shim_buf direct(JNIEnv *env, jobject buf) {
   rsk_shim_buf b = {NULL, 0};
@@ -32,146 +47,461 @@ static int raise(JNIEnv *env, int rc) {
   return 1;
 }
 
+static int throw_iae(JNIEnv *env, const char *msg) {
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+  return 1;
+}
+
+/* A Java String as modified UTF-8 (NULL with a pending exception on failure). */
+typedef struct {
+  jstring s;
+  const char *c;
+} jname;
+
+static int name_get(JNIEnv *env, jstring s, jname *out) {
+  out->s = s;
+  out->c = NULL;
+  if (!s) return throw_iae(env, "name is null");
+  out->c = (*env)->GetStringUTFChars(env, s, NULL);
+  return out->c == NULL; /* OutOfMemoryError pending */
+}
+static void name_put(JNIEnv *env, jname *n) {
+  if (n->c) (*env)->ReleaseStringUTFChars(env, n->s, n->c);
+}
+
+/* String[] -> const char *[] (at most 4096 names). */
+typedef struct {
+  int k;
+  jname *ns;
+  const char **cs;
+} jnames;
+
+/* 0 on success; 1 with a pending exception. */
+static int names_get(JNIEnv *env, jobjectArray arr, jnames *out) {
+  out->k = 0;
+  out->ns = NULL;
+  out->cs = NULL;
+  if (!arr) return throw_iae(env, "names is null");
+  const jsize k = (*env)->GetArrayLength(env, arr);
+  if (k > 4096) return throw_iae(env, "at most 4096 keys per call");
+  out->ns = calloc((size_t)(k > 0 ? k : 1), sizeof(jname));
+  out->cs = calloc((size_t)(k > 0 ? k : 1), sizeof(const char *));
+  if (!out->ns || !out->cs) {
+    free(out->ns);
+    free(out->cs);
+    out->ns = NULL;
+    out->cs = NULL;
+    jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (c) (*env)->ThrowNew(env, c, "names");
+    return 1;
+  }
+  for (jsize i = 0; i < k; ++i) {
+    if (name_get(env, (jstring)(*env)->GetObjectArrayElement(env, arr, i), &out->ns[i])) {
+      out->k = (int)i;
+      return 1;
+    }
+    out->cs[i] = out->ns[i].c;
+  }
+  out->k = (int)k;
+  return 0;
+}
+static void names_put(JNIEnv *env, jnames *n) {
+  for (int i = 0; i < n->k; ++i) name_put(env, &n->ns[i]);
+  free(n->ns);
+  free(n->cs);
+  n->ns = NULL;
+  n->cs = NULL;
+  n->k = 0;
+}
+
 #define JNI_FN(ret, name) JNIEXPORT ret JNICALL Java_org_redisson_gpu_RSketchNative_##name
 
-JNI_FN(jlong, init)(JNIEnv *env, jclass cls, jint device) {
+JNI_FN(jlong, init)(JNIEnv *env, jclass cls, jint device, jboolean extended) {
   (void)cls;
-  int64_t ctx = 0;
-  return raise(env, rsk_shim_init(device, &ctx)) ? 0 : (jlong)ctx;
+  int64_t s = 0;
+  return raise(env, rsk_shim_init(device, extended ? 1 : 0, &s)) ? 0 : (jlong)s;
 }
 
-JNI_FN(void, shutdown)(JNIEnv *env, jclass cls, jlong ctx) {
+JNI_FN(void, shutdown)(JNIEnv *env, jclass cls, jlong space) {
   (void)cls;
-  raise(env, rsk_shim_shutdown(ctx));
+  raise(env, rsk_shim_shutdown(space));
 }
 
-JNI_FN(jlong, hllCreate)(JNIEnv *env, jclass cls, jlong ctx, jlong n) {
+JNI_FN(jint, type)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
+  jname n;
+  if (name_get(env, name, &n)) return 0;
+  int32_t t = 0;
   int64_t h = 0;
-  return raise(env, rsk_shim_hll_create(ctx, n, &h)) ? 0 : (jlong)h;
+  const int rc = rsk_shim_lookup(space, n.c, &t, &h);
+  name_put(env, &n);
+  return raise(env, rc) ? 0 : (jint)t;
 }
 
-JNI_FN(void, hllDestroy)(JNIEnv *env, jclass cls, jlong hll) {
+JNI_FN(jboolean, delete)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
-  raise(env, rsk_shim_hll_destroy(hll));
+  jname n;
+  if (name_get(env, name, &n)) return JNI_FALSE;
+  int32_t d = 0;
+  const int rc = rsk_shim_delete(space, n.c, &d);
+  name_put(env, &n);
+  return raise(env, rc) ? JNI_FALSE : (d ? JNI_TRUE : JNI_FALSE);
 }
 
-JNI_FN(jboolean, hllAdd)(JNIEnv *env, jclass cls, jlong hll, jlong id, jobject keys, jobject offsets, jlong n) {
+JNI_FN(jboolean, rename)(JNIEnv *env, jclass cls, jlong space, jstring oldName, jstring newName, jboolean nx) {
   (void)cls;
+  jname a, b;
+  if (name_get(env, oldName, &a)) return JNI_FALSE;
+  if (name_get(env, newName, &b)) {
+    name_put(env, &a);
+    return JNI_FALSE;
+  }
+  int32_t done = 0;
+  const int rc = rsk_shim_rename(space, a.c, b.c, nx ? 1 : 0, &done);
+  name_put(env, &b);
+  name_put(env, &a);
+  return raise(env, rc) ? JNI_FALSE : (done ? JNI_TRUE : JNI_FALSE);
+}
+
+/* ------------------------------------------------------------------ HLL */
+JNI_FN(jboolean, hllAdd)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets, jlong n) {
+  (void)cls;
+  jname nm;
+  if (name_get(env, name, &nm)) return JNI_FALSE;
   uint8_t changed = 0;
-  if (raise(env, rsk_shim_hll_add(hll, id, direct(env, keys), direct(env, offsets), n, &changed))) return JNI_FALSE;
+  const int rc = rsk_shim_hll_add(space, nm.c, direct(env, keys), direct(env, offsets), n, &changed);
+  name_put(env, &nm);
+  if (raise(env, rc)) return JNI_FALSE;
   return changed ? JNI_TRUE : JNI_FALSE;
 }
 
-/* boolean[] replies: jboolean is an unsigned byte, so the library writes the
- * replies straight into the array's elements. */
-JNI_FN(jbooleanArray, hllAddEach)(JNIEnv *env, jclass cls, jlong hll, jlong id, jobject keys, jobject offsets,
-                                  jlong n) {
-  (void)cls;
-  if (n < 0 || n > 0x7fffffff) {
-    raise(env, RSK_ERR_INVALID_ARG);
-    return NULL;
-  }
+/* Replies into a fresh boolean[] (jboolean is an unsigned byte): the shim
+ * writes a C buffer, copied with SetBooleanArrayRegion (no pinned array
+ * element pointers to check or release). */
+static jbooleanArray replies_array(JNIEnv *env, const uint8_t *r, jlong n) {
   jbooleanArray arr = (*env)->NewBooleanArray(env, (jsize)n);
-  if (!arr) return NULL;
-  jboolean *r = (*env)->GetBooleanArrayElements(env, arr, NULL);
-  int rc = rsk_shim_hll_add_each(hll, id, direct(env, keys), direct(env, offsets), n, (uint8_t *)r, n);
-  (*env)->ReleaseBooleanArrayElements(env, arr, r, rc ? JNI_ABORT : 0);
-  return raise(env, rc) ? NULL : arr;
-}
-
-JNI_FN(jlong, hllCount)(JNIEnv *env, jclass cls, jlong hll, jlong id) {
-  (void)cls;
-  int64_t v = 0;
-  return raise(env, rsk_shim_hll_count(hll, id, &v)) ? 0 : (jlong)v;
-}
-
-JNI_FN(jlong, hllCountUnion)(JNIEnv *env, jclass cls, jlongArray hlls, jlongArray ids) {
-  (void)cls;
-  const jsize k = (*env)->GetArrayLength(env, hlls);
-  if (k != (*env)->GetArrayLength(env, ids)) {
-    raise(env, RSK_ERR_INVALID_ARG);
-    return 0;
-  }
-  jlong *h = (*env)->GetLongArrayElements(env, hlls, NULL);
-  jlong *i = (*env)->GetLongArrayElements(env, ids, NULL);
-  int64_t v = 0;
-  int rc = rsk_shim_hll_count_union((const int64_t *)h, (const int64_t *)i, (int32_t)k, &v);
-  (*env)->ReleaseLongArrayElements(env, ids, i, JNI_ABORT);
-  (*env)->ReleaseLongArrayElements(env, hlls, h, JNI_ABORT);
-  return raise(env, rc) ? 0 : (jlong)v;
-}
-
-JNI_FN(void, hllMerge)(JNIEnv *env, jclass cls, jlong dst, jlong dstId, jlongArray srcs, jlongArray srcIds) {
-  (void)cls;
-  const jsize k = (*env)->GetArrayLength(env, srcs);
-  if (k != (*env)->GetArrayLength(env, srcIds)) {
-    raise(env, RSK_ERR_INVALID_ARG);
-    return;
-  }
-  jlong *h = (*env)->GetLongArrayElements(env, srcs, NULL);
-  jlong *i = (*env)->GetLongArrayElements(env, srcIds, NULL);
-  int rc = rsk_shim_hll_merge(dst, dstId, (const int64_t *)h, (const int64_t *)i, (int32_t)k);
-  (*env)->ReleaseLongArrayElements(env, srcIds, i, JNI_ABORT);
-  (*env)->ReleaseLongArrayElements(env, srcs, h, JNI_ABORT);
-  raise(env, rc);
-}
-
-JNI_FN(void, hllDelete)(JNIEnv *env, jclass cls, jlong hll, jlong id) {
-  (void)cls;
-  raise(env, rsk_shim_hll_delete(hll, id));
-}
-
-/* {size, k} */
-JNI_FN(jlongArray, bloomParams)(JNIEnv *env, jclass cls, jlong n, jdouble p, jboolean extended) {
-  (void)cls;
-  int64_t size = 0;
-  int32_t k = 0;
-  if (raise(env, rsk_shim_bloom_params(n, p, extended ? 1 : 0, &size, &k))) return NULL;
-  jlongArray arr = (*env)->NewLongArray(env, 2);
-  if (!arr) return NULL;
-  const jlong v[2] = {(jlong)size, (jlong)k};
-  (*env)->SetLongArrayRegion(env, arr, 0, 2, v);
+  if (arr && n) (*env)->SetBooleanArrayRegion(env, arr, 0, (jsize)n, (const jboolean *)r);
   return arr;
 }
 
-JNI_FN(jlong, bloomCreate)(JNIEnv *env, jclass cls, jlong ctx, jlong size, jint k) {
-  (void)cls;
-  int64_t b = 0;
-  return raise(env, rsk_shim_bloom_create(ctx, size, k, &b)) ? 0 : (jlong)b;
-}
-
-JNI_FN(void, bloomDestroy)(JNIEnv *env, jclass cls, jlong bloom) {
-  (void)cls;
-  raise(env, rsk_shim_bloom_destroy(bloom));
-}
-
-static jbooleanArray bloom_batch(JNIEnv *env, jlong bloom, jobject keys, jobject offsets, jlong n, int add) {
+static uint8_t *reply_buf(JNIEnv *env, jlong n) {
   if (n < 0 || n > 0x7fffffff) {
-    raise(env, RSK_ERR_INVALID_ARG);
+    throw_iae(env, "batch larger than 2^31 - 1 elements");
     return NULL;
   }
-  jbooleanArray arr = (*env)->NewBooleanArray(env, (jsize)n);
-  if (!arr) return NULL;
-  jboolean *r = (*env)->GetBooleanArrayElements(env, arr, NULL);
-  int rc = add ? rsk_shim_bloom_add(bloom, direct(env, keys), direct(env, offsets), n, (uint8_t *)r, n)
-               : rsk_shim_bloom_contains(bloom, direct(env, keys), direct(env, offsets), n, (uint8_t *)r, n);
-  (*env)->ReleaseBooleanArrayElements(env, arr, r, rc ? JNI_ABORT : 0);
-  return raise(env, rc) ? NULL : arr;
+  uint8_t *r = malloc((size_t)(n > 0 ? n : 1));
+  if (!r) {
+    jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (c) (*env)->ThrowNew(env, c, "reply buffer");
+  }
+  return r;
 }
 
-JNI_FN(jbooleanArray, bloomAdd)(JNIEnv *env, jclass cls, jlong bloom, jobject keys, jobject offsets, jlong n) {
+JNI_FN(jbooleanArray, hllAddEach)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets,
+                                  jlong n) {
   (void)cls;
-  return bloom_batch(env, bloom, keys, offsets, n, 1);
+  uint8_t *r = reply_buf(env, n);
+  if (!r) return NULL;
+  jname nm;
+  if (name_get(env, name, &nm)) {
+    free(r);
+    return NULL;
+  }
+  const int rc = rsk_shim_hll_add_each(space, nm.c, direct(env, keys), direct(env, offsets), n, r, n);
+  name_put(env, &nm);
+  jbooleanArray arr = raise(env, rc) ? NULL : replies_array(env, r, n);
+  free(r);
+  return arr;
 }
 
-JNI_FN(jbooleanArray, bloomContains)(JNIEnv *env, jclass cls, jlong bloom, jobject keys, jobject offsets, jlong n) {
+JNI_FN(jlong, hllCount)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
-  return bloom_batch(env, bloom, keys, offsets, n, 0);
+  jname nm;
+  if (name_get(env, name, &nm)) return 0;
+  int64_t v = 0;
+  const int rc = rsk_shim_hll_count(space, nm.c, &v);
+  name_put(env, &nm);
+  return raise(env, rc) ? 0 : (jlong)v;
 }
 
-JNI_FN(jint, bloomCount)(JNIEnv *env, jclass cls, jlong bloom) {
+JNI_FN(jlong, hllCountWith)(JNIEnv *env, jclass cls, jlong space, jobjectArray names) {
   (void)cls;
+  jnames ns;
+  if (names_get(env, names, &ns)) {
+    names_put(env, &ns);
+    return 0;
+  }
+  int64_t v = 0;
+  const int rc = rsk_shim_hll_count_with(space, ns.cs, ns.k, &v);
+  names_put(env, &ns);
+  return raise(env, rc) ? 0 : (jlong)v;
+}
+
+JNI_FN(void, hllMergeWith)(JNIEnv *env, jclass cls, jlong space, jstring dst, jobjectArray srcs) {
+  (void)cls;
+  jname d;
+  if (name_get(env, dst, &d)) return;
+  jnames ns;
+  if (names_get(env, srcs, &ns)) {
+    names_put(env, &ns);
+    name_put(env, &d);
+    return;
+  }
+  const int rc = rsk_shim_hll_merge_with(space, d.c, ns.cs, ns.k);
+  names_put(env, &ns);
+  name_put(env, &d);
+  raise(env, rc);
+}
+
+JNI_FN(jbooleanArray, batchHllAdd)(JNIEnv *env, jclass cls, jlong space, jobjectArray names, jintArray nameOf,
+                                   jobject keys, jobject offsets, jlong n) {
+  (void)cls;
+  if (!nameOf || (*env)->GetArrayLength(env, nameOf) < n) {
+    throw_iae(env, "nameOf shorter than the batch");
+    return NULL;
+  }
+  uint8_t *r = reply_buf(env, n);
+  if (!r) return NULL;
+  int32_t *of = malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  if (!of) {
+    free(r);
+    return NULL;
+  }
+  if (n) (*env)->GetIntArrayRegion(env, nameOf, 0, (jsize)n, (jint *)of);
+  jnames ns;
+  jbooleanArray arr = NULL;
+  if (!names_get(env, names, &ns)) {
+    const int rc = rsk_shim_batch_hll_add(space, ns.cs, ns.k, of, direct(env, keys), direct(env, offsets), n, r, n);
+    if (!raise(env, rc)) arr = replies_array(env, r, n);
+  }
+  names_put(env, &ns);
+  free(of);
+  free(r);
+  return arr;
+}
+
+/* --------------------------------------------------------------- async */
+enum { K_BOOL = 0, K_LONG = 1, K_VOID = 2, K_ARRAY = 3 };
+
+typedef struct {
+  jobject promise; /* global reference */
+  int kind;
+  uint8_t *out; /* K_ARRAY: the replies, n bytes */
+  int64_t n;
+} job;
+
+/* The shim's callback, on a HIP runtime thread (or the calling thread for an
+ * answer known at once): attach, complete the promise through Java, detach
+ * nothing (daemon attachment stays for the runtime's thread). */
+static void jni_done(void *user, int status, uint64_t value) {
+  job *j = user;
+  JNIEnv *env = NULL;
+  int attached = 0;
+  if ((*g_vm)->GetEnv(g_vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK) {
+    if ((*g_vm)->AttachCurrentThreadAsDaemon(g_vm, (void **)&env, NULL) != JNI_OK) return;
+    attached = 1;
+  }
+  (void)attached;
+  jclass cls = (*env)->FindClass(env, "org/redisson/gpu/RSketchNative");
+  jmethodID m = cls ? (*env)->GetStaticMethodID(env, cls, "complete", "(Ljava/lang/Object;IIJ[Z)V") : NULL;
+  jbooleanArray arr = NULL;
+  if (j->kind == K_ARRAY && status == RSK_OK) arr = replies_array(env, j->out, j->n);
+  if (m) (*env)->CallStaticVoidMethod(env, cls, m, j->promise, (jint)j->kind, (jint)status, (jlong)value, arr);
+  if ((*env)->ExceptionCheck(env)) (*env)->ExceptionClear(env);
+  (*env)->DeleteGlobalRef(env, j->promise);
+  if (arr) (*env)->DeleteLocalRef(env, arr);
+  if (cls) (*env)->DeleteLocalRef(env, cls);
+  free(j->out);
+  free(j);
+}
+
+static job *job_new(JNIEnv *env, jobject promise, int kind, int64_t n) {
+  job *j = calloc(1, sizeof *j);
+  if (!j) return NULL;
+  j->kind = kind;
+  j->n = n;
+  if (kind == K_ARRAY) {
+    j->out = malloc((size_t)(n > 0 ? n : 1));
+    if (!j->out) {
+      free(j);
+      return NULL;
+    }
+  }
+  j->promise = (*env)->NewGlobalRef(env, promise);
+  return j;
+}
+
+/* A call the shim refused never fires: free the job, throw. */
+static void job_refused(JNIEnv *env, job *j, int rc) {
+  (*env)->DeleteGlobalRef(env, j->promise);
+  free(j->out);
+  free(j);
+  raise(env, rc);
+}
+
+JNI_FN(void, hllAddAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets, jlong n,
+                          jobject promise) {
+  (void)cls;
+  jname nm;
+  if (name_get(env, name, &nm)) return;
+  job *j = job_new(env, promise, K_BOOL, 0);
+  if (!j) {
+    name_put(env, &nm);
+    return;
+  }
+  const int rc = rsk_shim_hll_add_async(space, nm.c, direct(env, keys), direct(env, offsets), n, jni_done, j);
+  name_put(env, &nm);
+  if (rc) job_refused(env, j, rc);
+}
+
+JNI_FN(void, hllCountAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject promise) {
+  (void)cls;
+  jname nm;
+  if (name_get(env, name, &nm)) return;
+  job *j = job_new(env, promise, K_LONG, 0);
+  if (!j) {
+    name_put(env, &nm);
+    return;
+  }
+  const int rc = rsk_shim_hll_count_async(space, nm.c, jni_done, j);
+  name_put(env, &nm);
+  if (rc) job_refused(env, j, rc);
+}
+
+JNI_FN(void, hllCountWithAsync)(JNIEnv *env, jclass cls, jlong space, jobjectArray names, jobject promise) {
+  (void)cls;
+  jnames ns;
+  if (names_get(env, names, &ns)) {
+    names_put(env, &ns);
+    return;
+  }
+  job *j = job_new(env, promise, K_LONG, 0);
+  const int rc = j ? rsk_shim_hll_count_with_async(space, ns.cs, ns.k, jni_done, j) : RSK_ERR_OUT_OF_MEMORY;
+  names_put(env, &ns);
+  if (rc && j) job_refused(env, j, rc);
+  else if (rc) raise(env, rc);
+}
+
+JNI_FN(void, hllMergeWithAsync)(JNIEnv *env, jclass cls, jlong space, jstring dst, jobjectArray srcs, jobject promise) {
+  (void)cls;
+  jname d;
+  if (name_get(env, dst, &d)) return;
+  jnames ns;
+  if (names_get(env, srcs, &ns)) {
+    names_put(env, &ns);
+    name_put(env, &d);
+    return;
+  }
+  job *j = job_new(env, promise, K_VOID, 0);
+  const int rc = j ? rsk_shim_hll_merge_with_async(space, d.c, ns.cs, ns.k, jni_done, j) : RSK_ERR_OUT_OF_MEMORY;
+  names_put(env, &ns);
+  name_put(env, &d);
+  if (rc && j) job_refused(env, j, rc);
+  else if (rc) raise(env, rc);
+}
+
+/* ---------------------------------------------------------------- Bloom */
+/* cfg[0] = size, cfg[1] = hashIterations, cfg[2] = expectedInsertions; fpp[0] = falseProbability */
+static void put_config(JNIEnv *env, const rsk_shim_bloom_config *c, jlongArray cfg, jdoubleArray fpp) {
+  const jlong v[3] = {(jlong)c->size, (jlong)c->hash_iterations, (jlong)c->expected_insertions};
+  const jdouble p = c->false_probability;
+  if (cfg) (*env)->SetLongArrayRegion(env, cfg, 0, 3, v);
+  if (fpp) (*env)->SetDoubleArrayRegion(env, fpp, 0, 1, &p);
+}
+
+JNI_FN(jboolean, bloomTryInit)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong n, jdouble p, jlongArray cfg,
+                               jdoubleArray fpp) {
+  (void)cls;
+  jname nm;
+  if (name_get(env, name, &nm)) return JNI_FALSE;
+  int32_t created = 0;
+  rsk_shim_bloom_config c;
+  const int rc = rsk_shim_bloom_try_init(space, nm.c, n, p, &created, &c);
+  name_put(env, &nm);
+  if (raise(env, rc)) return JNI_FALSE;
+  put_config(env, &c, cfg, fpp);
+  return created ? JNI_TRUE : JNI_FALSE;
+}
+
+JNI_FN(void, bloomConfig)(JNIEnv *env, jclass cls, jlong space, jstring name, jlongArray cfg, jdoubleArray fpp) {
+  (void)cls;
+  jname nm;
+  if (name_get(env, name, &nm)) return;
+  rsk_shim_bloom_config c;
+  const int rc = rsk_shim_bloom_get_config(space, nm.c, &c);
+  name_put(env, &nm);
+  if (!raise(env, rc)) put_config(env, &c, cfg, fpp);
+}
+
+static jbooleanArray bloom_batch(JNIEnv *env, jlong space, jstring name, jlong size, jint k, jobject keys,
+                                 jobject offsets, jlong n, int add) {
+  uint8_t *r = reply_buf(env, n);
+  if (!r) return NULL;
+  jname nm;
+  if (name_get(env, name, &nm)) {
+    free(r);
+    return NULL;
+  }
+  const int rc = add ? rsk_shim_bloom_add(space, nm.c, size, k, direct(env, keys), direct(env, offsets), n, r, n)
+                     : rsk_shim_bloom_contains(space, nm.c, size, k, direct(env, keys), direct(env, offsets), n, r, n);
+  name_put(env, &nm);
+  jbooleanArray arr = raise(env, rc) ? NULL : replies_array(env, r, n);
+  free(r);
+  return arr;
+}
+
+JNI_FN(jbooleanArray, bloomAdd)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k, jobject keys,
+                                jobject offsets, jlong n) {
+  (void)cls;
+  return bloom_batch(env, space, name, size, k, keys, offsets, n, 1);
+}
+
+JNI_FN(jbooleanArray, bloomContains)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k,
+                                     jobject keys, jobject offsets, jlong n) {
+  (void)cls;
+  return bloom_batch(env, space, name, size, k, keys, offsets, n, 0);
+}
+
+JNI_FN(jint, bloomCount)(JNIEnv *env, jclass cls, jlong space, jstring name) {
+  (void)cls;
+  jname nm;
+  if (name_get(env, name, &nm)) return 0;
   int32_t v = 0;
-  return raise(env, rsk_shim_bloom_count(bloom, &v)) ? 0 : (jint)v;
+  const int rc = rsk_shim_bloom_count(space, nm.c, &v);
+  name_put(env, &nm);
+  return raise(env, rc) ? 0 : (jint)v;
+}
+
+static void bloom_async(JNIEnv *env, jlong space, jstring name, jlong size, jint k, jobject keys, jobject offsets,
+                        jlong n, jobject promise, int add) {
+  if (n < 0 || n > 0x7fffffff) {
+    throw_iae(env, "batch larger than 2^31 - 1 elements");
+    return;
+  }
+  jname nm;
+  if (name_get(env, name, &nm)) return;
+  job *j = job_new(env, promise, K_ARRAY, n);
+  if (!j) {
+    name_put(env, &nm);
+    return;
+  }
+  const int rc = add ? rsk_shim_bloom_add_async(space, nm.c, size, k, direct(env, keys), direct(env, offsets), n,
+                                                j->out, n, jni_done, j)
+                     : rsk_shim_bloom_contains_async(space, nm.c, size, k, direct(env, keys), direct(env, offsets),
+                                                     n, j->out, n, jni_done, j);
+  name_put(env, &nm);
+  if (rc) job_refused(env, j, rc);
+}
+
+JNI_FN(void, bloomAddAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k, jobject keys,
+                            jobject offsets, jlong n, jobject promise) {
+  (void)cls;
+  bloom_async(env, space, name, size, k, keys, offsets, n, promise, 1);
+}
+
+JNI_FN(void, bloomContainsAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k, jobject keys,
+                                 jobject offsets, jlong n, jobject promise) {
+  (void)cls;
+  bloom_async(env, space, name, size, k, keys, offsets, n, promise, 0);
 }

@@ -5,11 +5,22 @@
  * native method of org.redisson.gpu.RSketchNative into one call below: it
  * fetches the direct buffers' addresses and capacities (GetDirectBufferAddress /
  * GetDirectBufferCapacity), calls the shim, and on a non-zero status throws
- * rsk_shim_exception_class(rc) with rsk_last_error() as the message.  Keeping
- * every check and conversion here lets tests/c/shim_caller.c drive exactly the
- * code a JVM would run, with plain C buffers standing in for direct buffers.
+ * rsk_shim_exception_class(rc) with rsk_shim_last_error() as the message.  Keeping
+ * every check, conversion and decision here lets tests/c/shim_caller.c drive
+ * exactly the code a JVM would run, with plain C buffers standing in for
+ * direct buffers.
  *
- * Handles cross the boundary as jlong (int64_t): rsk_ctx* / rsk_hll* / rsk_bloom*.
+ * The keyspace.  Redis resolves every object by NAME: two RHyperLogLog or
+ * RBloomFilter instances with one name are one key, PFCOUNT of a missing key
+ * is 0 and creates nothing, a Bloom filter's size and k live in the hash
+ * {name}__config that any instance (or client) re-reads
+ * (RedissonBloomFilter.java:206-221), and a getter on a filter nobody
+ * initialised throws IllegalStateException("Bloom filter is not initialized!")
+ * (:258-287).  The shim keeps that keyspace next to the GPU context: a space
+ * = one rsk_ctx + a name -> object registry (reference counted, thread-safe),
+ * so the Java objects hold only their name, exactly like the Redis-backed ones.
+ *
+ * Handles cross the boundary as jlong (int64_t): the space (rsk_shim_space*).
  */
 #ifndef RSKETCH_SHIM_H
 #define RSKETCH_SHIM_H
@@ -20,6 +31,13 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* Shim-level status on top of rsk_status: a Bloom call made with a stale
+ * (size, k) -- another client re-initialised the filter.  The reference's Lua
+ * guard raises RedisException "Bloom filter config has been changed"
+ * (RedissonBloomFilter.java:180-186) and the Java object retries after
+ * re-reading {name}__config (:108-112, :162-166). */
+#define RSK_SHIM_CONFIG_CHANGED 100
 
 /* A java.nio direct buffer as JNI reports it: address + capacity in ELEMENTS
  * (bytes for a ByteBuffer, longs for a LongBuffer).  addr == NULL means the
@@ -45,33 +63,97 @@ const char *rsk_shim_last_error(void);
  * buffer must stop here, not fault in a kernel. */
 int rsk_shim_keys(rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, rsk_keys *out);
 
-int rsk_shim_init(int32_t device, int64_t *ctx_out);
-int rsk_shim_shutdown(int64_t ctx);
+/* ------------------------------------------------------------- space */
+/* One GPU context and its keyspace.  extended_bloom: tryInit sizes above
+ * RedissonBloomFilter.MAX_SIZE are allowed (RSK_BLOOM_EXTENDED) instead of
+ * refused with IllegalArgumentException like the reference (:226-227). */
+int rsk_shim_init(int32_t device, int32_t extended_bloom, int64_t *space_out);
+int rsk_shim_shutdown(int64_t space);
 
-/* RHyperLogLog (RedissonHyperLogLog.java:40-97) */
-int rsk_shim_hll_create(int64_t ctx, int64_t n_sketches, int64_t *hll_out);
-int rsk_shim_hll_destroy(int64_t hll);
-int rsk_shim_hll_add(int64_t hll, int64_t id, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n,
+#define RSK_SHIM_NONE 0
+#define RSK_SHIM_HLL 1
+#define RSK_SHIM_BLOOM 2
+/* TYPE-like probe of a name (RSK_SHIM_NONE / _HLL / _BLOOM) and the object's
+ * library handle (the same handle for every lookup of one name; 0 if none). */
+int rsk_shim_lookup(int64_t space, const char *name, int32_t *type_out, int64_t *handle_out);
+/* DEL name (a Bloom filter's {name}__config with it, RedissonBloomFilter.java:
+ * 201-204); *deleted_out = 1 iff something existed.  Calls still running on
+ * the object finish first; the object is released after the last of them. */
+int rsk_shim_delete(int64_t space, const char *name, int32_t *deleted_out);
+
+/* RENAME / RENAMENX old new (RedissonObject.java:72-110): the object moves to
+ * the new name (a Bloom filter with its config); RENAME replaces an object
+ * the new name held, RENAMENX leaves both and answers 0 then.  A missing old
+ * name is RSK_ERR_INVALID_ARG ("ERR no such key"). *renamed_out may be NULL. */
+int rsk_shim_rename(int64_t space, const char *old_name, const char *new_name, int32_t nx, int32_t *renamed_out);
+
+/* --------------------------------- RHyperLogLog (RedissonHyperLogLog.java:40-97) */
+/* PFADD name e1..en (creates the key); *changed_out = the reply. */
+int rsk_shim_hll_add(int64_t space, const char *name, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n,
                      uint8_t *changed_out);
-/* replies: n bytes (the jbooleanArray region, jboolean == uint8_t) */
-int rsk_shim_hll_add_each(int64_t hll, int64_t id, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n,
+/* n x PFADD name e (RBatch of add()s); replies: n bytes (jboolean == uint8_t). */
+int rsk_shim_hll_add_each(int64_t space, const char *name, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n,
                           uint8_t *replies, int64_t replies_len);
-int rsk_shim_hll_count(int64_t hll, int64_t id, int64_t *out);
-/* countWith: k >= 1 (pool, id) members; mergeWith: dst <- max(dst, srcs) */
-int rsk_shim_hll_count_union(const int64_t *hlls, const int64_t *ids, int32_t k, int64_t *out);
-int rsk_shim_hll_merge(int64_t dst, int64_t dst_id, const int64_t *srcs, const int64_t *src_ids, int32_t k);
-int rsk_shim_hll_delete(int64_t hll, int64_t id);
+/* PFCOUNT name: 0 for a missing key, which stays missing. */
+int rsk_shim_hll_count(int64_t space, const char *name, int64_t *out);
+/* PFCOUNT names[0..k): missing keys are skipped (all missing: 0). */
+int rsk_shim_hll_count_with(int64_t space, const char *const *names, int32_t k, int64_t *out);
+/* PFMERGE dst srcs[0..k): dst created (dense), missing sources skipped. */
+int rsk_shim_hll_merge_with(int64_t space, const char *dst, const char *const *srcs, int32_t k);
+/* The RBatch of the reference (RedissonBatch.java:76-83 getHyperLogLog, :226-233
+ * execute) for add(): element i is "PFADD names[name_of[i]] e_i"; the replies
+ * come back in input order.  One rsk_hll_add_each per distinct name, its
+ * elements in input order (different keys are independent). */
+int rsk_shim_batch_hll_add(int64_t space, const char *const *names, int32_t n_names, const int32_t *name_of,
+                           rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, uint8_t *replies, int64_t replies_len);
 
-/* RBloomFilter (RedissonBloomFilter.java:52-252) */
-int rsk_shim_bloom_params(int64_t expected_insertions, double false_probability, int32_t extended,
-                          int64_t *size_out, int32_t *k_out);
-int rsk_shim_bloom_create(int64_t ctx, int64_t size, int32_t k, int64_t *bloom_out);
-int rsk_shim_bloom_destroy(int64_t bloom);
-int rsk_shim_bloom_add(int64_t bloom, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, uint8_t *replies,
-                       int64_t replies_len);
-int rsk_shim_bloom_contains(int64_t bloom, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, uint8_t *out,
-                            int64_t out_len);
-int rsk_shim_bloom_count(int64_t bloom, int32_t *out);
+/* Asynchronous twins (RHyperLogLogAsync.java:22-33): cb(user, status, value)
+ * fires once per accepted call, from a runtime thread (value: the reply, as
+ * rsketch.h's rsk_done_fn); a refused call returns the error and never fires.
+ * A count of a missing key fires on the calling thread with 0. */
+int rsk_shim_hll_add_async(int64_t space, const char *name, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n,
+                           rsk_done_fn cb, void *user);
+int rsk_shim_hll_count_async(int64_t space, const char *name, rsk_done_fn cb, void *user);
+int rsk_shim_hll_count_with_async(int64_t space, const char *const *names, int32_t k, rsk_done_fn cb, void *user);
+int rsk_shim_hll_merge_with_async(int64_t space, const char *dst, const char *const *srcs, int32_t k, rsk_done_fn cb,
+                                  void *user);
+
+/* ------------------------------ RBloomFilter (RedissonBloomFilter.java:52-287) */
+/* The {name}__config hash (:237-240). */
+typedef struct rsk_shim_bloom_config {
+  int64_t size;
+  int32_t hash_iterations;
+  int64_t expected_insertions;
+  double false_probability;
+} rsk_shim_bloom_config;
+/* tryInit(n, p) (:223-252): the size is computed first (IllegalArgument above
+ * MAX_SIZE in compat mode, as the reference throws before looking at Redis);
+ * then *created_out = 1 and a zeroed filter if the name has no config, else 0
+ * and the stored config (the reference's readConfig on "config has been
+ * changed").  cfg_out (may be NULL) = the config in force after the call. */
+int rsk_shim_bloom_try_init(int64_t space, const char *name, int64_t expected_insertions, double false_probability,
+                            int32_t *created_out, rsk_shim_bloom_config *cfg_out);
+/* HGETALL {name}__config: RSK_ERR_NOT_INITIALIZED when absent (getSize,
+ * getHashIterations, getExpectedInsertions, getFalseProbability, :258-287). */
+int rsk_shim_bloom_get_config(int64_t space, const char *name, rsk_shim_bloom_config *out);
+/* add / contains / count with the caller's cached (size, k), like the
+ * reference's batch with its Lua config guard: a missing filter is
+ * RSK_ERR_NOT_INITIALIZED (:206-221), a different stored config
+ * RSK_SHIM_CONFIG_CHANGED (re-read, retry).  add's replies: 1 iff one of the
+ * first k-1 SETBITs found its bit clear (:100-107); contains: AND of the
+ * first k-1 GETBITs (:147-168); replies / out NULL allowed for add only. */
+int rsk_shim_bloom_add(int64_t space, const char *name, int64_t size, int32_t k, rsk_shim_buf keys,
+                       rsk_shim_buf offsets, int64_t n, uint8_t *replies, int64_t replies_len);
+int rsk_shim_bloom_contains(int64_t space, const char *name, int64_t size, int32_t k, rsk_shim_buf keys,
+                            rsk_shim_buf offsets, int64_t n, uint8_t *out, int64_t out_len);
+/* count() (:188-199): config and BITCOUNT read together. */
+int rsk_shim_bloom_count(int64_t space, const char *name, int32_t *out);
+int rsk_shim_bloom_add_async(int64_t space, const char *name, int64_t size, int32_t k, rsk_shim_buf keys,
+                             rsk_shim_buf offsets, int64_t n, uint8_t *replies, int64_t replies_len, rsk_done_fn cb,
+                             void *user);
+int rsk_shim_bloom_contains_async(int64_t space, const char *name, int64_t size, int32_t k, rsk_shim_buf keys,
+                                  rsk_shim_buf offsets, int64_t n, uint8_t *out, int64_t out_len, rsk_done_fn cb,
+                                  void *user);
 
 #ifdef __cplusplus
 }

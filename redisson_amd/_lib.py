@@ -1,4 +1,6 @@
-"""ctypes binding of librsketch.so (include/rsketch.h).
+"""ctypes binding of librsketch.so (include/rsketch.h) and of the test /
+bench support library librsketch_diag.so (include/rsketch_diag.h: generators,
+microbenchmarks, tuning variants, route overrides).
 
 The HIP library is the only compute path: importing this module without the
 built library, or creating an Engine without a gfx950 device, raises.  There
@@ -12,6 +14,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RSKETCH_LIB", os.path.join(HERE, "librsketch.so"))
+DIAG_PATH = os.path.join(HERE, "librsketch_diag.so")
 
 RSK_OK = 0
 RSK_ERR_INVALID_ARG = 1
@@ -63,7 +66,8 @@ _STATUS_EXC = {
 
 
 class rsk_options(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int32), ("redis_version", ctypes.c_int32), ("staging_bytes", ctypes.c_uint64)]
+    _fields_ = [("device", ctypes.c_int32), ("redis_version", ctypes.c_int32), ("staging_bytes", ctypes.c_uint64),
+                ("stage_threads", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class rsk_keys(ctypes.Structure):
@@ -80,6 +84,9 @@ class rsk_keys(ctypes.Structure):
 _vp, _u64, _u32, _i32, _i64, _sz = (ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32,
                                     ctypes.c_int64, ctypes.c_size_t)
 _P = ctypes.POINTER
+# rsk_done_fn: void (*)(void *user, int status, uint64_t value)
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64)
+
 SIGNATURES = {
     "rsk_init": (ctypes.c_int, [_P(rsk_options), _P(_vp)]),
     "rsk_shutdown": (ctypes.c_int, [_vp]),
@@ -87,6 +94,7 @@ SIGNATURES = {
     "rsk_abi_version": (ctypes.c_int, []),
     "rsk_ctx_stream": (_vp, [_vp]),
     "rsk_sync": (ctypes.c_int, [_vp]),
+    "rsk_trim": (ctypes.c_int, [_vp]),
     "rsk_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rsk_prof_reset": (ctypes.c_int, [_vp]),
     "rsk_prof_read": (ctypes.c_int, [_vp, ctypes.c_char_p, _P(ctypes.c_double), _P(_u64)]),
@@ -105,6 +113,11 @@ SIGNATURES = {
     "rsk_hll_merge": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u32]),
     "rsk_hll_merge_batch": (ctypes.c_int, [_vp, _vp, _vp, _u64]),
     "rsk_hll_merge_raw": (ctypes.c_int, [_vp, _u64, _vp, _u32]),
+    "rsk_hll_add_async": (ctypes.c_int, [_vp, _u64, _P(rsk_keys), DONE_FN, _vp]),
+    "rsk_hll_count_async": (ctypes.c_int, [_vp, _u64, DONE_FN, _vp]),
+    "rsk_hll_count_union_async": (ctypes.c_int, [_vp, _vp, _u32, DONE_FN, _vp]),
+    "rsk_hll_merge_async": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u32, DONE_FN, _vp]),
+    "rsk_hll_merge_batch_async": (ctypes.c_int, [_vp, _vp, _vp, _u64, DONE_FN, _vp]),
     "rsk_hll_get_registers": (ctypes.c_int, [_vp, _u64, _vp, _u32]),
     "rsk_hll_device_registers": (_vp, [_vp]),
     "rsk_hll_export_redis": (ctypes.c_int, [_vp, _u64, _vp, _sz, _P(_sz)]),
@@ -117,6 +130,8 @@ SIGNATURES = {
     "rsk_bloom_add": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
     "rsk_bloom_contains": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
     "rsk_bloom_count": (ctypes.c_int, [_vp, _P(_i32)]),
+    "rsk_bloom_add_async": (ctypes.c_int, [_vp, _P(rsk_keys), _vp, DONE_FN, _vp]),
+    "rsk_bloom_contains_async": (ctypes.c_int, [_vp, _P(rsk_keys), _vp, DONE_FN, _vp]),
     "rsk_bloom_bitcount": (ctypes.c_int, [_vp, _P(_u64)]),
     "rsk_hash_to_base64": (ctypes.c_int, [_vp, _P(rsk_keys), _vp]),
     "rsk_bloom_export_bits": (ctypes.c_int, [_vp, _vp, _sz, _P(_sz)]),
@@ -154,6 +169,11 @@ SIGNATURES = {
     "rsk_plan_fetch": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _vp, _u64, _u32, _vp, _P(_u64), _vp]),
     "rsk_bloom_allreduce_or": (ctypes.c_int, [_vp]),
     "rsk_bloom_allreduce_or_flags": (ctypes.c_int, [_vp, _u32]),
+}
+
+DIAG_SIGNATURES = {
+    "rsk_diag_last_error": (ctypes.c_char_p, []),
+    "rsk_diag_set_route": (ctypes.c_int, [_vp, ctypes.c_char_p, _i64]),
     "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
     "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),
     "rsk_diag_bloom_contains_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _u64, _vp,
@@ -163,12 +183,13 @@ SIGNATURES = {
     "rsk_gen_keys16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp]),
     "rsk_gen_grouped": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _vp, _vp]),
     "rsk_gen_grouped_zipf": (ctypes.c_int, [_vp, _u64, _u64, ctypes.c_double, _u64, _u64, _vp, _vp]),
-    "rsk_diag_occupancy": (ctypes.c_int, [ctypes.c_int, _vp, _vp]),
     "rsk_gen_queries16": (ctypes.c_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
     "rsk_gen_varlen": (ctypes.c_int, [_vp, _u64, _u64, _u64, _vp, _vp, _u64, _P(_u64)]),
+
 }
 
 _lib = None
+_diag = None
 _lock = threading.Lock()
 
 
@@ -197,6 +218,31 @@ def load():
                 fn.argtypes = args
             _lib = L
     return _lib
+
+
+def diag():
+    """librsketch_diag.so (test / bench support: generators, microbenchmarks,
+    tuning variants, route overrides).  Never used by the product path."""
+    global _diag
+    load()  # the product library (and the system comgr) first
+    with _lock:
+        if _diag is None:
+            if not os.path.exists(DIAG_PATH):
+                raise ImportError("librsketch_diag.so not found at %s: build it with `make`" % DIAG_PATH)
+            D = ctypes.CDLL(DIAG_PATH)
+            for name, (res, args) in DIAG_SIGNATURES.items():
+                fn = getattr(D, name)
+                fn.restype = res
+                fn.argtypes = args
+            _diag = D
+    return _diag
+
+
+def check_diag(rc: int, what: str = ""):
+    if rc != RSK_OK:
+        msg = diag().rsk_diag_last_error().decode(errors="replace")
+        exc = _STATUS_EXC.get(rc, EngineError)
+        raise exc(msg if not what else "%s: %s" % (what, msg))
 
 
 def check(rc: int, what: str = ""):
@@ -246,6 +292,26 @@ class Engine:
         n = ctypes.c_uint64()
         check(self.lib.rsk_prof_read(self.ctx, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    def set_route(self, name: str, value: int):
+        """Route override of this context (rsk_diag_set_route): tests force
+        every pipeline of the library; "reset" restores the automatic routes."""
+        check_diag(diag().rsk_diag_set_route(self.ctx, name.encode(), int(value)), "rsk_diag_set_route")
+
+    def routes(self, **kw):
+        """Context manager: the given route overrides, then automatic routes."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            for k, v in kw.items():
+                self.set_route(k, v)
+            try:
+                yield self
+            finally:
+                self.set_route("reset", 0)
+
+        return cm()
 
     def close(self):
         if self.ctx:

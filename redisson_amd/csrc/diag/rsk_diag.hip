@@ -1,0 +1,175 @@
+// rsk_diag.hip -- memory-system microbenchmarks that give the sketch kernels
+// their measured roofline denominators on the box they run on:
+//   mode 0: streaming read (16 B/lane nontemporal loads)  -> GB/s
+//   mode 1: random 4 B gathers over the buffer            -> gathers/s
+//   mode 2: random 4 B atomicOr over the buffer           -> atomics/s
+//   mode 3: streaming copy (read + write halves)          -> GB/s (read+write)
+// Indices come from splitmix64(i), as uniform as the Bloom probe stream.
+// Also: the route overrides of a context (rsk_diag_set_route) and the timed
+// launches of the kernels' tuning variants (rsk_diag_kernels.hip).
+#include <cstring>
+
+#include "rsk_diag_internal.h"
+
+namespace rsk {
+
+__global__ __launch_bounds__(256) void diag_stream_read(const uint4* __restrict__ p, uint64_t n16,
+                                                        uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 v = ld_nt16(p + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the loads alive
+}
+
+__global__ __launch_bounds__(256) void diag_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = ld_nt16(src + i);
+}
+
+__global__ __launch_bounds__(256) void diag_gather(const uint32_t* __restrict__ w, uint64_t nwords, uint64_t nops,
+                                                   uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nops; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t r = splitmix64(i);
+    acc ^= w[__umul64hi(r, nwords)];
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void diag_atomic_or(uint32_t* __restrict__ w, uint64_t nwords, uint64_t nops) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nops; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t r = splitmix64(i);
+    atomicOr(&w[__umul64hi(r, nwords)], 1u << (r & 31));
+  }
+}
+
+}  // namespace rsk
+
+namespace rsk {
+namespace diag {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+// Device time of whatever `launch` enqueues on the context stream.
+template <class F>
+double timed(rsk_ctx* c, F&& launch) {
+  hipEvent_t a, b;
+  RSK_HIP(hipEventCreate(&a));
+  RSK_HIP(hipEventCreate(&b));
+  RSK_HIP(hipEventRecord(a, c->stream));
+  launch();
+  RSK_HIP(hipEventRecord(b, c->stream));
+  RSK_HIP(hipEventSynchronize(b));
+  float f = 0;
+  RSK_HIP(hipEventElapsedTime(&f, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return f;
+}
+}  // namespace diag
+}  // namespace rsk
+
+using namespace rsk;
+
+extern "C" {
+
+const char* rsk_diag_last_error(void) { return diag::g_err.c_str(); }
+
+int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
+  return diag::guarded([&] {
+    diag::need(c && name, "NULL argument");
+    diag::Lock l(c);
+    const std::string k(name);
+    Tuning& t = c->tune;
+    if (k == "bloom_stream") t.bloom_stream = (int)value;
+    else if (k == "bloom_part") t.bloom_part = (int)value;
+    else if (k == "bloom_chunk") t.bloom_chunk = (uint64_t)value;
+    else if (k == "sa_tiny") t.sa_tiny = (int)value;
+    else if (k == "sa_parts") t.sa_parts = (uint32_t)value;
+    else if (k == "reply") t.reply = (int)value;
+    else if (k == "reply_chunk") t.reply_chunk = (uint64_t)value;
+    else if (k == "gpart") t.gpart = (int)value;
+    else if (k == "reset") t = Tuning{};
+    else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};
+  });
+}
+
+int rsk_diag_hll_variant(rsk_ctx* c, int variant, const void* dev_keys16, uint64_t n, double* ms) {
+  return diag::guarded([&] {
+    diag::need(c && dev_keys16 && ms && n, "bad arguments");
+    diag::Lock l(c);
+    *ms = diag::timed(c, [&] { hll_variant_launch(c, variant, reinterpret_cast<const uint4*>(dev_keys16), n); });
+  });
+}
+
+int rsk_diag_bloom_contains_variant(rsk_ctx* c, int variant, rsk_bloom* bf, const void* dev_keys16, uint64_t n,
+                                    uint8_t* dev_out, double* ms) {
+  return diag::guarded([&] {
+    diag::need(c && bf && dev_keys16 && dev_out && ms && n, "bad arguments");
+    diag::Lock l(c);
+    *ms = diag::timed(c, [&] {
+      bloom_contains_variant_launch(c, bf, reinterpret_cast<const uint4*>(dev_keys16), n, dev_out, variant);
+    });
+  });
+}
+
+int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t nops, double* ms) {
+  return diag::guarded([&] {
+    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 3, "bad arguments");
+    diag::Lock l(c);
+    uint32_t* sink = reinterpret_cast<uint32_t*>(c->d_small + 512);
+    const uint32_t grid = (uint32_t)c->num_cus * 8;
+    *ms = diag::timed(c, [&] {
+      switch (mode) {
+        case 0:
+          hipLaunchKernelGGL(diag_stream_read, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<const uint4*>(buf),
+                             bytes / 16, sink);
+          break;
+        case 1:
+          hipLaunchKernelGGL(diag_gather, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<const uint32_t*>(buf),
+                             bytes / 4, nops, sink);
+          break;
+        case 2:
+          hipLaunchKernelGGL(diag_atomic_or, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<uint32_t*>(buf),
+                             bytes / 4, nops);
+          break;
+        default: {
+          const uint64_t half = bytes / 32;  // uint4 elements per half
+          hipLaunchKernelGGL(diag_copy, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<const uint4*>(buf),
+                             reinterpret_cast<uint4*>(buf) + half, half);
+          break;
+        }
+      }
+      RSK_CHECK_LAUNCH("diag");
+    });
+  });
+}
+
+int rsk_diag_bloom_contains_probes(rsk_ctx* c, rsk_bloom* bf, const void* dev_keys16, uint64_t n, uint8_t* dev_out,
+                                   uint64_t* probes) {
+  return diag::guarded([&] {
+    diag::need(c && bf && dev_keys16 && dev_out && probes && n, "bad arguments");
+    diag::Lock l(c);
+    auto* d = reinterpret_cast<unsigned long long*>(c->d_small + 384);
+    RSK_HIP(hipMemsetAsync(d, 0, 8, c->stream));
+    bloom_contains_probe_count_launch(c, bf, reinterpret_cast<const uint4*>(dev_keys16), n, dev_out, d);
+    RSK_HIP(hipMemcpyAsync(c->h_small + 384, d, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(probes, c->h_small + 384, 8);
+  });
+}
+
+int rsk_diag_hll_var_variant(rsk_ctx* c, int variant, const void* dev_data, const uint64_t* dev_offsets, uint64_t n,
+                             double* ms) {
+  return diag::guarded([&] {
+    diag::need(c && dev_data && dev_offsets && ms && n, "bad arguments");
+    diag::Lock l(c);
+    *ms = diag::timed(c, [&] {
+      hll_var_variant_launch(c, variant, reinterpret_cast<const uint8_t*>(dev_data), dev_offsets, n);
+    });
+  });
+}
+
+}  // extern "C"

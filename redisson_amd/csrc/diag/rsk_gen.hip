@@ -6,7 +6,7 @@
 
 #include <hipcub/hipcub.hpp>
 
-#include "rsk_internal.h"
+#include "rsk_diag_internal.h"
 
 namespace rsk {
 
@@ -151,8 +151,12 @@ void gen_varlen_lengths_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64
   // Inclusive scan of offsets[1..n] in place (offsets[0] = 0).
   size_t tmp_bytes = 0;
   (void)hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, offsets + 1, offsets + 1, (int)n, c->stream);
-  void* tmp = c->work(tmp_bytes + 256);
-  RSK_HIP(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, offsets + 1, offsets + 1, (int)n, c->stream));
+  void* tmp = nullptr;  // the support library keeps no scratch of its own
+  RSK_HIP(hipMalloc(&tmp, tmp_bytes + 256));
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, offsets + 1, offsets + 1, (int)n, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(tmp);
+  RSK_HIP(e);
 }
 
 void gen_varlen_bytes_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, const uint64_t* offsets,
@@ -163,3 +167,78 @@ void gen_varlen_bytes_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t
 }
 
 }  // namespace rsk
+
+using namespace rsk;
+
+extern "C" {
+
+// ----------------------------------------------------------- generators
+int rsk_gen_keys16(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* dev_out) {
+  return diag::guarded([&] {
+    diag::need(c && (dev_out || n == 0), "NULL argument");
+    diag::Lock l(c);
+    if (n) gen_keys16_launch(c, seed, start, n, dev_out);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_gen_grouped(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* dev_groups,
+                    void* dev_keys) {
+  return diag::guarded([&] {
+    diag::need(c && G > 0 && ((dev_groups && dev_keys) || n == 0), "bad arguments");
+    diag::Lock l(c);
+    if (n) gen_grouped_launch(c, seed, G, start, n, dev_groups, dev_keys);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_gen_grouped_zipf(rsk_ctx* c, uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n,
+                         uint32_t* dev_groups, void* dev_keys) {
+  return diag::guarded([&] {
+    diag::need(c && G > 0 && G < (1ull << 32) && ((dev_groups && dev_keys) || n == 0), "bad arguments");
+    diag::need(s > 0.0 && s < 16.0, "Zipf exponent must be in (0, 16)");
+    diag::Lock l(c);
+    if (!n) return;
+    const std::vector<uint64_t> cdf = zipf_cdf((uint32_t)G, s);
+    uint64_t* d_cdf = nullptr;
+    RSK_HIP(hipMalloc(&d_cdf, 8 * G));
+    hipError_t e = hipMemcpyAsync(d_cdf, cdf.data(), 8 * G, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+      gen_grouped_zipf_launch(c, seed, d_cdf, (uint32_t)G, start, n, dev_groups, dev_keys);
+      e = hipStreamSynchronize(c->stream);
+    }
+    (void)hipFree(d_cdf);
+    RSK_HIP(e);
+  });
+}
+
+int rsk_gen_queries16(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
+                      void* dev_out) {
+  return diag::guarded([&] {
+    diag::need(c && n_ins > 0 && (dev_out || n == 0), "bad arguments");
+    diag::Lock l(c);
+    if (n) gen_queries16_launch(c, qseed, iseed, n_ins, start, n, dev_out);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rsk_gen_varlen(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* dev_offsets, void* dev_blob,
+                   uint64_t blob_cap, uint64_t* total_bytes) {
+  return diag::guarded([&] {
+    diag::need(c && dev_offsets && total_bytes, "NULL argument");
+    diag::need(n < (1ull << 31), "n must be < 2^31 per call");
+    diag::Lock l(c);
+    gen_varlen_lengths_launch(c, seed, start, n, dev_offsets);
+    uint64_t tot = 0;
+    RSK_HIP(hipMemcpyAsync(&tot, dev_offsets + n, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    *total_bytes = tot;
+    if (dev_blob) {
+      diag::need(blob_cap >= tot, "blob capacity too small");
+      gen_varlen_bytes_launch(c, seed, start, n, dev_offsets, reinterpret_cast<uint8_t*>(dev_blob));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+    }
+  });
+}
+
+}  // extern "C"

@@ -12,7 +12,6 @@
 #include <new>
 #include <thread>
 #include <vector>
-#include <cstdlib>
 #include <unordered_map>
 
 #include "rsk_internal.h"
@@ -95,10 +94,7 @@ uint8_t* rsk_ctx::work(uint64_t bytes) {
 }
 
 uint8_t* rsk_ctx::pinned(uint64_t bytes) {
-  if (batch_pending) {  // an earlier call's DMA may still read the buffer
-    RSK_HIP(hipEventSynchronize(batch_ev));
-    batch_pending = false;
-  }
+  // every call that fills this buffer waits for its DMA before returning
   if (bytes > h_batch_bytes) {
     if (h_batch) {
       RSK_HIP(hipStreamSynchronize(stream));
@@ -131,26 +127,19 @@ void need(bool cond, const char* msg) {
 
 // Device output scratch that is distinct from ctx->work (used inside
 // algorithms).  Kept per context, grown on demand.
-struct OutScratch {
-  uint8_t* p = nullptr;
-  uint64_t bytes = 0;
-};
-thread_local std::map<rsk_ctx*, OutScratch> g_out;
-
 uint8_t* out_scratch(rsk_ctx* c, uint64_t bytes) {
-  OutScratch& s = g_out[c];
-  if (bytes > s.bytes) {
-    if (s.p) {
+  if (bytes > c->out_bytes) {
+    if (c->d_out) {
       RSK_HIP(hipStreamSynchronize(c->stream));
-      RSK_HIP(hipFree(s.p));
-      s.p = nullptr;
-      s.bytes = 0;
+      RSK_HIP(hipFree(c->d_out));
+      c->d_out = nullptr;
+      c->out_bytes = 0;
     }
     uint64_t sz = std::max<uint64_t>(bytes, 16ull << 20);
-    RSK_HIP(hipMalloc(&s.p, sz));
-    s.bytes = sz;
+    RSK_HIP(hipMalloc(&c->d_out, sz));
+    c->out_bytes = sz;
   }
-  return s.p;
+  return c->d_out;
 }
 
 void ensure_stage(rsk_ctx* c) {
@@ -193,19 +182,10 @@ void check_out(const rsk_ctx* c, const rsk_keys* k, const void* out) {
 // (par_copy) while the DMA of the other runs, so the pageable user buffer is
 // read at memcpy speed and the link carries pinned transfers.  Each stage has
 // its own device twin, so chunk i+1's DMA may queue behind chunk i's kernels
-// without a host wait.  RSK_STAGE_THREADS (default 8) sets the copy threads.
-unsigned stage_threads() {
-  static const unsigned n = [] {
-    const char* e = std::getenv("RSK_STAGE_THREADS");
-    const long v = e ? std::strtol(e, nullptr, 10) : 8;
-    return (unsigned)std::max<long>(1, std::min<long>(v, 64));
-  }();
-  return n;
-}
-
-void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+// without a host wait.  rsk_options.stage_threads (default 8) sets the copy threads.
+void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n, unsigned threads) {
   const uint64_t min_piece = 8ull << 20;
-  const unsigned nt = (unsigned)std::min<uint64_t>(stage_threads(), n / min_piece);
+  const unsigned nt = (unsigned)std::min<uint64_t>(threads, n / min_piece);
   if (nt <= 1) {
     if (n) std::memcpy(dst, src, n);
     return;
@@ -277,7 +257,7 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
   auto h2d = [&](int slot, uint64_t at, const void* from, uint64_t bytes) {
     if (!bytes) return;
     if (pinned) {
-      par_copy(c->h_pin[slot] + at, reinterpret_cast<const uint8_t*>(from), bytes);
+      par_copy(c->h_pin[slot] + at, reinterpret_cast<const uint8_t*>(from), bytes, c->stage_threads);
       RSK_HIP(hipMemcpyAsync(dbuf[slot] + at, c->h_pin[slot] + at, bytes, hipMemcpyHostToDevice, c->stream));
     } else {
       RSK_HIP(hipMemcpyAsync(dbuf[slot] + at, from, bytes, hipMemcpyHostToDevice, c->stream));
@@ -327,6 +307,7 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
 void check_hll(const rsk_hll* h, uint64_t id) {
   need(h != nullptr, "hll handle is NULL");
   need(id < h->n, "sketch id out of range");
+  CtxLock l(h->ctx);         // the pool's host state is the context's
   rsk::hll_materialize(h);  // every caller reads or writes registers
   rsk::hll_touch(h);        // conservatively: every caller may write them
 }
@@ -483,6 +464,8 @@ int rsk_init(const rsk_options* opts, rsk_ctx** out) {
     // Each stage holds stage_bytes of key bytes plus stage_bytes/4 of u64 offsets.
     need(o.staging_bytes == 0 || (o.staging_bytes >= (1ull << 20) && o.staging_bytes % 256 == 0),
          "staging_bytes must be 0 (default) or a multiple of 256 that is >= 1 MiB");
+    need(o.stage_threads <= 64, "stage_threads must be in [0, 64]");
+    need(o.reserved == 0, "rsk_options.reserved must be 0");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail(RSK_ERR_NO_DEVICE, "no HIP device visible");
     need(o.device >= 0 && o.device < ndev, "device ordinal out of range");
@@ -497,6 +480,7 @@ int rsk_init(const rsk_options* opts, rsk_ctx** out) {
     RSK_HIP(hipSetDevice(c->device));
     RSK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->stage_bytes = o.staging_bytes ? o.staging_bytes : (256ull << 20);
+    c->stage_threads = o.stage_threads ? o.stage_threads : 8;
     c->slab_count = std::min<uint32_t>(RSK_MAX_SLABS, 8u * (uint32_t)c->num_cus);
     RSK_HIP(hipMalloc(&c->d_slab, (uint64_t)c->slab_count * HLL_REGS));
     c->small_bytes = 1 << 20;
@@ -533,14 +517,17 @@ int rsk_shutdown(rsk_ctx* c) {
     (void)hipFree(c->d_small);
     (void)hipHostFree(c->h_small);
     if (c->h_batch) (void)hipHostFree(c->h_batch);
-    if (c->batch_ev) (void)hipEventDestroy(c->batch_ev);
     (void)hipFree(c->d_work);
+    (void)hipFree(c->d_out);
     (void)hipFree(c->d_lc);
-    auto it = g_out.find(c);
-    if (it != g_out.end()) {
-      (void)hipFree(it->second.p);
-      g_out.erase(it);
+    for (rsk::AsyncOp* op : c->async_all) {  // the stream is drained: every completion has run
+      if (op->h_buf) (void)hipHostFree(op->h_buf);
+      if (op->h_res) (void)hipHostFree(op->h_res);
+      if (op->d_buf) (void)hipFree(op->d_buf);
+      delete op;
     }
+    c->async_all.clear();
+    c->async_free.clear();
     if (c->comm) (void)rsk_comm_destroy(c);
     (void)hipStreamDestroy(c->stream);
   });
@@ -549,6 +536,21 @@ int rsk_shutdown(rsk_ctx* c) {
 }
 
 void* rsk_ctx_stream(rsk_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int rsk_trim(rsk_ctx* c) {
+  return guarded([&] {
+    need(c != nullptr, "ctx is NULL");
+    CtxLock l(c);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    RSK_HIP(hipFree(c->d_work));
+    RSK_HIP(hipFree(c->d_out));
+    c->d_work = c->d_out = nullptr;
+    c->work_bytes = c->out_bytes = 0;
+    if (c->h_batch) RSK_HIP(hipHostFree(c->h_batch));
+    c->h_batch = nullptr;
+    c->h_batch_bytes = 0;
+  });
+}
 
 int rsk_sync(rsk_ctx* c) {
   return guarded([&] {
@@ -640,6 +642,7 @@ int rsk_hll_delete(rsk_hll* h, uint64_t id) {
   return guarded([&] {
     check_hll(h, id);
     CtxLock l(h->ctx);
+    hll_forget_import(h, id);
     RSK_HIP(hipMemsetAsync(regs_of(h, id), 0, HLL_REGS, h->ctx->stream));
     RSK_HIP(hipMemsetAsync(h->d_card + id, 0, 8, h->ctx->stream));
     h->exists[id] = 0;
@@ -651,6 +654,7 @@ int rsk_hll_clear(rsk_hll* h) {
   return guarded([&] {
     if (!h) throw RskError{RSK_ERR_INVALID_ARG, "NULL handle"};
     CtxLock l(h->ctx);
+    hll_forget_imports(h);
     {
       ProfScope ps(h->ctx, "hll_clear");
       // registers: lazily (hll_materialize, or rewritten whole by the next grouped add)
@@ -669,6 +673,7 @@ int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     check_keys(c, keys);  // before the key is created: a refused batch leaves it absent
+    hll_forget_import(h, id);
     bool created;
     create_if_missing(h, id, &created);
     // The reduce kernel raises the flag to this call's epoch when a register
@@ -704,6 +709,7 @@ int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out
     bool created;
     check_keys(c, keys);
     check_out(c, keys, out);
+    hll_forget_import(h, id);
     create_if_missing(h, id, &created);
     // Sub-chunks bounded for the 32-bit sort; replies compose sequentially.
     const uint64_t max_chunk = 1ull << 26;
@@ -755,6 +761,7 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     CtxLock l(c);
     check_keys(c, keys);
     if (keys->n == 0) return;
+    hll_forget_imports(h);
     check_out(c, keys, groups);
     const bool pool_zero = h->zero;
     hll_touch(h);
@@ -772,13 +779,11 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
       }
       // A pending lazy clear is completed by the partitioned add's first
       // launch (every row written); any other path zeroes the pool first.
-      const bool write_all = h->pending_clear && hll_grouped_partition_applies(dk, h->n);
+      const bool write_all = h->pending_clear && hll_grouped_partition_applies(c, dk, h->n);
       if (!write_all) hll_materialize(h);
       hll_touch(h);  // estimates of earlier chunks are stale once this one lands
-      const char* pe = std::getenv("RSK_HLL_PCOUNT");  // "0": no estimates from the grouped add (A/B)
-      const bool est = !(pe && pe[0] == '0');
       hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0, write_all,
-                             PCount{est ? h->d_pcount : nullptr, h->d_pepoch, h->pc_epoch});
+                             PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
       h->pending_clear = false;
     });
     if (keys->location == RSK_MEM_DEVICE) {
@@ -846,6 +851,92 @@ void union_impl(rsk_ctx* c, const uint8_t* const* ptrs, uint32_t arity, uint64_t
 }
 }  // namespace
 
+namespace {
+// rsk_hll_merge_batch(_async): PFMERGEs run in input order in Redis; a batch
+// whose destinations are also sources of other pairs depends on that order.
+// Level the pairs: a pair runs after the last writer of its source (RAW) and
+// of its destination (WAW), and after the last reader of its destination
+// (WAR).  Pairs of one level are independent and run as one launch.
+// Per-sketch last writer / last reader levels live in one flat per-pool
+// array, reset lazily by an epoch stamp (no hashing, no clearing).
+uint64_t merge_batch_seg(uint64_t n) { return (8 * n + 255) & ~255ull; }
+uint64_t merge_batch_host_bytes(uint64_t n) { return 3 * merge_batch_seg(n) + 4 * n + 256; }
+uint64_t merge_batch_dev_bytes(uint64_t n) { return 3 * merge_batch_seg(n) + 512; }
+
+void merge_batch_check(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_ids, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    check_hll(h, dst_ids[i]);
+    check_hll(h, src_ids[i]);
+  }
+}
+
+// hb: pinned host buffer of merge_batch_host_bytes(n); d: device scratch of
+// merge_batch_dev_bytes(n) -- pointer arrays built in hb, one DMA, one merge
+// launch per level, one cache invalidation for the batch.
+void merge_batch_enqueue(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_ids, uint64_t n, uint8_t* hb,
+                         uint8_t* d) {
+  rsk_ctx* c = h->ctx;
+  for (uint64_t i = 0; i < n && !h->imported.empty(); ++i) hll_forget_import(h, dst_ids[i]);
+  if (h->lv.size() != h->n) {
+    h->lv.assign(h->n, rsk_hll::Level{0, 0, 0});
+    h->lv_epoch = 0;
+  }
+  if (++h->lv_epoch == 0) {
+    for (auto& e : h->lv) e.stamp = 0;
+    h->lv_epoch = 1;
+  }
+  const uint32_t ep = h->lv_epoch;
+  auto touch = [&](uint64_t id) -> rsk_hll::Level& {
+    rsk_hll::Level& e = h->lv[id];
+    if (e.stamp != ep) e = rsk_hll::Level{ep, 0, 0};
+    return e;
+  };
+  // pinned: [dst pointers n][src pointers n][dst ids n][level n (u32)]
+  const uint64_t seg = merge_batch_seg(n);
+  auto* dps = reinterpret_cast<uint8_t**>(hb);
+  auto* sps = reinterpret_cast<const uint8_t**>(hb + seg);
+  auto* ids = reinterpret_cast<uint64_t*>(hb + 2 * seg);
+  auto* level = reinterpret_cast<uint32_t*>(hb + 3 * seg);
+  uint32_t max_level = 0;
+  std::vector<uint8_t> src_exists(n);  // as of the pair's turn in input order
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t s_ = src_ids[i], dd = dst_ids[i];
+    src_exists[i] = h->exists[s_];
+    h->exists[dd] = 1;
+    h->dense[dd] = 1;
+    rsk_hll::Level& ls = touch(s_);
+    rsk_hll::Level& ld = touch(dd);
+    const uint32_t lv = std::max(std::max(ls.w, ld.w), ld.r) + 1;
+    level[i] = lv;
+    ld.w = lv;
+    ls.r = std::max(ls.r, lv);
+    max_level = std::max(max_level, lv);
+  }
+  std::vector<uint64_t> start(max_level + 2, 0);
+  for (uint64_t i = 0; i < n; ++i) start[level[i] + 1]++;
+  for (uint32_t l = 1; l <= max_level + 1; ++l) start[l] += start[l - 1];
+  {
+    std::vector<uint64_t> fill(start.begin(), start.end());
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t p = fill[level[i]]++;
+      sps[p] = src_exists[i] ? regs_of(h, src_ids[i]) : nullptr;
+      dps[p] = regs_of(h, dst_ids[i]);
+    }
+  }
+  std::memcpy(ids, dst_ids, n * 8);
+  auto* d_dst = reinterpret_cast<uint8_t**>(d);
+  auto* d_src = reinterpret_cast<const uint8_t**>(d + seg);
+  auto* d_ids = reinterpret_cast<uint64_t*>(d + 2 * seg);
+  RSK_HIP(hipMemcpyAsync(d_dst, dps, 3 * seg, hipMemcpyHostToDevice, c->stream));  // pointers and ids, one DMA
+  for (uint32_t l = 1; l <= max_level; ++l)
+    hll_merge_launch(c, d_dst + start[l], d_src + start[l], 1, start[l + 1] - start[l]);
+  // PFMERGE invalidates every destination's cache (one launch for the batch).
+  hipLaunchKernelGGL(invalidate_list_kernel, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0,
+                     c->stream, h->d_card, d_ids, n);
+  RSK_CHECK_LAUNCH("invalidate_list");
+}
+}  // namespace
+
 int rsk_hll_count_union(rsk_hll* const* hs, const uint64_t* ids, uint32_t k, uint64_t* out) {
   return guarded([&] {
     need(hs && ids && out && k >= 1, "bad arguments");
@@ -889,6 +980,7 @@ int rsk_hll_merge(rsk_hll* dst, uint64_t dst_id, rsk_hll* const* srcs, const uin
       sp[a] = srcs[a]->exists[src_ids[a]] ? regs_of(srcs[a], src_ids[a]) : nullptr;
     }
     bool created;
+    hll_forget_import(dst, dst_id);
     create_if_missing(dst, dst_id, &created);
     dst->dense[dst_id] = 1;  // pfmergeCommand converts the destination to dense
     if (k) {
@@ -911,82 +1003,10 @@ int rsk_hll_merge_batch(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     if (n == 0) return;
-    for (uint64_t i = 0; i < n; ++i) {
-      check_hll(h, dst_ids[i]);
-      check_hll(h, src_ids[i]);
-    }
-    // PFMERGEs run in input order in Redis; a batch whose destinations are
-    // also sources of other pairs depends on that order.  Level the pairs:
-    // a pair runs after the last writer of its source (RAW) and of its
-    // destination (WAW), and after the last reader of its destination (WAR).
-    // Pairs of one level are independent and run as one launch.
-    // Per-sketch last writer / last reader levels live in one flat per-pool
-    // array, reset lazily by an epoch stamp (no hashing, no clearing).
-    if (h->lv.size() != h->n) {
-      h->lv.assign(h->n, rsk_hll::Level{0, 0, 0});
-      h->lv_epoch = 0;
-    }
-    if (++h->lv_epoch == 0) {
-      for (auto& e : h->lv) e.stamp = 0;
-      h->lv_epoch = 1;
-    }
-    const uint32_t ep = h->lv_epoch;
-    auto touch = [&](uint64_t id) -> rsk_hll::Level& {
-      rsk_hll::Level& e = h->lv[id];
-      if (e.stamp != ep) e = rsk_hll::Level{ep, 0, 0};
-      return e;
-    };
-    // pinned: [dst pointers n][src pointers n][dst ids n][level n (u32)]
-    const uint64_t seg = (8 * n + 255) & ~255ull;
-    uint8_t* hb = c->pinned(3 * seg + 4 * n + 256);
-    auto* dps = reinterpret_cast<uint8_t**>(hb);
-    auto* sps = reinterpret_cast<const uint8_t**>(hb + seg);
-    auto* ids = reinterpret_cast<uint64_t*>(hb + 2 * seg);
-    auto* level = reinterpret_cast<uint32_t*>(hb + 3 * seg);
-    uint32_t max_level = 0;
-    std::vector<uint8_t> src_exists(n);  // as of the pair's turn in input order
-    for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t s_ = src_ids[i], d = dst_ids[i];
-      src_exists[i] = h->exists[s_];
-      h->exists[d] = 1;
-      h->dense[d] = 1;
-      rsk_hll::Level& ls = touch(s_);
-      rsk_hll::Level& ld = touch(d);
-      const uint32_t lv = std::max(std::max(ls.w, ld.w), ld.r) + 1;
-      level[i] = lv;
-      ld.w = lv;
-      ls.r = std::max(ls.r, lv);
-      max_level = std::max(max_level, lv);
-    }
-    std::vector<uint64_t> start(max_level + 2, 0);
-    for (uint64_t i = 0; i < n; ++i) start[level[i] + 1]++;
-    for (uint32_t l = 1; l <= max_level + 1; ++l) start[l] += start[l - 1];
-    {
-      std::vector<uint64_t> fill(start.begin(), start.end());
-      for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t p = fill[level[i]]++;
-        sps[p] = src_exists[i] ? regs_of(h, src_ids[i]) : nullptr;
-        dps[p] = regs_of(h, dst_ids[i]);
-      }
-    }
-    std::memcpy(ids, dst_ids, n * 8);
-    uint8_t* s = out_scratch(c, 3 * seg + 512);
-    auto* d_dst = reinterpret_cast<uint8_t**>(s);
-    auto* d_src = reinterpret_cast<const uint8_t**>(s + seg);
-    auto* d_ids = reinterpret_cast<uint64_t*>(s + 2 * seg);
-    RSK_HIP(hipMemcpyAsync(d_dst, dps, 3 * seg, hipMemcpyHostToDevice, c->stream));  // pointers and ids, one DMA
-    if (!c->batch_ev) RSK_HIP(hipEventCreateWithFlags(&c->batch_ev, hipEventDisableTiming));
-    RSK_HIP(hipEventRecord(c->batch_ev, c->stream));
-    c->batch_pending = true;
-    for (uint32_t l = 1; l <= max_level; ++l)
-      hll_merge_launch(c, d_dst + start[l], d_src + start[l], 1, start[l + 1] - start[l]);
-    // PFMERGE invalidates every destination's cache (one launch for the batch).
-    hipLaunchKernelGGL(invalidate_list_kernel, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256), 0,
-                       c->stream, h->d_card, d_ids, n);
-    RSK_CHECK_LAUNCH("invalidate_list");
-    // No reply (PFMERGE answers OK): the call returns with the merges queued
-    // on the context stream, which orders every later call behind them
-    // (mergeWithAsync's future completes on the next synchronising call).
+    merge_batch_check(h, dst_ids, src_ids, n);
+    merge_batch_enqueue(h, dst_ids, src_ids, n, c->pinned(merge_batch_host_bytes(n)),
+                        out_scratch(c, merge_batch_dev_bytes(n)));
+    RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }
 
@@ -998,6 +1018,7 @@ int rsk_hll_merge_raw(rsk_hll* h, uint64_t id, const uint8_t* regs, uint32_t loc
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     bool created;
+    hll_forget_import(h, id);
     create_if_missing(h, id, &created);
     h->dense[id] = 1;
     const uint8_t* src = regs;
@@ -1028,6 +1049,7 @@ void* rsk_hll_device_registers(rsk_hll* h) {  // the caller may read or write th
   if (!h) return nullptr;
   try {
     rsk::hll_materialize(h);
+    hll_forget_imports(h);
     hll_touch(h);
     RSK_HIP(hipStreamSynchronize(h->ctx->stream));
   } catch (const RskError&) {
@@ -1051,6 +1073,15 @@ int rsk_hll_export_redis(rsk_hll* h, uint64_t id, uint8_t* buf, size_t cap, size
     RSK_HIP(hipMemcpyAsync(raw.data(), regs_of(h, id), HLL_REGS, hipMemcpyDeviceToHost, h->ctx->stream));
     RSK_HIP(hipMemcpyAsync(&card, h->d_card + id, 8, hipMemcpyDeviceToHost, h->ctx->stream));
     RSK_HIP(hipStreamSynchronize(h->ctx->stream));
+    const auto imp = h->imported.find(id);
+    if (imp != h->imported.end()) {  // SET bytes, unwritten since: returned as they are
+      const std::vector<uint8_t>& v = imp->second;
+      need(cap >= v.size(), "buffer smaller than the stored string");
+      std::memcpy(buf, v.data(), v.size());
+      for (int b = 0; b < 8; ++b) buf[8 + b] = (uint8_t)(card >> (8 * b));  // PFCOUNT's cache, as Redis keeps it
+      *len = v.size();
+      return;
+    }
     std::memset(buf, 0, RSK_HLL_DENSE_BYTES);
     std::memcpy(buf, "HYLL", 4);
     for (int b = 0; b < 8; ++b) buf[8 + b] = (uint8_t)(card >> (8 * b));
@@ -1132,6 +1163,7 @@ int rsk_hll_import_redis(rsk_hll* h, uint64_t id, const uint8_t* buf, size_t len
     RSK_HIP(hipStreamSynchronize(c->stream));
     h->exists[id] = 1;
     h->dense[id] = buf[4] == 0;
+    h->imported[id].assign(buf, buf + len);
   });
 }
 
@@ -1336,73 +1368,375 @@ int rsk_bloom_or_bits(rsk_bloom* b, const uint8_t* bits, size_t len, uint32_t lo
 
 void* rsk_bloom_device_bits(rsk_bloom* b) { return b ? b->d_bits : nullptr; }
 
-// ----------------------------------------------------------- generators
-int rsk_gen_keys16(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* dev_out) {
-  return guarded([&] {
-    need(c && (dev_out || n == 0), "NULL argument");
-    CtxLock l(c);
-    if (n) gen_keys16_launch(c, seed, start, n, dev_out);
-    RSK_HIP(hipStreamSynchronize(c->stream));
-  });
+}  // extern "C"
+
+// ------------------------------------------------------------ asynchronous
+namespace {
+
+enum AsyncKind { K_PRESET = 0, K_RES_U64 = 1, K_HLL_FLAG = 2, K_OUT_BYTES = 3 };
+constexpr uint64_t ASYNC_STAGE_MAX = 256ull << 20;  // larger host batches run synchronously
+
+// Runs on the runtime's callback thread once the stream reaches it: no HIP
+// call here.  Derives the reply, copies per-key outputs to the caller, hands
+// the op back to the pool, then calls the caller.
+void op_complete(void* p) {
+  auto* op = static_cast<AsyncOp*>(p);
+  uint64_t v = op->value;
+  switch (op->kind) {
+    case K_RES_U64:
+      v = op->h_res[0];
+      break;
+    case K_HLL_FLAG:
+      v = ((uint32_t)op->h_res[0] == op->epoch || op->created) ? 1 : 0;
+      break;
+    case K_OUT_BYTES:
+      if (op->user_out && op->n_out) std::memcpy(op->user_out, op->h_out, op->n_out);
+      break;
+    default:
+      break;
+  }
+  const rsk_done_fn cb = op->cb;
+  void* user = op->user;
+  rsk_ctx* c = op->c;
+  {
+    std::lock_guard<std::mutex> g(c->async_mu);
+    c->async_free.push_back(op);
+  }
+  if (cb) cb(user, RSK_OK, v);
 }
 
-int rsk_gen_grouped(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* dev_groups,
-                    void* dev_keys) {
-  return guarded([&] {
-    need(c && G > 0 && ((dev_groups && dev_keys) || n == 0), "bad arguments");
-    CtxLock l(c);
-    if (n) gen_grouped_launch(c, seed, G, start, n, dev_groups, dev_keys);
-    RSK_HIP(hipStreamSynchronize(c->stream));
-  });
-}
-
-int rsk_gen_grouped_zipf(rsk_ctx* c, uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n,
-                         uint32_t* dev_groups, void* dev_keys) {
-  return guarded([&] {
-    need(c && G > 0 && G < (1ull << 32) && ((dev_groups && dev_keys) || n == 0), "bad arguments");
-    need(s > 0.0 && s < 16.0, "Zipf exponent must be in (0, 16)");
-    CtxLock l(c);
-    if (!n) return;
-    const std::vector<uint64_t> cdf = zipf_cdf((uint32_t)G, s);
-    uint64_t* d_cdf = nullptr;
-    RSK_HIP(hipMalloc(&d_cdf, 8 * G));
-    hipError_t e = hipMemcpyAsync(d_cdf, cdf.data(), 8 * G, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) {
-      gen_grouped_zipf_launch(c, seed, d_cdf, (uint32_t)G, start, n, dev_groups, dev_keys);
-      e = hipStreamSynchronize(c->stream);
+// An op with >= host_bytes of pinned and >= dev_bytes of device buffer
+// (called under the context lock; a pooled op is never in flight).
+AsyncOp* op_get(rsk_ctx* c, uint64_t host_bytes, uint64_t dev_bytes) {
+  AsyncOp* op = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->async_mu);
+    if (!c->async_free.empty()) {
+      op = c->async_free.back();
+      c->async_free.pop_back();
     }
-    (void)hipFree(d_cdf);
-    RSK_HIP(e);
-  });
+  }
+  if (!op) {
+    op = new AsyncOp();
+    op->c = c;
+    if (hipHostMalloc(&op->h_res, 64, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      delete op;
+      throw RskError{RSK_ERR_OUT_OF_MEMORY, "pinned allocation for an asynchronous call failed"};
+    }
+    std::lock_guard<std::mutex> g(c->async_mu);
+    c->async_all.push_back(op);
+  }
+  auto give_back = [&] {
+    std::lock_guard<std::mutex> g(c->async_mu);
+    c->async_free.push_back(op);
+  };
+  try {
+    if (host_bytes > op->h_bytes) {
+      if (op->h_buf) RSK_HIP(hipHostFree(op->h_buf));
+      op->h_buf = nullptr;
+      op->h_bytes = 0;
+      const uint64_t sz = std::max<uint64_t>(host_bytes, 1ull << 20);
+      RSK_HIP(hipHostMalloc(&op->h_buf, sz, hipHostMallocDefault));
+      op->h_bytes = sz;
+    }
+    if (dev_bytes > op->d_bytes) {
+      if (op->d_buf) RSK_HIP(hipFree(op->d_buf));
+      op->d_buf = nullptr;
+      op->d_bytes = 0;
+      const uint64_t sz = std::max<uint64_t>(dev_bytes, 1ull << 20);
+      RSK_HIP(hipMalloc(&op->d_buf, sz));
+      op->d_bytes = sz;
+    }
+  } catch (...) {
+    give_back();
+    throw;
+  }
+  op->cb = nullptr;
+  op->user = nullptr;
+  op->kind = K_PRESET;
+  op->value = 0;
+  op->user_out = op->h_out = nullptr;
+  op->n_out = 0;
+  op->created = false;
+  op->epoch = 0;
+  return op;
 }
 
-int rsk_gen_queries16(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
-                      void* dev_out) {
-  return guarded([&] {
-    need(c && n_ins > 0 && (dev_out || n == 0), "bad arguments");
-    CtxLock l(c);
-    if (n) gen_queries16_launch(c, qseed, iseed, n_ins, start, n, dev_out);
-    RSK_HIP(hipStreamSynchronize(c->stream));
-  });
+void op_release(AsyncOp* op) {  // an op that was taken but will not be submitted
+  std::lock_guard<std::mutex> g(op->c->async_mu);
+  op->c->async_free.push_back(op);
 }
 
-int rsk_gen_varlen(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* dev_offsets, void* dev_blob,
-                   uint64_t blob_cap, uint64_t* total_bytes) {
+void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
+  op->cb = cb;
+  op->user = user;
+  RSK_HIP(hipLaunchHostFunc(op->c->stream, op_complete, op));
+}
+
+uint64_t al256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+// Bytes of a host batch's keys (+ offsets) as one staged copy.
+uint64_t host_key_bytes(const rsk_keys* k) {
+  if (k->n == 0) return 0;
+  if (!k->offsets) return k->n * k->fixed_len;
+  need(k->offsets[k->n] >= k->offsets[0], "offsets must be non-decreasing");
+  return al256(k->offsets[k->n] - k->offsets[0]) + 8 * (k->n + 1);
+}
+
+// Copies a host batch into op's pinned buffer at `at` (one memcpy by host
+// threads) and enqueues one DMA to the op's device buffer; returns the device
+// view of the keys.  Device batches are used in place.
+DevKeys stage_keys(rsk_ctx* c, const rsk_keys* k, AsyncOp* op, uint64_t at) {
+  if (k->location == RSK_MEM_DEVICE || k->n == 0)
+    return DevKeys{reinterpret_cast<const uint8_t*>(k->data), k->offsets, k->n, k->fixed_len};
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(k->data);
+  if (!k->offsets) {
+    const uint64_t bytes = k->n * k->fixed_len;
+    par_copy(op->h_buf + at, src, bytes, c->stage_threads);
+    RSK_HIP(hipMemcpyAsync(op->d_buf + at, op->h_buf + at, bytes, hipMemcpyHostToDevice, c->stream));
+    return DevKeys{op->d_buf + at, nullptr, k->n, k->fixed_len};
+  }
+  for (uint64_t i = 0; i < k->n; ++i) need(k->offsets[i + 1] >= k->offsets[i], "offsets must be non-decreasing");
+  const uint64_t base = k->offsets[0], data_bytes = al256(k->offsets[k->n] - base);
+  par_copy(op->h_buf + at, src + base, k->offsets[k->n] - base, c->stage_threads);
+  std::memcpy(op->h_buf + at + data_bytes, k->offsets, 8 * (k->n + 1));
+  RSK_HIP(hipMemcpyAsync(op->d_buf + at, op->h_buf + at, data_bytes + 8 * (k->n + 1), hipMemcpyHostToDevice,
+                         c->stream));
+  // offsets stay absolute: shift the data pointer instead of rebasing
+  return DevKeys{op->d_buf + at - base, reinterpret_cast<const uint64_t*>(op->d_buf + at + data_bytes), k->n, 0};
+}
+
+// The synchronous call, then the callback on the calling thread (host batches
+// above ASYNC_STAGE_MAX: staging them whole would pin that much memory).
+template <class F>
+int run_now(F&& sync_call, rsk_done_fn cb, void* user, uint64_t value_if_void, bool value_from_call) {
+  uint64_t v = value_if_void;
+  const int rc = sync_call(&v);
+  if (rc == RSK_OK && cb) cb(user, RSK_OK, value_from_call ? v : value_if_void);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsk_hll_add_async(rsk_hll* h, uint64_t id, const rsk_keys* keys, rsk_done_fn cb, void* user) {
+  if (keys && keys->location == RSK_MEM_HOST && keys->n && h && id < h->n) {
+    uint64_t kb = 0;
+    int rc = guarded([&] { kb = host_key_bytes(keys); });
+    if (rc != RSK_OK) return rc;
+    if (kb > ASYNC_STAGE_MAX)
+      return run_now([&](uint64_t* v) {
+        uint8_t ch = 0;
+        const int r = rsk_hll_add(h, id, keys, &ch);
+        *v = ch;
+        return r;
+      }, cb, user, 0, true);
+  }
   return guarded([&] {
-    need(c && dev_offsets && total_bytes, "NULL argument");
-    need(n < (1ull << 31), "n must be < 2^31 per call");
+    check_hll(h, id);
+    rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    gen_varlen_lengths_launch(c, seed, start, n, dev_offsets);
-    uint64_t tot = 0;
-    RSK_HIP(hipMemcpyAsync(&tot, dev_offsets + n, 8, hipMemcpyDeviceToHost, c->stream));
-    RSK_HIP(hipStreamSynchronize(c->stream));
-    *total_bytes = tot;
-    if (dev_blob) {
-      need(blob_cap >= tot, "blob capacity too small");
-      gen_varlen_bytes_launch(c, seed, start, n, dev_offsets, reinterpret_cast<uint8_t*>(dev_blob));
-      RSK_HIP(hipStreamSynchronize(c->stream));
+    check_keys(c, keys);
+    const uint64_t kb = keys->location == RSK_MEM_HOST ? host_key_bytes(keys) : 0;
+    AsyncOp* op = op_get(c, kb, kb);
+    bool created = false;
+    try {
+      create_if_missing(h, id, &created);
+      hll_forget_import(h, id);
+      uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->d_small);
+      if (++c->epoch == 0) {
+        RSK_HIP(hipMemsetAsync(d_flag, 0, 4, c->stream));
+        c->epoch = 1;
+      }
+      op->epoch = c->epoch;
+      op->created = created;
+      op->kind = K_HLL_FLAG;
+      const DevKeys dk = stage_keys(c, keys, op, 0);
+      if (dk.n) hll_add_launch(c, dk, regs_of(h, id), h->d_card + id, d_flag, op->epoch, created);
+      else if (created) invalidate(h, id, nullptr, true);
+      RSK_HIP(hipMemcpyAsync(op->h_res, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
     }
   });
+}
+
+int rsk_hll_count_async(rsk_hll* h, uint64_t id, rsk_done_fn cb, void* user) {
+  return guarded([&] {
+    check_hll(h, id);
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    AsyncOp* op = op_get(c, 0, 256);
+    try {
+      SmallIds small{};
+      small.v[0] = id;
+      small.n = 1;
+      uint64_t* d_out = reinterpret_cast<uint64_t*>(op->d_buf);
+      hll_count_launch(c, h->d_regs, h->d_card, nullptr, small, 1, d_out, PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
+      RSK_HIP(hipMemcpyAsync(op->h_res, d_out, 8, hipMemcpyDeviceToHost, c->stream));
+      op->kind = K_RES_U64;
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+int rsk_hll_count_union_async(rsk_hll* const* hs, const uint64_t* ids, uint32_t k, rsk_done_fn cb, void* user) {
+  return guarded([&] {
+    need(hs && ids && k >= 1 && hs[0], "bad arguments");
+    rsk_ctx* c = hs[0]->ctx;
+    CtxLock l(c);
+    for (uint32_t a = 0; a < k; ++a) {
+      check_hll(hs[a], ids[a]);
+      need(hs[a]->ctx == c, "all sketches must share one context");
+    }
+    const uint64_t pb = al256(8ull * k);
+    AsyncOp* op = op_get(c, pb, pb + 256);
+    try {
+      auto* ptrs = reinterpret_cast<const uint8_t**>(op->h_buf);
+      for (uint32_t a = 0; a < k; ++a) ptrs[a] = hs[a]->exists[ids[a]] ? regs_of(hs[a], ids[a]) : nullptr;
+      auto* d_ptrs = reinterpret_cast<const uint8_t**>(op->d_buf);
+      auto* d_out = reinterpret_cast<uint64_t*>(op->d_buf + pb);
+      RSK_HIP(hipMemcpyAsync(d_ptrs, ptrs, 8ull * k, hipMemcpyHostToDevice, c->stream));
+      hll_union_count_launch(c, d_ptrs, k, 1, d_out);
+      RSK_HIP(hipMemcpyAsync(op->h_res, d_out, 8, hipMemcpyDeviceToHost, c->stream));
+      op->kind = K_RES_U64;
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+int rsk_hll_merge_async(rsk_hll* dst, uint64_t dst_id, rsk_hll* const* srcs, const uint64_t* src_ids, uint32_t k,
+                        rsk_done_fn cb, void* user) {
+  return guarded([&] {
+    check_hll(dst, dst_id);
+    need(k == 0 || (srcs && src_ids), "srcs is NULL");
+    rsk_ctx* c = dst->ctx;
+    CtxLock l(c);
+    for (uint32_t a = 0; a < k; ++a) {
+      check_hll(srcs[a], src_ids[a]);
+      need(srcs[a]->ctx == c, "all sketches must share one context");
+    }
+    const uint64_t pb = al256(8ull * k + 8);
+    AsyncOp* op = op_get(c, pb, pb);
+    try {
+      auto* ptrs = reinterpret_cast<const uint8_t**>(op->h_buf);
+      ptrs[0] = regs_of(dst, dst_id);
+      for (uint32_t a = 0; a < k; ++a) ptrs[1 + a] = srcs[a]->exists[src_ids[a]] ? regs_of(srcs[a], src_ids[a]) : nullptr;
+      bool created;
+      create_if_missing(dst, dst_id, &created);
+      hll_forget_import(dst, dst_id);
+      dst->dense[dst_id] = 1;  // pfmergeCommand converts the destination to dense
+      if (k) {
+        RSK_HIP(hipMemcpyAsync(op->d_buf, ptrs, 8ull * (k + 1), hipMemcpyHostToDevice, c->stream));
+        hll_merge_launch(c, reinterpret_cast<uint8_t**>(op->d_buf), reinterpret_cast<const uint8_t**>(op->d_buf) + 1, k, 1);
+      }
+      invalidate(dst, dst_id, nullptr, true);
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+int rsk_hll_merge_batch_async(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_ids, uint64_t n, rsk_done_fn cb,
+                              void* user) {
+  return guarded([&] {
+    need(h && (n == 0 || (dst_ids && src_ids)), "NULL argument");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    merge_batch_check(h, dst_ids, src_ids, n);
+    AsyncOp* op = op_get(c, n ? merge_batch_host_bytes(n) : 0, n ? merge_batch_dev_bytes(n) : 0);
+    try {
+      if (n) merge_batch_enqueue(h, dst_ids, src_ids, n, op->h_buf, op->d_buf);
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+}  // extern "C"
+
+namespace {
+// Shared body of the Bloom async calls: keys staged, `launch` enqueues the
+// kernels writing per-key outputs to d_out, outputs read back for host keys.
+template <class L>
+int bloom_async(rsk_bloom* b, const rsk_keys* keys, uint8_t* out, bool out_required, rsk_done_fn cb, void* user,
+                L&& launch, int (*sync_call)(rsk_bloom*, const rsk_keys*, uint8_t*)) {
+  if (b && keys && keys->location == RSK_MEM_HOST && keys->n) {
+    uint64_t kb = 0;
+    int rc = guarded([&] { kb = host_key_bytes(keys) + keys->n; });
+    if (rc != RSK_OK) return rc;
+    if (kb > ASYNC_STAGE_MAX)
+      return run_now([&](uint64_t*) { return sync_call(b, keys, out); }, cb, user, keys->n, false);
+  }
+  return guarded([&] {
+    need(b != nullptr, "bloom handle is NULL");
+    need(!out_required || out != nullptr, "out is NULL");
+    rsk_ctx* c = b->ctx;
+    CtxLock l(c);
+    check_keys(c, keys);
+    check_out(c, keys, out);
+    const bool host = keys->location == RSK_MEM_HOST;
+    const uint64_t kb = host ? al256(host_key_bytes(keys)) : 0;
+    const uint64_t ob = (host && out) ? keys->n : 0;
+    AsyncOp* op = op_get(c, kb + ob, kb + ob);
+    try {
+      const DevKeys dk = stage_keys(c, keys, op, 0);
+      uint8_t* d_out = out ? (host ? op->d_buf + kb : out) : nullptr;
+      if (dk.n) launch(c, b, dk, d_out);
+      if (host && out && keys->n) {
+        RSK_HIP(hipMemcpyAsync(op->h_buf + kb, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
+        op->h_out = op->h_buf + kb;
+        op->user_out = out;
+        op->n_out = keys->n;
+      }
+      op->kind = K_OUT_BYTES;
+      op->value = keys->n;
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+}  // namespace
+
+extern "C" {
+
+int rsk_bloom_add_async(rsk_bloom* b, const rsk_keys* keys, uint8_t* added_out, rsk_done_fn cb, void* user) {
+  return bloom_async(
+      b, keys, added_out, false, cb, user,
+      [](rsk_ctx* c, rsk_bloom* bf, const DevKeys& dk, uint8_t* d_out) {
+        if (d_out) bloom_add_replies_launch(c, bf, dk, d_out);
+        else bloom_add_launch(c, bf, dk);
+      },
+      rsk_bloom_add);
+}
+
+int rsk_bloom_contains_async(rsk_bloom* b, const rsk_keys* keys, uint8_t* out, rsk_done_fn cb, void* user) {
+  return bloom_async(
+      b, keys, out, true, cb, user,
+      [](rsk_ctx* c, rsk_bloom* bf, const DevKeys& dk, uint8_t* d_out) { bloom_contains_launch(c, bf, dk, d_out); },
+      rsk_bloom_contains);
 }
 
 }  // extern "C"

@@ -343,17 +343,6 @@ __global__ __launch_bounds__(APPLY_T) void bloom_slice_apply_kernel(const uint32
   }
 }
 
-static int part_mode() {
-  const char* e = std::getenv("RSK_BLOOM_PARTITION");  // unset: auto; "0": never; "1": always
-  if (!e || !*e) return -1;
-  return e[0] == '0' ? 0 : 1;
-}
-
-static uint32_t env_u32(const char* name, uint32_t dflt) {  // tuning knobs (scripts/bloom_part_tune.py)
-  const char* e = std::getenv(name);
-  return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
-}
-
 static uint32_t bits_for(uint64_t v) {  // bits needed to hold v (0 -> 0)
   uint32_t b = 0;
   while (v) {
@@ -364,11 +353,11 @@ static uint32_t bits_for(uint64_t v) {  // bits needed to hold v (0 -> 0)
 }
 
 bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
-  const int mode = part_mode();
+  const int mode = c->tune.bloom_part;  // 0 auto, 1 at any batch size, -1 never
   const uint64_t k = (uint64_t)b->k;
   const uint64_t nslices = ((uint64_t)b->size + (1ull << SLICE_LOG) - 1) >> SLICE_LOG;
-  if (mode == 0 || k < 1 || k > TILE || nslices > MAX_SLICES || keys.n == 0) return false;
-  if (mode < 0 && keys.n * k < (1ull << 22)) return false;  // small batches: direct atomics
+  if (mode < 0 || k < 1 || k > TILE || nslices > MAX_SLICES || keys.n == 0) return false;
+  if (mode == 0 && keys.n * k < (1ull << 22)) return false;  // small batches: direct atomics
   const bool f16 =
       keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
   const uint32_t sb = bits_for(nslices - 1);
@@ -377,8 +366,8 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
   const uint32_t nbins1 = (uint32_t)(((nslices - 1) >> f2) + 1);
   const uint32_t ns = (uint32_t)nslices;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t G = std::max<uint32_t>(1, env_u32("RSK_BLOOM_G_PER_CU", 2)) * cus;  // hist / part1 blocks
-  const uint32_t p2_grid = std::max<uint32_t>(1, env_u32("RSK_BLOOM_P2_PER_CU", 4)) * cus;
+  const uint32_t G = 2 * cus;        // hist / part1 blocks (3 and 4 per CU measured slower)
+  const uint32_t p2_grid = 4 * cus;
 
   const uint64_t chunk = std::max<uint64_t>(1, PROBE_CAP / k);
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk) * k;

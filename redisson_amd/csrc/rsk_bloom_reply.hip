@@ -54,7 +54,7 @@ constexpr uint32_t RA_T = 1024;                       // rp_apply workgroup
 constexpr uint64_t MAX_CHUNK_KEYS = 0xFFFFFFFEull;    // key indices < NONE
 constexpr uint64_t DEFAULT_CHUNK_PROBES = 1ull << 33;  // scratch bound: ~2.3 x 8 B per probe
 #ifndef RSK_RP_U
-#define RSK_RP_U 2  // rp_reply: keys (gather chains) per lane
+#define RSK_RP_U 2  // rp_reply: keys (gather chains) per lane (1, 2 and 4 measured alike)
 #endif
 
 // ------------------------------------------------------------------ sizing
@@ -330,11 +330,6 @@ __global__ __launch_bounds__(256) void rp_reply_kernel(const uint8_t* __restrict
   }
 }
 
-uint32_t env_knob(const char* name, uint32_t dflt) {
-  const char* e = std::getenv(name);
-  return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
-}
-
 }  // namespace
 
 // add() with replies through the partition (see the file comment).  Returns
@@ -342,9 +337,9 @@ uint32_t env_knob(const char* name, uint32_t dflt) {
 bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uint8_t* d_out) {
   const uint64_t k = (uint64_t)b->k;
   const uint64_t nslices = ((uint64_t)b->size + (1ull << SL_LOG) - 1) >> SL_LOG;
-  const char* mode = std::getenv("RSK_BLOOM_REPLY");  // "0": always the sort path; "1": this path at any size
-  const bool force = mode && mode[0] == '1';
-  if ((mode && mode[0] == '0') || keys.n == 0 || k > 16 || nslices > SL_MAX) return false;
+  const int route = c->tune.reply;  // 0 auto, 1 this path at any batch size, -1 always the sort path
+  const bool force = route > 0;
+  if (route < 0 || keys.n == 0 || k > 16 || nslices > SL_MAX) return false;
   if (!force && keys.n * k < (1ull << 22)) return false;
   if (k == 1) {  // no reply looks at any probe (the first k-1 = none)
     RSK_HIP(hipMemsetAsync(d_out, 0, keys.n, c->stream));
@@ -365,9 +360,9 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint32_t ns = (uint32_t)nslices;
   const uint64_t nblocks = ((uint64_t)b->size + RB_BITS - 1) / RB_BITS;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t P = std::max<uint32_t>(1, env_knob("RSK_BLOOM_SA_P", 4 * cus / nb1));  // as the insert's sa2
+  const uint32_t P = std::max<uint32_t>(1, c->tune.sa_parts ? c->tune.sa_parts : 4 * cus / nb1);  // as the insert's sa2
   const uint32_t ncp = nb1 * P;
-  const uint64_t probe_cap = env_knob("RSK_BLOOM_REPLY_CHUNK", 0) ? env_knob("RSK_BLOOM_REPLY_CHUNK", 0) : DEFAULT_CHUNK_PROBES;
+  const uint64_t probe_cap = c->tune.reply_chunk ? c->tune.reply_chunk : DEFAULT_CHUNK_PROBES;
   uint64_t chunk = std::max<uint64_t>(1, probe_cap / k / kst) * kst;  // keys per chunk, whole super-tiles
   if (chunk > MAX_CHUNK_KEYS) chunk = MAX_CHUNK_KEYS / kst * kst;
   chunk = std::min<uint64_t>(chunk, keys.n);
@@ -379,7 +374,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const double share = std::min(1.0, (double)(1ull << shift1) / (double)(uint64_t)b->size);  // of a coarse bin
   const uint64_t q64 = (uint64_t)(1.25 * share * (double)max_np / W) + kst * k + (max_nst / W + 1) + 64;
   const uint32_t quota = (uint32_t)((q64 + 3) & ~uint64_t(3));
-  const uint32_t limit = env_knob("RSK_BLOOM_SA_TINY", 0) ? 32 : quota;  // tests force the overflow fallback
+  const uint32_t limit = c->tune.sa_tiny ? 32 : quota;  // tests force the overflow fallback
   if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;
   const uint64_t region_probes = (uint64_t)W * nb1 * quota;
   const uint64_t slots = sa2_slots<uint64_t>();
@@ -392,6 +387,25 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
                         al(8 * (ns + 1)) * 2 + al(4 * (ns + 1)) * 3;
   const uint64_t bytes = al(8 * reg_probes) + al(8 * l2_probes) + 2 * h2_bytes + al(8 * tt_max) +
                          al(tt3_max * (RB_PER_SL + 1) * 2) + al(8 * tt3_max) + al(4 * nblocks * RB_BITS) + meta;
+  // The scratch (4 B of first-key table per filter bit, 8-byte records of
+  // three passes: ~165 GB at C3) must fit the device next to everything
+  // else: when it does not, the sort path answers the batch instead (it
+  // needs far less).  Reserved before any chunk is applied.
+  {
+    size_t free_b = 0, total_b = 0;
+    if (bytes > c->work_bytes) {  // growing frees the old buffer first
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && (double)bytes > 0.9 * (double)(free_b + c->work_bytes))
+        return false;
+      (void)hipGetLastError();
+    }
+    try {
+      c->work(bytes);
+    } catch (const RskError& e) {
+      if (e.code != RSK_ERR_OUT_OF_MEMORY) throw;
+      (void)hipGetLastError();
+      return false;
+    }
+  }
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     // Scratch is per chunk; taken again each chunk (the sort fallback below may
     // have regrown the work buffer).
@@ -433,7 +447,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       ProfScope ps(c, "bloom_rp1");
 #define RSK_RP1(F16, KM)                                                                                          \
   hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint64_t>), dim3(Wc), dim3(T1), 0, c->stream, dk.data,        \
-                     dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, overflow, 0)
+                     dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, overflow)
       if (f16 && kmax == 8) RSK_RP1(true, 8);
       else if (f16) RSK_RP1(true, 16);
       else if (kmax == 8) RSK_RP1(false, 8);
@@ -461,9 +475,8 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp2");
-      auto k2 = env_knob("RSK_BLOOM_SA2_PF", 0) ? bloom_sa2_kernel<uint64_t, true> : bloom_sa2_kernel<uint64_t, false>;
-      hipLaunchKernelGGL(k2, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P, nb2, reg_off,
-                         tile_off, tiles, l2, h2, tb2, 0);
+      hipLaunchKernelGGL(bloom_sa2_kernel<uint64_t>, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc,
+                         nb1, P, nb2, reg_off, tile_off, tiles, l2, h2, tb2);
       RSK_CHECK_LAUNCH("bloom_rp2");
     }
     {
@@ -493,22 +506,15 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp_reply");
-      // keys per lane: RSK_RP_U at build time, RSK_BLOOM_RP_U=1|2|4 at run time (tuning)
-      const uint32_t u = env_knob("RSK_BLOOM_RP_U", RSK_RP_U);
-      auto launch = [&](auto U_) {
-        constexpr int U = decltype(U_)::value;
-        const uint64_t g = (m + 256 * U - 1) / (256 * U);
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
-        if (f16)
-          hipLaunchKernelGGL((rp_reply_kernel<true, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                             dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
-        else
-          hipLaunchKernelGGL((rp_reply_kernel<false, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                             dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
-      };
-      if (u == 4) launch(std::integral_constant<int, 4>());
-      else if (u == 1) launch(std::integral_constant<int, 1>());
-      else launch(std::integral_constant<int, 2>());
+      constexpr int U = RSK_RP_U;  // keys (gather chains) per lane
+      const uint64_t g = (m + 256 * U - 1) / (256 * U);
+      const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
+      if (f16)
+        hipLaunchKernelGGL((rp_reply_kernel<true, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
+                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
+      else
+        hipLaunchKernelGGL((rp_reply_kernel<false, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
+                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
       RSK_CHECK_LAUNCH("bloom_rp_reply");
     }
   }

@@ -248,26 +248,17 @@ constexpr uint32_t sa2_pad() { return (16 / sizeof(R) - 1) * 128; }  // pad slot
 constexpr uint32_t SA2_SLOTS = sa2_slots<uint32_t>();
 constexpr uint32_t SA2_PAD = sa2_pad<uint32_t>();
 
-RSK_DEV void sa_bar(int dbg) {  // dbg (RSK_BLOOM_SA_DBG): full __syncthreads instead of the LDS-only barrier
-  if (dbg) __syncthreads();
-  else lds_barrier();
-}
-
 // 512-lane workgroups: at most 80 VGPRs with 4-byte records, so 3 workgroups
 // (6 waves per SIMD) share a CU; 8-byte records: 2 workgroups (73 KiB of LDS).
 // u64 records carry the key's index in the chunk (the host keeps a chunk
 // below 2^32 - 1 keys).
-// DIAG (timing diagnostics only, RSK_BLOOM_SA1_DIAG; results are not a
-// filter): 1 = the key words instead of XXH64 / farmhash, 2 = also probe
-// indices by one multiply-high instead of the exact u63 remainders, 3 = as 2
-// and no write-out (which leaves the image, so the scatter, dead as well).
 // KPL: keys per lane (default 16 / KMAX); more keys per super-tile make every
 // bin's run longer.
-template <bool FIXED16, int KMAX, int T1, class R, int DIAG = 0, int KPL = 16 / KMAX>
+template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX>
 __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
     FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
-    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow, int dbg) {
+    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow) {
   constexpr uint32_t KST = T1 * KPL;
   constexpr int NP = KPL * KMAX;
   constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
@@ -304,7 +295,7 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
     const uint4* img4 = reinterpret_cast<const uint4*>(img);
     for (uint32_t g = threadIdx.x; g < total4; g += T1) {
       const uint32_t d = dst[ibin[g]];
-      if (DIAG != 3 && d != INVALID) {
+      if (d != INVALID) {
         const uint4 v = img4[g];
         u32x4 x = {v.x, v.y, v.z, v.w};
         *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
@@ -334,36 +325,30 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
         if (FIXED16) {
           uint64_t w0, w1;
           key_words(cur[u], &w0, &w1);
-          if constexpr (DIAG >= 1) {
-            h1 = w0;
-            h2 = w1;
-          } else {
-            h1 = xxh64_16(w0, w1);
-            h2 = farm_16(w0, w1);
-          }
+          h1 = xxh64_16(w0, w1);
+          h2 = farm_16(w0, w1);
         } else {
           bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
         }
       }
-      ProbeSeq ps;
-      if constexpr (DIAG < 2) ps = ProbeSeq(h1, h2, fm);
+      ProbeSeq ps(h1, h2, fm);
 #pragma unroll
       for (int t = 0; t < KMAX; ++t) {
         const int s = u * KMAX + t;
         tag[s] = INVALID;
         pay[s] = 0;
         if (ok && t < k) {
-          const uint64_t idx = DIAG >= 2 ? __umul64hi(h1 + (uint64_t)t * h2, fm.d) : ps.idx;
+          const uint64_t idx = ps.idx;
           const uint32_t bin = (uint32_t)(idx >> shift1);
           pay[s] = rec_make<R>((uint32_t)(idx & low), key);
           tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
-          if (DIAG < 2 && t + 1 < k) ps.next(t, fm);
+          if (t + 1 < k) ps.next(t, fm);
         }
       }
     }
     if (FIXED16) fetch(st + gridDim.x);
     write_out(pend4);  // tile t - 1
-    sa_bar(dbg);  // (A) every rank taken, the previous image written out
+    lds_barrier();  // (A) every rank taken, the previous image written out
     // wave 0: bin starts and run destinations (runs of L probes take
     // L4 = round_up(L, RG) slots, the tail rec_pad): image position j of bin b
     // goes to mine[j + dst[b]] (mod 2^32), dst[b] = b quota + pos[b] - lstart[b]
@@ -398,7 +383,7 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
       }
       if (lane == 63) s_total = incl;
     }
-    sa_bar(dbg);  // (B) lstart / dst / total ready
+    lds_barrier();  // (B) lstart / dst / total ready
 #pragma unroll
     for (int s = 0; s < NP; ++s)
       if (tag[s] != INVALID) {
@@ -407,7 +392,7 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
         if ((r & (RG - 1)) == 0) ibin[j / RG] = (uint8_t)b;  // the group's first slot always holds a probe
       }
     pend4 = s_total / RG;
-    sa_bar(dbg);  // (C) image complete
+    lds_barrier();  // (C) image complete
   }
   write_out(pend4);  // the last tile
   __syncthreads();
@@ -435,19 +420,18 @@ __global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict
   bud[cp] = tiles;
 }
 
-// PF: tile t + 1's loads issue after tile t's ranks (otherwise at the top of
-// tile t + 1, as the other loads' latency is covered by the second
-// workgroup of the CU).  __launch_bounds__(1024, 8): at most 64 VGPRs, so two
-// workgroups share a CU.
-template <class R, bool PF = false>
+// A tile's loads issue at its top (a register prefetch of the next tile
+// needs 64+ VGPRs: the second workgroup of the CU covers the latency
+// instead).  __launch_bounds__(1024, 8): at most 64 VGPRs, so two workgroups
+// share a CU.
+template <class R>
 __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict__ region, uint32_t quota,
                                                           const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
                                                           uint32_t P, uint32_t nb2,
                                                           const uint64_t* __restrict__ reg_off,
                                                           const uint32_t* __restrict__ tile_off,
                                                           uint32_t* __restrict__ tiles_out, R* __restrict__ out,
-                                                          uint16_t* __restrict__ h2, uint64_t* __restrict__ tb2,
-                                                          int dbg) {
+                                                          uint16_t* __restrict__ h2, uint64_t* __restrict__ tb2) {
   constexpr uint32_t RG = 16 / sizeof(R);
   constexpr int NV = SA2_V * RG;
   constexpr uint32_t SLOTS = sa2_slots<R>();
@@ -464,9 +448,8 @@ __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict
   uint64_t written = 0;
   uint32_t ntile = 0;
   // Tiles run over the sub-regions (w, c) of this part in order.  As in sa1,
-  // the loads of tile t + 1 issue after tile t's ranks and the image of tile
-  // t is written out during tile t + 1 (one vmcnt for loads and stores: see
-  // bloom_sa1_kernel).  A uint4 is loaded when its first record is below
+  // the image of tile t is written out during tile t + 1, after its ranks
+  // (one vmcnt for loads and stores: see bloom_sa1_kernel).  A uint4 is loaded when its first record is below
   // `used` (quota is a multiple of RG, so it lies inside the sub-region); the
   // records past `used` are replaced by rec_pad.
   const uint32_t wbeg = W * p / P, wend = W * (p + 1) / P;
@@ -494,16 +477,14 @@ __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict
     }
   };
   bool have = w < wend;
-  if (PF && have) fetch(w, 0, nu);
   uint32_t pend = 0;  // records of the previous tile still in the image
   uint64_t pend_at = 0;
   __syncthreads();
   while (have) {
-    if (!PF) fetch(w, t0, nu);
+    fetch(w, t0, nu);
     uint4 cur[SA2_V];
 #pragma unroll
     for (int v = 0; v < SA2_V; ++v) cur[v] = nxt[v];
-    if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t's records, before tile t + 1's loads issue
     const uint32_t ct0 = t0, cnu = nu;
     t0 += SLOTS;
     if (t0 >= nu) {
@@ -530,11 +511,10 @@ __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict
         tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
       }
     }
-    if (PF && have) fetch(w, t0, nu);
     write_out(pend, pend_at);  // tile t - 1
-    sa_bar(dbg);  // (A) ranks taken, the previous image written out
+    lds_barrier();  // (A) ranks taken, the previous image written out
     if (threadIdx.x < 64) wave0_bin_starts_pad<128, R>(hist, lstart, nb2, s_hdr, &s_total, srt[0]);
-    sa_bar(dbg);  // (B)
+    lds_barrier();  // (B)
     const uint32_t total = s_total;  // padded: a multiple of RG
     if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
     if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
@@ -547,7 +527,7 @@ __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict
     pend_at = written;
     written += total;
     ++ntile;
-    sa_bar(dbg);  // (C)
+    lds_barrier();  // (C)
   }
   write_out(pend, pend_at);
   if (threadIdx.x == 0) tiles_out[cp] = ntile;

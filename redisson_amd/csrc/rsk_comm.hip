@@ -190,6 +190,7 @@ int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
     if (ok) {
       rsk::hll_materialize(h);
       rsk::hll_touch(h);
+      rsk::hll_forget_import(h, id);
     } else {
       RSK_HIP(hipMemsetAsync(regs, 0, rsk::HLL_REGS, c->stream));
     }
@@ -210,10 +211,11 @@ int rsk_hll_allreduce(rsk_hll* h, uint64_t id) {
 int rsk_hll_allreduce_pool(rsk_hll* h) {
   return guarded([&] {
     need(h != nullptr, "bad pool");
-    rsk::hll_materialize(h);
-    rsk::hll_touch(h);
     rsk_ctx* c = h->ctx;
     Lock l(c);
+    rsk::hll_materialize(h);
+    rsk::hll_touch(h);
+    rsk::hll_forget_imports(h);
     ncclComm_t comm = comm_of(c);
     {
       rsk::ProfScope ps(c, "hll_allreduce_pool");
@@ -231,10 +233,11 @@ int rsk_hll_allreduce_pool(rsk_hll* h) {
 int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_out) {
   return guarded([&] {
     need(h && first_out && count_out, "NULL argument");
-    rsk::hll_materialize(h);
-    rsk::hll_touch(h);
     rsk_ctx* c = h->ctx;
     Lock l(c);
+    rsk::hll_materialize(h);
+    rsk::hll_touch(h);
+    rsk::hll_forget_imports(h);
     ncclComm_t comm = comm_of(c);
     const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank, R = rsk::HLL_REGS;
     const uint64_t q = h->n / N, tail = h->n - q * N;
@@ -257,18 +260,22 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
 
 int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32_t flags) {
   return guarded([&] {
-    need(h && (ids || n == 0), "NULL argument");
-    need((flags & ~RSK_FETCH_SELF) == 0, "unknown flags");
-    rsk::hll_materialize(h);
-    rsk::hll_touch(h);
+    need(h != nullptr, "NULL handle");  // no communicator to agree through without one
     rsk_ctx* c = h->ctx;
     Lock l(c);
+    rsk::hll_materialize(h);
+    rsk::hll_touch(h);
+    rsk::hll_forget_imports(h);
     ncclComm_t comm = comm_of(c);
     const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank, R = rsk::HLL_REGS;
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+    // Local argument errors (NULL ids, unknown flags, an id outside the pool)
+    // are not thrown here: they go into the agreed "bad" word below, so no
+    // other rank is left waiting in a collective.
+    const bool args_ok = (ids != nullptr || n == 0) && (flags & ~RSK_FETCH_SELF) == 0;
     // Plan (rsk_plan.hip): distinct requested ids ascending = grouped by owner.
     std::vector<uint64_t> want, cnt_out;
-    const bool ok_local = rsk::plan_fetch(h->n, N, r, ids, n, flags, &want, &cnt_out);
+    const bool ok_local = args_ok && rsk::plan_fetch(h->n, N, r, ids, n, flags, &want, &cnt_out);
     // Every rank agrees on argument errors (and on the pool size, which fixes
     // every rank's owner map) before any exchange: one MAX all-reduce of
     // {bad, n, ~n}; max(~n) = ~min(n).
@@ -285,8 +292,9 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
     }
     RSK_HIP(hipMemcpyAsync(h_meta, d_meta, 24, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
+    need(args_ok, "rsk_hll_fetch_rows: ids is NULL or unknown flags");
     need(ok_local, "sketch id out of range");
-    need(h_meta[0] == 0, "rsk_hll_fetch_rows: another rank passed an invalid sketch id");
+    need(h_meta[0] == 0, "rsk_hll_fetch_rows: another rank passed an invalid argument");
     need(h_meta[1] == ~h_meta[2], "rsk_hll_fetch_rows: pool sizes differ across ranks");
     // Counts: one u64 each way per peer ([0, N): rows asked of rank j; [N, 2N): rows rank j asks of us).
     std::vector<uint64_t> cnt(2 * N, 0);

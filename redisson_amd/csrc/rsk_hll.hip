@@ -18,186 +18,11 @@
 // global atomics), and raises a flag if any register grew.
 #include <hipcub/hipcub.hpp>
 
+#include "rsk_hll_kern.h"
 #include "rsk_hllcount.h"
 #include "rsk_internal.h"
 
 namespace rsk {
-
-// Byte-wise max of four 7-bit lanes (registers are <= 63).
-RSK_DEV uint32_t bmax4(uint32_t a, uint32_t b) {
-  uint32_t d = (a | 0x80808080u) - b;
-  uint32_t m = ((d & 0x80808080u) >> 7) * 0xFFu;
-  return (a & m) | (b & ~m);
-}
-RSK_DEV uint4 bmax16(uint4 a, uint4 b) {
-  return make_uint4(bmax4(a.x, b.x), bmax4(a.y, b.y), bmax4(a.z, b.z), bmax4(a.w, b.w));
-}
-
-// ------------------------------------------------------------------ PFADD
-__device__ __forceinline__ void lds_zero(uint32_t* regs) {
-  uint4* r4 = reinterpret_cast<uint4*>(regs);
-  for (int j = threadIdx.x; j < HLL_REGS / 4; j += blockDim.x) r4[j] = make_uint4(0, 0, 0, 0);
-}
-
-// Pack the LDS file (u32 per register) into 16384 bytes of the slab.
-__device__ __forceinline__ void lds_to_slab(const uint32_t* regs, uint8_t* slab) {
-  const uint4* r4 = reinterpret_cast<const uint4*>(regs);
-  uint4* out = reinterpret_cast<uint4*>(slab);
-  for (int j = threadIdx.x; j < HLL_REGS / 16; j += blockDim.x) {
-    uint4 a = r4[4 * j], b = r4[4 * j + 1], c = r4[4 * j + 2], d = r4[4 * j + 3];
-    uint4 o;
-    o.x = a.x | (a.y << 8) | (a.z << 16) | (a.w << 24);
-    o.y = b.x | (b.y << 8) | (b.z << 16) | (b.w << 24);
-    o.z = c.x | (c.y << 8) | (c.z << 16) | (c.w << 24);
-    o.w = d.x | (d.y << 8) | (d.z << 16) | (d.w << 24);
-    out[j] = o;
-  }
-}
-
-RSK_DEV void hll_update(uint32_t* regs, uint64_t h) {
-  atomicMax(&regs[hll_index(h)], hll_rank(h));
-}
-
-// Fixed 16-byte keys: the C2 hot path.  U keys per lane in flight, T lanes
-// per workgroup (256 measured fastest: fewer waves contend for the LDS file).
-template <int U, int T>
-__global__ __launch_bounds__(T) void hll_add16_kernel(const uint4* __restrict__ keys, uint64_t n,
-                                                      uint64_t per_block, uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
-  lds_zero(regs);
-  __syncthreads();
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  uint64_t i = begin + threadIdx.x;
-  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[i + (uint64_t)u * T]);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x;
-      uint64_t w1 = ((uint64_t)v[u].w << 32) | v[u].z;
-      hll_update(regs, murmur64a_16(w0, w1));
-    }
-  }
-  for (; i < end; i += T) {
-    uint4 v = keys[i];
-    hll_update(regs, murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z));
-  }
-  __syncthreads();
-  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-// Tuning variants of the 16-byte kernel (rsk_diag_hll_variant): keys in
-// flight per lane U, workgroup size T, nontemporal loads NT.
-template <int U, int T, bool NT>
-__global__ __launch_bounds__(T) void hll_add16_variant(const uint4* __restrict__ keys, uint64_t n, uint64_t per_block,
-                                                       uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
-  lds_zero(regs);
-  __syncthreads();
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  uint64_t i = begin + threadIdx.x;
-  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = NT ? ld_nt16(&keys[i + (uint64_t)u * T]) : keys[i + (uint64_t)u * T];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      hll_update(regs, murmur64a_16(((uint64_t)v[u].y << 32) | v[u].x, ((uint64_t)v[u].w << 32) | v[u].z));
-  }
-  for (; i < end; i += T) {
-    uint4 v = keys[i];
-    hll_update(regs, murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z));
-  }
-  __syncthreads();
-  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-template <int U, int T, bool NT>
-static void launch_variant(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu) {
-  uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * wg_per_cu, c->slab_count);
-  const uint64_t tile = (uint64_t)T * U;
-  uint64_t per_block = (n + blocks - 1) / blocks;
-  per_block = (per_block + tile - 1) / tile * tile;
-  blocks = (n + per_block - 1) / per_block;
-  hipLaunchKernelGGL((hll_add16_variant<U, T, NT>), dim3((uint32_t)blocks), dim3(T), 0, c->stream, keys, n, per_block,
-                     c->d_slab);
-}
-
-// Software-pipelined variant: the next U keys per lane load while the
-// current U are hashed (no stores in the loop, so the in-order vmcnt lets
-// the wait cover only the older loads).
-template <int U, int T>
-__global__ __launch_bounds__(T) void hll_add16_pf(const uint4* __restrict__ keys, uint64_t n, uint64_t per_block,
-                                                  uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs[HLL_REGS];
-  lds_zero(regs);
-  __syncthreads();
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  uint64_t i = begin + threadIdx.x;
-  uint4 v[U];
-  if (i + (uint64_t)(U - 1) * T < end) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[i + (uint64_t)u * T]);
-  }
-  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
-    uint4 cur[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) cur[u] = v[u];
-    const uint64_t j = i + (uint64_t)U * T;
-    if (j + (uint64_t)(U - 1) * T < end) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[j + (uint64_t)u * T]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      hll_update(regs, murmur64a_16(((uint64_t)cur[u].y << 32) | cur[u].x, ((uint64_t)cur[u].w << 32) | cur[u].z));
-  }
-  for (; i < end; i += T) {
-    uint4 x = keys[i];
-    hll_update(regs, murmur64a_16(((uint64_t)x.y << 32) | x.x, ((uint64_t)x.w << 32) | x.z));
-  }
-  __syncthreads();
-  lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-template <int U, int T>
-static void launch_pf(rsk_ctx* c, const uint4* keys, uint64_t n) {
-  uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * 2, c->slab_count);
-  const uint64_t tile = (uint64_t)T * U;
-  uint64_t per_block = (n + blocks - 1) / blocks;
-  per_block = (per_block + tile - 1) / tile * tile;
-  blocks = (n + per_block - 1) / per_block;
-  hipLaunchKernelGGL((hll_add16_pf<U, T>), dim3((uint32_t)blocks), dim3(T), 0, c->stream, keys, n, per_block, c->d_slab);
-}
-
-template <int U, int T>
-static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu);
-
-void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n) {
-  switch (variant) {
-    case 8: launch_b8<4, 512>(c, keys, n, 4); break;
-    case 9: launch_b8<4, 256>(c, keys, n, 8); break;
-    case 10: launch_b8<8, 512>(c, keys, n, 4); break;
-    case 11: launch_b8<4, 1024>(c, keys, n, 2); break;
-    case 12: launch_pf<4, 256>(c, keys, n); break;
-    case 13: launch_pf<2, 256>(c, keys, n); break;
-    case 14: launch_pf<8, 256>(c, keys, n); break;
-    case 0: launch_variant<4, 512, true>(c, keys, n, 2); break;
-    case 1: launch_variant<8, 512, true>(c, keys, n, 2); break;
-    case 2: launch_variant<2, 512, true>(c, keys, n, 2); break;
-    case 3: launch_variant<4, 512, false>(c, keys, n, 2); break;
-    case 4: launch_variant<4, 1024, true>(c, keys, n, 2); break;
-    case 5: launch_variant<4, 256, true>(c, keys, n, 2); break;
-    case 6: launch_variant<8, 1024, true>(c, keys, n, 2); break;
-    case 7: launch_variant<2, 1024, true>(c, keys, n, 2); break;
-    default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
-  }
-  RSK_CHECK_LAUNCH("hll_variant");
-}
 
 // Any fixed stride or blob+offsets: lane-per-key MurmurHash64A.
 template <bool VAR>
@@ -224,378 +49,6 @@ __global__ __launch_bounds__(RSK_ADD_THREADS, 2) void hll_add_bytes_kernel(const
   }
   __syncthreads();
   lds_to_slab(regs, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-// ---- byte-register LDS file (16 KiB): check-then-CAS update.  After the
-// first few keys per register almost every key only reads its register
-// (a rank above the current value is rare), so the RMW is rarely taken and
-// the 4x smaller file leaves LDS for staging and for more workgroups.
-RSK_DEV void hll_update8(uint32_t* regs32, uint64_t h) {
-  const uint32_t idx = hll_index(h), rank = hll_rank(h);
-  uint32_t* w = regs32 + (idx >> 2);
-  const uint32_t sh = (idx & 3u) * 8;
-  uint32_t cur = *w;
-  while (((cur >> sh) & 0xFFu) < rank) {
-    const uint32_t nw = (cur & ~(0xFFu << sh)) | (rank << sh);
-    const uint32_t prev = atomicCAS(w, cur, nw);
-    if (prev == cur) break;
-    cur = prev;
-  }
-}
-
-__device__ __forceinline__ void lds8_zero(uint32_t* regs32) {
-  uint4* r4 = reinterpret_cast<uint4*>(regs32);
-  for (int j = threadIdx.x; j < HLL_REGS / 16; j += blockDim.x) r4[j] = make_uint4(0, 0, 0, 0);
-}
-__device__ __forceinline__ void lds8_to_slab(const uint32_t* regs32, uint8_t* slab) {
-  const uint4* r4 = reinterpret_cast<const uint4*>(regs32);
-  uint4* out = reinterpret_cast<uint4*>(slab);
-  for (int j = threadIdx.x; j < HLL_REGS / 16; j += blockDim.x) out[j] = r4[j];
-}
-
-// 16-byte keys with the byte-register file (tuning variant).
-template <int U, int T>
-__global__ __launch_bounds__(T) void hll_add16_b8_kernel(const uint4* __restrict__ keys, uint64_t n,
-                                                         uint64_t per_block, uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
-  lds8_zero(regs32);
-  __syncthreads();
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  uint64_t i = begin + threadIdx.x;
-  for (; i + (uint64_t)(U - 1) * T < end; i += (uint64_t)U * T) {
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld_nt16(&keys[i + (uint64_t)u * T]);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      hll_update8(regs32, murmur64a_16(((uint64_t)v[u].y << 32) | v[u].x, ((uint64_t)v[u].w << 32) | v[u].z));
-  }
-  for (; i < end; i += T) {
-    uint4 v = keys[i];
-    hll_update8(regs32, murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z));
-  }
-  __syncthreads();
-  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-template <int U, int T>
-static void launch_b8(rsk_ctx* c, const uint4* keys, uint64_t n, uint32_t wg_per_cu) {
-  uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * wg_per_cu, c->slab_count);
-  const uint64_t tile = (uint64_t)T * U;
-  uint64_t per_block = (n + blocks - 1) / blocks;
-  per_block = (per_block + tile - 1) / tile * tile;
-  blocks = (n + per_block - 1) / per_block;
-  hipLaunchKernelGGL((hll_add16_b8_kernel<U, T>), dim3((uint32_t)blocks), dim3(T), 0, c->stream, keys, n, per_block,
-                     c->d_slab);
-}
-
-// Blob + offsets, LDS-staged (the C4 path).  A workgroup takes tiles of 512
-// consecutive keys; their bytes are one contiguous blob range, copied into
-// LDS with coalesced 16-byte loads that are issued one tile ahead (register
-// prefetch; the tile's end offset is itself loaded a tile earlier, so the
-// stage loads never wait on an offset load).  MurmurHash64A is a serial
-// chain of ceil(len/8) multiply-bound steps and a wave runs as long as its
-// longest key, so the tile's keys are counting-sorted by step count in LDS
-// (one LDS atomic per key gives its rank in its class) and each lane then
-// hashes KPL adjacent keys of that order, so the lanes of a wave see nearly
-// equal lengths.  KPL = 1 in production (measured: KPL 2 and 4 interleave
-// independent chains but lose more to registers and selects than they win,
-// scripts/var_variants.py).  A tile whose bytes exceed the stage is hashed
-// from global memory, unsorted.  The tile's barriers order LDS only
-// (lds_barrier): __syncthreads' fence would wait for the next tile's stage
-// loads at the first barrier after they are issued, undoing the prefetch.
-constexpr int VAR_TILE = 512;                   // keys per tile
-constexpr int VAR_STAGE = 32768;                // bytes per tile (64 B per key)
-constexpr uint32_t VAR_MAXCLS = 16;             // step classes 0..16 (16 = that long or longer)
-constexpr uint32_t VAR_NONE = VAR_MAXCLS + 1;   // slot past the end of the tile
-constexpr int VAR_NCLS_PAD = 20;                // classes 0..17, padded
-
-// One unaligned 8-byte LDS read (gfx950 LDS takes byte-aligned ds_read_b64;
-// hipcc emits it for the memcpy).
-RSK_DEV uint64_t lds_u64(const uint8_t* p) {
-  uint64_t v;
-  __builtin_memcpy(&v, p, 8);
-  return v;
-}
-
-// MurmurHash64A of KPL keys of the stage (bytes [off, off+len)), as KPL
-// interleaved chains over max(len/8) steps; a chain past its own blocks
-// keeps its value (its clamped read stays inside its key + 7 bytes).  The
-// tail read may run up to 7 bytes past a key, inside the stage's slack;
-// those bytes are masked off.
-// The loop runs ceil(len/8) - 1 full blocks and the last step is a select
-// (the tail masked, or the last full block mixed): every key of one step
-// class takes the same trip count, so a class-sorted wave does not pay the
-// full loop + odd remainder + tail of its mixed nb = len >> 3 (measured form
-// before: 5.8 step-times per wave on the C4 lengths 8..64 instead of 4.9).
-RSK_DEV uint64_t murmur64a_lds(const uint8_t* p, uint32_t len) {
-  const uint32_t steps = (len + 7) >> 3, t = len & 7;
-  uint64_t h = (uint64_t)HLL_SEED ^ ((uint64_t)len * MM_M);
-  if (steps) {
-    for (uint32_t j = 0; j + 1 < steps; ++j) {
-      h ^= mm_mix(lds_u64(p + 8 * j));
-      h *= MM_M;
-    }
-    const uint64_t v = lds_u64(p + 8 * (steps - 1));
-    const uint64_t x = t ? (v & ((1ULL << (8 * t)) - 1)) : mm_mix(v);
-    h = (h ^ x) * MM_M;
-  }
-  return mm_final(h);
-}
-template <int KPL>
-RSK_DEV void murmur64a_lds_multi(const uint8_t* st, const uint32_t (&off)[KPL], const uint32_t (&len)[KPL],
-                                 uint64_t (&h)[KPL]) {
-  if constexpr (KPL == 1) {
-    h[0] = murmur64a_lds(st + off[0], len[0]);
-    return;
-  }
-  uint32_t nb[KPL], nmax = 0;
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) {
-    nb[q] = len[q] >> 3;
-    nmax = nb[q] > nmax ? nb[q] : nmax;
-    h[q] = (uint64_t)HLL_SEED ^ ((uint64_t)len[q] * MM_M);
-  }
-  for (uint32_t j = 0; j < nmax; ++j) {
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const uint32_t jj = j < nb[q] ? j : nb[q];
-      const uint64_t hn = (h[q] ^ mm_mix(lds_u64(st + off[q] + 8 * jj))) * MM_M;
-      h[q] = j < nb[q] ? hn : h[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < KPL; ++q) {
-    const uint32_t t = len[q] & 7;
-    if (t) h[q] = (h[q] ^ (lds_u64(st + off[q] + 8 * nb[q]) & ((1ULL << (8 * t)) - 1))) * MM_M;
-    h[q] = mm_final(h[q]);
-  }
-}
-
-// Bytes [off, off+len) of the stage, or of global memory for an unstaged tile.
-RSK_DEV uint64_t var_hash(bool staged, const uint64_t* st, uint32_t off, const uint8_t* g, uint64_t len) {
-  if (staged) return murmur64a_lds(reinterpret_cast<const uint8_t*>(st) + off, (uint32_t)len);
-  return len <= 64 ? murmur64a_le64(g, (uint32_t)len) : murmur64a(g, len);
-}
-
-// KPL keys per lane, 512 / KPL lanes; 3 workgroups per CU (LDS ~50 KiB each).
-// DIAG (rsk_diag_hll_var_variant only): bit 0 replaces MurmurHash64A by one
-// 8-byte read of the key, bit 1 skips the register update (XOR-folded into a
-// slab byte instead): the cost of the rest of the kernel without them.
-template <int KPL, int DIAG = 0>
-__global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_add_var_staged_kernel(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint64_t n, uint64_t per_block,
-    uint8_t* __restrict__ slabs) {
-  constexpr int T = VAR_TILE / KPL;
-  constexpr int PF = VAR_STAGE / 16 / T;  // 16-byte stage chunks per lane
-  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
-  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
-  __shared__ uint32_t perm[VAR_TILE];  // sorted keys: stage offset | len << 16
-  __shared__ uint32_t cnt[VAR_NCLS_PAD], cbase[VAR_NCLS_PAD];
-  const uint32_t tid = threadIdx.x;
-  lds8_zero(regs32);
-  if (tid < VAR_NCLS_PAD) cnt[tid] = 0;
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  const uintptr_t dbase = reinterpret_cast<uintptr_t>(data);
-  const uint8_t* st8 = reinterpret_cast<const uint8_t*>(stage);
-  uint64_t diag_acc = 0;
-
-  // Tile state, one tile ahead.  The stage window starts at the 16-byte-
-  // aligned ADDRESS at or below the tile's first byte, so no chunk load
-  // crosses into a page the blob does not touch.  Lane key q is tile key
-  // tid + q*T (coalesced offset loads).
-  uint64_t last = 0, hi_ahead = 0, s[KPL], e[KPL];
-  uintptr_t a0 = 0;
-  uint32_t nchunk = 0;
-  bool staged = false;
-  uint4 pf[PF];
-  auto fetch = [&](uint64_t b, uint64_t lo, uint64_t hi) {
-    last = b + VAR_TILE < end ? b + VAR_TILE : end;
-    a0 = (dbase + lo) & ~uintptr_t(15);
-    const uint64_t span = dbase + hi - a0;
-    staged = span <= (uint64_t)VAR_STAGE;
-    nchunk = staged ? (uint32_t)((span + 15) >> 4) : 0;
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const uint32_t c = tid + (uint32_t)u * T;
-      // addressed from `data` (a global kernel argument), not from the integer
-      // a0: a pointer rebuilt from an integer is generic, and its flat loads
-      // count in lgkmcnt, so every LDS-only barrier of the tile would wait
-      // for this prefetch
-      if (c < nchunk) pf[u] = ld_nt16(reinterpret_cast<const uint4*>(data + (a0 - dbase)) + c);
-    }
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const uint64_t i = b + tid + (uint64_t)q * T;
-      s[q] = i < last ? offsets[i] : 0;
-      e[q] = i < last ? offsets[i + 1] : 0;
-    }
-    hi_ahead = offsets[last + VAR_TILE < end ? last + VAR_TILE : end];  // the following tile's end
-  };
-  uint64_t cur_hi = 0;
-  if (begin < end) {
-    cur_hi = offsets[begin + VAR_TILE < end ? begin + VAR_TILE : end];
-    fetch(begin, offsets[begin], cur_hi);
-  }
-
-  for (uint64_t base = begin; base < end;) {
-    lds_barrier();  // [A] previous tile's stage / perm / cbase reads are done
-    uint4* st16 = reinterpret_cast<uint4*>(stage);
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const uint32_t c = tid + (uint32_t)u * T;
-      if (c < nchunk) st16[c] = pf[u];
-    }
-    const bool cur_staged = staged;  // workgroup-uniform
-    uint32_t cls[KPL], rk[KPL], coff[KPL];
-    uint64_t clen[KPL], cs[KPL];
-#pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const bool mine = base + tid + (uint64_t)q * T < last;
-      clen[q] = e[q] - s[q];
-      cs[q] = s[q];
-      coff[q] = (uint32_t)(dbase + s[q] - a0);
-      const uint64_t steps = (clen[q] + 7) >> 3;
-      cls[q] = !mine ? VAR_NONE : (steps < VAR_MAXCLS ? (uint32_t)steps : VAR_MAXCLS);
-      rk[q] = (cur_staged && cls[q] != VAR_NONE) ? atomicAdd(&cnt[cls[q]], 1u) : 0u;  // rank inside the class
-    }
-    // Issue the next tile's loads (they land while this tile hashes).
-    const uint64_t next = last;
-    if (next < end) {
-      const uint64_t lo_n = cur_hi;
-      cur_hi = hi_ahead;
-      fetch(next, lo_n, cur_hi);
-    }
-    lds_barrier();  // [B] stage written, class counts final
-    if (cur_staged) {
-      if (tid < 64) {  // class starts: wave 0's exclusive prefix over the counts (one LDS read per lane)
-        const uint32_t v = tid < VAR_NCLS_PAD ? cnt[tid] : 0;
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          const uint32_t y = __shfl_up(x, o, 64);
-          if (tid >= (uint32_t)o) x += y;
-        }
-        if (tid < VAR_NCLS_PAD) cbase[tid] = x - v;
-      }
-      lds_barrier();  // [C]
-#pragma unroll
-      for (int q = 0; q < KPL; ++q)
-        if (cls[q] != VAR_NONE) perm[cbase[cls[q]] + rk[q]] = coff[q] | ((uint32_t)clen[q] << 16);
-      lds_barrier();  // [D]
-      if (tid < VAR_NCLS_PAD) cnt[tid] = 0;
-      const uint32_t nvalid = cbase[VAR_NONE];
-      uint32_t o[KPL], l[KPL], pos[KPL];
-#pragma unroll
-      for (int q = 0; q < KPL; ++q) {
-        // adjacent sorted keys: one class per lane, nearly.  With one key per
-        // lane, wave w takes sorted chunk w (w < 4) or 11 - w, so the two waves
-        // a SIMD holds (w, w + 4) get a short and a long chunk: the SIMDs
-        // finish a tile together instead of the one with the longest keys
-        // holding the workgroup at the next barrier.
-        if constexpr (KPL == 1 && T == 512) {
-          const uint32_t w = tid >> 6;
-          pos[q] = (w < 4 ? w : 11 - w) * 64 + (tid & 63);
-        } else {
-          pos[q] = tid * KPL + q;
-        }
-        const uint32_t p = pos[q] < nvalid ? perm[pos[q]] : 0u;
-        o[q] = p & 0xFFFFu;
-        l[q] = p >> 16;
-      }
-      uint64_t h[KPL];
-      if constexpr (DIAG & 1) {
-#pragma unroll
-        for (int q = 0; q < KPL; ++q) h[q] = lds_u64(st8 + o[q]) ^ l[q];
-      } else {
-        murmur64a_lds_multi<KPL>(st8, o, l, h);
-      }
-#pragma unroll
-      for (int q = 0; q < KPL; ++q)
-        if (pos[q] < nvalid) {
-          if constexpr (DIAG & 2) diag_acc ^= h[q];
-          else hll_update8(regs32, h[q]);
-        }
-    } else {
-#pragma unroll
-      for (int q = 0; q < KPL; ++q)
-        if (cls[q] != VAR_NONE) hll_update8(regs32, var_hash(false, stage, 0, data + cs[q], clen[q]));
-    }
-    base = next;
-  }
-  __syncthreads();
-  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-  if constexpr ((DIAG & 2) != 0) slabs[(uint64_t)blockIdx.x * HLL_REGS + tid] = (uint8_t)(diag_acc % 51);
-}
-
-// The round-1 form (no prefetch, no sort): the A/B baseline of the diag.
-constexpr int VAR_T = 512;
-__global__ __launch_bounds__(VAR_T) void hll_add_var_simple_kernel(const uint8_t* __restrict__ data,
-                                                                   const uint64_t* __restrict__ offsets, uint64_t n,
-                                                                   uint64_t per_block, uint8_t* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
-  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
-  lds8_zero(regs32);
-  const uint64_t begin = (uint64_t)blockIdx.x * per_block;
-  const uint64_t end = begin + per_block < n ? begin + per_block : n;
-  const uintptr_t dbase = reinterpret_cast<uintptr_t>(data);
-  for (uint64_t base = begin; base < end; base += VAR_T) {
-    const uint64_t last = base + VAR_T < end ? base + VAR_T : end;
-    const uint64_t i = base + threadIdx.x;
-    const bool mine = i < last;
-    const uint64_t s = mine ? offsets[i] : 0;
-    const uint64_t e = mine ? offsets[i + 1] : 0;
-    const uintptr_t a0 = (dbase + offsets[base]) & ~uintptr_t(15);
-    const uint64_t span = dbase + offsets[last] - a0;
-    const bool staged = span <= (uint64_t)VAR_STAGE;
-    __syncthreads();  // previous tile's stage reads are done
-    if (staged) {
-      const uint32_t nchunk = (uint32_t)((span + 15) >> 4);
-      const uint4* src = reinterpret_cast<const uint4*>(data + (a0 - dbase));
-      uint4* dst = reinterpret_cast<uint4*>(stage);
-      for (uint32_t c = threadIdx.x; c < nchunk; c += VAR_T) dst[c] = ld_nt16(src + c);
-    }
-    __syncthreads();
-    if (mine) hll_update8(regs32, var_hash(staged, stage, (uint32_t)(dbase + s - a0), data + s, e - s));
-  }
-  __syncthreads();
-  lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
-}
-
-static void var_grid(rsk_ctx* c, uint64_t n, uint64_t* blocks, uint64_t* per_block) {
-  // LDS-staged tiles: ~50 KiB of LDS per workgroup -> 3 workgroups per CU.
-  uint64_t b = std::min<uint64_t>((n + VAR_TILE - 1) / VAR_TILE, std::min<uint64_t>(3ull * c->num_cus, c->slab_count));
-  if (b == 0) b = 1;
-  uint64_t pb = (n + b - 1) / b;
-  pb = (pb + VAR_TILE - 1) / VAR_TILE * VAR_TILE;
-  *per_block = pb;
-  *blocks = (n + pb - 1) / pb;
-}
-
-void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const uint64_t* offsets, uint64_t n) {
-  uint64_t blocks, per_block;
-  var_grid(c, n, &blocks, &per_block);
-  const dim3 g((uint32_t)blocks);
-  switch (variant) {
-    case 0: hipLaunchKernelGGL(hll_add_var_staged_kernel<1>, g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
-                               per_block, c->d_slab); break;
-    case 1: hipLaunchKernelGGL(hll_add_var_staged_kernel<2>, g, dim3(VAR_TILE / 2), 0, c->stream, data, offsets, n,
-                               per_block, c->d_slab); break;
-    case 2: hipLaunchKernelGGL(hll_add_var_simple_kernel, g, dim3(VAR_T), 0, c->stream, data, offsets, n, per_block,
-                               c->d_slab); break;
-    case 3: hipLaunchKernelGGL(hll_add_var_staged_kernel<4>, g, dim3(VAR_TILE / 4), 0, c->stream, data, offsets, n,
-                               per_block, c->d_slab); break;
-    case 4: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 1>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
-                               per_block, c->d_slab); break;
-    case 5: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 2>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
-                               per_block, c->d_slab); break;
-    case 6: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 3>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
-                               per_block, c->d_slab); break;
-    default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
-  }
-  RSK_CHECK_LAUNCH("hll_var_variant");
 }
 
 // Max-merge `nslabs` slabs and the sketch's registers; 64 registers per

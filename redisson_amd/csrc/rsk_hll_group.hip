@@ -3,18 +3,11 @@
 // LDS and written once; PFCOUNT estimated on the way out.
 #include <hipcub/hipcub.hpp>
 
-#include <cstdlib>
-
 #include "rsk_hllcount.h"
 #include "rsk_internal.h"
 #include "rsk_part.h"
 
 namespace rsk {
-
-static uint32_t env_u32(const char* name, uint32_t dflt) {  // tuning knobs (scripts/c5_part_tune.py)
-  const char* e = std::getenv(name);
-  return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
-}
 
 // ===================================================== grouped PFADD (C5)
 // RHyperLogLog.add on many sketches (rsk_hll_add_grouped, C5): pair i adds
@@ -328,19 +321,13 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_extra_kernel(const uint32_t* 
   }
 }
 
-static int gpart_mode() {
-  const char* e = std::getenv("RSK_HLL_GPART");  // unset: auto; "0": never; "1": always
-  if (!e || !*e) return -1;
-  return e[0] == '0' ? 0 : 1;
-}
-
-bool hll_grouped_partition_applies(const DevKeys& keys, uint64_t G) {
-  const int mode = gpart_mode();
+bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& keys, uint64_t G) {
+  const int mode = c->tune.gpart;  // 0 auto, 1 always, -1 never
   const bool f16 =
       keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
-  if (mode == 0 || !f16 || keys.n == 0 || G == 0 || G > (1ull << (GP_BIN_SHIFT + 8))) return false;
+  if (mode < 0 || !f16 || keys.n == 0 || G == 0 || G > (1ull << (GP_BIN_SHIFT + 8))) return false;
   // auto: large batches dense enough that reading + writing each touched sketch once pays
-  if (mode < 0 && (keys.n < (1ull << 22) || keys.n < 16 * G)) return false;
+  if (mode == 0 && (keys.n < (1ull << 22) || keys.n < 16 * G)) return false;
   return true;
 }
 
@@ -348,14 +335,14 @@ bool hll_grouped_partition_applies(const DevKeys& keys, uint64_t G) {
 // row of the pool, zero rows for sketches without records.
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
                                  uint64_t G, bool pool_zero, bool write_all, PCount pc) {
-  if (!hll_grouped_partition_applies(keys, G)) return false;
+  if (!hll_grouped_partition_applies(c, keys, G)) return false;
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
   const uint32_t cus = (uint32_t)c->num_cus;
-  const uint32_t GU = std::max<uint32_t>(1, env_u32("RSK_HLL_GPART_GU", GP_GU));  // part1 blocks per part2 unit
-  const uint32_t gpc = std::max<uint32_t>(1, env_u32("RSK_HLL_GPART_G", 2));     // gcount / gpart1 blocks per CU
-  const uint32_t G1 = GU * ((gpc * cus + GU - 1) / GU);                          // a multiple of GU
-  const uint32_t p2_grid = std::max<uint32_t>(1, env_u32("RSK_HLL_GPART_P2", 4)) * cus;
+  constexpr uint32_t GU = GP_GU;   // part1 blocks per part2 unit
+  constexpr uint32_t gpc = 2;      // gcount / gpart1 blocks per CU
+  const uint32_t G1 = GU * ((gpc * cus + GU - 1) / GU);  // a multiple of GU
+  const uint32_t p2_grid = 4 * cus;
   const uint64_t chunk = PROBE_CAP;
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
   const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)nfine * G1 + 1;

@@ -6,11 +6,11 @@
 
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
 #include "../../include/rsketch.h"
-#include "../../include/rsketch_diag.h"
 #include "rsk_device.h"
 
 namespace rsk {
@@ -36,6 +36,46 @@ struct RskError {
     if (_e != hipSuccess)                                                                   \
       throw ::rsk::RskError{RSK_ERR_DEVICE, std::string("launch ") + (name) + ": " + hipGetErrorString(_e)}; \
   } while (0)
+
+// Route overrides of one context.  The library reads no environment
+// variables: a context starts with every route automatic (the zero defaults
+// below) and only the test and bench support library changes them
+// (librsketch_diag.so: rsk_diag_set_route), so behaviour never depends on the
+// process that embeds the library.  Every route is bit-exact; they differ in
+// speed and scratch only (DESIGN.md 3 lists which batches take which).
+struct Tuning {
+  int bloom_stream = 0;      // slice-routed insert (st1/apply, sa1/sa2/apply): 0 auto (>= 2^22 probes), 1 any size, -1 never
+  int bloom_part = 0;        // exact-offset insert (rsk_bloom_part.hip): 0 auto, 1 any size, -1 never
+  uint64_t bloom_chunk = 0;  // probes per chunk of the slice-routed insert (0: 2^33)
+  int sa_tiny = 0;           // sub-regions of 32 probes: forces the overflow fallbacks
+  uint32_t sa_parts = 0;     // sa2 / rp2 parts per coarse bin (0: 4 x CUs / bins)
+  int reply = 0;             // add() replies: 0 auto, 1 first-key pipeline at any size, -1 the sort path
+  uint64_t reply_chunk = 0;  // probes per chunk of the first-key pipeline (0: 2^33)
+  int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
+};
+
+// An asynchronous call (rsk_*_async): its host inputs are copied into the
+// op's own pinned buffer (so the caller may reuse them at once), its result
+// is read back into pinned memory on the context stream, and a host function
+// enqueued behind it (hipLaunchHostFunc) computes the reply and invokes the
+// caller's callback.  Ops and their buffers are recycled.
+struct AsyncOp {
+  rsk_ctx* c = nullptr;
+  rsk_done_fn cb = nullptr;
+  void* user = nullptr;
+  int kind = 0;             // how op_complete derives the callback's value
+  uint32_t epoch = 0;       // hll add: the call's epoch (reply = flag == epoch || created)
+  bool created = false;
+  uint64_t value = 0;       // preset value (kinds without a device result)
+  uint8_t* h_buf = nullptr; // pinned: staged keys / pointer arrays, then per-key outputs
+  uint64_t h_bytes = 0;
+  uint8_t* d_buf = nullptr; // device twin
+  uint64_t d_bytes = 0;
+  uint64_t* h_res = nullptr;  // 64 B pinned result words
+  uint8_t* h_out = nullptr;   // per-key outputs read back (inside h_buf)
+  uint8_t* user_out = nullptr;
+  uint64_t n_out = 0;
+};
 
 struct ProfEntry {
   double ms = 0;
@@ -69,6 +109,7 @@ struct rsk_ctx {
   // host -> device staging for RSK_MEM_HOST key batches
   uint8_t* d_stage = nullptr;
   uint64_t stage_bytes = 0;
+  unsigned stage_threads = 8;
   // double-buffered pinned host stages (filled by host threads while the
   // previous chunk's DMA runs), their device twins and "DMA done" events;
   // pin_off: pinned allocation failed, copy from the pageable source
@@ -83,18 +124,17 @@ struct rsk_ctx {
   uint8_t* d_small = nullptr;
   uint8_t* h_small = nullptr;
   uint64_t small_bytes = 0;
-  // grow-on-demand device scratch for batched calls
+  // grow-on-demand device scratch for batched calls (released by rsk_trim)
   uint8_t* d_work = nullptr;
   uint64_t work_bytes = 0;
+  // grow-on-demand device output scratch, distinct from d_work
+  uint8_t* d_out = nullptr;
+  uint64_t out_bytes = 0;
   // grow-on-demand pinned host scratch: per-op arrays of batched calls
   // (countWith / mergeWith sketch pointers) built in place and copied with
-  // one asynchronous DMA; a call that returns before its DMA has run (the
-  // reply-less rsk_hll_merge_batch) records batch_ev, and pinned() waits for
-  // it before the buffer is written again
+  // one asynchronous DMA (the call waits for it before returning)
   uint8_t* h_batch = nullptr;
   uint64_t h_batch_bytes = 0;
-  hipEvent_t batch_ev = nullptr;
-  bool batch_pending = false;
   // m*log(m/ez) for ez = 0..16384, computed with the host libm (Redis's log)
   double* d_lc = nullptr;
   rsk::Profiler prof;
@@ -104,6 +144,12 @@ struct rsk_ctx {
   int rank = 0;
   // call number written by kernels that report "something changed" (no reset)
   uint32_t epoch = 0;
+  rsk::Tuning tune;
+  // asynchronous calls: op pool (the completion runs on the runtime's
+  // callback thread and returns its op under async_mu)
+  std::mutex async_mu;
+  std::vector<rsk::AsyncOp*> async_free;
+  std::vector<rsk::AsyncOp*> async_all;
 
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);
@@ -146,6 +192,11 @@ struct rsk_hll {
   };
   std::vector<Level> lv;
   uint32_t lv_epoch = 0;
+  // SET of a Redis string (rsk_hll_import_redis) keeps the string itself: GET
+  // returns those bytes (card bytes as PFCOUNT last left them) until the key is
+  // next written, as Redis does -- a canonical re-encoding could chunk the
+  // runs of a non-canonical sparse string differently.
+  mutable std::unordered_map<uint64_t, std::vector<uint8_t>> imported;
 };
 
 struct rsk_bloom {
@@ -187,6 +238,11 @@ void hll_add_launch(rsk_ctx* c, const DevKeys& k, uint8_t* d_regs_sketch, uint64
                     uint32_t epoch, bool created);
 // Registers of h may change: drop "known zero" and every precomputed PFCOUNT.
 void hll_touch(const rsk_hll* h);
+// Key id (all keys) written: an imported Redis string is no longer its GET.
+inline void hll_forget_import(const rsk_hll* h, uint64_t id) {
+  if (!h->imported.empty()) h->imported.erase(id);
+}
+inline void hll_forget_imports(const rsk_hll* h) { h->imported.clear(); }
 struct PCount {  // where hll_gapply leaves its estimates (none: pcount == nullptr)
   uint64_t* pcount;
   uint32_t* pepoch;
@@ -207,9 +263,6 @@ void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* con
                       uint64_t n);
 void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out);
 void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag);
-void hll_variant_launch(rsk_ctx* c, int variant, const uint4* keys, uint64_t n);
-// Blob+offsets PFADD variants (rsk_diag_hll_var_variant), slabs only.
-void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const uint64_t* offsets, uint64_t n);
 
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
@@ -222,7 +275,7 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
 // batch is not worth it (or not 16-byte keys): use the direct kernel.
-bool hll_grouped_partition_applies(const DevKeys& k, uint64_t G);
+bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& k, uint64_t G);
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
                                  bool pool_zero, bool write_all, PCount pc);
 // Performs a pending lazy clear (rsk_api.hip).
@@ -235,9 +288,6 @@ void bloom_add_replies_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_
 void bloom_add_replies_sorted(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 void bloom_contains_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
-void bloom_contains_variant_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out, int variant);
-void bloom_contains_probe_count_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out,
-                                       unsigned long long* d_probes);
 void bloom_bitcount_launch(rsk_ctx* c, const uint32_t* d_bits, uint64_t nwords, uint64_t* d_out);
 // misc/Hash.hashToBase64 of every key: 22 chars per key into d_out.
 void hash_b64_launch(rsk_ctx* c, const DevKeys& k, char* d_out);
@@ -253,17 +303,5 @@ uint64_t plan_owner(uint64_t n, uint64_t N, uint64_t id);
 uint64_t plan_bloom_slice_words(uint64_t nwords, uint64_t N);
 bool plan_fetch(uint64_t n, uint64_t N, uint64_t r, const uint64_t* ids, uint64_t n_ids, uint32_t flags,
                 std::vector<uint64_t>* want, std::vector<uint64_t>* counts);
-
-// ---- generators (rsk_gen.hip)
-void gen_keys16_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, void* out);
-void gen_grouped_launch(rsk_ctx* c, uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t* g, void* keys);
-std::vector<uint64_t> zipf_cdf(uint32_t G, double s);
-void gen_grouped_zipf_launch(rsk_ctx* c, uint64_t seed, const uint64_t* d_cdf, uint32_t G, uint64_t start, uint64_t n,
-                             uint32_t* g, void* keys);
-void gen_queries16_launch(rsk_ctx* c, uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n,
-                          void* out);
-void gen_varlen_lengths_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, uint64_t* offsets);
-void gen_varlen_bytes_launch(rsk_ctx* c, uint64_t seed, uint64_t start, uint64_t n, const uint64_t* offsets,
-                             uint8_t* blob);
 
 }  // namespace rsk

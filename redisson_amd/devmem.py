@@ -63,35 +63,35 @@ class DeviceBuffer:
 
 def gen_keys16(engine, seed: int, start: int, n: int) -> DeviceBuffer:
     b = DeviceBuffer(engine, 16 * n)
-    _lib.check(_lib.load().rsk_gen_keys16(engine.ctx, seed, start, n, b.ptr))
+    _lib.check_diag(_lib.diag().rsk_gen_keys16(engine.ctx, seed, start, n, b.ptr))
     return b
 
 
 def gen_queries16(engine, qseed: int, iseed: int, n_ins: int, start: int, n: int) -> DeviceBuffer:
     b = DeviceBuffer(engine, 16 * n)
-    _lib.check(_lib.load().rsk_gen_queries16(engine.ctx, qseed, iseed, n_ins, start, n, b.ptr))
+    _lib.check_diag(_lib.diag().rsk_gen_queries16(engine.ctx, qseed, iseed, n_ins, start, n, b.ptr))
     return b
 
 
 def gen_grouped(engine, seed: int, G: int, start: int, n: int):
     g = DeviceBuffer(engine, 4 * n)
     k = DeviceBuffer(engine, 16 * n)
-    _lib.check(_lib.load().rsk_gen_grouped(engine.ctx, seed, G, start, n, g.ptr, k.ptr))
+    _lib.check_diag(_lib.diag().rsk_gen_grouped(engine.ctx, seed, G, start, n, g.ptr, k.ptr))
     return g, k
 
 
 def gen_grouped_zipf(engine, seed: int, G: int, s: float, start: int, n: int):
     g = DeviceBuffer(engine, 4 * n)
     k = DeviceBuffer(engine, 16 * n)
-    _lib.check(_lib.load().rsk_gen_grouped_zipf(engine.ctx, seed, G, s, start, n, g.ptr, k.ptr))
+    _lib.check_diag(_lib.diag().rsk_gen_grouped_zipf(engine.ctx, seed, G, s, start, n, g.ptr, k.ptr))
     return g, k
 
 
 def gen_varlen(engine, seed: int, start: int, n: int):
     offs = DeviceBuffer(engine, 8 * (n + 1))
     tot = ctypes.c_uint64()
-    L = _lib.load()
-    _lib.check(L.rsk_gen_varlen(engine.ctx, seed, start, n, offs.ptr, None, 0, ctypes.byref(tot)))
+    D = _lib.diag()
+    _lib.check_diag(D.rsk_gen_varlen(engine.ctx, seed, start, n, offs.ptr, None, 0, ctypes.byref(tot)))
     blob = DeviceBuffer(engine, max(1, tot.value))
-    _lib.check(L.rsk_gen_varlen(engine.ctx, seed, start, n, offs.ptr, blob.ptr, blob.nbytes, ctypes.byref(tot)))
+    _lib.check_diag(D.rsk_gen_varlen(engine.ctx, seed, start, n, offs.ptr, blob.ptr, blob.nbytes, ctypes.byref(tot)))
     return blob, offs, tot.value

@@ -22,6 +22,7 @@ def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else "bloom_variants.json"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000_000
     L = _lib.load()
+    D = _lib.diag()
     eng = _lib.Engine(0)
     size = ctypes.c_int64()
     k = ctypes.c_int32()
@@ -38,7 +39,7 @@ def main():
     for _ in range(4):
         for v in NAMES:
             ms = ctypes.c_double()
-            _lib.check(L.rsk_diag_bloom_contains_variant(eng.ctx, v, b, qs.ptr, n, outs[v].ptr, ctypes.byref(ms)))
+            _lib.check_diag(D.rsk_diag_bloom_contains_variant(eng.ctx, v, b, qs.ptr, n, outs[v].ptr, ctypes.byref(ms)))
             t[v].append(ms.value)
     ref = outs[0].to_numpy()
     res = {"n": n, "size": size.value, "k": k.value, "variants": {}}

@@ -19,12 +19,13 @@ from redisson_amd import _lib, devmem  # noqa: E402
 def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else "membench.json"
     L = _lib.load()
+    D = _lib.diag()
     eng = _lib.Engine(0)
     res = {"membench": {}, "hll_variants": {}}
 
     def mb(mode, buf, nbytes, nops):
         ms = ctypes.c_double()
-        _lib.check(L.rsk_diag_membench(eng.ctx, mode, buf.ptr, nbytes, nops, ctypes.byref(ms)))
+        _lib.check_diag(D.rsk_diag_membench(eng.ctx, mode, buf.ptr, nbytes, nops, ctypes.byref(ms)))
         return ms.value
 
     rounds = 5
@@ -64,7 +65,7 @@ def main():
     for _ in range(rounds):
         for v in names:
             ms = ctypes.c_double()
-            _lib.check(L.rsk_diag_hll_variant(eng.ctx, v, keys.ptr, n, ctypes.byref(ms)))
+            _lib.check_diag(D.rsk_diag_hll_variant(eng.ctx, v, keys.ptr, n, ctypes.byref(ms)))
             vs[v].append(ms.value)
     for v, nm in names.items():
         med = statistics.median(vs[v])

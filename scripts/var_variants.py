@@ -21,13 +21,14 @@ def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else "var_variants.json"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000_000
     L = _lib.load()
+    D = _lib.diag()
     eng = _lib.Engine(0)
     blob, offs, tot = devmem.gen_varlen(eng, 0x5EED0005, 0, n)
     t = {v: [] for v in NAMES}
     for _ in range(5):
         for v in NAMES:
             ms = ctypes.c_double()
-            _lib.check(L.rsk_diag_hll_var_variant(eng.ctx, v, blob.ptr, offs.ptr, n, ctypes.byref(ms)))
+            _lib.check_diag(D.rsk_diag_hll_var_variant(eng.ctx, v, blob.ptr, offs.ptr, n, ctypes.byref(ms)))
             t[v].append(ms.value)
     res = {"n": n, "bytes": tot + 8 * n, "variants": {}}
     for v, nm in NAMES.items():

@@ -37,6 +37,24 @@ def engine():
 
 
 @pytest.fixture()
+def route(engine):
+    """Route overrides of the shared engine (rsk_diag_set_route, from the
+    support library): route(bloom_stream=1, sa_parts=13) or route("reply=1,sa_tiny=1");
+    every route is automatic again after the test."""
+
+    def set_(spec=None, **kw):
+        if spec:
+            for kv in filter(None, spec.split(",")):
+                k, v = kv.split("=")
+                kw[k] = int(v)
+        for k, v in kw.items():
+            engine.set_route(k, v)
+
+    yield set_
+    engine.set_route("reset", 0)
+
+
+@pytest.fixture()
 def client():
     from redisson_amd import Redisson
 

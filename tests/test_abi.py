@@ -1,4 +1,6 @@
-"""The C ABI library loads and exports every symbol include/*.h declares;
+"""The C ABI libraries load and export every symbol their headers declare:
+librsketch.so exactly include/rsketch.h (hidden visibility: no test or tuning
+entry point, no internal symbol), librsketch_diag.so include/rsketch_diag.h;
 host-only entry points agree with the oracle (CPU only, no kernel launches)."""
 import ctypes
 import os
@@ -9,8 +11,9 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "rsketch.h")
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("rsketch.h", "rsketch_diag.h")]
+DIAG_HEADER = os.path.join(ROOT, "include", "rsketch_diag.h")
 LIB = os.path.join(ROOT, "redisson_amd", "librsketch.so")
+DIAG_LIB = os.path.join(ROOT, "redisson_amd", "librsketch_diag.so")
 
 
 @pytest.fixture(scope="module")
@@ -22,10 +25,14 @@ def lib():
     return _lib.load()
 
 
-def declared_functions():
-    text = "".join(open(h).read() for h in HEADERS)
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+def declared_functions(header=HEADER):
+    text = re.sub(r"/\*.*?\*/", "", open(header).read(), flags=re.S)
     return sorted(set(re.findall(r"\b(rsk_[a-z0-9_]+)\s*\(", text)))
+
+
+def exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
 
 
 def test_header_declares_api():
@@ -40,12 +47,40 @@ def test_every_declared_symbol_is_exported(lib):
     raw = ctypes.CDLL(LIB)
     missing = [n for n in declared_functions() if not hasattr(raw, n)]
     assert not missing, missing
+    from redisson_amd import _lib
+
+    d = _lib.diag()
+    missing = [n for n in declared_functions(DIAG_HEADER) if not hasattr(d, n)]
+    assert not missing, missing
+
+
+def test_product_library_exports_only_its_abi(lib):
+    """Frozen product library: the C symbols it exports are exactly those of
+    rsketch.h -- no rsk_diag_* / rsk_gen_*, no internal C++ helper (kernel
+    entry symbols, which the HIP runtime registers by name, aside)."""
+    syms = exported(LIB)
+    c_syms = {s for s in syms if s.startswith("rsk_")}
+    assert c_syms == set(declared_functions())
+    assert not [s for s in syms if "diag" in s or s.startswith("rsk_gen")]
+    internal = [s for s in syms if s.startswith("_ZN3rsk") and "_kernel" not in s]
+    assert not internal, internal[:10]
+    assert {s for s in exported(DIAG_LIB) if s.startswith("rsk_")} == set(declared_functions(DIAG_HEADER))
+
+
+def test_no_environment_knobs_in_the_library():
+    """The product library reads no environment variable (routes are set per
+    context, and only through the support library)."""
+    for root, _, files in os.walk(os.path.join(ROOT, "redisson_amd", "csrc")):
+        for f in files:
+            text = open(os.path.join(root, f)).read()
+            assert "getenv" not in text, f
 
 
 def test_python_binding_covers_header(lib):
     from redisson_amd import _lib
 
     assert set(declared_functions()) == set(_lib.SIGNATURES)
+    assert set(declared_functions(DIAG_HEADER)) == set(_lib.DIAG_SIGNATURES)
 
 
 def test_abi_version(lib):

@@ -1,0 +1,261 @@
+"""The asynchronous C ABI (rsk_*_async, include/rsketch.h) -- the C side of
+RHyperLogLogAsync / RBloomFilter futures (RHyperLogLogAsync.java:22-33;
+CommandAsyncService.java:86-105): every accepted call fires its callback once
+with the reply the synchronous call gives, calls on different handles may be
+issued from several threads at once, host inputs may be reused as soon as the
+call returns.  Also: rsk_trim, the now-synchronous rsk_hll_merge_batch, and the
+Redis GET of an imported (SET) string returned byte-identical until the key is
+next written."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class Waiter:
+    """Collects (status, value) of callbacks; keeps the ctypes thunk alive."""
+
+    def __init__(self, lib):
+        self.results = {}
+        self.cond = threading.Condition()
+        self.threads = set()
+
+        def fire(user, status, value):
+            user = user or 0  # ctypes hands a NULL void * over as None
+            with self.cond:
+                self.results[user] = (status, value)
+                self.threads.add(threading.get_ident())
+                self.cond.notify_all()
+
+        self.fn = lib.DONE_FN(fire)
+
+    def wait(self, keys, timeout=60):
+        with self.cond:
+            ok = self.cond.wait_for(lambda: all(k in self.results for k in keys), timeout)
+        assert ok, "callbacks did not fire: %s" % [k for k in keys if k not in self.results]
+        return [self.results[k] for k in keys]
+
+
+@pytest.fixture(scope="module")
+def L():
+    from redisson_amd import _lib
+
+    return _lib.load()
+
+
+def _pool(L, engine, n=1):
+    from redisson_amd import _lib
+
+    h = ctypes.c_void_p()
+    _lib.check(L.rsk_hll_create(engine.ctx, n, ctypes.byref(h)))
+    return h
+
+
+def test_hll_async_matches_sync(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib, devmem
+
+    w = Waiter(_lib)
+    h = _pool(L, engine, 4)
+    keys = orc.gen_keys16(0x5EED0002, 0, 300_000)
+    ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+    _lib.check(L.rsk_hll_add_async(h, 0, ctypes.byref(ks), w.fn, 1))
+    keys[:] = 0  # host input reusable at once: the call staged its own copy
+    _lib.check(L.rsk_hll_add_async(h, 0, ctypes.byref(ks), w.fn, 2))  # all-zero keys: one more register at most
+    (s1, v1), (s2, v2) = w.wait([1, 2])
+    assert s1 == s2 == 0 and v1 == 1
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, orc.gen_keys16(0x5EED0002, 0, 300_000), None, 16, 300_000)
+    orc.hll_add(ref, keys, None, 16, 300_000)
+    out = np.zeros(16384, np.uint8)
+    _lib.check(L.rsk_hll_get_registers(h, 0, out.ctypes.data, _lib.RSK_MEM_HOST))
+    assert np.array_equal(out, ref)
+    # a repeat changes nothing: reply 0 (device-resident keys)
+    dk = devmem.gen_keys16(engine, 0x5EED0002, 0, 300_000)
+    kd = dk.keys_fixed(300_000, 16).as_struct()
+    _lib.check(L.rsk_hll_add_async(h, 0, ctypes.byref(kd), w.fn, 3))
+    assert w.wait([3]) == [(0, 0)]
+    # PFCOUNT, countWith, mergeWith, batched mergeWith
+    _lib.check(L.rsk_hll_add_async(h, 1, ctypes.byref(kd), w.fn, 4))
+    _lib.check(L.rsk_hll_count_async(h, 0, w.fn, 5))
+    hs = (ctypes.c_void_p * 2)(h.value, h.value)
+    ids = (ctypes.c_uint64 * 2)(0, 3)  # 3 does not exist: skipped like a missing key
+    _lib.check(L.rsk_hll_count_union_async(hs, ids, 2, w.fn, 6))
+    src = (ctypes.c_void_p * 1)(h.value)
+    sid = (ctypes.c_uint64 * 1)(1)
+    _lib.check(L.rsk_hll_merge_async(h, 2, src, sid, 1, w.fn, 7))
+    d_ids = np.array([3], np.uint64)
+    s_ids = np.array([2], np.uint64)
+    _lib.check(L.rsk_hll_merge_batch_async(h, d_ids.ctypes.data, s_ids.ctypes.data, 1, w.fn, 8))
+    res = w.wait([4, 5, 6, 7, 8])
+    assert res[0] == (0, 1)
+    assert res[1] == (0, orc.hll_count_dense(ref))
+    assert res[2] == (0, orc.hll_count_raw(ref))
+    assert res[3][0] == 0 and res[4][0] == 0
+    sync = np.zeros(4, np.uint64)
+    _lib.check(L.rsk_hll_count(h, None, 4, sync.ctypes.data))
+    ref1 = np.zeros(16384, np.uint8)
+    orc.hll_add(ref1, dk.to_numpy(), None, 16, 300_000)
+    assert int(sync[2]) == int(sync[3]) == orc.hll_count_dense(ref1)
+    dk.free()
+    L.rsk_hll_destroy(h)
+
+
+def test_two_handles_concurrently(L, engine, orc):
+    """Two threads, two handles, async adds issued at once: both callbacks
+    fire with the right replies and both sketches hold their own keys."""
+    from redisson_amd import KeyBatch, _lib
+
+    w = Waiter(_lib)
+    hs = [_pool(L, engine) for _ in range(2)]
+    batches = [orc.gen_keys16(0x5EED0100 + t, 0, 200_000) for t in range(2)]
+    go = threading.Barrier(2)
+    errs = []
+
+    def issue(t):
+        try:
+            ks = KeyBatch.from_numpy(batches[t].reshape(-1, 16)).as_struct()
+            go.wait()
+            for r in range(4):  # the first creates the key (reply 1), repeats change nothing
+                _lib.check(L.rsk_hll_add_async(hs[t], 0, ctypes.byref(ks), w.fn, 10 * t + r))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=issue, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs
+    res = w.wait([0, 1, 2, 3, 10, 11, 12, 13])
+    assert [v for _, v in res] == [1, 0, 0, 0, 1, 0, 0, 0]
+    assert threading.get_ident() not in w.threads  # completed on the runtime's thread
+    for t in range(2):
+        ref = np.zeros(16384, np.uint8)
+        orc.hll_add(ref, batches[t], None, 16, 200_000)
+        out = np.zeros(16384, np.uint8)
+        _lib.check(L.rsk_hll_get_registers(hs[t], 0, out.ctypes.data, _lib.RSK_MEM_HOST))
+        assert np.array_equal(out, ref)
+        L.rsk_hll_destroy(hs[t])
+
+
+def test_bloom_async_replies_and_contains(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib
+
+    w = Waiter(_lib)
+    size, k, n = 958506, 7, 100_000
+    b = ctypes.c_void_p()
+    _lib.check(L.rsk_bloom_create(engine.ctx, size, k, ctypes.byref(b)))
+    keys = orc.gen_keys16(0x5EED0003, 0, n)
+    vk = [bytes(keys[16 * i: 16 * i + 16]) for i in range(n)] + [b"", b"x" * 70]
+    batch = KeyBatch.from_bytes_list(vk)  # owns the blob and offsets the struct points at
+    kb = batch.as_struct()
+    added = np.full(len(vk), 7, np.uint8)
+    _lib.check(L.rsk_bloom_add_async(b, ctypes.byref(kb), added.ctypes.data, w.fn, 1))
+    got = np.zeros(len(vk), np.uint8)
+    _lib.check(L.rsk_bloom_contains_async(b, ctypes.byref(kb), got.ctypes.data, w.fn, 2))
+    assert w.wait([1, 2]) == [(0, len(vk)), (0, len(vk))]
+    bits = np.zeros((size + 7) // 8, np.uint8)
+    blob, offs = orc.pack_keys(vk)
+    want = orc.bloom_add_batch(bits, size, k, blob, offs)
+    assert np.array_equal(added, want)
+    assert got.all()
+    # reply-less add, device bits equal the oracle's
+    _lib.check(L.rsk_bloom_add_async(b, ctypes.byref(kb), None, w.fn, 3))
+    assert w.wait([3]) == [(0, len(vk))]
+    out = np.zeros_like(bits)
+    nb = ctypes.c_size_t()
+    _lib.check(L.rsk_bloom_export_bits(b, out.ctypes.data, out.size, ctypes.byref(nb)))
+    assert np.array_equal(out, bits)
+    # refused calls never fire
+    with pytest.raises(_lib.IllegalArgumentException):
+        _lib.check(L.rsk_bloom_contains_async(b, ctypes.byref(kb), None, w.fn, 4))
+    L.rsk_bloom_destroy(b)
+    assert 4 not in w.results
+
+
+def test_large_host_batch_completes_inline(L, engine, orc):
+    """A host batch above 256 MiB is not pinned whole: it runs before the call
+    returns and the callback fires on the calling thread."""
+    from redisson_amd import KeyBatch, _lib
+
+    w = Waiter(_lib)
+    n = (256 << 20) // 16 + 1000
+    keys = np.frombuffer(np.random.default_rng(3).bytes(16 * n), np.uint8)
+    h = _pool(L, engine)
+    ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+    _lib.check(L.rsk_hll_add_async(h, 0, ctypes.byref(ks), w.fn, 1))
+    assert 1 in w.results and threading.get_ident() in w.threads
+    assert w.results[1] == (0, 1)
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add_fixed_mt(ref, keys, 16, n, 8)
+    out = np.zeros(16384, np.uint8)
+    _lib.check(L.rsk_hll_get_registers(h, 0, out.ctypes.data, _lib.RSK_MEM_HOST))
+    assert np.array_equal(out, ref)
+    L.rsk_hll_destroy(h)
+
+
+def test_trim_and_synchronous_merge_batch(L, engine, orc):
+    from redisson_amd import KeyBatch, _lib
+
+    h = _pool(L, engine, 3)
+    keys = orc.gen_keys16(0x5EED0002, 0, 50_000)
+    ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+    _lib.check(L.rsk_hll_add(h, 0, ctypes.byref(ks), None))
+    d = np.array([1, 2], np.uint64)
+    s = np.array([0, 1], np.uint64)  # 2 <- 1 <- 0: ordered by level
+    _lib.check(L.rsk_hll_merge_batch(h, d.ctypes.data, s.ctypes.data, 2))
+    # returns with the merges done: the registers read on any stream are final
+    out = np.zeros(16384, np.uint8)
+    _lib.check(L.rsk_hll_get_registers(h, 2, out.ctypes.data, _lib.RSK_MEM_HOST))
+    ref = np.zeros(16384, np.uint8)
+    orc.hll_add(ref, keys, None, 16, 50_000)
+    assert np.array_equal(out, ref)
+    _lib.check(L.rsk_trim(engine.ctx))
+    cnt = np.zeros(3, np.uint64)
+    _lib.check(L.rsk_hll_count(h, None, 3, cnt.ctypes.data))  # scratch regrown on demand
+    assert len(set(cnt.tolist())) == 1
+    L.rsk_hll_destroy(h)
+
+
+def _sparse(ops):
+    """A Redis sparse HLL string from (kind, value, run) opcodes."""
+    out = bytearray(b"HYLL" + bytes([1, 0, 0, 0]) + bytes(8))
+    for kind, v, run in ops:
+        if kind == "zero":
+            out.append(run - 1)
+        elif kind == "xzero":
+            out += bytes([0x40 | ((run - 1) >> 8), (run - 1) & 0xFF])
+        else:
+            out.append(0x80 | ((v - 1) << 2) | (run - 1))
+    return bytes(out)
+
+
+def test_import_returns_set_bytes_until_written(L, engine, orc):
+    """SET of a non-canonical sparse string (VAL 3 x3 then VAL 3 x2, where the
+    canonical form is x4 + x1) is what GET returns until the key is written;
+    PFCOUNT only refreshes the card bytes; a PFADD re-encodes (registers
+    unchanged by the import either way)."""
+    from redisson_amd import KeyBatch, _lib
+
+    s = _sparse([("val", 3, 3), ("val", 3, 2), ("xzero", 0, 16384 - 5)])
+    h = _pool(L, engine)
+    _lib.check(L.rsk_hll_import_redis(h, 0, s, len(s)))
+    buf = (ctypes.c_uint8 * 12304)()
+    n = ctypes.c_size_t()
+    _lib.check(L.rsk_hll_export_redis(h, 0, buf, 12304, ctypes.byref(n)))
+    assert bytes(buf[: n.value]) == s
+    cnt = np.zeros(1, np.uint64)
+    _lib.check(L.rsk_hll_count(h, None, 1, cnt.ctypes.data))
+    _lib.check(L.rsk_hll_export_redis(h, 0, buf, 12304, ctypes.byref(n)))
+    got = bytes(buf[: n.value])
+    assert got[:8] == s[:8] and got[16:] == s[16:]
+    assert int.from_bytes(got[8:16], "little") == int(cnt[0])  # the cached cardinality, valid
+    keys = orc.gen_keys16(0x5EED0002, 0, 3)
+    ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+    _lib.check(L.rsk_hll_add(h, 0, ctypes.byref(ks), None))
+    _lib.check(L.rsk_hll_export_redis(h, 0, buf, 12304, ctypes.byref(n)))
+    assert bytes(buf[16: n.value]) != s[16:]  # re-encoded after the write
+    L.rsk_hll_destroy(h)

@@ -131,13 +131,12 @@ def test_c3_stream_device_resident(L, engine, orc):
 
 @pytest.mark.parametrize("size,k,n", [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 33, 20000),
                                       (19170117, 7, 300000), (157298745, 7, 400000), (157298745, 3, 700000)])
-def test_partitioned_add_parity(L, engine, orc, monkeypatch, size, k, n):
+def test_partitioned_add_parity(L, engine, orc, route, size, k, n):
     """Slice-partitioned add (forced on) gives the oracle's bit string: one partition
     level (<= 256 slices of 2^19 bits) and two levels (157M bits = 301 slices)."""
     from redisson_amd import KeyBatch
 
-    monkeypatch.setenv("RSK_BLOOM_PARTITION", "1")
-    monkeypatch.setenv("RSK_BLOOM_ST", "0")
+    route(bloom_part=1, bloom_stream=-1)
     keys = orc.gen_keys16(0x5EED0003, 0, n)
     b = _filter(L, engine, size, k)
     _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)), replies=False)
@@ -158,34 +157,23 @@ ST_CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000
             (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000), (4014142460, 8, 600000)]
 
 
-ST_KNOBS = ["RSK_BLOOM_ST=1", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_T1=1024", "RSK_BLOOM_ST=1,RSK_BLOOM_ST_CHUNK=300000",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA_TINY=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA_DBG=3",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0", "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_TINY_BUDGET=1",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_T2=512,RSK_BLOOM_ST_UA=4",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA=0,RSK_BLOOM_ST_CHUNK=300000",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA_P=1", "RSK_BLOOM_ST=1,RSK_BLOOM_SA_P=13,RSK_BLOOM_SA2_PF=1",
-            "RSK_BLOOM_ST=1,RSK_BLOOM_SA1_KPL=2"]
+ST_KNOBS = ["bloom_stream=1", "bloom_stream=1,bloom_chunk=300000", "bloom_stream=1,sa_tiny=1",
+            "bloom_stream=1,sa_parts=1", "bloom_stream=1,sa_parts=13"]
 
 
 @pytest.mark.parametrize("size,k,n", ST_CASES)
 @pytest.mark.parametrize("knobs", ST_KNOBS)
-def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs):
-    """The super-tile insert (rsk_bloom_st.hip), forced on, gives the oracle's
-    bit string: one level (<= 256 slices) and two (301 and 7,657 slices), k in
-    {1, 2, 5, 7, 8} (1024-key super-tiles) and {9, 16} (512-key), 1024-lane
-    super-tiles, many chunks; two-level filters through the append pipeline
-    (sa1/sa2, default; full barriers instead of LDS-only ones; sub-regions too
-    small, which overflow into the exact-offset fallback) and through the
-    header pipeline (st1/st2, RSK_BLOOM_SA=0) with a one-tile budget
-    (overflow), 512-lane st2 and many chunks; sa2 with one part per coarse bin
-    (every workgroup walks all sub-regions) and with 13 (parts without any
-    sub-region when the batch has few super-tiles) plus its register
-    prefetch; sa1 with 2 keys per lane."""
+def test_slice_routed_add_parity(L, engine, orc, route, size, k, n, knobs):
+    """The slice-routed insert (rsk_bloom_st.hip), forced on, gives the oracle's
+    bit string: one level (<= 256 slices: st1 + apply) and two (301, 7,657 and
+    7,657 slices through the append pipeline sa1/sa2/apply), k in {1, 2, 5, 7,
+    8} (2 or 4 keys per lane) and {9, 16} (1 key per lane); many chunks;
+    sub-regions too small (overflow into the exact-offset fallback); sa2 with
+    one part per coarse bin (every workgroup walks all sub-regions) and with 13
+    (parts without any sub-region when the batch has few super-tiles)."""
     from redisson_amd import KeyBatch
 
-    for kv in filter(None, knobs.split(",")):
-        key, val = kv.split("=")
-        monkeypatch.setenv(key, val)
+    route(knobs)
     keys = orc.gen_keys16(0x5EED0003, 0, n)
     b = _filter(L, engine, size, k)
     _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)), replies=False)
@@ -204,15 +192,13 @@ def test_slice_routed_add_parity(L, engine, orc, monkeypatch, size, k, n, knobs)
 
 
 @pytest.mark.parametrize("knobs", ST_KNOBS)
-def test_slice_routed_skewed_keys(L, engine, orc, monkeypatch, knobs):
+def test_slice_routed_skewed_keys(L, engine, orc, route, knobs):
     """One key repeated 300,000 times plus a few distinct ones: every probe of
     the repeated key lands in the same k slices (one long segment per
     super-tile and bin), so st2 tiles and apply segments are full-length runs."""
     from redisson_amd import KeyBatch
 
-    for kv in filter(None, knobs.split(",")):
-        key, val = kv.split("=")
-        monkeypatch.setenv(key, val)
+    route(knobs)
     size, k = 157298745, 7
     base = orc.gen_keys16(0x5EED0003, 0, 1000).reshape(-1, 16)
     keys = np.concatenate([np.repeat(base[:1], 300000, axis=0), base[1:]]).reshape(-1)
@@ -224,8 +210,7 @@ def test_slice_routed_skewed_keys(L, engine, orc, monkeypatch, knobs):
     L.rsk_bloom_destroy(b)
 
 
-@pytest.mark.parametrize("sa", ["1", "0"])
-def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, sa):
+def test_slice_routed_matches_direct_c3_size(L, engine, route):
     """At the C3 filter size (9,585,058,377 bits, 18,283 slices: 143 coarse bins
     x 128 slices) the super-tile insert and the direct atomicOr kernel set
     identical bits."""
@@ -235,10 +220,8 @@ def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, sa):
     ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
     ks = ins.keys_fixed(n, 16).as_struct()
     filters = {}
-    monkeypatch.setenv("RSK_BLOOM_SA", sa)
     for mode in ("1", "0"):
-        monkeypatch.setenv("RSK_BLOOM_ST", mode)
-        monkeypatch.setenv("RSK_BLOOM_PARTITION", "0")
+        route(bloom_stream=1 if mode == "1" else -1, bloom_part=-1)
         f = _filter(L, engine, size, k)
         _lib.check(L.rsk_bloom_add(f, ctypes.byref(ks), None))
         filters[mode] = f
@@ -259,7 +242,7 @@ def test_slice_routed_matches_direct_c3_size(L, engine, monkeypatch, sa):
     ins.free()
 
 
-def test_partitioned_add_matches_direct_c3_size(L, engine, monkeypatch):
+def test_partitioned_add_matches_direct_c3_size(L, engine, route):
     """At the C3 filter size (9,585,058,377 bits, 18,283 slices, two levels) the
     exact-offset partitioned add (the k > 16 path and the super-tile fallback)
     and the direct atomicOr kernel set identical bits."""
@@ -269,9 +252,8 @@ def test_partitioned_add_matches_direct_c3_size(L, engine, monkeypatch):
     ins = devmem.gen_keys16(engine, 0x5EED0003, 0, n)
     ks = ins.keys_fixed(n, 16).as_struct()
     filters = {}
-    monkeypatch.setenv("RSK_BLOOM_ST", "0")
     for mode in ("1", "0"):
-        monkeypatch.setenv("RSK_BLOOM_PARTITION", mode)
+        route(bloom_stream=-1, bloom_part=1 if mode == "1" else -1)
         f = _filter(L, engine, size, k)
         _lib.check(L.rsk_bloom_add(f, ctypes.byref(ks), None))
         filters[mode] = f

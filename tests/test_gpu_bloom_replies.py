@@ -16,12 +16,6 @@ def L():
     return _lib.load()
 
 
-def _knobs(monkeypatch, knobs):
-    for kv in filter(None, knobs.split(",")):
-        key, val = kv.split("=")
-        monkeypatch.setenv(key, val)
-
-
 def test_sampled_reply_oracle_matches_sequential(orc):
     """The sampled full-size reply oracle (hash table of the sample's bits, min
     sequence number over the whole stream) equals the sequential SETBIT oracle."""
@@ -38,24 +32,23 @@ def test_sampled_reply_oracle_matches_sequential(orc):
 CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000), (1000003, 3, 200000), (1000003, 33, 20000),
          (19170117, 7, 300000), (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000),
          (4014142460, 8, 600000)]
-KNOBS = ["RSK_BLOOM_REPLY=1", "RSK_BLOOM_REPLY=1,RSK_BLOOM_REPLY_CHUNK=300000", "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_TINY=1",
-         "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_P=13,RSK_BLOOM_RP_U=4", "RSK_BLOOM_REPLY=1,RSK_BLOOM_SA_P=1,RSK_BLOOM_RP_U=1"]
+KNOBS = ["reply=1", "reply=1,reply_chunk=300000", "reply=1,sa_tiny=1", "reply=1,sa_parts=13", "reply=1,sa_parts=1"]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("size,k,n", CASES)
 @pytest.mark.parametrize("knobs", KNOBS)
-def test_replies_parity(L, engine, orc, monkeypatch, size, k, n, knobs):
+def test_replies_parity(L, engine, orc, route, size, k, n, knobs):
     """Forced on at every size: one partition level (<= 256 slices) and two
     (301 and 7,657 slices), k in {1, 2, 3, 5, 7, 8, 9, 16} (33: the sort path); many chunks (each
     answered against the filter the earlier ones left); sub-regions too small
     (the chunk falls back to the sort path); rp2 with 13 parts per coarse bin
-    and with one, rp_reply with 4 and 1 keys per lane.  A second batch of variable-length
+    and with one.  A second batch of variable-length
     keys repeats keys of the first and of itself (bits already set before the
     batch, first probes inside it)."""
     from redisson_amd import KeyBatch
 
-    _knobs(monkeypatch, knobs)
+    route(knobs)
     keys = orc.gen_keys16(0x5EED0003, 0, n)
     b = _filter(L, engine, size, k)
     got = _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)))
@@ -77,12 +70,12 @@ def test_replies_parity(L, engine, orc, monkeypatch, size, k, n, knobs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("knobs", KNOBS[:2])
-def test_replies_skewed_keys(L, engine, orc, monkeypatch, knobs):
+def test_replies_skewed_keys(L, engine, orc, route, knobs):
     """One key repeated 300,000 times among distinct ones: only its first copy
     can answer true; every probe of the copies lands on the same k bits."""
     from redisson_amd import KeyBatch
 
-    _knobs(monkeypatch, knobs)
+    route(knobs)
     size, k = 157298745, 7
     base = orc.gen_keys16(0x5EED0003, 0, 1000).reshape(-1, 16)
     keys = np.concatenate([base[1:500], np.repeat(base[:1], 300000, axis=0), base[500:]]).reshape(-1)
@@ -98,7 +91,7 @@ def test_replies_skewed_keys(L, engine, orc, monkeypatch, knobs):
 
 
 @pytest.mark.gpu
-def test_replies_match_sort_path_c3_filter(L, engine, monkeypatch):
+def test_replies_match_sort_path_c3_filter(L, engine, route):
     """At the C3 filter size (9,585,058,377 bits, k = 7: 143 coarse bins x 128
     slices x 16 blocks) 20M device-resident keys give the same replies and bit
     string through the partitioned pipeline and through the sort path, into an
@@ -111,7 +104,7 @@ def test_replies_match_sort_path_c3_filter(L, engine, monkeypatch):
     half = ins.keys_fixed(n // 2, 16).as_struct()
     res = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RSK_BLOOM_REPLY", mode)
+        route(reply=1 if mode == "1" else -1)
         f = _filter(L, engine, size, k)
         out = devmem.DeviceBuffer(engine, n)
         _lib.check(L.rsk_bloom_add(f, ctypes.byref(ks), out.ptr))

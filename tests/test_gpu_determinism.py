@@ -72,7 +72,7 @@ def test_hll_order_and_split_independent(L, engine, orc):
         L.rsk_hll_destroy(h)
 
 
-def test_grouped_order_independent(L, engine, orc, monkeypatch):
+def test_grouped_order_independent(L, engine, orc, route):
     """3M (sketch, key) pairs over 20,000 sketches: in order and shuffled, through
     the partitioned path and the direct one: identical pools."""
     from redisson_amd import KeyBatch, _lib, devmem
@@ -85,7 +85,7 @@ def test_grouped_order_independent(L, engine, orc, monkeypatch):
     perm = np.random.default_rng(5).permutation(n)
     pools = []
     for mode, p in (("1", None), ("1", perm), ("0", perm)):
-        monkeypatch.setenv("RSK_HLL_GPART", mode)
+        route(gpart=1 if mode == "1" else -1)
         gg = groups if p is None else np.ascontiguousarray(groups[p])
         kk = keys if p is None else np.ascontiguousarray(keys[p])
         h = _pool(L, engine, G)

@@ -270,7 +270,7 @@ def _pool_regs(L, engine, h, G):
 
 
 @pytest.mark.parametrize("G,n", [(8205, 3_000_000), (1, 50_000), (4096 * 3, 2_000_001), (20, 4_500_003)])
-def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, monkeypatch, G, n):
+def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, route, G, n):
     """Grouped PFADD partitioned by sketch (coarse bins of 4096 sketches, fine
     bins of 16, LDS halves of 8; G not a multiple of any of them) equals the
     direct random-CAS kernel and the oracle over the whole pool."""
@@ -280,7 +280,7 @@ def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, monkeypat
     ks = k.keys_fixed(n, 16).as_struct()
     pools = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RSK_HLL_GPART", mode)
+        route(gpart=1 if mode == "1" else -1)
         h = _pool(L, engine, G)
         _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
         pools[mode] = h
@@ -295,13 +295,13 @@ def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, monkeypat
         L.rsk_hll_destroy(h)
 
 
-def test_grouped_partitioned_host_pairs_skip_out_of_range(L, engine, orc, monkeypatch):
+def test_grouped_partitioned_host_pairs_skip_out_of_range(L, engine, orc, route):
     """Host-resident pairs through the partitioned path: group ids >= G are
     ignored (as by the direct kernel), every other pair lands in its sketch;
     a second batch max-merges into the existing registers."""
     from redisson_amd import KeyBatch, _lib
 
-    monkeypatch.setenv("RSK_HLL_GPART", "1")
+    route(gpart=1)
     G, n = 100, 300_000
     rng = np.random.default_rng(7)
     keys = orc.gen_keys16(0x5EED0107, 0, n).reshape(-1, 16)
@@ -320,13 +320,13 @@ def test_grouped_partitioned_host_pairs_skip_out_of_range(L, engine, orc, monkey
     L.rsk_hll_destroy(h)
 
 
-def test_grouped_partitioned_pool_state_after_other_writers(L, engine, orc, monkeypatch):
+def test_grouped_partitioned_pool_state_after_other_writers(L, engine, orc, route):
     """The partitioned add skips reading a pool known to be all zero (fresh or
     cleared): a PFADD into one sketch beforehand, and a clear afterwards, must
     both be honoured."""
     from redisson_amd import KeyBatch, _lib, devmem
 
-    monkeypatch.setenv("RSK_HLL_GPART", "1")
+    route(gpart=1)
     G, n = 64, 200_000
     h = _pool(L, engine, G)
     ka = orc.gen_keys16(0x5EED0200, 0, 5000)
@@ -584,7 +584,7 @@ def test_count_estimator_branches(L, engine, orc, n, branch):
     L.rsk_hll_destroy(h)
 
 
-def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, monkeypatch):
+def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, route):
     """C5 Zipf(1.1) stress variant: the device generator equals the
     oracle's pair stream; the partitioned grouped add over it (one coarse bin
     holding most pairs, one fine bin a third of them) equals the direct kernel
@@ -599,7 +599,7 @@ def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, monkeypa
     ks = k.keys_fixed(n, 16).as_struct()
     pools = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RSK_HLL_GPART", mode)
+        route(gpart=1 if mode == "1" else -1)
         h = _pool(L, engine, G)
         _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
         pools[mode] = h
@@ -640,14 +640,14 @@ def test_c5_zipf_full_size_hot_groups_bit_exact(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
-def test_grouped_add_precomputed_counts_follow_later_writes(L, engine, orc, monkeypatch):
+def test_grouped_add_precomputed_counts_follow_later_writes(L, engine, orc, route):
     """The partitioned grouped add leaves every written row's PFCOUNT estimate
     for rsk_hll_count (no 16 KiB re-read); any later write to the pool (PFADD,
     PFMERGE, raw merge, import, clear, a second grouped add) must retire those
     estimates, and every count must equal the oracle's on the current registers."""
     from redisson_amd import KeyBatch, _lib, devmem
 
-    monkeypatch.setenv("RSK_HLL_GPART", "1")
+    route(gpart=1)
     G, n = 300, 600_000
     h = _pool(L, engine, G)
     g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
