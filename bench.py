@@ -419,6 +419,7 @@ def main():
         remote = np.concatenate([cw[:, 1], ms_])
         kern, unit_bytes = "hll_add_grouped16", 20.0 * n
         bufs = [groups, gkeys]
+        counts_out = np.empty(max(G, own_count), np.uint64)  # the caller's reply buffer, reused across steps
 
     def step():
         if wl == "c5":
@@ -426,10 +427,10 @@ def main():
             pool.add(kb, groups)
             if world > 1:
                 assert shard.hll_reducescatter_pool(pool.pool) == (own_first, own_count)  # RCCL MAX
-                c = pool.count(own_ids)
+                c = pool.count(own_ids, out=counts_out)
                 shard.hll_fetch_rows(pool.pool, remote)  # partner / source rows from their owners
             else:
-                c = pool.count()
+                c = pool.count(out=counts_out)
             pool.countWith(cw)
             pool.mergeWith(md, ms_)
             return int(c[0])

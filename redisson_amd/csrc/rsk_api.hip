@@ -184,7 +184,7 @@ void check_out(const rsk_ctx* c, const rsk_keys* k, const void* out) {
 // its own device twin, so chunk i+1's DMA may queue behind chunk i's kernels
 // without a host wait.  rsk_options.stage_threads (default 8) sets the copy threads.
 void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n, unsigned threads) {
-  const uint64_t min_piece = 8ull << 20;
+  const uint64_t min_piece = 2ull << 20;
   const unsigned nt = (unsigned)std::min<uint64_t>(threads, n / min_piece);
   if (nt <= 1) {
     if (n) std::memcpy(dst, src, n);
@@ -310,6 +310,19 @@ void check_hll(const rsk_hll* h, uint64_t id) {
   CtxLock l(h->ctx);         // the pool's host state is the context's
   rsk::hll_materialize(h);  // every caller reads or writes registers
   rsk::hll_touch(h);        // conservatively: every caller may write them
+}
+
+// check_hll for a batch of ids of one pool: ranges checked in one pass, the
+// pool materialised and touched once (10^5-pair countWith / mergeWith batches).
+void check_hll_ids(const rsk_hll* h, const uint64_t* a, uint64_t na, const uint64_t* b = nullptr, uint64_t nb = 0) {
+  need(h != nullptr, "hll handle is NULL");
+  uint64_t bad = 0;
+  for (uint64_t i = 0; i < na; ++i) bad |= a[i] >= h->n;
+  for (uint64_t i = 0; i < nb; ++i) bad |= b[i] >= h->n;
+  need(!bad, "sketch id out of range");
+  CtxLock l(h->ctx);
+  rsk::hll_materialize(h);
+  rsk::hll_touch(h);
 }
 
 uint8_t* regs_of(rsk_hll* h, uint64_t id) { return h->d_regs + id * (uint64_t)HLL_REGS; }
@@ -827,9 +840,12 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
       RSK_HIP(hipMemcpyAsync(c->h_small + 4096, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
       std::memcpy(out, c->h_small + 4096, n * 8);
-    } else {
-      RSK_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
+    } else {  // large ones (count of a whole pool: 8 MB at 10^6 sketches) through the
+              // pinned per-call buffer: one full-speed DMA, then host threads copy out
+      uint8_t* hb = c->pinned(n * 8);
+      RSK_HIP(hipMemcpyAsync(hb, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
+      par_copy(reinterpret_cast<uint8_t*>(out), hb, n * 8, c->stage_threads);
     }
   });
 }
@@ -864,10 +880,7 @@ uint64_t merge_batch_host_bytes(uint64_t n) { return 3 * merge_batch_seg(n) + 4 
 uint64_t merge_batch_dev_bytes(uint64_t n) { return 3 * merge_batch_seg(n) + 512; }
 
 void merge_batch_check(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_ids, uint64_t n) {
-  for (uint64_t i = 0; i < n; ++i) {
-    check_hll(h, dst_ids[i]);
-    check_hll(h, src_ids[i]);
-  }
+  check_hll_ids(h, dst_ids, n, src_ids, n);
 }
 
 // hb: pinned host buffer of merge_batch_host_bytes(n); d: device scratch of
@@ -958,10 +971,12 @@ int rsk_hll_count_union_batch(rsk_hll* h, const uint64_t* member_ids, uint32_t a
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     if (n == 0) return;
+    check_hll_ids(h, member_ids, n * arity);
     auto* ptrs = reinterpret_cast<const uint8_t**>(c->pinned(8ull * n * arity + 8ull * n));
+    const uint8_t* e = h->exists.data();
     for (uint64_t i = 0; i < n * arity; ++i) {
-      check_hll(h, member_ids[i]);
-      ptrs[i] = h->exists[member_ids[i]] ? regs_of(h, member_ids[i]) : nullptr;
+      const uint64_t id = member_ids[i];
+      ptrs[i] = e[id] ? regs_of(h, id) : nullptr;
     }
     union_impl(c, ptrs, arity, n, out);
   });

@@ -533,5 +533,144 @@ __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict
   if (threadIdx.x == 0) tiles_out[cp] = ntile;
 }
 
+// ==================================== sa2 with 16-bit records (the insert)
+// The insert's second pass re-sorts each coarse bin by BUCKET = the slice and
+// the top 3 bits of the 19-bit offset inside it (2^(f2+3) <= 1024 buckets), so
+// every output record keeps only the low 16 bits: half the bytes sa2 writes
+// and apply reads.  A tile's buckets are contiguous and unpadded (the tile
+// itself starts 16-byte aligned); its header row holds the 1025 bucket starts
+// (u16, [nbk] = the tile's record count) -- apply reads a slice's 9 entries
+// and tells the 8 sub-buckets of a record apart by its position.
+constexpr uint32_t SAH_BK_MAX = 1024;  // buckets per coarse bin, at most (f2 <= 7)
+constexpr uint32_t SAH_SUB = 3;         // offset bits [16, 19) sorted by bucket
+
+// tot[cp] = u16 slots of (c, p)'s sa2h tiles (records + up to 7 of alignment
+// per tile), bud[cp] = its tiles.
+__global__ __launch_bounds__(256) __attribute__((unused)) void sah_size_kernel(const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
+                                                       uint32_t P, uint32_t ncp, uint64_t* __restrict__ tot,
+                                                       uint32_t* __restrict__ bud) {
+  const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cp >= ncp) return;
+  const uint32_t c = cp / P, p = cp - c * P;
+  uint64_t recs = 0;
+  uint32_t tiles = 0;
+  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
+    const uint32_t u = used[(uint64_t)w * nb1 + c];
+    recs += u;
+    tiles += (u + SA2_SLOTS - 1) / SA2_SLOTS;
+  }
+  tot[cp] = ((recs + 7) & ~7ull) + 8ull * tiles;
+  bud[cp] = tiles;
+}
+
+__global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_kernel(const uint32_t* __restrict__ region, uint32_t quota,
+                                                           const uint32_t* __restrict__ used, uint32_t W,
+                                                           uint32_t nb1, uint32_t P, uint32_t nbk,
+                                                           const uint64_t* __restrict__ reg_off,
+                                                           const uint32_t* __restrict__ tile_off,
+                                                           uint32_t* __restrict__ tiles_out,
+                                                           uint16_t* __restrict__ out, uint16_t* __restrict__ h2,
+                                                           uint32_t* __restrict__ tb2) {
+  constexpr int NV = SA2_V * 4;  // records per lane per tile
+  constexpr uint32_t PER = SAH_BK_MAX / 64;  // buckets per wave-0 lane
+  __shared__ __attribute__((aligned(16))) uint16_t img[SA2_SLOTS + 8];
+  __shared__ uint32_t hist[SAH_BK_MAX], lstart[SAH_BK_MAX + 1];
+  __shared__ uint32_t s_used[SA2_WMAX];
+  const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
+  for (uint32_t b = threadIdx.x; b < SAH_BK_MAX; b += SA2_T) hist[b] = 0;
+  const uint64_t base = reg_off[cp];
+  const uint32_t tbeg = tile_off[cp];
+  uint64_t written = 0;
+  uint32_t ntile = 0;
+  const uint32_t wbeg = W * p / P, wend = W * (p + 1) / P;
+  for (uint32_t i = threadIdx.x; i < wend - wbeg; i += SA2_T) s_used[i] = used[(uint64_t)(wbeg + i) * nb1 + c];
+  __syncthreads();
+  uint32_t w = wbeg, t0 = 0, nu = 0;
+  while (w < wend && (nu = s_used[w - wbeg]) == 0) ++w;
+  // tile t's image is written out during tile t + 1, after its ranks (one
+  // vmcnt for loads and stores: see bloom_sa1_kernel)
+  auto write_out = [&](uint32_t total, uint64_t at) {
+    u32x4* o4 = reinterpret_cast<u32x4*>(out + base + at);  // base, at: multiples of 8 slots
+    const uint4* i4 = reinterpret_cast<const uint4*>(img);
+    for (uint32_t j = threadIdx.x; j < (total + 7) / 8; j += SA2_T) {
+      const uint4 v = i4[j];
+      u32x4 x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, o4 + j);
+    }
+  };
+  bool have = w < wend;
+  uint32_t pend = 0;
+  uint64_t pend_at = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  while (have) {
+    const uint4* in = reinterpret_cast<const uint4*>(region + ((uint64_t)w * nb1 + c) * quota);
+    uint4 cur[SA2_V];
+#pragma unroll
+    for (int v = 0; v < SA2_V; ++v) {
+      const uint32_t q4 = t0 / 4 + v * SA2_T + threadIdx.x;
+      cur[v] = 4 * q4 < nu ? ld_nt16(in + q4) : make_uint4(INVALID, INVALID, INVALID, INVALID);
+    }
+    const uint32_t ct0 = t0, cnu = nu;
+    t0 += SA2_SLOTS;
+    if (t0 >= nu) {
+      t0 = 0;
+      do ++w;
+      while (w < wend && (nu = s_used[w - wbeg]) == 0);
+    }
+    have = w < wend;
+    uint32_t pay[NV], tag[NV];
+#pragma unroll
+    for (int v = 0; v < SA2_V; ++v) {
+      const uint32_t q4 = ct0 / 4 + v * SA2_T + threadIdx.x;
+      const uint32_t x[4] = {cur[v].x, cur[v].y, cur[v].z, cur[v].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pay[4 * v + e] = 4 * q4 + e < cnu ? x[e] : INVALID;
+    }
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      tag[r] = INVALID;
+      if (pay[r] != INVALID) {
+        const uint32_t bk = pay[r] >> 16;
+        tag[r] = (bk << 16) | atomicAdd(&hist[bk], 1u);
+      }
+    }
+    write_out(pend, pend_at);  // tile t - 1
+    lds_barrier();             // (A) ranks taken, the previous image written out
+    if (threadIdx.x < 64) {    // bucket starts (and counts reset)
+      uint32_t v[PER], sum = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        v[i] = b < nbk ? hist[b] : 0;
+        if (b < nbk) hist[b] = 0;
+        sum += v[i];
+      }
+      const uint32_t incl = wave_scan_incl(sum, lane);
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t b = lane * PER + i;
+        if (b < nbk) lstart[b] = run;
+        run += v[i];
+      }
+      if (lane == 63) lstart[nbk] = incl;
+    }
+    lds_barrier();  // (B)
+    const uint32_t total = lstart[nbk];
+    for (uint32_t b = threadIdx.x; b <= nbk; b += SA2_T) h2[(uint64_t)(tbeg + ntile) * (nbk + 1) + b] = (uint16_t)lstart[b];
+    if (threadIdx.x == 0) tb2[tbeg + ntile] = (uint32_t)written;  // u16 slots past reg_off[cp]
+#pragma unroll
+    for (int r = 0; r < NV; ++r)
+      if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = (uint16_t)pay[r];
+    pend = total;
+    pend_at = written;
+    written += (total + 7) & ~7u;
+    ++ntile;
+    lds_barrier();  // (C)
+  }
+  write_out(pend, pend_at);
+  if (threadIdx.x == 0) tiles_out[cp] = ntile;
+}
+
 }  // namespace
 }  // namespace rsk

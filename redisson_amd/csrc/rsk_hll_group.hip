@@ -174,7 +174,11 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
       for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = make_uint4(0, 0, 0, 0);
     else
       for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
-    __syncthreads();
+    // LDS-only barriers (lds_barrier) throughout: the previous item's
+    // write-back stores stay in flight while this item's LDS file is cleared
+    // and its records are applied (one workgroup per CU: a full fence here
+    // serialised every item's 128 KiB write behind its record phase)
+    lds_barrier();
     for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += GP_T * GP_U) {
       uint32_t rv[GP_U];  // GP_U record loads in flight per lane
 #pragma unroll
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     const bool est = pc.pcount && e0 - a <= GP_CH;  // (a split bin's extra chunks change the rows later)
     if (!est) {
       for (uint32_t q = threadIdx.x; q < n4; q += GP_T) gp[q] = lp[q];
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
       }
       sd = wave_reduce(sd);
       if (lane == 0) part[wv] = sd;
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x < nsk) {  // one lane per sketch: its two wave partials
         const SumD p0 = part[2 * threadIdx.x], p1 = part[2 * threadIdx.x + 1];  // exact sums: any order
         SumD t{p0.t + p1.t, p0.ez + p1.ez, p0.rmax > p1.rmax ? p0.rmax : p1.rmax};
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
         }
       }
     }
-    __syncthreads();
+    lds_barrier();  // every lane has read the LDS file (its stores may still be in flight)
   }
 }
 

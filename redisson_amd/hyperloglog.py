@@ -174,15 +174,18 @@ class GroupedHyperLogLog:
         ks = keys.as_struct()
         _lib.check(_lib.load().rsk_hll_add_grouped(self.pool, ctypes.byref(ks), gp))
 
-    def count(self, ids=None) -> np.ndarray:
+    def count(self, ids=None, out=None) -> np.ndarray:
+        """PFCOUNT of every sketch (ids None) or of ids; `out` (uint64, reused
+        across calls) receives the counts."""
+        n = self.n if ids is None else len(ids)
+        if out is None or out.dtype != np.uint64 or out.size < n or not out.flags.c_contiguous:
+            out = np.empty(n, dtype=np.uint64)
         if ids is None:
-            out = np.zeros(self.n, dtype=np.uint64)
             _lib.check(_lib.load().rsk_hll_count(self.pool, None, self.n, out.ctypes.data))
-            return out
+            return out[:n]
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
-        out = np.zeros(ids.size, dtype=np.uint64)
         _lib.check(_lib.load().rsk_hll_count(self.pool, ids.ctypes.data, ids.size, out.ctypes.data))
-        return out
+        return out[:n]
 
     def countWith(self, member_ids) -> np.ndarray:
         m = np.ascontiguousarray(member_ids, dtype=np.uint64)

@@ -32,6 +32,8 @@ for p in ${PART//,/ }; do
       step bench_c5 200 python bench.py --workload c5 || exit 1 ;;
     c5z)
       step bench_c5_zipf 200 python bench.py --workload c5 --zipf 1.1 || exit 1 ;;
+    c5prof)
+      step c5prof 300 python scripts/c5_host_profile.py 500000000 1000000 10 || exit 1 ;;
     prof)
       B="python3 bench.py --no-cpu --no-bloom-replies"
       rm -rf gpurun_out/prof_stats
