@@ -29,7 +29,6 @@ const char *rsk_diag_last_error(void);
  *   reply         add() replies: 0 auto, 1 first-key pipeline at any size, -1 sort path
  *   reply_chunk   probes per chunk of the first-key pipeline (0 = default)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
- *   sah_apply     insert apply kernel shape: 0 default, 1 1024 lanes x 2 rounds, 2 512 x 4, 3 512 x 6
  *   reset         every route back to automatic
  * Every route gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);

@@ -91,7 +91,6 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "reply") t.reply = (int)value;
     else if (k == "reply_chunk") t.reply_chunk = (uint64_t)value;
     else if (k == "gpart") t.gpart = (int)value;
-    else if (k == "sah_apply") t.sah_apply = (int)value;
     else if (k == "reset") t = Tuning{};
     else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};
   });

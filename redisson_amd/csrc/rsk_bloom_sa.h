@@ -538,9 +538,11 @@ __global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict
 // the top 3 bits of the 19-bit offset inside it (2^(f2+3) <= 1024 buckets), so
 // every output record keeps only the low 16 bits: half the bytes sa2 writes
 // and apply reads.  A tile's buckets are contiguous and unpadded (the tile
-// itself starts 16-byte aligned); its header row holds the 1025 bucket starts
-// (u16, [nbk] = the tile's record count) -- apply reads a slice's 9 entries
-// and tells the 8 sub-buckets of a record apart by its position.
+// itself starts 16-byte aligned).  Its bucket starts go straight to the
+// layout apply reads: row f (slice f of the bin) holds, per tile, one uint4 =
+// the 8 u16 starts of buckets 8f .. 8f+7; row 2^f2 holds the tile's record
+// count in .x, so slice f's segment ends where row f + 1 starts.  The 16-byte
+// pieces of consecutive tiles of one workgroup fill a row's cache lines in L2.
 constexpr uint32_t SAH_BK_MAX = 1024;  // buckets per coarse bin, at most (f2 <= 7)
 constexpr uint32_t SAH_SUB = 3;         // offset bits [16, 19) sorted by bucket
 
@@ -569,8 +571,8 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
                                                            const uint64_t* __restrict__ reg_off,
                                                            const uint32_t* __restrict__ tile_off,
                                                            uint32_t* __restrict__ tiles_out,
-                                                           uint16_t* __restrict__ out, uint16_t* __restrict__ h2,
-                                                           uint32_t* __restrict__ tb2) {
+                                                           uint16_t* __restrict__ out, uint4* __restrict__ hp,
+                                                           uint64_t hp_stride, uint32_t* __restrict__ tb2) {
   constexpr int NV = SA2_V * 4;  // records per lane per tile
   constexpr uint32_t PER = SAH_BK_MAX / 64;  // buckets per wave-0 lane
   __shared__ __attribute__((aligned(16))) uint16_t img[SA2_SLOTS + 8];
@@ -657,8 +659,14 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
     }
     lds_barrier();  // (B)
     const uint32_t total = lstart[nbk];
-    for (uint32_t b = threadIdx.x; b <= nbk; b += SA2_T) h2[(uint64_t)(tbeg + ntile) * (nbk + 1) + b] = (uint16_t)lstart[b];
-    if (threadIdx.x == 0) tb2[tbeg + ntile] = (uint32_t)written;  // u16 slots past reg_off[cp]
+    if (threadIdx.x <= nbk / 8) {  // row f: starts of buckets 8f .. 8f+7; row nbk / 8: the count
+      const uint32_t* ls = lstart + 8 * threadIdx.x;
+      const uint4 v = threadIdx.x < nbk / 8
+                          ? make_uint4(ls[0] | ls[1] << 16, ls[2] | ls[3] << 16, ls[4] | ls[5] << 16, ls[6] | ls[7] << 16)
+                          : make_uint4(total, 0, 0, 0);
+      hp[(uint64_t)threadIdx.x * hp_stride + tbeg + ntile] = v;
+    }
+    if (threadIdx.x == 0) tb2[tbeg + ntile] = (uint32_t)((base + written) / 8);  // the tile's first uint4
 #pragma unroll
     for (int r = 0; r < NV; ++r)
       if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = (uint16_t)pay[r];

@@ -202,20 +202,35 @@ __global__ __launch_bounds__(TA) void bloom_st_apply_kernel(const uint32_t* __re
   }
 }
 
-// Apply for the append pipeline's sa2h tiles (16-bit records, rsk_bloom_sa.h):
-// slice s = bucket rows 8 f .. 8 f + 8 of the transposed headers of every tile
-// of its coarse bin (f = s mod 2^f2).  A quarter-wave takes one tile's
-// segment [beg, end): each of its 16 lanes loads one aligned uint4 (8
-// records; 128 per quarter) and derives the 8 records' sub-buckets (offset
-// bits 16..18) from the 7 inner bucket starts at once: nibble e of S is the
-// number of starts at or below position p0 + e.  SAH_NR rounds of 4 tiles per
-// quarter-set are loaded before any is applied (16 segments per wave).
+// Apply for the append pipeline's sa2h tiles (16-bit records, rsk_bloom_sa.h).
+// Slice s = bucket row f = s mod 2^f2 of coarse bin c = s >> f2; the bin's
+// tiles are contiguous over its parts.  Lane l of a wave fetches tile g + l's
+// row-f uint4 (its 8 bucket starts), the segment end (row f + 1) and the
+// tile's base; then a quarter-wave takes one tile's segment [beg, end): each
+// of its 16 lanes loads one aligned uint4 (8 records; 128 per quarter), two
+// segments per quarter in flight, and derives the 8 records' sub-buckets
+// (offset bits 16..18) from the 7 inner starts at once: nibble e of S counts
+// the starts at or below position p0 + e.  (One segment per lane instead was
+// 2.3x slower: 64 scattered 16-byte loads per instruction.)
 RSK_DEV uint32_t shfl32(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
-template <uint32_t TT, int SAH_NR, int WPE>
-__global__ __launch_bounds__(TT, WPE) void bloom_sah_apply_kernel(const uint16_t* __restrict__ recs,
-                                                             const uint16_t* __restrict__ ht, uint64_t row_stride,
+RSK_DEV void sah_prep(uint32_t p0, uint32_t beg, uint32_t end, const uint32_t* hk, uint32_t& S, uint32_t& vm) {
+  uint32_t sub0 = 0, cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    sub0 += p0 >= hk[k] ? 1u : 0u;
+    const uint32_t d = hk[k] - p0;  // wraps when hk[k] < p0: then >= 8
+    cnt += (d - 1u < 7u) ? 1u << (4 * d) : 0u;
+  }
+  S = (sub0 + cnt) * 0x11111111u;  // nibble e: sub0 + the starts in (p0, p0 + e]
+  const uint32_t lo = beg > p0 ? beg - p0 : 0, hi = end - p0 < 8 ? end - p0 : 8;
+  vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+constexpr int SAH_NR = 2;  // segments per quarter in flight (64 VGPRs at 8 waves per SIMD)
+
+__global__ __launch_bounds__(TA, 8) void bloom_sah_apply_kernel(const uint16_t* __restrict__ recs,
+                                                             const uint4* __restrict__ hp, uint64_t hp_stride,
                                                              uint32_t f2, const uint32_t* __restrict__ tb,
                                                              const uint64_t* __restrict__ reg_off,
                                                              const uint32_t* __restrict__ tile_off,
@@ -225,21 +240,7 @@ __global__ __launch_bounds__(TT, WPE) void bloom_sah_apply_kernel(const uint16_t
   __shared__ __attribute__((aligned(16))) uint32_t sl[SL_WORDS];
   const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t qt = lane >> 4, ql = lane & 15;  // quarter of the wave, lane inside it
-  constexpr uint32_t NW = TT / 64;
-  const uint32_t rs = (uint32_t)row_stride;  // headers < 4 GiB: 32-bit offsets off uniform bases
-  // S (sub-bucket nibbles) and the valid-record mask of the uint4 at p0
-  auto prep = [](uint32_t p0, uint32_t beg, uint32_t end, const uint32_t* hk, uint32_t& S, uint32_t& vm) {
-    uint32_t sub0 = 0, cnt = 0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      sub0 += p0 >= hk[k] ? 1u : 0u;
-      const uint32_t d = hk[k] - p0;  // wraps when hk[k] < p0: then >= 8
-      cnt += (d - 1u < 7u) ? 1u << (4 * d) : 0u;
-    }
-    S = sub0 * 0x11111111u + cnt * 0x11111111u;
-    const uint32_t lo = beg > p0 ? beg - p0 : 0, hi = end - p0 < 8 ? end - p0 : 8;
-    vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-  };
+  constexpr uint32_t NW = TA / 64;
   auto apply8 = [&](const uint4& x, uint32_t S, uint32_t vm) {
     const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -249,80 +250,83 @@ __global__ __launch_bounds__(TT, WPE) void bloom_sah_apply_kernel(const uint16_t
         atomicOr(&sl[off >> 5], bloom_bit_mask(off));
       }
   };
-  for (uint32_t s = blockIdx.x; s < nslices; s += gridDim.x) {
+  for (uint32_t s = xcd_slot(blockIdx.x, gridDim.x); s < nslices; s += gridDim.x) {  // neighbours share segment edges
     const uint64_t w0 = (uint64_t)s * SL_WORDS;
     const uint32_t nw4 = (uint32_t)((nwords - w0 < SL_WORDS ? nwords - w0 : SL_WORDS) / 4);
     uint4* g4 = reinterpret_cast<uint4*>(bits + w0);
     uint4* l4 = reinterpret_cast<uint4*>(sl);
-    for (uint32_t q = threadIdx.x; q < nw4; q += TT) l4[q] = g4[q];
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) l4[q] = g4[q];
     lds_barrier();  // LDS only: the previous slice's write-back stays in flight
     const uint32_t c = s >> f2, f = s & ((1u << f2) - 1);
-    const uint16_t* rows = ht + (uint64_t)(f << SAH_SUB) * row_stride;
-    for (uint32_t pr = 0; pr < P; ++pr) {
-      const uint32_t ta = tile_off[(uint64_t)c * P + pr], te = ta + used[(uint64_t)c * P + pr];
-      const uint4* r4 = reinterpret_cast<const uint4*>(recs + reg_off[(uint64_t)c * P + pr]);  // 16-byte aligned
-      // lane l: tile g + l -- its 9 bucket starts packed in pairs, its base / 8
-      uint32_t nh[5], ntb = 0;
-      auto hload = [&](uint32_t gg) {
-        const uint32_t t = gg + lane;
-        uint32_t v[9];
+    const uint4* hrow = hp + (uint64_t)f * hp_stride;
+    const uint32_t* erow = reinterpret_cast<const uint32_t*>(hp + (uint64_t)(f + 1) * hp_stride);
+    const uint32_t te = tile_off[(uint64_t)c * P + P - 1] + used[(uint64_t)c * P + P - 1];
+    // the bin's records (all parts: contiguous, < 4 GiB) off one uniform base: 32-bit lane offsets
+    const uint32_t base8 = (uint32_t)(reg_off[(uint64_t)c * P] / 8);
+    const char* rb = reinterpret_cast<const char*>(recs) + 16ull * base8;
+    auto rec4 = [&](uint32_t i) { return reinterpret_cast<const uint4*>(rb + 16u * (i - base8)); };
+    // lane l: tile g + l -- its 8 bucket starts (pairs), the segment end, its first uint4
+    uint32_t nh[5], ntb = 0;
+    auto hload = [&](uint32_t gg) {
+      const uint32_t t = gg + lane;
+      const uint4 v = t < te ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(hrow) + 16u * t)
+                             : make_uint4(0, 0, 0, 0);
+      nh[0] = v.x;
+      nh[1] = v.y;
+      nh[2] = v.z;
+      nh[3] = v.w;
+      nh[4] = t < te ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(erow) + 16u * t) & 0xFFFFu : 0;
+      ntb = t < te ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tb) + 4u * t) : 0;
+    };
+    const uint32_t ta = tile_off[(uint64_t)c * P];
+    hload(ta + 64 * w);
+    for (uint32_t g = ta + 64 * w; g < te; g += 64 * NW) {
+      uint32_t h[5];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) v[j] = t < te ? rows[j * rs + t] : 0;
+      for (int j = 0; j < 5; ++j) h[j] = nh[j];
+      const uint32_t tbl = ntb;
+      hload(g + 64 * NW);
+      const uint32_t ng = te - g < 64 ? te - g : 64;
+      for (uint32_t j = 0; j < ng; j += 4 * SAH_NR) {
+        uint4 v[SAH_NR];
+        uint32_t S[SAH_NR], vm[SAH_NR], pe[SAH_NR], tbq[SAH_NR];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) nh[j] = v[2 * j] | (v[2 * j + 1] << 16);
-        nh[4] = v[8];
-        ntb = t < te ? tb[t] >> 3 : 0;
-      };
-      hload(ta + 64 * w);
-      for (uint32_t g = ta + 64 * w; g < te; g += 64 * NW) {
-        uint32_t h[5];
+        for (int rd = 0; rd < SAH_NR; ++rd) {
+          const uint32_t ti = j + 4 * rd + qt, src = ti < 63 ? ti : 63;
+          uint32_t H[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) h[j] = nh[j];
-        const uint32_t tbl = ntb;
-        hload(g + 64ull * NW);
-        const uint32_t ng = (uint32_t)(te - g < 64 ? te - g : 64);
-        for (uint32_t j = 0; j < ng; j += 4 * SAH_NR) {
-          uint4 v[SAH_NR];
-          uint32_t S[SAH_NR], vm[SAH_NR], pe[SAH_NR], tbq[SAH_NR], pq[SAH_NR];
+          for (int k = 0; k < 5; ++k) H[k] = shfl32(h[k], src);
+          tbq[rd] = shfl32(tbl, src);
+          const uint32_t beg = H[0] & 0xFFFFu, end = ti < ng ? H[4] : beg;
+          const uint32_t hk[7] = {H[0] >> 16, H[1] & 0xFFFFu, H[1] >> 16, H[2] & 0xFFFFu,
+                                  H[2] >> 16, H[3] & 0xFFFFu, H[3] >> 16};
+          const uint32_t p0 = (beg & ~7u) + 8 * ql;
+          v[rd] = p0 < end ? ld_nt16(rec4(tbq[rd] + p0 / 8)) : make_uint4(0, 0, 0, 0);
+          pe[rd] = end > p0 + 128 ? end : 0;  // nonzero: a long segment (the rest after this pass)
+          vm[rd] = 0;
+          S[rd] = 0;
+          if (p0 < end) sah_prep(p0, beg, end, hk, S[rd], vm[rd]);
+        }
 #pragma unroll
-          for (int rd = 0; rd < SAH_NR; ++rd) {
-            const uint32_t ti = j + 4 * rd + qt, src = ti < 63 ? ti : 63;
-            uint32_t H[5];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) H[k] = shfl32(h[k], src);
-            tbq[rd] = shfl32(tbl, src);
-            const uint32_t beg = H[0] & 0xFFFFu, end = ti < ng ? H[4] : beg;
-            const uint32_t hk[7] = {H[0] >> 16, H[1] & 0xFFFFu, H[1] >> 16, H[2] & 0xFFFFu,
-                                    H[2] >> 16, H[3] & 0xFFFFu, H[3] >> 16};
-            const uint32_t p0 = (beg & ~7u) + 8 * ql;
-            v[rd] = p0 < end ? ld_nt16(r4 + tbq[rd] + p0 / 8) : make_uint4(0, 0, 0, 0);
-            pe[rd] = end;
-            pq[rd] = p0;
-            vm[rd] = 0;
-            S[rd] = 0;
-            if (p0 < end) prep(p0, beg, end, hk, S[rd], vm[rd]);
-          }
-#pragma unroll
-          for (int rd = 0; rd < SAH_NR; ++rd) {
-            apply8(v[rd], S[rd], vm[rd]);
-            if (pq[rd] + 128 < pe[rd]) {  // segments longer than 128 records (rare): headers again
-              const uint32_t t = g + j + 4 * rd + qt;
-              uint32_t hk[7];
-#pragma unroll
-              for (int k = 0; k < 7; ++k) hk[k] = rows[(k + 1) * rs + t];
-              const uint32_t beg = rows[t];
-              for (uint32_t p0 = pq[rd] + 128; p0 < pe[rd]; p0 += 128) {
-                uint32_t S2, vm2;
-                prep(p0, beg, pe[rd], hk, S2, vm2);
-                apply8(r4[tbq[rd] + p0 / 8], S2, vm2);
-              }
+        for (int rd = 0; rd < SAH_NR; ++rd) {
+          apply8(v[rd], S[rd], vm[rd]);
+          if (pe[rd]) {  // segments longer than 128 records (rare): starts again
+            const uint32_t t = g + j + 4 * rd + qt;
+            const uint4 hv = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(hrow) + 16u * t);
+            const uint32_t hk[7] = {hv.x >> 16, hv.y & 0xFFFFu, hv.y >> 16, hv.z & 0xFFFFu,
+                                    hv.z >> 16, hv.w & 0xFFFFu, hv.w >> 16};
+            const uint32_t beg = hv.x & 0xFFFFu;
+            for (uint32_t p0 = (beg & ~7u) + 8 * ql + 128; p0 < pe[rd]; p0 += 128) {
+              uint32_t S2, vm2;
+              sah_prep(p0, beg, pe[rd], hk, S2, vm2);
+              apply8(*rec4(tbq[rd] + p0 / 8), S2, vm2);
             }
           }
         }
       }
     }
     lds_barrier();
-    for (uint32_t q = threadIdx.x; q < nw4; q += TT) g4[q] = l4[q];
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) g4[q] = l4[q];
     lds_barrier();
   }
 }
@@ -391,11 +395,11 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   const uint32_t nbk = nb2 << SAH_SUB;  // sa2h buckets per coarse bin
   const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / SA2_SLOTS + (uint64_t)W * nb1 + 64;  // bound on sa2 tiles
   const uint64_t l2_slots = max_np + 3ull * nb1 * max_nst + 8 * tt_max + 8ull * ncp;  // sa2h output (u16), aligned tiles
-  const uint64_t h2_bytes = al(tt_max * (nbk + 1) * 2);
-  // apply's 32-bit offsets: header elements, u16 slots of one (bin, part)
-  if (tt_max * (nbk + 1) >= (1ull << 31) || 2ull * W * quota >= (1ull << 32)) return false;
+  const uint64_t hp_bytes = al(16 * tt_max * (nb2 + 1));  // bucket-start rows: nb2 + 1 rows of tt_max uint4
+  // apply's 32-bit uint4 indices of the records
+  if (l2_slots / 8 >= (1ull << 32)) return false;
   const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256;
-  const uint64_t bytes = al(4 * region_probes) + al(2 * l2_slots) + 2 * h2_bytes + al(8 * tt_max) + meta;
+  const uint64_t bytes = al(4 * region_probes) + al(2 * l2_slots) + hp_bytes + al(4 * tt_max) + meta;
   uint8_t* w = c->work(bytes);
   uint8_t* q = w;
   auto take = [&](uint64_t n) {
@@ -405,9 +409,8 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   };
   uint32_t* region = reinterpret_cast<uint32_t*>(take(al(4 * region_probes)));
   uint16_t* l2 = reinterpret_cast<uint16_t*>(take(al(2 * l2_slots)));
-  uint16_t* h2 = reinterpret_cast<uint16_t*>(take(h2_bytes));
-  uint16_t* h2t = reinterpret_cast<uint16_t*>(take(h2_bytes));
-  uint32_t* tb2 = reinterpret_cast<uint32_t*>(take(al(8 * tt_max)));
+  uint4* hp = reinterpret_cast<uint4*>(take(hp_bytes));
+  uint32_t* tb2 = reinterpret_cast<uint32_t*>(take(al(4 * tt_max)));
   uint64_t* tot = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
   uint64_t* reg_off = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
   uint32_t* bud = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
@@ -451,30 +454,15 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     {
       ProfScope ps(c, "bloom_st2");
       hipLaunchKernelGGL(bloom_sa2h_kernel, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P,
-                         nbk, reg_off, tile_off, tiles, l2, h2, tb2);
+                         nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2);
       RSK_CHECK_LAUNCH("bloom_sa2");
     }
     {
-      ProfScope ps(c, "bloom_st_mid");
-      hipLaunchKernelGGL(st_transpose_kernel, dim3((uint32_t)((tt_max + 63) / 64), (nbk + 1 + 63) / 64), dim3(256), 0,
-                         c->stream, h2, tt_max, nbk + 1, h2t);
-      RSK_CHECK_LAUNCH("bloom_st_transpose2");
-    }
-    {
       ProfScope ps(c, "bloom_st_apply");
-      // 64 KiB of LDS -> 2 workgroups per CU; 1024 lanes at 8 waves per SIMD
-      // (<= 64 VGPRs, 2 segments per quarter in flight) or 512 at 4 (<= 128, 4)
+      // __launch_bounds__(TA, 8): <= 64 VGPRs, 64 KiB of LDS -> 2 workgroups per CU
       const uint32_t ga = std::min<uint32_t>(ns, 2 * cus);
-#define RSK_SAH(T, NR, WPE)                                                                                    \
-  hipLaunchKernelGGL((bloom_sah_apply_kernel<T, NR, WPE>), dim3(ga), dim3(T), 0, c->stream, l2, h2t, tt_max, f2, \
-                     tb2, reg_off, tile_off, tiles, P, ns, b->d_bits, b->nwords)
-      switch (c->tune.sah_apply) {
-        case 1: RSK_SAH(1024, 2, 8); break;
-        case 2: RSK_SAH(512, 4, 4); break;
-        case 3: RSK_SAH(512, 6, 4); break;
-        default: RSK_SAH(1024, 2, 8); break;
-      }
-#undef RSK_SAH
+      hipLaunchKernelGGL(bloom_sah_apply_kernel, dim3(ga), dim3(TA), 0, c->stream, l2, hp, tt_max, f2, tb2, reg_off,
+                         tile_off, tiles, P, ns, b->d_bits, b->nwords);
       RSK_CHECK_LAUNCH("bloom_st_apply");
     }
     uint32_t ov = 0;

@@ -42,6 +42,14 @@ RSK_DEV uint4 ld_nt16(const void* p) {
   u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// XCD-aware work order: blocks b and b + 8 share an XCD (its L2), so a
+// persistent grid (a multiple of 8 blocks) that walks items in rounds of
+// gridDim.x gives XCD b % 8 the consecutive slots [(b % 8) n, (b % 8 + 1) n),
+// n = gridDim.x / 8: neighbouring items, which share boundary cache lines or
+// whole inputs, are then fetched into one L2.  Placement is a speed hint only.
+RSK_DEV uint32_t xcd_slot(uint32_t b, uint32_t grid) {
+  return (grid & 7u) ? b : (b & 7u) * (grid >> 3) + (b >> 3);
+}
 RSK_DEV uint64_t rotr(uint64_t v, int s) { return (v >> s) | (v << (64 - s)); }
 RSK_DEV uint64_t rotl(uint64_t v, int s) { return (v << s) | (v >> (64 - s)); }
 

@@ -160,7 +160,8 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
                                                           const double* __restrict__ lc) {
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
   __shared__ SumD part[GP_T / 64];
-  for (uint32_t w = blockIdx.x; w < GP_NP * nfine; w += gridDim.x) {
+  // the GP_NP parts of a fine bin read the same records: one XCD (one L2) for both
+  for (uint32_t w = xcd_slot(blockIdx.x, gridDim.x); w < GP_NP * nfine; w += gridDim.x) {
     const uint32_t s = w / GP_NP, half = w % GP_NP;
     const uint32_t a = off2[(uint64_t)s * G1], e0 = off2[(uint64_t)(s + 1) * G1];
     const uint32_t e = e0 - a > GP_CH ? a + GP_CH : e0;  // the rest: hll_gapply_extra

@@ -52,7 +52,6 @@ struct Tuning {
   int reply = 0;             // add() replies: 0 auto, 1 first-key pipeline at any size, -1 the sort path
   uint64_t reply_chunk = 0;  // probes per chunk of the first-key pipeline (0: 2^33)
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
-  int sah_apply = 0;         // insert apply kernel shape (rsk_bloom_st.hip): 0 default, 1..3 variants
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the

@@ -7,6 +7,8 @@
 #     bench  : bench.py (C2 headline + node Bloom + CPU baselines)
 #     c4|c5|c5z : the other workloads
 #     prof   : rocprofv3 kernel trace of the headline bench + PMC passes
+#     insprof: the C3 insert under rocprofv3 (trace, FETCH, WRITE, SQ passes)
+#     routes : scripts/insert_routes.py over the given route specs
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -32,8 +34,19 @@ for p in ${PART//,/ }; do
       step bench_c5 200 python bench.py --workload c5 || exit 1 ;;
     c5z)
       step bench_c5_zipf 200 python bench.py --workload c5 --zipf 1.1 || exit 1 ;;
+    routes)
+      step routes 600 python -u scripts/insert_routes.py gpurun_out/ins_routes.json "$@" || exit 1 ;;
     c5prof)
       step c5prof 300 python scripts/c5_host_profile.py 500000000 1000000 10 || exit 1 ;;
+    insprof)  # the reply-less C3 insert alone: kernel trace, then one PMC pass per counter group
+      I="python3 scripts/insert_routes.py gpurun_out/ins_prof.json default"
+      export ROUNDS=1
+      rm -rf gpurun_out/ins_stats gpurun_out/ins_fetch gpurun_out/ins_write gpurun_out/ins_sq
+      step ins_stats 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ins_stats -o run -- $I || exit 1
+      step ins_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/ins_fetch -o run -- $I || exit 1
+      step ins_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/ins_write -o run -- $I || exit 1
+      step ins_sq 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/ins_sq -o run -- $I || exit 1
+      unset ROUNDS ;;
     prof)
       B="python3 bench.py --no-cpu --no-bloom-replies"
       rm -rf gpurun_out/prof_stats
