@@ -419,21 +419,29 @@ def main():
         remote = np.concatenate([cw[:, 1], ms_])
         kern, unit_bytes = "hll_add_grouped16", 20.0 * n
         bufs = [groups, gkeys]
-        counts_out = np.empty(max(G, own_count), np.uint64)  # the caller's reply buffer, reused across steps
+        counts_out = np.empty(max(G, own_count), np.uint64)  # the caller's reply buffers, reused across steps
+        cw_out = np.empty(args.batch_ops, np.uint64)
 
     def step():
         if wl == "c5":
+            # One pipelined batch per step (the async calls, ordered on the
+            # context stream; RBatch-style): the host work of each call
+            # overlaps the GPU work queued before it, one wait at the end.
             pool.clear()  # every step builds the G sketches from empty (fresh PFADDs, not idempotent re-adds)
-            pool.add(kb, groups)
             if world > 1:
+                pool.add(kb, groups)
                 assert shard.hll_reducescatter_pool(pool.pool) == (own_first, own_count)  # RCCL MAX
-                c = pool.count(own_ids, out=counts_out)
+                ops = [pool.count_async(counts_out, own_ids)]
+                ops[0].wait()
                 shard.hll_fetch_rows(pool.pool, remote)  # partner / source rows from their owners
+                ops = []
             else:
-                c = pool.count(out=counts_out)
-            pool.countWith(cw)
-            pool.mergeWith(md, ms_)
-            return int(c[0])
+                ops = [pool.add_async(kb, groups), pool.count_async(counts_out)]
+            ops.append(pool.countWith_async(cw, cw_out))
+            ops.append(pool.mergeWith_async(md, ms_))
+            for op in ops:
+                op.wait()
+            return int(counts_out[0])
         hll.addAll(kb)
         if world > 1:
             slot = client._hll_slot("bench", False)
@@ -486,7 +494,8 @@ def main():
         "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
         "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
         "c5": "Grouped HLL: %d sketches cleared each step, grouped add + count(all) + %d countWith + %d mergeWith "
-              "(BASELINE configs[4]); N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
+              "(BASELINE configs[4]), issued as one pipelined batch per step (the library's async calls, one wait); "
+              "N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
               "own 1/N of the sketches and running countWith/mergeWith led by them against partners from "
               "all G, fetched from their owners over RCCL" % (args.groups, args.batch_ops, args.batch_ops),
     }

@@ -178,6 +178,15 @@ int rsk_hll_merge_async(rsk_hll *dst, uint64_t dst_id, rsk_hll *const *srcs, con
                         rsk_done_fn cb, void *user);
 int rsk_hll_merge_batch_async(rsk_hll *h, const uint64_t *dst_ids, const uint64_t *src_ids, uint64_t n,
                               rsk_done_fn cb, void *user);
+/* Pool forms (a pipelined batch of the grouped calls above): grouped PFADD
+ * (value n), PFCOUNT of ids (NULL: sketches 0..n-1) and batched countWith
+ * into out (value n).  out is written before cb fires; keep it alive until
+ * then.  Members of a countWith are taken as they stand at that point of the
+ * call order, exactly like the synchronous call issued there. */
+int rsk_hll_add_grouped_async(rsk_hll *h, const rsk_keys *keys, const uint32_t *groups, rsk_done_fn cb, void *user);
+int rsk_hll_count_ids_async(rsk_hll *h, const uint64_t *ids, uint64_t n, uint64_t *out, rsk_done_fn cb, void *user);
+int rsk_hll_count_union_batch_async(rsk_hll *h, const uint64_t *member_ids, uint32_t arity, uint64_t n,
+                                    uint64_t *out, rsk_done_fn cb, void *user);
 
 /* PFMERGE from raw registers (one byte per register, any location): the
  * receive side of the multi-GPU RCCL MAX merge. */

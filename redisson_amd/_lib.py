@@ -118,6 +118,9 @@ SIGNATURES = {
     "rsk_hll_count_union_async": (ctypes.c_int, [_vp, _vp, _u32, DONE_FN, _vp]),
     "rsk_hll_merge_async": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u32, DONE_FN, _vp]),
     "rsk_hll_merge_batch_async": (ctypes.c_int, [_vp, _vp, _vp, _u64, DONE_FN, _vp]),
+    "rsk_hll_add_grouped_async": (ctypes.c_int, [_vp, _P(rsk_keys), _vp, DONE_FN, _vp]),
+    "rsk_hll_count_ids_async": (ctypes.c_int, [_vp, _vp, _u64, _vp, DONE_FN, _vp]),
+    "rsk_hll_count_union_batch_async": (ctypes.c_int, [_vp, _vp, _u32, _u64, _vp, DONE_FN, _vp]),
     "rsk_hll_get_registers": (ctypes.c_int, [_vp, _u64, _vp, _u32]),
     "rsk_hll_device_registers": (_vp, [_vp]),
     "rsk_hll_export_redis": (ctypes.c_int, [_vp, _u64, _vp, _sz, _P(_sz)]),
@@ -250,6 +253,40 @@ def check(rc: int, what: str = ""):
         msg = load().rsk_last_error().decode(errors="replace")
         exc = _STATUS_EXC.get(rc, EngineError)
         raise exc(msg if not what else "%s: %s" % (what, msg))
+
+
+class NativeOp:
+    """One asynchronous library call (rsk_*_async): `fn` is the completion
+    callback to pass, `wait()` blocks until it fired and returns its value.
+    Objects in `keep` (input and output buffers) stay referenced until then."""
+
+    def __init__(self, *keep):
+        self._ev = threading.Event()
+        self.status = None
+        self.value = None
+        self._keep = keep
+
+        def done(user, status, value):
+            self.status = status
+            self.value = value
+            self._ev.set()
+
+        self.fn = DONE_FN(done)
+
+    def issued(self, rc: int, what: str = "async call"):
+        """The call's own status: on failure the callback never fires."""
+        if rc != RSK_OK:
+            self._keep = None
+            check(rc, what)
+        return self
+
+    def wait(self, timeout=None):
+        if not self._ev.wait(timeout):
+            raise TimeoutError("asynchronous call did not complete")
+        self._keep = None
+        if self.status != RSK_OK:
+            raise EngineError("asynchronous call failed with status %d" % self.status)
+        return self.value
 
 
 class Engine:

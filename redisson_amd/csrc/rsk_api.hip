@@ -766,6 +766,51 @@ int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out
   });
 }
 
+}  // extern "C"
+
+namespace {
+// Grouped PFADD in pieces: the host marks the touched sketches (host group
+// ids; device ids mark the whole pool), each chunk is launched, then every
+// cache of the pool is invalidated.  A pending lazy clear is completed by the
+// partitioned add's first launch (every row written); any other path zeroes
+// the pool first.
+void hll_mark_groups(rsk_hll* h, const uint32_t* groups, uint64_t n) {
+  if (!groups) {
+    std::fill(h->exists.begin(), h->exists.end(), 1);
+    return;
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (groups[i] < h->n) h->exists[groups[i]] = 1;
+}
+// pool_zero: the pool was all zero when the call began (first chunk only).
+void hll_add_grouped_chunk(rsk_hll* h, const DevKeys& dk, const uint32_t* d_groups, bool pool_zero) {
+  rsk_ctx* c = h->ctx;
+  const bool write_all = h->pending_clear && hll_grouped_partition_applies(c, dk, h->n);
+  if (!write_all) hll_materialize(h);
+  hll_touch(h);  // estimates of earlier chunks are stale once this one lands
+  hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero, write_all,
+                         PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
+  h->pending_clear = false;
+}
+void hll_add_grouped_finish(rsk_hll* h) {
+  // Every pool member may have changed: invalidate all caches (card |= bit 63).
+  hipLaunchKernelGGL(invalidate_all_kernel, dim3(256), dim3(256), 0, h->ctx->stream, h->d_card, h->n);
+  RSK_CHECK_LAUNCH("invalidate_all");
+}
+// Device keys (any size) in one piece; host_groups (the caller's ids, when
+// they are on the host) mark the sketches touched.
+void hll_add_grouped_enqueue(rsk_hll* h, const DevKeys& dk, const uint32_t* d_groups, const uint32_t* host_groups) {
+  hll_forget_imports(h);
+  const bool pool_zero = h->zero;
+  hll_touch(h);
+  hll_mark_groups(h, host_groups, dk.n);
+  hll_add_grouped_chunk(h, dk, d_groups, pool_zero);
+  hll_add_grouped_finish(h);
+}
+}  // namespace
+
+extern "C" {
+
 int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups) {
   return guarded([&] {
     need(h != nullptr, "hll handle is NULL");
@@ -774,39 +819,24 @@ int rsk_hll_add_grouped(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups
     CtxLock l(c);
     check_keys(c, keys);
     if (keys->n == 0) return;
-    hll_forget_imports(h);
     check_out(c, keys, groups);
-    const bool pool_zero = h->zero;
-    hll_touch(h);
-    uint32_t* d_groups = nullptr;
-    if (keys->location == RSK_MEM_HOST) {
-      for (uint64_t i = 0; i < keys->n; ++i)
-        if (groups[i] < h->n) h->exists[groups[i]] = 1;
-    }
-    for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
-      if (keys->location == RSK_MEM_DEVICE) {
-        d_groups = const_cast<uint32_t*>(groups);
-      } else {
-        d_groups = reinterpret_cast<uint32_t*>(out_scratch(c, cnt * 4));
+    const bool host = keys->location == RSK_MEM_HOST;
+    if (!host) {
+      hll_add_grouped_enqueue(h, DevKeys{reinterpret_cast<const uint8_t*>(keys->data), keys->offsets, keys->n,
+                                         keys->fixed_len},
+                              groups, nullptr);
+    } else {  // staged in chunks
+      hll_forget_imports(h);
+      const bool pool_zero = h->zero;
+      hll_touch(h);
+      hll_mark_groups(h, groups, keys->n);
+      for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t first, uint64_t cnt) {
+        auto* d_groups = reinterpret_cast<uint32_t*>(out_scratch(c, cnt * 4));
         RSK_HIP(hipMemcpyAsync(d_groups, groups + first, cnt * 4, hipMemcpyHostToDevice, c->stream));
-      }
-      // A pending lazy clear is completed by the partitioned add's first
-      // launch (every row written); any other path zeroes the pool first.
-      const bool write_all = h->pending_clear && hll_grouped_partition_applies(c, dk, h->n);
-      if (!write_all) hll_materialize(h);
-      hll_touch(h);  // estimates of earlier chunks are stale once this one lands
-      hll_add_grouped_launch(c, dk, d_groups, h->d_regs, h->n, pool_zero && first == 0, write_all,
-                             PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
-      h->pending_clear = false;
-    });
-    if (keys->location == RSK_MEM_DEVICE) {
-      // Group ids stay on the device: every sketch of the pool is treated as
-      // materialised (a pool-wide PFADD target), and every cache invalidated.
-      std::fill(h->exists.begin(), h->exists.end(), 1);
+        hll_add_grouped_chunk(h, dk, d_groups, pool_zero && first == 0);
+      });
+      hll_add_grouped_finish(h);
     }
-    // Every pool member may have changed: invalidate all caches (card |= bit 63).
-    hipLaunchKernelGGL(invalidate_all_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card, h->n);
-    RSK_CHECK_LAUNCH("invalidate_all");
     RSK_HIP(hipStreamSynchronize(c->stream));
   });
 }
@@ -1404,8 +1434,8 @@ void op_complete(void* p) {
     case K_HLL_FLAG:
       v = ((uint32_t)op->h_res[0] == op->epoch || op->created) ? 1 : 0;
       break;
-    case K_OUT_BYTES:
-      if (op->user_out && op->n_out) std::memcpy(op->user_out, op->h_out, op->n_out);
+    case K_OUT_BYTES:  // large outputs (a pool's counts: 8 MB at 10^6 sketches) on host threads
+      if (op->user_out && op->n_out) par_copy(op->user_out, op->h_out, op->n_out, op->c->stage_threads);
       break;
     default:
       break;
@@ -1678,6 +1708,120 @@ int rsk_hll_merge_batch_async(rsk_hll* h, const uint64_t* dst_ids, const uint64_
     AsyncOp* op = op_get(c, n ? merge_batch_host_bytes(n) : 0, n ? merge_batch_dev_bytes(n) : 0);
     try {
       if (n) merge_batch_enqueue(h, dst_ids, src_ids, n, op->h_buf, op->d_buf);
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+int rsk_hll_add_grouped_async(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups, rsk_done_fn cb,
+                              void* user) {
+  if (h && keys && keys->location == RSK_MEM_HOST && keys->n) {
+    uint64_t kb = 0;
+    int rc = guarded([&] { kb = host_key_bytes(keys) + 4 * keys->n; });
+    if (rc != RSK_OK) return rc;
+    if (kb > ASYNC_STAGE_MAX) return run_now([&](uint64_t*) { return rsk_hll_add_grouped(h, keys, groups); }, cb, user, 0, false);
+  }
+  return guarded([&] {
+    need(h != nullptr, "hll handle is NULL");
+    need(keys == nullptr || keys->n == 0 || groups != nullptr, "groups is NULL");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    check_keys(c, keys);
+    check_out(c, keys, groups);
+    const bool host = keys->location == RSK_MEM_HOST;
+    const uint64_t kb = host ? al256(host_key_bytes(keys)) : 0;
+    const uint64_t gb = host ? al256(4 * keys->n) : 0;
+    AsyncOp* op = op_get(c, kb + gb, kb + gb);
+    try {
+      if (keys->n) {
+        const DevKeys dk = stage_keys(c, keys, op, 0);
+        const uint32_t* d_groups = groups;
+        if (host) {
+          std::memcpy(op->h_buf + kb, groups, 4 * keys->n);
+          RSK_HIP(hipMemcpyAsync(op->d_buf + kb, op->h_buf + kb, 4 * keys->n, hipMemcpyHostToDevice, c->stream));
+          d_groups = reinterpret_cast<const uint32_t*>(op->d_buf + kb);
+        }
+        hll_add_grouped_enqueue(h, dk, d_groups, host ? groups : nullptr);
+      }
+      op->value = keys->n;
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+int rsk_hll_count_ids_async(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out, rsk_done_fn cb, void* user) {
+  return guarded([&] {
+    need(h != nullptr && out != nullptr, "NULL argument");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    if (ids) check_hll_ids(h, ids, n);
+    else need(n <= h->n, "n exceeds pool size");
+    const uint64_t ib = ids ? al256(8 * n) : 0, ob = al256(8 * n);
+    AsyncOp* op = op_get(c, ib + ob, ib + ob);
+    try {
+      hll_materialize(h);
+      if (n) {
+        uint64_t* d_ids = nullptr;
+        if (ids) {
+          std::memcpy(op->h_buf, ids, 8 * n);
+          RSK_HIP(hipMemcpyAsync(op->d_buf, op->h_buf, 8 * n, hipMemcpyHostToDevice, c->stream));
+          d_ids = reinterpret_cast<uint64_t*>(op->d_buf);
+        }
+        auto* d_out = reinterpret_cast<uint64_t*>(op->d_buf + ib);
+        hll_count_launch(c, h->d_regs, h->d_card, d_ids, SmallIds{}, n, d_out,
+                         PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
+        RSK_HIP(hipMemcpyAsync(op->h_buf + ib, d_out, 8 * n, hipMemcpyDeviceToHost, c->stream));
+        op->h_out = op->h_buf + ib;
+        op->user_out = reinterpret_cast<uint8_t*>(out);
+        op->n_out = 8 * n;
+      }
+      op->kind = K_OUT_BYTES;
+      op->value = n;
+      op_submit(op, cb, user);
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      op_release(op);
+      throw;
+    }
+  });
+}
+
+int rsk_hll_count_union_batch_async(rsk_hll* h, const uint64_t* member_ids, uint32_t arity, uint64_t n,
+                                    uint64_t* out, rsk_done_fn cb, void* user) {
+  return guarded([&] {
+    need(h && member_ids && out && arity >= 1, "bad arguments");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    check_hll_ids(h, member_ids, n * arity);
+    const uint64_t pb = al256(8 * n * arity), ob = al256(8 * n);
+    AsyncOp* op = op_get(c, pb + ob, pb + ob);
+    try {
+      if (n) {
+        auto* ptrs = reinterpret_cast<const uint8_t**>(op->h_buf);
+        const uint8_t* e = h->exists.data();
+        for (uint64_t i = 0; i < n * arity; ++i) {  // members as they stand at this point of the call order
+          const uint64_t id = member_ids[i];
+          ptrs[i] = e[id] ? regs_of(h, id) : nullptr;
+        }
+        auto* d_ptrs = reinterpret_cast<const uint8_t**>(op->d_buf);
+        auto* d_out = reinterpret_cast<uint64_t*>(op->d_buf + pb);
+        RSK_HIP(hipMemcpyAsync(d_ptrs, ptrs, 8 * n * arity, hipMemcpyHostToDevice, c->stream));
+        hll_union_count_launch(c, d_ptrs, arity, n, d_out);
+        RSK_HIP(hipMemcpyAsync(op->h_buf + pb, d_out, 8 * n, hipMemcpyDeviceToHost, c->stream));
+        op->h_out = op->h_buf + pb;
+        op->user_out = reinterpret_cast<uint8_t*>(out);
+        op->n_out = 8 * n;
+      }
+      op->kind = K_OUT_BYTES;
+      op->value = n;
       op_submit(op, cb, user);
     } catch (...) {
       (void)hipStreamSynchronize(c->stream);

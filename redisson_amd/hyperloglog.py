@@ -205,3 +205,46 @@ class GroupedHyperLogLog:
         out = np.zeros(_lib.HLL_REGISTERS, dtype=np.uint8)
         _lib.check(_lib.load().rsk_hll_get_registers(self.pool, gid, out.ctypes.data, _lib.RSK_MEM_HOST))
         return out
+
+    # -- pipelined forms (the library's async calls, ordered on the context
+    # stream like the synchronous ones; each returns a NativeOp to wait on)
+    def add_async(self, keys: KeyBatch, groups) -> "_lib.NativeOp":
+        if hasattr(groups, "ptr"):
+            gp = groups.ptr
+        else:
+            groups = np.ascontiguousarray(groups, np.uint32)
+            gp = groups.ctypes.data
+        ks = keys.as_struct()
+        op = _lib.NativeOp(keys, groups, ks)
+        return op.issued(_lib.load().rsk_hll_add_grouped_async(self.pool, ctypes.byref(ks), gp, op.fn, None), "PFADD")
+
+    def count_async(self, out: np.ndarray, ids=None) -> "_lib.NativeOp":
+        """PFCOUNT of every sketch (ids None) or of ids into `out` (uint64),
+        written when the op completes."""
+        n = self.n if ids is None else len(ids)
+        if out.dtype != np.uint64 or out.size < n or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint64 array of at least %d entries" % n)
+        idp = None
+        if ids is not None:
+            ids = np.ascontiguousarray(ids, dtype=np.uint64)
+            idp = ids.ctypes.data
+        op = _lib.NativeOp(out, ids)
+        return op.issued(_lib.load().rsk_hll_count_ids_async(self.pool, idp, n, out.ctypes.data, op.fn, None),
+                         "PFCOUNT")
+
+    def countWith_async(self, member_ids, out: np.ndarray) -> "_lib.NativeOp":
+        m = np.ascontiguousarray(member_ids, dtype=np.uint64)
+        if m.ndim != 2:
+            raise ValueError("member_ids must be [n, arity]")
+        if out.dtype != np.uint64 or out.size < m.shape[0] or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint64 array of at least %d entries" % m.shape[0])
+        op = _lib.NativeOp(m, out)
+        return op.issued(_lib.load().rsk_hll_count_union_batch_async(self.pool, m.ctypes.data, m.shape[1], m.shape[0],
+                                                                     out.ctypes.data, op.fn, None), "PFCOUNT")
+
+    def mergeWith_async(self, dst_ids, src_ids) -> "_lib.NativeOp":
+        d = np.ascontiguousarray(dst_ids, dtype=np.uint64)
+        s = np.ascontiguousarray(src_ids, dtype=np.uint64)
+        op = _lib.NativeOp(d, s)
+        return op.issued(_lib.load().rsk_hll_merge_batch_async(self.pool, d.ctypes.data, s.ctypes.data, d.size, op.fn,
+                                                               None), "PFMERGE")

@@ -259,3 +259,49 @@ def test_import_returns_set_bytes_until_written(L, engine, orc):
     _lib.check(L.rsk_hll_export_redis(h, 0, buf, 12304, ctypes.byref(n)))
     assert bytes(buf[16: n.value]) != s[16:]  # re-encoded after the write
     L.rsk_hll_destroy(h)
+
+
+def test_grouped_pipeline_matches_sync(engine):
+    """The pool's async forms (rsk_hll_add_grouped_async, rsk_hll_count_ids_async,
+    rsk_hll_count_union_batch_async, rsk_hll_merge_batch_async), issued back to
+    back, give what the synchronous calls give in the same order."""
+    from redisson_amd import KeyBatch, devmem
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    G, n = 5000, 1 << 22
+    groups, gkeys = devmem.gen_grouped(engine, 0x5EED0107, G, 0, n)
+    kb = gkeys.keys_fixed(n, 16)
+    rng = np.random.default_rng(3)
+    cw = np.stack([rng.integers(0, G, 2000, dtype=np.uint64), rng.integers(0, G, 2000, dtype=np.uint64)], 1)
+    md = rng.integers(0, G, 2000, dtype=np.uint64)
+    ms = rng.integers(0, G, 2000, dtype=np.uint64)
+    hkeys = np.frombuffer(rng.bytes(16 * 3000), np.uint8).reshape(3000, 16).copy()
+    hg = rng.integers(0, G, 3000, dtype=np.uint32)
+    ref, got = GroupedHyperLogLog(engine, G), GroupedHyperLogLog(engine, G)
+    try:
+        ref.add(kb, groups)
+        c_ref = ref.count().copy()
+        w_ref = ref.countWith(cw)
+        ref.mergeWith(md, ms)
+        ref.add(KeyBatch.from_numpy(hkeys), hg)
+        c2_ref = ref.count().copy()
+        for _ in range(2):  # twice: the second round starts from a cleared pool
+            got.clear()
+            c_out, w_out, c2_out = np.zeros(G, np.uint64), np.zeros(len(cw), np.uint64), np.zeros(G, np.uint64)
+            hk = hkeys.copy()
+            ops = [got.add_async(kb, groups), got.count_async(c_out), got.countWith_async(cw, w_out),
+                   got.mergeWith_async(md, ms), got.add_async(KeyBatch.from_numpy(hk), hg), got.count_async(c2_out)]
+            hk[:] = 0  # host keys were staged by the call
+            assert ops[0].wait(60) == n
+            for op in ops[1:]:
+                op.wait(60)
+            assert np.array_equal(c_out, c_ref)
+            assert np.array_equal(w_out, w_ref)
+            assert np.array_equal(c2_out, c2_ref)
+        ids = np.array([7, 0, G - 1, 7], np.uint64)
+        sub = np.zeros(4, np.uint64)
+        got.count_async(sub, ids).wait(60)
+        assert np.array_equal(sub, c2_ref[ids.astype(np.int64)])
+    finally:
+        ref.close()
+        got.close()
