@@ -4,6 +4,8 @@
 //   mode 1: random 4 B gathers over the buffer            -> gathers/s
 //   mode 2: random 4 B atomicOr over the buffer           -> atomics/s
 //   mode 3: streaming copy (read + write halves)          -> GB/s (read+write)
+//   mode 4: streaming write (16 B/lane plain stores)       -> GB/s
+//   mode 5: streaming write (16 B/lane nontemporal stores) -> GB/s
 // Indices come from splitmix64(i), as uniform as the Bloom probe stream.
 // Also: the route overrides of a context (rsk_diag_set_route) and the timed
 // launches of the kernels' tuning variants (rsk_diag_kernels.hip).
@@ -26,6 +28,19 @@ __global__ __launch_bounds__(256) void diag_stream_read(const uint4* __restrict_
 __global__ __launch_bounds__(256) void diag_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = ld_nt16(src + i);
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void diag_stream_write(uint4* __restrict__ p, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = (uint32_t)i;
+    if (NT) {
+      u32x4 x = {v, v, v, v};
+      __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p + i));
+    } else {
+      p[i] = make_uint4(v, v, v, v);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void diag_gather(const uint32_t* __restrict__ w, uint64_t nwords, uint64_t nops,
@@ -117,7 +132,7 @@ int rsk_diag_bloom_contains_variant(rsk_ctx* c, int variant, rsk_bloom* bf, cons
 
 int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t nops, double* ms) {
   return diag::guarded([&] {
-    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 3, "bad arguments");
+    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 5, "bad arguments");
     diag::Lock l(c);
     uint32_t* sink = reinterpret_cast<uint32_t*>(c->d_small + 512);
     const uint32_t grid = (uint32_t)c->num_cus * 8;
@@ -134,6 +149,14 @@ int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t 
         case 2:
           hipLaunchKernelGGL(diag_atomic_or, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<uint32_t*>(buf),
                              bytes / 4, nops);
+          break;
+        case 4:
+          hipLaunchKernelGGL(diag_stream_write<false>, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<uint4*>(buf),
+                             bytes / 16);
+          break;
+        case 5:
+          hipLaunchKernelGGL(diag_stream_write<true>, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<uint4*>(buf),
+                             bytes / 16);
           break;
         default: {
           const uint64_t half = bytes / 32;  // uint4 elements per half
