@@ -359,6 +359,10 @@ def main():
     from redisson_amd import _lib as _early
 
     _early.load()
+    # The bench support library (generators) too: loaded after torch, its HIP
+    # calls bound to a runtime rocprofv3 had not hooked (a launch through a
+    # null dispatch entry under --kernel-trace).
+    _early.diag()
     import torch
     import torch.distributed as dist
 

@@ -25,6 +25,25 @@ __global__ __launch_bounds__(256) void diag_stream_read(const uint4* __restrict_
   if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the loads alive
 }
 
+// FETCH_SIZE calibration for segment reads (the Bloom apply passes): groups
+// of L lanes each load one 16 L-byte segment (one uint4 per lane), segments
+// visited in a scattered order (index times an odd constant, mod a power of
+// two), every byte of the buffer read exactly once.
+template <int L>
+__global__ __launch_bounds__(256) void diag_segment_read(const uint4* __restrict__ p, uint64_t nseg_log,
+                                                         uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  const uint64_t nseg = 1ull << nseg_log, mask = nseg - 1;
+  const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / L, lane = threadIdx.x % L;
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x / L;
+  for (uint64_t g = g0; g < nseg; g += gs) {
+    const uint64_t s = (g * 0x9E3779B97F4A7C15ull) & mask;
+    const uint4 v = ld_nt16(p + s * L + lane);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 __global__ __launch_bounds__(256) void diag_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = ld_nt16(src + i);
@@ -132,7 +151,13 @@ int rsk_diag_bloom_contains_variant(rsk_ctx* c, int variant, rsk_bloom* bf, cons
 
 int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t nops, double* ms) {
   return diag::guarded([&] {
-    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 5, "bad arguments");
+    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 6, "bad arguments");
+    // mode 6: segment reads of nops bytes (256, 512 or 1024) over the largest
+    // power-of-two number of segments that fits
+    diag::need(mode != 6 || nops == 256 || nops == 512 || nops == 1024, "segment bytes must be 256, 512 or 1024");
+    uint64_t nseg_log = 0;
+    if (mode == 6)
+      while ((2ull << nseg_log) * nops <= bytes) ++nseg_log;
     diag::Lock l(c);
     uint32_t* sink = reinterpret_cast<uint32_t*>(c->d_small + 512);
     const uint32_t grid = (uint32_t)c->num_cus * 8;
@@ -158,6 +183,16 @@ int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t 
           hipLaunchKernelGGL(diag_stream_write<true>, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<uint4*>(buf),
                              bytes / 16);
           break;
+        case 6: {
+          const uint4* p = reinterpret_cast<const uint4*>(buf);
+          if (nops == 256)
+            hipLaunchKernelGGL(diag_segment_read<16>, dim3(grid), dim3(256), 0, c->stream, p, nseg_log, sink);
+          else if (nops == 512)
+            hipLaunchKernelGGL(diag_segment_read<32>, dim3(grid), dim3(256), 0, c->stream, p, nseg_log, sink);
+          else
+            hipLaunchKernelGGL(diag_segment_read<64>, dim3(grid), dim3(256), 0, c->stream, p, nseg_log, sink);
+          break;
+        }
         default: {
           const uint64_t half = bytes / 32;  // uint4 elements per half
           hipLaunchKernelGGL(diag_copy, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<const uint4*>(buf),

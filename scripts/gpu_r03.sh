@@ -9,6 +9,7 @@
 #     prof   : rocprofv3 kernel trace of the headline bench + PMC passes
 #     insprof: the C3 insert under rocprofv3 (trace, FETCH, WRITE, SQ passes)
 #     routes : scripts/insert_routes.py over the given route specs
+#     calib  : FETCH_SIZE calibration per access pattern
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -47,6 +48,10 @@ for p in ${PART//,/ }; do
       step ins_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/ins_write -o run -- $I || exit 1
       step ins_sq 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/ins_sq -o run -- $I || exit 1
       unset ROUNDS ;;
+    calib)  # FETCH_SIZE against known bytes per access pattern (scripts/fetch_calib.py)
+      rm -rf gpurun_out/calib_fetch
+      step calib 120 python3 scripts/fetch_calib.py || exit 1
+      step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- python3 scripts/fetch_calib.py || exit 1 ;;
     prof)
       B="python3 bench.py --no-cpu --no-bloom-replies"
       rm -rf gpurun_out/prof_stats

@@ -100,10 +100,15 @@ def main():
     # per stage and summed.  Append pipeline (default): sa1 reads the keys, sa2 its sub-regions and
     # apply its tiles with 16 B/lane loads, so FETCH is doubled per the guide; the header pipeline
     # (st1/st2/st_apply, RSK_BLOOM_SA=0) reads probe tags with 4 B loads (uncalibrated: raw).
+    # Round 3: sa2 writes 16-bit records (bloom_sa2h_kernel) that bloom_sah_apply_kernel reads with
+    # quarter-wave 256 B segment loads; the doubling is applied to it only as far as
+    # scripts/fetch_calib.py shows it holds for that pattern (FETCH_CALIB, below).
+    calib = json.loads(os.environ.get("FETCH_CALIB", "{}"))
     for name, st, wide in (("bloom_insert_supertile",
-                            ("bloom_sa1_kernel", "sa_size_kernel", "st_offsets_kernel", "bloom_sa2_kernel",
-                             "st_transpose_kernel", "bloom_sa_apply_kernel"),
-                            ("bloom_sa1_kernel", "bloom_sa2_kernel", "bloom_sa_apply_kernel")),
+                            ("bloom_sa1_kernel", "sah_size_kernel", "st_offsets_kernel", "bloom_sa2h_kernel",
+                             "bloom_sah_apply_kernel"),
+                            ("bloom_sa1_kernel", "bloom_sa2h_kernel") + (
+                                ("bloom_sah_apply_kernel",) if calib.get("segment_256B", 1.0) > 1.5 else ())),
                            ("bloom_insert_header_pipeline",
                             ("bloom_st1_kernel", "st_transpose_kernel", "st_size_kernel", "st_offsets_kernel",
                              "bloom_st2_kernel", "bloom_st_apply_kernel"), ("bloom_st1_kernel",))):

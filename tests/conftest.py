@@ -15,6 +15,8 @@ if os.path.exists(os.path.join(ROOT, "redisson_amd", "librsketch.so")) and not o
     from redisson_amd import _lib as _rsk_lib
 
     _rsk_lib.load()
+    if os.path.exists(_rsk_lib.DIAG_PATH):
+        _rsk_lib.diag()  # the support library too, before torch (see bench.py)
 
 
 def pytest_configure(config):
