@@ -149,99 +149,169 @@ __global__ __launch_bounds__(PT) void hll_gunits_kernel(const uint32_t* __restri
 constexpr uint32_t GP_CH = 1u << 20;
 
 // work item w: fine bin s = w / GP_NP (16 sketches from c*4096 + f*16), part w % GP_NP.
-// With pc.pcount: the PFCOUNT of every row written is estimated from LDS on
-// the way out (the write-back's uint4 i of each thread belongs to sketch i)
-// and left in pc (hll_count_kernel takes it instead of re-reading the row);
-// rows of split heavy bins and inexact sums are left for the count kernel.
+// With pc.pcount: the PFCOUNT of every row written is estimated on the way
+// out and left in pc (hll_count_kernel takes it instead of re-reading the
+// row); rows of split heavy bins and inexact sums are left for the count kernel.
+//
+// One workgroup per CU (128 KiB of LDS), persistent, its waves specialised:
+// waves 0-7 (loaders) load an item's records and max them into the LDS file;
+// waves 8-15 (writers) hold the previous item's rows in registers (one
+// sketch per wave, 16 uint4 per lane), store them and sum their PFCOUNT
+// terms meanwhile.  gfx9 counts a wave's loads and stores in one in-order
+// vmcnt, so a wave that stored 128 KiB and then loads records waits for the
+// stores before it can use them; split this way the loaders' counters hold
+// loads only (their next round is issued during the hand-over) and the
+// writers never wait.  Per item: [loaders apply j | writers store j-1]
+// barrier [writers read j out of LDS and zero it | loaders prefetch j+1] barrier.
+constexpr uint32_t GP_LT = GP_T / 2;  // loader lanes (waves 0 .. GP_LT/64 - 1)
+constexpr int GP_R = 4;               // uint4 record loads per loader lane per round (8192 records)
+constexpr int GP_Q = HLL_REGS / 16 / 64;  // uint4 of one sketch per writer lane (16)
+struct GItem {
+  uint32_t a, e, e0;
+  uint64_t g0;
+};
+RSK_DEV bool gitem(uint32_t w, const uint32_t* __restrict__ off2, uint32_t G1, uint64_t G, int write_all, GItem& it) {
+  const uint32_t s = w / GP_NP, half = w % GP_NP;
+  it.a = off2[(uint64_t)s * G1];
+  it.e0 = off2[(uint64_t)(s + 1) * G1];
+  it.e = it.e0 - it.a > GP_CH ? it.a + GP_CH : it.e0;  // the rest: hll_gapply_extra
+  it.g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
+  return !((it.a == it.e && !write_all) || it.g0 >= G);  // uniform across the workgroup
+}
+// a round of records from r0 (a multiple of 4): loader lane l loads uint4 r0/4 + l + GP_LT u
+RSK_DEV void gload(const uint32_t* __restrict__ recs, uint32_t r0, uint32_t e, uint4 (&rv)[GP_R]) {
+#pragma unroll
+  for (int u = 0; u < GP_R; ++u) {
+    const uint32_t q = r0 / 4 + threadIdx.x + u * GP_LT;
+    rv[u] = 4 * q < e ? ld_nt16(reinterpret_cast<const uint4*>(recs) + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
+}
+
 __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
                                                           uint32_t nfine, uint64_t G, int pool_zero,
                                                           int write_all, uint8_t* __restrict__ regs, PCount pc,
                                                           const double* __restrict__ lc) {
+  static_assert(GP_T == 1024 && GP_SK == 8, "8 writer waves, one sketch each");
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
-  __shared__ SumD part[GP_T / 64];
+  __shared__ SumD part[GP_SK];
+  constexpr uint32_t RREC = 4 * GP_R * GP_LT;  // records per round
+  const uint32_t nitems = GP_NP * nfine;
+  const bool writer = threadIdx.x >= GP_LT;
+  const uint32_t lane = threadIdx.x & 63, sw = (threadIdx.x - GP_LT) >> 6;  // writer wave = sketch of the item
+  uint4* lp = reinterpret_cast<uint4*>(r32);
   // the GP_NP parts of a fine bin read the same records: one XCD (one L2) for both
-  for (uint32_t w = xcd_slot(blockIdx.x, gridDim.x); w < GP_NP * nfine; w += gridDim.x) {
-    const uint32_t s = w / GP_NP, half = w % GP_NP;
-    const uint32_t a = off2[(uint64_t)s * G1], e0 = off2[(uint64_t)(s + 1) * G1];
-    const uint32_t e = e0 - a > GP_CH ? a + GP_CH : e0;  // the rest: hll_gapply_extra
-    const uint64_t g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
-    if ((a == e && !write_all) || g0 >= G) continue;  // uniform across the workgroup
-    const uint32_t nsk = (uint32_t)(G - g0 < GP_SK ? G - g0 : GP_SK);
-    const uint32_t n4 = nsk * (HLL_REGS / 16);
-    uint4* gp = reinterpret_cast<uint4*>(regs + g0 * HLL_REGS);
-    uint4* lp = reinterpret_cast<uint4*>(r32);
-    if (pool_zero)  // the pool is known to be all zero: nothing to read
-      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = make_uint4(0, 0, 0, 0);
-    else
-      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
-    // LDS-only barriers (lds_barrier) throughout: the previous item's
-    // write-back stores stay in flight while this item's LDS file is cleared
-    // and its records are applied (one workgroup per CU: a full fence here
-    // serialised every item's 128 KiB write behind its record phase)
-    lds_barrier();
-    for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += GP_T * GP_U) {
-      uint32_t rv[GP_U];  // GP_U record loads in flight per lane
+  uint32_t w = xcd_slot(blockIdx.x, gridDim.x);
+  GItem it, prev{0, 0, 0, 0};
+  while (w < nitems && !gitem(w, off2, G1, G, write_all, it)) w += gridDim.x;
+  uint4 rv[GP_R];
+  uint4 keep[GP_Q];  // writer: the previous item's sketch sw
+  bool have_prev = false;
+  if (!writer && w < nitems) gload(recs, it.a & ~3u, it.e, rv);
+  // the LDS file of the first item
+  if (pool_zero) {
+    for (uint32_t q = threadIdx.x; q < GP_SK * HLL_REGS / 16; q += GP_T) lp[q] = make_uint4(0, 0, 0, 0);
+  } else if (w < nitems) {
+    const uint32_t n4 = (uint32_t)(G - it.g0 < GP_SK ? G - it.g0 : GP_SK) * (HLL_REGS / 16);
+    const uint4* gp = reinterpret_cast<const uint4*>(regs + it.g0 * HLL_REGS);
+    for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
+  }
+  __syncthreads();
+  while (w < nitems || have_prev) {
+    const bool cur_ok = w < nitems;
+    // ---- [loaders: records of item w into LDS | writers: rows of prev out]
+    if (!writer) {
+      if (cur_ok) {
+        const uint32_t half = w % GP_NP;
+        for (uint32_t r0 = it.a & ~3u; r0 < it.e; r0 += RREC) {
+          if (r0 != (it.a & ~3u)) gload(recs, r0, it.e, rv);  // the first round was prefetched
 #pragma unroll
-      for (int u = 0; u < GP_U; ++u) {
-        const uint32_t i = i0 + u * GP_T;
-        rv[u] = i < e ? __builtin_nontemporal_load(&recs[i]) : 0xFFFFFFFFu;
-      }
+          for (int u = 0; u < GP_R; ++u) {
+            const uint32_t q = r0 / 4 + threadIdx.x + u * GP_LT;
+            const uint32_t x[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
 #pragma unroll
-      for (int u = 0; u < GP_U; ++u) {
-        const uint32_t r = rv[u];
-        const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
-        if (r == 0xFFFFFFFFu || sk / GP_SK != half) continue;  // (rank 63 never occurs: no real record is all ones)
-        const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
-        const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
-        uint32_t* word = &r32[byte >> 2];
-        uint32_t old = *word;
-        while (((old >> sh) & 0xFFu) < rank) {
-          const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
-          if (prev == old) break;
-          old = prev;
+            for (int m = 0; m < 4; ++m) {
+              const uint32_t r = x[m], i = 4 * q + m;
+              const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
+              if (i < it.a || i >= it.e || sk / GP_SK != half) continue;
+              const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
+              const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
+              uint32_t* word = &r32[byte >> 2];
+              uint32_t old = *word;
+              while (((old >> sh) & 0xFFu) < rank) {
+                const uint32_t pv = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+                if (pv == old) break;
+                old = pv;
+              }
+            }
+          }
         }
       }
-    }
-    lds_barrier();
-    const bool est = pc.pcount && e0 - a <= GP_CH;  // (a split bin's extra chunks change the rows later)
-    if (!est) {
-      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) gp[q] = lp[q];
-      if (pc.pcount && threadIdx.x < nsk) pc.pepoch[g0 + threadIdx.x] = 0;  // no estimate for these rows
-    } else {
-      static_assert(GP_T / 64 == 2 * GP_SK, "two waves per sketch");
-      // wave w writes back (and sums) half w & 1 of sketch w >> 1: 8 uint4 per lane, one reduction per wave
-      const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = wv >> 1;
+    } else if (have_prev) {
+      const uint32_t nsk = (uint32_t)(G - prev.g0 < GP_SK ? G - prev.g0 : GP_SK);
+      const bool est = pc.pcount && prev.e0 - prev.a <= GP_CH;  // (a split bin's extra chunks change the rows later)
       SumD sd{0.0, 0, 0};
-      if (i < nsk) {
-        const uint32_t q0 = i * (HLL_REGS / 16) + (wv & 1) * (HLL_REGS / 32);
+      if (sw < nsk) {
+        uint4* gp = reinterpret_cast<uint4*>(regs + (prev.g0 + sw) * HLL_REGS);
 #pragma unroll
-        for (int u = 0; u < HLL_REGS / 32 / 64; ++u) {
-          const uint32_t q = q0 + u * 64 + lane;
-          const uint4 v = lp[q];
-          gp[q] = v;
-          acc_word(sd, v.x);
-          acc_word(sd, v.y);
-          acc_word(sd, v.z);
-          acc_word(sd, v.w);
+        for (int u = 0; u < GP_Q; ++u) gp[u * 64 + lane] = keep[u];
+        if (est) {
+#pragma unroll
+          for (int u = 0; u < GP_Q; ++u) {
+            acc_word(sd, keep[u].x);
+            acc_word(sd, keep[u].y);
+            acc_word(sd, keep[u].z);
+            acc_word(sd, keep[u].w);
+          }
+          sd = wave_reduce(sd);
         }
       }
-      sd = wave_reduce(sd);
-      if (lane == 0) part[wv] = sd;
-      lds_barrier();
-      if (threadIdx.x < nsk) {  // one lane per sketch: its two wave partials
-        const SumD p0 = part[2 * threadIdx.x], p1 = part[2 * threadIdx.x + 1];  // exact sums: any order
-        SumD t{p0.t + p1.t, p0.ez + p1.ez, p0.rmax > p1.rmax ? p0.rmax : p1.rmax};
-        const uint64_t g = g0 + threadIdx.x;
-        if (exact_total(t)) {
-          pc.pcount[g] = hll_estimate(t.t, (int)t.ez, lc);
-          pc.pepoch[g] = pc.epoch;
-        } else {
-          pc.pepoch[g] = 0;  // Redis's dense order: left to hll_count_kernel
-        }
-      }
+      if (lane == 0) part[sw] = sd;
     }
-    lds_barrier();  // every lane has read the LDS file (its stores may still be in flight)
+    lds_barrier();
+    // ---- [writers: finish prev's estimates, read item w out of LDS and clear it | loaders: prefetch]
+    const GItem cur = it;
+    uint32_t wn = w;
+    if (cur_ok) {
+      wn = w + gridDim.x;
+      while (wn < nitems && !gitem(wn, off2, G1, G, write_all, it)) wn += gridDim.x;
+    }
+    if (writer) {
+      if (have_prev && pc.pcount) {
+        const uint32_t nsk = (uint32_t)(G - prev.g0 < GP_SK ? G - prev.g0 : GP_SK);
+        const uint32_t t = threadIdx.x - GP_LT;
+        if (t < nsk) {  // one lane per sketch
+          const uint64_t g = prev.g0 + t;
+          const SumD p = part[t];
+          if (prev.e0 - prev.a <= GP_CH && exact_total(p)) {
+            pc.pcount[g] = hll_estimate(p.t, (int)p.ez, lc);
+            pc.pepoch[g] = pc.epoch;
+          } else {
+            pc.pepoch[g] = 0;  // split bin or inexact sum: left to hll_count_kernel
+          }
+        }
+      }
+      if (cur_ok) {
+#pragma unroll
+        for (int u = 0; u < GP_Q; ++u) {
+          const uint32_t q = sw * (HLL_REGS / 16) + u * 64 + lane;
+          keep[u] = lp[q];
+          if (pool_zero) lp[q] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    } else if (cur_ok && wn < nitems) {
+      gload(recs, it.a & ~3u, it.e, rv);
+    }
+    have_prev = cur_ok;
+    prev = cur;
+    w = wn;
+    if (!pool_zero && w < nitems) {  // the next item's old registers (not the C5 bench path)
+      lds_barrier();
+      const uint32_t n4 = (uint32_t)(G - it.g0 < GP_SK ? G - it.g0 : GP_SK) * (HLL_REGS / 16);
+      const uint4* gp = reinterpret_cast<const uint4*>(regs + it.g0 * HLL_REGS);
+      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
+    }
+    lds_barrier();
   }
 }
 
@@ -358,7 +428,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint32_t xcap = (uint32_t)(GP_NP * (chunk / GP_CH + 1) + 16);  // extra work items per chunk, at most
   const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1)) +
                         al(4 * (ncnt1 + 1));
-  uint8_t* w = c->work(meta + 2 * al(4 * max_np));
+  uint8_t* w = c->work(meta + 2 * al(4 * max_np) + 256);  // + slack: hll_gapply's uint4 loads round e up
   uint32_t* cnt1 = reinterpret_cast<uint32_t*>(w);
   uint32_t* off1 = reinterpret_cast<uint32_t*>(w + al(4 * ncnt1));
   uint32_t* cnt2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1));
@@ -402,8 +472,8 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
     }
     {
       ProfScope ps(c, "hll_gapply");
-      const uint32_t per_cu = (160u * 1024) / (GP_SK * HLL_REGS + 1024);  // workgroups resident per CU
-      hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, 2 * per_cu * cus)), dim3(GP_T), 0,
+      // persistent: one resident workgroup per CU (128 KiB of LDS), items strided
+      hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, cus)), dim3(GP_T), 0,
                          c->stream,
                          buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0,
                          (write_all && first == 0) ? 1 : 0, d_regs, pc, c->d_lc);
