@@ -6,6 +6,7 @@
 //   mode 3: streaming copy (read + write halves)          -> GB/s (read+write)
 //   mode 4: streaming write (16 B/lane plain stores)       -> GB/s
 //   mode 5: streaming write (16 B/lane nontemporal stores) -> GB/s
+//   mode 6: scattered 256 B / 512 B / 1 KiB segment reads  -> GB/s (FETCH_SIZE calibration)
 // Indices come from splitmix64(i), as uniform as the Bloom probe stream.
 // Also: the route overrides of a context (rsk_diag_set_route) and the timed
 // launches of the kernels' tuning variants (rsk_diag_kernels.hip).
