@@ -479,8 +479,8 @@ def main():
         add_launches = reads["hll_gapply"][1]
         add_ms = sum(v[0] for v in reads.values())
         stage_ms = {st: v[0] / max(1, v[1]) for st, v in reads.items()}
-        kern_label = ("hll_add_grouped (partitioned: hll_gcount + scan, hll_gpart1, hll_gcount2 + scan + "
-                      "bloom_part2, hll_gapply)")
+        kern_label = ("hll_add_grouped (partitioned: hll_gcount + scan, hll_gpart1, hll_gparts + hll_gcount2p + "
+                      "scan + hll_gfine + hll_gpart2p, hll_gapply)")
     red_ms, red_launches = engine.prof_read("hll_reduce")
     side = {name: engine.prof_read(name) for name in ("hll_count", "hll_union_count", "hll_merge",
                                                        "hll_allreduce", "hll_allreduce_pool",

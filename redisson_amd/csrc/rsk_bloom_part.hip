@@ -439,12 +439,4 @@ bool bloom_add_partitioned(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys) {
 }
 
 
-// part2 for other callers (the grouped PFADD, rsk_hll_group.hip).
-void part2_launch(rsk_ctx* c, uint32_t grid, const uint32_t* in, const uint32_t* off1, const uint32_t* off2,
-                  uint32_t G, uint32_t GU, uint32_t nunits, uint32_t f2, uint32_t nslices, uint32_t bin_shift,
-                  uint32_t pay_mask, const uint32_t* ustart, const uint32_t* d_nunits, uint32_t* out) {
-  hipLaunchKernelGGL(bloom_part2_kernel, dim3(grid), dim3(PT), 0, c->stream, in, off1, off2, G, GU, nunits, f2,
-                     nslices, bin_shift, pay_mask, ustart, d_nunits, out);
-}
-
 }  // namespace rsk

@@ -18,13 +18,14 @@ namespace rsk {
 //   gcount : cnt1[c][b] = pairs of block b in coarse bin c = g >> 12 (<= 256 bins)
 //   gpart1 : block b hashes its pairs into records rec = (g & 0xFFF) << 20 |
 //            idx << 6 | rank and counting-sorts them by coarse bin (exact offsets)
-//   gcount2: cnt2[c*256 + f][b] = records of unit (c, b) in fine bin f = rec >> 24
-//            (16 sketches)
-//   part2  : the Bloom part2 kernel re-sorts each unit by fine bin (records kept)
+//   gparts / gcount2p / gfine / gpart2p: each coarse bin's run cut into parts
+//            of about equal record counts, re-sorted by fine bin f = rec >> 24
+//            (16 sketches) with exact offsets (counts per (bin, fine bin, part))
 //   gapply : one workgroup per (fine bin, half): 8 sketches' registers in LDS
-//            (byte max by LDS CAS), read and written back once
-// HBM per pair: 4 (gcount) + 20 + 4 (gpart1) + 4 (gcount2) + 8 (part2) + 8 (gapply,
-// two halves), plus 32 KiB per touched sketch -- against a random read + CAS.
+//            (byte max by LDS CAS), written back once with their PFCOUNT estimates
+// HBM per pair: 4 (gcount) + 20 + 4 (gpart1) + 4 (gcount2p) + 8 (gpart2p) + 4
+// (gapply; both halves of a fine bin on one XCD), plus 16 KiB per written
+// sketch (and its read unless the pool is known to be zero).
 constexpr uint32_t GP_BIN_SHIFT = 12;  // sketches per coarse bin = 4096 (rec keeps 12 bits of g)
 #ifndef RSK_GP_SK
 #define RSK_GP_SK 8
@@ -38,7 +39,6 @@ constexpr uint32_t GP_T = 1024;        // gcount / gapply workgroup
 #endif
 constexpr uint32_t GP_TILE = RSK_GP_TILE;  // records per gpart1 tile
 constexpr int GP_E = GP_TILE / PT;
-constexpr uint32_t GP_GU = 8;          // gpart1 blocks per part2 unit (G1 is a multiple)
 
 __global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __restrict__ groups, uint64_t n,
                                                           uint64_t per, uint64_t G, uint32_t nbins,
@@ -96,38 +96,44 @@ __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict_
   }
 }
 
-// unit u = c * G1 + b is [off1[u], off1[u+1]); cnt2[(c * 256 + f) * G1 + b].
-__global__ __launch_bounds__(PT) void hll_gcount2_kernel(const uint32_t* __restrict__ recs,
-                                                         const uint32_t* __restrict__ off1, uint32_t G1,
-                                                         uint32_t* __restrict__ cnt2) {
-  __shared__ uint32_t h[PT];
-  const uint32_t u = blockIdx.x;
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t a = off1[u], e = off1[u + 1];
-  for (uint32_t i = a + threadIdx.x; i < e; i += PT) atomicAdd(&h[__builtin_nontemporal_load(&recs[i]) >> 24], 1u);
-  __syncthreads();
-  const uint32_t c = u / G1, b = u - c * G1;
-  cnt2[((uint64_t)c * PT + threadIdx.x) * G1 + b] = h[threadIdx.x];
+// ---- fine-bin pass: gpart1's coarse-bin runs re-sorted by fine bin (16
+// sketches, rec >> 24).  Each coarse bin c is cut into nq_c parts of about
+// `target` records (parts sized by records, so a heavy bin -- Zipf -- gets
+// many); part q of bin c = records [lo, hi) of its run.  gcount2p counts the
+// fine bins of every part into cnt[(q0_c + j) ...] laid out bin-major, then
+// fine-bin-major, then part (index q0_c 256 + f nq_c + j), so one exclusive
+// scan gives every (c, f, part)'s first output slot and fine bin s = c 256 + f
+// starts at offf[q0_c 256 + f nq_c]; gpart2p sorts each part's tiles by fine
+// bin in LDS and writes its runs at those cursors.  1024-lane workgroups and
+// uint4 record loads (records are 4 B; part edges are masked).
+RSK_DEV uint32_t gq_scan_incl(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x;
 }
+constexpr uint32_t GQ_T = 1024;
+constexpr int GQ_V = 3;                              // uint4 loads per lane per tile
+constexpr uint32_t GQ_TILE = GQ_T * GQ_V * 4;        // 12288 records
+struct GPart {
+  uint32_t c, q0, nq, lo, hi;
+};
 
-// part2 units: GU part1 blocks each, or one block each in a coarse bin whose
-// GU-block units would be above a quarter of a part2 workgroup's share of the
-// records (skewed groups: Zipf(1.1) puts ~60 % of all pairs into bin 0, whose
-// GU-block units were ten shares each).  One workgroup; lane c = bin c.
-__global__ __launch_bounds__(PT) void hll_gunits_kernel(const uint32_t* __restrict__ off1, uint32_t G1, uint32_t GU,
-                                                        uint32_t nbins1, uint32_t p2_grid,
-                                                        uint32_t* __restrict__ ustart, uint32_t* __restrict__ d_nunits) {
+// One workgroup, lane c = coarse bin: its parts (at most nbins1 + total / target).
+__global__ __launch_bounds__(PT) void hll_gparts_kernel(const uint32_t* __restrict__ off1, uint32_t G1,
+                                                        uint32_t nbins1, uint32_t target, uint32_t qmax,
+                                                        GPart* __restrict__ parts, uint32_t* __restrict__ d_nq) {
   __shared__ uint32_t cnt[PT];
   const uint32_t c = threadIdx.x;
-  const uint64_t total = off1[(uint64_t)nbins1 * G1];
-  uint32_t gu = GU, n = 0;
+  uint32_t lo = 0, len = 0, nq = 0;
   if (c < nbins1) {
-    const uint64_t r = off1[(uint64_t)(c + 1) * G1] - off1[(uint64_t)c * G1];
-    if (r * GU > (uint64_t)G1 * (total / (4ull * p2_grid) + 1)) gu = 1;
-    n = G1 / gu;
+    lo = off1[(uint64_t)c * G1];
+    len = off1[(uint64_t)(c + 1) * G1] - lo;
+    nq = len / target + 1;
   }
-  cnt[c] = n;
+  cnt[c] = nq;
   __syncthreads();
   if (c == 0) {  // exclusive prefix over <= 256 bins
     uint32_t run = 0;
@@ -136,11 +142,144 @@ __global__ __launch_bounds__(PT) void hll_gunits_kernel(const uint32_t* __restri
       cnt[i] = run;
       run += v;
     }
-    ustart[run] = nbins1 * G1;
-    *d_nunits = run;
+    *d_nq = run < qmax ? run : qmax;
   }
   __syncthreads();
-  for (uint32_t q = 0; q < n; ++q) ustart[cnt[c] + q] = c * G1 + q * gu;
+  const uint32_t q0 = cnt[c];
+  for (uint32_t j = 0; j < nq && q0 + j < qmax; ++j)
+    parts[q0 + j] = GPart{c, q0, nq, lo + (uint32_t)((uint64_t)len * j / nq), lo + (uint32_t)((uint64_t)len * (j + 1) / nq)};
+}
+
+// Record r of the part: uint4 q = r / 4 of the (16-byte aligned) record array.
+RSK_DEV void gq_load(const uint32_t* __restrict__ recs, uint32_t r0, uint32_t hi, uint4 (&v)[GQ_V]) {
+#pragma unroll
+  for (int u = 0; u < GQ_V; ++u) {
+    const uint32_t q = r0 / 4 + threadIdx.x + u * GQ_T;
+    v[u] = 4 * q < hi ? ld_nt16(reinterpret_cast<const uint4*>(recs) + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
+}
+
+__global__ __launch_bounds__(GQ_T) void hll_gcount2p_kernel(const uint32_t* __restrict__ recs,
+                                                            const GPart* __restrict__ parts,
+                                                            const uint32_t* __restrict__ d_nq,
+                                                            uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[4][PT];  // one histogram per wave mod 4 (less contention)
+  const uint32_t q = blockIdx.x;
+  if (q >= *d_nq) return;  // uniform
+  const GPart pt = parts[q];
+  for (uint32_t i = threadIdx.x; i < 4 * PT; i += GQ_T) (&h[0][0])[i] = 0;
+  __syncthreads();
+  uint32_t* hw = h[(threadIdx.x >> 6) & 3];
+  for (uint32_t r0 = pt.lo & ~3u; r0 < pt.hi; r0 += GQ_TILE) {
+    uint4 v[GQ_V];
+    gq_load(recs, r0, pt.hi, v);
+#pragma unroll
+    for (int u = 0; u < GQ_V; ++u) {
+      const uint32_t i0 = 4 * (r0 / 4 + threadIdx.x + u * GQ_T);
+      const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (i0 + m >= pt.lo && i0 + m < pt.hi) atomicAdd(&hw[x[m] >> 24], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < PT) {
+    const uint32_t f = threadIdx.x;
+    cnt[(uint64_t)pt.q0 * PT + (uint64_t)f * pt.nq + (q - pt.q0)] = h[0][f] + h[1][f] + h[2][f] + h[3][f];
+  }
+}
+
+// off2[s] (s = c 256 + f < nfine) = first slot of fine bin s; off2[nfine] = the total.
+__global__ __launch_bounds__(256) void hll_gfine_kernel(const uint32_t* __restrict__ offf,
+                                                        const GPart* __restrict__ parts,
+                                                        const uint32_t* __restrict__ d_nq, uint32_t nbins1,
+                                                        uint32_t* __restrict__ off2) {
+  const uint32_t nq = *d_nq;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nbins1 * PT) return;
+  if (s == nbins1 * PT) {
+    off2[s] = offf[(uint64_t)nq * PT];
+    return;
+  }
+  const uint32_t c = s / PT, f = s % PT;
+  // the first part of bin c: parts are ordered by bin, nq_c >= 1 each (binary search)
+  uint32_t lo = 0, hi = nq;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (parts[mid].c < c) lo = mid + 1;
+    else hi = mid;
+  }
+  const GPart pt = parts[lo];
+  off2[s] = offf[(uint64_t)pt.q0 * PT + (uint64_t)f * pt.nq];
+}
+
+__global__ __launch_bounds__(GQ_T) void hll_gpart2p_kernel(const uint32_t* __restrict__ recs,
+                                                           const GPart* __restrict__ parts,
+                                                           const uint32_t* __restrict__ d_nq,
+                                                           const uint32_t* __restrict__ offf,
+                                                           uint32_t* __restrict__ out) {
+  __shared__ uint32_t img[GQ_TILE];
+  __shared__ uint8_t sbin[GQ_TILE];
+  __shared__ uint32_t hist[PT], dlt[PT], cur[PT], wsum[GQ_T / 64];
+  const uint32_t q = blockIdx.x;
+  if (q >= *d_nq) return;  // uniform
+  const GPart pt = parts[q];
+  if (threadIdx.x < PT) {
+    cur[threadIdx.x] = offf[(uint64_t)pt.q0 * PT + (uint64_t)threadIdx.x * pt.nq + (q - pt.q0)];
+    hist[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  for (uint32_t r0 = pt.lo & ~3u; r0 < pt.hi; r0 += GQ_TILE) {
+    uint4 v[GQ_V];
+    gq_load(recs, r0, pt.hi, v);
+    uint32_t rec[4 * GQ_V], tag[4 * GQ_V];
+#pragma unroll
+    for (int u = 0; u < GQ_V; ++u) {
+      const uint32_t i0 = 4 * (r0 / 4 + threadIdx.x + u * GQ_T);
+      const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        rec[4 * u + m] = x[m];
+        tag[4 * u + m] = 0xFFFFFFFFu;
+        if (i0 + m >= pt.lo && i0 + m < pt.hi) {
+          const uint32_t b = x[m] >> 24;
+          tag[4 * u + m] = (b << 16) | atomicAdd(&hist[b], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    // bin starts inside the tile (lanes 0..255: one bin each; four waves)
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t hv = 0, incl = 0;
+    if (threadIdx.x < PT) {
+      hv = hist[threadIdx.x];
+      incl = gq_scan_incl(hv, lane);
+      if (lane == 63) wsum[w] = incl;
+    }
+    __syncthreads();
+    if (threadIdx.x < PT) {
+      uint32_t pre = 0;
+      for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
+      const uint32_t ls = pre + incl - hv;
+      dlt[threadIdx.x] = cur[threadIdx.x] - ls;
+      cur[threadIdx.x] += hv;
+      hist[threadIdx.x] = ls;  // the bin's start inside the tile (reset to 0 below)
+    }
+    __syncthreads();
+    uint32_t ntile = 0;
+#pragma unroll
+    for (int e = 0; e < 4 * GQ_V; ++e)
+      if (tag[e] != 0xFFFFFFFFu) {
+        const uint32_t b = tag[e] >> 16, j = hist[b] + (tag[e] & 0xFFFFu);
+        img[j] = rec[e];
+        sbin[j] = (uint8_t)b;
+      }
+    ntile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    if (threadIdx.x < PT) hist[threadIdx.x] = 0;
+    for (uint32_t j = threadIdx.x; j < ntile; j += GQ_T) out[dlt[sbin[j]] + j] = img[j];
+    __syncthreads();
+  }
 }
 
 // A fine bin's records beyond its first GP_CH go to hll_gapply_extra (skewed
@@ -414,30 +553,38 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
   const uint32_t cus = (uint32_t)c->num_cus;
-  constexpr uint32_t GU = GP_GU;   // part1 blocks per part2 unit
-  constexpr uint32_t gpc = 2;      // gcount / gpart1 blocks per CU
-  const uint32_t G1 = GU * ((gpc * cus + GU - 1) / GU);  // a multiple of GU
-  const uint32_t p2_grid = 4 * cus;
+  constexpr uint32_t gpc = 2;  // gcount / gpart1 blocks per CU
+  const uint32_t G1 = gpc * cus;
   const uint64_t chunk = PROBE_CAP;
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
-  const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)nfine * G1 + 1;
+  // fine-bin pass parts: about four per CU over the whole chunk, at least 16 tiles each
+  const uint32_t target = (uint32_t)std::max<uint64_t>(16ull * GQ_TILE, max_np / (4ull * cus) + 1);
+  const uint32_t qmax = nbins1 + (uint32_t)(max_np / target) + 2;
+  const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)qmax * PT + 1;
   size_t sb1 = 0, sb2 = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt1, c->stream);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt2, c->stream);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   const uint32_t xcap = (uint32_t)(GP_NP * (chunk / GP_CH + 1) + 16);  // extra work items per chunk, at most
   const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1)) +
-                        al(4 * (ncnt1 + 1));
-  uint8_t* w = c->work(meta + 2 * al(4 * max_np) + 256);  // + slack: hll_gapply's uint4 loads round e up
-  uint32_t* cnt1 = reinterpret_cast<uint32_t*>(w);
-  uint32_t* off1 = reinterpret_cast<uint32_t*>(w + al(4 * ncnt1));
-  uint32_t* cnt2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1));
-  uint32_t* off2 = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1) + al(4 * ncnt2));
-  void* scan_tmp = w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2);
-  uint32_t* xlist = reinterpret_cast<uint32_t*>(w + 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)));
+                        al(sizeof(GPart) * qmax) + al(4 * (nfine + 1)) + 256;
+  uint8_t* w = c->work(meta + 2 * al(4 * max_np) + 256);  // + slack: the uint4 record loads round their ends up
+  uint8_t* q = w;
+  auto take = [&](uint64_t n) {
+    uint8_t* r = q;
+    q += n;
+    return r;
+  };
+  uint32_t* cnt1 = reinterpret_cast<uint32_t*>(take(al(4 * ncnt1)));
+  uint32_t* off1 = reinterpret_cast<uint32_t*>(take(al(4 * ncnt1)));
+  uint32_t* cnt2 = reinterpret_cast<uint32_t*>(take(al(4 * ncnt2)));
+  uint32_t* offf = reinterpret_cast<uint32_t*>(take(al(4 * ncnt2)));
+  void* scan_tmp = take(al(std::max(sb1, sb2)));
+  uint32_t* xlist = reinterpret_cast<uint32_t*>(take(al(4 * (xcap + 1))));
   uint32_t* xcount = xlist + xcap;
-  uint32_t* ustart = reinterpret_cast<uint32_t*>(w + meta - al(4 * (ncnt1 + 1)));  // part2 units + [ncnt1]: count
-  uint32_t* d_nunits = ustart + ncnt1;
+  GPart* parts = reinterpret_cast<GPart*>(take(al(sizeof(GPart) * qmax)));
+  uint32_t* off2 = reinterpret_cast<uint32_t*>(take(al(4 * (nfine + 1))));
+  uint32_t* d_nq = reinterpret_cast<uint32_t*>(take(256));
   uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta);
   uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np));
   for (uint64_t first = 0; first < keys.n; first += chunk) {
@@ -459,30 +606,31 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
     }
     {
       ProfScope ps(c, "hll_gpart2");
-      RSK_HIP(hipMemsetAsync(cnt2 + ncnt2 - 1, 0, 4, c->stream));
-      hipLaunchKernelGGL(hll_gcount2_kernel, dim3(nbins1 * G1), dim3(PT), 0, c->stream, buf_a, off1, G1, cnt2);
-      RSK_CHECK_LAUNCH("hll_gcount2");
-      RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, off2, (int)ncnt2, c->stream));
-      hipLaunchKernelGGL(hll_gunits_kernel, dim3(1), dim3(PT), 0, c->stream, off1, G1, GU, nbins1, p2_grid, ustart,
-                         d_nunits);
-      RSK_CHECK_LAUNCH("hll_gunits");
-      part2_launch(c, p2_grid, buf_a, off1, off2, G1, GU, nbins1 * (G1 / GU), 8u, nfine, 24u, 0xFFFFFFFFu, ustart,
-                   d_nunits, buf_b);
-      RSK_CHECK_LAUNCH("hll_gpart2");
+      RSK_HIP(hipMemsetAsync(cnt2, 0, 4 * ncnt2, c->stream));
+      hipLaunchKernelGGL(hll_gparts_kernel, dim3(1), dim3(PT), 0, c->stream, off1, G1, nbins1, target, qmax, parts,
+                         d_nq);
+      RSK_CHECK_LAUNCH("hll_gparts");
+      hipLaunchKernelGGL(hll_gcount2p_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, cnt2);
+      RSK_CHECK_LAUNCH("hll_gcount2p");
+      RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, offf, (int)ncnt2, c->stream));
+      hipLaunchKernelGGL(hll_gfine_kernel, dim3(nfine / 256 + 1), dim3(256), 0, c->stream, offf, parts, d_nq, nbins1,
+                         off2);
+      RSK_CHECK_LAUNCH("hll_gfine");
+      hipLaunchKernelGGL(hll_gpart2p_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b);
+      RSK_CHECK_LAUNCH("hll_gpart2p");
     }
     {
       ProfScope ps(c, "hll_gapply");
       // persistent: one resident workgroup per CU (128 KiB of LDS), items strided
       hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, cus)), dim3(GP_T), 0,
-                         c->stream,
-                         buf_b, off2, G1, nfine, G, (pool_zero && first == 0) ? 1 : 0,
+                         c->stream, buf_b, off2, 1u, nfine, G, (pool_zero && first == 0) ? 1 : 0,
                          (write_all && first == 0) ? 1 : 0, d_regs, pc, c->d_lc);
       RSK_CHECK_LAUNCH("hll_gapply");
       RSK_HIP(hipMemsetAsync(xcount, 0, 4, c->stream));
-      hipLaunchKernelGGL(hll_gextra_list_kernel, dim3((nfine + 255) / 256), dim3(256), 0, c->stream, off2, G1, nfine,
+      hipLaunchKernelGGL(hll_gextra_list_kernel, dim3((nfine + 255) / 256), dim3(256), 0, c->stream, off2, 1u, nfine,
                          xcap, xlist, xcount);
       RSK_CHECK_LAUNCH("hll_gextra_list");
-      hipLaunchKernelGGL(hll_gapply_extra_kernel, dim3(2 * cus), dim3(GP_T), 0, c->stream, buf_b, off2, G1, G, xlist,
+      hipLaunchKernelGGL(hll_gapply_extra_kernel, dim3(2 * cus), dim3(GP_T), 0, c->stream, buf_b, off2, 1u, G, xlist,
                          xcount, xcap, d_regs);
       RSK_CHECK_LAUNCH("hll_gapply_extra");
     }

@@ -83,11 +83,4 @@ __device__ __forceinline__ void tile_write(S& L, uint32_t np, uint32_t cnt, uint
   L.hist[threadIdx.x] = 0;
 }
 
-// part2 (rsk_bloom_part.hip): re-sort units of part1 runs by fine bin.  Units
-// are GU consecutive part1 blocks of a bucket, or (ustart != nullptr) the
-// device table ustart[0..*d_nunits] of first blocks.
-void part2_launch(rsk_ctx* c, uint32_t grid, const uint32_t* in, const uint32_t* off1, const uint32_t* off2,
-                  uint32_t G, uint32_t GU, uint32_t nunits, uint32_t f2, uint32_t nslices, uint32_t bin_shift,
-                  uint32_t pay_mask, const uint32_t* ustart, const uint32_t* d_nunits, uint32_t* out);
-
 }  // namespace rsk
