@@ -40,20 +40,42 @@ constexpr uint32_t GP_T = 1024;        // gcount / gapply workgroup
 constexpr uint32_t GP_TILE = RSK_GP_TILE;  // records per gpart1 tile
 constexpr int GP_E = GP_TILE / PT;
 
+// Group ids are read as uint4 (4 ids) with 4 loads in flight per lane when
+// the block's range is 16-byte aligned (the host keeps `per` a multiple of
+// 4; `aligned` = the ids' address is), one histogram per wave mod 4.
 __global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __restrict__ groups, uint64_t n,
-                                                          uint64_t per, uint64_t G, uint32_t nbins,
+                                                          uint64_t per, uint64_t G, uint32_t nbins, int aligned,
                                                           uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t h[PT];
-  for (uint32_t s = threadIdx.x; s < PT; s += GP_T) h[s] = 0;
+  __shared__ uint32_t h[4][PT];
+  for (uint32_t s = threadIdx.x; s < 4 * PT; s += GP_T) (&h[0][0])[s] = 0;
   __syncthreads();
+  uint32_t* hw = h[(threadIdx.x >> 6) & 3];
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
-  for (uint64_t i = begin + threadIdx.x; i < end; i += GP_T) {
-    const uint32_t g = __builtin_nontemporal_load(&groups[i]);
-    if (g < G) atomicAdd(&h[g >> GP_BIN_SHIFT], 1u);
+  auto add = [&](uint32_t g) {
+    if (g < G) atomicAdd(&hw[g >> GP_BIN_SHIFT], 1u);
+  };
+  uint64_t i = begin;
+  if (aligned) {
+    constexpr int U = 4;
+    const uint4* g4 = reinterpret_cast<const uint4*>(groups);
+    for (; i + 4ull * GP_T * U <= end; i += 4ull * GP_T * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld_nt16(g4 + i / 4 + threadIdx.x + u * GP_T);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        add(v[u].x);
+        add(v[u].y);
+        add(v[u].z);
+        add(v[u].w);
+      }
+    }
   }
+  for (i += threadIdx.x; i < end; i += GP_T) add(__builtin_nontemporal_load(&groups[i]));
   __syncthreads();
-  for (uint32_t s = threadIdx.x; s < nbins; s += GP_T) cnt[(uint64_t)s * gridDim.x + blockIdx.x] = h[s];
+  for (uint32_t s = threadIdx.x; s < nbins; s += GP_T)
+    cnt[(uint64_t)s * gridDim.x + blockIdx.x] = h[0][s] + h[1][s] + h[2][s] + h[3][s];
 }
 
 __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict__ keys,
@@ -589,13 +611,14 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np));
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
-    const uint64_t per = (m + G1 - 1) / G1;
+    const uint64_t per = ((m + G1 - 1) / G1 + 3) & ~3ull;  // a multiple of 4: uint4 id loads in hll_gcount
     const uint4* kd = reinterpret_cast<const uint4*>(keys.data) + first;
     const uint32_t* gd = d_groups + first;
     {
       ProfScope ps(c, "hll_gpart_count");
       RSK_HIP(hipMemsetAsync(cnt1 + ncnt1 - 1, 0, 4, c->stream));
-      hipLaunchKernelGGL(hll_gcount_kernel, dim3(G1), dim3(GP_T), 0, c->stream, gd, m, per, G, nbins1, cnt1);
+      const int aligned = (reinterpret_cast<uintptr_t>(gd) & 15) == 0;
+      hipLaunchKernelGGL(hll_gcount_kernel, dim3(G1), dim3(GP_T), 0, c->stream, gd, m, per, G, nbins1, aligned, cnt1);
       RSK_CHECK_LAUNCH("hll_gcount");
       RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb1, cnt1, off1, (int)ncnt1, c->stream));
     }
