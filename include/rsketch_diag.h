@@ -39,7 +39,8 @@ int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
  * 3 stream copy (buffer halves), 4 stream write, 5 stream write with
  * nontemporal stores, 6 scattered segment reads of n_ops (256, 512 or 1024)
  * bytes, one uint4 per lane, every byte of the largest power-of-two number
- * of segments that fits read once (FETCH_SIZE calibration).
+ * of segments that fits read once (FETCH_SIZE calibration), 7 stream copy
+ * (buffer halves) with the loads and the stores in different waves.
  * *ms = device time of the one launch. */
 int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
 /* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */

@@ -7,6 +7,7 @@
 //   mode 4: streaming write (16 B/lane plain stores)       -> GB/s
 //   mode 5: streaming write (16 B/lane nontemporal stores) -> GB/s
 //   mode 6: scattered 256 B / 512 B / 1 KiB segment reads  -> GB/s (FETCH_SIZE calibration)
+//   mode 7: streaming copy, loads and stores in different waves -> GB/s (read+write)
 // Indices come from splitmix64(i), as uniform as the Bloom probe stream.
 // Also: the route overrides of a context (rsk_diag_set_route) and the timed
 // launches of the kernels' tuning variants (rsk_diag_kernels.hip).
@@ -48,6 +49,39 @@ __global__ __launch_bounds__(256) void diag_segment_read(const uint4* __restrict
 __global__ __launch_bounds__(256) void diag_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = ld_nt16(src + i);
+}
+
+// Copy with the loads and the stores in different waves (mode 7): gfx9's
+// vmcnt counts a wave's loads and stores in issue order, so a wave that
+// copies waits for its stores each time it waits for its next loads.  Waves
+// 0-3 load 16 KiB chunks (the next one in flight) into a double-buffered LDS
+// stage, waves 4-7 store them; one barrier per chunk.
+__global__ __launch_bounds__(512) void diag_copy_split(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                       uint64_t n16) {
+  constexpr uint32_t CH = 256 * 4;  // uint4 per chunk (16 KiB)
+  __shared__ uint4 buf[2][CH];
+  const bool loader = threadIdx.x < 256;
+  const uint32_t t = threadIdx.x & 255;
+  const uint64_t nch = n16 / CH;
+  uint4 v[4];
+  uint64_t c = blockIdx.x;
+  if (loader && c < nch)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld_nt16(src + c * CH + t + u * 256);
+  for (uint32_t j = 0; c < nch; ++j, c += gridDim.x) {
+    if (loader) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) buf[j & 1][t + u * 256] = v[u];
+      const uint64_t cn = c + gridDim.x;
+      if (cn < nch)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ld_nt16(src + cn * CH + t + u * 256);
+    }
+    lds_barrier();
+    if (!loader)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dst[c * CH + t + u * 256] = buf[j & 1][t + u * 256];
+  }
 }
 
 template <bool NT>
@@ -152,7 +186,7 @@ int rsk_diag_bloom_contains_variant(rsk_ctx* c, int variant, rsk_bloom* bf, cons
 
 int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t nops, double* ms) {
   return diag::guarded([&] {
-    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 6, "bad arguments");
+    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 7, "bad arguments");
     // mode 6: segment reads of nops bytes (256, 512 or 1024) over the largest
     // power-of-two number of segments that fits
     diag::need(mode != 6 || nops == 256 || nops == 512 || nops == 1024, "segment bytes must be 256, 512 or 1024");
@@ -184,6 +218,12 @@ int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t 
           hipLaunchKernelGGL(diag_stream_write<true>, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<uint4*>(buf),
                              bytes / 16);
           break;
+        case 7: {  // split copy: buffer halves, as mode 3
+          const uint64_t half = bytes / 32;
+          hipLaunchKernelGGL(diag_copy_split, dim3((uint32_t)c->num_cus * 4), dim3(512), 0, c->stream,
+                             reinterpret_cast<const uint4*>(buf), reinterpret_cast<uint4*>(buf) + half, half);
+          break;
+        }
         case 6: {
           const uint4* p = reinterpret_cast<const uint4*>(buf);
           if (nops == 256)

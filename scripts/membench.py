@@ -34,6 +34,7 @@ def main():
     cases = [
         ("stream_read_16GiB", 0, 16 << 30, 0, lambda ms: (16 << 30) / ms / 1e6, "GB/s"),
         ("stream_copy_8GiB_each_way", 3, 16 << 30, 0, lambda ms: (16 << 30) / ms / 1e6, "GB/s (read+write)"),
+        ("stream_copy_split_8GiB_each_way", 7, 16 << 30, 0, lambda ms: (16 << 30) / ms / 1e6, "GB/s (read+write)"),
         ("stream_write_16GiB", 4, 16 << 30, 0, lambda ms: (16 << 30) / ms / 1e6, "GB/s"),
         ("stream_write_nt_16GiB", 5, 16 << 30, 0, lambda ms: (16 << 30) / ms / 1e6, "GB/s"),
         ("gather4B_1.2GB", 1, 1_198_132_298, 1 << 30, lambda ms: (1 << 30) / ms * 1e3, "gathers/s"),
