@@ -348,6 +348,10 @@ RSK_DEV void gload(const uint32_t* __restrict__ recs, uint32_t r0, uint32_t e, u
   }
 }
 
+// The two roles run separate loops with the same barrier sequence, so the
+// compiler allocates registers per role (the writers' 64 VGPRs of rows are
+// not live in the loaders' loop).  Per iteration: [Z] barrier [X] (barrier +
+// old rows into LDS, when the pool is not known zero) barrier.
 __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __restrict__ recs,
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
                                                           uint32_t nfine, uint64_t G, int pool_zero,
@@ -358,17 +362,25 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
   __shared__ SumD part[GP_SK];
   constexpr uint32_t RREC = 4 * GP_R * GP_LT;  // records per round
   const uint32_t nitems = GP_NP * nfine;
-  const bool writer = threadIdx.x >= GP_LT;
-  const uint32_t lane = threadIdx.x & 63, sw = (threadIdx.x - GP_LT) >> 6;  // writer wave = sketch of the item
+  const uint32_t lane = threadIdx.x & 63;
   uint4* lp = reinterpret_cast<uint4*>(r32);
   // the GP_NP parts of a fine bin read the same records: one XCD (one L2) for both
   uint32_t w = xcd_slot(blockIdx.x, gridDim.x);
-  GItem it, prev{0, 0, 0, 0};
+  GItem it;
   while (w < nitems && !gitem(w, off2, G1, G, write_all, it)) w += gridDim.x;
-  uint4 rv[GP_R];
-  uint4 keep[GP_Q];  // writer: the previous item's sketch sw
-  bool have_prev = false;
-  if (!writer && w < nitems) gload(recs, it.a & ~3u, it.e, rv);
+  auto next_item = [&](uint32_t from) {  // the item after `from` (it = its bounds)
+    uint32_t wn = from + gridDim.x;
+    while (wn < nitems && !gitem(wn, off2, G1, G, write_all, it)) wn += gridDim.x;
+    return wn;
+  };
+  auto old_rows = [&]() {  // the next item's old registers into LDS (not the C5 bench path)
+    if (!pool_zero && w < nitems) {
+      lds_barrier();
+      const uint32_t n4 = (uint32_t)(G - it.g0 < GP_SK ? G - it.g0 : GP_SK) * (HLL_REGS / 16);
+      const uint4* gp = reinterpret_cast<const uint4*>(regs + it.g0 * HLL_REGS);
+      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
+    }
+  };
   // the LDS file of the first item
   if (pool_zero) {
     for (uint32_t q = threadIdx.x; q < GP_SK * HLL_REGS / 16; q += GP_T) lp[q] = make_uint4(0, 0, 0, 0);
@@ -377,12 +389,15 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
     const uint4* gp = reinterpret_cast<const uint4*>(regs + it.g0 * HLL_REGS);
     for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
   }
-  __syncthreads();
-  while (w < nitems || have_prev) {
-    const bool cur_ok = w < nitems;
-    // ---- [loaders: records of item w into LDS | writers: rows of prev out]
-    if (!writer) {
-      if (cur_ok) {
+  if (threadIdx.x < GP_LT) {
+    // ================================ loaders (waves 0-7): item w's records into LDS
+    uint4 rv[GP_R];
+    if (w < nitems) gload(recs, it.a & ~3u, it.e, rv);
+    __syncthreads();
+    bool have_prev = false;
+    while (w < nitems || have_prev) {
+      const bool cur_ok = w < nitems;
+      if (cur_ok) {  // [Z]
         const uint32_t half = w % GP_NP;
         for (uint32_t r0 = it.a & ~3u; r0 < it.e; r0 += RREC) {
           if (r0 != (it.a & ~3u)) gload(recs, r0, it.e, rv);  // the first round was prefetched
@@ -408,39 +423,62 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
           }
         }
       }
-    } else if (have_prev) {
-      const uint32_t nsk = (uint32_t)(G - prev.g0 < GP_SK ? G - prev.g0 : GP_SK);
-      const bool est = pc.pcount && prev.e0 - prev.a <= GP_CH;  // (a split bin's extra chunks change the rows later)
-      SumD sd{0.0, 0, 0};
-      if (sw < nsk) {
-        uint4* gp = reinterpret_cast<uint4*>(regs + (prev.g0 + sw) * HLL_REGS);
+      lds_barrier();
+      // [X] the next item's first round
+      const uint32_t wn = cur_ok ? next_item(w) : w;
+      if (cur_ok && wn < nitems) gload(recs, it.a & ~3u, it.e, rv);
+      have_prev = cur_ok;
+      w = wn;
+      old_rows();
+      lds_barrier();
+    }
+  } else {
+    // ================================ writers (waves 8-15): item w-1's rows out
+    const uint32_t sw = (threadIdx.x - GP_LT) >> 6, t = threadIdx.x - GP_LT;  // wave = sketch of the item
+    uint4 keep[GP_Q];
+    SumQ kq{0, 0, 0};
+    GItem prev{0, 0, 0, 0};
+    __syncthreads();
+    bool have_prev = false;
+    while (w < nitems || have_prev) {
+      const bool cur_ok = w < nitems;
+      if (have_prev) {  // [Z] store prev and sum its PFCOUNT terms
+        const uint32_t nsk = (uint32_t)(G - prev.g0 < GP_SK ? G - prev.g0 : GP_SK);
+        const bool est = pc.pcount && prev.e0 - prev.a <= GP_CH;  // (a split bin's extra chunks change the rows later)
+        SumD sd{0.0, 0, 0};
+        if (sw < nsk) {
+          uint4* gp = reinterpret_cast<uint4*>(regs + (prev.g0 + sw) * HLL_REGS);
 #pragma unroll
-        for (int u = 0; u < GP_Q; ++u) gp[u * 64 + lane] = keep[u];
-        if (est) {
+          for (int u = 0; u < GP_Q; ++u) gp[u * 64 + lane] = keep[u];
+          if (est) {
+            if (__any(kq.big != 0)) {  // a register >= 15 (rare here): the FP64 sum (uniform per wave = per sketch)
 #pragma unroll
-          for (int u = 0; u < GP_Q; ++u) {
-            acc_word(sd, keep[u].x);
-            acc_word(sd, keep[u].y);
-            acc_word(sd, keep[u].z);
-            acc_word(sd, keep[u].w);
+              for (int u = 0; u < GP_Q; ++u) {
+                acc_word(sd, keep[u].x);
+                acc_word(sd, keep[u].y);
+                acc_word(sd, keep[u].z);
+                acc_word(sd, keep[u].w);
+              }
+              sd = wave_reduce(sd);
+            } else {
+              SumQ q = kq;
+#pragma unroll
+              for (int o = 32; o > 0; o >>= 1) {
+                q.s += (uint32_t)__shfl_xor((int)q.s, o, 64);
+                q.ez += (uint32_t)__shfl_xor((int)q.ez, o, 64);
+              }
+              sd = SumD{(double)q.s * 0x1p-14, q.ez, 14};
+            }
           }
-          sd = wave_reduce(sd);
         }
+        if (lane == 0) part[sw] = sd;
       }
-      if (lane == 0) part[sw] = sd;
-    }
-    lds_barrier();
-    // ---- [writers: finish prev's estimates, read item w out of LDS and clear it | loaders: prefetch]
-    const GItem cur = it;
-    uint32_t wn = w;
-    if (cur_ok) {
-      wn = w + gridDim.x;
-      while (wn < nitems && !gitem(wn, off2, G1, G, write_all, it)) wn += gridDim.x;
-    }
-    if (writer) {
+      lds_barrier();
+      // [X] finish prev's estimates, read item w out of LDS and clear it
+      const GItem cur = it;
+      const uint32_t wn = cur_ok ? next_item(w) : w;
       if (have_prev && pc.pcount) {
         const uint32_t nsk = (uint32_t)(G - prev.g0 < GP_SK ? G - prev.g0 : GP_SK);
-        const uint32_t t = threadIdx.x - GP_LT;
         if (t < nsk) {  // one lane per sketch
           const uint64_t g = prev.g0 + t;
           const SumD p = part[t];
@@ -452,27 +490,25 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
           }
         }
       }
-      if (cur_ok) {
+      if (cur_ok) {  // (its fixed-point PFCOUNT terms summed on the way: kq)
+        kq = SumQ{0, 0, 0};
 #pragma unroll
         for (int u = 0; u < GP_Q; ++u) {
           const uint32_t q = sw * (HLL_REGS / 16) + u * 64 + lane;
           keep[u] = lp[q];
           if (pool_zero) lp[q] = make_uint4(0, 0, 0, 0);
+          accq_word(kq, keep[u].x);
+          accq_word(kq, keep[u].y);
+          accq_word(kq, keep[u].z);
+          accq_word(kq, keep[u].w);
         }
       }
-    } else if (cur_ok && wn < nitems) {
-      gload(recs, it.a & ~3u, it.e, rv);
-    }
-    have_prev = cur_ok;
-    prev = cur;
-    w = wn;
-    if (!pool_zero && w < nitems) {  // the next item's old registers (not the C5 bench path)
+      have_prev = cur_ok;
+      prev = cur;
+      w = wn;
+      old_rows();
       lds_barrier();
-      const uint32_t n4 = (uint32_t)(G - it.g0 < GP_SK ? G - it.g0 : GP_SK) * (HLL_REGS / 16);
-      const uint4* gp = reinterpret_cast<const uint4*>(regs + it.g0 * HLL_REGS);
-      for (uint32_t q = threadIdx.x; q < n4; q += GP_T) lp[q] = gp[q];
     }
-    lds_barrier();
   }
 }
 

@@ -52,6 +52,29 @@ RSK_DEV void acc_word(SumD& s, uint32_t w) {
   s.t += (pe(r0) + pe(r1)) + (pe(r2) + pe(r3));
 }
 
+// Registers below 15 (sparse sketches: the grouped add's fresh rows): 2^-r
+// as the integer 2^(14-r), two bytes per packed 16-bit shift summed by a
+// dot product -- 15 VALU per word against acc_word's ~25.  `big` flags a
+// byte of 15 or more (the caller then sums with acc_word).  A lane's 256
+// bytes sum below 2^22, a sketch's below 2^28; t = s 2^-14 is exact and,
+// with every register below 15, below 2^(53-14).
+struct SumQ {
+  uint32_t s;    // sum of 2^(14-r)
+  uint32_t ez;   // zero registers
+  uint32_t big;  // bit 7 of a byte set: a register >= 15
+};
+RSK_DEV void accq_word(SumQ& q, uint32_t w) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 base = {0x4000, 0x4000}, one = {1, 1};
+  const us2 r01 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(0u, w, 0x0c010c00u));  // bytes 0, 1 -> halves
+  const us2 r23 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(0u, w, 0x0c030c02u));  // bytes 2, 3 -> halves
+  q.s = __builtin_amdgcn_udot2(base >> r01, one, q.s, false);
+  q.s = __builtin_amdgcn_udot2(base >> r23, one, q.s, false);
+  const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+  q.ez += __popc(z);
+  q.big |= (w + 0x71717171u) & 0x80808080u;  // bytes <= 63: no carry between bytes
+}
+
 RSK_DEV SumD wave_reduce(SumD s) {
   for (int off = 32; off > 0; off >>= 1) {
     s.t += __shfl_down(s.t, off, 64);
