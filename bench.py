@@ -311,12 +311,12 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, rank: int = 0, world: i
 
 def insert_roofline(n: int, k: int, size: int, secs: float):
     """HBM view of the C3 insert: the streaming floor (every key read once, the
-    filter read and written once) and the super-tile pipeline's own traffic model
-    (st1 writes 4k B/key of probe tags, st2 reads and rewrites them, apply reads
-    them again), both as bytes / measured insert time."""
+    filter read and written once) and the append pipeline's own traffic model
+    (sa1 writes 4 B per probe, sa2h reads them and writes 2 B records, apply
+    reads those: 12 B per probe), both as bytes / measured insert time."""
     filt = (size + 7) // 8
     floor_b = 16.0 * n + 2.0 * filt
-    model_b = 16.0 * n + 16.0 * k * n + 2.0 * filt
+    model_b = 16.0 * n + 12.0 * k * n + 2.0 * filt
     return {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
             "algorithmic_bytes": floor_b, "achieved": floor_b / secs / 1e9,
             "frac": floor_b / secs / 1e9 / HBM_PEAK_GBS,
