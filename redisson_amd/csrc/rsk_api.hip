@@ -1455,10 +1455,28 @@ void op_complete(void* p) {
 AsyncOp* op_get(rsk_ctx* c, uint64_t host_bytes, uint64_t dev_bytes) {
   AsyncOp* op = nullptr;
   {
+    // Best fit: the smallest free op whose buffers already hold the call, else
+    // the largest one (grown below).  Growing frees and reallocates pinned and
+    // device memory, and hipFree waits for the device: taking ops LIFO made a
+    // pipelined C5 step (add, count, countWith, mergeWith: four sizes) regrow
+    // buffers every step, with the GPU idle behind each regrowth.
     std::lock_guard<std::mutex> g(c->async_mu);
-    if (!c->async_free.empty()) {
-      op = c->async_free.back();
-      c->async_free.pop_back();
+    size_t best = c->async_free.size();
+    for (size_t i = 0; i < c->async_free.size(); ++i) {
+      const AsyncOp* o = c->async_free[i];
+      const bool fits = o->h_bytes >= host_bytes && o->d_bytes >= dev_bytes;
+      if (best == c->async_free.size()) {
+        best = i;
+        continue;
+      }
+      const AsyncOp* b = c->async_free[best];
+      const bool bfits = b->h_bytes >= host_bytes && b->d_bytes >= dev_bytes;
+      if (fits && (!bfits || o->h_bytes + o->d_bytes < b->h_bytes + b->d_bytes)) best = i;
+      else if (!fits && !bfits && o->h_bytes + o->d_bytes > b->h_bytes + b->d_bytes) best = i;
+    }
+    if (best < c->async_free.size()) {
+      op = c->async_free[best];
+      c->async_free.erase(c->async_free.begin() + best);
     }
   }
   if (!op) {

@@ -611,7 +611,10 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
   const uint32_t cus = (uint32_t)c->num_cus;
-  constexpr uint32_t gpc = 2;  // gcount / gpart1 blocks per CU
+#ifndef RSK_GP_PC
+#define RSK_GP_PC 2
+#endif
+  constexpr uint32_t gpc = RSK_GP_PC;  // gcount / gpart1 blocks per CU
   const uint32_t G1 = gpc * cus;
   const uint64_t chunk = PROBE_CAP;
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
