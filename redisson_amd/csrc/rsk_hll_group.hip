@@ -42,14 +42,18 @@ constexpr int GP_E = GP_TILE / PT;
 
 // Group ids are read as uint4 (4 ids) with 4 loads in flight per lane when
 // the block's range is 16-byte aligned (the host keeps `per` a multiple of
-// 4; `aligned` = the ids' address is), one histogram per wave mod 4.
+// 4; `aligned` = the ids' address is).  16 histograms, one per (wave mod 4,
+// 16-lane group), rows padded so a bin's copies sit in different banks: lanes
+// of one LDS atomic contend only within their group, which matters for
+// skewed groups (Zipf(1.1): a third of the ids in one bin).
 __global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __restrict__ groups, uint64_t n,
                                                           uint64_t per, uint64_t G, uint32_t nbins, int aligned,
                                                           uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t h[4][PT];
-  for (uint32_t s = threadIdx.x; s < 4 * PT; s += GP_T) (&h[0][0])[s] = 0;
+  constexpr int NH = 16;
+  __shared__ uint32_t h[NH][PT + 1];  // + 1: a bin's 16 copies in 16 different banks
+  for (uint32_t s = threadIdx.x; s < NH * (PT + 1); s += GP_T) (&h[0][0])[s] = 0;
   __syncthreads();
-  uint32_t* hw = h[(threadIdx.x >> 6) & 3];
+  uint32_t* hw = h[(((threadIdx.x >> 6) & 3) << 2) | ((threadIdx.x & 63) >> 4)];
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
   auto add = [&](uint32_t g) {
@@ -74,8 +78,12 @@ __global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __rest
   }
   for (i += threadIdx.x; i < end; i += GP_T) add(__builtin_nontemporal_load(&groups[i]));
   __syncthreads();
-  for (uint32_t s = threadIdx.x; s < nbins; s += GP_T)
-    cnt[(uint64_t)s * gridDim.x + blockIdx.x] = h[0][s] + h[1][s] + h[2][s] + h[3][s];
+  for (uint32_t s = threadIdx.x; s < nbins; s += GP_T) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) t += h[k][s];
+    cnt[(uint64_t)s * gridDim.x + blockIdx.x] = t;
+  }
 }
 
 __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict__ keys,
