@@ -193,13 +193,14 @@ __global__ __launch_bounds__(GQ_T) void hll_gcount2p_kernel(const uint32_t* __re
                                                             const GPart* __restrict__ parts,
                                                             const uint32_t* __restrict__ d_nq,
                                                             uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t h[4][PT];  // one histogram per wave mod 4 (less contention)
+  constexpr int NH = 16;  // one histogram per (wave mod 4, 16-lane group), rows padded across banks (as hll_gcount)
+  __shared__ uint32_t h[NH][PT + 1];
   const uint32_t q = blockIdx.x;
   if (q >= *d_nq) return;  // uniform
   const GPart pt = parts[q];
-  for (uint32_t i = threadIdx.x; i < 4 * PT; i += GQ_T) (&h[0][0])[i] = 0;
+  for (uint32_t i = threadIdx.x; i < NH * (PT + 1); i += GQ_T) (&h[0][0])[i] = 0;
   __syncthreads();
-  uint32_t* hw = h[(threadIdx.x >> 6) & 3];
+  uint32_t* hw = h[(((threadIdx.x >> 6) & 3) << 2) | ((threadIdx.x & 63) >> 4)];
   for (uint32_t r0 = pt.lo & ~3u; r0 < pt.hi; r0 += GQ_TILE) {
     uint4 v[GQ_V];
     gq_load(recs, r0, pt.hi, v);
@@ -215,7 +216,10 @@ __global__ __launch_bounds__(GQ_T) void hll_gcount2p_kernel(const uint32_t* __re
   __syncthreads();
   if (threadIdx.x < PT) {
     const uint32_t f = threadIdx.x;
-    cnt[(uint64_t)pt.q0 * PT + (uint64_t)f * pt.nq + (q - pt.q0)] = h[0][f] + h[1][f] + h[2][f] + h[3][f];
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) t += h[k][f];
+    cnt[(uint64_t)pt.q0 * PT + (uint64_t)f * pt.nq + (q - pt.q0)] = t;
   }
 }
 
@@ -251,14 +255,26 @@ __global__ __launch_bounds__(GQ_T) void hll_gpart2p_kernel(const uint32_t* __res
   __shared__ uint32_t img[GQ_TILE];
   __shared__ uint8_t sbin[GQ_TILE];
   __shared__ uint32_t hist[PT], dlt[PT], cur[PT], wsum[GQ_T / 64];
+  __shared__ uint32_t s_hot;
   const uint32_t q = blockIdx.x;
   if (q >= *d_nq) return;  // uniform
   const GPart pt = parts[q];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_hot = 0;
+  __syncthreads();
   if (threadIdx.x < PT) {
-    cur[threadIdx.x] = offf[(uint64_t)pt.q0 * PT + (uint64_t)threadIdx.x * pt.nq + (q - pt.q0)];
+    const uint64_t ix = (uint64_t)pt.q0 * PT + (uint64_t)threadIdx.x * pt.nq + (q - pt.q0);
+    cur[threadIdx.x] = offf[ix];
     hist[threadIdx.x] = 0;
+    // a fine bin with more than an eighth of the part's records (skewed
+    // groups): its ranks are taken once per wave (ballot + one atomic), not
+    // by 64 lanes contending for one LDS word
+    const uint32_t c = offf[ix + 1] - offf[ix];
+    if ((uint64_t)c * 8 > (uint64_t)(pt.hi - pt.lo)) atomicMax(&s_hot, 0x100u | threadIdx.x);
   }
   __syncthreads();
+  const bool hot_mode = s_hot != 0;  // uniform
+  const uint32_t hot = s_hot & 0xFFu;
   for (uint32_t r0 = pt.lo & ~3u; r0 < pt.hi; r0 += GQ_TILE) {
     uint4 v[GQ_V];
     gq_load(recs, r0, pt.hi, v);
@@ -271,15 +287,24 @@ __global__ __launch_bounds__(GQ_T) void hll_gpart2p_kernel(const uint32_t* __res
       for (int m = 0; m < 4; ++m) {
         rec[4 * u + m] = x[m];
         tag[4 * u + m] = 0xFFFFFFFFu;
-        if (i0 + m >= pt.lo && i0 + m < pt.hi) {
-          const uint32_t b = x[m] >> 24;
-          tag[4 * u + m] = (b << 16) | atomicAdd(&hist[b], 1u);
+        const bool valid = i0 + m >= pt.lo && i0 + m < pt.hi;
+        const uint32_t b = x[m] >> 24;
+        const bool ish = hot_mode && valid && b == hot;
+        if (hot_mode) {
+          const uint64_t mh = __ballot(ish);
+          if (mh) {  // wave-uniform
+            const int leader = __builtin_ctzll(mh);
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(&hist[hot], (uint32_t)__popcll(mh));
+            base = (uint32_t)__shfl((int)base, leader, 64);
+            if (ish) tag[4 * u + m] = (hot << 16) | (base + (uint32_t)__popcll(mh & ((1ull << lane) - 1)));
+          }
         }
+        if (valid && !ish) tag[4 * u + m] = (b << 16) | atomicAdd(&hist[b], 1u);
       }
     }
     __syncthreads();
     // bin starts inside the tile (lanes 0..255: one bin each; four waves)
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t hv = 0, incl = 0;
     if (threadIdx.x < PT) {
       hv = hist[threadIdx.x];
