@@ -295,6 +295,32 @@ def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, route, G,
         L.rsk_hll_destroy(h)
 
 
+def test_grouped_partitioned_unaligned_group_ids(L, engine, orc, route):
+    """Device-resident pairs from element 1 on: the group ids are then not
+    16-byte aligned (hll_gcount's scalar path) while the keys are; the
+    partitioned add equals the direct kernel and the oracle."""
+    from redisson_amd import _lib, devmem
+
+    G, n = 5000, 2_000_003
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n + 1)
+    ks = k.keys_fixed(n, 16, offset=16).as_struct()
+    pools = {}
+    for mode in ("1", "0"):
+        route(gpart=1 if mode == "1" else -1)
+        h = _pool(L, engine, G)
+        _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr + 4))
+        pools[mode] = h
+    part, direct = (_pool_regs(L, engine, pools[m], G) for m in ("1", "0"))
+    assert np.array_equal(part, direct)
+    ref = np.zeros(G * 16384, np.uint8)
+    orc.hll_add_gen_grouped(ref, G, 0x5EED0006, 1, n)
+    assert np.array_equal(part, ref)
+    for h in pools.values():
+        L.rsk_hll_destroy(h)
+    g.free()
+    k.free()
+
+
 def test_grouped_partitioned_host_pairs_skip_out_of_range(L, engine, orc, route):
     """Host-resident pairs through the partitioned path: group ids >= G are
     ignored (as by the direct kernel), every other pair lands in its sketch;
