@@ -89,8 +89,11 @@ typedef struct rsk_keys {
  * 22-33; CommandAsyncService.java:86-105 completes a Netty promise the same
  * way).  status: RSK_OK (the call's device work finished); value: the reply
  * -- PFADD's changed flag (0/1), PFCOUNT's count, the number of keys of a
- * Bloom add/contains whose per-key outputs are in place.  It runs on a
- * runtime thread, once per accepted call, and must not call librsketch. */
+ * Bloom add/contains whose per-key outputs are in place.  It runs once per
+ * accepted call on the context's completion thread, in submission order
+ * (the stream only queues it there, so a slow callback does not hold up
+ * later device work), and must not call librsketch.  rsk_sync returns after
+ * every callback of the calls before it has returned. */
 typedef void (*rsk_done_fn)(void *user, int status, uint64_t value);
 
 /* ---------------------------------------------------------------- context */

@@ -440,6 +440,24 @@ FastMod63 make_fastmod(uint64_t d) {
   return f;
 }
 
+// Waits until every queued completion has run (its copy done, its callback
+// returned).  Completions take no context lock, so callers may hold it.
+void drain_done(rsk_ctx* c) {
+  std::unique_lock<std::mutex> lk(c->done_mu);
+  c->done_cv.wait(lk, [c] { return c->done_q.empty() && !c->done_busy; });
+}
+
+// Drains and joins the completion thread (the stream must be drained first,
+// so no host function can queue another op).
+void stop_done(rsk_ctx* c) {
+  {
+    std::lock_guard<std::mutex> g(c->done_mu);
+    c->done_stop = true;
+  }
+  c->done_cv.notify_all();
+  if (c->done_thr.joinable()) c->done_thr.join();
+}
+
 }  // namespace
 
 namespace rsk {
@@ -518,6 +536,7 @@ int rsk_shutdown(rsk_ctx* c) {
   int rc = guarded([&] {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    stop_done(c);
     rsk::prof_fold(c);
     for (auto e : c->prof.free_events) (void)hipEventDestroy(e);
     (void)hipFree(c->d_stage);
@@ -533,7 +552,7 @@ int rsk_shutdown(rsk_ctx* c) {
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_lc);
-    for (rsk::AsyncOp* op : c->async_all) {  // the stream is drained: every completion has run
+    for (rsk::AsyncOp* op : c->async_all) {  // stream and completion queue drained: every op is idle
       if (op->h_buf) (void)hipHostFree(op->h_buf);
       if (op->h_res) (void)hipHostFree(op->h_res);
       if (op->d_buf) (void)hipFree(op->d_buf);
@@ -570,6 +589,7 @@ int rsk_sync(rsk_ctx* c) {
     need(c != nullptr, "ctx is NULL");
     CtxLock l(c);
     RSK_HIP(hipStreamSynchronize(c->stream));
+    drain_done(c);
   });
 }
 
@@ -1421,9 +1441,9 @@ namespace {
 enum AsyncKind { K_PRESET = 0, K_RES_U64 = 1, K_HLL_FLAG = 2, K_OUT_BYTES = 3 };
 constexpr uint64_t ASYNC_STAGE_MAX = 256ull << 20;  // larger host batches run synchronously
 
-// Runs on the runtime's callback thread once the stream reaches it: no HIP
-// call here.  Derives the reply, copies per-key outputs to the caller, hands
-// the op back to the pool, then calls the caller.
+// Runs on the context's completion thread after the stream passed the op: no
+// HIP call here.  Derives the reply, copies per-key outputs to the caller,
+// hands the op back to the pool, then calls the caller.
 void op_complete(void* p) {
   auto* op = static_cast<AsyncOp*>(p);
   uint64_t v = op->value;
@@ -1531,10 +1551,42 @@ void op_release(AsyncOp* op) {  // an op that was taken but will not be submitte
   op->c->async_free.push_back(op);
 }
 
+void done_loop(rsk_ctx* c) {
+  std::unique_lock<std::mutex> lk(c->done_mu);
+  for (;;) {
+    c->done_cv.wait(lk, [c] { return c->done_stop || !c->done_q.empty(); });
+    if (c->done_q.empty()) return;  // stopping, queue drained
+    AsyncOp* op = c->done_q.front();
+    c->done_q.pop_front();
+    c->done_busy = true;
+    lk.unlock();
+    op_complete(op);
+    lk.lock();
+    c->done_busy = false;
+    if (c->done_q.empty()) c->done_cv.notify_all();  // drain_done waiters
+  }
+}
+
+// The stream's host function: queue the op and return at once.
+void op_reached(void* p) {
+  auto* op = static_cast<AsyncOp*>(p);
+  rsk_ctx* c = op->c;
+  {
+    std::lock_guard<std::mutex> g(c->done_mu);
+    c->done_q.push_back(op);
+  }
+  c->done_cv.notify_all();
+}
+
 void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
+  rsk_ctx* c = op->c;
   op->cb = cb;
   op->user = user;
-  RSK_HIP(hipLaunchHostFunc(op->c->stream, op_complete, op));
+  {
+    std::lock_guard<std::mutex> g(c->done_mu);
+    if (!c->done_thr.joinable()) c->done_thr = std::thread(done_loop, c);
+  }
+  RSK_HIP(hipLaunchHostFunc(c->stream, op_reached, op));
 }
 
 uint64_t al256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -1573,10 +1625,13 @@ DevKeys stage_keys(rsk_ctx* c, const rsk_keys* k, AsyncOp* op, uint64_t at) {
 // The synchronous call, then the callback on the calling thread (host batches
 // above ASYNC_STAGE_MAX: staging them whole would pin that much memory).
 template <class F>
-int run_now(F&& sync_call, rsk_done_fn cb, void* user, uint64_t value_if_void, bool value_from_call) {
+int run_now(rsk_ctx* c, F&& sync_call, rsk_done_fn cb, void* user, uint64_t value_if_void, bool value_from_call) {
   uint64_t v = value_if_void;
   const int rc = sync_call(&v);
-  if (rc == RSK_OK && cb) cb(user, RSK_OK, value_from_call ? v : value_if_void);
+  if (rc == RSK_OK && cb) {
+    drain_done(c);  // earlier calls' callbacks first
+    cb(user, RSK_OK, value_from_call ? v : value_if_void);
+  }
   return rc;
 }
 
@@ -1590,7 +1645,7 @@ int rsk_hll_add_async(rsk_hll* h, uint64_t id, const rsk_keys* keys, rsk_done_fn
     int rc = guarded([&] { kb = host_key_bytes(keys); });
     if (rc != RSK_OK) return rc;
     if (kb > ASYNC_STAGE_MAX)
-      return run_now([&](uint64_t* v) {
+      return run_now(h->ctx, [&](uint64_t* v) {
         uint8_t ch = 0;
         const int r = rsk_hll_add(h, id, keys, &ch);
         *v = ch;
@@ -1741,7 +1796,7 @@ int rsk_hll_add_grouped_async(rsk_hll* h, const rsk_keys* keys, const uint32_t* 
     uint64_t kb = 0;
     int rc = guarded([&] { kb = host_key_bytes(keys) + 4 * keys->n; });
     if (rc != RSK_OK) return rc;
-    if (kb > ASYNC_STAGE_MAX) return run_now([&](uint64_t*) { return rsk_hll_add_grouped(h, keys, groups); }, cb, user, 0, false);
+    if (kb > ASYNC_STAGE_MAX) return run_now(h->ctx, [&](uint64_t*) { return rsk_hll_add_grouped(h, keys, groups); }, cb, user, 0, false);
   }
   return guarded([&] {
     need(h != nullptr, "hll handle is NULL");
@@ -1862,7 +1917,7 @@ int bloom_async(rsk_bloom* b, const rsk_keys* keys, uint8_t* out, bool out_requi
     int rc = guarded([&] { kb = host_key_bytes(keys) + keys->n; });
     if (rc != RSK_OK) return rc;
     if (kb > ASYNC_STAGE_MAX)
-      return run_now([&](uint64_t*) { return sync_call(b, keys, out); }, cb, user, keys->n, false);
+      return run_now(b->ctx, [&](uint64_t*) { return sync_call(b, keys, out); }, cb, user, keys->n, false);
   }
   return guarded([&] {
     need(b != nullptr, "bloom handle is NULL");

@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <string>
 #include <vector>
@@ -145,11 +148,20 @@ struct rsk_ctx {
   // call number written by kernels that report "something changed" (no reset)
   uint32_t epoch = 0;
   rsk::Tuning tune;
-  // asynchronous calls: op pool (the completion runs on the runtime's
-  // callback thread and returns its op under async_mu)
+  // asynchronous calls: op pool (a completion returns its op under async_mu)
   std::mutex async_mu;
   std::vector<rsk::AsyncOp*> async_free;
   std::vector<rsk::AsyncOp*> async_all;
+  // completions: the stream's host function only queues its op here (the
+  // runtime runs host functions in stream order, so a slow one -- an 8 MB
+  // reply copy, a callback waiting for a lock -- would stall the kernels
+  // behind it); done_thr runs them in FIFO order
+  std::thread done_thr;
+  std::mutex done_mu;
+  std::condition_variable done_cv;
+  std::deque<rsk::AsyncOp*> done_q;
+  bool done_busy = false;
+  bool done_stop = false;
 
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);

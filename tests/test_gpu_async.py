@@ -305,3 +305,37 @@ def test_grouped_pipeline_matches_sync(engine):
     finally:
         ref.close()
         got.close()
+
+
+def test_callbacks_ordered_and_off_the_stream(L, engine):
+    """Callbacks fire in submission order on the context's completion thread;
+    a callback that blocks does not hold up later device work (a synchronous
+    call issued behind it returns while it is still blocked), and rsk_sync
+    returns only after every earlier callback has returned."""
+    from redisson_amd import _lib
+
+    h = _pool(L, engine, 2)
+    release = threading.Event()
+    order, released = [], []
+
+    def fire(user, status, value):
+        user = user or 0
+        if user == 1:
+            released.append(release.wait(20))
+        order.append((user, status))
+
+    fn = _lib.DONE_FN(fire)
+    try:
+        for u in range(1, 21):
+            _lib.check(L.rsk_hll_count_async(h, u % 2, fn, u))
+        out = np.zeros(2, np.uint64)
+        _lib.check(L.rsk_hll_count(h, None, 2, out.ctypes.data))  # behind 20 queued completions
+        assert out.tolist() == [0, 0]
+        release.set()
+        _lib.check(L.rsk_sync(engine.ctx))
+        assert released == [True], "the synchronous call waited for a blocked callback"
+        assert order == [(u, 0) for u in range(1, 21)]
+    finally:
+        release.set()
+        L.rsk_sync(engine.ctx)
+        L.rsk_hll_destroy(h)
