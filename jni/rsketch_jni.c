@@ -10,7 +10,7 @@
  * tests/c/shim_caller.c runs on the GPU.
  *
  * Async methods take the Netty Promise the Java object returns; the shim's
- * completion callback (a HIP runtime thread) attaches to the JVM and calls
+ * completion callback (the context's completion thread) attaches to the JVM and calls
  * RSketchNative.complete(promise, kind, value, replies), which completes it --
  * the listeners then run on the promise's executor (the Netty event loop), as
  * for a Redis reply (CommandAsyncService.java:86-105).
@@ -291,9 +291,9 @@ typedef struct {
   int64_t n;
 } job;
 
-/* The shim's callback, on a HIP runtime thread (or the calling thread for an
+/* The shim's callback, on the context's completion thread (or the calling thread for an
  * answer known at once): attach, complete the promise through Java, detach
- * nothing (daemon attachment stays for the runtime's thread). */
+ * nothing (daemon attachment stays for that thread). */
 static void jni_done(void *user, int status, uint64_t value) {
   job *j = user;
   JNIEnv *env = NULL;

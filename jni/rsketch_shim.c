@@ -577,7 +577,7 @@ static shim_async *async_new(space *s, rsk_done_fn cb, void *user, int32_t cap) 
   return a;
 }
 
-static void async_done(void *p, int status, uint64_t value) { /* runtime thread: no library call */
+static void async_done(void *p, int status, uint64_t value) { /* completion thread: no library call */
   shim_async *a = p;
   for (int32_t i = 0; i < a->m; ++i) release_ex(a->s, a->es[i], 1);
   if (a->cb) a->cb(a->user, status, value);

@@ -108,7 +108,7 @@ int rsk_shim_batch_hll_add(int64_t space, const char *const *names, int32_t n_na
                            rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, uint8_t *replies, int64_t replies_len);
 
 /* Asynchronous twins (RHyperLogLogAsync.java:22-33): cb(user, status, value)
- * fires once per accepted call, from a runtime thread (value: the reply, as
+ * fires once per accepted call, from the context's completion thread (value: the reply, as
  * rsketch.h's rsk_done_fn); a refused call returns the error and never fires.
  * A count of a missing key fires on the calling thread with 0. */
 int rsk_shim_hll_add_async(int64_t space, const char *name, rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n,
