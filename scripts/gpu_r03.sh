@@ -52,6 +52,11 @@ for p in ${PART//,/ }; do
       rm -rf gpurun_out/calib_fetch
       step calib 120 python3 scripts/fetch_calib.py || exit 1
       step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- python3 scripts/fetch_calib.py || exit 1 ;;
+    sq)  # SQ instruction / wait counters of the C5 and C4 kernels (one PMC pass each)
+      SQC="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
+      rm -rf gpurun_out/sq_c5 gpurun_out/sq_c4
+      step sq_c5 200 rocprofv3 --pmc $SQC --output-format csv -d gpurun_out/sq_c5 -o run -- python3 bench.py --workload c5 --steps 3 --warmup 2 --no-cpu || exit 1
+      step sq_c4 200 rocprofv3 --pmc $SQC --output-format csv -d gpurun_out/sq_c4 -o run -- python3 bench.py --workload c4 --steps 3 --warmup 2 --no-cpu || exit 1 ;;
     prof)
       B="python3 bench.py --no-cpu --no-bloom-replies"
       rm -rf gpurun_out/prof_stats
