@@ -444,6 +444,7 @@ FastMod63 make_fastmod(uint64_t d) {
 // returned).  Completions take no context lock, so callers may hold it.
 void drain_done(rsk_ctx* c) {
   std::unique_lock<std::mutex> lk(c->done_mu);
+  if (c->done_thr.get_id() == std::this_thread::get_id()) return;  // a callback calling in: do not wait for itself
   c->done_cv.wait(lk, [c] { return c->done_q.empty() && !c->done_busy; });
 }
 

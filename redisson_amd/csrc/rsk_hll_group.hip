@@ -372,12 +372,41 @@ RSK_DEV bool gitem(uint32_t w, const uint32_t* __restrict__ off2, uint32_t G1, u
   it.g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
   return !((it.a == it.e && !write_all) || it.g0 >= G);  // uniform across the workgroup
 }
-// a round of records from r0 (a multiple of 4): loader lane l loads uint4 r0/4 + l + GP_LT u
+// a round of records from r0 (a multiple of 4): loader lane l loads uint4 r0/4 + l + GP_LT u.
+// Every load is issued (lanes past e load uint4 0 instead; gapply_round drops
+// records at or past e by index), so the compiler's load counts are static
+// and waiting for one round does not wait for a round issued after it.
 RSK_DEV void gload(const uint32_t* __restrict__ recs, uint32_t r0, uint32_t e, uint4 (&rv)[GP_R]) {
 #pragma unroll
   for (int u = 0; u < GP_R; ++u) {
     const uint32_t q = r0 / 4 + threadIdx.x + u * GP_LT;
-    rv[u] = 4 * q < e ? ld_nt16(reinterpret_cast<const uint4*>(recs) + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    rv[u] = ld_nt16(reinterpret_cast<const uint4*>(recs) + (4 * q < e ? q : 0u));
+  }
+}
+
+// One round of records (loaded by gload at r0) maxed into the LDS file:
+// records of [a, e) whose sketch falls in this half.
+RSK_DEV void gapply_round(const uint4 (&rv)[GP_R], uint32_t r0, uint32_t a, uint32_t e, uint32_t half,
+                          uint32_t* r32) {
+#pragma unroll
+  for (int u = 0; u < GP_R; ++u) {
+    const uint32_t q = r0 / 4 + threadIdx.x + u * GP_LT;
+    const uint32_t x[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t r = x[m], i = 4 * q + m;
+      const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
+      if (i < a || i >= e || sk / GP_SK != half) continue;
+      const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
+      const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
+      uint32_t* word = &r32[byte >> 2];
+      uint32_t old = *word;
+      while (((old >> sh) & 0xFFu) < rank) {
+        const uint32_t pv = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+        if (pv == old) break;
+        old = pv;
+      }
+    }
   }
 }
 
@@ -424,44 +453,46 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
   }
   if (threadIdx.x < GP_LT) {
     // ================================ loaders (waves 0-7): item w's records into LDS
-    uint4 rv[GP_R];
-    if (w < nitems) gload(recs, it.a & ~3u, it.e, rv);
+    // The next item's first round is issued at the start of this item's
+    // apply (into rn, moved to rv in [X]), so it has the whole [Z] to land
+    // instead of [X] alone.
+    uint4 rv[GP_R], rn[GP_R];
+    GItem itn = it;
+    uint32_t wn = w;
+    if (w < nitems) {
+      gload(recs, it.a & ~3u, it.e, rv);
+      wn = w + gridDim.x;
+      while (wn < nitems && !gitem(wn, off2, G1, G, write_all, itn)) wn += gridDim.x;
+    }
     __syncthreads();
     bool have_prev = false;
     while (w < nitems || have_prev) {
       const bool cur_ok = w < nitems;
       if (cur_ok) {  // [Z]
-        const uint32_t half = w % GP_NP;
-        for (uint32_t r0 = it.a & ~3u; r0 < it.e; r0 += RREC) {
-          if (r0 != (it.a & ~3u)) gload(recs, r0, it.e, rv);  // the first round was prefetched
-#pragma unroll
-          for (int u = 0; u < GP_R; ++u) {
-            const uint32_t q = r0 / 4 + threadIdx.x + u * GP_LT;
-            const uint32_t x[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-              const uint32_t r = x[m], i = 4 * q + m;
-              const uint32_t sk = (r >> 20) & 15u;  // sketch within the fine bin
-              if (i < it.a || i >= it.e || sk / GP_SK != half) continue;
-              const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
-              const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
-              uint32_t* word = &r32[byte >> 2];
-              uint32_t old = *word;
-              while (((old >> sh) & 0xFFu) < rank) {
-                const uint32_t pv = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
-                if (pv == old) break;
-                old = pv;
-              }
-            }
-          }
+        const bool pf = wn < nitems;
+        gload(recs, pf ? itn.a & ~3u : 0u, pf ? itn.e : 0u, rn);  // (unconditional: see gload)
+        // the first round (prefetched) apart from the rest, so waiting for it
+        // does not wait for rn
+        const uint32_t half = w % GP_NP, r00 = it.a & ~3u;
+        if (r00 < it.e) gapply_round(rv, r00, it.a, it.e, half, r32);
+        for (uint32_t r0 = r00 + RREC; r0 < it.e; r0 += RREC) {
+          gload(recs, r0, it.e, rv);
+          gapply_round(rv, r0, it.a, it.e, half, r32);
         }
+#pragma unroll
+        for (int u = 0; u < GP_R; ++u) rv[u] = rn[u];
       }
       lds_barrier();
-      // [X] the next item's first round
-      const uint32_t wn = cur_ok ? next_item(w) : w;
-      if (cur_ok && wn < nitems) gload(recs, it.a & ~3u, it.e, rv);
+      // [X]
       have_prev = cur_ok;
-      w = wn;
+      if (cur_ok) {
+        w = wn;
+        it = itn;
+        if (w < nitems) {
+          wn = w + gridDim.x;
+          while (wn < nitems && !gitem(wn, off2, G1, G, write_all, itn)) wn += gridDim.x;
+        }
+      }
       old_rows();
       lds_barrier();
     }
