@@ -350,8 +350,9 @@ constexpr uint32_t GP_CH = 1u << 20;
 // One workgroup per CU (128 KiB of LDS), persistent, its waves specialised:
 // waves 0-7 (loaders) load an item's records and max them into the LDS file;
 // waves 8-15 (writers) hold the previous item's rows in registers (one
-// sketch per wave, 16 uint4 per lane), store them and sum their PFCOUNT
-// terms meanwhile.  gfx9 counts a wave's loads and stores in one in-order
+// sketch per wave, 16 uint4 per lane), sum their PFCOUNT terms and store them
+// while the loaders apply the next item (the read-out phase, where the
+// loaders wait, only copies the rows out of LDS and clears it).  gfx9 counts a wave's loads and stores in one in-order
 // vmcnt, so a wave that stored 128 KiB and then loads records waits for the
 // stores before it can use them; split this way the loaders' counters hold
 // loads only (their next round is issued during the hand-over) and the
@@ -500,7 +501,6 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
     // ================================ writers (waves 8-15): item w-1's rows out
     const uint32_t sw = (threadIdx.x - GP_LT) >> 6, t = threadIdx.x - GP_LT;  // wave = sketch of the item
     uint4 keep[GP_Q];
-    SumQ kq{0, 0, 0};
     GItem prev{0, 0, 0, 0};
     __syncthreads();
     bool have_prev = false;
@@ -511,6 +511,16 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
         const bool est = pc.pcount && prev.e0 - prev.a <= GP_CH;  // (a split bin's extra chunks change the rows later)
         SumD sd{0.0, 0, 0};
         if (sw < nsk) {
+          SumQ kq{0, 0, 0};  // fixed-point PFCOUNT terms (here, not in [X], where the loaders wait)
+          if (est) {
+#pragma unroll
+            for (int u = 0; u < GP_Q; ++u) {
+              accq_word(kq, keep[u].x);
+              accq_word(kq, keep[u].y);
+              accq_word(kq, keep[u].z);
+              accq_word(kq, keep[u].w);
+            }
+          }
           uint4* gp = reinterpret_cast<uint4*>(regs + (prev.g0 + sw) * HLL_REGS);
 #pragma unroll
           for (int u = 0; u < GP_Q; ++u) gp[u * 64 + lane] = keep[u];
@@ -538,7 +548,7 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
         if (lane == 0) part[sw] = sd;
       }
       lds_barrier();
-      // [X] finish prev's estimates, read item w out of LDS and clear it
+      // [X] finish prev's estimates, read item w out of LDS and clear it (no arithmetic: the loaders wait)
       const GItem cur = it;
       const uint32_t wn = cur_ok ? next_item(w) : w;
       if (have_prev && pc.pcount) {
@@ -554,17 +564,12 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
           }
         }
       }
-      if (cur_ok) {  // (its fixed-point PFCOUNT terms summed on the way: kq)
-        kq = SumQ{0, 0, 0};
+      if (cur_ok) {
 #pragma unroll
         for (int u = 0; u < GP_Q; ++u) {
           const uint32_t q = sw * (HLL_REGS / 16) + u * 64 + lane;
           keep[u] = lp[q];
           if (pool_zero) lp[q] = make_uint4(0, 0, 0, 0);
-          accq_word(kq, keep[u].x);
-          accq_word(kq, keep[u].y);
-          accq_word(kq, keep[u].z);
-          accq_word(kq, keep[u].w);
         }
       }
       have_prev = cur_ok;
