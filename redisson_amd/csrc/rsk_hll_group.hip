@@ -521,9 +521,12 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
               accq_word(kq, keep[u].w);
             }
           }
-          uint4* gp = reinterpret_cast<uint4*>(regs + (prev.g0 + sw) * HLL_REGS);
+          u32x4* gp = reinterpret_cast<u32x4*>(regs + (prev.g0 + sw) * HLL_REGS);
 #pragma unroll
-          for (int u = 0; u < GP_Q; ++u) gp[u * 64 + lane] = keep[u];
+          for (int u = 0; u < GP_Q; ++u) {  // streaming stores: rows are written once, read back by later calls only
+            const u32x4 x = {keep[u].x, keep[u].y, keep[u].z, keep[u].w};
+            __builtin_nontemporal_store(x, gp + u * 64 + lane);
+          }
           if (est) {
             if (__any(kq.big != 0)) {  // a register >= 15 (rare here): the FP64 sum (uniform per wave = per sketch)
 #pragma unroll
