@@ -268,7 +268,7 @@ __global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restri
     for (uint32_t o = threadIdx.x; o < RB_BITS; o += RA_T) {  // a wave covers 64 bits = words o/32, o/32 + 1
       const uint32_t v = ms[o];
       const uint32_t was = f0[o >> 5] & bloom_bit_mask(o);
-      fkb[o] = was ? NONE : v;
+      __builtin_nontemporal_store(was ? NONE : v, &fkb[o]);  // read back by rp_reply's gathers only
       const uint64_t hit = __ballot(v != NONE);
       if (lane == 0 || lane == 32) {
         const uint32_t lo = (uint32_t)(lane == 0 ? hit : hit >> 32);

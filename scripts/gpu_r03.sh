@@ -37,6 +37,8 @@ for p in ${PART//,/ }; do
       step bench_c5_zipf 200 python bench.py --workload c5 --zipf 1.1 || exit 1 ;;
     routes)
       step routes 600 python -u scripts/insert_routes.py gpurun_out/ins_routes.json "$@" || exit 1 ;;
+    replies)  # C3 add() with replies, 1B keys (scripts/reply_profile.py)
+      step reply_bench 300 python3 scripts/reply_profile.py 1000000000 2 || exit 1 ;;
     c5prof)
       step c5prof 300 python scripts/c5_host_profile.py 500000000 1000000 10 || exit 1 ;;
     insprof)  # the reply-less C3 insert alone: kernel trace, then one PMC pass per counter group
