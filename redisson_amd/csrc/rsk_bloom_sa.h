@@ -298,7 +298,10 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
       if (d != INVALID) {
         const uint4 v = img4[g];
         u32x4 x = {v.x, v.y, v.z, v.w};
-        *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
+        // 8-byte records (the replies pipeline's rp1): streaming stores measured 19.4 -> 18.4 ms;
+        // 4-byte records (the insert's sa1): no gain
+        if constexpr (sizeof(R) == 8) __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(mine + (RG * g + d)));
+        else *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
       }
     }
   };
