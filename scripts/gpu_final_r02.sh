@@ -27,7 +27,7 @@ if [ "$PART" = all ] || [ "$PART" = prof ]; then
   python3 scripts/prof_agree.py gpurun_out/prof_stats gpurun_out/prof_bench.log gpurun_out/${TAG}_roofline_check.json
   step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- $B || exit 1
   step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- $B || exit 1
-  python3 scripts/pmc_summary.py gpurun_out/prof_stats gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/${TAG}_pmc 1000000000 \
+  FETCH_CALIB='{"segment_256B": 2.0}' python3 scripts/pmc_summary.py gpurun_out/prof_stats gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/${TAG}_pmc 1000000000 \
     '{"workload": "c2", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}'
   C5="python3 bench.py --workload c5"
   step prof5 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5_stats -o run -- $C5 || exit 1
