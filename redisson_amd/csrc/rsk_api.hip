@@ -445,7 +445,7 @@ FastMod63 make_fastmod(uint64_t d) {
 void drain_done(rsk_ctx* c) {
   std::unique_lock<std::mutex> lk(c->done_mu);
   if (c->done_thr.get_id() == std::this_thread::get_id()) return;  // a callback calling in: do not wait for itself
-  c->done_cv.wait(lk, [c] { return c->done_q.empty() && !c->done_busy; });
+  c->done_cv.wait(lk, [c] { return c->done_delivered == c->done_submitted && !c->done_busy; });
 }
 
 // Drains and joins the completion thread (the stream must be drained first,
@@ -511,6 +511,8 @@ int rsk_init(const rsk_options* opts, rsk_ctx** out) {
     c->num_cus = prop.multiProcessorCount;
     RSK_HIP(hipSetDevice(c->device));
     RSK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    RSK_HIP(hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
+    RSK_HIP(hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
     c->stage_bytes = o.staging_bytes ? o.staging_bytes : (256ull << 20);
     c->stage_threads = o.stage_threads ? o.stage_threads : 8;
     c->slab_count = std::min<uint32_t>(RSK_MAX_SLABS, 8u * (uint32_t)c->num_cus);
@@ -537,6 +539,8 @@ int rsk_shutdown(rsk_ctx* c) {
   int rc = guarded([&] {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->xin) (void)hipStreamSynchronize(c->xin);
+    if (c->xout) (void)hipStreamSynchronize(c->xout);
     stop_done(c);
     rsk::prof_fold(c);
     for (auto e : c->prof.free_events) (void)hipEventDestroy(e);
@@ -557,12 +561,16 @@ int rsk_shutdown(rsk_ctx* c) {
       if (op->h_buf) (void)hipHostFree(op->h_buf);
       if (op->h_res) (void)hipHostFree(op->h_res);
       if (op->d_buf) (void)hipFree(op->d_buf);
+      if (op->ev_in) (void)hipEventDestroy(op->ev_in);
+      if (op->ev_out) (void)hipEventDestroy(op->ev_out);
       delete op;
     }
     c->async_all.clear();
     c->async_free.clear();
     if (c->comm) (void)rsk_comm_destroy(c);
     (void)hipStreamDestroy(c->stream);
+    if (c->xin) (void)hipStreamDestroy(c->xin);
+    if (c->xout) (void)hipStreamDestroy(c->xout);
   });
   delete c;
   return rc;
@@ -575,6 +583,8 @@ int rsk_trim(rsk_ctx* c) {
     need(c != nullptr, "ctx is NULL");
     CtxLock l(c);
     RSK_HIP(hipStreamSynchronize(c->stream));
+    RSK_HIP(hipStreamSynchronize(c->xin));
+    RSK_HIP(hipStreamSynchronize(c->xout));
     RSK_HIP(hipFree(c->d_work));
     RSK_HIP(hipFree(c->d_out));
     c->d_work = c->d_out = nullptr;
@@ -590,6 +600,8 @@ int rsk_sync(rsk_ctx* c) {
     need(c != nullptr, "ctx is NULL");
     CtxLock l(c);
     RSK_HIP(hipStreamSynchronize(c->stream));
+    RSK_HIP(hipStreamSynchronize(c->xin));
+    RSK_HIP(hipStreamSynchronize(c->xout));
     drain_done(c);
   });
 }
@@ -937,8 +949,10 @@ void merge_batch_check(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_
 // hb: pinned host buffer of merge_batch_host_bytes(n); d: device scratch of
 // merge_batch_dev_bytes(n) -- pointer arrays built in hb, one DMA, one merge
 // launch per level, one cache invalidation for the batch.
+void op_stage_in(AsyncOp* op, void* dst, const void* src, uint64_t bytes);  // (below)
+
 void merge_batch_enqueue(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* src_ids, uint64_t n, uint8_t* hb,
-                         uint8_t* d) {
+                         uint8_t* d, AsyncOp* op = nullptr) {
   rsk_ctx* c = h->ctx;
   for (uint64_t i = 0; i < n && !h->imported.empty(); ++i) hll_forget_import(h, dst_ids[i]);
   if (h->lv.size() != h->n) {
@@ -991,7 +1005,8 @@ void merge_batch_enqueue(rsk_hll* h, const uint64_t* dst_ids, const uint64_t* sr
   auto* d_dst = reinterpret_cast<uint8_t**>(d);
   auto* d_src = reinterpret_cast<const uint8_t**>(d + seg);
   auto* d_ids = reinterpret_cast<uint64_t*>(d + 2 * seg);
-  RSK_HIP(hipMemcpyAsync(d_dst, dps, 3 * seg, hipMemcpyHostToDevice, c->stream));  // pointers and ids, one DMA
+  if (op) op_stage_in(op, d_dst, dps, 3 * seg);  // pointers and ids, one DMA (async call: on the input stream)
+  else RSK_HIP(hipMemcpyAsync(d_dst, dps, 3 * seg, hipMemcpyHostToDevice, c->stream));
   for (uint32_t l = 1; l <= max_level; ++l)
     hll_merge_launch(c, d_dst + start[l], d_src + start[l], 1, start[l + 1] - start[l]);
   // PFMERGE invalidates every destination's cache (one launch for the batch).
@@ -1544,6 +1559,15 @@ AsyncOp* op_get(rsk_ctx* c, uint64_t host_bytes, uint64_t dev_bytes) {
   op->n_out = 0;
   op->created = false;
   op->epoch = 0;
+  op->on_xfer = false;
+  if (!op->ev_in) {
+    if (hipEventCreateWithFlags(&op->ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&op->ev_out, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      give_back();
+      throw RskError{RSK_ERR_OUT_OF_MEMORY, "event creation for an asynchronous call failed"};
+    }
+  }
   return op;
 }
 
@@ -1554,29 +1578,52 @@ void op_release(AsyncOp* op) {  // an op that was taken but will not be submitte
 
 void done_loop(rsk_ctx* c) {
   std::unique_lock<std::mutex> lk(c->done_mu);
+  auto ready = [c] { return !c->done_arrived.empty() && c->done_arrived.begin()->first == c->done_delivered + 1; };
   for (;;) {
-    c->done_cv.wait(lk, [c] { return c->done_stop || !c->done_q.empty(); });
-    if (c->done_q.empty()) return;  // stopping, queue drained
-    AsyncOp* op = c->done_q.front();
-    c->done_q.pop_front();
+    c->done_cv.wait(lk, [&] { return ready() || (c->done_stop && c->done_delivered == c->done_submitted); });
+    if (!ready()) return;  // stopping, every op delivered
+    AsyncOp* op = c->done_arrived.begin()->second;
+    c->done_arrived.erase(c->done_arrived.begin());
     c->done_busy = true;
     lk.unlock();
     op_complete(op);
     lk.lock();
     c->done_busy = false;
-    if (c->done_q.empty()) c->done_cv.notify_all();  // drain_done waiters
+    ++c->done_delivered;
+    c->done_cv.notify_all();  // drain_done waiters
   }
 }
 
-// The stream's host function: queue the op and return at once.
+// A stream's host function: file the op and return at once.
 void op_reached(void* p) {
   auto* op = static_cast<AsyncOp*>(p);
   rsk_ctx* c = op->c;
   {
     std::lock_guard<std::mutex> g(c->done_mu);
-    c->done_q.push_back(op);
+    c->done_arrived.emplace(op->seq, op);
   }
   c->done_cv.notify_all();
+}
+
+// Inputs of an async call: host (pinned, inside op->h_buf) -> device on the
+// input stream (so they are not queued behind an earlier call's read-back);
+// the context stream waits for them before its next launch.
+void op_stage_in(AsyncOp* op, void* dst, const void* src, uint64_t bytes) {
+  rsk_ctx* c = op->c;
+  RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->xin));
+  RSK_HIP(hipEventRecord(op->ev_in, c->xin));
+  RSK_HIP(hipStreamWaitEvent(c->stream, op->ev_in, 0));
+}
+
+// Outputs of an async call (device memory owned by the op): read back on the
+// output stream once the context stream's work so far is done; the call then
+// completes on the output stream.
+void op_read_back(AsyncOp* op, void* dst, const void* src, uint64_t bytes) {
+  rsk_ctx* c = op->c;
+  RSK_HIP(hipEventRecord(op->ev_out, c->stream));
+  RSK_HIP(hipStreamWaitEvent(c->xout, op->ev_out, 0));
+  RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->xout));
+  op->on_xfer = true;
 }
 
 void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
@@ -1586,8 +1633,16 @@ void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
   {
     std::lock_guard<std::mutex> g(c->done_mu);
     if (!c->done_thr.joinable()) c->done_thr = std::thread(done_loop, c);
+    op->seq = ++c->done_submitted;  // (callers hold the context lock: one submitter at a time)
   }
-  RSK_HIP(hipLaunchHostFunc(c->stream, op_reached, op));
+  const hipError_t e = hipLaunchHostFunc(op->on_xfer ? c->xout : c->stream, op_reached, op);
+  if (e != hipSuccess) {
+    {
+      std::lock_guard<std::mutex> g(c->done_mu);
+      --c->done_submitted;
+    }
+    RSK_HIP(e);
+  }
 }
 
 uint64_t al256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -1610,15 +1665,14 @@ DevKeys stage_keys(rsk_ctx* c, const rsk_keys* k, AsyncOp* op, uint64_t at) {
   if (!k->offsets) {
     const uint64_t bytes = k->n * k->fixed_len;
     par_copy(op->h_buf + at, src, bytes, c->stage_threads);
-    RSK_HIP(hipMemcpyAsync(op->d_buf + at, op->h_buf + at, bytes, hipMemcpyHostToDevice, c->stream));
+    op_stage_in(op, op->d_buf + at, op->h_buf + at, bytes);
     return DevKeys{op->d_buf + at, nullptr, k->n, k->fixed_len};
   }
   for (uint64_t i = 0; i < k->n; ++i) need(k->offsets[i + 1] >= k->offsets[i], "offsets must be non-decreasing");
   const uint64_t base = k->offsets[0], data_bytes = al256(k->offsets[k->n] - base);
   par_copy(op->h_buf + at, src + base, k->offsets[k->n] - base, c->stage_threads);
   std::memcpy(op->h_buf + at + data_bytes, k->offsets, 8 * (k->n + 1));
-  RSK_HIP(hipMemcpyAsync(op->d_buf + at, op->h_buf + at, data_bytes + 8 * (k->n + 1), hipMemcpyHostToDevice,
-                         c->stream));
+  op_stage_in(op, op->d_buf + at, op->h_buf + at, data_bytes + 8 * (k->n + 1));
   // offsets stay absolute: shift the data pointer instead of rebasing
   return DevKeys{op->d_buf + at - base, reinterpret_cast<const uint64_t*>(op->d_buf + at + data_bytes), k->n, 0};
 }
@@ -1781,7 +1835,7 @@ int rsk_hll_merge_batch_async(rsk_hll* h, const uint64_t* dst_ids, const uint64_
     merge_batch_check(h, dst_ids, src_ids, n);
     AsyncOp* op = op_get(c, n ? merge_batch_host_bytes(n) : 0, n ? merge_batch_dev_bytes(n) : 0);
     try {
-      if (n) merge_batch_enqueue(h, dst_ids, src_ids, n, op->h_buf, op->d_buf);
+      if (n) merge_batch_enqueue(h, dst_ids, src_ids, n, op->h_buf, op->d_buf, op);
       op_submit(op, cb, user);
     } catch (...) {
       (void)hipStreamSynchronize(c->stream);
@@ -1816,7 +1870,7 @@ int rsk_hll_add_grouped_async(rsk_hll* h, const rsk_keys* keys, const uint32_t* 
         const uint32_t* d_groups = groups;
         if (host) {
           std::memcpy(op->h_buf + kb, groups, 4 * keys->n);
-          RSK_HIP(hipMemcpyAsync(op->d_buf + kb, op->h_buf + kb, 4 * keys->n, hipMemcpyHostToDevice, c->stream));
+          op_stage_in(op, op->d_buf + kb, op->h_buf + kb, 4 * keys->n);
           d_groups = reinterpret_cast<const uint32_t*>(op->d_buf + kb);
         }
         hll_add_grouped_enqueue(h, dk, d_groups, host ? groups : nullptr);
@@ -1846,13 +1900,13 @@ int rsk_hll_count_ids_async(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_
         uint64_t* d_ids = nullptr;
         if (ids) {
           std::memcpy(op->h_buf, ids, 8 * n);
-          RSK_HIP(hipMemcpyAsync(op->d_buf, op->h_buf, 8 * n, hipMemcpyHostToDevice, c->stream));
+          op_stage_in(op, op->d_buf, op->h_buf, 8 * n);
           d_ids = reinterpret_cast<uint64_t*>(op->d_buf);
         }
         auto* d_out = reinterpret_cast<uint64_t*>(op->d_buf + ib);
         hll_count_launch(c, h->d_regs, h->d_card, d_ids, SmallIds{}, n, d_out,
                          PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
-        RSK_HIP(hipMemcpyAsync(op->h_buf + ib, d_out, 8 * n, hipMemcpyDeviceToHost, c->stream));
+        op_read_back(op, op->h_buf + ib, d_out, 8 * n);
         op->h_out = op->h_buf + ib;
         op->user_out = reinterpret_cast<uint8_t*>(out);
         op->n_out = 8 * n;
@@ -1887,9 +1941,9 @@ int rsk_hll_count_union_batch_async(rsk_hll* h, const uint64_t* member_ids, uint
         }
         auto* d_ptrs = reinterpret_cast<const uint8_t**>(op->d_buf);
         auto* d_out = reinterpret_cast<uint64_t*>(op->d_buf + pb);
-        RSK_HIP(hipMemcpyAsync(d_ptrs, ptrs, 8 * n * arity, hipMemcpyHostToDevice, c->stream));
+        op_stage_in(op, d_ptrs, ptrs, 8 * n * arity);
         hll_union_count_launch(c, d_ptrs, arity, n, d_out);
-        RSK_HIP(hipMemcpyAsync(op->h_buf + pb, d_out, 8 * n, hipMemcpyDeviceToHost, c->stream));
+        op_read_back(op, op->h_buf + pb, d_out, 8 * n);
         op->h_out = op->h_buf + pb;
         op->user_out = reinterpret_cast<uint8_t*>(out);
         op->n_out = 8 * n;
@@ -1936,7 +1990,7 @@ int bloom_async(rsk_bloom* b, const rsk_keys* keys, uint8_t* out, bool out_requi
       uint8_t* d_out = out ? (host ? op->d_buf + kb : out) : nullptr;
       if (dk.n) launch(c, b, dk, d_out);
       if (host && out && keys->n) {
-        RSK_HIP(hipMemcpyAsync(op->h_buf + kb, d_out, keys->n, hipMemcpyDeviceToHost, c->stream));
+        op_read_back(op, op->h_buf + kb, d_out, keys->n);
         op->h_out = op->h_buf + kb;
         op->user_out = out;
         op->n_out = keys->n;

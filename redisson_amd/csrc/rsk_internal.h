@@ -5,7 +5,6 @@
 #include <stdint.h>
 
 #include <condition_variable>
-#include <deque>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -59,8 +58,9 @@ struct Tuning {
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the
 // op's own pinned buffer (so the caller may reuse them at once), its result
-// is read back into pinned memory on the context stream, and a host function
-// enqueued behind it (hipLaunchHostFunc) computes the reply and invokes the
+// is read back into pinned memory (large ones on the transfer stream), and a
+// host function enqueued behind it (hipLaunchHostFunc) files the op for the
+// context's completion thread, which computes the reply and invokes the
 // caller's callback.  Ops and their buffers are recycled.
 struct AsyncOp {
   rsk_ctx* c = nullptr;
@@ -78,6 +78,12 @@ struct AsyncOp {
   uint8_t* h_out = nullptr;   // per-key outputs read back (inside h_buf)
   uint8_t* user_out = nullptr;
   uint64_t n_out = 0;
+  // copy-stream ordering: ev_in (inputs staged on c->xin, the context stream
+  // waits for it), ev_out (the context stream's work done, c->xout waits for
+  // it before the read-back); on_xfer: completes on c->xout
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  bool on_xfer = false;
+  uint64_t seq = 0;         // submission number: callbacks run in this order
 };
 
 struct ProfEntry {
@@ -152,14 +158,21 @@ struct rsk_ctx {
   std::mutex async_mu;
   std::vector<rsk::AsyncOp*> async_free;
   std::vector<rsk::AsyncOp*> async_all;
-  // completions: the stream's host function only queues its op here (the
+  // asynchronous calls' host->device input copies (xin) and device->host
+  // read-backs (xout) run on two more streams, ordered against the context
+  // stream by events, so they overlap the kernels of earlier calls instead of
+  // queueing between them (and inputs never wait behind a read-back)
+  hipStream_t xin = nullptr, xout = nullptr;
+  // completions: a stream's host function only files its op here (the
   // runtime runs host functions in stream order, so a slow one -- an 8 MB
-  // reply copy, a callback waiting for a lock -- would stall the kernels
-  // behind it); done_thr runs them in FIFO order
+  // reply copy, a callback waiting for a lock -- would stall the work behind
+  // it); done_thr runs them in submission order (ops reach it from two
+  // streams, so out of order at times)
   std::thread done_thr;
   std::mutex done_mu;
   std::condition_variable done_cv;
-  std::deque<rsk::AsyncOp*> done_q;
+  std::map<uint64_t, rsk::AsyncOp*> done_arrived;  // by seq
+  uint64_t done_submitted = 0, done_delivered = 0;
   bool done_busy = false;
   bool done_stop = false;
 
