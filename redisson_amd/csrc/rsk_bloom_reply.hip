@@ -10,7 +10,7 @@
 // bit (t* <= t < k-1) found it clear; otherwise every one of them followed an
 // earlier key's probe (or the bit was set before the batch).  Instead of
 // sorting all k n (bit, p) pairs, this path partitions 8-byte records
-// (key << 32 | offset) down to 2 KiB blocks of the filter and takes the
+// (key << 32 | offset) down to 2 KiB blocks (2^14 bits) of the filter and takes the
 // minimum key per bit in LDS:
 //
 //   rp1, rp2 : the append partition's sa1 / sa2 (rsk_bloom_sa.h) with 8-byte
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__
 }
 
 // ---------------------------------------------------------------- rp_apply
-// Workgroup = block b (bits [b 2^15, (b + 1) 2^15)): every segment of it in
+// Workgroup = block b (bits [b 2^14, (b + 1) 2^14), RB_LOG = 14): every segment of it in
 // its slice's rp3 tiles (wave w takes tiles w, w + 16, ...; 4 records per lane
 // in flight), atomicMin of the key into minkey; then fk[bit] and the filter words,
 // 64 bits per wave step (a ballot of "touched" is the MSB-first word pair).
