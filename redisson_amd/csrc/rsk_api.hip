@@ -836,8 +836,8 @@ void hll_add_grouped_enqueue(rsk_hll* h, const DevKeys& dk, const uint32_t* d_gr
   hll_forget_imports(h);
   const bool pool_zero = h->zero;
   hll_touch(h);
-  hll_mark_groups(h, host_groups, dk.n);
   hll_add_grouped_chunk(h, dk, d_groups, pool_zero);
+  hll_mark_groups(h, host_groups, dk.n);  // host bookkeeping after the launches: the device starts sooner
   hll_add_grouped_finish(h);
 }
 }  // namespace
@@ -1635,7 +1635,14 @@ void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
     if (!c->done_thr.joinable()) c->done_thr = std::thread(done_loop, c);
     op->seq = ++c->done_submitted;  // (callers hold the context lock: one submitter at a time)
   }
-  const hipError_t e = hipLaunchHostFunc(op->on_xfer ? c->xout : c->stream, op_reached, op);
+  // every call completes on the output stream (after an event for the
+  // context stream's part): a host function on the context stream would hold
+  // the kernels queued behind it for the runtime's round trip (~40 us)
+  if (!op->on_xfer) {
+    RSK_HIP(hipEventRecord(op->ev_out, c->stream));
+    RSK_HIP(hipStreamWaitEvent(c->xout, op->ev_out, 0));
+  }
+  const hipError_t e = hipLaunchHostFunc(c->xout, op_reached, op);
   if (e != hipSuccess) {
     {
       std::lock_guard<std::mutex> g(c->done_mu);
