@@ -1571,7 +1571,10 @@ AsyncOp* op_get(rsk_ctx* c, uint64_t host_bytes, uint64_t dev_bytes) {
   return op;
 }
 
-void op_release(AsyncOp* op) {  // an op that was taken but will not be submitted
+void op_release(AsyncOp* op) {  // an op that was taken but will not be submitted (error paths)
+  // its copies on the copy streams may still be in flight into its buffers
+  (void)hipStreamSynchronize(op->c->xin);
+  (void)hipStreamSynchronize(op->c->xout);
   std::lock_guard<std::mutex> g(op->c->async_mu);
   op->c->async_free.push_back(op);
 }
@@ -1630,11 +1633,6 @@ void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
   rsk_ctx* c = op->c;
   op->cb = cb;
   op->user = user;
-  {
-    std::lock_guard<std::mutex> g(c->done_mu);
-    if (!c->done_thr.joinable()) c->done_thr = std::thread(done_loop, c);
-    op->seq = ++c->done_submitted;  // (callers hold the context lock: one submitter at a time)
-  }
   // every call completes on the output stream (after an event for the
   // context stream's part): a host function on the context stream would hold
   // the kernels queued behind it for the runtime's round trip (~40 us)
@@ -1642,8 +1640,13 @@ void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
     RSK_HIP(hipEventRecord(op->ev_out, c->stream));
     RSK_HIP(hipStreamWaitEvent(c->xout, op->ev_out, 0));
   }
+  {
+    std::lock_guard<std::mutex> g(c->done_mu);
+    if (!c->done_thr.joinable()) c->done_thr = std::thread(done_loop, c);
+    op->seq = ++c->done_submitted;  // (callers hold the context lock: one submitter at a time)
+  }
   const hipError_t e = hipLaunchHostFunc(c->xout, op_reached, op);
-  if (e != hipSuccess) {
+  if (e != hipSuccess) {  // never filed: take its number back
     {
       std::lock_guard<std::mutex> g(c->done_mu);
       --c->done_submitted;
