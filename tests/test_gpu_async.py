@@ -339,3 +339,49 @@ def test_callbacks_ordered_and_off_the_stream(L, engine):
         release.set()
         L.rsk_sync(engine.ctx)
         L.rsk_hll_destroy(h)
+
+
+def test_async_reads_back_state_at_call_time(engine):
+    """Read-backs run on the output copy stream and staged inputs on the
+    input stream: an async count still answers with the pool as it stood at
+    its call, when a synchronous add to the same pool follows at once, and an
+    async add of host keys whose buffer is overwritten after the call adds
+    the keys as they were."""
+    from redisson_amd import KeyBatch
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    G = 3000
+    rng = np.random.default_rng(11)
+    ka = np.frombuffer(rng.bytes(16 * 200_000), np.uint8).reshape(-1, 16).copy()
+    ga = rng.integers(0, G, len(ka), dtype=np.uint32)
+    kb = np.frombuffer(rng.bytes(16 * 150_000), np.uint8).reshape(-1, 16).copy()
+    gb = rng.integers(0, G, len(kb), dtype=np.uint32)
+    ref, got = GroupedHyperLogLog(engine, G), GroupedHyperLogLog(engine, G)
+    try:
+        ref.add(KeyBatch.from_numpy(ka), ga)
+        c_a = ref.count().copy()
+        ref.add(KeyBatch.from_numpy(kb), gb)
+        c_ab = ref.count().copy()
+        for _ in range(3):
+            got.clear()
+            got.add(KeyBatch.from_numpy(ka), ga)
+            out1, out2 = np.zeros(G, np.uint64), np.zeros(G, np.uint64)
+            op1 = got.count_async(out1)
+            got.add(KeyBatch.from_numpy(kb), gb)  # synchronous, right behind the async count
+            op2 = got.count_async(out2)
+            op1.wait(60)
+            op2.wait(60)
+            assert np.array_equal(out1, c_a)
+            assert np.array_equal(out2, c_ab)
+            got.clear()
+            hk = ka.copy()
+            op3 = got.add_async(KeyBatch.from_numpy(hk), ga)
+            hk[:] = 0  # the call staged its own copy
+            out3 = np.zeros(G, np.uint64)
+            op4 = got.count_async(out3)
+            op3.wait(60)
+            op4.wait(60)
+            assert np.array_equal(out3, c_a)
+    finally:
+        ref.close()
+        got.close()
