@@ -51,13 +51,43 @@ __global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ cnt) {
   constexpr int NH = 16;
   __shared__ uint32_t h[NH][PT + 1];  // + 1: a bin's 16 copies in 16 different banks
+  __shared__ uint32_t s_hot;
   for (uint32_t s = threadIdx.x; s < NH * (PT + 1); s += GP_T) (&h[0][0])[s] = 0;
-  __syncthreads();
-  uint32_t* hw = h[(((threadIdx.x >> 6) & 3) << 2) | ((threadIdx.x & 63) >> 4)];
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
+  // The block's most frequent bin in its first GP_T ids (a sample; skewed
+  // groups -- Zipf -- put a third of all ids in one bin): its lanes of a wave
+  // are counted with one atomic (ballot + popcount) instead of one each.
+  {
+    const uint64_t i = begin + threadIdx.x;
+    const uint32_t g = i < end ? groups[i] : 0xFFFFFFFFu;
+    __syncthreads();
+    if (g < G) atomicAdd(&h[0][g >> GP_BIN_SHIFT], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      uint32_t best = 0, bv = 0;
+      for (uint32_t b = threadIdx.x; b < PT; b += 64)
+        if (h[0][b] > bv) bv = h[0][b], best = b;
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t ov = __shfl_xor(bv, o, 64), ob = __shfl_xor(best, o, 64);
+        if (ov > bv || (ov == bv && ob < best)) bv = ov, best = ob;
+      }
+      if (threadIdx.x == 0) s_hot = best;
+    }
+    __syncthreads();
+    if (threadIdx.x < PT) h[0][threadIdx.x] = 0;
+    __syncthreads();
+  }
+  const uint32_t hot = s_hot, lane = threadIdx.x & 63;
+  uint32_t* hw = h[(((threadIdx.x >> 6) & 3) << 2) | ((threadIdx.x & 63) >> 4)];
   auto add = [&](uint32_t g) {
-    if (g < G) atomicAdd(&hw[g >> GP_BIN_SHIFT], 1u);
+    const bool in = g < G, ishot = in && (g >> GP_BIN_SHIFT) == hot;
+    const uint64_t m = __ballot(ishot);
+    if (ishot) {
+      if (lane == (uint32_t)__builtin_ctzll(m)) atomicAdd(&hw[hot], (uint32_t)__builtin_popcountll(m));
+    } else if (in) {
+      atomicAdd(&hw[g >> GP_BIN_SHIFT], 1u);
+    }
   };
   uint64_t i = begin;
   if (aligned) {
