@@ -380,6 +380,11 @@ def main():
         shard.init_comm(engine)
     elif not args.no_bloom and args.workload == "c2":
         shard.init_comm_single(engine)  # the node-level Bloom merge runs through the same call at N = 1
+    # what RCCL itself reports (ncclCommCount): every rank must have joined
+    rccl_nranks, rccl_rank = shard.comm_info(engine)
+    if world > 1 and (rccl_nranks, rccl_rank) != (world, rank):
+        raise SystemExit("RCCL reports %d ranks (this one %d), WORLD_SIZE is %d (RANK %d)"
+                         % (rccl_nranks, rccl_rank, world, rank))
     wl = args.workload
     n = args.keys if args.keys is not None else (500_000_000 if wl == "c5" else 1_000_000_000)
     extra = {}
@@ -463,11 +468,22 @@ def main():
     engine.prof_reset()
     engine.prof_enable(True)
     barrier()
+    cards = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         card = step()
+        cards.append(card)
     barrier()
     elapsed = time.perf_counter() - t0
+    cards_agree = None
+    if world > 1 and wl != "c5":
+        # after each step's RCCL MAX all-reduce every rank holds the same
+        # registers, so every rank's count() of every step must agree
+        everyone = [None] * world
+        dist.all_gather_object(everyone, cards)
+        cards_agree = all(c == cards for c in everyone)
+        if not cards_agree:
+            raise SystemExit("count() differs between ranks after the all-reduce: %r" % (everyone,))
     engine.prof_enable(False)
     add_ms, add_launches = engine.prof_read(kern)
     kern_label = kern + "_kernel"
@@ -528,7 +544,10 @@ def main():
                      "algorithmic_bytes_per_launch": unit_bytes},
         "side_kernels_ms_per_launch": {k: (v[0] / v[1] if v[1] else None) for k, v in side.items()},
         "count": int(card),
+        "rccl_nranks": rccl_nranks,
     }
+    if cards_agree is not None:
+        result["count_identical_across_ranks_every_step"] = cards_agree
     pmc_cfg = {"workload": wl, "keys": n, "zipf": args.zipf,
                "bloom_keys": args.bloom_keys if (wl == "c2" and not args.no_bloom) else 0}
     tr = pmc_traffic("hll_add_grouped_partitioned" if stage_ms else kern + "_kernel", pmc_cfg)

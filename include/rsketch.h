@@ -42,7 +42,10 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
-#define RSK_ABI_VERSION 1
+/* rsk_abi_version() returns this; a caller built against another header must
+ * not call in.  2: rsk_options is 24 bytes (stage_threads, reserved) and the
+ * asynchronous entry points exist (1 had a 16-byte rsk_options). */
+#define RSK_ABI_VERSION 2
 #define RSK_HLL_REGISTERS 16384
 #define RSK_HLL_DENSE_BYTES 12304 /* 16-byte "HYLL" header + 12288 register bytes */
 
@@ -87,13 +90,20 @@ typedef struct rsk_keys {
 /* Completion callback of the asynchronous entry points (rsk_*_async), the
  * C side of RHyperLogLogAsync / RBloomFilter futures (RHyperLogLogAsync.java:
  * 22-33; CommandAsyncService.java:86-105 completes a Netty promise the same
- * way).  status: RSK_OK (the call's device work finished); value: the reply
- * -- PFADD's changed flag (0/1), PFCOUNT's count, the number of keys of a
- * Bloom add/contains whose per-key outputs are in place.  It runs once per
- * accepted call on the context's completion thread, in submission order
- * (the stream only queues it there, so a slow callback does not hold up
- * later device work), and must not call librsketch.  rsk_sync returns after
- * every callback of the calls before it has returned. */
+ * way).  status: RSK_OK (the call's device work finished) or RSK_ERR_DEVICE
+ * (a device error on the context's streams: value 0, per-key outputs not
+ * written, and every later call on the context fails with RSK_ERR_DEVICE);
+ * value: the reply -- PFADD's changed flag (0/1), PFCOUNT's count, the number
+ * of keys of a Bloom add/contains whose per-key outputs are in place.  It runs
+ * once per accepted call on the context's completion thread, in submission
+ * order (the stream only queues it there, so a slow callback does not hold up
+ * later device work).  A callback may call librsketch again, synchronously or
+ * asynchronously, on any context -- except rsk_shutdown of its own context; a
+ * call it makes runs while later callbacks wait, so a callback that blocks on
+ * the completion of a LATER asynchronous call of its own context deadlocks
+ * (as a Netty listener that blocks on its own event loop does).  rsk_sync
+ * returns after the callbacks of every call issued before it have returned
+ * (it does not hold the context while it waits for them). */
 typedef void (*rsk_done_fn)(void *user, int status, uint64_t value);
 
 /* ---------------------------------------------------------------- context */
@@ -286,6 +296,17 @@ int rsk_bitset_bitop(int op, rsk_bitset *dst, rsk_bitset *const *srcs, uint32_t 
 int rsk_bitset_get_bytes(rsk_bitset *b, uint8_t *buf, size_t cap, size_t *len);
 int rsk_bitset_set_bytes(rsk_bitset *b, const uint8_t *buf, size_t len);
 int rsk_bitset_clear(rsk_bitset *b);
+/* A Bloom filter's bit string as an RBitSet.  In Redis the filter's bits ARE
+ * the string key `name` (RedissonBloomFilter SETBITs it, RedissonBitSet GETs
+ * it), so getBitSet(filterName) -- Redisson.java:515-517, RedissonBatch.java:191
+ * -- reads and writes them: every rsk_bitset_* call above works on the view.
+ * STRLEN is Redis's (the highest byte a SETBIT touched + 1: for the filter's
+ * own adds, which only set bits, the last non-zero byte + 1), so GET returns
+ * the bytes Redis would; writes through the view change the filter.  The view
+ * cannot grow the string past the filter's ceil(size/8) bytes (such a SETBIT /
+ * SET / BITOP is refused with RSK_ERR_INVALID_ARG).  rsk_bitset_destroy of
+ * the view releases only the view; destroy every view before its filter. */
+int rsk_bloom_bitset(rsk_bloom *b, rsk_bitset **out);
 
 /* ------------------------------------------------------- device memory */
 /* HBM buffers for keys / replies that stay resident (JNI: wrap as direct
@@ -306,6 +327,9 @@ int rsk_memset(rsk_ctx *ctx, void *p, int value, uint64_t bytes);
 int rsk_comm_unique_id(uint8_t *id_out);
 int rsk_comm_init(rsk_ctx *ctx, int nranks, int rank, const uint8_t *id);
 int rsk_comm_destroy(rsk_ctx *ctx);
+/* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank), so
+ * a caller can check that every rank joined; 1 and 0 without one. */
+int rsk_comm_info(rsk_ctx *ctx, int *nranks, int *rank);
 /* Sketch id := register-wise MAX over all ranks (ncclAllReduce uint8 MAX,
  * in place, 16 KiB).  Equals PFMERGE of the ranks' sketches; the cache is
  * invalidated. */

@@ -1,17 +1,19 @@
 /*
  * RBatch for GPU sketches (RedissonBatch.java:55-83 getHyperLogLog, :226-233
  * execute; RedissonBatch on Redis pipelines the queued commands in one flush).
- * getHyperLogLog(name) returns an RHyperLogLogAsync whose calls are queued and
+ * getHyperLogLog(name) / getBitSet(name) (:191) return async objects whose calls are queued and
  * answered by execute(), in the order they were queued: every run of queued
  * add()s -- whatever names they go to -- becomes ONE native call
  * (rsk_shim_batch_hll_add: one rsk_hll_add_each per name, replies in input
- * order); the other calls run in their queue position.  executeAsync() does the
+ * order), every run of queued SETBITs on one name with one value becomes ONE
+ * rsk_bitset_setbits call; the other calls run in their queue position.  executeAsync() does the
  * same off the calling thread's future.  The futures the queued calls return
  * complete with their replies when execute() runs.
  */
 package org.redisson.gpu;
 
 import java.util.ArrayList;
+import java.util.BitSet;
 import java.util.Collection;
 import java.util.List;
 
@@ -19,6 +21,7 @@ import io.netty.util.concurrent.Future;
 import io.netty.util.concurrent.Promise;
 
 import org.redisson.client.codec.Codec;
+import org.redisson.core.RBitSetAsync;
 import org.redisson.core.RHyperLogLogAsync;
 
 public final class GpuBatch {
@@ -50,6 +53,21 @@ public final class GpuBatch {
         }
     }
 
+    /* setAsync(bit[, value]) / clearAsync(bit): a run of them on one name with
+     * one value becomes one SETBIT-many call (rsk_bitset_setbits). */
+    private static final class SetBitOp extends Op {
+        final String name;
+        final long index;
+        final boolean value;
+
+        SetBitOp(Promise<Object> p, String name, long index, boolean value) {
+            super(p);
+            this.name = name;
+            this.index = index;
+            this.value = value;
+        }
+    }
+
     private static final class CallOp extends Op {
         final java.util.concurrent.Callable<Object> call;
 
@@ -73,6 +91,12 @@ public final class GpuBatch {
         return new BatchHyperLogLog<V>(name, codec);
     }
 
+    /* RBatch.getBitSet (RedissonBatch.java:191): on a Bloom filter's name it
+     * reads and writes the filter's bits, as GpuBitSet does. */
+    public RBitSetAsync getBitSet(String name) {
+        return new BatchBitSet(name);
+    }
+
     /* Runs the queued calls; their replies, in queue order (RBatch.execute). */
     public synchronized List<?> execute() {
         if (executed) {
@@ -88,6 +112,15 @@ public final class GpuBatch {
                     j++;
                 }
                 runAdds(ops.subList(i, j));
+                i = j;
+            } else if (ops.get(i) instanceof SetBitOp) {
+                SetBitOp first = (SetBitOp) ops.get(i);
+                int j = i;
+                while (j < ops.size() && ops.get(j) instanceof SetBitOp && ((SetBitOp) ops.get(j)).name.equals(first.name)
+                        && ((SetBitOp) ops.get(j)).value == first.value) {
+                    j++;
+                }
+                runSetBits(ops.subList(i, j));
                 i = j;
             } else {
                 CallOp c = (CallOp) ops.get(i++);
@@ -144,6 +177,222 @@ public final class GpuBatch {
             for (Op op : run) {
                 op.promise.setFailure(e);
             }
+        }
+    }
+
+    private void runSetBits(List<Op> run) {
+        SetBitOp first = (SetBitOp) run.get(0);
+        long[] indexes = new long[run.size()];
+        for (int q = 0; q < run.size(); q++) {
+            indexes[q] = ((SetBitOp) run.get(q)).index;
+        }
+        try {
+            RSketchNative.bitsetSetBits(gpu.space, first.name, indexes, first.value);
+            for (Op op : run) {
+                op.promise.setSuccess(null);
+            }
+        } catch (RuntimeException e) {
+            for (Op op : run) {
+                op.promise.setFailure(e);
+            }
+        }
+    }
+
+    private final class BatchBitSet implements RBitSetAsync {
+        private final String name;
+
+        BatchBitSet(String name) {
+            this.name = name;
+        }
+
+        private Promise<Object> promise() {
+            return gpu.newPromise();
+        }
+
+        private <R> Future<R> call(java.util.concurrent.Callable<Object> c) {
+            return queue(new CallOp(promise(), c));
+        }
+
+        private <R> Future<R> op(final int op, final String... others) {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    RSketchNative.bitsetOp(gpu.space, name, op, others);
+                    return null;
+                }
+            });
+        }
+
+        public String getName() {
+            return name;
+        }
+
+        public Future<byte[]> toByteArrayAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return RSketchNative.bitsetGet(gpu.space, name);
+                }
+            });
+        }
+
+        public Future<Long> lengthAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return Long.valueOf(RSketchNative.bitsetLength(gpu.space, name));
+                }
+            });
+        }
+
+        public Future<Void> setAsync(final long fromIndex, final long toIndex, final boolean value) {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    RSketchNative.bitsetSetRange(gpu.space, name, fromIndex, toIndex, value);
+                    return null;
+                }
+            });
+        }
+
+        public Future<Void> clearAsync(long fromIndex, long toIndex) {
+            return setAsync(fromIndex, toIndex, false);
+        }
+
+        public Future<Void> setAsync(long fromIndex, long toIndex) {
+            return setAsync(fromIndex, toIndex, true);
+        }
+
+        public Future<Void> setAsync(BitSet bs) {
+            final byte[] bytes = GpuBitSet.encode(bs);
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    RSketchNative.bitsetSet(gpu.space, name, bytes);
+                    return null;
+                }
+            });
+        }
+
+        public Future<Void> notAsync() {
+            return op(RSketchNative.BITOP_NOT);
+        }
+
+        public Future<Integer> sizeAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return Integer.valueOf((int) (RSketchNative.bitsetStrlen(gpu.space, name) * 8));
+                }
+            });
+        }
+
+        public Future<Boolean> getAsync(final long bitIndex) {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return Boolean.valueOf(RSketchNative.bitsetGetBits(gpu.space, name, new long[] {bitIndex})[0]);
+                }
+            });
+        }
+
+        public Future<Void> setAsync(long bitIndex) {
+            return setAsync(bitIndex, true);
+        }
+
+        public Future<Void> setAsync(long bitIndex, boolean value) {
+            return queue(new SetBitOp(promise(), name, bitIndex, value));
+        }
+
+        public Future<Long> cardinalityAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return Long.valueOf(RSketchNative.bitsetCardinality(gpu.space, name));
+                }
+            });
+        }
+
+        public Future<Void> clearAsync(long bitIndex) {
+            return setAsync(bitIndex, false);
+        }
+
+        public Future<Void> clearAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    RSketchNative.bitsetClear(gpu.space, name);
+                    return null;
+                }
+            });
+        }
+
+        public Future<Void> orAsync(String... bitSetNames) {
+            return op(RSketchNative.BITOP_OR, bitSetNames);
+        }
+
+        public Future<Void> andAsync(String... bitSetNames) {
+            return op(RSketchNative.BITOP_AND, bitSetNames);
+        }
+
+        public Future<Void> xorAsync(String... bitSetNames) {
+            return op(RSketchNative.BITOP_XOR, bitSetNames);
+        }
+
+        public Future<Boolean> deleteAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return Boolean.valueOf(RSketchNative.bitsetClear(gpu.space, name));
+                }
+            });
+        }
+
+        public Future<Boolean> isExistsAsync() {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return Boolean.valueOf(RSketchNative.bitsetStrlen(gpu.space, name) > 0);
+                }
+            });
+        }
+
+        public Future<Void> renameAsync(final String newName) {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    GpuKeyspace.rename(gpu, name, newName, false);
+                    return null;
+                }
+            });
+        }
+
+        public Future<Boolean> renamenxAsync(final String newName) {
+            return call(new java.util.concurrent.Callable<Object>() {
+                public Object call() {
+                    return GpuKeyspace.rename(gpu, name, newName, true);
+                }
+            });
+        }
+
+        public Future<Void> migrateAsync(String host, int port, int database) {
+            return gpu.failed(GpuKeyspace.notOnGpu("migrate"));
+        }
+
+        public Future<Boolean> moveAsync(int database) {
+            return gpu.failed(GpuKeyspace.notOnGpu("move"));
+        }
+
+        public Future<Boolean> expireAsync(long timeToLive, java.util.concurrent.TimeUnit timeUnit) {
+            return gpu.failed(GpuKeyspace.noTtl());
+        }
+
+        public Future<Boolean> expireAtAsync(long timestamp) {
+            return gpu.failed(GpuKeyspace.noTtl());
+        }
+
+        public Future<Boolean> expireAtAsync(java.util.Date timestamp) {
+            return gpu.failed(GpuKeyspace.noTtl());
+        }
+
+        public Future<Boolean> clearExpireAsync() {
+            Promise<Boolean> p = gpu.newPromise();
+            p.setSuccess(Boolean.FALSE);
+            return p;
+        }
+
+        public Future<Long> remainTimeToLiveAsync() {
+            Promise<Long> p = gpu.newPromise();
+            p.setSuccess(Long.valueOf(-1));
+            return p;
         }
     }
 

@@ -127,10 +127,11 @@ public class GpuBloomFilter<T> extends RedissonBloomFilter<T> {
                 readConfig();
             }
             if (add) {
-                RSketchNative.bloomAddAsync(gpu.space, getName(), size, hashIterations, kb.bytes, kb.offsets, kb.n, p);
+                RSketchNative.bloomAddAsync(gpu.space, getName(), size, hashIterations, kb.bytes, kb.offsets, kb.n,
+                        gpu.completion(p));
             } else {
                 RSketchNative.bloomContainsAsync(gpu.space, getName(), size, hashIterations, kb.bytes, kb.offsets, kb.n,
-                        p);
+                        gpu.completion(p));
             }
         } catch (RedisException e) {
             if (e.getMessage() != null && e.getMessage().contains(CONFIG_CHANGED)) {

@@ -96,7 +96,7 @@ public class GpuHyperLogLog<V> extends RedissonHyperLogLog<V> {
         Promise<Boolean> p = gpu.newPromise();
         try {
             KeyBuffer kb = KeyBuffer.encode(valueCodec, objects);
-            RSketchNative.hllAddAsync(gpu.space, getName(), kb.bytes, kb.offsets, kb.n, p);
+            RSketchNative.hllAddAsync(gpu.space, getName(), kb.bytes, kb.offsets, kb.n, gpu.completion(p));
         } catch (RuntimeException e) {
             p.tryFailure(e);
         }
@@ -107,7 +107,7 @@ public class GpuHyperLogLog<V> extends RedissonHyperLogLog<V> {
     public Future<Long> countAsync() {
         Promise<Long> p = gpu.newPromise();
         try {
-            RSketchNative.hllCountAsync(gpu.space, getName(), p);
+            RSketchNative.hllCountAsync(gpu.space, getName(), gpu.completion(p));
         } catch (RuntimeException e) {
             p.tryFailure(e);
         }
@@ -118,7 +118,7 @@ public class GpuHyperLogLog<V> extends RedissonHyperLogLog<V> {
     public Future<Long> countWithAsync(String... otherLogNames) {
         Promise<Long> p = gpu.newPromise();
         try {
-            RSketchNative.hllCountWithAsync(gpu.space, withSelf(otherLogNames), p);
+            RSketchNative.hllCountWithAsync(gpu.space, withSelf(otherLogNames), gpu.completion(p));
         } catch (RuntimeException e) {
             p.tryFailure(e);
         }
@@ -129,7 +129,7 @@ public class GpuHyperLogLog<V> extends RedissonHyperLogLog<V> {
     public Future<Void> mergeWithAsync(String... otherLogNames) {
         Promise<Void> p = gpu.newPromise();
         try {
-            RSketchNative.hllMergeWithAsync(gpu.space, getName(), otherLogNames, p);
+            RSketchNative.hllMergeWithAsync(gpu.space, getName(), otherLogNames, gpu.completion(p));
         } catch (RuntimeException e) {
             p.tryFailure(e);
         }

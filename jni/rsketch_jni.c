@@ -9,24 +9,56 @@
  * shim (all checks, the name -> object keyspace, the config guard) is what
  * tests/c/shim_caller.c runs on the GPU.
  *
- * Async methods take the Netty Promise the Java object returns; the shim's
- * completion callback (the context's completion thread) attaches to the JVM and calls
- * RSketchNative.complete(promise, kind, value, replies), which completes it --
- * the listeners then run on the promise's executor (the Netty event loop), as
- * for a Redis reply (CommandAsyncService.java:86-105).
+ * Async methods take a Completion (RSketchNative.java: the Netty promise and
+ * the executor its listeners run on).  The shim's callback runs on the
+ * library's completion thread: it attaches that thread to the JVM once (as a
+ * daemon), and calls RSketchNative.complete(completion, kind, status, value,
+ * replies), which only hands the result to the completion's executor -- the
+ * Netty event loop GpuSketchContext pinned, as a Redis reply is decoded and
+ * its promise completed on a connection's event loop
+ * (CommandAsyncService.java:86-105) -- so user listeners never run on the
+ * library's thread.  The class and method are resolved once, in JNI_OnLoad
+ * (which runs inside RSketchNative's static initializer, so FindClass sees the
+ * class loader that loaded the binding: a natively attached thread would only
+ * see the system loader).  A result is never dropped: if the completion
+ * thread cannot attach, the job is parked and delivered by the next native
+ * call (or RSketchNative.reap) on any Java thread.
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "rsketch_shim.h"
 
 static JavaVM *g_vm;
+static jclass g_native;      /* global ref: org.redisson.gpu.RSketchNative */
+static jmethodID g_complete; /* static void complete(Object, int, int, long, boolean[]) */
+
+static void reap(JNIEnv *env); /* delivers parked completions (below) */
 
 JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM *vm, void *reserved) {
   (void)reserved;
+  JNIEnv *env = NULL;
+  if ((*vm)->GetEnv(vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK) return JNI_ERR;
+  jclass c = (*env)->FindClass(env, "org/redisson/gpu/RSketchNative");
+  if (!c) return JNI_ERR; /* NoClassDefFoundError pending: System.loadLibrary fails */
+  g_native = (jclass)(*env)->NewGlobalRef(env, c);
+  (*env)->DeleteLocalRef(env, c);
+  if (!g_native) return JNI_ERR;
+  g_complete = (*env)->GetStaticMethodID(env, g_native, "complete", "(Ljava/lang/Object;IIJ[Z)V");
+  if (!g_complete) return JNI_ERR;
   g_vm = vm;
   return JNI_VERSION_1_6;
+}
+
+JNIEXPORT void JNICALL JNI_OnUnload(JavaVM *vm, void *reserved) {
+  (void)reserved;
+  JNIEnv *env = NULL;
+  if ((*vm)->GetEnv(vm, (void **)&env, JNI_VERSION_1_6) == JNI_OK && g_native) (*env)->DeleteGlobalRef(env, g_native);
+  g_native = NULL;
+  g_complete = NULL;
 }
 
 static rsk_shim_buf direct(JNIEnv *env, jobject buf) {
@@ -119,17 +151,20 @@ static void names_put(JNIEnv *env, jnames *n) {
 
 JNI_FN(jlong, init)(JNIEnv *env, jclass cls, jint device, jboolean extended) {
   (void)cls;
+  reap(env);
   int64_t s = 0;
   return raise(env, rsk_shim_init(device, extended ? 1 : 0, &s)) ? 0 : (jlong)s;
 }
 
 JNI_FN(void, shutdown)(JNIEnv *env, jclass cls, jlong space) {
   (void)cls;
+  reap(env);
   raise(env, rsk_shim_shutdown(space));
 }
 
 JNI_FN(jint, type)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
+  reap(env);
   jname n;
   if (name_get(env, name, &n)) return 0;
   int32_t t = 0;
@@ -141,6 +176,7 @@ JNI_FN(jint, type)(JNIEnv *env, jclass cls, jlong space, jstring name) {
 
 JNI_FN(jboolean, delete)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
+  reap(env);
   jname n;
   if (name_get(env, name, &n)) return JNI_FALSE;
   int32_t d = 0;
@@ -151,6 +187,7 @@ JNI_FN(jboolean, delete)(JNIEnv *env, jclass cls, jlong space, jstring name) {
 
 JNI_FN(jboolean, rename)(JNIEnv *env, jclass cls, jlong space, jstring oldName, jstring newName, jboolean nx) {
   (void)cls;
+  reap(env);
   jname a, b;
   if (name_get(env, oldName, &a)) return JNI_FALSE;
   if (name_get(env, newName, &b)) {
@@ -167,6 +204,7 @@ JNI_FN(jboolean, rename)(JNIEnv *env, jclass cls, jlong space, jstring oldName, 
 /* ------------------------------------------------------------------ HLL */
 JNI_FN(jboolean, hllAdd)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets, jlong n) {
   (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return JNI_FALSE;
   uint8_t changed = 0;
@@ -201,6 +239,7 @@ static uint8_t *reply_buf(JNIEnv *env, jlong n) {
 JNI_FN(jbooleanArray, hllAddEach)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets,
                                   jlong n) {
   (void)cls;
+  reap(env);
   uint8_t *r = reply_buf(env, n);
   if (!r) return NULL;
   jname nm;
@@ -217,6 +256,7 @@ JNI_FN(jbooleanArray, hllAddEach)(JNIEnv *env, jclass cls, jlong space, jstring 
 
 JNI_FN(jlong, hllCount)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return 0;
   int64_t v = 0;
@@ -227,6 +267,7 @@ JNI_FN(jlong, hllCount)(JNIEnv *env, jclass cls, jlong space, jstring name) {
 
 JNI_FN(jlong, hllCountWith)(JNIEnv *env, jclass cls, jlong space, jobjectArray names) {
   (void)cls;
+  reap(env);
   jnames ns;
   if (names_get(env, names, &ns)) {
     names_put(env, &ns);
@@ -240,6 +281,7 @@ JNI_FN(jlong, hllCountWith)(JNIEnv *env, jclass cls, jlong space, jobjectArray n
 
 JNI_FN(void, hllMergeWith)(JNIEnv *env, jclass cls, jlong space, jstring dst, jobjectArray srcs) {
   (void)cls;
+  reap(env);
   jname d;
   if (name_get(env, dst, &d)) return;
   jnames ns;
@@ -257,6 +299,7 @@ JNI_FN(void, hllMergeWith)(JNIEnv *env, jclass cls, jlong space, jstring dst, jo
 JNI_FN(jbooleanArray, batchHllAdd)(JNIEnv *env, jclass cls, jlong space, jobjectArray names, jintArray nameOf,
                                    jobject keys, jobject offsets, jlong n) {
   (void)cls;
+  reap(env);
   if (!nameOf || (*env)->GetArrayLength(env, nameOf) < n) {
     throw_iae(env, "nameOf shorter than the batch");
     return NULL;
@@ -284,39 +327,111 @@ JNI_FN(jbooleanArray, batchHllAdd)(JNIEnv *env, jclass cls, jlong space, jobject
 /* --------------------------------------------------------------- async */
 enum { K_BOOL = 0, K_LONG = 1, K_VOID = 2, K_ARRAY = 3 };
 
-typedef struct {
-  jobject promise; /* global reference */
+typedef struct job {
+  jobject target; /* global reference: the RSketchNative.Completion */
   int kind;
   uint8_t *out; /* K_ARRAY: the replies, n bytes */
   int64_t n;
+  int status; /* the result, kept while the job waits to be delivered */
+  uint64_t value;
+  struct job *next;
 } job;
 
-/* The shim's callback, on the context's completion thread (or the calling thread for an
- * answer known at once): attach, complete the promise through Java, detach
- * nothing (daemon attachment stays for that thread). */
-static void jni_done(void *user, int status, uint64_t value) {
-  job *j = user;
-  JNIEnv *env = NULL;
-  int attached = 0;
-  if ((*g_vm)->GetEnv(g_vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK) {
-    if ((*g_vm)->AttachCurrentThreadAsDaemon(g_vm, (void **)&env, NULL) != JNI_OK) return;
-    attached = 1;
-  }
-  (void)attached;
-  jclass cls = (*env)->FindClass(env, "org/redisson/gpu/RSketchNative");
-  jmethodID m = cls ? (*env)->GetStaticMethodID(env, cls, "complete", "(Ljava/lang/Object;IIJ[Z)V") : NULL;
+/* Jobs whose completion thread could not attach to the JVM: delivered by the
+ * next native call on a Java thread (reap), never dropped. */
+static pthread_mutex_t g_park_mu = PTHREAD_MUTEX_INITIALIZER;
+static job *g_parked;
+static volatile int g_parked_n;
+
+/* Completes one job through Java and frees it.  The replies array is made
+ * here; if that fails (OutOfMemoryError) the job completes with
+ * RSK_ERR_OUT_OF_MEMORY instead, and if complete() itself throws, once more
+ * with RSK_ERR_DEVICE -- the future always completes. */
+static void deliver(JNIEnv *env, job *j) {
+  int status = j->status;
   jbooleanArray arr = NULL;
-  if (j->kind == K_ARRAY && status == RSK_OK) arr = replies_array(env, j->out, j->n);
-  if (m) (*env)->CallStaticVoidMethod(env, cls, m, j->promise, (jint)j->kind, (jint)status, (jlong)value, arr);
-  if ((*env)->ExceptionCheck(env)) (*env)->ExceptionClear(env);
-  (*env)->DeleteGlobalRef(env, j->promise);
+  if (j->kind == K_ARRAY && status == RSK_OK) {
+    arr = replies_array(env, j->out, j->n);
+    if (!arr) {
+      (*env)->ExceptionClear(env);
+      status = RSK_ERR_OUT_OF_MEMORY;
+    }
+  }
+  (*env)->CallStaticVoidMethod(env, g_native, g_complete, j->target, (jint)j->kind, (jint)status,
+                               (jlong)j->value, arr);
+  if ((*env)->ExceptionCheck(env)) {
+    (*env)->ExceptionClear(env);
+    (*env)->CallStaticVoidMethod(env, g_native, g_complete, j->target, (jint)j->kind, (jint)RSK_ERR_DEVICE,
+                                 (jlong)0, (jbooleanArray)NULL);
+    if ((*env)->ExceptionCheck(env)) (*env)->ExceptionClear(env);
+  }
   if (arr) (*env)->DeleteLocalRef(env, arr);
-  if (cls) (*env)->DeleteLocalRef(env, cls);
+  (*env)->DeleteGlobalRef(env, j->target);
   free(j->out);
   free(j);
 }
 
-static job *job_new(JNIEnv *env, jobject promise, int kind, int64_t n) {
+/* Delivers parked jobs (a Java thread, at the top of every native method). */
+static void reap(JNIEnv *env) {
+  if (!g_parked_n) return;
+  pthread_mutex_lock(&g_park_mu);
+  job *j = g_parked;
+  g_parked = NULL;
+  g_parked_n = 0;
+  pthread_mutex_unlock(&g_park_mu);
+  while (j) { /* parked newest first: deliver in submission order */
+    job *rev = NULL;
+    while (j) {
+      job *nx = j->next;
+      j->next = rev;
+      rev = j;
+      j = nx;
+    }
+    j = rev;
+    while (j) {
+      job *nx = j->next;
+      deliver(env, j);
+      j = nx;
+    }
+  }
+}
+
+/* The shim's callback, on the library's completion thread (or the calling
+ * thread for an answer known at once).  The thread is attached once, as a
+ * daemon, and stays attached (the completion thread lives as long as the
+ * context). */
+static void jni_done(void *user, int status, uint64_t value) {
+  job *j = user;
+  j->status = status;
+  j->value = value;
+  JNIEnv *env = NULL;
+  if ((*g_vm)->GetEnv(g_vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK) {
+    env = NULL;
+    for (int attempt = 0; attempt < 3 && !env; ++attempt) {
+      if ((*g_vm)->AttachCurrentThreadAsDaemon(g_vm, (void **)&env, NULL) != JNI_OK) {
+        env = NULL;
+        const struct timespec ts = {0, 1000000L << (2 * attempt)}; /* 1, 4, 16 ms */
+        nanosleep(&ts, NULL);
+      }
+    }
+  }
+  if (!env) { /* park it for the next native call */
+    pthread_mutex_lock(&g_park_mu);
+    j->next = g_parked;
+    g_parked = j;
+    g_parked_n = 1;
+    pthread_mutex_unlock(&g_park_mu);
+    return;
+  }
+  reap(env); /* earlier parked jobs first: keep submission order */
+  deliver(env, j);
+}
+
+static job *job_new(JNIEnv *env, jobject target, int kind, int64_t n) {
+  if (!target) {
+    throw_iae(env, "completion is null");
+    return NULL;
+  }
   job *j = calloc(1, sizeof *j);
   if (!j) return NULL;
   j->kind = kind;
@@ -328,24 +443,42 @@ static job *job_new(JNIEnv *env, jobject promise, int kind, int64_t n) {
       return NULL;
     }
   }
-  j->promise = (*env)->NewGlobalRef(env, promise);
+  j->target = (*env)->NewGlobalRef(env, target);
+  if (!j->target) {
+    free(j->out);
+    free(j);
+    return NULL;
+  }
   return j;
 }
 
 /* A call the shim refused never fires: free the job, throw. */
 static void job_refused(JNIEnv *env, job *j, int rc) {
-  (*env)->DeleteGlobalRef(env, j->promise);
+  (*env)->DeleteGlobalRef(env, j->target);
   free(j->out);
   free(j);
   raise(env, rc);
 }
 
-JNI_FN(void, hllAddAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets, jlong n,
-                          jobject promise) {
+JNI_FN(void, reap)(JNIEnv *env, jclass cls) {
   (void)cls;
+  reap(env);
+}
+
+JNI_FN(void, sync)(JNIEnv *env, jclass cls, jlong space) {
+  (void)cls;
+  reap(env);
+  raise(env, rsk_shim_sync(space));
+  reap(env);
+}
+
+JNI_FN(void, hllAddAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject keys, jobject offsets, jlong n,
+                          jobject done) {
+  (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return;
-  job *j = job_new(env, promise, K_BOOL, 0);
+  job *j = job_new(env, done, K_BOOL, 0);
   if (!j) {
     name_put(env, &nm);
     return;
@@ -355,11 +488,12 @@ JNI_FN(void, hllAddAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jo
   if (rc) job_refused(env, j, rc);
 }
 
-JNI_FN(void, hllCountAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject promise) {
+JNI_FN(void, hllCountAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jobject done) {
   (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return;
-  job *j = job_new(env, promise, K_LONG, 0);
+  job *j = job_new(env, done, K_LONG, 0);
   if (!j) {
     name_put(env, &nm);
     return;
@@ -369,22 +503,24 @@ JNI_FN(void, hllCountAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, 
   if (rc) job_refused(env, j, rc);
 }
 
-JNI_FN(void, hllCountWithAsync)(JNIEnv *env, jclass cls, jlong space, jobjectArray names, jobject promise) {
+JNI_FN(void, hllCountWithAsync)(JNIEnv *env, jclass cls, jlong space, jobjectArray names, jobject done) {
   (void)cls;
+  reap(env);
   jnames ns;
   if (names_get(env, names, &ns)) {
     names_put(env, &ns);
     return;
   }
-  job *j = job_new(env, promise, K_LONG, 0);
+  job *j = job_new(env, done, K_LONG, 0);
   const int rc = j ? rsk_shim_hll_count_with_async(space, ns.cs, ns.k, jni_done, j) : RSK_ERR_OUT_OF_MEMORY;
   names_put(env, &ns);
   if (rc && j) job_refused(env, j, rc);
   else if (rc) raise(env, rc);
 }
 
-JNI_FN(void, hllMergeWithAsync)(JNIEnv *env, jclass cls, jlong space, jstring dst, jobjectArray srcs, jobject promise) {
+JNI_FN(void, hllMergeWithAsync)(JNIEnv *env, jclass cls, jlong space, jstring dst, jobjectArray srcs, jobject done) {
   (void)cls;
+  reap(env);
   jname d;
   if (name_get(env, dst, &d)) return;
   jnames ns;
@@ -393,7 +529,7 @@ JNI_FN(void, hllMergeWithAsync)(JNIEnv *env, jclass cls, jlong space, jstring ds
     name_put(env, &d);
     return;
   }
-  job *j = job_new(env, promise, K_VOID, 0);
+  job *j = job_new(env, done, K_VOID, 0);
   const int rc = j ? rsk_shim_hll_merge_with_async(space, d.c, ns.cs, ns.k, jni_done, j) : RSK_ERR_OUT_OF_MEMORY;
   names_put(env, &ns);
   name_put(env, &d);
@@ -413,6 +549,7 @@ static void put_config(JNIEnv *env, const rsk_shim_bloom_config *c, jlongArray c
 JNI_FN(jboolean, bloomTryInit)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong n, jdouble p, jlongArray cfg,
                                jdoubleArray fpp) {
   (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return JNI_FALSE;
   int32_t created = 0;
@@ -426,6 +563,7 @@ JNI_FN(jboolean, bloomTryInit)(JNIEnv *env, jclass cls, jlong space, jstring nam
 
 JNI_FN(void, bloomConfig)(JNIEnv *env, jclass cls, jlong space, jstring name, jlongArray cfg, jdoubleArray fpp) {
   (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return;
   rsk_shim_bloom_config c;
@@ -454,17 +592,20 @@ static jbooleanArray bloom_batch(JNIEnv *env, jlong space, jstring name, jlong s
 JNI_FN(jbooleanArray, bloomAdd)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k, jobject keys,
                                 jobject offsets, jlong n) {
   (void)cls;
+  reap(env);
   return bloom_batch(env, space, name, size, k, keys, offsets, n, 1);
 }
 
 JNI_FN(jbooleanArray, bloomContains)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k,
                                      jobject keys, jobject offsets, jlong n) {
   (void)cls;
+  reap(env);
   return bloom_batch(env, space, name, size, k, keys, offsets, n, 0);
 }
 
 JNI_FN(jint, bloomCount)(JNIEnv *env, jclass cls, jlong space, jstring name) {
   (void)cls;
+  reap(env);
   jname nm;
   if (name_get(env, name, &nm)) return 0;
   int32_t v = 0;
@@ -474,14 +615,14 @@ JNI_FN(jint, bloomCount)(JNIEnv *env, jclass cls, jlong space, jstring name) {
 }
 
 static void bloom_async(JNIEnv *env, jlong space, jstring name, jlong size, jint k, jobject keys, jobject offsets,
-                        jlong n, jobject promise, int add) {
+                        jlong n, jobject done, int add) {
   if (n < 0 || n > 0x7fffffff) {
     throw_iae(env, "batch larger than 2^31 - 1 elements");
     return;
   }
   jname nm;
   if (name_get(env, name, &nm)) return;
-  job *j = job_new(env, promise, K_ARRAY, n);
+  job *j = job_new(env, done, K_ARRAY, n);
   if (!j) {
     name_put(env, &nm);
     return;
@@ -495,13 +636,182 @@ static void bloom_async(JNIEnv *env, jlong space, jstring name, jlong size, jint
 }
 
 JNI_FN(void, bloomAddAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k, jobject keys,
-                            jobject offsets, jlong n, jobject promise) {
+                            jobject offsets, jlong n, jobject done) {
   (void)cls;
-  bloom_async(env, space, name, size, k, keys, offsets, n, promise, 1);
+  reap(env);
+  bloom_async(env, space, name, size, k, keys, offsets, n, done, 1);
 }
 
 JNI_FN(void, bloomContainsAsync)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong size, jint k, jobject keys,
-                                 jobject offsets, jlong n, jobject promise) {
+                                 jobject offsets, jlong n, jobject done) {
   (void)cls;
-  bloom_async(env, space, name, size, k, keys, offsets, n, promise, 0);
+  reap(env);
+  bloom_async(env, space, name, size, k, keys, offsets, n, done, 0);
+}
+
+/* -------------------------------------------------------------- RBitSet */
+/* long[] -> C copy (NULL with a pending exception on failure). */
+static int64_t *long_array(JNIEnv *env, jlongArray a, jsize *n) {
+  *n = a ? (*env)->GetArrayLength(env, a) : 0;
+  if (!a) {
+    throw_iae(env, "bit indexes are null");
+    return NULL;
+  }
+  int64_t *v = malloc(sizeof(int64_t) * (size_t)(*n > 0 ? *n : 1));
+  if (!v) {
+    jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (c) (*env)->ThrowNew(env, c, "bit indexes");
+    return NULL;
+  }
+  if (*n) (*env)->GetLongArrayRegion(env, a, 0, *n, (jlong *)v);
+  return v;
+}
+
+JNI_FN(jlong, bitsetStrlen)(JNIEnv *env, jclass cls, jlong space, jstring name) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return 0;
+  int64_t v = 0;
+  const int rc = rsk_shim_bitset_strlen(space, nm.c, &v);
+  name_put(env, &nm);
+  return raise(env, rc) ? 0 : (jlong)v;
+}
+
+JNI_FN(jbyteArray, bitsetGet)(JNIEnv *env, jclass cls, jlong space, jstring name) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return NULL;
+  uint8_t *bytes = NULL;
+  int64_t len = -1;
+  const int rc = rsk_shim_bitset_get_bytes(space, nm.c, &bytes, &len);
+  name_put(env, &nm);
+  jbyteArray arr = NULL;
+  if (!raise(env, rc) && len >= 0) { /* len -1: GET nil -> null */
+    arr = (*env)->NewByteArray(env, (jsize)len);
+    if (arr && len) (*env)->SetByteArrayRegion(env, arr, 0, (jsize)len, (const jbyte *)bytes);
+  }
+  rsk_shim_free(bytes);
+  return arr;
+}
+
+JNI_FN(jbooleanArray, bitsetGetBits)(JNIEnv *env, jclass cls, jlong space, jstring name, jlongArray indexes) {
+  (void)cls;
+  reap(env);
+  jsize n = 0;
+  int64_t *offs = long_array(env, indexes, &n);
+  if (!offs) return NULL;
+  uint8_t *r = reply_buf(env, n);
+  jname nm;
+  jbooleanArray arr = NULL;
+  if (r && !name_get(env, name, &nm)) {
+    const int rc = rsk_shim_bitset_getbits(space, nm.c, offs, n, r, n);
+    name_put(env, &nm);
+    if (!raise(env, rc)) arr = replies_array(env, r, n);
+  }
+  free(r);
+  free(offs);
+  return arr;
+}
+
+JNI_FN(void, bitsetSetBits)(JNIEnv *env, jclass cls, jlong space, jstring name, jlongArray indexes,
+                            jboolean value) {
+  (void)cls;
+  reap(env);
+  jsize n = 0;
+  int64_t *offs = long_array(env, indexes, &n);
+  if (!offs) return;
+  jname nm;
+  if (!name_get(env, name, &nm)) {
+    const int rc = rsk_shim_bitset_setbits(space, nm.c, offs, n, value ? 1 : 0);
+    name_put(env, &nm);
+    raise(env, rc);
+  }
+  free(offs);
+}
+
+JNI_FN(void, bitsetSetRange)(JNIEnv *env, jclass cls, jlong space, jstring name, jlong from, jlong to,
+                             jboolean value) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return;
+  const int rc = rsk_shim_bitset_set_range(space, nm.c, from, to, value ? 1 : 0);
+  name_put(env, &nm);
+  raise(env, rc);
+}
+
+JNI_FN(jlong, bitsetCardinality)(JNIEnv *env, jclass cls, jlong space, jstring name) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return 0;
+  int64_t v = 0;
+  const int rc = rsk_shim_bitset_cardinality(space, nm.c, &v);
+  name_put(env, &nm);
+  return raise(env, rc) ? 0 : (jlong)v;
+}
+
+JNI_FN(jlong, bitsetLength)(JNIEnv *env, jclass cls, jlong space, jstring name) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return 0;
+  int64_t v = 0;
+  const int rc = rsk_shim_bitset_length(space, nm.c, &v);
+  name_put(env, &nm);
+  return raise(env, rc) ? 0 : (jlong)v;
+}
+
+JNI_FN(void, bitsetSet)(JNIEnv *env, jclass cls, jlong space, jstring name, jbyteArray bytes) {
+  (void)cls;
+  reap(env);
+  if (!bytes) {
+    throw_iae(env, "bytes is null");
+    return;
+  }
+  const jsize n = (*env)->GetArrayLength(env, bytes);
+  uint8_t *v = malloc((size_t)(n > 0 ? n : 1));
+  if (!v) {
+    jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (c) (*env)->ThrowNew(env, c, "bytes");
+    return;
+  }
+  if (n) (*env)->GetByteArrayRegion(env, bytes, 0, n, (jbyte *)v);
+  jname nm;
+  if (!name_get(env, name, &nm)) {
+    const int rc = rsk_shim_bitset_set_bytes(space, nm.c, v, n);
+    name_put(env, &nm);
+    raise(env, rc);
+  }
+  free(v);
+}
+
+JNI_FN(jboolean, bitsetClear)(JNIEnv *env, jclass cls, jlong space, jstring name) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return JNI_FALSE;
+  int32_t d = 0;
+  const int rc = rsk_shim_bitset_clear(space, nm.c, &d);
+  name_put(env, &nm);
+  return raise(env, rc) ? JNI_FALSE : (d ? JNI_TRUE : JNI_FALSE);
+}
+
+JNI_FN(void, bitsetOp)(JNIEnv *env, jclass cls, jlong space, jstring name, jint op, jobjectArray others) {
+  (void)cls;
+  reap(env);
+  jname nm;
+  if (name_get(env, name, &nm)) return;
+  jnames ns;
+  if (names_get(env, others, &ns)) {
+    names_put(env, &ns);
+    name_put(env, &nm);
+    return;
+  }
+  const int rc = rsk_shim_bitset_op(space, nm.c, op, ns.cs, ns.k);
+  names_put(env, &ns);
+  name_put(env, &nm);
+  raise(env, rc);
 }

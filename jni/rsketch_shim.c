@@ -44,7 +44,7 @@ const char *rsk_shim_exception_class(int rc) {
       return "java/lang/IllegalStateException";
     case RSK_ERR_OUT_OF_MEMORY:
       return "java/lang/OutOfMemoryError";
-    default: /* WRONGTYPE, INVALID_HLL, DEVICE, NO_DEVICE, RSK_SHIM_CONFIG_CHANGED */
+    default: /* WRONGTYPE, INVALID_HLL, DEVICE, NO_DEVICE, RSK_SHIM_CONFIG_CHANGED, RSK_SHIM_REDIS_ERROR */
       return "org/redisson/client/RedisException";
   }
 }
@@ -72,9 +72,12 @@ int rsk_shim_keys(rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, rsk_keys *
 typedef struct entry {
   char *name;
   uint64_t hash;
-  int32_t type; /* RSK_SHIM_HLL / RSK_SHIM_BLOOM */
+  int32_t type; /* RSK_SHIM_HLL / RSK_SHIM_BLOOM / RSK_SHIM_BITSET */
   rsk_hll *hll; /* a one-sketch pool */
   rsk_bloom *bloom;
+  /* RSK_SHIM_BITSET: the string; RSK_SHIM_BLOOM: the view of the filter's
+   * bits (rsk_bloom_bitset), made on the first RBitSet call on the name */
+  rsk_bitset *bits;
   rsk_shim_bloom_config cfg;
   int refs; /* the map's reference + calls in flight */
   struct entry *next;
@@ -97,6 +100,7 @@ static uint64_t name_hash(const char *s) { /* FNV-1a */
 
 static void destroy_entry(entry *e) {
   if (e->hll) (void)rsk_hll_destroy(e->hll);
+  if (e->bits) (void)rsk_bitset_destroy(e->bits); /* a view goes before its filter */
   if (e->bloom) (void)rsk_bloom_destroy(e->bloom);
   free(e->name);
   free(e);
@@ -259,6 +263,11 @@ int rsk_shim_init(int32_t device, int32_t extended_bloom, int64_t *space_out) {
     free(s);
     return fail_code(RSK_ERR_OUT_OF_MEMORY, "host allocation failed");
   }
+  if (rsk_abi_version() != RSK_ABI_VERSION) {
+    free(s->buckets);
+    free(s);
+    return fail_code(RSK_ERR_NO_DEVICE, "librsketch.so was built against another rsketch.h (RSK_ABI_VERSION)");
+  }
   rsk_options o;
   memset(&o, 0, sizeof o);
   o.device = device;
@@ -296,6 +305,15 @@ int rsk_shim_shutdown(int64_t h) {
   return rc;
 }
 
+int rsk_shim_sync(int64_t h) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  const int rc = rsk_sync(s->ctx); /* every call issued so far has completed and its callback returned */
+  drain(s);
+  return rc;
+}
+
 int rsk_shim_lookup(int64_t h, const char *name, int32_t *type_out, int64_t *handle_out) {
   ENTER();
   space *s = sp(h);
@@ -303,7 +321,7 @@ int rsk_shim_lookup(int64_t h, const char *name, int32_t *type_out, int64_t *han
   drain(s);
   entry *e = acquire(s, name);
   *type_out = e ? e->type : RSK_SHIM_NONE;
-  *handle_out = e ? (int64_t)(intptr_t)(e->hll ? (void *)e->hll : (void *)e->bloom) : 0;
+  *handle_out = e ? (int64_t)(intptr_t)(e->hll ? (void *)e->hll : e->bloom ? (void *)e->bloom : (void *)e->bits) : 0;
   release(s, e);
   return RSK_OK;
 }
@@ -849,4 +867,314 @@ int rsk_shim_bloom_contains_async(int64_t h, const char *name, int64_t size, int
   a->es[a->m++] = e;
   rc = rsk_bloom_contains_async(e->bloom, &kk, out, async_done, a);
   return rc ? async_refused(a, rc) : RSK_OK;
+}
+
+/* ------------------------------------------------------------ RBitSet */
+#define RSK_BITOFF_MAX 4294967295LL /* Redis: a string holds at most 512 MB */
+
+static int redis_err(const char *msg) { return fail_code(RSK_SHIM_REDIS_ERROR, msg); }
+
+/* The string of `name` as an rsk_bitset, referenced: a plain RBitSet string,
+ * or the bits of a Bloom filter (the view, made once per filter).  *bits_out
+ * NULL (and *e_out NULL) when the name is absent and !create; an HLL is
+ * refused with WRONGTYPE (its Redis string is not exposed bit-wise here). */
+static int bits_entry(space *s, const char *name, int create, entry **e_out, rsk_bitset **bits_out) {
+  *e_out = NULL;
+  *bits_out = NULL;
+  if (!name) return fail("name is null");
+  entry *e = acquire(s, name);
+  if (!e) {
+    if (!create) return RSK_OK;
+    entry *f = new_entry(name, RSK_SHIM_BITSET);
+    if (!f) return fail_code(RSK_ERR_OUT_OF_MEMORY, "host allocation failed");
+    int rc = rsk_bitset_create(s->ctx, &f->bits);
+    if (rc) {
+      free(f->name);
+      free(f);
+      return rc;
+    }
+    int ins = 0;
+    e = insert_or_get(s, f, &ins);
+  }
+  if (e->type == RSK_SHIM_HLL) {
+    release(s, e);
+    return fail_code(RSK_ERR_WRONGTYPE,
+                     "WRONGTYPE the key holds a GPU HyperLogLog; its Redis string is not exposed as an RBitSet");
+  }
+  if (e->type == RSK_SHIM_BLOOM) {
+    pthread_mutex_lock(&s->mu);
+    rsk_bitset *v = e->bits;
+    pthread_mutex_unlock(&s->mu);
+    if (!v) { /* made outside the mutex (a library call); the first one made wins */
+      int rc = rsk_bloom_bitset(e->bloom, &v);
+      if (rc) {
+        release(s, e);
+        return rc;
+      }
+      pthread_mutex_lock(&s->mu);
+      rsk_bitset *won = e->bits;
+      if (!won) e->bits = v;
+      pthread_mutex_unlock(&s->mu);
+      if (won) {
+        (void)rsk_bitset_destroy(v);
+        v = won;
+      }
+    }
+    *bits_out = v;
+  } else {
+    *bits_out = e->bits;
+  }
+  *e_out = e;
+  return RSK_OK;
+}
+
+static int offsets_ok(const int64_t *offs, int64_t n) {
+  if (n < 0) return fail("negative element count");
+  if (n > 0 && !offs) return fail("offsets is null");
+  for (int64_t i = 0; i < n; ++i)
+    if (offs[i] < 0 || offs[i] > RSK_BITOFF_MAX) return redis_err("ERR bit offset is not an integer or out of range");
+  return RSK_OK;
+}
+
+int rsk_shim_bitset_strlen(int64_t h, const char *name, int64_t *out) {
+  ENTER();
+  space *s = sp(h);
+  if (!s || !out) return fail("null argument");
+  drain(s);
+  entry *e;
+  rsk_bitset *b;
+  *out = 0;
+  int rc = bits_entry(s, name, 0, &e, &b);
+  if (rc || !e) return rc;
+  uint64_t v = 0;
+  rc = rsk_bitset_strlen(b, &v);
+  *out = (int64_t)v;
+  release(s, e);
+  return rc;
+}
+
+int rsk_shim_bitset_get_bytes(int64_t h, const char *name, uint8_t **bytes_out, int64_t *len_out) {
+  ENTER();
+  space *s = sp(h);
+  if (!s || !bytes_out || !len_out) return fail("null argument");
+  drain(s);
+  *bytes_out = NULL;
+  *len_out = -1; /* GET of a missing key: nil */
+  entry *e;
+  rsk_bitset *b;
+  int rc = bits_entry(s, name, 0, &e, &b);
+  if (rc || !e) return rc;
+  for (;;) { /* another thread may grow the string between STRLEN and GET: size again */
+    uint64_t n = 0;
+    if ((rc = rsk_bitset_strlen(b, &n))) break;
+    uint8_t *buf = malloc((size_t)n + 1);
+    if (!buf) {
+      rc = fail_code(RSK_ERR_OUT_OF_MEMORY, "host allocation failed");
+      break;
+    }
+    size_t got = 0;
+    rc = rsk_bitset_get_bytes(b, buf, (size_t)n + 1, &got);
+    if (rc == RSK_ERR_INVALID_ARG) { /* grew meanwhile */
+      free(buf);
+      continue;
+    }
+    if (rc) {
+      free(buf);
+      break;
+    }
+    if (got == 0) { /* no string: a filter nothing was added to yet, or an emptied string (Redis deletes it) */
+      free(buf);
+      break;
+    }
+    *bytes_out = buf;
+    *len_out = (int64_t)got;
+    break;
+  }
+  release(s, e);
+  return rc;
+}
+
+void rsk_shim_free(void *p) { free(p); }
+
+int rsk_shim_bitset_getbits(int64_t h, const char *name, const int64_t *offs, int64_t n, uint8_t *out,
+                            int64_t out_len) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  drain(s);
+  int rc = offsets_ok(offs, n);
+  if (rc) return rc;
+  if (out_len < n || (n > 0 && !out)) return fail("reply array shorter than the batch");
+  entry *e;
+  rsk_bitset *b;
+  if ((rc = bits_entry(s, name, 0, &e, &b))) return rc;
+  if (!e) { /* GETBIT of a missing key: 0 */
+    if (n) memset(out, 0, (size_t)n);
+    return RSK_OK;
+  }
+  rc = rsk_bitset_getbits(b, (const uint64_t *)offs, (uint64_t)n, RSK_MEM_HOST, out);
+  release(s, e);
+  return rc;
+}
+
+int rsk_shim_bitset_setbits(int64_t h, const char *name, const int64_t *offs, int64_t n, int32_t value) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  drain(s);
+  int rc = offsets_ok(offs, n);
+  if (rc) return rc;
+  if (n == 0) return RSK_OK;
+  entry *e;
+  rsk_bitset *b;
+  if ((rc = bits_entry(s, name, 1, &e, &b))) return rc;
+  rc = rsk_bitset_setbits(b, (const uint64_t *)offs, (uint64_t)n, value ? 1 : 0, RSK_MEM_HOST);
+  release(s, e);
+  return rc;
+}
+
+int rsk_shim_bitset_set_range(int64_t h, const char *name, int64_t from, int64_t to, int32_t value) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  drain(s);
+  if (to <= from) return RSK_OK; /* the reference's loop issues no SETBIT */
+  if (from < 0 || to - 1 > RSK_BITOFF_MAX) return redis_err("ERR bit offset is not an integer or out of range");
+  entry *e;
+  rsk_bitset *b;
+  int rc = bits_entry(s, name, 1, &e, &b);
+  if (rc) return rc;
+  rc = rsk_bitset_set_range(b, (uint64_t)from, (uint64_t)to, value ? 1 : 0);
+  release(s, e);
+  return rc;
+}
+
+int rsk_shim_bitset_cardinality(int64_t h, const char *name, int64_t *out) {
+  ENTER();
+  space *s = sp(h);
+  if (!s || !out) return fail("null argument");
+  drain(s);
+  *out = 0;
+  entry *e;
+  rsk_bitset *b;
+  int rc = bits_entry(s, name, 0, &e, &b);
+  if (rc || !e) return rc;
+  uint64_t v = 0;
+  rc = rsk_bitset_bitcount(b, &v);
+  *out = (int64_t)v;
+  release(s, e);
+  return rc;
+}
+
+int rsk_shim_bitset_length(int64_t h, const char *name, int64_t *out) {
+  ENTER();
+  space *s = sp(h);
+  if (!s || !out) return fail("null argument");
+  drain(s);
+  *out = 0;
+  entry *e;
+  rsk_bitset *b;
+  int rc = bits_entry(s, name, 0, &e, &b);
+  if (rc || !e) return rc;
+  uint64_t v = 0;
+  rc = rsk_bitset_length(b, &v);
+  *out = (int64_t)v;
+  release(s, e);
+  return rc;
+}
+
+int rsk_shim_bitset_set_bytes(int64_t h, const char *name, const uint8_t *bytes, int64_t len) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  drain(s);
+  if (len < 0 || (len > 0 && !bytes)) return fail("bad byte array");
+  if (len > (RSK_BITOFF_MAX >> 3) + 1) return redis_err("ERR string exceeds maximum allowed size (512MB)");
+  entry *e;
+  rsk_bitset *b;
+  int rc = bits_entry(s, name, 1, &e, &b);
+  if (rc) return rc;
+  rc = rsk_bitset_set_bytes(b, bytes, (size_t)len);
+  release(s, e);
+  return rc;
+}
+
+/* Removes a plain string's entry if it is (still) empty: Redis holds no key
+ * for an empty result (BITOP of empty sources, DEL). */
+static void drop_if_empty(space *s, const char *name) {
+  entry *e = acquire(s, name);
+  if (!e) return;
+  uint64_t n = 1;
+  if (e->type == RSK_SHIM_BITSET && rsk_bitset_strlen(e->bits, &n) == RSK_OK && n == 0) {
+    pthread_mutex_lock(&s->mu);
+    entry **p = slot_of(s, name, e->hash);
+    const int mine = *p == e;
+    if (mine) {
+      *p = e->next;
+      --s->count;
+    }
+    pthread_mutex_unlock(&s->mu);
+    if (mine) release(s, e); /* the map's reference */
+  }
+  release(s, e);
+}
+
+int rsk_shim_bitset_clear(int64_t h, const char *name, int32_t *deleted_out) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  drain(s);
+  if (deleted_out) *deleted_out = 0;
+  entry *e;
+  rsk_bitset *b;
+  int rc = bits_entry(s, name, 0, &e, &b);
+  if (rc || !e) return rc;
+  uint64_t n = 0;
+  if (!(rc = rsk_bitset_strlen(b, &n))) rc = rsk_bitset_clear(b); /* a filter keeps its {name}__config */
+  if (!rc && deleted_out) *deleted_out = n > 0;
+  release(s, e);
+  if (!rc) drop_if_empty(s, name);
+  return rc;
+}
+
+#define SHIM_MAX_BITOP 16
+
+int rsk_shim_bitset_op(int64_t h, const char *name, int32_t op, const char *const *others, int32_t k) {
+  ENTER();
+  space *s = sp(h);
+  if (!s) return fail("space is null");
+  drain(s);
+  if (op < RSK_BITOP_AND || op > RSK_BITOP_NOT) return fail("bad BITOP operation");
+  if (k < 0 || (k > 0 && !others)) return fail("names is null");
+  if (op == RSK_BITOP_NOT && k != 0) return redis_err("ERR BITOP NOT must be called with a single source key.");
+  if (k + 1 > SHIM_MAX_BITOP) return fail("at most 15 other names per BITOP");
+  /* BITOP op name name others... (RedissonBitSet.java:138-145): the
+   * destination and the sources; missing sources read as empty strings */
+  entry *es[SHIM_MAX_BITOP + 1];
+  rsk_bitset *srcs[SHIM_MAX_BITOP];
+  rsk_bitset *empty = NULL;
+  int m = 0, rc = RSK_OK;
+  for (int32_t j = -1; j < k && rc == RSK_OK; ++j) {
+    entry *e;
+    rsk_bitset *b;
+    rc = bits_entry(s, j < 0 ? name : others[j], 0, &e, &b);
+    if (rc) break;
+    if (e) es[m] = e;
+    else {
+      if (!empty && (rc = rsk_bitset_create(s->ctx, &empty))) break;
+      b = empty;
+      es[m] = NULL;
+    }
+    srcs[m++] = b;
+  }
+  entry *d = NULL;
+  rsk_bitset *db = NULL;
+  if (!rc) rc = bits_entry(s, name, 1, &d, &db);
+  if (!rc) rc = rsk_bitset_bitop(op, db, srcs, (uint32_t)m);
+  if (d) release(s, d);
+  for (int j = 0; j < m; ++j)
+    if (es[j]) release(s, es[j]);
+  if (empty) (void)rsk_bitset_destroy(empty);
+  if (!rc) drop_if_empty(s, name);
+  return rc;
 }

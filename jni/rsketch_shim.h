@@ -38,6 +38,10 @@ extern "C" {
  * (RedissonBloomFilter.java:180-186) and the Java object retries after
  * re-reading {name}__config (:108-112, :162-166). */
 #define RSK_SHIM_CONFIG_CHANGED 100
+/* Shim-level status: an error reply Redis itself would give (a bit offset
+ * outside [0, 2^32), BITOP NOT with other keys): RedisException with Redis's
+ * message, as CommandDecoder raises for -ERR (CommandDecoder.java:239-243). */
+#define RSK_SHIM_REDIS_ERROR 101
 
 /* A java.nio direct buffer as JNI reports it: address + capacity in ELEMENTS
  * (bytes for a ByteBuffer, longs for a LongBuffer).  addr == NULL means the
@@ -69,11 +73,16 @@ int rsk_shim_keys(rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, rsk_keys *
  * refused with IllegalArgumentException like the reference (:226-227). */
 int rsk_shim_init(int32_t device, int32_t extended_bloom, int64_t *space_out);
 int rsk_shim_shutdown(int64_t space);
+/* Waits until every call issued so far has completed and its callback has
+ * returned (rsk_sync).  Callbacks may call the shim again (rsketch.h,
+ * rsk_done_fn): this wait does not hold the context. */
+int rsk_shim_sync(int64_t space);
 
 #define RSK_SHIM_NONE 0
 #define RSK_SHIM_HLL 1
 #define RSK_SHIM_BLOOM 2
-/* TYPE-like probe of a name (RSK_SHIM_NONE / _HLL / _BLOOM) and the object's
+#define RSK_SHIM_BITSET 3
+/* TYPE-like probe of a name (RSK_SHIM_NONE / _HLL / _BLOOM / _BITSET) and the object's
  * library handle (the same handle for every lookup of one name; 0 if none). */
 int rsk_shim_lookup(int64_t space, const char *name, int32_t *type_out, int64_t *handle_out);
 /* DEL name (a Bloom filter's {name}__config with it, RedissonBloomFilter.java:
@@ -154,6 +163,34 @@ int rsk_shim_bloom_add_async(int64_t space, const char *name, int64_t size, int3
 int rsk_shim_bloom_contains_async(int64_t space, const char *name, int64_t size, int32_t k, rsk_shim_buf keys,
                                   rsk_shim_buf offsets, int64_t n, uint8_t *out, int64_t out_len, rsk_done_fn cb,
                                   void *user);
+
+/* ------------------------------------ RBitSet (RedissonBitSet.java:32-270) */
+/* getBitSet(name) (Redisson.java:515-517; RBatch.getBitSet, RedissonBatch.java:
+ * 191) on the keyspace.  The name holds a plain string (made by the first
+ * write), or a Bloom filter -- whose bits ARE the string key in Redis, so
+ * these calls read and write the filter's bits (rsk_bloom_bitset: GET returns
+ * exactly the bytes Redis would) -- or nothing (an empty string: GET nil,
+ * GETBIT / BITCOUNT / length 0).  An HLL name is WRONGTYPE.  Offsets outside
+ * [0, 2^32) are RSK_SHIM_REDIS_ERROR, as Redis replies. */
+int rsk_shim_bitset_strlen(int64_t space, const char *name, int64_t *bytes_out); /* size() = 8 * STRLEN */
+/* GET (toByteArray, :88-91): *bytes_out malloc'd (free with rsk_shim_free),
+ * *len_out = -1 and NULL for a missing key (nil). */
+int rsk_shim_bitset_get_bytes(int64_t space, const char *name, uint8_t **bytes_out, int64_t *len_out);
+void rsk_shim_free(void *p);
+int rsk_shim_bitset_getbits(int64_t space, const char *name, const int64_t *offsets, int64_t n, uint8_t *out,
+                            int64_t out_len);                                          /* GETBIT x n */
+int rsk_shim_bitset_setbits(int64_t space, const char *name, const int64_t *offsets, int64_t n, int32_t value);
+int rsk_shim_bitset_set_range(int64_t space, const char *name, int64_t from, int64_t to, int32_t value);
+int rsk_shim_bitset_cardinality(int64_t space, const char *name, int64_t *out);       /* BITCOUNT */
+int rsk_shim_bitset_length(int64_t space, const char *name, int64_t *out);            /* length() */
+int rsk_shim_bitset_set_bytes(int64_t space, const char *name, const uint8_t *bytes, int64_t len); /* SET */
+/* clear() = DEL name: a plain string goes away; a Bloom filter's bits are
+ * zeroed and its {name}__config stays (DEL removes only the string key).
+ * *deleted_out (may be NULL) = 1 iff a non-empty string existed. */
+int rsk_shim_bitset_clear(int64_t space, const char *name, int32_t *deleted_out);
+/* BITOP op name name others[0..k) (or/and/xor/not, :125-145,216-268; op as
+ * rsk_bitop, NOT with k = 0). */
+int rsk_shim_bitset_op(int64_t space, const char *name, int32_t op, const char *const *others, int32_t k);
 
 #ifdef __cplusplus
 }

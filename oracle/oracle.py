@@ -61,6 +61,9 @@ def lib():
             "orc_hll_add_gen_grouped_subset": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                       ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                       ctypes.c_int]),
+            "orc_hll_add_gen_grouped_ids": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                   ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                   ctypes.c_uint64, ctypes.c_int]),
             "orc_hll_dense_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
             "orc_hll_raw_sum": (ctypes.c_double, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
             "orc_hll_dense_sum": (ctypes.c_double, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
@@ -579,6 +582,16 @@ def bloom_add_replies_sample_gen16_mt(size: int, k: int, seed: int, n: int, samp
     out = np.zeros(sample.size, np.uint8)
     lib().orc_bloom_add_replies_sample_gen16_mt(size, k, seed, n, _ptr(sample), sample.size, _ptr(out), nthreads)
     return out
+
+
+def hll_add_gen_grouped_ids(regs: np.ndarray, G: int, ids: np.ndarray, seed: int, start: int, n: int,
+                            nthreads: int = 1):
+    """The C5 pair stream's registers for the (distinct) groups `ids` only:
+    regs row s = group ids[s]."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    assert regs.dtype == np.uint8 and regs.size == ids.size * REGISTERS
+    assert np.unique(ids).size == ids.size and (ids.size == 0 or int(ids.max()) < G)
+    lib().orc_hll_add_gen_grouped_ids(_ptr(regs), G, _ptr(ids), ids.size, seed, start, n, nthreads)
 
 
 def hll_add_gen_grouped_subset(regs: np.ndarray, G: int, gsub: int, seed: int, start: int, n: int,

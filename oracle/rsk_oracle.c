@@ -387,6 +387,41 @@ void orc_hll_add_gen_grouped_subset(uint8_t *regs, uint64_t G, uint64_t gsub, ui
     }
 }
 
+/* Any set of groups: ids[0..nids) (distinct, < G); regs is [nids][16384],
+ * row s = group ids[s].  Each thread owns the rows s with s % nt == t. */
+void orc_hll_add_gen_grouped_ids(uint8_t *regs, uint64_t G, const uint64_t *ids, uint64_t nids, uint64_t seed,
+                                 uint64_t start, uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    uint32_t *slot = malloc(sizeof(uint32_t) * (size_t)G);
+    if (!slot) return;
+    for (uint64_t g = 0; g < G; ++g) slot[g] = UINT32_MAX;
+    for (uint64_t s = 0; s < nids; ++s) slot[ids[s]] = (uint32_t)s;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+#ifdef _OPENMP
+        const uint32_t t = (uint32_t)omp_get_thread_num(), nt = (uint32_t)omp_get_num_threads();
+#else
+        const uint32_t t = 0, nt = 1;
+#endif
+        for (uint64_t j = 0; j < n; j++) {
+            const uint64_t i = start + j;
+            const uint32_t s = slot[orc_splitmix64(seed + 3 * i) % G];
+            if (s == UINT32_MAX || s % nt != t) continue;
+            uint8_t key[16];
+            uint64_t lo = orc_splitmix64(seed + 3 * i + 1), hi = orc_splitmix64(seed + 3 * i + 2);
+            memcpy(key, &lo, 8);
+            memcpy(key + 8, &hi, 8);
+            long idx;
+            int c = orc_hll_patlen(key, 16, &idx);
+            uint8_t *r = regs + (uint64_t)s * ORC_HLL_REGISTERS;
+            if (c > r[idx]) r[idx] = (uint8_t)c;
+        }
+    }
+    free(slot);
+}
+
 /* ===================================================================== */
 /* Redis 3.2.0 dense register access (HLL_DENSE_GET/SET_REGISTER).        */
 /* ===================================================================== */

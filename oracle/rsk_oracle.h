@@ -56,6 +56,9 @@ void orc_hll_add_gen_grouped(uint8_t *regs, uint64_t G, uint64_t seed, uint64_t 
 /* Groups [0, gsub) only (regs is [gsub][16384]), on nthreads cores. */
 void orc_hll_add_gen_grouped_subset(uint8_t *regs, uint64_t G, uint64_t gsub, uint64_t seed, uint64_t start,
                                     uint64_t n, int nthreads);
+/* Groups ids[0..nids) (distinct), regs [nids][16384], on nthreads cores. */
+void orc_hll_add_gen_grouped_ids(uint8_t *regs, uint64_t G, const uint64_t *ids, uint64_t nids, uint64_t seed,
+                                 uint64_t start, uint64_t n, int nthreads);
 
 int orc_hll_dense_get(const uint8_t *dense_regs, int j);
 void orc_hll_dense_set(uint8_t *dense_regs, int j, int v);

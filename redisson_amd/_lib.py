@@ -32,6 +32,7 @@ RSK_BLOOM_EXTENDED = 1
 RSK_FETCH_SELF = 1
 HLL_REGISTERS = 16384
 HLL_DENSE_BYTES = 12304
+ABI_VERSION = 2  # include/rsketch.h RSK_ABI_VERSION
 
 
 class RedissonError(Exception):
@@ -153,6 +154,7 @@ SIGNATURES = {
     "rsk_bitset_get_bytes": (ctypes.c_int, [_vp, _vp, _sz, _P(_sz)]),
     "rsk_bitset_set_bytes": (ctypes.c_int, [_vp, _vp, _sz]),
     "rsk_bitset_clear": (ctypes.c_int, [_vp]),
+    "rsk_bloom_bitset": (ctypes.c_int, [_vp, _P(_vp)]),
     "rsk_dev_alloc": (ctypes.c_int, [_vp, _u64, _P(_vp)]),
     "rsk_dev_free": (ctypes.c_int, [_vp, _vp]),
     "rsk_memcpy": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32]),
@@ -160,6 +162,7 @@ SIGNATURES = {
     "rsk_comm_unique_id": (ctypes.c_int, [_vp]),
     "rsk_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
     "rsk_comm_destroy": (ctypes.c_int, [_vp]),
+    "rsk_comm_info": (ctypes.c_int, [_vp, _P(ctypes.c_int), _P(ctypes.c_int)]),
     "rsk_hll_allreduce": (ctypes.c_int, [_vp, _u64]),
     "rsk_hll_allreduce_pool": (ctypes.c_int, [_vp]),
     "rsk_hll_reducescatter_pool": (ctypes.c_int, [_vp, _P(_u64), _P(_u64)]),
@@ -219,17 +222,47 @@ def load():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
+            if L.rsk_abi_version() != ABI_VERSION:
+                raise ImportError("librsketch.so has ABI %d, this binding expects %d: rebuild it"
+                                  % (L.rsk_abi_version(), ABI_VERSION))
             _lib = L
     return _lib
 
 
+def foreign_hip_runtime():
+    """Path of a HIP runtime (libamdhip64) mapped into this process from
+    outside the ROCm install -- torch's bundled copy, once `import torch` has
+    run -- or None."""
+    rocm = os.path.realpath(os.environ.get("ROCM_PATH", "/opt/rocm"))
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6 and "libamdhip64" in parts[5]:
+                    path = os.path.realpath(parts[5].strip())
+                    if not path.startswith(rocm + os.sep) and not path.startswith("/opt/rocm"):
+                        return path
+    except OSError:
+        return None
+    return None
+
+
 def diag():
     """librsketch_diag.so (test / bench support: generators, microbenchmarks,
-    tuning variants, route overrides).  Never used by the product path."""
+    tuning variants, route overrides).  Never used by the product path.
+
+    It must be loaded before torch: loaded after torch's own HIP runtime is
+    mapped, rocprofv3 crashed through a null dispatch entry (round 3, commit
+    c380052).  A late first load is therefore refused."""
     global _diag
     load()  # the product library (and the system comgr) first
     with _lock:
         if _diag is None:
+            foreign = foreign_hip_runtime()
+            if foreign is not None:
+                raise ImportError(
+                    "librsketch_diag.so must be loaded before torch: a foreign HIP runtime (%s) is already "
+                    "mapped in this process; call redisson_amd._lib.diag() before `import torch`" % foreign)
             if not os.path.exists(DIAG_PATH):
                 raise ImportError("librsketch_diag.so not found at %s: build it with `make`" % DIAG_PATH)
             D = ctypes.CDLL(DIAG_PATH)

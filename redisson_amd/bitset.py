@@ -2,7 +2,9 @@
 
 Mirror of src/main/java/org/redisson/core/RBitSet.java:25-61, implemented by
 RedissonBitSet.java: a Redis string addressed as bits, MSB-first (bit i in
-byte i>>3 under mask 0x80>>(i&7)).  Every command runs through the rsk_bitset
+byte i>>3 under mask 0x80>>(i&7)).  On the name of a Bloom filter it is the
+filter's bit string (rsk_bloom_bitset), as in Redis where the filter's bits
+are the string key of that name.  Every command runs through the rsk_bitset
 C ABI on the GPU; only the java.util.BitSet conversions (fromByteArrayReverse /
 toByteArrayReverse, :152-173) happen on the host, as in the reference.
 """
@@ -205,6 +207,14 @@ class RBitSet:
         self._op("NOT", ())
 
     def delete(self) -> bool:
+        """DEL name.  On a Bloom filter's name that deletes only its bit string
+        (the filter stays initialised: {name}__config is another key)."""
+        with self._client._lock:
+            v = self._client._db.get(self._name)
+            if v is not None and v[0] == "bloom":
+                existed = self.size() > 0
+                _lib.check(_lib.load().rsk_bitset_clear(self._h(False)), "DEL")
+                return existed
         return self._client.delete(self._name) > 0
 
 

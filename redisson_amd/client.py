@@ -43,6 +43,7 @@ class Redisson:
         self.codec = self.config.codec
         self.engine = _lib.Engine.get(self.config.device)
         self._db: dict = {}
+        self._views: dict = {}  # Bloom filter name -> rsk_bloom_bitset view of its bits
         self._lock = threading.RLock()
         self._pool = cf.ThreadPoolExecutor(max_workers=max(1, self.config.threads))
 
@@ -92,6 +93,9 @@ class Redisson:
         if kind == "hll":
             _lib.load().rsk_hll_destroy(obj.pool)
         elif kind == "bloom":
+            view = self._views.pop(name, None)
+            if view is not None:  # the view of the filter's bits goes first
+                _lib.load().rsk_bitset_destroy(view)
             _lib.load().rsk_bloom_destroy(obj)
         elif kind == "bitset":
             _lib.load().rsk_bitset_destroy(obj)
@@ -132,9 +136,20 @@ class Redisson:
             return h
 
     def _bitset_handle(self, name: str, create: bool):
+        """The string of `name` as an rsk_bitset: a plain RBitSet string, or the
+        bits of the Bloom filter of that name -- in Redis a filter's bits ARE the
+        string key `name` (RedissonBloomFilter SETBITs it), so getBitSet(name)
+        reads them (rsk_bloom_bitset)."""
         with self._lock:
             v = self._db.get(name)
             if v is not None:
+                if v[0] == "bloom":
+                    view = self._views.get(name)
+                    if view is None:
+                        h = ctypes.c_void_p()
+                        _lib.check(_lib.load().rsk_bloom_bitset(v[1], ctypes.byref(h)), "rsk_bloom_bitset")
+                        view = self._views[name] = h
+                    return view
                 if v[0] != "bitset":
                     self._wrongtype(name)
                 return v[1]

@@ -6,6 +6,7 @@
 // mapping.  All arithmetic on keys runs in the HIP kernels of rsk_hll.hip /
 // rsk_bloom.hip; nothing here hashes a key.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -116,6 +117,7 @@ using namespace rsk;
 struct CtxLock {
   std::lock_guard<std::recursive_mutex> g;
   explicit CtxLock(rsk_ctx* c) : g(c->mu) {
+    if (c->dead) fail(RSK_ERR_DEVICE, "the context's device work failed earlier; shut it down");
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) fail(RSK_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
@@ -440,12 +442,21 @@ FastMod63 make_fastmod(uint64_t d) {
   return f;
 }
 
-// Waits until every queued completion has run (its copy done, its callback
-// returned).  Completions take no context lock, so callers may hold it.
-void drain_done(rsk_ctx* c) {
+// The submission number of the last asynchronous call issued so far.
+uint64_t done_mark(rsk_ctx* c) {
+  std::lock_guard<std::mutex> g(c->done_mu);
+  return c->done_submitted;
+}
+
+// Waits until the completions of every call up to submission number `upto`
+// have run (copy done, callback returned).  Callbacks may call back into the
+// library (and take the context lock), so this must never run under the
+// context lock: a thread holding it while waiting here would wait for a
+// callback that waits for the lock.
+void drain_done(rsk_ctx* c, uint64_t upto) {
   std::unique_lock<std::mutex> lk(c->done_mu);
   if (c->done_thr.get_id() == std::this_thread::get_id()) return;  // a callback calling in: do not wait for itself
-  c->done_cv.wait(lk, [c] { return c->done_delivered == c->done_submitted && !c->done_busy; });
+  c->done_cv.wait(lk, [&] { return c->done_delivered >= upto; });
 }
 
 // Drains and joins the completion thread (the stream must be drained first,
@@ -598,11 +609,17 @@ int rsk_trim(rsk_ctx* c) {
 int rsk_sync(rsk_ctx* c) {
   return guarded([&] {
     need(c != nullptr, "ctx is NULL");
-    CtxLock l(c);
-    RSK_HIP(hipStreamSynchronize(c->stream));
-    RSK_HIP(hipStreamSynchronize(c->xin));
-    RSK_HIP(hipStreamSynchronize(c->xout));
-    drain_done(c);
+    uint64_t upto;
+    {
+      CtxLock l(c);
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      RSK_HIP(hipStreamSynchronize(c->xin));
+      RSK_HIP(hipStreamSynchronize(c->xout));
+      upto = done_mark(c);  // every call so far has reached the completion thread
+    }
+    // outside the lock: a callback still running may call into this context
+    drain_done(c, upto);
+    if (c->dead) fail(RSK_ERR_DEVICE, "the context's device work failed");
   });
 }
 
@@ -719,7 +736,9 @@ int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     check_keys(c, keys);  // before the key is created: a refused batch leaves it absent
-    hll_forget_import(h, id);
+    // An imported string stays the key's GET until a register changes (Redis
+    // leaves the string alone after a PFADD that changes nothing).
+    const bool had_import = h->imported.count(id) != 0;
     bool created;
     create_if_missing(h, id, &created);
     // The reduce kernel raises the flag to this call's epoch when a register
@@ -736,12 +755,14 @@ int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_
       any_chunk = true;
     });
     if (!any_chunk && created) invalidate(h, id, nullptr, true);  // PFADD key (no elements) creates it
-    if (changed_out) {
+    if (changed_out || had_import) {
       RSK_HIP(hipMemcpyAsync(c->h_small, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
       uint32_t f;
       std::memcpy(&f, c->h_small, 4);
-      *changed_out = (uint8_t)((f == epoch) || created);
+      const bool changed = (f == epoch) || created;
+      if (changed_out) *changed_out = (uint8_t)changed;
+      if (changed) hll_forget_import(h, id);
     }
   });
 }
@@ -1244,7 +1265,19 @@ int rsk_hll_import_redis(rsk_hll* h, uint64_t id, const uint8_t* buf, size_t len
     RSK_HIP(hipStreamSynchronize(c->stream));
     h->exists[id] = 1;
     h->dense[id] = buf[4] == 0;
-    h->imported[id].assign(buf, buf + len);
+    // GET must return the SET bytes until the key is written.  Export
+    // re-encodes canonically (dense packing; sparse runs cut into the longest
+    // opcodes), so a copy is kept only when that re-encoding would differ:
+    // non-zero unused header bytes, or a sparse string Redis would hold in
+    // another form (other run chunking, or longer than the sparse limit).
+    bool canonical = buf[5] == 0 && buf[6] == 0 && buf[7] == 0;
+    if (canonical && buf[4] == 1) {
+      std::vector<uint8_t> enc(RSK_HLL_DENSE_BYTES);
+      const size_t n = encode_sparse(raw.data(), enc.data(), enc.size());
+      canonical = n != 0 && 16 + n <= HLL_SPARSE_MAX_BYTES && 16 + n == len && std::memcmp(enc.data(), buf + 16, n) == 0;
+    }
+    if (canonical) hll_forget_import(h, id);
+    else h->imported[id].assign(buf, buf + len);
   });
 }
 
@@ -1457,12 +1490,21 @@ namespace {
 enum AsyncKind { K_PRESET = 0, K_RES_U64 = 1, K_HLL_FLAG = 2, K_OUT_BYTES = 3 };
 constexpr uint64_t ASYNC_STAGE_MAX = 256ull << 20;  // larger host batches run synchronously
 
-// Runs on the context's completion thread after the stream passed the op: no
-// HIP call here.  Derives the reply, copies per-key outputs to the caller,
-// hands the op back to the pool, then calls the caller.
-void op_complete(void* p) {
-  auto* op = static_cast<AsyncOp*>(p);
+// Runs on the context's completion thread after the stream passed the op.
+// Derives the reply, copies per-key outputs to the caller, hands the op back
+// to the pool, then calls the caller.  A device error recorded on the op's
+// stream (its completion event reports it) is passed on as RSK_ERR_DEVICE.
+void op_complete(AsyncOp* op) {
   uint64_t v = op->value;
+  int status = RSK_OK;
+  const hipError_t e = hipEventQuery(op->ev_out);
+  if (e != hipSuccess && e != hipErrorNotReady) {
+    (void)hipGetLastError();
+    status = RSK_ERR_DEVICE;
+    op->kind = K_PRESET;  // nothing valid to read back
+    v = 0;
+    op->c->dead = true;
+  }
   switch (op->kind) {
     case K_RES_U64:
       v = op->h_res[0];
@@ -1483,7 +1525,7 @@ void op_complete(void* p) {
     std::lock_guard<std::mutex> g(c->async_mu);
     c->async_free.push_back(op);
   }
-  if (cb) cb(user, RSK_OK, v);
+  if (cb) cb(user, status, v);
 }
 
 // An op with >= host_bytes of pinned and >= dev_bytes of device buffer
@@ -1579,19 +1621,53 @@ void op_release(AsyncOp* op) {  // an op that was taken but will not be submitte
   op->c->async_free.push_back(op);
 }
 
+// A sticky error on one of the context's streams (a faulted kernel or copy):
+// the host functions queued behind it may never run.
+bool streams_failed(rsk_ctx* c) {
+  for (hipStream_t s : {c->stream, c->xin, c->xout}) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipSuccess && e != hipErrorNotReady) {
+      (void)hipGetLastError();
+      return true;
+    }
+  }
+  return false;
+}
+
 void done_loop(rsk_ctx* c) {
+  (void)hipSetDevice(c->device);
   std::unique_lock<std::mutex> lk(c->done_mu);
   auto ready = [c] { return !c->done_arrived.empty() && c->done_arrived.begin()->first == c->done_delivered + 1; };
   for (;;) {
-    c->done_cv.wait(lk, [&] { return ready() || (c->done_stop && c->done_delivered == c->done_submitted); });
+    const bool woke = c->done_cv.wait_for(lk, std::chrono::milliseconds(500), [&] {
+      return ready() || (c->done_stop && c->done_delivered == c->done_submitted);
+    });
+    if (!woke) {
+      // Calls outstanding and nothing arrived for a while: if a stream holds a
+      // device error, their host functions may never fire; fail them (in
+      // order) rather than leave their callers waiting forever.
+      if (c->done_pending.empty() || !streams_failed(c)) continue;
+      c->dead = true;
+      while (!c->done_pending.empty()) {
+        auto it = c->done_pending.begin();
+        AsyncOp* op = it->second;
+        c->done_pending.erase(it);
+        c->done_arrived.erase(op->seq);
+        lk.unlock();
+        if (op->cb) op->cb(op->user, RSK_ERR_DEVICE, 0);  // the op is not recycled: its copies may still be queued
+        lk.lock();
+        c->done_delivered = std::max(c->done_delivered, op->seq);
+        c->done_cv.notify_all();
+      }
+      continue;
+    }
     if (!ready()) return;  // stopping, every op delivered
     AsyncOp* op = c->done_arrived.begin()->second;
     c->done_arrived.erase(c->done_arrived.begin());
-    c->done_busy = true;
+    c->done_pending.erase(op->seq);
     lk.unlock();
     op_complete(op);
     lk.lock();
-    c->done_busy = false;
     ++c->done_delivered;
     c->done_cv.notify_all();  // drain_done waiters
   }
@@ -1603,6 +1679,7 @@ void op_reached(void* p) {
   rsk_ctx* c = op->c;
   {
     std::lock_guard<std::mutex> g(c->done_mu);
+    if (op->seq <= c->done_delivered) return;  // already failed by the watchdog
     c->done_arrived.emplace(op->seq, op);
   }
   c->done_cv.notify_all();
@@ -1644,11 +1721,13 @@ void op_submit(AsyncOp* op, rsk_done_fn cb, void* user) {
     std::lock_guard<std::mutex> g(c->done_mu);
     if (!c->done_thr.joinable()) c->done_thr = std::thread(done_loop, c);
     op->seq = ++c->done_submitted;  // (callers hold the context lock: one submitter at a time)
+    c->done_pending.emplace(op->seq, op);
   }
   const hipError_t e = hipLaunchHostFunc(c->xout, op_reached, op);
   if (e != hipSuccess) {  // never filed: take its number back
     {
       std::lock_guard<std::mutex> g(c->done_mu);
+      c->done_pending.erase(op->seq);
       --c->done_submitted;
     }
     RSK_HIP(e);
@@ -1694,7 +1773,7 @@ int run_now(rsk_ctx* c, F&& sync_call, rsk_done_fn cb, void* user, uint64_t valu
   uint64_t v = value_if_void;
   const int rc = sync_call(&v);
   if (rc == RSK_OK && cb) {
-    drain_done(c);  // earlier calls' callbacks first
+    drain_done(c, done_mark(c));  // earlier calls' callbacks first
     cb(user, RSK_OK, value_from_call ? v : value_if_void);
   }
   return rc;

@@ -21,6 +21,16 @@ struct rsk_bitset {
   uint8_t* d = nullptr;    // device bytes, capacity `cap` (zero beyond len)
   uint64_t len = 0;        // STRLEN
   uint64_t cap = 0;
+  // A view of a Bloom filter's bit string (rsk_bloom_bitset): in Redis the
+  // filter's bits ARE the string key `name` (RedissonBloomFilter SETBITs it,
+  // RedissonBitSet reads it), so getBitSet(filterName) sees them.  d is the
+  // filter's buffer (not owned); the string can hold at most the filter's
+  // ceil(size/8) bytes.  STRLEN is Redis's: the highest byte any SETBIT
+  // touched + 1 -- a Bloom add only sets bits, so for its part that is the
+  // last non-zero byte + 1; `floor` carries what writes through the view
+  // (clears, SET, BITOP) fixed beyond that.
+  rsk_bloom* alias = nullptr;
+  uint64_t floor = 0;
 };
 
 namespace {
@@ -54,8 +64,44 @@ struct Lock {
 // Redis limits a string to 512 MB: offsets up to 2^32 - 1 bits.
 constexpr uint64_t MAX_BIT_OFFSET = (1ull << 32) - 1;
 
+uint32_t grid_of(rsk_ctx* c, uint64_t n);
+__global__ void length_kernel(const uint4* __restrict__ d, uint64_t len, unsigned long long* __restrict__ out);
+
+// Highest set bit + 1 of bytes [0, len) (0 when none); the buffer is padded
+// to 16 bytes and zero past len.  Under the context lock.
+uint64_t length_bits(rsk_ctx* c, const uint8_t* d, uint64_t len) {
+  if (len == 0) return 0;
+  auto* dl = reinterpret_cast<unsigned long long*>(c->d_small + 320);
+  RSK_HIP(hipMemsetAsync(dl, 0, 8, c->stream));
+  hipLaunchKernelGGL(length_kernel, dim3(grid_of(c, (len + 15) / 16)), dim3(256), 0, c->stream,
+                     reinterpret_cast<const uint4*>(d), len, dl);
+  RSK_CHECK_LAUNCH("bitset_length");
+  RSK_HIP(hipMemcpyAsync(c->h_small + 320, dl, 8, hipMemcpyDeviceToHost, c->stream));
+  RSK_HIP(hipStreamSynchronize(c->stream));
+  uint64_t v;
+  std::memcpy(&v, c->h_small + 320, 8);
+  return v;
+}
+
+// A view's STRLEN as it stands now (Bloom adds may have grown it since the
+// last call): refreshes b->d / cap / len.  Plain strings are left alone.
+void sync_view(rsk_bitset* b) {
+  if (!b->alias) return;
+  b->d = reinterpret_cast<uint8_t*>(b->alias->d_bits);
+  b->cap = b->alias->nwords * 4;
+  const uint64_t bits = length_bits(b->ctx, b->d, b->alias->nbytes);
+  const uint64_t used = bits ? ((bits - 1) >> 3) + 1 : 0;
+  b->len = std::max(b->floor, used);
+}
+
 // Grow the string to `newlen` bytes (zero filled), keeping 16-byte padding.
 void grow(rsk_bitset* b, uint64_t newlen) {
+  if (b->alias) {  // the filter's buffer is the string: it cannot move or grow past the filter
+    need(newlen <= b->alias->nbytes, "ERR the string of a GPU Bloom filter cannot grow past the filter's size");
+    b->floor = std::max(b->floor, newlen);
+    b->len = std::max(b->len, newlen);
+    return;
+  }
   if (newlen <= b->len) return;
   rsk_ctx* c = b->ctx;
   if (newlen > b->cap) {
@@ -219,15 +265,32 @@ int rsk_bitset_destroy(rsk_bitset* b) {
   int rc = guarded([&] {
     Lock l(b->ctx);
     RSK_HIP(hipStreamSynchronize(b->ctx->stream));
-    if (b->d) RSK_HIP(hipFree(b->d));
+    if (b->d && !b->alias) RSK_HIP(hipFree(b->d));
   });
   delete b;
   return rc;
 }
 
+// The bit string of Bloom filter f as an RBitSet (see rsk_bitset.alias).
+int rsk_bloom_bitset(rsk_bloom* f, rsk_bitset** out) {
+  return guarded([&] {
+    need(f && out, "NULL argument");
+    Lock l(f->ctx);
+    auto* b = new rsk_bitset();
+    b->ctx = f->ctx;
+    b->alias = f;
+    sync_view(b);
+    *out = b;
+  });
+}
+
 int rsk_bitset_strlen(rsk_bitset* b, uint64_t* out) {
   return guarded([&] {
     need(b && out, "NULL argument");
+    if (b->alias) {
+      Lock l(b->ctx);
+      sync_view(b);
+    }
     *out = b->len;
   });
 }
@@ -239,9 +302,11 @@ int rsk_bitset_setbits(rsk_bitset* b, const uint64_t* offs, uint64_t n, int valu
     if (n == 0) return;
     rsk_ctx* c = b->ctx;
     Lock l(c);
+    sync_view(b);
     uint64_t mx = 0;
     const uint64_t* d_offs = device_offsets(c, offs, n, location, &mx);
     need(mx <= MAX_BIT_OFFSET, "ERR bit offset is not an integer or out of range");
+    if (b->alias && value == 0) b->floor = std::max(b->floor, b->len);  // cleared bits keep the length
     grow(b, (mx >> 3) + 1);
     rsk::ProfScope ps(c, "bitset_setbits");
     hipLaunchKernelGGL(setbits_kernel, dim3(grid_of(c, n)), dim3(256), 0, c->stream, b->d, d_offs, n, value);
@@ -256,6 +321,7 @@ int rsk_bitset_getbits(rsk_bitset* b, const uint64_t* offs, uint64_t n, uint32_t
     if (n == 0) return;
     rsk_ctx* c = b->ctx;
     Lock l(c);
+    sync_view(b);
     uint64_t mx = 0;
     const uint64_t* d_offs = device_offsets(c, offs, n, location, &mx);
     need(mx <= MAX_BIT_OFFSET, "ERR bit offset is not an integer or out of range");
@@ -281,6 +347,8 @@ int rsk_bitset_set_range(rsk_bitset* b, uint64_t from, uint64_t to, int value) {
     need(to - 1 <= MAX_BIT_OFFSET, "ERR bit offset is not an integer or out of range");
     rsk_ctx* c = b->ctx;
     Lock l(c);
+    sync_view(b);
+    if (b->alias && value == 0) b->floor = std::max(b->floor, b->len);
     grow(b, ((to - 1) >> 3) + 1);
     // Whole bytes by a memset; the partial first / last byte by the mask kernel.
     const uint64_t full_lo = (from + 7) >> 3, full_hi = to >> 3;  // bytes [full_lo, full_hi) are covered whole
@@ -303,6 +371,7 @@ int rsk_bitset_bitcount(rsk_bitset* b, uint64_t* out) {
     need(b && out, "NULL argument");
     rsk_ctx* c = b->ctx;
     Lock l(c);
+    sync_view(b);
     if (b->len == 0) {
       *out = 0;
       return;
@@ -321,18 +390,8 @@ int rsk_bitset_length(rsk_bitset* b, uint64_t* out) {
     need(b && out, "NULL argument");
     rsk_ctx* c = b->ctx;
     Lock l(c);
-    if (b->len == 0) {
-      *out = 0;
-      return;
-    }
-    auto* d = reinterpret_cast<unsigned long long*>(c->d_small + 320);
-    RSK_HIP(hipMemsetAsync(d, 0, 8, c->stream));
-    hipLaunchKernelGGL(length_kernel, dim3(grid_of(c, (b->len + 15) / 16)), dim3(256), 0, c->stream,
-                       reinterpret_cast<const uint4*>(b->d), b->len, d);
-    RSK_CHECK_LAUNCH("bitset_length");
-    RSK_HIP(hipMemcpyAsync(c->h_small + 320, d, 8, hipMemcpyDeviceToHost, c->stream));
-    RSK_HIP(hipStreamSynchronize(c->stream));
-    std::memcpy(out, c->h_small + 320, 8);
+    sync_view(b);
+    *out = length_bits(c, b->d, b->len);
   });
 }
 
@@ -343,21 +402,26 @@ int rsk_bitset_bitop(int op, rsk_bitset* dst, rsk_bitset* const* srcs, uint32_t 
     need(op != RSK_BITOP_NOT || k == 1, "BITOP NOT must be called with a single source key.");
     rsk_ctx* c = dst->ctx;
     Lock l(c);
+    sync_view(dst);
     SrcList s{};
     s.k = k;
     uint64_t maxlen = 0;
     for (uint32_t j = 0; j < k; ++j) {
       need(srcs[j] && srcs[j]->ctx == c, "sources must share the context");
+      sync_view(srcs[j]);
       s.p[j] = srcs[j]->d;
       s.len[j] = srcs[j]->len;
       maxlen = std::max(maxlen, srcs[j]->len);
     }
     if (maxlen == 0) {  // every source empty: Redis deletes the destination
       dst->len = 0;
+      dst->floor = 0;
       if (dst->d) RSK_HIP(hipMemsetAsync(dst->d, 0, dst->cap, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
       return;
     }
+    if (dst->alias)
+      need(maxlen <= dst->alias->nbytes, "ERR the string of a GPU Bloom filter cannot grow past the filter's size");
     // Compute into a fresh buffer (dst may be one of the sources), then swap.
     const uint64_t cap = (maxlen + 16 + 15) & ~uint64_t(15);
     uint8_t* nd = nullptr;
@@ -366,6 +430,14 @@ int rsk_bitset_bitop(int op, rsk_bitset* dst, rsk_bitset* const* srcs, uint32_t 
     hipLaunchKernelGGL(bitop_kernel, dim3(grid_of(c, (maxlen + 15) / 16)), dim3(256), 0, c->stream,
                        reinterpret_cast<uint4*>(nd), maxlen, s, op);
     RSK_CHECK_LAUNCH("bitset_bitop");
+    if (dst->alias) {  // written into the filter's own buffer (zero past the result)
+      RSK_HIP(hipMemsetAsync(dst->d, 0, dst->cap, c->stream));
+      RSK_HIP(hipMemcpyAsync(dst->d, nd, maxlen, hipMemcpyDeviceToDevice, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      RSK_HIP(hipFree(nd));
+      dst->floor = dst->len = maxlen;
+      return;
+    }
     RSK_HIP(hipStreamSynchronize(c->stream));
     if (dst->d) RSK_HIP(hipFree(dst->d));
     dst->d = nd;
@@ -377,8 +449,9 @@ int rsk_bitset_bitop(int op, rsk_bitset* dst, rsk_bitset* const* srcs, uint32_t 
 int rsk_bitset_get_bytes(rsk_bitset* b, uint8_t* buf, size_t cap, size_t* len) {
   return guarded([&] {
     need(b && len, "NULL argument");
-    need(cap >= b->len && (buf || b->len == 0), "buffer smaller than STRLEN");
     Lock l(b->ctx);
+    sync_view(b);
+    need(cap >= b->len && (buf || b->len == 0), "buffer smaller than STRLEN");
     if (b->len) {
       RSK_HIP(hipMemcpyAsync(buf, b->d, b->len, hipMemcpyDeviceToHost, b->ctx->stream));
       RSK_HIP(hipStreamSynchronize(b->ctx->stream));
@@ -392,8 +465,12 @@ int rsk_bitset_set_bytes(rsk_bitset* b, const uint8_t* buf, size_t len) {
     need(b && (buf || len == 0), "NULL argument");
     rsk_ctx* c = b->ctx;
     Lock l(c);
+    sync_view(b);
+    if (b->alias)
+      need(len <= b->alias->nbytes, "ERR the string of a GPU Bloom filter cannot grow past the filter's size");
     if (b->d) RSK_HIP(hipMemsetAsync(b->d, 0, b->cap, c->stream));
     b->len = 0;
+    b->floor = 0;
     grow(b, len);
     if (len) RSK_HIP(hipMemcpyAsync(b->d, buf, len, hipMemcpyHostToDevice, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
@@ -404,9 +481,11 @@ int rsk_bitset_clear(rsk_bitset* b) {
   return guarded([&] {
     need(b != nullptr, "NULL argument");
     Lock l(b->ctx);
+    sync_view(b);
     if (b->d) RSK_HIP(hipMemsetAsync(b->d, 0, b->cap, b->ctx->stream));
     RSK_HIP(hipStreamSynchronize(b->ctx->stream));
     b->len = 0;
+    b->floor = 0;
   });
 }
 

@@ -163,6 +163,26 @@ int rsk_comm_init(rsk_ctx* c, int nranks, int rank, const uint8_t* id) {
   });
 }
 
+// What RCCL itself reports for the context's communicator (not the arguments
+// rsk_comm_init was given): a bench line or a test can then show that every
+// rank joined.  Without a communicator: 1 rank, rank 0.
+int rsk_comm_info(rsk_ctx* c, int* nranks, int* rank) {
+  return guarded([&] {
+    need(c && nranks && rank, "NULL argument");
+    Lock l(c);
+    if (!c->comm) {
+      *nranks = 1;
+      *rank = 0;
+      return;
+    }
+    int n = 0, r = -1;
+    RSK_NCCL(ncclCommCount(reinterpret_cast<ncclComm_t>(c->comm), &n));
+    RSK_NCCL(ncclCommUserRank(reinterpret_cast<ncclComm_t>(c->comm), &r));
+    *nranks = n;
+    *rank = r;
+  });
+}
+
 int rsk_comm_destroy(rsk_ctx* c) {
   return guarded([&] {
     need(c != nullptr, "ctx is NULL");

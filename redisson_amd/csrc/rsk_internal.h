@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <map>
 #include <mutex>
@@ -172,9 +173,13 @@ struct rsk_ctx {
   std::mutex done_mu;
   std::condition_variable done_cv;
   std::map<uint64_t, rsk::AsyncOp*> done_arrived;  // by seq
+  std::map<uint64_t, rsk::AsyncOp*> done_pending;  // submitted, not delivered (by seq)
   uint64_t done_submitted = 0, done_delivered = 0;
-  bool done_busy = false;
   bool done_stop = false;
+  // A device error was seen on one of the context's streams while calls were
+  // outstanding: their callbacks got RSK_ERR_DEVICE and every later call on
+  // the context fails with it (its streams cannot be trusted any more).
+  std::atomic<bool> dead{false};
 
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);

@@ -59,6 +59,14 @@ def init_comm(engine, group=None) -> None:
     _lib.check(L.rsk_comm_init(engine.ctx, world, rank, uid), "rsk_comm_init")
 
 
+def comm_info(engine):
+    """(nranks, rank) as RCCL itself reports them for this context's
+    communicator (ncclCommCount / ncclCommUserRank); (1, 0) without one."""
+    n, r = ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.load().rsk_comm_info(engine.ctx, ctypes.byref(n), ctypes.byref(r)), "rsk_comm_info")
+    return n.value, r.value
+
+
 def hll_allreduce(pool, sketch_id: int = 0) -> None:
     _lib.check(_lib.load().rsk_hll_allreduce(pool, sketch_id), "rsk_hll_allreduce")
 

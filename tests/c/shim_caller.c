@@ -8,15 +8,24 @@
  * every getter and of add/contains on a filter nobody initialised, tryInit's
  * idempotence ACROSS instances (two lookups of one name = one filter), count
  * of a missing HLL creating nothing, the "config has been changed" guard --
- * then the RBatch of add()s, async calls from two threads on two handles, and
- * a 200k-element batch checked against the CPU oracle.  Needs a GPU; run by
+ * then the RBatch of add()s, async calls from two threads on two handles,
+ * completion callbacks that call back into the shim (a further async add and
+ * a synchronous count from inside a callback, a delete whose last reference
+ * drops in a callback, a callback's call while another thread waits in
+ * rsk_shim_sync -- none may deadlock: a watchdog fails the run), RBitSet on a
+ * plain name and on a Bloom filter's name (getBitSet(filterName) reads the
+ * filter's bits: GET equals rsk_bloom_export_bits up to Redis's STRLEN), and a
+ * 200k-element batch checked against the CPU oracle.  Needs a GPU; run by
  * tests/test_jni_shim.py (-m gpu).
  * Exit 0 = all checks passed; prints one line per failed check otherwise.
  */
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "../../jni/rsketch_shim.h"
 #include "../../oracle/rsk_oracle.h"
@@ -142,7 +151,65 @@ static void *issue(void *p) {
   return NULL;
 }
 
+/* ------------------------------------------------- re-entrant callbacks */
+static batch RE; /* the keys the callbacks add */
+static volatile int re_rc_async = -1, re_rc_count = -1;
+static volatile int64_t re_count = -1;
+
+/* Slot 40: from inside the completion, issue a further async add (slot 41)
+ * and a synchronous count on the same space. */
+static void reenter(void *user, int status, uint64_t value) {
+  (void)user;
+  (void)status;
+  (void)value;
+  re_rc_async = rsk_shim_hll_add_async(S, "reent", kbuf(&RE), obuf(&RE), 2, done, (void *)(intptr_t)41);
+  int64_t c = -1;
+  re_rc_count = rsk_shim_hll_count(S, "reent", &c);
+  re_count = c;
+  done((void *)(intptr_t)40, status, value);
+}
+
+/* Slot 42: waits until the main thread is (about to be) inside
+ * rsk_shim_sync, then makes a synchronous library call -- the round-3 code
+ * held the context lock while waiting for this callback. */
+static volatile int sync_started;
+static void late_caller(void *user, int status, uint64_t value) {
+  (void)user;
+  while (!sync_started) {
+    const struct timespec ts = {0, 1000000L};
+    nanosleep(&ts, NULL);
+  }
+  const struct timespec ts = {0, 50000000L}; /* 50 ms: the main thread is inside the wait by now */
+  nanosleep(&ts, NULL);
+  int64_t c = -1;
+  const int rc = rsk_shim_hll_count(S, "reent", &c);
+  done((void *)(intptr_t)42, rc == RSK_OK ? status : rc, (uint64_t)c);
+  (void)value;
+}
+
+/* Slot 43: deletes the name its own call went to -- the map's reference is
+ * the last one, so the sketch is destroyed from inside the callback. */
+static void deleter(void *user, int status, uint64_t value) {
+  (void)user;
+  int32_t d = -1;
+  const int rc = rsk_shim_delete(S, "doomed", &d);
+  done((void *)(intptr_t)43, rc == RSK_OK && d == 1 ? status : 99, value);
+}
+
+static void on_alarm(int sig) {
+  (void)sig;
+  static const char msg[] = "FAIL watchdog: a call deadlocked\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  _exit(3);
+}
+
+static int contains_bytes(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
+  return na == nb && (na == 0 || memcmp(a, b, na) == 0);
+}
+
 int main(void) {
+  signal(SIGALRM, on_alarm);
+  alarm(100); /* every check below finishes in seconds; a deadlock does not */
   if (rsk_shim_init(0, 0, &S)) {
     fprintf(stderr, "init: %s (%s)\n", rsk_shim_last_error(), rsk_shim_exception_class(RSK_ERR_NO_DEVICE));
     return 2;
@@ -380,6 +447,126 @@ int main(void) {
     CHECK(all);
     free(got), free(want), free(con), free(bits), free(offs);
     free(keys[0]), free(keys[1]);
+  }
+
+  /* Completion callbacks that call back into the shim. */
+  {
+    put(&RE, "\"r1\"");
+    put(&RE, "\"r2\"");
+    CHECK(rsk_shim_hll_add_async(S, "reent", kbuf(&RE), obuf(&RE), 1, reenter, NULL) == RSK_OK);
+    wait_slots(40, 42);
+    CHECK(re_rc_async == RSK_OK && re_rc_count == RSK_OK && re_count >= 1);
+    CHECK(W.value[40] == 1 && W.value[41] == 1); /* "r1" created the key; "r2" grew it */
+    CHECK(rsk_shim_hll_count(S, "reent", &cnt) == RSK_OK && cnt == 2);
+
+    /* a callback's synchronous call while the main thread waits in rsk_shim_sync */
+    CHECK(rsk_shim_hll_add_async(S, "reent", kbuf(&RE), obuf(&RE), 2, late_caller, NULL) == RSK_OK);
+    sync_started = 1;
+    CHECK(rsk_shim_sync(S) == RSK_OK);
+    CHECK(W.fired[42] == 1 && W.status[42] == RSK_OK && W.value[42] == 2); /* sync waited for the callback */
+
+    /* the last reference drops inside the callback (the callback deletes) */
+    CHECK(rsk_shim_hll_add_async(S, "doomed", kbuf(&RE), obuf(&RE), 2, deleter, NULL) == RSK_OK);
+    wait_slots(43, 44);
+    CHECK(W.status[43] == RSK_OK);
+    CHECK(rsk_shim_lookup(S, "doomed", &type, &hnd) == RSK_OK && type == RSK_SHIM_NONE);
+    /* ... and the last reference drops in the shim's own completion (delete while in flight) */
+    CHECK(rsk_shim_hll_add_async(S, "doomed2", kbuf(&RE), obuf(&RE), 2, done, (void *)(intptr_t)44) == RSK_OK);
+    CHECK(rsk_shim_delete(S, "doomed2", &deleted) == RSK_OK && deleted == 1);
+    wait_slots(44, 45);
+    CHECK(rsk_shim_sync(S) == RSK_OK);
+    CHECK(rsk_shim_lookup(S, "doomed2", &type, &hnd) == RSK_OK && type == RSK_SHIM_NONE);
+  }
+
+  /* RBitSet on plain names (RedissonBitSetTest.java:12-137 semantics) */
+  {
+    int64_t v = -1;
+    uint8_t *bytes = NULL;
+    int64_t len = 0;
+    CHECK(rsk_shim_bitset_get_bytes(S, "bs", &bytes, &len) == RSK_OK && len == -1 && !bytes); /* nil */
+    CHECK(rsk_shim_bitset_cardinality(S, "bs", &v) == RSK_OK && v == 0);
+    const int64_t idx[3] = {3, 5, 17};
+    CHECK(rsk_shim_bitset_setbits(S, "bs", idx, 3, 1) == RSK_OK);
+    CHECK(rsk_shim_bitset_strlen(S, "bs", &v) == RSK_OK && v == 3); /* (17 >> 3) + 1 */
+    CHECK(rsk_shim_bitset_cardinality(S, "bs", &v) == RSK_OK && v == 3);
+    CHECK(rsk_shim_bitset_length(S, "bs", &v) == RSK_OK && v == 18);
+    CHECK(rsk_shim_bitset_get_bytes(S, "bs", &bytes, &len) == RSK_OK && len == 3);
+    if (len == 3) CHECK(bytes[0] == 0x14 && bytes[1] == 0 && bytes[2] == 0x40); /* MSB-first */
+    rsk_shim_free(bytes);
+    uint8_t g[4];
+    const int64_t q[4] = {3, 4, 17, 100000};
+    CHECK(rsk_shim_bitset_getbits(S, "bs", q, 4, g, 4) == RSK_OK && g[0] == 1 && g[1] == 0 && g[2] == 1 && g[3] == 0);
+    const int64_t bad[1] = {-1};
+    CHECK(rsk_shim_bitset_setbits(S, "bs", bad, 1, 1) == RSK_SHIM_REDIS_ERROR);
+    CHECK(strcmp(rsk_shim_exception_class(RSK_SHIM_REDIS_ERROR), "org/redisson/client/RedisException") == 0);
+    /* BITOP AND bs bs other (RedissonBitSetTest.testAnd): other missing -> empty -> bs goes away */
+    const char *other[1] = {"bs-other"};
+    CHECK(rsk_shim_bitset_set_range(S, "bs-other", 0, 8, 1) == RSK_OK); /* byte 0 = 0xFF */
+    CHECK(rsk_shim_bitset_op(S, "bs", RSK_BITOP_AND, other, 1) == RSK_OK);
+    CHECK(rsk_shim_bitset_get_bytes(S, "bs", &bytes, &len) == RSK_OK && len == 3);
+    if (len == 3) CHECK(bytes[0] == 0x14 && bytes[1] == 0 && bytes[2] == 0);
+    rsk_shim_free(bytes);
+    const char *nobody[1] = {"bs-nobody"};
+    CHECK(rsk_shim_bitset_op(S, "bs-new", RSK_BITOP_OR, nobody, 1) == RSK_OK); /* all empty: no key */
+    CHECK(rsk_shim_lookup(S, "bs-new", &type, &hnd) == RSK_OK && type == RSK_SHIM_NONE);
+    CHECK(rsk_shim_bitset_op(S, "bs", RSK_BITOP_NOT, other, 1) == RSK_SHIM_REDIS_ERROR);
+    int32_t dd = 0;
+    CHECK(rsk_shim_bitset_clear(S, "bs", &dd) == RSK_OK && dd == 1);
+    CHECK(rsk_shim_lookup(S, "bs", &type, &hnd) == RSK_OK && type == RSK_SHIM_NONE);
+    CHECK(rsk_shim_bitset_cardinality(S, "log", &v) == RSK_ERR_WRONGTYPE); /* an HLL name */
+    CHECK(rsk_shim_delete(S, "bs-other", &deleted) == RSK_OK && deleted == 1);
+  }
+
+  /* getBitSet(bloomName): the filter's bits, as Redis's GET of the filter key */
+  {
+    const int64_t n = 20000;
+    unsigned char *keys = malloc((size_t)n * 16);
+    int64_t *offs = malloc((size_t)(n + 1) * 8);
+    orc_gen_keys16(0x5EED0200, 0, (uint64_t)n, keys);
+    for (int64_t i = 0; i <= n; ++i) offs[i] = 16 * i;
+    rsk_shim_buf kb = {keys, 16 * n}, ob = {offs, n + 1};
+    CHECK(rsk_shim_bloom_try_init(S, "bf", n, 0.01, &created, &cfg) == RSK_OK && created == 1);
+    uint8_t *bytes = NULL;
+    int64_t len = 0, v = -1;
+    CHECK(rsk_shim_bitset_get_bytes(S, "bf", &bytes, &len) == RSK_OK && len == -1); /* nothing added: no string */
+    CHECK(rsk_shim_bloom_add(S, "bf", cfg.size, cfg.hash_iterations, kb, ob, n, NULL, 0) == RSK_OK);
+    CHECK(rsk_shim_lookup(S, "bf", &type, &hnd) == RSK_OK && type == RSK_SHIM_BLOOM);
+    const size_t nb = (size_t)((cfg.size + 7) / 8);
+    uint8_t *exp = malloc(nb);
+    size_t elen = 0;
+    CHECK(rsk_bloom_export_bits((rsk_bloom *)(intptr_t)hnd, exp, nb, &elen) == RSK_OK && elen == nb);
+    size_t redis_len = elen; /* STRLEN: the last byte a SETBIT touched (adds only set bits) */
+    while (redis_len > 0 && exp[redis_len - 1] == 0) --redis_len;
+    CHECK(rsk_shim_bitset_get_bytes(S, "bf", &bytes, &len) == RSK_OK);
+    CHECK(contains_bytes(bytes, (size_t)len, exp, redis_len));
+    rsk_shim_free(bytes);
+    CHECK(rsk_shim_bitset_strlen(S, "bf", &v) == RSK_OK && v == (int64_t)redis_len);
+    uint64_t pc = 0;
+    for (size_t i = 0; i < nb; ++i) pc += (uint64_t)__builtin_popcount(exp[i]);
+    CHECK(rsk_shim_bitset_cardinality(S, "bf", &v) == RSK_OK && (uint64_t)v == pc);
+    /* the oracle's bit string for the same adds */
+    uint8_t *obits = calloc(nb, 1);
+    orc_bloom_add_batch(obits, cfg.size, cfg.hash_iterations, keys, NULL, 16, (uint64_t)n, NULL);
+    CHECK(memcmp(obits, exp, nb) == 0);
+    /* GETBIT of the first set bit and of a clear one */
+    int64_t first = -1, clear = -1;
+    for (int64_t i = 0; i < (int64_t)nb * 8 && (first < 0 || clear < 0); ++i) {
+      const int set = (exp[i >> 3] >> (7 - (i & 7))) & 1;
+      if (set && first < 0) first = i;
+      if (!set && clear < 0) clear = i;
+    }
+    const int64_t q[2] = {first, clear};
+    uint8_t g[2] = {9, 9};
+    CHECK(rsk_shim_bitset_getbits(S, "bf", q, 2, g, 2) == RSK_OK && g[0] == 1 && g[1] == 0);
+    /* a write through the RBitSet is a write to the filter: clear() = DEL of the
+     * string; the filter stays initialised (its {name}__config) with no bits */
+    int32_t dd = 0, bc = -1;
+    CHECK(rsk_shim_bitset_clear(S, "bf", &dd) == RSK_OK && dd == 1);
+    CHECK(rsk_shim_bloom_count(S, "bf", &bc) == RSK_OK && bc == 0);
+    CHECK(rsk_shim_bloom_get_config(S, "bf", &cfg) == RSK_OK);
+    CHECK(rsk_shim_bitset_strlen(S, "bf", &v) == RSK_OK && v == 0);
+    CHECK(rsk_shim_delete(S, "bf", &deleted) == RSK_OK && deleted == 1);
+    free(keys), free(offs), free(exp), free(obits);
   }
 
   /* A 200k-element addAll through one "direct buffer" pair against the oracle. */

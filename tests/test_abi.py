@@ -84,7 +84,49 @@ def test_python_binding_covers_header(lib):
 
 
 def test_abi_version(lib):
-    assert lib.rsk_abi_version() == 1
+    """RSK_ABI_VERSION 2: the 24-byte rsk_options (stage_threads, reserved)
+    and the asynchronous entry points.  The C layout is pinned by the
+    compiler, the ctypes mirror against it."""
+    from redisson_amd import _lib
+
+    assert lib.rsk_abi_version() == 2 == _lib.ABI_VERSION
+    assert ctypes.sizeof(_lib.rsk_options) == 24
+    assert ctypes.sizeof(_lib.rsk_keys) == 32
+    src = ("#include <stddef.h>\n#include \"rsketch.h\"\n"
+           "_Static_assert(RSK_ABI_VERSION == 2, \"abi\");\n"
+           "_Static_assert(sizeof(rsk_options) == 24, \"rsk_options\");\n"
+           "_Static_assert(offsetof(rsk_options, stage_threads) == 16, \"stage_threads\");\n"
+           "_Static_assert(sizeof(rsk_keys) == 32, \"rsk_keys\");\n")
+    r = subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), "-x", "c", "-"],
+                       input=src, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_diag_library_refused_after_torch():
+    """librsketch_diag.so loaded after torch's HIP runtime is mapped crashed
+    rocprofv3 (round 3, commit c380052): _lib.diag() refuses that order with a
+    clear error, and accepts the right one."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from redisson_amd import _lib\n"
+            "_lib.load()\n"
+            "import torch\n"
+            "try:\n"
+            "    _lib.diag()\n"
+            "except ImportError as e:\n"
+            "    print('refused:', e)\n"
+            "else:\n"
+            "    print('loaded')\n") % ROOT
+    r = subprocess.run(["python3", "-c", code], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert "refused:" in r.stdout and "before torch" in r.stdout, r.stdout
+    ok = ("import sys; sys.path.insert(0, %r)\n"
+          "from redisson_amd import _lib\n"
+          "_lib.diag()\n"
+          "import torch\n"
+          "_lib.diag()\n"
+          "print('loaded')\n") % ROOT
+    r = subprocess.run(["python3", "-c", ok], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "loaded" in r.stdout, r.stdout + r.stderr
 
 
 def test_init_without_gpu_fails_loudly(lib):

@@ -20,7 +20,12 @@ def test_one_rank_communicator(engine, orc):
     L = _lib.load()
     uid = (ctypes.c_uint8 * 128)()
     _lib.check(L.rsk_comm_unique_id(uid))
+    from redisson_amd import shard
+
+    _lib.check(L.rsk_comm_destroy(engine.ctx))
+    assert shard.comm_info(engine) == (1, 0)  # no communicator
     _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    assert shard.comm_info(engine) == (1, 0)  # RCCL's own count and rank of the 1-rank communicator
     try:
         h = ctypes.c_void_p()
         _lib.check(L.rsk_hll_create(engine.ctx, 3, ctypes.byref(h)))

@@ -458,14 +458,36 @@ def test_c4_full_size_bit_exact(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
+def _c5_stratified_sample(G: int, per_bin: int = 34, seed: int = 11) -> np.ndarray:
+    """Sketch ids spread over the whole pool: from every coarse bin of the
+    partitioned grouped add (4096 sketches, g >> 12) `per_bin` ids whose fine-
+    bin slots (16 sketches, g & 15) cycle through all 16 positions and whose
+    fine bins spread over the coarse bin; plus the pool's first and last ids."""
+    rng = np.random.default_rng(seed)
+    ids = [0, G - 1]
+    for c in range((G + 4095) // 4096):
+        lo, hi = c * 4096, min(G, (c + 1) * 4096)
+        fines = (hi - lo + 15) // 16
+        for j, fb in enumerate(rng.choice(fines, size=min(per_bin, fines), replace=False)):
+            g = lo + 16 * int(fb) + j % 16
+            ids.append(min(g, hi - 1))
+    return np.unique(np.array(ids, np.uint64))
+
+
 def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
     """BASELINE configs[4] at its per-GPU size: 1M sketches, 500M (group, key)
-    pairs through the grouped PFADD; the first 2048 sketches are bit-exact
-    against the oracle over the whole pair stream, and PFCOUNT of the pool
-    matches the oracle's estimator on them."""
+    pairs through the grouped PFADD.  A stratified sample of >= 8192 sketches --
+    ids from every coarse bin of the partitioned add and every slot of a fine
+    bin, spread over the whole pool -- is bit-exact against the oracle over the
+    whole pair stream, and PFCOUNT of the pool matches the oracle's estimator
+    on them."""
     from redisson_amd import _lib, devmem
 
-    G, n, gs = 1_000_000, 500_000_000, 2048
+    G, n = 1_000_000, 500_000_000
+    sample = _c5_stratified_sample(G)
+    gs = sample.size
+    assert gs >= 8192 and np.unique(sample >> 12).size == (G + 4095) // 4096
+    assert np.unique(sample & 15).size == 16
     g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
     h = _pool(L, engine, G)
     ks = k.keys_fixed(n, 16).as_struct()
@@ -473,33 +495,41 @@ def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
     g.free()
     k.free()
     ref = np.zeros((gs, 16384), np.uint8)
-    orc.hll_add_gen_grouped_subset(ref, G, gs, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
-    got = np.zeros((gs, 16384), np.uint8)
-    _lib.check(L.rsk_memcpy(engine.ctx, got.ctypes.data, L.rsk_hll_device_registers(h), got.nbytes, 1))
-    assert np.array_equal(got, ref)
-    cnt = _count(L, h, list(range(gs)))
-    assert [int(c) for c in cnt[:64]] == [orc.hll_count_dense(ref[i]) for i in range(64)]
+    orc.hll_add_gen_grouped_ids(ref, G, sample, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
+    base = L.rsk_hll_device_registers(h)
+    bad = []
+    for s, gid in enumerate(sample.tolist()):  # one 16 KiB row per sampled sketch
+        row = np.zeros(16384, np.uint8)
+        _lib.check(L.rsk_memcpy(engine.ctx, row.ctypes.data, ctypes.c_void_p(base + gid * 16384), 16384, 1))
+        if not np.array_equal(row, ref[s]):
+            bad.append(gid)
+    assert not bad, (len(bad), bad[:10])
+    cnt = _count(L, h, sample.tolist())
+    chk = np.linspace(0, gs - 1, 128).astype(np.int64)
+    assert [int(cnt[i]) for i in chk] == [orc.hll_count_dense(ref[i]) for i in chk]
     # the bench's batched countWith / mergeWith at full size: 10^5 ops over the
     # 1M sketches in one call each; the first 256 ops use only sampled sketches
-    # (checked against the oracle), the rest draw from the other sketches.
+    # (checked against the oracle), the rest draw from the whole pool.
     rng = np.random.default_rng(9)
     ops, chk = 100_000, 256
-    cw = rng.integers(gs, G, size=(ops, 2), dtype=np.uint64)
-    cw[:chk] = rng.integers(0, gs, size=(chk, 2), dtype=np.uint64)
+    slot = {int(gid): s for s, gid in enumerate(sample.tolist())}
+    cw = rng.integers(0, G, size=(ops, 2), dtype=np.uint64)
+    cw[:chk] = sample[rng.integers(0, gs, size=(chk, 2))]
     out = np.zeros(ops, np.uint64)
     _lib.check(L.rsk_hll_count_union_batch(h, cw.ctypes.data, 2, ops, out.ctypes.data))
     for i in range(chk):
-        a, b = int(cw[i, 0]), int(cw[i, 1])
+        a, b = slot[int(cw[i, 0])], slot[int(cw[i, 1])]
         assert int(out[i]) == orc.hll_count_raw(np.maximum(ref[a], ref[b])), i
-    perm = rng.permutation(gs).astype(np.uint64)  # distinct sampled dst / src sketches
-    md = rng.integers(gs, G, size=ops, dtype=np.uint64)
-    ms = rng.integers(gs, G, size=ops, dtype=np.uint64)
+    perm = sample[rng.permutation(gs)]  # distinct sampled dst / src sketches
+    rest = np.setdiff1d(np.arange(G, dtype=np.uint64), sample)
+    md = rest[rng.integers(0, rest.size, size=ops)]
+    ms = rest[rng.integers(0, rest.size, size=ops)]
     md[:chk], ms[:chk] = perm[:chk], perm[chk:2 * chk]
     _lib.check(L.rsk_hll_merge_batch(h, md.ctypes.data, ms.ctypes.data, ops))
     for i in range(0, chk, 8):
         d, sr = int(md[i]), int(ms[i])
-        assert np.array_equal(_regs(L, h, d), np.maximum(ref[d], ref[sr])), i
-        assert np.array_equal(_regs(L, h, sr), ref[sr]), i
+        assert np.array_equal(_regs(L, h, d), np.maximum(ref[slot[d]], ref[slot[sr]])), i
+        assert np.array_equal(_regs(L, h, sr), ref[slot[sr]]), i
     L.rsk_hll_destroy(h)
 
 

@@ -44,6 +44,8 @@ def test_exception_classes(shim):
     assert cls[2] == b"java/lang/IllegalStateException"     # "Bloom filter is not initialized!" :217
     assert cls[3] == cls[4] == b"org/redisson/client/RedisException"  # -WRONGTYPE / -INVALIDOBJ
     assert cls[6] == b"java/lang/OutOfMemoryError"
+    assert shim.rsk_shim_exception_class(100) == b"org/redisson/client/RedisException"  # config changed
+    assert shim.rsk_shim_exception_class(101) == b"org/redisson/client/RedisException"  # -ERR bit offset ...
 
 
 def test_key_buffer_checks(shim):
@@ -84,6 +86,33 @@ def test_jni_glue_covers_every_native_method():
     impl = open(os.path.join(JNI, "rsketch_shim.c")).read()
     for fn in re.findall(r"\b(rsk_shim_\w+)\(", hdr):
         assert re.search(r"\b%s\([^;]*\{" % fn, impl, re.S), fn
+
+
+def test_java_sources_use_completions_not_raw_promises():
+    """Async natives take a Completion (promise + the event loop its listeners
+    run on); RSketchNative.complete only hands off to that executor."""
+    src = open(os.path.join(JNI, "java", "org", "redisson", "gpu", "RSketchNative.java")).read()
+    for m in re.finditer(r"static native void (\w+Async)\(([^)]*)\)", src):
+        assert "Completion<" in m.group(2), m.group(1)
+    body = src[src.index("static void complete("):]
+    body = body[: body.index("\n    }\n")]
+    assert "executor.execute" in body and "trySuccess" not in body
+    glue = open(os.path.join(JNI, "rsketch_jni.c")).read()
+    done = glue[glue.index("static void jni_done("):]
+    done = done[: done.index("\n}\n")]
+    assert "FindClass" not in done  # resolved once in JNI_OnLoad
+    assert "g_complete" in glue and "JNI_OnLoad" in glue
+
+
+@pytest.mark.gpu
+def test_jni_glue_on_gpu():
+    """jni/rsketch_jni.c compiled against tests/c/jni_mock/jni.h and driven by a
+    fake JVM (tests/c/jni_caller.c): completions, parking, re-entrancy."""
+    exe = os.path.join(JNI, "bin", "jni_caller")
+    assert os.path.exists(exe), "build it first: make -C jni"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "jni_caller ok" in r.stdout
 
 
 @pytest.mark.gpu

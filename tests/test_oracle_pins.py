@@ -225,6 +225,11 @@ def test_grouped_subset_oracle_matches_full(orc):
         sub = np.zeros((7, orc.REGISTERS), np.uint8)
         orc.hll_add_gen_grouped_subset(sub, G, 7, 0x5EED0006, 0, n, threads)
         assert np.array_equal(sub, full[:7]), threads
+    ids = np.array([49, 3, 17, 0, 32], np.uint64)
+    for threads in (1, 4):
+        sub = np.zeros((ids.size, orc.REGISTERS), np.uint8)
+        orc.hll_add_gen_grouped_ids(sub, G, ids, 0x5EED0006, 0, n, threads)
+        assert np.array_equal(sub, full[ids.astype(np.int64)]), threads
 
 
 def test_hash_to_base64_cpu_form_shape(orc):
