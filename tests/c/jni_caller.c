@@ -401,13 +401,22 @@ int main(void) {
   CHECK(C[20].fired == 1 && C[20].kind == 1 && (uint64_t)C[20].value == want);
   CHECK(find_class_calls == finds_after_load); /* the completion thread looked nothing up */
 
-  /* the completion thread cannot attach: parked, delivered by the next native call */
-  attach_failures = 1000;
-  Java_org_redisson_gpu_RSketchNative_hllCountAsync(env, CLS, SPACE, nm, completion(21));
-  /* the library has run the callback (it parked the job) once sync returns; sync reaps */
-  Java_org_redisson_gpu_RSketchNative_sync(env, CLS, SPACE);
-  CHECK(C[21].fired == 1 && C[21].status == 0 && (uint64_t)C[21].value == want && C[21].on_main);
-  attach_failures = 0;
+  /* a completion thread that cannot attach (a second context: its completion
+   * thread has never been attached): parked, delivered by the next native call */
+  {
+    const jlong space2 = Java_org_redisson_gpu_RSketchNative_init(env, CLS, 0, JNI_FALSE);
+    CHECK(space2 != 0);
+    attach_failures = 1000;
+    Java_org_redisson_gpu_RSketchNative_hllAddAsync(env, CLS, space2, nm, b.keys, b.offs, 100000, completion(21));
+    Java_org_redisson_gpu_RSketchNative_hllCountAsync(env, CLS, space2, nm, completion(22));
+    /* rsk_shim_sync returns after the callbacks ran (they parked the jobs); sync then reaps */
+    Java_org_redisson_gpu_RSketchNative_sync(env, CLS, space2);
+    CHECK(C[21].fired == 1 && C[21].status == 0 && C[21].value == 1 && C[21].on_main);
+    CHECK(C[22].fired == 1 && C[22].status == 0 && (uint64_t)C[22].value == want && C[22].on_main);
+    CHECK(C[22].order == C[21].order + 1); /* parked jobs keep submission order */
+    attach_failures = 0;
+    Java_org_redisson_gpu_RSketchNative_shutdown(env, CLS, space2);
+  }
 
   /* a reply array that cannot be allocated, and a complete() that throws */
   {
