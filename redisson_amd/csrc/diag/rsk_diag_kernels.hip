@@ -233,6 +233,25 @@ void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const 
                                per_block, c->d_slab); break;
     case 6: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 3>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
                                per_block, c->d_slab); break;
+    case 8:
+    case 9: {  // the production LDS-DMA ring form (9: without MurmurHash64A) (the route for blobs of short keys)
+      uint64_t rb = std::min<uint64_t>((n + VAR_TILE - 1) / VAR_TILE, std::min<uint64_t>(2ull * c->num_cus,
+                                                                                 c->slab_count));
+      if (rb == 0) rb = 1;
+      uint64_t rpb = (n + rb - 1) / rb;
+      rpb = (rpb + VAR_TILE - 1) / VAR_TILE * VAR_TILE;
+      rb = (n + rpb - 1) / rpb;
+      if (variant == 8)
+        hipLaunchKernelGGL(hll_add_var_ring_kernel<0>, dim3((uint32_t)rb), dim3(VAR_TILE), 0, c->stream, data, offsets,
+                           n, rpb, c->d_slab);
+      else
+        hipLaunchKernelGGL(hll_add_var_ring_kernel<1>, dim3((uint32_t)rb), dim3(VAR_TILE), 0, c->stream, data, offsets,
+                           n, rpb, c->d_slab);
+      break;
+    }
+    case 7:  // the round-3 form (ceil(len/8) classes, branch on the last step, 64-bit rank, long update)
+      hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 0, 0>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
+                         per_block, c->d_slab); break;
     default: throw RskError{RSK_ERR_INVALID_ARG, "unknown variant"};
   }
   RSK_CHECK_LAUNCH("hll_var_variant");

@@ -18,6 +18,8 @@
 // global atomics), and raises a flag if any register grew.
 #include <hipcub/hipcub.hpp>
 
+#include <cstring>
+
 #include "rsk_hll_kern.h"
 #include "rsk_hllcount.h"
 #include "rsk_internal.h"

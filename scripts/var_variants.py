@@ -1,7 +1,9 @@
 """C4 (blob+offsets) PFADD kernel variants on the C4 stream, interleaved
 rounds in one process: 0 production (step-count sort, 1 key per lane),
 1 sorted, 2 keys per lane, 2 round-1 form, 3 sorted, 4 keys per lane; diagnostics of
-the production kernel: 4 without MurmurHash64A, 5 without the register update, 6 without either.   python scripts/var_variants.py OUT.json [n]"""
+the production kernel: 4 without MurmurHash64A, 5 without the register update, 6 without either;
+7 the round-3 production form (ceil(len/8) classes, branch on the last block); 8 the LDS-DMA ring
+form (the production route for short keys, C4).  VARIANTS=0,7 picks some.   python scripts/var_variants.py OUT.json [n]"""
 import ctypes
 import json
 import os
@@ -13,8 +15,11 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
-NAMES = {0: "sorted_1_per_lane", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane",
-         4: "diag_trivial_hash", 5: "diag_no_update", 6: "diag_trivial_hash_no_update"}
+NAMES = {0: "staged_form1", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane",
+         4: "diag_trivial_hash", 5: "diag_no_update", 6: "diag_trivial_hash_no_update", 7: "round3_form",
+         8: "ring_lds_dma", 9: "diag_ring_trivial_hash"}
+if os.environ.get("VARIANTS"):
+    NAMES = {int(v): NAMES[int(v)] for v in os.environ["VARIANTS"].split(",")}
 
 
 def main():
@@ -25,7 +30,7 @@ def main():
     eng = _lib.Engine(0)
     blob, offs, tot = devmem.gen_varlen(eng, 0x5EED0005, 0, n)
     t = {v: [] for v in NAMES}
-    for _ in range(5):
+    for _ in range(int(os.environ.get("ROUNDS", "5"))):
         for v in NAMES:
             ms = ctypes.c_double()
             _lib.check_diag(D.rsk_diag_hll_var_variant(eng.ctx, v, blob.ptr, offs.ptr, n, ctypes.byref(ms)))
