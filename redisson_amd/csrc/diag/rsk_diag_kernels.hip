@@ -233,6 +233,9 @@ void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const 
                                per_block, c->d_slab); break;
     case 6: hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 3>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
                                per_block, c->d_slab); break;
+    case 10:  // form 1: 8-byte LDS reads at byte offsets (ds_read_b128 pairs)
+      hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 0, 1>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
+                         per_block, c->d_slab); break;
     case 8:
     case 9: {  // the production LDS-DMA ring form (9: without MurmurHash64A) (the route for blobs of short keys)
       uint64_t rb = std::min<uint64_t>((n + VAR_TILE - 1) / VAR_TILE, std::min<uint64_t>(2ull * c->num_cus,

@@ -176,7 +176,7 @@ RSK_DEV uint64_t murmur64a_lds(const uint8_t* p, uint32_t len) {
   }
   return mm_final(h);
 }
-// Form 1 (production): the loop runs the key's FULL blocks (len >> 3, the
+// Form 1 (form 2 is production: the same with aligned LDS reads): the loop runs the key's FULL blocks (len >> 3, the
 // class the tile is sorted by) and the tail step (h ^= masked tail; h *= m)
 // is computed for every key and kept by a select where len & 7 != 0.  Form 0
 // above sorts by ceil(len/8) and ends in a branch between the masked tail
@@ -191,6 +191,36 @@ RSK_DEV uint64_t murmur64a_lds_full(const uint8_t* p, uint32_t len, uint64_t h0)
     h *= MM_M;
   }
   const uint64_t x = lds_u64(p + 8 * nfull) & ((1ULL << (8 * t)) - 1);  // t == 0: nothing (mask 0)
+  const uint64_t ht = (h ^ x) * MM_M;
+  h = t ? ht : h;
+  return mm_final(h);
+}
+
+// Form 2: the same hash with only dword-aligned LDS reads.  The stage holds
+// the blob verbatim, so a key starts at any byte; form 1's 8-byte reads at
+// byte offsets (hipcc pairs them into ds_read_b128) are unaligned LDS
+// accesses, and the C4 counters (profiles/r04_c4_sq.json) show the LDS
+// stalled on them for about half of the kernel.  Here block j is assembled
+// from the aligned dwords around it with one v_alignbit per 32 bits (shift =
+// 8 x (offset mod 4)).
+RSK_DEV uint32_t lds_dw(const uint32_t* w, uint32_t i) { return w[i]; }
+RSK_DEV uint64_t murmur64a_lds_aligned(const uint8_t* p, uint32_t len, uint64_t h0) {
+  const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p - (a & 3));
+  const uint32_t s = (a & 3) * 8;
+  const uint32_t nfull = len >> 3, t = len & 7;
+  uint64_t h = h0;
+  uint32_t v0 = lds_dw(w, 0);
+  for (uint32_t j = 0; j < nfull; ++j) {
+    const uint32_t v1 = lds_dw(w, 2 * j + 1), v2 = lds_dw(w, 2 * j + 2);
+    const uint32_t lo = __builtin_amdgcn_alignbit(v1, v0, s), hi = __builtin_amdgcn_alignbit(v2, v1, s);
+    h ^= mm_mix(((uint64_t)hi << 32) | lo);
+    h *= MM_M;
+    v0 = v2;
+  }
+  const uint32_t v1 = lds_dw(w, 2 * nfull + 1), v2 = lds_dw(w, 2 * nfull + 2);
+  const uint64_t tail = ((uint64_t)__builtin_amdgcn_alignbit(v2, v1, s) << 32) | __builtin_amdgcn_alignbit(v1, v0, s);
+  const uint64_t x = tail & ((1ULL << (8 * t)) - 1);  // t == 0: nothing (mask 0)
   const uint64_t ht = (h ^ x) * MM_M;
   h = t ? ht : h;
   return mm_final(h);
@@ -236,15 +266,16 @@ RSK_DEV uint64_t var_hash(bool staged, const uint64_t* st, uint32_t off, const u
 // DIAG (the support library's variants only): bit 0 replaces MurmurHash64A by one
 // 8-byte read of the key, bit 1 skips the register update (XOR-folded into a
 // slab byte instead): the cost of the rest of the kernel without them.
-// F (form): 1 = production (full-block classes, select tail, h0 table,
-// short register update); 0 = the round-3 form (support library A/B only).
-template <int KPL, int DIAG = 0, int F = 1>
+// F (form): 2 = production (full-block classes, select tail, h0 table,
+// short register update, dword-aligned LDS reads); 1 = the same with 8-byte
+// reads at byte offsets; 0 = the round-3 form (support library A/B only).
+template <int KPL, int DIAG = 0, int F = 2>
 __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_add_var_staged_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint64_t n, uint64_t per_block,
     uint8_t* __restrict__ slabs) {
   constexpr int T = VAR_TILE / KPL;
   constexpr int PF = VAR_STAGE / 16 / T;  // 16-byte stage chunks per lane
-  constexpr bool FULL = F == 1 && KPL == 1;
+  constexpr bool FULL = F >= 1 && KPL == 1;  // F 1: unaligned 8-byte reads; F 2: aligned dwords
   __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
   __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
   __shared__ uint32_t perm[VAR_TILE];  // sorted keys: stage offset | len << 16
@@ -371,7 +402,7 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
       } else if constexpr (FULL) {
         uint64_t h0 = h0tab[l[0] <= 64 ? l[0] : 0];
         if (l[0] > 64) h0 = (uint64_t)HLL_SEED ^ ((uint64_t)l[0] * MM_M);
-        h[0] = murmur64a_lds_full(st8 + o[0], l[0], h0);
+        h[0] = F == 2 ? murmur64a_lds_aligned(st8 + o[0], l[0], h0) : murmur64a_lds_full(st8 + o[0], l[0], h0);
       } else {
         murmur64a_lds_multi<KPL>(st8, o, l, h);
       }
@@ -397,7 +428,8 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
   if constexpr ((DIAG & 2) != 0) slabs[(uint64_t)blockIdx.x * HLL_REGS + tid] = (uint8_t)(diag_acc % 51);
 }
 
-// ---- The ring form (production for blobs of keys <= ~37 B on average: C4).
+// ---- The ring form (a support-library experiment, not routed: C4 11.3 ms
+// against 9.4 for form 2, profiles/r04_c4_sq.json).
 // The stage of a tile is filled by LDS-DMA (global_load_lds_dwordx4: no
 // VGPRs) into a ring of three 20 KiB slots, TWO tiles ahead, and the tile's
 // key offsets are loaded a tile ahead; the waits are counted (vmcnt) and the

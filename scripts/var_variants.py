@@ -15,9 +15,9 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
-NAMES = {0: "staged_form1", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane",
+NAMES = {0: "production_form2", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane",
          4: "diag_trivial_hash", 5: "diag_no_update", 6: "diag_trivial_hash_no_update", 7: "round3_form",
-         8: "ring_lds_dma", 9: "diag_ring_trivial_hash"}
+         8: "ring_lds_dma", 9: "diag_ring_trivial_hash", 10: "staged_form1_unaligned_lds"}
 if os.environ.get("VARIANTS"):
     NAMES = {int(v): NAMES[int(v)] for v in os.environ["VARIANTS"].split(",")}
 
