@@ -256,21 +256,21 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, rank: int = 0, world: i
             L.rsk_bloom_destroy(b)
         engine.prof_enable(False)
         rstages = {}
-        for name in ("bloom_rp1", "bloom_rp_mid", "bloom_rp2", "bloom_rp3", "bloom_rp_apply", "bloom_rp_reply"):
+        for name in ("bloom_rp1", "bloom_rp_mid", "bloom_rp2", "bloom_rp_apply", "bloom_rp_reply", "bloom_rp_fallback"):
             ms, cnt = engine.prof_read(name)
             if cnt:
                 rstages[name] = ms
         chunks = -(-n_ins * k.value // (1 << 33))  # rsk_bloom_reply.hip: chunks of <= 2^33 probes
-        # per probe: 8 B record written by rp1, read + written by rp2 and rp3, read by
-        # rp_apply; per chunk: the first-probe table (4 B per filter bit) written,
+        # per probe: 4 B record written by rp1, read + written by rp2, read by
+        # rp_tapply; per chunk: the group-tag table T (2 B per filter bit) written,
         # the filter read and written; keys read by rp1 and by the reply pass
-        model = n_ins * k.value * 48 + chunks * (4 * size.value + 2 * (size.value // 8)) + 32 * n_ins
+        model = n_ins * k.value * 16 + chunks * (2 * size.value + 2 * (size.value // 8)) + 32 * n_ins
         replies = {"keys": n_ins, "ms": dt * 1e3, "keys_per_s": n_ins / dt,
                    "replies_true": int(rout.to_numpy().sum()), "stage_ms": rstages, "chunks": chunks,
                    "traffic_model_GB": model / 1e9, "model_GBps": model / dt / 1e9,
                    "model_frac_of_8TBps": model / dt / 8e12,
                    "note": "rsk_bloom_add with added_out (sequential SETBIT-reply semantics), fresh filter, "
-                           "partitioned first-probe pipeline (rsk_bloom_reply.hip); model excludes the reply "
+                           "partitioned group-tag pipeline (rsk_bloom_reply.hip); model excludes the reply "
                            "pass's random gathers"}
         rout.free()
     for buf in (ins, qs, out):

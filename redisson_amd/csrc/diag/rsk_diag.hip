@@ -159,6 +159,9 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "sa_parts") t.sa_parts = (uint32_t)value;
     else if (k == "reply") t.reply = (int)value;
     else if (k == "reply_chunk") t.reply_chunk = (uint64_t)value;
+    else if (k == "reply_u") t.reply_u = (int)value;
+    else if (k == "reply_v") t.reply_v = (int)value;
+    else if (k == "reply_dbg") t.reply_dbg = (int)value;
     else if (k == "gpart") t.gpart = (int)value;
     else if (k == "reset") t = Tuning{};
     else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};

@@ -2,34 +2,44 @@
 //
 // RedissonBloomFilter.add (src/main/java/org/redisson/RedissonBloomFilter.java:80-114)
 // sends the k SETBITs of an element in one pipeline and answers true iff one
-// of the FIRST k-1 replies was 0 (:100-107).  Over a batch the SETBITs run in
-// sequence order p = i k + t, so probe p finds its bit clear iff the bit was
-// clear before the batch and no probe q < p hit the same bit.  For the reply
-// of key i only the smallest KEY over the probes of a bit matters: if
-// minkey[b_t] == i for some t < k-1, the first of key i's own probes on that
-// bit (t* <= t < k-1) found it clear; otherwise every one of them followed an
-// earlier key's probe (or the bit was set before the batch).  Instead of
-// sorting all k n (bit, p) pairs, this path partitions 8-byte records
-// (key << 32 | offset) down to 2 KiB blocks (2^14 bits) of the filter and takes the
-// minimum key per bit in LDS:
+// of the FIRST k-1 replies was 0 (:100-107; BitSetReplayConvertor: true = the
+// old bit was 0).  Over a batch the SETBITs run in sequence order p = i k + t,
+// so key i answers true iff for some t < k-1 its probe (i, t) is the FIRST
+// probe of bit b_t in the batch and b_t was clear before it.
 //
-//   rp1, rp2 : the append partition's sa1 / sa2 (rsk_bloom_sa.h) with 8-byte
-//              records: coarse bins, then 64 KiB slices of the filter.
-//   rp3      : one workgroup per slice re-sorts its records into the slice's
-//              32 blocks of 2^14 bits through LDS (tiles of RP3_TILE records,
-//              a 33-entry u16 header per tile), written contiguously.
-//   rp_apply : one workgroup per block: minkey[16384] in LDS (64 KiB),
-//              atomicMin of every record's key; then the block's first-key
-//              table fk[bit] = minkey (NONE where the bit was already set: no
-//              probe finds it clear) and the block ORed into the filter.
-//   rp_reply : per key, its first k-1 probe indices again; true at the first
-//              t with fk[idx_t] == i (early exit, ~1.4 gathers per key at the
-//              C3 fill).
-// Chunks (< 2^32 - 1 keys, and a bound on the probes for scratch) run one
-// after the other, each seeing the filter the previous ones left, exactly
-// like the sequential SETBITs; C3 (1B keys, k = 7) is one chunk.
-// HBM per probe: 8 B (rp1 write) + 16 (rp2) + 16 (rp3) + 8 (rp_apply), plus
-// 4 B per filter bit (fk) and 2 x the filter per chunk, plus the reply pass.
+// Key groups.  The keys of a chunk are cut into <= 32766 groups of
+// consecutive keys (a group = gs super-tiles of one sa1 workgroup's
+// contiguous range), numbered in key order: tag(i).  The first prober of a
+// bit then lies in the group with the smallest tag among the bit's probes,
+// and when that group probed the bit only once, that one probe is the first.
+// So the partition only has to carry each probe's 15-bit group tag, not its
+// key index, and the per-bit answer is 2 bytes:
+//
+//   rp1 (sa1, TAGGED) : keys hashed once, 4-byte records (bin offset | group
+//                       in the top 6 bits) appended to per-workgroup
+//                       sub-regions of 2^26-bit coarse bins.
+//   rp2 (sa2h<u32>)   : each coarse bin re-sorted into buckets of 2^16 bits;
+//                       records (tag << 16 | offset).
+//   rp_tapply         : one workgroup per bucket: e[bit] = (min tag << 1) |
+//                       (min tag seen once) in 128 KiB of LDS (u16 per bit,
+//                       CAS on the word pair); T[bit] = e, or NONE where the
+//                       bit was set before the batch; the bucket ORed into
+//                       the filter.
+//   rp_treply         : one workgroup per group: key i's first k-1 probes
+//                       gathered from T (early exit): T == tag(i) << 1 | 1 ->
+//                       true.  T == tag(i) << 1 (the group probed the bit more
+//                       than once: rare, ~2.5 x group size per chunk) leaves
+//                       the key pending; the workgroup then scans its group's
+//                       keys again for the pending bits (LDS hash, minimum
+//                       (key, t) per bit) and answers them exactly.
+//
+// A chunk whose sub-regions overflow (adversarial keys; before anything is
+// applied), or whose pending probes do not fit a group's LDS tables (e.g. a
+// batch of adjacent duplicates), is answered by the sort path: in the second
+// case the filter is first restored from T (bits with T != NONE were clear).
+// HBM per probe: 4 B (rp1 write) + 8 (rp2) + 4 (rp_tapply) = 16 B, plus 2 B
+// of T per filter bit and 2 x the filter per chunk, the keys read twice and
+// the reply pass's ~1.4 random 2-byte gathers per key.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -40,284 +50,199 @@ namespace rsk {
 
 namespace {
 
-constexpr int RB_LOG = 14;                            // bits per block
-constexpr uint32_t RB_BITS = 1u << RB_LOG;            // 16384: minkey in LDS = 64 KiB (2 workgroups per CU)
-constexpr uint32_t RB_WORDS = RB_BITS / 32;           // 512 filter words per block
-constexpr uint32_t RB_PER_SL = 1u << (SL_LOG - RB_LOG);  // 32 blocks per slice
-constexpr uint32_t RP3_CHUNKS = 128;                  // rp3: 64-record chunks per round
-constexpr uint32_t NONE = 0xFFFFFFFFu;                // fk: no probe finds this bit clear (never a key index)
-constexpr uint32_t RP3_T = 1024;                      // rp3 workgroup
-constexpr uint32_t RP3_PER = 8;                       // records per lane per rp3 round
-constexpr uint32_t RP3_TILE = RP3_T * RP3_PER;        // 8192 records per rp3 tile
-constexpr uint32_t RP3_GROUP = RP3_T;                 // sa2 tiles per rp3 group (one header per lane)
-constexpr uint32_t RA_T = 1024;                       // rp_apply workgroup
-constexpr uint64_t MAX_CHUNK_KEYS = 0xFFFFFFFEull;    // key indices < NONE
-constexpr uint64_t DEFAULT_CHUNK_PROBES = 1ull << 33;  // scratch bound: ~2.3 x 8 B per probe
-#ifndef RSK_RP_U
-#define RSK_RP_U 2  // rp_reply: keys (gather chains) per lane (1, 2 and 4 measured alike)
-#endif
+constexpr uint32_t BK_LOG = 16;                        // bits per bucket (rp2's unit)
+constexpr uint32_t BK_BITS = 1u << BK_LOG;             // u16 entry per bit in LDS: 128 KiB
+constexpr uint32_t BK_WORDS = BK_BITS / 32;            // 2048 filter words per bucket
+constexpr uint32_t T_NONE = 0xFFFFu;                   // T: no probe finds this bit clear
+constexpr uint32_t MAX_TAGS = 32766;                   // group tags: (tag << 1) | 1 < T_NONE
+constexpr uint32_t TA_T = 1024;                        // rp_tapply workgroup
+constexpr uint32_t RR_T = 256;                         // rp_treply workgroup
+constexpr uint32_t PEND_CAP = 256;                     // rp_treply: pending keys per group
+constexpr uint32_t HS = 1024;                          // rp_treply: hash slots for pending bits
+constexpr uint32_t HS_MAX = 768;                       // ... at most this many distinct bits
+constexpr uint64_t HS_EMPTY = ~0ull;
+constexpr uint64_t MAX_CHUNK_KEYS = 1ull << 32;
+constexpr uint64_t DEFAULT_CHUNK_PROBES = 1ull << 33;  // scratch bound: ~10 B per probe
 
-// ------------------------------------------------------------------ sizing
-// Slice s = blockIdx.x: its records in the sa2 tiles of coarse bin s >> f2
-// (all parts), and the bound on its rp3 tiles (a group of <= RP3_GROUP sa2
-// tiles of one part ends in at most one partial rp3 tile).
-__global__ __launch_bounds__(256) void rp_size_kernel(const uint16_t* __restrict__ h2t, uint64_t row_stride,
-                                                      uint32_t f2, const uint32_t* __restrict__ tile_off,
-                                                      const uint32_t* __restrict__ ntile, uint32_t P,
-                                                      uint64_t* __restrict__ tot, uint32_t* __restrict__ bud) {
-  __shared__ uint64_t part[4];
-  const uint32_t s = blockIdx.x, c = s >> f2, f = s & ((1u << f2) - 1);
-  const uint16_t* ra = h2t + (uint64_t)f * row_stride;
-  const uint16_t* rb = ra + row_stride;
-  uint64_t n = 0;
-  uint32_t groups = 0;
-  for (uint32_t pr = 0; pr < P; ++pr) {
-    const uint64_t t0 = tile_off[(uint64_t)c * P + pr], nt = ntile[(uint64_t)c * P + pr];
-    for (uint64_t t = t0 + threadIdx.x; t < t0 + nt; t += 256) n += (uint32_t)(rb[t] - ra[t]);
-    groups += (uint32_t)((nt + RP3_GROUP - 1) / RP3_GROUP);
-  }
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t total = part[0] + part[1] + part[2] + part[3];
-    const uint32_t rounds = (uint32_t)((total + RP3_TILE - 1) / RP3_TILE) + groups;
-    tot[s] = total + (uint64_t)RB_PER_SL * rounds;  // records + a pad per odd block segment; even (16-byte aligned)
-    bud[s] = rounds;
+RSK_DEV uint32_t shfl_u32(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+
+// e = (tag << 1) | once: fold one probe of group `tag` into the u16 entry of
+// bit `off` (two entries per LDS word; CAS on the word).
+RSK_DEV void tap_fold(uint32_t* tt, uint32_t rec) {
+  const uint32_t tag = rec >> 16, off = rec & 0xFFFFu;
+  uint32_t* wp = tt + (off >> 1);
+  const uint32_t sh = (off & 1u) * 16u;
+  uint32_t old = *wp;
+  while (true) {
+    const uint32_t cur = (old >> sh) & 0xFFFFu, ctag = cur >> 1;
+    if (tag > ctag || (tag == ctag && !(cur & 1u))) break;  // an earlier group, or already seen twice
+    const uint32_t ne = tag < ctag ? (tag << 1) | 1u : tag << 1;
+    const uint32_t nw = (old & ~(0xFFFFu << sh)) | (ne << sh);
+    const uint32_t prev = atomicCAS(wp, old, nw);
+    if (prev == old) break;
+    old = prev;
   }
 }
 
-// --------------------------------------------------------------------- rp3
-// Workgroup = slice s.  Its input is one segment (the slice's fine bin) of
-// every sa2 tile of coarse bin c: taken a group of <= 1024 tiles at a time
-// (lane j: tile j's segment; a block scan gives the concatenation), in rounds
-// of RP3_TILE records: record i of the round is found from a table of the
-// segment holding each 64-record chunk start (then a short forward walk over
-// the group's starts), ranked by block with an LDS atomic, placed in an LDS
-// image and written contiguously at the slice's region with a header
-// h3[tile][0..32] (block starts) and its position tb3[tile].  Padding records
-// (low word INVALID) are dropped.  The round's barriers order LDS only
-// (lds_barrier): a wave's record loads and tile stores stay in flight across
-// them (no global data is shared inside the workgroup).
-__global__ __launch_bounds__(RP3_T) void rp3_kernel(const uint64_t* __restrict__ in, const uint16_t* __restrict__ h2t,
-                                                    uint64_t row_stride, uint32_t f2, const uint64_t* __restrict__ tb2,
-                                                    const uint32_t* __restrict__ tile_off,
-                                                    const uint32_t* __restrict__ ntile, uint32_t P,
-                                                    const uint64_t* __restrict__ slice_off,
-                                                    const uint32_t* __restrict__ tile3_off,
-                                                    uint64_t* __restrict__ out, uint16_t* __restrict__ h3,
-                                                    uint64_t* __restrict__ tb3, uint32_t* __restrict__ ntile3) {
-  __shared__ __attribute__((aligned(16))) uint64_t img[RP3_TILE + RB_PER_SL];  // + one pad per odd block segment
-  __shared__ uint64_t s_pos[RP3_GROUP];
-  __shared__ uint32_t s_pre[RP3_GROUP + 1];
-  __shared__ uint16_t tbl[RP3_CHUNKS];
-  __shared__ uint32_t wsum[RP3_T / 64];
-  __shared__ uint32_t hist[RB_PER_SL + 1], lstart[RB_PER_SL + 1];
-  const uint32_t s = blockIdx.x, c = s >> f2, f = s & ((1u << f2) - 1);
-  const uint16_t* ra = h2t + (uint64_t)f * row_stride;
-  const uint16_t* rb = ra + row_stride;
-  const uint64_t base = slice_off[s];
-  const uint32_t tbeg = tile3_off[s];
-  if (threadIdx.x <= RB_PER_SL) hist[threadIdx.x] = 0;
-  uint64_t written = 0;
-  uint32_t nt3 = 0;
-  // a round's image is written out during the next round, after its record
-  // loads and ranks (one vmcnt counts loads and stores: the stores then have
-  // the scan and the scatter to drain before the next loads are waited for)
-  uint32_t pend = 0;
-  uint64_t pend_at = 0;
-  auto write_out = [&]() {
-    u32x4* o4 = reinterpret_cast<u32x4*>(out + base + pend_at);
-    const uint4* i4 = reinterpret_cast<const uint4*>(img);
-    for (uint32_t j = threadIdx.x; j < pend / 2; j += RP3_T) {
-      const uint4 v = i4[j];
-      u32x4 x = {v.x, v.y, v.z, v.w};
-      __builtin_nontemporal_store(x, o4 + j);
-    }
+// ---------------------------------------------------------------- rp_tapply
+// Workgroup = bucket u (bits [u 2^16, (u + 1) 2^16)) = sub-bucket e = u mod 8
+// of slice s = u / 8, in coarse bin c = s >> f2 (row f = s mod 2^f2 of the
+// rp2 headers: per tile one uint4 of the 8 u16 starts of the slice's
+// buckets; row f + 1's first u16 ends sub-bucket 7).  Lane l of a wave loads
+// tile g + l's bounds; then four lanes take one tile's segment (two aligned
+// uint4 each = 32 record slots, the rest of a long segment in a loop), 16
+// segments per wave step.  Consecutive buckets run on one XCD (xcd_slot):
+// the 8 buckets of a slice share their segments' cache lines in its L2.
+__global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restrict__ recs,
+                                                         const uint4* __restrict__ hp, uint64_t hp_stride,
+                                                         uint32_t f2, const uint32_t* __restrict__ tb,
+                                                         const uint32_t* __restrict__ tile_off,
+                                                         const uint32_t* __restrict__ ntiles, uint32_t P,
+                                                         uint64_t nbuckets, uint32_t* __restrict__ bits,
+                                                         uint64_t nwords, uint16_t* __restrict__ T, int dbg) {
+  __shared__ __attribute__((aligned(16))) uint32_t tt[BK_BITS / 2];
+  __shared__ __attribute__((aligned(16))) uint32_t f0[BK_WORDS];
+  const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  constexpr uint32_t NW = TA_T / 64;
+  const uint4* r4 = reinterpret_cast<const uint4*>(recs);
+  auto fold4 = [&](const uint4& v, uint32_t p, uint32_t sb, uint32_t se) {
+    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (p + j >= sb && p + j < se) {
+        if (dbg & 1) tt[x[j] & 0x7FFFu] |= x[j] >> 31;  // timing only: one plain LDS op per record
+        else tap_fold(tt, x[j]);
+      }
   };
-  for (uint32_t pr = 0; pr < P; ++pr) {
-    const uint64_t t0 = tile_off[(uint64_t)c * P + pr], nt = ntile[(uint64_t)c * P + pr];
-    for (uint64_t g0 = 0; g0 < nt; g0 += RP3_GROUP) {
-      const uint32_t ng = (uint32_t)(nt - g0 < RP3_GROUP ? nt - g0 : RP3_GROUP);
-      uint32_t len = 0;
-      if (threadIdx.x < ng) {
-        const uint64_t t = t0 + g0 + threadIdx.x;
-        const uint32_t beg = ra[t];
-        len = (uint32_t)rb[t] - beg;
-        s_pos[threadIdx.x] = tb2[t] + beg;
-      }
-      uint32_t total;
-      const uint32_t pre = block_scan<RP3_T>(len, &total, wsum);  // (barriers inside)
-      if (threadIdx.x < ng) s_pre[threadIdx.x] = pre;
-      s_pre[ng] = total;  // (sentinel; written by every lane, same value)
-      __syncthreads();
-      for (uint32_t r0 = 0; r0 < total; r0 += RP3_TILE) {
-        // chunk table: tbl[c] = the segment holding record r0 + 64 c (each
-        // non-empty segment claims the chunk starts that fall inside it)
-        if (threadIdx.x < ng && len) {
-          const uint32_t a = pre, e = pre + len;
-          const uint32_t c0 = a > r0 ? (a - r0 + 63) >> 6 : 0;
-          const uint32_t c1 = e > r0 ? min(RP3_CHUNKS, (e - r0 + 63) >> 6) : 0;
-          for (uint32_t cc = c0; cc < c1; ++cc) tbl[cc] = (uint16_t)threadIdx.x;
-        }
-        lds_barrier();
-        uint64_t rec[RP3_PER];
-        uint32_t tag[RP3_PER];
-        // two records per lane and load: segments start at even records of
-        // 16-byte aligned tiles and have even lengths (sa2 pads runs), so a
-        // pair never straddles two segments
-#pragma unroll
-        for (uint32_t m = 0; m < RP3_PER / 2; ++m) {
-          const uint32_t i = r0 + 2 * (m * RP3_T + threadIdx.x);
-          rec[2 * m] = rec[2 * m + 1] = rec_pad<uint64_t>();
-          if (i < total) {
-            uint32_t j = tbl[(i - r0) >> 6];  // then forward over the (few) segments of the chunk
-            while (s_pre[j + 1] <= i) ++j;
-            unpack16<uint64_t>(ld_nt16(in + s_pos[j] + (i - s_pre[j])), rec + 2 * m);
-          }
-        }
-#pragma unroll
-        for (uint32_t m = 0; m < RP3_PER; ++m) {
-          tag[m] = INVALID;
-          const uint32_t off = rec_off(rec[m]);
-          if (off != INVALID) {
-            const uint32_t blk = off >> RB_LOG;
-            tag[m] = (blk << 16) | atomicAdd(&hist[blk], 1u);
-          }
-        }
-        write_out();  // the previous round
-        lds_barrier();
-        if (threadIdx.x < 64) {  // block segments padded to even lengths: 16-byte aligned record pairs
-          const uint32_t lane = threadIdx.x;
-          const uint32_t v = lane < RB_PER_SL ? hist[lane] : 0, v2 = (v + 1) & ~1u;
-          const uint32_t incl = wave_scan_incl(v2, lane);
-          if (lane < RB_PER_SL) {
-            lstart[lane] = incl - v2;
-            hist[lane] = 0;
-            if (v & 1) img[incl - 1] = rec_pad<uint64_t>();
-            h3[(uint64_t)(tbeg + nt3) * (RB_PER_SL + 1) + lane] = (uint16_t)(incl - v2);
-          }
-          const uint32_t tot = rdl(incl, RB_PER_SL - 1);
-          if (lane == 0) {
-            h3[(uint64_t)(tbeg + nt3) * (RB_PER_SL + 1) + RB_PER_SL] = (uint16_t)tot;
-            tb3[tbeg + nt3] = base + written;
-            lstart[RB_PER_SL] = tot;
-          }
-        }
-        lds_barrier();
-#pragma unroll
-        for (uint32_t m = 0; m < RP3_PER; ++m)
-          if (tag[m] != INVALID) img[lstart[tag[m] >> 16] + (tag[m] & 0xFFFFu)] = rec[m];
-        pend = lstart[RB_PER_SL];  // even: every segment is
-        pend_at = written;
-        written += pend;
-        ++nt3;
-        // the next round's first barrier orders this image before its write-out
-      }
-    }
-  }
-  lds_barrier();
-  write_out();
-  if (threadIdx.x == 0) ntile3[s] = nt3;
-}
-
-// ---------------------------------------------------------------- rp_apply
-// Workgroup = block b (bits [b 2^14, (b + 1) 2^14), RB_LOG = 14): every segment of it in
-// its slice's rp3 tiles (wave w takes tiles w, w + 16, ...; 4 records per lane
-// in flight), atomicMin of the key into minkey; then fk[bit] and the filter words,
-// 64 bits per wave step (a ballot of "touched" is the MSB-first word pair).
-__global__ __launch_bounds__(RA_T) void rp_apply_kernel(const uint64_t* __restrict__ in,
-                                                        const uint16_t* __restrict__ h3,
-                                                        const uint64_t* __restrict__ tb3,
-                                                        const uint32_t* __restrict__ tile3_off,
-                                                        const uint32_t* __restrict__ ntile3, uint64_t nblocks,
-                                                        uint32_t* __restrict__ bits, uint64_t nwords,
-                                                        uint32_t* __restrict__ fk) {
-  __shared__ __attribute__((aligned(16))) uint32_t ms[RB_BITS];
-  __shared__ uint32_t f0[RB_WORDS];
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr uint32_t NW = RA_T / 64;
-  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    const uint64_t wbase = b * RB_WORDS;
-    uint4* m4 = reinterpret_cast<uint4*>(ms);
-    for (uint32_t q = threadIdx.x; q < RB_BITS / 4; q += RA_T) m4[q] = make_uint4(NONE, NONE, NONE, NONE);
-    for (uint32_t q = threadIdx.x; q < RB_WORDS; q += RA_T) f0[q] = wbase + q < nwords ? bits[wbase + q] : 0u;
+  for (uint64_t u = xcd_slot(blockIdx.x, gridDim.x); u < nbuckets; u += gridDim.x) {
+    uint4* t4 = reinterpret_cast<uint4*>(tt);
+    for (uint32_t q = threadIdx.x; q < BK_BITS / 8; q += TA_T) t4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    const uint64_t w0 = u * BK_WORDS;
+    for (uint32_t q = threadIdx.x; q < BK_WORDS; q += TA_T) f0[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
     lds_barrier();
-    const uint32_t s = (uint32_t)(b / RB_PER_SL), sub = (uint32_t)(b % RB_PER_SL);
-    const uint32_t t0 = tile3_off[s], nt = ntile3[s];
-    for (uint32_t j = w; j < nt; j += NW) {
-      const uint16_t* hr = h3 + (uint64_t)(t0 + j) * (RB_PER_SL + 1);
-      const uint32_t beg = hr[sub], end = hr[sub + 1];
-      // segments are even and 16-byte aligned: record pairs, 2 loads in flight per lane
-      const uint4* seg = reinterpret_cast<const uint4*>(in + tb3[t0 + j]);
-      for (uint32_t o = beg / 2 + lane; o < end / 2; o += 2 * 64) {
-        uint64_t r[4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const uint32_t x = o + 64 * u;
-          if (x < end / 2) unpack16<uint64_t>(ld_nt16(seg + x), r + 2 * u);
-          else r[2 * u] = r[2 * u + 1] = rec_pad<uint64_t>();
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (rec_off(r[u]) != INVALID) atomicMin(&ms[rec_off(r[u]) & (RB_BITS - 1)], (uint32_t)(r[u] >> 32));
+    const uint32_t s = (uint32_t)(u >> 3), e = (uint32_t)(u & 7), c = s >> f2, f = s & ((1u << f2) - 1);
+    const uint4* hrow = hp + (uint64_t)f * hp_stride;
+    const uint32_t* erow = reinterpret_cast<const uint32_t*>(hp + (uint64_t)(f + 1) * hp_stride);
+    const uint32_t ta = tile_off[(uint64_t)c * P];
+    const uint32_t te = tile_off[(uint64_t)c * P + P - 1] + ntiles[(uint64_t)c * P + P - 1];
+    for (uint32_t g = ta + 64 * w; g < te; g += 64 * NW) {
+      const uint32_t t = g + lane;
+      uint32_t beg = 0, end = 0, tbl = 0;
+      if (t < te) {
+        const uint4 v = hrow[t];
+        const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
+        beg = (hw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        end = e < 7 ? (hw[(e + 1) >> 1] >> (16 * ((e + 1) & 1))) & 0xFFFFu : erow[4ull * t] & 0xFFFFu;
+        tbl = tb[t];
+      }
+      const uint32_t ng = te - g < 64 ? te - g : 64;
+      for (uint32_t j = 0; j < ng; j += 16) {
+        const uint32_t si = j + (lane >> 2), src = si < 63 ? si : 63;
+        const uint32_t sb = shfl_u32(beg, src), se0 = shfl_u32(end, src), st = shfl_u32(tbl, src);
+        const uint32_t se = si < ng ? se0 : sb;
+        const uint32_t p0 = (sb & ~3u) + 4 * (lane & 3);
+        // plain loads: the slice's 8 buckets (on one XCD at about the same time) share these lines in L2
+        const uint4 v0 = p0 < se ? r4[st + p0 / 4] : make_uint4(0, 0, 0, 0);
+        const uint4 v1 = p0 + 16 < se ? r4[st + p0 / 4 + 4] : make_uint4(0, 0, 0, 0);
+        fold4(v0, p0, sb, se);
+        fold4(v1, p0 + 16, sb, se);
+        for (uint32_t p = p0 + 32; p < se; p += 16) fold4(r4[st + p / 4], p, sb, se);  // long segments (rare)
       }
     }
     lds_barrier();
-    uint32_t* fkb = fk + b * RB_BITS;
-    for (uint32_t o = threadIdx.x; o < RB_BITS; o += RA_T) {  // a wave covers 64 bits = words o/32, o/32 + 1
-      const uint32_t v = ms[o];
-      const uint32_t was = f0[o >> 5] & bloom_bit_mask(o);
-      __builtin_nontemporal_store(was ? NONE : v, &fkb[o]);  // read back by rp_reply's gathers only
-      const uint64_t hit = __ballot(v != NONE);
-      if (lane == 0 || lane == 32) {
-        const uint32_t lo = (uint32_t)(lane == 0 ? hit : hit >> 32);
-        const uint32_t word = o >> 5;  // MSB-first bytes of a LE u32 word: bit j -> byte j/8, 0x80 >> j%8
-        const uint32_t msk = __builtin_bswap32(__builtin_bitreverse32(lo));
-        if (wbase + word < nwords) bits[wbase + word] = f0[word] | msk;
+    // T and the filter, one byte of the Redis string (8 bits, MSB first) per lane step
+    uint4* T4 = reinterpret_cast<uint4*>(T + u * BK_BITS);
+    uint8_t* fb = reinterpret_cast<uint8_t*>(f0);
+    for (uint32_t q = threadIdx.x; q < BK_BITS / 8; q += TA_T) {
+      const uint4 v = t4[q];
+      const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t was = fb[q];  // byte q of the bucket: bits 8q .. 8q+7, bit 8q at 0x80
+      uint32_t probed = 0, o[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint32_t bit = 2 * h + j, ent = (hw[h] >> (16 * j)) & 0xFFFFu;
+          probed |= (ent != T_NONE ? 1u : 0u) << (7 - bit);
+          r |= (((was >> (7 - bit)) & 1u) ? T_NONE : ent) << (16 * j);
+        }
+        o[h] = r;
       }
+      u32x4 ov = {o[0], o[1], o[2], o[3]};
+      if (!(dbg & 2)) __builtin_nontemporal_store(ov, reinterpret_cast<u32x4*>(T4 + q));  // read back by rp_treply's gathers only
+      fb[q] = (uint8_t)(was | probed);
     }
-    lds_barrier();  // ms / f0 are reset for the next block
+    lds_barrier();
+    for (uint32_t q = threadIdx.x; q < BK_WORDS; q += TA_T)
+      if (w0 + q < nwords) bits[w0 + q] = f0[q];
+    lds_barrier();  // f0 read out before the next bucket loads it
   }
 }
 
-// ---------------------------------------------------------------- rp_reply
-// Key i of the chunk: true iff fk[idx_t] == i for some t < k - 1.  U
-// keys per lane keep U gather chains in flight; a wave stops when every key
-// is decided.
+// ---------------------------------------------------------------- rp_treply
+// Workgroup = group tag = blockIdx.x = w Gw + g: super-tiles
+// [w S + g gs, min(w S + (g + 1) gs, (w + 1) S, nst)) of the chunk.
+RSK_DEV uint32_t hs_slot(uint64_t b) { return (uint32_t)((b * 0x9E3779B97F4A7C15ull) >> (64 - 10)); }
+
 template <bool FIXED16, int U>
-__global__ __launch_bounds__(256) void rp_reply_kernel(const uint8_t* __restrict__ data,
-                                                       const uint64_t* __restrict__ offsets, uint32_t fixed_len,
-                                                       uint64_t n, FastMod63 fm, int k,
-                                                       const uint32_t* __restrict__ fk, uint8_t* __restrict__ out) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < n; base += stride) {
+__global__ __launch_bounds__(RR_T) void rp_treply_kernel(const uint8_t* __restrict__ data,
+                                                         const uint64_t* __restrict__ offsets, uint32_t fixed_len,
+                                                         uint64_t m, FastMod63 fm, int k,
+                                                         const uint16_t* __restrict__ T, uint8_t* __restrict__ out,
+                                                         uint64_t kst, uint32_t S, uint32_t gs, uint32_t Gw,
+                                                         uint64_t nst, uint32_t* __restrict__ fallback) {
+  __shared__ uint32_t p_key[PEND_CAP], p_mask[PEND_CAP];
+  __shared__ uint64_t hkey[HS];
+  __shared__ uint32_t hmin[HS];
+  __shared__ uint32_t s_np, s_nh;
+  const uint32_t tag = blockIdx.x, w = tag / Gw, g = tag - w * Gw;
+  const uint64_t sw = (uint64_t)w * S, st_a = sw + (uint64_t)g * gs;
+  const uint64_t st_b = std::min<uint64_t>(st_a + gs, std::min<uint64_t>(sw + S, nst));
+  if (st_a >= st_b || st_a * kst >= m) return;  // an empty group (uniform)
+  const uint64_t ka = st_a * kst, kb = std::min<uint64_t>(st_b * kst, m);
+  if (threadIdx.x == 0) {
+    s_np = 0;
+    s_nh = 0;
+  }
+  __syncthreads();
+  // U keys per lane (gather chains in flight); a wave stops when each of its
+  // keys is decided.  (Chains that take their next key as soon as theirs is
+  // decided -- a gather per chain every round -- measured 48-54 ms against
+  // 33: every round then repeats the hashing for the lanes that refill.)
+  for (uint64_t base = ka + threadIdx.x; base < kb; base += (uint64_t)RR_T * U) {
     ProbeSeq ps[U];
-    bool live[U], yes[U];
+    bool live[U], open[U], yes[U];
+    uint32_t pend[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + (uint64_t)u * blockDim.x;
-      live[u] = i < n;
+      const uint64_t i = base + (uint64_t)u * RR_T;
+      live[u] = i < kb;
       yes[u] = false;
+      pend[u] = 0;
       if (live[u]) {
         uint64_t h1, h2;
         bloom_key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
         ps[u] = ProbeSeq(h1, h2, fm);
       }
+      open[u] = live[u];
     }
-    bool open[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) open[u] = live[u];
     for (int t = 0; t < k - 1; ++t) {
       uint32_t v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = open[u] ? fk[ps[u].idx] : NONE;
+      for (int u = 0; u < U; ++u) v[u] = open[u] ? (uint32_t)T[ps[u].idx] : T_NONE;
       bool any = false;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (open[u] && v[u] == (uint32_t)(base + (uint64_t)u * blockDim.x)) {
-          yes[u] = true;
-          open[u] = false;
+        if (open[u] && (v[u] >> 1) == tag) {
+          if (v[u] & 1u) {
+            yes[u] = true;
+            open[u] = false;
+          } else {
+            pend[u] |= 1u << t;  // the group probed this bit more than once
+          }
         }
         if (t + 2 < k) ps[u].next(t, fm);
         any |= open[u];
@@ -326,7 +251,108 @@ __global__ __launch_bounds__(256) void rp_reply_kernel(const uint8_t* __restrict
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (live[u]) out[base + (uint64_t)u * blockDim.x] = (uint8_t)yes[u];
+      if (live[u]) {
+        const uint64_t i = base + (uint64_t)u * RR_T;
+        out[i] = (uint8_t)yes[u];
+        if (!yes[u] && pend[u]) {
+          const uint32_t q = atomicAdd(&s_np, 1u);
+          if (q < PEND_CAP) {
+            p_key[q] = (uint32_t)(i - ka);
+            p_mask[q] = pend[u];
+          }
+        }
+      }
+  }
+  __syncthreads();
+  const uint32_t np = s_np;
+  if (np == 0) return;
+  if (np > PEND_CAP) {
+    if (threadIdx.x == 0) atomicOr(fallback, 1u);
+    return;
+  }
+  // Pending keys: is (i, t) the group's first probe of b_t?  The minimum
+  // (key - ka) << 4 | t over every probe of the group on each pending bit.
+  for (uint32_t q = threadIdx.x; q < HS; q += RR_T) {
+    hkey[q] = HS_EMPTY;
+    hmin[q] = ~0u;
+  }
+  __syncthreads();
+  auto probes_of = [&](uint64_t i) {
+    uint64_t h1, h2;
+    bloom_key_hashes<FIXED16>(data, offsets, fixed_len, i, h1, h2);
+    return ProbeSeq(h1, h2, fm);
+  };
+  for (uint32_t e = threadIdx.x; e < np; e += RR_T) {
+    ProbeSeq ps = probes_of(ka + p_key[e]);
+    const uint32_t mask = p_mask[e];
+    for (int t = 0; t < k - 1; ++t) {
+      if ((mask >> t) & 1u) {
+        uint32_t sl = hs_slot(ps.idx);
+        for (uint32_t n = 0; n < HS; ++n) {
+          const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(&hkey[sl]), HS_EMPTY, ps.idx);
+          if (old == HS_EMPTY) {
+            atomicAdd(&s_nh, 1u);
+            break;
+          }
+          if (old == ps.idx) break;
+          sl = (sl + 1) & (HS - 1);
+        }
+      }
+      if (t + 2 < k) ps.next(t, fm);
+    }
+  }
+  __syncthreads();
+  if (s_nh > HS_MAX) {
+    if (threadIdx.x == 0) atomicOr(fallback, 1u);
+    return;
+  }
+  auto lookup = [&](uint64_t b) {
+    uint32_t sl = hs_slot(b);
+    while (true) {
+      const uint64_t x = hkey[sl];
+      if (x == b) return sl;
+      if (x == HS_EMPTY) return HS;
+      sl = (sl + 1) & (HS - 1);
+    }
+  };
+  for (uint64_t j = ka + threadIdx.x; j < kb; j += RR_T) {
+    ProbeSeq ps = probes_of(j);
+    for (int t = 0; t < k; ++t) {
+      const uint32_t sl = lookup(ps.idx);
+      if (sl < HS) atomicMin(&hmin[sl], ((uint32_t)(j - ka) << 4) | (uint32_t)t);
+      if (t + 1 < k) ps.next(t, fm);
+    }
+  }
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < np; e += RR_T) {
+    ProbeSeq ps = probes_of(ka + p_key[e]);
+    const uint32_t mask = p_mask[e];
+    bool y = false;
+    for (int t = 0; t < k - 1; ++t) {
+      if ((mask >> t) & 1u) y |= hmin[lookup(ps.idx)] == ((p_key[e] << 4) | (uint32_t)t);
+      if (t + 2 < k) ps.next(t, fm);
+    }
+    if (y) out[ka + p_key[e]] = 1;
+  }
+}
+
+// The filter as it was before the chunk: bits with T != NONE were clear.
+__global__ __launch_bounds__(256) void rp_restore_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
+                                                         const uint16_t* __restrict__ T) {
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nwords; q += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t wv = bits[q];
+    if (!wv) continue;
+    const uint4* t4 = reinterpret_cast<const uint4*>(T + 32 * q);
+    uint32_t clear = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint4 v = t4[h];
+      const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (((hw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) != T_NONE) clear |= bloom_bit_mask(8 * h + j);
+    }
+    bits[q] = wv & ~clear;
   }
 }
 
@@ -349,16 +375,17 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const bool f16 =
       keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
   const uint32_t kmax = k <= 8 ? 8 : 16;
+  const bool kpl4 = f16 && kmax == 8;  // 4 keys per lane, as the insert's sa1
   constexpr uint32_t T1 = 512;
-  const uint64_t kst = (uint64_t)T1 * (16 / kmax);
+  const uint64_t kst = kpl4 ? 2048 : (uint64_t)T1 * (16 / kmax);
   uint32_t sb = 0;
   for (uint64_t v = nslices - 1; v; v >>= 1) ++sb;
   const uint32_t f2 = sb > 8 ? sb - 8 : 0;
   const uint32_t shift1 = SL_LOG + f2;
   const uint32_t nb1 = (uint32_t)(((nslices - 1) >> f2) + 1);
   const uint32_t nb2 = 1u << f2;
-  const uint32_t ns = (uint32_t)nslices;
-  const uint64_t nblocks = ((uint64_t)b->size + RB_BITS - 1) / RB_BITS;
+  const uint32_t nbk = nb2 << SAH_SUB;  // rp2 buckets per coarse bin
+  const uint64_t nbuckets = ((uint64_t)b->size + BK_BITS - 1) / BK_BITS;
   const uint32_t cus = (uint32_t)c->num_cus;
   const uint32_t P = std::max<uint32_t>(1, c->tune.sa_parts ? c->tune.sa_parts : 4 * cus / nb1);  // as the insert's sa2
   const uint32_t ncp = nb1 * P;
@@ -369,28 +396,27 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint64_t max_nst = (chunk + kst - 1) / kst;
   const uint64_t max_np = max_nst * kst * k;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  // sa1<u64>: 73 KiB of LDS and <= 128 VGPRs -> 2 workgroups per CU
-  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({max_nst, 2ull * cus, SA2_WMAX}));
+  // sa1 workgroups per CU from their budgets (not the occupancy query: DESIGN.md 2):
+  // 4 keys per lane 73 KiB of LDS -> 2; otherwise 80 VGPRs, 43 KiB -> 3
+  const uint32_t W = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({max_nst, (kpl4 ? 2ull : 3ull) * cus, SA2_WMAX}));
   const double share = std::min(1.0, (double)(1ull << shift1) / (double)(uint64_t)b->size);  // of a coarse bin
-  const uint64_t q64 = (uint64_t)(1.25 * share * (double)max_np / W) + kst * k + (max_nst / W + 1) + 64;
+  const uint64_t q64 = (uint64_t)(1.25 * share * (double)max_np / W) + kst * k + 3 * (max_nst / W + 1) + 64;
   const uint32_t quota = (uint32_t)((q64 + 3) & ~uint64_t(3));
   const uint32_t limit = c->tune.sa_tiny ? 32 : quota;  // tests force the overflow fallback
   if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;
   const uint64_t region_probes = (uint64_t)W * nb1 * quota;
-  const uint64_t slots = sa2_slots<uint64_t>();
-  const uint64_t tt_max = (max_np + (uint64_t)nb1 * max_nst) / slots + (uint64_t)W * nb1 + 64;  // sa2 tiles
-  const uint64_t l2_probes = max_np + (uint64_t)nb1 * max_nst + tt_max * sa2_pad<uint64_t>() + 2ull * ncp;
-  const uint64_t tt3_max = l2_probes / RP3_TILE + (uint64_t)ns * (1 + P) + (uint64_t)nb2 * (tt_max / RP3_GROUP + 1) + 64;
-  const uint64_t reg_probes = std::max(region_probes, l2_probes + RB_PER_SL * tt3_max);  // rp3 writes into the sa1 region
-  const uint64_t h2_bytes = al(tt_max * (nb2 + 1) * 2);
-  const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256 +
-                        al(8 * (ns + 1)) * 2 + al(4 * (ns + 1)) * 3;
-  const uint64_t bytes = al(8 * reg_probes) + al(8 * l2_probes) + 2 * h2_bytes + al(8 * tt_max) +
-                         al(tt3_max * (RB_PER_SL + 1) * 2) + al(8 * tt3_max) + al(4 * nblocks * RB_BITS) + meta;
-  // The scratch (4 B of first-key table per filter bit, 8-byte records of
-  // three passes: ~165 GB at C3) must fit the device next to everything
-  // else: when it does not, the sort path answers the batch instead (it
-  // needs far less).  Reserved before any chunk is applied.
+  const int V2 = c->tune.reply_v == 6 ? 6 : 3;  // rp2: uint4 per lane per tile
+  const uint32_t slots2 = SA2_T * 4 * V2;          // records per rp2 tile
+  const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / slots2 + (uint64_t)W * nb1 + 64;  // bound on rp2 tiles
+  const uint64_t l2_slots = max_np + 3ull * nb1 * max_nst + 8 * tt_max + 8ull * ncp;  // rp2 output (u32), aligned tiles
+  if (l2_slots / 4 >= (1ull << 32)) return false;  // rp_tapply's 32-bit uint4 indices
+  const uint64_t hp_bytes = al(16 * tt_max * (nb2 + 1));
+  // T (2 B per bit of whole buckets) reuses rp1's region, dead once rp2 has read it
+  const uint64_t reg_bytes = std::max(al(4 * region_probes), al(2 * nbuckets * BK_BITS));
+  const uint64_t meta = al(8 * (ncp + 1)) * 2 + al(4 * (ncp + 1)) * 3 + al(4ull * W * nb1) + 256;
+  const uint64_t bytes = reg_bytes + al(4 * l2_slots) + hp_bytes + al(4 * tt_max) + meta;
+  // Reserved before any chunk is applied; when it does not fit next to
+  // everything else the sort path answers the batch instead.
   {
     size_t free_b = 0, total_b = 0;
     if (bytes > c->work_bytes) {  // growing frees the old buffer first
@@ -415,48 +441,51 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       q += n;
       return r;
     };
-    uint64_t* region = reinterpret_cast<uint64_t*>(take(al(8 * reg_probes)));
-    uint64_t* l2 = reinterpret_cast<uint64_t*>(take(al(8 * l2_probes)));
-    uint16_t* h2 = reinterpret_cast<uint16_t*>(take(h2_bytes));
-    uint16_t* h2t = reinterpret_cast<uint16_t*>(take(h2_bytes));
-    uint64_t* tb2 = reinterpret_cast<uint64_t*>(take(al(8 * tt_max)));
-    uint16_t* h3 = reinterpret_cast<uint16_t*>(take(al(tt3_max * (RB_PER_SL + 1) * 2)));
-    uint64_t* tb3 = reinterpret_cast<uint64_t*>(take(al(8 * tt3_max)));
-    uint32_t* fk = reinterpret_cast<uint32_t*>(take(al(4 * nblocks * RB_BITS)));
+    uint8_t* reg = take(reg_bytes);
+    uint32_t* region = reinterpret_cast<uint32_t*>(reg);
+    uint16_t* T = reinterpret_cast<uint16_t*>(reg);
+    uint32_t* l2 = reinterpret_cast<uint32_t*>(take(al(4 * l2_slots)));
+    uint4* hp = reinterpret_cast<uint4*>(take(hp_bytes));
+    uint32_t* tb2 = reinterpret_cast<uint32_t*>(take(al(4 * tt_max)));
     uint64_t* tot = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
     uint64_t* reg_off = reinterpret_cast<uint64_t*>(take(al(8 * (ncp + 1))));
     uint32_t* bud = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
     uint32_t* tile_off = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
     uint32_t* tiles = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
     uint32_t* used = reinterpret_cast<uint32_t*>(take(al(4ull * W * nb1)));
-    uint32_t* overflow = reinterpret_cast<uint32_t*>(take(256));
-    uint64_t* tot3 = reinterpret_cast<uint64_t*>(take(al(8 * (ns + 1))));
-    uint64_t* slice_off = reinterpret_cast<uint64_t*>(take(al(8 * (ns + 1))));
-    uint32_t* bud3 = reinterpret_cast<uint32_t*>(take(al(4 * (ns + 1))));
-    uint32_t* tile3_off = reinterpret_cast<uint32_t*>(take(al(4 * (ns + 1))));
-    uint32_t* ntile3 = reinterpret_cast<uint32_t*>(take(al(4 * (ns + 1))));
+    uint32_t* flags = reinterpret_cast<uint32_t*>(take(256));  // [0] sub-region overflow, [1] reply fallback
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
     const uint64_t nst = (m + kst - 1) / kst;
+    // contiguous super-tile ranges of S per sa1 workgroup, groups of gs super-tiles
     const uint32_t Wc = (uint32_t)std::min<uint64_t>(W, nst);
+    const uint32_t S = (uint32_t)((nst + Wc - 1) / Wc);
+    const uint32_t Wl = (uint32_t)((nst + S - 1) / S);
+    const uint32_t Gw = std::min<uint32_t>(63, MAX_TAGS / Wl);
+    const uint32_t gs = (S + Gw - 1) / Gw;
     DevKeys dk = keys;
     dk.n = m;
     if (keys.offsets) dk.offsets = keys.offsets + first;
     else dk.data = keys.data + first * keys.fixed_len;
-    RSK_HIP(hipMemsetAsync(overflow, 0, 4, c->stream));
+    if ((uint64_t)gs * kst >= (1ull << 28)) {  // rp_treply packs (key - group start) << 4 | t in 32 bits
+      bloom_add_replies_sorted(c, b, dk, d_out + first);
+      continue;
+    }
+    RSK_HIP(hipMemsetAsync(flags, 0, 8, c->stream));
     {
       ProfScope ps(c, "bloom_rp1");
-#define RSK_RP1(F16, KM)                                                                                          \
-  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint64_t>), dim3(Wc), dim3(T1), 0, c->stream, dk.data,        \
-                     dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, overflow)
-      if (f16 && kmax == 8) RSK_RP1(true, 8);
-      else if (f16) RSK_RP1(true, 16);
-      else if (kmax == 8) RSK_RP1(false, 8);
-      else RSK_RP1(false, 16);
+#define RSK_RP1(F16, KM, KPL)                                                                                       \
+  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint32_t, KPL, true>), dim3(Wl), dim3(T1), 0, c->stream,       \
+                     dk.data, dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, \
+                     flags, S, gs)
+      if (kpl4) RSK_RP1(true, 8, 4);
+      else if (f16) RSK_RP1(true, 16, 1);
+      else if (kmax == 8) RSK_RP1(false, 8, 2);
+      else RSK_RP1(false, 16, 1);
 #undef RSK_RP1
       RSK_CHECK_LAUNCH("bloom_rp1");
     }
     uint32_t ov = 0;
-    RSK_HIP(hipMemcpyAsync(c->h_small + 8448, overflow, 4, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipMemcpyAsync(c->h_small + 8448, flags, 4, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
     std::memcpy(&ov, c->h_small + 8448, 4);
     if (ov) {
@@ -467,55 +496,57 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp_mid");
-      hipLaunchKernelGGL(sa_size_kernel<uint64_t>, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, used, Wc, nb1, P,
-                         ncp, tot, bud);
+      hipLaunchKernelGGL(sah_size_kernel, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, used, Wl, nb1, P, ncp,
+                         tot, bud, slots2);
       RSK_CHECK_LAUNCH("bloom_rp_size2");
       hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot, bud, ncp, reg_off, tile_off);
       RSK_CHECK_LAUNCH("bloom_rp_offsets2");
     }
     {
       ProfScope ps(c, "bloom_rp2");
-      hipLaunchKernelGGL(bloom_sa2_kernel<uint64_t>, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc,
-                         nb1, P, nb2, reg_off, tile_off, tiles, l2, h2, tb2);
+      if (V2 == 6)
+        hipLaunchKernelGGL((bloom_sa2h_kernel<uint32_t, 6>), dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used,
+                           Wl, nb1, P, nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2, Gw);
+      else
+        hipLaunchKernelGGL((bloom_sa2h_kernel<uint32_t, 3>), dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used,
+                           Wl, nb1, P, nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2, Gw);
       RSK_CHECK_LAUNCH("bloom_rp2");
     }
     {
-      ProfScope ps(c, "bloom_rp_mid");
-      hipLaunchKernelGGL(st_transpose_kernel, dim3((uint32_t)((tt_max + 63) / 64), (nb2 + 1 + 63) / 64), dim3(256), 0,
-                         c->stream, h2, tt_max, nb2 + 1, h2t);
-      RSK_CHECK_LAUNCH("bloom_rp_transpose");
-      hipLaunchKernelGGL(rp_size_kernel, dim3(ns), dim3(256), 0, c->stream, h2t, tt_max, f2, tile_off, tiles, P, tot3,
-                         bud3);
-      RSK_CHECK_LAUNCH("bloom_rp_size3");
-      hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot3, bud3, ns, slice_off, tile3_off);
-      RSK_CHECK_LAUNCH("bloom_rp_offsets3");
-    }
-    {
-      ProfScope ps(c, "bloom_rp3");
-      hipLaunchKernelGGL(rp3_kernel, dim3(ns), dim3(RP3_T), 0, c->stream, l2, h2t, tt_max, f2, tb2, tile_off, tiles,
-                         P, slice_off, tile3_off, region, h3, tb3, ntile3);
-      RSK_CHECK_LAUNCH("bloom_rp3");
-    }
-    {
       ProfScope ps(c, "bloom_rp_apply");
-      // 66 KiB of LDS: two workgroups per CU, each looping over its blocks
-      const uint32_t ga = (uint32_t)std::min<uint64_t>(nblocks, 2ull * cus);
-      hipLaunchKernelGGL(rp_apply_kernel, dim3(ga), dim3(RA_T), 0, c->stream, region, h3, tb3, tile3_off, ntile3,
-                         nblocks, b->d_bits, b->nwords, fk);
+      // 136 KiB of LDS: one workgroup per CU, each looping over its buckets
+      const uint32_t ga = (uint32_t)std::min<uint64_t>(nbuckets, cus);
+      hipLaunchKernelGGL(rp_tapply_kernel, dim3(ga), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2, tile_off,
+                         tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg);
       RSK_CHECK_LAUNCH("bloom_rp_apply");
     }
     {
       ProfScope ps(c, "bloom_rp_reply");
-      constexpr int U = RSK_RP_U;  // keys (gather chains) per lane
-      const uint64_t g = (m + 256 * U - 1) / (256 * U);
-      const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 32ull * cus));
-      if (f16)
-        hipLaunchKernelGGL((rp_reply_kernel<true, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
-      else
-        hipLaunchKernelGGL((rp_reply_kernel<false, U>), dim3(grid), dim3(256), 0, c->stream, dk.data, dk.offsets,
-                           dk.fixed_len, m, b->fm, b->k, fk, d_out + first);
+      const uint32_t ng = Wl * Gw;  // one workgroup per key group
+#define RSK_RPR(F16, U)                                                                                            \
+  hipLaunchKernelGGL((rp_treply_kernel<F16, U>), dim3(ng), dim3(RR_T), 0, c->stream, dk.data, dk.offsets,         \
+                     dk.fixed_len, m, b->fm, b->k, T, d_out + first, kst, S, gs, Gw, nst, flags + 1)
+      const int u = c->tune.reply_u;  // gather chains per lane (default 2)
+      if (!f16) RSK_RPR(false, 2);
+      else if (u == 1) RSK_RPR(true, 1);
+      else if (u == 4) RSK_RPR(true, 4);
+      else RSK_RPR(true, 2);
+#undef RSK_RPR
       RSK_CHECK_LAUNCH("bloom_rp_reply");
+    }
+    uint32_t fb = 0;
+    RSK_HIP(hipMemcpyAsync(c->h_small + 8448, flags + 1, 4, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(&fb, c->h_small + 8448, 4);
+    if (fb) {
+      // A group's pending probes overflowed its LDS tables (many repeated
+      // keys inside one group): undo the chunk's bits and let the sort path
+      // answer it.
+      ProfScope ps(c, "bloom_rp_fallback");
+      const uint32_t gr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((b->nwords + 255) / 256, 8ull * cus));
+      hipLaunchKernelGGL(rp_restore_kernel, dim3(gr), dim3(256), 0, c->stream, b->d_bits, b->nwords, T);
+      RSK_CHECK_LAUNCH("bloom_rp_restore");
+      bloom_add_replies_sorted(c, b, dk, d_out + first);
     }
   }
   return true;

@@ -1,7 +1,7 @@
 // rsk_bloom_sa.h -- the append partition's first two stages (gfx950), shared
-// by the Bloom insert (rsk_bloom_st.hip, 4-byte probe records) and the
-// add()-with-replies pipeline (rsk_bloom_reply.hip, 8-byte records that also
-// carry the probe's sequence number).  Everything lives in an anonymous
+// by the Bloom insert (rsk_bloom_st.hip: bin offsets, then 16-bit bucket
+// offsets) and the add()-with-replies pipeline (rsk_bloom_reply.hip: the same
+// records with the key's group tag).  Everything lives in an anonymous
 // namespace: each translation unit instantiates its own kernels.  See
 // rsk_bloom_st.hip for the pipeline.
 #pragma once
@@ -17,30 +17,6 @@ constexpr uint32_t INVALID = 0xFFFFFFFFu;              // no probe (payloads are
 RSK_DEV uint32_t rdl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 RSK_DEV uint64_t rdl64(uint64_t v, uint32_t l) {
   return ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32) | rdl((uint32_t)v, l);
-}
-
-// Exclusive scan of one value per lane over a T-lane workgroup.
-template <int T>
-RSK_DEV uint32_t block_scan(uint32_t v, uint32_t* total, uint32_t* wsum) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int q = 0; q < T / 64; ++q) {
-    const uint32_t s = wsum[q];
-    pre += q < w ? s : 0;
-    tot += s;
-  }
-  *total = tot;
-  __syncthreads();
-  return pre + x - v;
 }
 
 RSK_DEV void key_words(const uint4& v, uint64_t* w0, uint64_t* w1) {
@@ -90,76 +66,15 @@ RSK_DEV void wave0_bin_starts(uint32_t* hist, uint32_t* lstart, uint32_t nb, uin
   }
 }
 
-// Probe records of the append partition.  u32: the probe's bit offset inside
-// its bin (the insert); u64: (key index << 32) | offset, the add()-with-replies
-// pipeline, whose last stage needs the key each probe belongs to.  Offsets
-// are < 2^26, so a record whose low word is INVALID is padding.
-template <class R>
-RSK_DEV uint32_t rec_off(R r) { return (uint32_t)r; }
-template <class R>
-RSK_DEV R rec_make(uint32_t off, uint32_t key) {
-  if constexpr (sizeof(R) == 8) return ((uint64_t)key << 32) | off;
-  else return off;
-}
-template <class R>
-RSK_DEV R rec_with_off(R r, uint32_t off) {  // same record, offset replaced
-  if constexpr (sizeof(R) == 8) return (r & ~0xFFFFFFFFull) | off;
-  else return off;
-}
+// Probe records of the append partition: the probe's bit offset inside its
+// coarse bin (< 2^26; the replies pipeline keeps its key group in bits
+// 26..31, group <= 62), so 0xFFFFFFFF (INVALID) is free for padding.
 template <class R>
 constexpr R rec_pad() { return (R)~(R)0; }
-template <class R>
-RSK_DEV void unpack16(const uint4& x, R* out) {  // one 16-byte group -> 16 / sizeof(R) records
-  if constexpr (sizeof(R) == 8) {
-    out[0] = ((uint64_t)x.y << 32) | x.x;
-    out[1] = ((uint64_t)x.w << 32) | x.z;
-  } else {
-    out[0] = x.x;
-    out[1] = x.y;
-    out[2] = x.z;
-    out[3] = x.w;
-  }
-}
-
-// wave0_bin_starts with every bin's run padded to a whole 16-byte group of
-// records (rec_pad in img), so runs start 16-byte aligned: starts and total padded.
-template <int NBMAX, class R>
-RSK_DEV void wave0_bin_starts_pad(uint32_t* hist, uint32_t* lstart, uint32_t nb, uint16_t* hdr_row,
-                                  uint32_t* s_total, R* img) {
-  constexpr uint32_t RG = 16 / sizeof(R);
-  constexpr int PER = NBMAX / 64;
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t v[PER], sum = 0;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const uint32_t b = lane * PER + i;
-    v[i] = b < nb ? hist[b] : 0;
-    if (b < nb) hist[b] = 0;
-    sum += (v[i] + RG - 1) & ~(RG - 1);
-  }
-  const uint32_t incl = wave_scan_incl(sum, lane);
-  uint32_t run = incl - sum;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const uint32_t b = lane * PER + i;
-    const uint32_t l4 = (v[i] + RG - 1) & ~(RG - 1);
-    if (b < nb) {
-      lstart[b] = run;
-      hdr_row[b] = (uint16_t)run;
-      for (uint32_t j = run + v[i]; j < run + l4; ++j) img[j] = rec_pad<R>();
-    }
-    run += l4;
-  }
-  const uint32_t total = rdl(incl, 63);
-  if (lane == 0) {
-    hdr_row[nb] = (uint16_t)total;
-    *s_total = total;
-  }
-}
 
 // ------------------------------------------------------ header transpose
 // in [rows][cols] -> out [cols][rows] (u16), 64 x 64 tiles through LDS.
-__global__ __launch_bounds__(256) void st_transpose_kernel(const uint16_t* __restrict__ in, uint64_t rows,
+__global__ __launch_bounds__(256) __attribute__((unused)) void st_transpose_kernel(const uint16_t* __restrict__ in, uint64_t rows,
                                                            uint32_t cols, uint16_t* __restrict__ out) {
   __shared__ uint16_t t[64][66];
   const uint64_t r0 = (uint64_t)blockIdx.x * 64;
@@ -241,27 +156,27 @@ __global__ __launch_bounds__(1024) void st_offsets_kernel(const uint64_t* __rest
 constexpr int SA2_V = RSK_SA2_V;    // sa2: uint4 loads per lane per tile (u32: 96 probes per fine bin: apply's 2 x 64 fast path)
 constexpr uint32_t SA2_T = 1024;    // sa2 workgroup
 constexpr uint32_t SA2_WMAX = 1024;  // sa1 workgroups per sa2 part, at most (the host keeps W <= this)
-template <class R>
-constexpr uint32_t sa2_slots() { return SA2_T * SA2_V * (16 / sizeof(R)); }
-template <class R>
-constexpr uint32_t sa2_pad() { return (16 / sizeof(R) - 1) * 128; }  // pad slots per sa2 tile, at most (per fine bin)
-constexpr uint32_t SA2_SLOTS = sa2_slots<uint32_t>();
-constexpr uint32_t SA2_PAD = sa2_pad<uint32_t>();
+constexpr uint32_t SA2_SLOTS = SA2_T * SA2_V * 4;  // records per sa2h tile
 
-// 512-lane workgroups: at most 80 VGPRs with 4-byte records, so 3 workgroups
-// (6 waves per SIMD) share a CU; 8-byte records: 2 workgroups (73 KiB of LDS).
-// u64 records carry the key's index in the chunk (the host keeps a chunk
-// below 2^32 - 1 keys).
+// 512-lane workgroups: at most 80 VGPRs, so 3 workgroups (6 waves per SIMD)
+// share a CU; with 4 keys per lane (73 KiB of LDS) 2.
 // KPL: keys per lane (default 16 / KMAX); more keys per super-tile make every
 // bin's run longer.
-template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX>
-__global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
+//
+// TAGGED (the add()-with-replies pipeline, rsk_bloom_reply.hip): workgroup w
+// takes the CONTIGUOUS super-tiles [w S, (w + 1) S) instead of every
+// gridDim.x-th one, and each record carries in its top 6 bits the key group
+// g = (super-tile - w S) / gs of its key (offsets are < 2^26): along any
+// sub-region (w, c) g never decreases, so key order is known per group.
+template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX, bool TAGGED = false>
+__global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
     FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
-    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow) {
+    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow, uint32_t S = 0, uint32_t gs = 1) {
   constexpr uint32_t KST = T1 * KPL;
   constexpr int NP = KPL * KMAX;
   constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
+  static_assert(sizeof(R) == 4, "4-byte probe records");
   constexpr uint32_t RG = 16 / sizeof(R);  // records per 16-byte group
   // runs are padded to whole 16-byte groups (rec_pad), so the write-out
   // moves 16-byte groups of one bin to 16-byte aligned destinations
@@ -276,12 +191,16 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
   }
   R* const mine = region + (uint64_t)blockIdx.x * nb1 * quota;  // sub-regions (blockIdx.x, 0..nb1)
   const uint4* keys16 = reinterpret_cast<const uint4*>(data);
+  // super-tiles of this workgroup: [s_beg, s_end) in steps of s_step
+  const uint64_t s_beg = TAGGED ? (uint64_t)blockIdx.x * S : blockIdx.x;
+  const uint64_t s_end = TAGGED ? (s_beg + S < nst ? s_beg + S : nst) : nst;
+  const uint64_t s_step = TAGGED ? 1 : gridDim.x;
   uint4 nxt[KPL];
   auto fetch = [&](uint64_t st) {
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
       const uint64_t i = st * KST + threadIdx.x + (uint64_t)u * T1;
-      nxt[u] = (FIXED16 && st < nst && i < n) ? ld_nt16(keys16 + i) : make_uint4(0, 0, 0, 0);
+      nxt[u] = (FIXED16 && st < s_end && i < n) ? ld_nt16(keys16 + i) : make_uint4(0, 0, 0, 0);
     }
   };
   // The image of tile t is written out during tile t + 1, after its hashes
@@ -300,17 +219,17 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
         u32x4 x = {v.x, v.y, v.z, v.w};
         // 8-byte records (the replies pipeline's rp1): streaming stores measured 19.4 -> 18.4 ms;
         // 4-byte records (the insert's sa1): no gain
-        if constexpr (sizeof(R) == 8) __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(mine + (RG * g + d)));
-        else *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;
+        *reinterpret_cast<u32x4*>(mine + (RG * g + d)) = x;  // (streaming stores: no gain measured)
       }
     }
   };
   uint32_t pend4 = 0;
-  if (FIXED16) fetch(blockIdx.x);
+  if (FIXED16) fetch(s_beg);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t st = blockIdx.x; st < nst; st += gridDim.x) {
+  for (uint64_t st = s_beg; st < s_end; st += s_step) {
     const uint64_t k0 = st * KST;
+    const uint32_t gtag = TAGGED ? (uint32_t)((st - s_beg) / gs) << 26 : 0u;
     const uint32_t nk = (uint32_t)(n - k0 < KST ? n - k0 : KST);
     uint4 cur[KPL];
 #pragma unroll
@@ -322,7 +241,6 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
     for (int u = 0; u < KPL; ++u) {
       const uint32_t q = threadIdx.x + u * T1;
       const bool ok = q < nk;
-      const uint32_t key = sizeof(R) == 8 ? (uint32_t)(k0 + q) : 0u;
       uint64_t h1 = 0, h2 = 0;
       if (ok) {
         if (FIXED16) {
@@ -343,13 +261,13 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
         if (ok && t < k) {
           const uint64_t idx = ps.idx;
           const uint32_t bin = (uint32_t)(idx >> shift1);
-          pay[s] = rec_make<R>((uint32_t)(idx & low), key);
+          pay[s] = (R)((uint32_t)(idx & low) | gtag);
           tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
           if (t + 1 < k) ps.next(t, fm);
         }
       }
     }
-    if (FIXED16) fetch(st + gridDim.x);
+    if (FIXED16) fetch(st + s_step);
     write_out(pend4);  // tile t - 1
     lds_barrier();  // (A) every rank taken, the previous image written out
     // wave 0: bin starts and run destinations (runs of L probes take
@@ -402,140 +320,6 @@ __global__ __launch_bounds__(T1, (sizeof(R) == 8 || KPL * KMAX > 16) ? 4 : (T1 =
   if (threadIdx.x < nb1) used[(uint64_t)blockIdx.x * nb1 + threadIdx.x] = pos[threadIdx.x];
 }
 
-// tot[cp] = records of (c, p), bud[cp] = its sa2 tiles (one per sa2_slots<R> of each sub-region)
-template <class R>
-__global__ __launch_bounds__(256) void sa_size_kernel(const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
-                                                      uint32_t P, uint32_t ncp, uint64_t* __restrict__ tot,
-                                                      uint32_t* __restrict__ bud) {
-  constexpr uint64_t RG = 16 / sizeof(R);
-  const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cp >= ncp) return;
-  const uint32_t c = cp / P, p = cp - c * P;
-  uint64_t probes = 0;
-  uint32_t tiles = 0;
-  for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
-    const uint32_t u = used[(uint64_t)w * nb1 + c];
-    probes += u;
-    tiles += (u + sa2_slots<R>() - 1) / sa2_slots<R>();
-  }
-  // sa2 output bound: its tiles pad fine-bin runs
-  tot[cp] = ((probes + RG - 1) & ~(RG - 1)) + (uint64_t)tiles * sa2_pad<R>();
-  bud[cp] = tiles;
-}
-
-// A tile's loads issue at its top (a register prefetch of the next tile
-// needs 64+ VGPRs: the second workgroup of the CU covers the latency
-// instead).  __launch_bounds__(1024, 8): at most 64 VGPRs, so two workgroups
-// share a CU.
-template <class R>
-__global__ __launch_bounds__(SA2_T, 8) void bloom_sa2_kernel(const R* __restrict__ region, uint32_t quota,
-                                                          const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
-                                                          uint32_t P, uint32_t nb2,
-                                                          const uint64_t* __restrict__ reg_off,
-                                                          const uint32_t* __restrict__ tile_off,
-                                                          uint32_t* __restrict__ tiles_out, R* __restrict__ out,
-                                                          uint16_t* __restrict__ h2, uint64_t* __restrict__ tb2) {
-  constexpr uint32_t RG = 16 / sizeof(R);
-  constexpr int NV = SA2_V * RG;
-  constexpr uint32_t SLOTS = sa2_slots<R>();
-  // one image buffer: tile t's write-out is done before (A) of t + 1, and
-  // the image is rewritten after (B)
-  __shared__ __attribute__((aligned(16))) R srt[1][SLOTS + RG * 128];  // + pad slots per fine bin
-  __shared__ uint32_t hist[128], lstart[128], s_total;
-  __shared__ uint16_t s_hdr[129];
-  __shared__ uint32_t s_used[SA2_WMAX];  // used[w][c] of this part's sub-regions
-  const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
-  if (threadIdx.x < 128) hist[threadIdx.x] = 0;
-  const uint64_t base = reg_off[cp];
-  const uint32_t tbeg = tile_off[cp];
-  uint64_t written = 0;
-  uint32_t ntile = 0;
-  // Tiles run over the sub-regions (w, c) of this part in order.  As in sa1,
-  // the image of tile t is written out during tile t + 1, after its ranks
-  // (one vmcnt for loads and stores: see bloom_sa1_kernel).  A uint4 is loaded when its first record is below
-  // `used` (quota is a multiple of RG, so it lies inside the sub-region); the
-  // records past `used` are replaced by rec_pad.
-  const uint32_t wbeg = W * p / P, wend = W * (p + 1) / P;
-  for (uint32_t i = threadIdx.x; i < wend - wbeg; i += SA2_T) s_used[i] = used[(uint64_t)(wbeg + i) * nb1 + c];
-  __syncthreads();
-  uint32_t w = wbeg, t0 = 0, nu = 0;
-  while (w < wend && (nu = s_used[w - wbeg]) == 0) ++w;
-  uint4 nxt[SA2_V];
-  auto fetch = [&](uint32_t w_, uint32_t t0_, uint32_t nu_) {
-    const uint4* in = reinterpret_cast<const uint4*>(region + ((uint64_t)w_ * nb1 + c) * quota);
-#pragma unroll
-    for (int v = 0; v < SA2_V; ++v) {
-      const uint32_t q4 = t0_ / RG + v * SA2_T + threadIdx.x;
-      nxt[v] = RG * q4 < nu_ ? ld_nt16(in + q4) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto write_out = [&](uint32_t total, uint64_t at) {
-    // 16-byte aligned: base and at are multiples of RG slots
-    u32x4* o4 = reinterpret_cast<u32x4*>(out + base + at);
-    const uint4* i4 = reinterpret_cast<const uint4*>(srt[0]);
-    for (uint32_t j = threadIdx.x; j < total / RG; j += SA2_T) {
-      const uint4 v = i4[j];
-      u32x4 x = {v.x, v.y, v.z, v.w};
-      __builtin_nontemporal_store(x, o4 + j);
-    }
-  };
-  bool have = w < wend;
-  uint32_t pend = 0;  // records of the previous tile still in the image
-  uint64_t pend_at = 0;
-  __syncthreads();
-  while (have) {
-    fetch(w, t0, nu);
-    uint4 cur[SA2_V];
-#pragma unroll
-    for (int v = 0; v < SA2_V; ++v) cur[v] = nxt[v];
-    const uint32_t ct0 = t0, cnu = nu;
-    t0 += SLOTS;
-    if (t0 >= nu) {
-      t0 = 0;
-      do ++w;
-      while (w < wend && (nu = s_used[w - wbeg]) == 0);
-    }
-    have = w < wend;
-    R pay[NV];
-    uint32_t tag[NV];
-#pragma unroll
-    for (int v = 0; v < SA2_V; ++v) {
-      const uint32_t q4 = ct0 / RG + v * SA2_T + threadIdx.x;
-      R x[RG];
-      unpack16<R>(cur[v], x);
-#pragma unroll
-      for (uint32_t e = 0; e < RG; ++e) pay[RG * v + e] = RG * q4 + e < cnu ? x[e] : rec_pad<R>();
-    }
-#pragma unroll
-    for (int r = 0; r < NV; ++r) {
-      tag[r] = INVALID;
-      if (rec_off(pay[r]) != INVALID) {
-        const uint32_t bin = rec_off(pay[r]) >> SL_LOG;
-        tag[r] = (bin << 16) | atomicAdd(&hist[bin], 1u);
-      }
-    }
-    write_out(pend, pend_at);  // tile t - 1
-    lds_barrier();  // (A) ranks taken, the previous image written out
-    if (threadIdx.x < 64) wave0_bin_starts_pad<128, R>(hist, lstart, nb2, s_hdr, &s_total, srt[0]);
-    lds_barrier();  // (B)
-    const uint32_t total = s_total;  // padded: a multiple of RG
-    if (threadIdx.x <= nb2) h2[(uint64_t)(tbeg + ntile) * (nb2 + 1) + threadIdx.x] = s_hdr[threadIdx.x];
-    if (threadIdx.x == 0) tb2[tbeg + ntile] = base + written;
-    R* img = srt[0];
-#pragma unroll
-    for (int r = 0; r < NV; ++r)
-      if (tag[r] != INVALID)
-        img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = rec_with_off(pay[r], rec_off(pay[r]) & ((1u << SL_LOG) - 1));
-    pend = total;
-    pend_at = written;
-    written += total;
-    ++ntile;
-    lds_barrier();  // (C)
-  }
-  write_out(pend, pend_at);
-  if (threadIdx.x == 0) tiles_out[cp] = ntile;
-}
-
 // ==================================== sa2 with 16-bit records (the insert)
 // The insert's second pass re-sorts each coarse bin by BUCKET = the slice and
 // the top 3 bits of the 19-bit offset inside it (2^(f2+3) <= 1024 buckets), so
@@ -553,7 +337,7 @@ constexpr uint32_t SAH_SUB = 3;         // offset bits [16, 19) sorted by bucket
 // per tile), bud[cp] = its tiles.
 __global__ __launch_bounds__(256) __attribute__((unused)) void sah_size_kernel(const uint32_t* __restrict__ used, uint32_t W, uint32_t nb1,
                                                        uint32_t P, uint32_t ncp, uint64_t* __restrict__ tot,
-                                                       uint32_t* __restrict__ bud) {
+                                                       uint32_t* __restrict__ bud, uint32_t slots = SA2_SLOTS) {
   const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
   if (cp >= ncp) return;
   const uint32_t c = cp / P, p = cp - c * P;
@@ -562,23 +346,36 @@ __global__ __launch_bounds__(256) __attribute__((unused)) void sah_size_kernel(c
   for (uint32_t w = W * p / P; w < W * (p + 1) / P; ++w) {
     const uint32_t u = used[(uint64_t)w * nb1 + c];
     recs += u;
-    tiles += (u + SA2_SLOTS - 1) / SA2_SLOTS;
+    tiles += (u + slots - 1) / slots;
   }
   tot[cp] = ((recs + 7) & ~7ull) + 8ull * tiles;
   bud[cp] = tiles;
 }
 
-__global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_kernel(const uint32_t* __restrict__ region, uint32_t quota,
+// O = uint16_t: the insert (16-bit offsets inside the bucket).  O = uint32_t:
+// the add()-with-replies pipeline, whose input records carry the key group g
+// in bits 26..31 (bloom_sa1_kernel<..., TAGGED>): the output record is
+// (tag << 16) | offset with tag = w Gw + g, w the sub-region's sa1
+// workgroup -- groups numbered in key order across the whole chunk.
+// V: uint4 loads per lane per tile (tile = 4096 V records; V = 6 takes 96 KiB
+// of LDS: one workgroup per CU).
+template <class O, int V = SA2_V>
+__global__ __launch_bounds__(SA2_T, V > 3 ? 4 : 8) __attribute__((unused)) void bloom_sa2h_kernel(const uint32_t* __restrict__ region, uint32_t quota,
                                                            const uint32_t* __restrict__ used, uint32_t W,
                                                            uint32_t nb1, uint32_t P, uint32_t nbk,
                                                            const uint64_t* __restrict__ reg_off,
                                                            const uint32_t* __restrict__ tile_off,
                                                            uint32_t* __restrict__ tiles_out,
-                                                           uint16_t* __restrict__ out, uint4* __restrict__ hp,
-                                                           uint64_t hp_stride, uint32_t* __restrict__ tb2) {
-  constexpr int NV = SA2_V * 4;  // records per lane per tile
+                                                           O* __restrict__ out, uint4* __restrict__ hp,
+                                                           uint64_t hp_stride, uint32_t* __restrict__ tb2,
+                                                           uint32_t Gw = 0) {
+  constexpr bool TAGGED = sizeof(O) == 4;
+  constexpr uint32_t RPU = 16 / sizeof(O);  // records per uint4
+  constexpr uint32_t OFFM = TAGGED ? (1u << 26) - 1 : 0xFFFFFFFFu;
+  constexpr int NV = V * 4;  // records per lane per tile
+  constexpr uint32_t SLOTS = SA2_T * V * 4;
   constexpr uint32_t PER = SAH_BK_MAX / 64;  // buckets per wave-0 lane
-  __shared__ __attribute__((aligned(16))) uint16_t img[SA2_SLOTS + 8];
+  __shared__ __attribute__((aligned(16))) O img[SLOTS + 8];
   __shared__ uint32_t hist[SAH_BK_MAX], lstart[SAH_BK_MAX + 1];
   __shared__ uint32_t s_used[SA2_WMAX];
   const uint32_t cp = blockIdx.x, c = cp / P, p = cp - c * P;
@@ -597,7 +394,7 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
   auto write_out = [&](uint32_t total, uint64_t at) {
     u32x4* o4 = reinterpret_cast<u32x4*>(out + base + at);  // base, at: multiples of 8 slots
     const uint4* i4 = reinterpret_cast<const uint4*>(img);
-    for (uint32_t j = threadIdx.x; j < (total + 7) / 8; j += SA2_T) {
+    for (uint32_t j = threadIdx.x; j < (total + RPU - 1) / RPU; j += SA2_T) {
       const uint4 v = i4[j];
       u32x4 x = {v.x, v.y, v.z, v.w};
       __builtin_nontemporal_store(x, o4 + j);
@@ -609,14 +406,14 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
   const uint32_t lane = threadIdx.x & 63;
   while (have) {
     const uint4* in = reinterpret_cast<const uint4*>(region + ((uint64_t)w * nb1 + c) * quota);
-    uint4 cur[SA2_V];
+    uint4 cur[V];
 #pragma unroll
-    for (int v = 0; v < SA2_V; ++v) {
+    for (int v = 0; v < V; ++v) {
       const uint32_t q4 = t0 / 4 + v * SA2_T + threadIdx.x;
       cur[v] = 4 * q4 < nu ? ld_nt16(in + q4) : make_uint4(INVALID, INVALID, INVALID, INVALID);
     }
-    const uint32_t ct0 = t0, cnu = nu;
-    t0 += SA2_SLOTS;
+    const uint32_t ct0 = t0, cnu = nu, tagbase = w * Gw;  // a tile never spans two sub-regions
+    t0 += SLOTS;
     if (t0 >= nu) {
       t0 = 0;
       do ++w;
@@ -625,7 +422,7 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
     have = w < wend;
     uint32_t pay[NV], tag[NV];
 #pragma unroll
-    for (int v = 0; v < SA2_V; ++v) {
+    for (int v = 0; v < V; ++v) {
       const uint32_t q4 = ct0 / 4 + v * SA2_T + threadIdx.x;
       const uint32_t x[4] = {cur[v].x, cur[v].y, cur[v].z, cur[v].w};
 #pragma unroll
@@ -635,7 +432,7 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
     for (int r = 0; r < NV; ++r) {
       tag[r] = INVALID;
       if (pay[r] != INVALID) {
-        const uint32_t bk = pay[r] >> 16;
+        const uint32_t bk = (pay[r] & OFFM) >> 16;
         tag[r] = (bk << 16) | atomicAdd(&hist[bk], 1u);
       }
     }
@@ -669,10 +466,14 @@ __global__ __launch_bounds__(SA2_T, 8) __attribute__((unused)) void bloom_sa2h_k
                           : make_uint4(total, 0, 0, 0);
       hp[(uint64_t)threadIdx.x * hp_stride + tbeg + ntile] = v;
     }
-    if (threadIdx.x == 0) tb2[tbeg + ntile] = (uint32_t)((base + written) / 8);  // the tile's first uint4
+    if (threadIdx.x == 0) tb2[tbeg + ntile] = (uint32_t)((base + written) / RPU);  // the tile's first uint4
 #pragma unroll
     for (int r = 0; r < NV; ++r)
-      if (tag[r] != INVALID) img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] = (uint16_t)pay[r];
+      if (tag[r] != INVALID) {
+        const uint32_t x = pay[r];
+        img[lstart[tag[r] >> 16] + (tag[r] & 0xFFFFu)] =
+            TAGGED ? (O)(((tagbase + (x >> 26)) << 16) | (x & 0xFFFFu)) : (O)x;
+      }
     pend = total;
     pend_at = written;
     written += (total + 7) & ~7u;

@@ -453,7 +453,7 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     }
     {
       ProfScope ps(c, "bloom_st2");
-      hipLaunchKernelGGL(bloom_sa2h_kernel, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P,
+      hipLaunchKernelGGL(bloom_sa2h_kernel<uint16_t>, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P,
                          nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2);
       RSK_CHECK_LAUNCH("bloom_sa2");
     }

@@ -52,8 +52,11 @@ struct Tuning {
   uint64_t bloom_chunk = 0;  // probes per chunk of the slice-routed insert (0: 2^33)
   int sa_tiny = 0;           // sub-regions of 32 probes: forces the overflow fallbacks
   uint32_t sa_parts = 0;     // sa2 / rp2 parts per coarse bin (0: 4 x CUs / bins)
-  int reply = 0;             // add() replies: 0 auto, 1 first-key pipeline at any size, -1 the sort path
-  uint64_t reply_chunk = 0;  // probes per chunk of the first-key pipeline (0: 2^33)
+  int reply = 0;             // add() replies: 0 auto, 1 group-tag pipeline at any size, -1 the sort path
+  uint64_t reply_chunk = 0;  // probes per chunk of the group-tag pipeline (0: 2^33)
+  int reply_u = 0;           // rp_treply gather chains per lane: 0 (= 2), 1, 2 or 4
+  int reply_v = 0;           // rp2 tile: uint4 per lane, 0 (= 3) or 6
+  int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
 };
 

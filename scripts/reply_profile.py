@@ -15,14 +15,19 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
-STAGES = ("bloom_rp1", "bloom_rp_mid", "bloom_rp2", "bloom_rp3", "bloom_rp_apply", "bloom_rp_reply")
+STAGES = ("bloom_rp1", "bloom_rp_mid", "bloom_rp2", "bloom_rp_apply", "bloom_rp_reply", "bloom_rp_fallback")
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
     runs = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    routes = dict(kv.split("=") for kv in sys.argv[3].split(",")) if len(sys.argv) > 3 else {}
     L = _lib.load()
+    if routes:
+        _lib.diag()
     eng = _lib.Engine(0)
+    for name, v in routes.items():
+        eng.set_route(name, int(v))
     size, k = ctypes.c_int64(), ctypes.c_int32()
     _lib.check(L.rsk_bloom_params(n, 0.01, _lib.RSK_BLOOM_EXTENDED, ctypes.byref(size), ctypes.byref(k)))
     keys = devmem.gen_keys16(eng, 0x5EED0003, 0, n)
@@ -49,7 +54,7 @@ def main():
         if cnt:
             stages[s] = ms / runs
     trues = int(out.to_numpy().sum())
-    print(json.dumps({"keys": n, "size_bits": size.value, "k": k.value, "runs": runs,
+    print(json.dumps({"routes": routes, "keys": n, "size_bits": size.value, "k": k.value, "runs": runs,
                       "ms_min": min(times) * 1e3, "ms_all": [t * 1e3 for t in times],
                       "keys_per_s": n / min(times), "stage_ms_per_call": stages, "replies_true": trues}))
 
