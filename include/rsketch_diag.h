@@ -26,12 +26,24 @@ const char *rsk_diag_last_error(void);
  *   bloom_chunk   probes per chunk of the slice-routed insert (0 = default)
  *   sa_tiny       1: sub-regions of 32 probes (forces the overflow fallbacks)
  *   sa_parts      sa2 / rp2 parts per coarse bin (0 = default)
- *   reply         add() replies: 0 auto, 1 first-key pipeline at any size, -1 sort path
- *   reply_chunk   probes per chunk of the first-key pipeline (0 = default)
+ *   reply         add() replies: 0 auto, 1 group-tag pipeline at any size, -1 sort path
+ *   reply_chunk   probes per chunk of the group-tag pipeline (0 = default)
+ *   reply_u       rp_treply keys (gather chains) per lane: 0 (= 2), 1, 2, 4
+ *   reply_v       rp2 tile: uint4 loads per lane, 0 (= 6) or 3
+ *   reply_s       rp_tapply: wave steps whose segment loads are issued together, 0 (= 2), 1, 4;
+ *                 -1: software-pipelined (next step's loads during this step's folds)
+ *   reply_dbg     TIMING ONLY (wrong replies and T): rp_tapply without its
+ *                 folds (bit 0) / without its T stores (bit 1)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
  *   reset         every route back to automatic
- * Every route gives bit-identical results; they differ in speed only. */
+ * Every route but reply_dbg gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
+
+/* add()-with-replies counters of a context since it was created: key groups
+ * whose pending probes (a bit probed more than once by the group that probed
+ * it first) were resolved in LDS, and chunks answered by the sort-path
+ * fallback (a group's pending probes overflowed its LDS tables). */
+int rsk_diag_reply_stats(rsk_ctx *ctx, uint64_t *pending_groups, uint64_t *fallbacks);
 
 /* --------------------------------------------------------- diagnostics */
 /* Memory-system microbenchmark on a device buffer (roofline denominators):

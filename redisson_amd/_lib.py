@@ -180,6 +180,7 @@ SIGNATURES = {
 DIAG_SIGNATURES = {
     "rsk_diag_last_error": (ctypes.c_char_p, []),
     "rsk_diag_set_route": (ctypes.c_int, [_vp, ctypes.c_char_p, _i64]),
+    "rsk_diag_reply_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
     "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),
     "rsk_diag_bloom_contains_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _u64, _vp,
@@ -367,6 +368,13 @@ class Engine:
         """Route override of this context (rsk_diag_set_route): tests force
         every pipeline of the library; "reset" restores the automatic routes."""
         check_diag(diag().rsk_diag_set_route(self.ctx, name.encode(), int(value)), "rsk_diag_set_route")
+
+    def reply_stats(self):
+        """(groups whose pending reply probes were resolved in LDS, chunks
+        answered by the sort-path fallback) of this context (rsk_diag_reply_stats)."""
+        pg, fb = ctypes.c_uint64(), ctypes.c_uint64()
+        check_diag(diag().rsk_diag_reply_stats(self.ctx, ctypes.byref(pg), ctypes.byref(fb)), "rsk_diag_reply_stats")
+        return pg.value, fb.value
 
     def routes(self, **kw):
         """Context manager: the given route overrides, then automatic routes."""

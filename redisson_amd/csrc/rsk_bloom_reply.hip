@@ -52,7 +52,6 @@ namespace {
 
 constexpr uint32_t BK_LOG = 16;                        // bits per bucket (rp2's unit)
 constexpr uint32_t BK_BITS = 1u << BK_LOG;             // u16 entry per bit in LDS: 128 KiB
-constexpr uint32_t BK_WORDS = BK_BITS / 32;            // 2048 filter words per bucket
 constexpr uint32_t T_NONE = 0xFFFFu;                   // T: no probe finds this bit clear
 constexpr uint32_t MAX_TAGS = 32766;                   // group tags: (tag << 1) | 1 < T_NONE
 constexpr uint32_t TA_T = 1024;                        // rp_tapply workgroup
@@ -93,40 +92,128 @@ RSK_DEV void tap_fold(uint32_t* tt, uint32_t rec) {
 // buckets; row f + 1's first u16 ends sub-bucket 7).  Lane l of a wave loads
 // tile g + l's bounds; then four lanes take one tile's segment (two aligned
 // uint4 each = 32 record slots, the rest of a long segment in a loop), 16
-// segments per wave step.  Consecutive buckets run on one XCD (xcd_slot):
-// the 8 buckets of a slice share their segments' cache lines in its L2.
-__global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restrict__ recs,
+// segments per wave step, the loads of S steps issued before the first of
+// them is folded (one workgroup per CU: the waves' loads in flight are what
+// hides the latency).  A record is folded by an LDS read and a CAS (retried
+// when another record took the word).  Consecutive buckets run on one XCD
+// (xcd_slot): the 8 buckets of a slice share their segments' cache lines in
+// its L2.  (Measured at C3, rp2 tiles of 24576 records, S = 1: 20.3-20.9 ms;
+// a step's 8 records folded as a batch -- every read, then every CAS --
+// 21.9 ms; two steps' loads and a 16-record batch spilled 27 VGPRs, 26.0 ms.)
+template <int S, bool HALF = false>
+__global__ __launch_bounds__(TA_T, HALF ? 8 : 4) void rp_tapply_kernel(const uint32_t* __restrict__ recs,
                                                          const uint4* __restrict__ hp, uint64_t hp_stride,
                                                          uint32_t f2, const uint32_t* __restrict__ tb,
                                                          const uint32_t* __restrict__ tile_off,
                                                          const uint32_t* __restrict__ ntiles, uint32_t P,
                                                          uint64_t nbuckets, uint32_t* __restrict__ bits,
                                                          uint64_t nwords, uint16_t* __restrict__ T, int dbg) {
-  __shared__ __attribute__((aligned(16))) uint32_t tt[BK_BITS / 2];
-  __shared__ __attribute__((aligned(16))) uint32_t f0[BK_WORDS];
+  // HALF: a unit is half a bucket (2^15 bits, 64 KiB of entries: two
+  // workgroups per CU); both halves read the bucket's segments (one L2 fetch)
+  // and each folds the records of its own half.
+  constexpr uint32_t UB = HALF ? BK_BITS / 2 : BK_BITS;  // bits per unit
+  __shared__ __attribute__((aligned(16))) uint32_t tt[UB / 2];
+  __shared__ __attribute__((aligned(16))) uint32_t f0[UB / 32];
   const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   constexpr uint32_t NW = TA_T / 64;
   const uint4* r4 = reinterpret_cast<const uint4*>(recs);
-  auto fold4 = [&](const uint4& v, uint32_t p, uint32_t sb, uint32_t se) {
-    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (p + j >= sb && p + j < se) {
-        if (dbg & 1) tt[x[j] & 0x7FFFu] |= x[j] >> 31;  // timing only: one plain LDS op per record
-        else tap_fold(tt, x[j]);
-      }
+  uint32_t hsel = 0;  // HALF: the unit's half (record offset bit 15)
+  auto fold1 = [&](uint32_t x) {
+    if (HALF) {
+      if (((x >> 15) & 1u) != hsel) return;
+      x &= ~0x8000u;
+    }
+    if (dbg & 1) tt[x & (UB / 2 - 1)] |= x >> 31;  // timing only: one plain LDS op per record
+    else tap_fold(tt, x);
   };
-  for (uint64_t u = xcd_slot(blockIdx.x, gridDim.x); u < nbuckets; u += gridDim.x) {
+  auto fold_step = [&](const auto& l) {
+    const uint32_t x[8] = {l.v0.x, l.v0.y, l.v0.z, l.v0.w, l.v1.x, l.v1.y, l.v1.z, l.v1.w};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t pos = l.p0 + (r < 4 ? r : 12 + r);
+      if (pos >= l.sb && pos < l.se) fold1(x[r]);
+    }
+    for (uint32_t p = l.p0 + 32; p < l.se; p += 16) {  // long segments (rare)
+      const uint4 v = r4[l.st + p / 4];
+      const uint32_t y[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (p + r >= l.sb && p + r < l.se) fold1(y[r]);
+    }
+  };
+  const uint64_t nunits = HALF ? 2 * nbuckets : nbuckets;
+  for (uint64_t un = xcd_slot(blockIdx.x, gridDim.x); un < nunits; un += gridDim.x) {
+    const uint64_t u = HALF ? un >> 1 : un;
+    hsel = HALF ? (uint32_t)(un & 1) : 0u;
     uint4* t4 = reinterpret_cast<uint4*>(tt);
-    for (uint32_t q = threadIdx.x; q < BK_BITS / 8; q += TA_T) t4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    const uint64_t w0 = u * BK_WORDS;
-    for (uint32_t q = threadIdx.x; q < BK_WORDS; q += TA_T) f0[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
+    for (uint32_t q = threadIdx.x; q < UB / 8; q += TA_T) t4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    const uint64_t w0 = un * (UB / 32);  // the unit's first filter word
+    for (uint32_t q = threadIdx.x; q < UB / 32; q += TA_T) f0[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
     lds_barrier();
     const uint32_t s = (uint32_t)(u >> 3), e = (uint32_t)(u & 7), c = s >> f2, f = s & ((1u << f2) - 1);
     const uint4* hrow = hp + (uint64_t)f * hp_stride;
     const uint32_t* erow = reinterpret_cast<const uint32_t*>(hp + (uint64_t)(f + 1) * hp_stride);
     const uint32_t ta = tile_off[(uint64_t)c * P];
     const uint32_t te = tile_off[(uint64_t)c * P + P - 1] + ntiles[(uint64_t)c * P + P - 1];
+    if constexpr (S == 0) {  // software-pipelined: step k + 1's loads (and group i + 1's bounds) in flight during step k's folds
+      struct Hd {
+        uint32_t beg, end, tbl, g, ng;
+      };
+      auto hload = [&](uint32_t gg) {
+        Hd h{0, 0, 0, gg, gg < te ? (te - gg < 64 ? te - gg : 64) : 0};
+        const uint32_t t = gg + lane;
+        if (t < te) {
+          const uint4 v = hrow[t];
+          const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
+          h.beg = (hw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+          h.end = e < 7 ? (hw[(e + 1) >> 1] >> (16 * ((e + 1) & 1))) & 0xFFFFu : erow[4ull * t] & 0xFFFFu;
+          h.tbl = tb[t];
+        }
+        return h;
+      };
+      struct Ld {
+        uint4 v0, v1;
+        uint32_t sb, se, st, p0;
+      };
+      auto sload = [&](const Hd& h, uint32_t j) {
+        Ld l;
+        const uint32_t si = j + (lane >> 2), src = si < 63 ? si : 63;
+        l.sb = shfl_u32(h.beg, src);
+        const uint32_t se0 = shfl_u32(h.end, src);
+        l.st = shfl_u32(h.tbl, src);
+        l.se = si < h.ng ? se0 : l.sb;
+        l.p0 = (l.sb & ~3u) + 4 * (lane & 3);
+        l.v0 = l.p0 < l.se ? r4[l.st + l.p0 / 4] : make_uint4(0, 0, 0, 0);
+        l.v1 = l.p0 + 16 < l.se ? r4[l.st + l.p0 / 4 + 4] : make_uint4(0, 0, 0, 0);
+        return l;
+      };
+      uint32_t g = ta + 64 * w;
+      if (g < te) {
+        Hd hc = hload(g), hn = hload(g + 64 * NW);
+        uint32_t j = 0;
+        Ld la = sload(hc, 0);
+        while (true) {
+          // the next step: (same group, j + 16) or (next group, 0)
+          bool more = true, cross = false;
+          uint32_t jn = j + 16;
+          if (jn >= hc.ng) {
+            jn = 0;
+            cross = true;
+            more = hn.ng > 0;
+          }
+          Ld lb;
+          if (more) lb = sload(cross ? hn : hc, jn);
+          fold_step(la);
+          if (!more) break;
+          if (cross) {
+            hc = hn;
+            hn = hload(hc.g + 64 * NW);
+          }
+          j = jn;
+          la = lb;
+        }
+      }
+    } else {
     for (uint32_t g = ta + 64 * w; g < te; g += 64 * NW) {
       const uint32_t t = g + lane;
       uint32_t beg = 0, end = 0, tbl = 0;
@@ -138,24 +225,45 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
         tbl = tb[t];
       }
       const uint32_t ng = te - g < 64 ? te - g : 64;
-      for (uint32_t j = 0; j < ng; j += 16) {
-        const uint32_t si = j + (lane >> 2), src = si < 63 ? si : 63;
-        const uint32_t sb = shfl_u32(beg, src), se0 = shfl_u32(end, src), st = shfl_u32(tbl, src);
-        const uint32_t se = si < ng ? se0 : sb;
-        const uint32_t p0 = (sb & ~3u) + 4 * (lane & 3);
-        // plain loads: the slice's 8 buckets (on one XCD at about the same time) share these lines in L2
-        const uint4 v0 = p0 < se ? r4[st + p0 / 4] : make_uint4(0, 0, 0, 0);
-        const uint4 v1 = p0 + 16 < se ? r4[st + p0 / 4 + 4] : make_uint4(0, 0, 0, 0);
-        fold4(v0, p0, sb, se);
-        fold4(v1, p0 + 16, sb, se);
-        for (uint32_t p = p0 + 32; p < se; p += 16) fold4(r4[st + p / 4], p, sb, se);  // long segments (rare)
+      for (uint32_t j0 = 0; j0 < ng; j0 += 16 * S) {
+        uint4 v0[S], v1[S];
+        uint32_t sb[S], se[S], st[S], p0[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+          const uint32_t si = j0 + 16 * q + (lane >> 2), src = si < 63 ? si : 63;
+          sb[q] = shfl_u32(beg, src);
+          const uint32_t se0 = shfl_u32(end, src);
+          st[q] = shfl_u32(tbl, src);
+          se[q] = si < ng ? se0 : sb[q];
+          p0[q] = (sb[q] & ~3u) + 4 * (lane & 3);
+          // plain loads: the slice's 8 buckets (on one XCD at about the same time) share these lines in L2
+          v0[q] = p0[q] < se[q] ? r4[st[q] + p0[q] / 4] : make_uint4(0, 0, 0, 0);
+          v1[q] = p0[q] + 16 < se[q] ? r4[st[q] + p0[q] / 4 + 4] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+          const uint32_t x[8] = {v0[q].x, v0[q].y, v0[q].z, v0[q].w, v1[q].x, v1[q].y, v1[q].z, v1[q].w};
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const uint32_t pos = p0[q] + (r < 4 ? r : 12 + r);
+            if (pos >= sb[q] && pos < se[q]) fold1(x[r]);
+          }
+          for (uint32_t p = p0[q] + 32; p < se[q]; p += 16) {  // long segments (rare)
+            const uint4 v = r4[st[q] + p / 4];
+            const uint32_t y[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (p + r >= sb[q] && p + r < se[q]) fold1(y[r]);
+          }
+        }
       }
+    }
     }
     lds_barrier();
     // T and the filter, one byte of the Redis string (8 bits, MSB first) per lane step
-    uint4* T4 = reinterpret_cast<uint4*>(T + u * BK_BITS);
+    uint4* T4 = reinterpret_cast<uint4*>(T + un * UB);
     uint8_t* fb = reinterpret_cast<uint8_t*>(f0);
-    for (uint32_t q = threadIdx.x; q < BK_BITS / 8; q += TA_T) {
+    for (uint32_t q = threadIdx.x; q < UB / 8; q += TA_T) {
       const uint4 v = t4[q];
       const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
       const uint32_t was = fb[q];  // byte q of the bucket: bits 8q .. 8q+7, bit 8q at 0x80
@@ -176,7 +284,7 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
       fb[q] = (uint8_t)(was | probed);
     }
     lds_barrier();
-    for (uint32_t q = threadIdx.x; q < BK_WORDS; q += TA_T)
+    for (uint32_t q = threadIdx.x; q < UB / 32; q += TA_T)
       if (w0 + q < nwords) bits[w0 + q] = f0[q];
     lds_barrier();  // f0 read out before the next bucket loads it
   }
@@ -334,6 +442,7 @@ __global__ __launch_bounds__(RR_T) void rp_treply_kernel(const uint8_t* __restri
     }
     if (y) out[ka + p_key[e]] = 1;
   }
+  if (threadIdx.x == 0) atomicAdd(fallback + 1, 1u);  // a group resolved in LDS (counted for tests)
 }
 
 // The filter as it was before the chunk: bits with T != NONE were clear.
@@ -405,7 +514,9 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   const uint32_t limit = c->tune.sa_tiny ? 32 : quota;  // tests force the overflow fallback
   if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;
   const uint64_t region_probes = (uint64_t)W * nb1 * quota;
-  const int V2 = c->tune.reply_v == 6 ? 6 : 3;  // rp2: uint4 per lane per tile
+  // rp2: uint4 per lane per tile; 6 (24576-record tiles, one workgroup per CU): bucket segments
+  // twice as long as at 3, apply 27.5 -> 20.9 ms at C3 with rp2 unchanged (11.1 -> 10.8)
+  const int V2 = c->tune.reply_v == 3 ? 3 : 6;
   const uint32_t slots2 = SA2_T * 4 * V2;          // records per rp2 tile
   const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / slots2 + (uint64_t)W * nb1 + 64;  // bound on rp2 tiles
   const uint64_t l2_slots = max_np + 3ull * nb1 * max_nst + 8 * tt_max + 8ull * ncp;  // rp2 output (u32), aligned tiles
@@ -453,7 +564,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     uint32_t* tile_off = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
     uint32_t* tiles = reinterpret_cast<uint32_t*>(take(al(4 * (ncp + 1))));
     uint32_t* used = reinterpret_cast<uint32_t*>(take(al(4ull * W * nb1)));
-    uint32_t* flags = reinterpret_cast<uint32_t*>(take(256));  // [0] sub-region overflow, [1] reply fallback
+    uint32_t* flags = reinterpret_cast<uint32_t*>(take(256));  // [0] sub-region overflow, [1] reply fallback, [2] groups resolved
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
     const uint64_t nst = (m + kst - 1) / kst;
     // contiguous super-tile ranges of S per sa1 workgroup, groups of gs super-tiles
@@ -470,7 +581,7 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       bloom_add_replies_sorted(c, b, dk, d_out + first);
       continue;
     }
-    RSK_HIP(hipMemsetAsync(flags, 0, 8, c->stream));
+    RSK_HIP(hipMemsetAsync(flags, 0, 12, c->stream));
     {
       ProfScope ps(c, "bloom_rp1");
 #define RSK_RP1(F16, KM, KPL)                                                                                       \
@@ -516,8 +627,16 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       ProfScope ps(c, "bloom_rp_apply");
       // 136 KiB of LDS: one workgroup per CU, each looping over its buckets
       const uint32_t ga = (uint32_t)std::min<uint64_t>(nbuckets, cus);
-      hipLaunchKernelGGL(rp_tapply_kernel, dim3(ga), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2, tile_off,
-                         tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg);
+#define RSK_TAP(S, H, G)                                                                                                  \
+  hipLaunchKernelGGL((rp_tapply_kernel<S, H>), dim3(G), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2, tile_off, \
+                     tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg)
+      const uint32_t gh = (uint32_t)std::min<uint64_t>(2 * nbuckets, 2ull * cus);  // half buckets: two per CU
+      if (c->tune.reply_h == 1) RSK_TAP(1, true, gh);
+      else if (c->tune.reply_s == 1) RSK_TAP(1, false, ga);
+      else if (c->tune.reply_s == 4) RSK_TAP(4, false, ga);
+      else if (c->tune.reply_s == -1) RSK_TAP(0, false, ga);
+      else RSK_TAP(2, false, ga);
+#undef RSK_TAP
       RSK_CHECK_LAUNCH("bloom_rp_apply");
     }
     {
@@ -534,11 +653,13 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
 #undef RSK_RPR
       RSK_CHECK_LAUNCH("bloom_rp_reply");
     }
-    uint32_t fb = 0;
-    RSK_HIP(hipMemcpyAsync(c->h_small + 8448, flags + 1, 4, hipMemcpyDeviceToHost, c->stream));
+    uint32_t fb[2] = {0, 0};
+    RSK_HIP(hipMemcpyAsync(c->h_small + 8448, flags + 1, 8, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
-    std::memcpy(&fb, c->h_small + 8448, 4);
-    if (fb) {
+    std::memcpy(fb, c->h_small + 8448, 8);
+    c->rp_pending_groups += fb[1];
+    if (fb[0]) {
+      ++c->rp_fallbacks;
       // A group's pending probes overflowed its LDS tables (many repeated
       // keys inside one group): undo the chunk's bits and let the sort path
       // answer it.

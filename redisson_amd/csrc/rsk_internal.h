@@ -55,7 +55,9 @@ struct Tuning {
   int reply = 0;             // add() replies: 0 auto, 1 group-tag pipeline at any size, -1 the sort path
   uint64_t reply_chunk = 0;  // probes per chunk of the group-tag pipeline (0: 2^33)
   int reply_u = 0;           // rp_treply gather chains per lane: 0 (= 2), 1, 2 or 4
-  int reply_v = 0;           // rp2 tile: uint4 per lane, 0 (= 3) or 6
+  int reply_v = 0;           // rp2 tile: uint4 per lane, 0 (= 6) or 3
+  int reply_s = 0;           // rp_tapply: wave steps whose loads are in flight together, 0 (= 2), 1 or 4
+  int reply_h = 0;           // rp_tapply over half buckets, two workgroups per CU: 0 (= no), 1
   int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
 };
@@ -158,6 +160,9 @@ struct rsk_ctx {
   // call number written by kernels that report "something changed" (no reset)
   uint32_t epoch = 0;
   rsk::Tuning tune;
+  // add()-with-replies counters (rsk_diag_reply_stats): groups whose pending
+  // probes were resolved in LDS, chunks answered by the sort-path fallback
+  uint64_t rp_pending_groups = 0, rp_fallbacks = 0;
   // asynchronous calls: op pool (a completion returns its op under async_mu)
   std::mutex async_mu;
   std::vector<rsk::AsyncOp*> async_free;

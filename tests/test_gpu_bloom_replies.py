@@ -32,7 +32,8 @@ def test_sampled_reply_oracle_matches_sequential(orc):
 CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000), (1000003, 3, 200000), (1000003, 33, 20000),
          (19170117, 7, 300000), (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000),
          (4014142460, 8, 600000)]
-KNOBS = ["reply=1", "reply=1,reply_chunk=300000", "reply=1,sa_tiny=1", "reply=1,sa_parts=13", "reply=1,sa_parts=1"]
+KNOBS = ["reply=1", "reply=1,reply_chunk=300000", "reply=1,sa_tiny=1", "reply=1,sa_parts=13", "reply=1,sa_parts=1",
+         "reply=1,reply_v=3", "reply=1,reply_h=1", "reply=1,reply_s=-1,reply_u=4"]
 
 
 @pytest.mark.gpu
@@ -43,7 +44,8 @@ def test_replies_parity(L, engine, orc, route, size, k, n, knobs):
     (301 and 7,657 slices), k in {1, 2, 3, 5, 7, 8, 9, 16} (33: the sort path); many chunks (each
     answered against the filter the earlier ones left); sub-regions too small
     (the chunk falls back to the sort path); rp2 with 13 parts per coarse bin
-    and with one.  A second batch of variable-length
+    and with one; the kernel forms (rp2 tiles of 12288 records, rp_tapply on
+    half buckets, software-pipelined, 4 gather chains per lane).  A second batch of variable-length
     keys repeats keys of the first and of itself (bits already set before the
     batch, first probes inside it)."""
     from redisson_amd import KeyBatch
@@ -87,6 +89,41 @@ def test_replies_skewed_keys(L, engine, orc, route, knobs):
     assert np.array_equal(got, want)
     assert want[499] == 1 and not want[500:300499].any()
     assert np.array_equal(_bits(L, b, size), ref)
+    L.rsk_bloom_destroy(b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dup", [False, True])
+def test_replies_pending_groups(L, engine, orc, route, dup):
+    """Bits probed more than once by the key group that probed them first:
+    in a 2M-bit filter every 2048-key group has ~50 such bits, and a key whose
+    only candidate bits are among them stays pending until its workgroup has
+    scanned the group again (resolved in LDS, no fallback).  With every key
+    repeated right after itself each group holds ~1000 pending keys, more than
+    its LDS tables take: the chunk's bits are restored from T and the sort path
+    answers it.  Both against the sequential SETBITs."""
+    from redisson_amd import KeyBatch, _lib
+
+    route("reply=1")
+    size, k, n = 2000003, 7, 100000
+    keys = orc.gen_keys16(0x5EED0007, 0, n).reshape(-1, 16)
+    if dup:
+        keys = np.repeat(keys[: n // 2], 2, axis=0)
+    keys = np.ascontiguousarray(keys).reshape(-1)
+    ref = np.zeros((size + 7) // 8, np.uint8)
+    ref[:1000] = 0xA5  # bits set before the batch: no probe on them answers true
+    b = _filter(L, engine, size, k)
+    _lib.check(L.rsk_bloom_import_bits(b, ref.ctypes.data, ref.size))
+    pg0, fb0 = engine.reply_stats()
+    got = _add(L, b, KeyBatch.from_numpy(keys.reshape(-1, 16)))
+    want = orc.bloom_add_batch(ref, size, k, keys, None, 16, keys.size // 16)
+    assert np.array_equal(got, want)
+    assert np.array_equal(_bits(L, b, size), ref)
+    pg1, fb1 = engine.reply_stats()
+    if dup:
+        assert fb1 > fb0  # answered by the fallback
+    else:
+        assert pg1 > pg0 and fb1 == fb0  # pending probes resolved in LDS
     L.rsk_bloom_destroy(b)
 
 
