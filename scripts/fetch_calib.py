@@ -19,7 +19,24 @@ from redisson_amd import _lib, devmem  # noqa: E402
 CASES = [("stream_read", 0, 0), ("segment_256B", 6, 256), ("segment_512B", 6, 512), ("segment_1KiB", 6, 1024)]
 
 
+def gathers():
+    """`fetch_calib.py gathers`: 2^30 random 4-byte gathers (membench mode 1)
+    over a 16 GiB buffer -- FETCH_SIZE per gather for the reply pass's model."""
+    _lib.load()
+    D = _lib.diag()
+    eng = _lib.Engine(0)
+    nbytes, nops = 16 << 30, 1 << 30
+    buf = devmem.DeviceBuffer(eng, nbytes)
+    buf.zero()
+    ms = ctypes.c_double()
+    _lib.check_diag(D.rsk_diag_membench(eng.ctx, 1, buf.ptr, nbytes, nops, ctypes.byref(ms)))
+    print("gather4B buffer=%d ops=%d ms=%.3f gathers/s=%.3e" % (nbytes, nops, ms.value, nops / ms.value * 1e3), flush=True)
+    buf.free()
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "gathers":
+        return gathers()
     _lib.load()
     D = _lib.diag()
     eng = _lib.Engine(0)
