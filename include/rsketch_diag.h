@@ -25,6 +25,8 @@ const char *rsk_diag_last_error(void);
  *   bloom_part    exact-offset insert: 0 auto, 1 at any batch size, -1 never
  *   bloom_chunk   probes per chunk of the slice-routed insert (0 = default)
  *   sa_tiny       1: sub-regions of 32 probes (forces the overflow fallbacks)
+ *   sa_dbg        TIMING ONLY (wrong filter): the insert's sa1 stores each tile's image
+ *                 contiguously and the insert stops after sa1
  *   sa_parts      sa2 / rp2 parts per coarse bin (0 = default)
  *   reply         add() replies: 0 auto, 1 group-tag pipeline at any size, -1 sort path
  *   reply_chunk   probes per chunk of the group-tag pipeline (0 = default)

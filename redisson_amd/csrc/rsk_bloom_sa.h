@@ -172,7 +172,8 @@ template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX, bool TAG
 __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
     FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
-    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow, uint32_t S = 0, uint32_t gs = 1) {
+    uint32_t limit, uint32_t* __restrict__ used, uint32_t* __restrict__ overflow, uint32_t S = 0, uint32_t gs = 1,
+    int dbg = 0) {
   constexpr uint32_t KST = T1 * KPL;
   constexpr int NP = KPL * KMAX;
   constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
@@ -210,8 +211,17 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
   // [wait keys t] [hash t] [loads t+1] [stores t-1] [scan, scatter t] leaves
   // the scan and scatter between the stores and the next wait, and the loads
   // of t + 1 are never in the wait that precedes their own issue.
+  uint64_t wst = 0;  // dbg: the super-tile being written out
   auto write_out = [&](uint32_t total4) {
     const uint4* img4 = reinterpret_cast<const uint4*>(img);
+    if (dbg) {  // TIMING ONLY (the host stops after this pass): each tile's image stored contiguously
+      u32x4* o4 = reinterpret_cast<u32x4*>(region + wst * IMG);
+      for (uint32_t g = threadIdx.x; g < total4; g += T1) {
+        const uint4 v = img4[g];
+        o4[g] = u32x4{v.x, v.y, v.z, v.w};
+      }
+      return;
+    }
     for (uint32_t g = threadIdx.x; g < total4; g += T1) {
       const uint32_t d = dst[ibin[g]];
       if (d != INVALID) {
@@ -269,6 +279,7 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
     }
     if (FIXED16) fetch(st + s_step);
     write_out(pend4);  // tile t - 1
+    wst = st;
     lds_barrier();  // (A) every rank taken, the previous image written out
     // wave 0: bin starts and run destinations (runs of L probes take
     // L4 = round_up(L, RG) slots, the tail rec_pad): image position j of bin b

@@ -429,12 +429,14 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     if (keys.offsets) dk.offsets = keys.offsets + first;
     else dk.data = keys.data + first * keys.fixed_len;
     RSK_HIP(hipMemsetAsync(overflow, 0, 4, c->stream));
+    // the timing-only contiguous form needs nst whole images in the region
+    const int sa_dbg = c->tune.sa_dbg && nst * (kst * kmax + 1024) <= region_probes ? 1 : 0;
     {
       ProfScope ps(c, "bloom_st1");
 #define RSK_SA1(F16, KM, ...)                                                                                   \
   hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint32_t, ##__VA_ARGS__>), dim3(Wc), dim3(T1), 0, c->stream, \
                      dk.data, dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit,  \
-                     used, overflow)
+                     used, overflow, 0u, 1u, sa_dbg)
       if (kpl4) RSK_SA1(true, 8, 4);
       else if (f16 && kmax == 8) RSK_SA1(true, 8);
       else if (f16) RSK_SA1(true, 16);
@@ -443,6 +445,7 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
 #undef RSK_SA1
       RSK_CHECK_LAUNCH("bloom_sa1");
     }
+    if (sa_dbg) continue;  // timing-only sa1 form: its output is not the sub-regions
     {
       ProfScope ps(c, "bloom_st_mid");
       hipLaunchKernelGGL(sah_size_kernel, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, used, Wc, nb1, P, ncp,

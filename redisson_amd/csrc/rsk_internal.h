@@ -50,6 +50,7 @@ struct Tuning {
   int bloom_stream = 0;      // slice-routed insert (st1/apply, sa1/sa2/apply): 0 auto (>= 2^22 probes), 1 any size, -1 never
   int bloom_part = 0;        // exact-offset insert (rsk_bloom_part.hip): 0 auto, 1 any size, -1 never
   uint64_t bloom_chunk = 0;  // probes per chunk of the slice-routed insert (0: 2^33)
+  int sa_dbg = 0;            // TIMING ONLY: the insert's sa1 stores each tile contiguously and the insert stops there
   int sa_tiny = 0;           // sub-regions of 32 probes: forces the overflow fallbacks
   uint32_t sa_parts = 0;     // sa2 / rp2 parts per coarse bin (0: 4 x CUs / bins)
   int reply = 0;             // add() replies: 0 auto, 1 group-tag pipeline at any size, -1 the sort path
