@@ -31,12 +31,13 @@ const char *rsk_diag_last_error(void);
  *   reply         add() replies: 0 auto, 1 group-tag pipeline at any size, -1 sort path
  *   reply_chunk   probes per chunk of the group-tag pipeline (0 = default)
  *   reply_u       rp_treply keys (gather chains) per lane: 0 (= 2), 1, 2, 4
- *   reply_v       rp2 tile: uint4 loads per lane, 0 (= 6) or 3
- *   reply_s       rp_tapply: wave steps whose segment loads are issued together, 0 (= 2), 1, 4;
- *                 -1: software-pipelined (next step's loads during this step's folds)
+ *   reply_v       rp2 tile: uint4 loads per lane, 0 (= 8), 3 or 6
+ *   reply_s       rp_tapply: wave steps whose segment loads are issued together, 0 (= 2), 1, 4
  *   reply_dbg     TIMING ONLY (wrong replies and T): rp_tapply without its
  *                 folds (bit 0) / without its T stores (bit 1)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
+ *   gpart_dbg     TIMING ONLY (wrong pool): hll_gpart1 writes each block's runs
+ *                 block-major and the grouped add stops after it
  *   reset         every route back to automatic
  * Every route but reply_dbg gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);

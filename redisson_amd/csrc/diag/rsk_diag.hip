@@ -163,9 +163,9 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "reply_u") t.reply_u = (int)value;
     else if (k == "reply_v") t.reply_v = (int)value;
     else if (k == "reply_dbg") t.reply_dbg = (int)value;
-    else if (k == "reply_h") t.reply_h = (int)value;
     else if (k == "reply_s") t.reply_s = (int)value;
     else if (k == "gpart") t.gpart = (int)value;
+    else if (k == "gpart_dbg") t.gpart_dbg = (int)value;
     else if (k == "reset") t = Tuning{};
     else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};
   });

@@ -93,140 +93,93 @@ RSK_DEV void tap_fold(uint32_t* tt, uint32_t rec) {
 // tile g + l's bounds; then four lanes take one tile's segment (two aligned
 // uint4 each = 32 record slots, the rest of a long segment in a loop), 16
 // segments per wave step, the loads of S steps issued before the first of
-// them is folded (one workgroup per CU: the waves' loads in flight are what
-// hides the latency).  A record is folded by an LDS read and a CAS (retried
-// when another record took the word).  Consecutive buckets run on one XCD
-// (xcd_slot): the 8 buckets of a slice share their segments' cache lines in
-// its L2.  (Measured at C3, rp2 tiles of 24576 records, S = 1: 20.3-20.9 ms;
-// a step's 8 records folded as a batch -- every read, then every CAS --
-// 21.9 ms; two steps' loads and a 16-record batch spilled 27 VGPRs, 26.0 ms.)
-template <int S, bool HALF = false>
-__global__ __launch_bounds__(TA_T, HALF ? 8 : 4) void rp_tapply_kernel(const uint32_t* __restrict__ recs,
+// them is folded.  A record is folded by an LDS read and a CAS (retried when
+// another record took the word).  One workgroup per CU, so the latencies at
+// a bucket's start are exposed: the next bucket's filter words and each
+// wave's first 64 tile bounds are loaded during this bucket's write-out.
+// Consecutive buckets run on one XCD (xcd_slot): the 8 buckets of a slice
+// share their segments' cache lines in its L2.  (Measured at C3, rp2 tiles of
+// 24576 records: S = 1 20.9 ms, 2 20.5, 4 21.3; a step's 8 records folded as
+// a batch -- every read, then every CAS -- 21.9; a software pipeline, next
+// step's loads during this step's folds, 21.8; half buckets, two workgroups
+// per CU, 26.5.)
+template <int S, int SU = 2>
+__global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restrict__ recs,
                                                          const uint4* __restrict__ hp, uint64_t hp_stride,
                                                          uint32_t f2, const uint32_t* __restrict__ tb,
                                                          const uint32_t* __restrict__ tile_off,
                                                          const uint32_t* __restrict__ ntiles, uint32_t P,
                                                          uint64_t nbuckets, uint32_t* __restrict__ bits,
                                                          uint64_t nwords, uint16_t* __restrict__ T, int dbg) {
-  // HALF: a unit is half a bucket (2^15 bits, 64 KiB of entries: two
-  // workgroups per CU); both halves read the bucket's segments (one L2 fetch)
-  // and each folds the records of its own half.
-  constexpr uint32_t UB = HALF ? BK_BITS / 2 : BK_BITS;  // bits per unit
-  __shared__ __attribute__((aligned(16))) uint32_t tt[UB / 2];
-  __shared__ __attribute__((aligned(16))) uint32_t f0[UB / 32];
+  __shared__ __attribute__((aligned(16))) uint32_t tt[BK_BITS / 2];
+  __shared__ __attribute__((aligned(16))) uint32_t f0[BK_BITS / 32];
+  constexpr uint32_t FW = BK_BITS / 32 / TA_T;  // filter words per lane (2)
   const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   constexpr uint32_t NW = TA_T / 64;
   const uint4* r4 = reinterpret_cast<const uint4*>(recs);
-  uint32_t hsel = 0;  // HALF: the unit's half (record offset bit 15)
   auto fold1 = [&](uint32_t x) {
-    if (HALF) {
-      if (((x >> 15) & 1u) != hsel) return;
-      x &= ~0x8000u;
-    }
-    if (dbg & 1) tt[x & (UB / 2 - 1)] |= x >> 31;  // timing only: one plain LDS op per record
+    if (dbg & 1) tt[x & 0x7FFFu] |= x >> 31;  // timing only: one plain LDS op per record
     else tap_fold(tt, x);
   };
-  auto fold_step = [&](const auto& l) {
-    const uint32_t x[8] = {l.v0.x, l.v0.y, l.v0.z, l.v0.w, l.v1.x, l.v1.y, l.v1.z, l.v1.w};
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const uint32_t pos = l.p0 + (r < 4 ? r : 12 + r);
-      if (pos >= l.sb && pos < l.se) fold1(x[r]);
-    }
-    for (uint32_t p = l.p0 + 32; p < l.se; p += 16) {  // long segments (rare)
-      const uint4 v = r4[l.st + p / 4];
-      const uint32_t y[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (p + r >= l.sb && p + r < l.se) fold1(y[r]);
+  // a bucket's place in the rp2 output
+  struct Bk {
+    uint32_t e, ta, te;
+    const uint4* hrow;
+    const uint32_t* erow;
+  };
+  auto bucket = [&](uint64_t u) {
+    const uint32_t s = (uint32_t)(u >> 3), c = s >> f2, f = s & ((1u << f2) - 1);
+    Bk k;
+    k.e = (uint32_t)(u & 7);
+    k.hrow = hp + (uint64_t)f * hp_stride;
+    k.erow = reinterpret_cast<const uint32_t*>(hp + (uint64_t)(f + 1) * hp_stride);
+    k.ta = tile_off[(uint64_t)c * P];
+    k.te = tile_off[(uint64_t)c * P + P - 1] + ntiles[(uint64_t)c * P + P - 1];
+    return k;
+  };
+  // lane's tile g + lane: segment bounds of the bucket and the tile's first uint4
+  auto hload = [&](const Bk& k, uint32_t g, uint32_t& beg, uint32_t& end, uint32_t& tbl) {
+    const uint32_t t = g + lane;
+    beg = end = tbl = 0;
+    if (t < k.te) {
+      const uint4 v = k.hrow[t];
+      const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
+      beg = (hw[k.e >> 1] >> (16 * (k.e & 1))) & 0xFFFFu;
+      end = k.e < 7 ? (hw[(k.e + 1) >> 1] >> (16 * ((k.e + 1) & 1))) & 0xFFFFu : k.erow[4ull * t] & 0xFFFFu;
+      tbl = tb[t];
     }
   };
-  const uint64_t nunits = HALF ? 2 * nbuckets : nbuckets;
-  for (uint64_t un = xcd_slot(blockIdx.x, gridDim.x); un < nunits; un += gridDim.x) {
-    const uint64_t u = HALF ? un >> 1 : un;
-    hsel = HALF ? (uint32_t)(un & 1) : 0u;
+  uint64_t u = xcd_slot(blockIdx.x, gridDim.x);
+  // prefetched for bucket u: its filter words and this wave's first tile bounds
+  uint32_t pfw[FW], pbeg = 0, pend = 0, ptb = 0;
+  Bk k{};
+  if (u < nbuckets) {
+    k = bucket(u);
+#pragma unroll
+    for (uint32_t i = 0; i < FW; ++i) {
+      const uint64_t q = u * (BK_BITS / 32) + threadIdx.x + i * TA_T;
+      pfw[i] = q < nwords ? bits[q] : 0u;
+    }
+    hload(k, k.ta + 64 * w, pbeg, pend, ptb);
+  }
+  for (; u < nbuckets; u += gridDim.x) {
     uint4* t4 = reinterpret_cast<uint4*>(tt);
-    for (uint32_t q = threadIdx.x; q < UB / 8; q += TA_T) t4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    const uint64_t w0 = un * (UB / 32);  // the unit's first filter word
-    for (uint32_t q = threadIdx.x; q < UB / 32; q += TA_T) f0[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
+    for (uint32_t q = threadIdx.x; q < BK_BITS / 8; q += TA_T) t4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+    for (uint32_t i = 0; i < FW; ++i) f0[threadIdx.x + i * TA_T] = pfw[i];
     lds_barrier();
-    const uint32_t s = (uint32_t)(u >> 3), e = (uint32_t)(u & 7), c = s >> f2, f = s & ((1u << f2) - 1);
-    const uint4* hrow = hp + (uint64_t)f * hp_stride;
-    const uint32_t* erow = reinterpret_cast<const uint32_t*>(hp + (uint64_t)(f + 1) * hp_stride);
-    const uint32_t ta = tile_off[(uint64_t)c * P];
-    const uint32_t te = tile_off[(uint64_t)c * P + P - 1] + ntiles[(uint64_t)c * P + P - 1];
-    if constexpr (S == 0) {  // software-pipelined: step k + 1's loads (and group i + 1's bounds) in flight during step k's folds
-      struct Hd {
-        uint32_t beg, end, tbl, g, ng;
-      };
-      auto hload = [&](uint32_t gg) {
-        Hd h{0, 0, 0, gg, gg < te ? (te - gg < 64 ? te - gg : 64) : 0};
-        const uint32_t t = gg + lane;
-        if (t < te) {
-          const uint4 v = hrow[t];
-          const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
-          h.beg = (hw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-          h.end = e < 7 ? (hw[(e + 1) >> 1] >> (16 * ((e + 1) & 1))) & 0xFFFFu : erow[4ull * t] & 0xFFFFu;
-          h.tbl = tb[t];
-        }
-        return h;
-      };
-      struct Ld {
-        uint4 v0, v1;
-        uint32_t sb, se, st, p0;
-      };
-      auto sload = [&](const Hd& h, uint32_t j) {
-        Ld l;
-        const uint32_t si = j + (lane >> 2), src = si < 63 ? si : 63;
-        l.sb = shfl_u32(h.beg, src);
-        const uint32_t se0 = shfl_u32(h.end, src);
-        l.st = shfl_u32(h.tbl, src);
-        l.se = si < h.ng ? se0 : l.sb;
-        l.p0 = (l.sb & ~3u) + 4 * (lane & 3);
-        l.v0 = l.p0 < l.se ? r4[l.st + l.p0 / 4] : make_uint4(0, 0, 0, 0);
-        l.v1 = l.p0 + 16 < l.se ? r4[l.st + l.p0 / 4 + 4] : make_uint4(0, 0, 0, 0);
-        return l;
-      };
-      uint32_t g = ta + 64 * w;
-      if (g < te) {
-        Hd hc = hload(g), hn = hload(g + 64 * NW);
-        uint32_t j = 0;
-        Ld la = sload(hc, 0);
-        while (true) {
-          // the next step: (same group, j + 16) or (next group, 0)
-          bool more = true, cross = false;
-          uint32_t jn = j + 16;
-          if (jn >= hc.ng) {
-            jn = 0;
-            cross = true;
-            more = hn.ng > 0;
-          }
-          Ld lb;
-          if (more) lb = sload(cross ? hn : hc, jn);
-          fold_step(la);
-          if (!more) break;
-          if (cross) {
-            hc = hn;
-            hn = hload(hc.g + 64 * NW);
-          }
-          j = jn;
-          la = lb;
-        }
+    for (uint32_t g = k.ta + 64 * w; g < k.te; g += 64 * NW) {
+      uint32_t beg, end, tbl;
+      if (g == k.ta + 64 * w) {
+        beg = pbeg;
+        end = pend;
+        tbl = ptb;
+      } else {
+        hload(k, g, beg, end, tbl);
       }
-    } else {
-    for (uint32_t g = ta + 64 * w; g < te; g += 64 * NW) {
-      const uint32_t t = g + lane;
-      uint32_t beg = 0, end = 0, tbl = 0;
-      if (t < te) {
-        const uint4 v = hrow[t];
-        const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
-        beg = (hw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-        end = e < 7 ? (hw[(e + 1) >> 1] >> (16 * ((e + 1) & 1))) & 0xFFFFu : erow[4ull * t] & 0xFFFFu;
-        tbl = tb[t];
-      }
-      const uint32_t ng = te - g < 64 ? te - g : 64;
+      const uint32_t ng = k.te - g < 64 ? k.te - g : 64;
       for (uint32_t j0 = 0; j0 < ng; j0 += 16 * S) {
-        uint4 v0[S], v1[S];
+        uint4 v[S][SU];
         uint32_t sb[S], se[S], st[S], p0[S];
 #pragma unroll
         for (int q = 0; q < S; ++q) {
@@ -237,18 +190,22 @@ __global__ __launch_bounds__(TA_T, HALF ? 8 : 4) void rp_tapply_kernel(const uin
           se[q] = si < ng ? se0 : sb[q];
           p0[q] = (sb[q] & ~3u) + 4 * (lane & 3);
           // plain loads: the slice's 8 buckets (on one XCD at about the same time) share these lines in L2
-          v0[q] = p0[q] < se[q] ? r4[st[q] + p0[q] / 4] : make_uint4(0, 0, 0, 0);
-          v1[q] = p0[q] + 16 < se[q] ? r4[st[q] + p0[q] / 4 + 4] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < SU; ++i)
+            v[q][i] = p0[q] + 16 * i < se[q] ? r4[st[q] + p0[q] / 4 + 4 * i] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < S; ++q) {
-          const uint32_t x[8] = {v0[q].x, v0[q].y, v0[q].z, v0[q].w, v1[q].x, v1[q].y, v1[q].z, v1[q].w};
 #pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const uint32_t pos = p0[q] + (r < 4 ? r : 12 + r);
-            if (pos >= sb[q] && pos < se[q]) fold1(x[r]);
+          for (int i = 0; i < SU; ++i) {
+            const uint32_t x[4] = {v[q][i].x, v[q][i].y, v[q][i].z, v[q][i].w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t pos = p0[q] + 16 * i + r;
+              if (pos >= sb[q] && pos < se[q]) fold1(x[r]);
+            }
           }
-          for (uint32_t p = p0[q] + 32; p < se[q]; p += 16) {  // long segments (rare)
+          for (uint32_t p = p0[q] + 16 * SU; p < se[q]; p += 16) {  // long segments (rare)
             const uint4 v = r4[st[q] + p / 4];
             const uint32_t y[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -258,33 +215,44 @@ __global__ __launch_bounds__(TA_T, HALF ? 8 : 4) void rp_tapply_kernel(const uin
         }
       }
     }
+    // the next bucket's filter words and first tile bounds, in flight during the write-out
+    const uint64_t un = u + gridDim.x;
+    const uint64_t w0 = u * (BK_BITS / 32);
+    if (un < nbuckets) {
+      const Bk kn = bucket(un);
+#pragma unroll
+      for (uint32_t i = 0; i < FW; ++i) {
+        const uint64_t q = un * (BK_BITS / 32) + threadIdx.x + i * TA_T;
+        pfw[i] = q < nwords ? bits[q] : 0u;
+      }
+      hload(kn, kn.ta + 64 * w, pbeg, pend, ptb);
+      k = kn;
     }
     lds_barrier();
     // T and the filter, one byte of the Redis string (8 bits, MSB first) per lane step
-    uint4* T4 = reinterpret_cast<uint4*>(T + un * UB);
+    uint4* T4 = reinterpret_cast<uint4*>(T + u * BK_BITS);
     uint8_t* fb = reinterpret_cast<uint8_t*>(f0);
-    for (uint32_t q = threadIdx.x; q < UB / 8; q += TA_T) {
+    for (uint32_t q = threadIdx.x; q < BK_BITS / 8; q += TA_T) {
       const uint4 v = t4[q];
       const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
       const uint32_t was = fb[q];  // byte q of the bucket: bits 8q .. 8q+7, bit 8q at 0x80
+      // two entries per dword: entry 2h (low half) is bit 7 - 2h of the byte, 2h + 1 bit 6 - 2h;
+      // a bit set before the batch turns its entry into NONE (all ones: an OR)
       uint32_t probed = 0, o[4];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const uint32_t bit = 2 * h + j, ent = (hw[h] >> (16 * j)) & 0xFFFFu;
-          probed |= (ent != T_NONE ? 1u : 0u) << (7 - bit);
-          r |= (((was >> (7 - bit)) & 1u) ? T_NONE : ent) << (16 * j);
-        }
-        o[h] = r;
+        const uint32_t wb = was >> (6 - 2 * h);  // bit 1: entry 2h, bit 0: entry 2h + 1
+        o[h] = hw[h] | ((wb & 2u) ? 0x0000FFFFu : 0u) | ((wb & 1u) ? 0xFFFF0000u : 0u);
+        const uint32_t nx = ~hw[h];  // a half is nonzero iff its entry is not NONE
+        probed |= ((nx & 0xFFFFu) ? 2u : 0u) << (6 - 2 * h);
+        probed |= ((nx >> 16) ? 1u : 0u) << (6 - 2 * h);
       }
       u32x4 ov = {o[0], o[1], o[2], o[3]};
       if (!(dbg & 2)) __builtin_nontemporal_store(ov, reinterpret_cast<u32x4*>(T4 + q));  // read back by rp_treply's gathers only
       fb[q] = (uint8_t)(was | probed);
     }
     lds_barrier();
-    for (uint32_t q = threadIdx.x; q < UB / 32; q += TA_T)
+    for (uint32_t q = threadIdx.x; q < BK_BITS / 32; q += TA_T)
       if (w0 + q < nwords) bits[w0 + q] = f0[q];
     lds_barrier();  // f0 read out before the next bucket loads it
   }
@@ -515,8 +483,9 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
   if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;
   const uint64_t region_probes = (uint64_t)W * nb1 * quota;
   // rp2: uint4 per lane per tile; 6 (24576-record tiles, one workgroup per CU): bucket segments
-  // twice as long as at 3, apply 27.5 -> 20.9 ms at C3 with rp2 unchanged (11.1 -> 10.8)
-  const int V2 = c->tune.reply_v == 3 ? 3 : 6;
+  // twice as long as at 3, apply 27.5 -> 20.9 ms at C3 with rp2 unchanged (11.1 -> 10.8); 8
+  // (32768): rp2 10.9 -> 10.5, apply 20.6 -> 20.3
+  const int V2 = c->tune.reply_v == 3 ? 3 : c->tune.reply_v == 6 ? 6 : 8;
   const uint32_t slots2 = SA2_T * 4 * V2;          // records per rp2 tile
   const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / slots2 + (uint64_t)W * nb1 + 64;  // bound on rp2 tiles
   const uint64_t l2_slots = max_np + 3ull * nb1 * max_nst + 8 * tt_max + 8ull * ncp;  // rp2 output (u32), aligned tiles
@@ -615,7 +584,10 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     }
     {
       ProfScope ps(c, "bloom_rp2");
-      if (V2 == 6)
+      if (V2 == 8)
+        hipLaunchKernelGGL((bloom_sa2h_kernel<uint32_t, 8>), dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used,
+                           Wl, nb1, P, nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2, Gw);
+      else if (V2 == 6)
         hipLaunchKernelGGL((bloom_sa2h_kernel<uint32_t, 6>), dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used,
                            Wl, nb1, P, nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2, Gw);
       else
@@ -627,15 +599,17 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       ProfScope ps(c, "bloom_rp_apply");
       // 136 KiB of LDS: one workgroup per CU, each looping over its buckets
       const uint32_t ga = (uint32_t)std::min<uint64_t>(nbuckets, cus);
-#define RSK_TAP(S, H, G)                                                                                                  \
-  hipLaunchKernelGGL((rp_tapply_kernel<S, H>), dim3(G), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2, tile_off, \
+#define RSK_TAP(S)                                                                                                \
+  hipLaunchKernelGGL(rp_tapply_kernel<S>, dim3(ga), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2, tile_off, \
                      tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg)
-      const uint32_t gh = (uint32_t)std::min<uint64_t>(2 * nbuckets, 2ull * cus);  // half buckets: two per CU
-      if (c->tune.reply_h == 1) RSK_TAP(1, true, gh);
-      else if (c->tune.reply_s == 1) RSK_TAP(1, false, ga);
-      else if (c->tune.reply_s == 4) RSK_TAP(4, false, ga);
-      else if (c->tune.reply_s == -1) RSK_TAP(0, false, ga);
-      else RSK_TAP(2, false, ga);
+#define RSK_TAP2(S, SU)                                                                                              \
+  hipLaunchKernelGGL((rp_tapply_kernel<S, SU>), dim3(ga), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2,     \
+                     tile_off, tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg)
+      if (V2 == 8) RSK_TAP2(2, 3);  // segments of ~32 records: 48 slots per four lanes
+      else if (c->tune.reply_s == 1) RSK_TAP(1);
+      else if (c->tune.reply_s == 4) RSK_TAP(4);
+      else RSK_TAP(2);
+#undef RSK_TAP2
 #undef RSK_TAP
       RSK_CHECK_LAUNCH("bloom_rp_apply");
     }

@@ -56,11 +56,11 @@ struct Tuning {
   int reply = 0;             // add() replies: 0 auto, 1 group-tag pipeline at any size, -1 the sort path
   uint64_t reply_chunk = 0;  // probes per chunk of the group-tag pipeline (0: 2^33)
   int reply_u = 0;           // rp_treply gather chains per lane: 0 (= 2), 1, 2 or 4
-  int reply_v = 0;           // rp2 tile: uint4 per lane, 0 (= 6) or 3
+  int reply_v = 0;           // rp2 tile: uint4 per lane, 0 (= 8), 3 or 6
   int reply_s = 0;           // rp_tapply: wave steps whose loads are in flight together, 0 (= 2), 1 or 4
-  int reply_h = 0;           // rp_tapply over half buckets, two workgroups per CU: 0 (= no), 1
   int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
+  int gpart_dbg = 0;         // TIMING ONLY: hll_gpart1 writes block-major runs and the grouped add stops there
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the

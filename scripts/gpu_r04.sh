@@ -26,6 +26,11 @@ for p in ${PART//,/ }; do
       step rp_stats 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_stats -o run -- $R || exit 1
       step rp_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/rp_fetch -o run -- $R || exit 1
       step rp_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/rp_write -o run -- $R || exit 1 ;;
+    rpsq)  # SQ counters of the reply pipeline's kernels (two PMC passes of 8 SQ counters)
+      R="python3 scripts/reply_profile.py 1000000000 1"
+      rm -rf gpurun_out/rpsq_a gpurun_out/rpsq_b
+      step rpsq_a 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS --output-format csv -d gpurun_out/rpsq_a -o run -- $R || exit 1
+      step rpsq_b 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM --output-format csv -d gpurun_out/rpsq_b -o run -- $R || exit 1 ;;
     gcal)  # FETCH_SIZE of random gathers of known count (membench modes 1: 4 B gathers)
       rm -rf gpurun_out/gcal_fetch
       step gcal 120 python3 scripts/fetch_calib.py gathers || exit 1

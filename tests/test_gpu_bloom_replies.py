@@ -33,7 +33,7 @@ CASES = [(1, 2, 5000), (729, 5, 20000), (95851, 7, 50000), (1000003, 1, 50000), 
          (19170117, 7, 300000), (157298745, 7, 400000), (157298745, 9, 200000), (157298745, 16, 150000),
          (4014142460, 8, 600000)]
 KNOBS = ["reply=1", "reply=1,reply_chunk=300000", "reply=1,sa_tiny=1", "reply=1,sa_parts=13", "reply=1,sa_parts=1",
-         "reply=1,reply_v=3", "reply=1,reply_h=1", "reply=1,reply_s=-1,reply_u=4"]
+         "reply=1,reply_v=3", "reply=1,reply_v=6", "reply=1,reply_s=4,reply_u=4", "reply=1,reply_s=1,reply_u=1"]
 
 
 @pytest.mark.gpu
@@ -45,7 +45,7 @@ def test_replies_parity(L, engine, orc, route, size, k, n, knobs):
     answered against the filter the earlier ones left); sub-regions too small
     (the chunk falls back to the sort path); rp2 with 13 parts per coarse bin
     and with one; the kernel forms (rp2 tiles of 12288 records, rp_tapply on
-    half buckets, software-pipelined, 4 gather chains per lane).  A second batch of variable-length
+    one or four steps of segment loads per fold, 1 or 4 gather chains per lane).  A second batch of variable-length
     keys repeats keys of the first and of itself (bits already set before the
     batch, first probes inside it)."""
     from redisson_amd import KeyBatch
