@@ -25,6 +25,7 @@ const char *rsk_diag_last_error(void);
  *   bloom_part    exact-offset insert: 0 auto, 1 at any batch size, -1 never
  *   bloom_chunk   probes per chunk of the slice-routed insert (0 = default)
  *   sa_tiny       1: sub-regions of 32 probes (forces the overflow fallbacks)
+ *   sa_v          the insert's sa2h tile: uint4 loads per lane, 0 (= 3), 6 or 8
  *   sa_dbg        TIMING ONLY (wrong filter): the insert's sa1 stores each tile's image
  *                 contiguously and the insert stops after sa1
  *   sa_parts      sa2 / rp2 parts per coarse bin (0 = default)
@@ -36,10 +37,8 @@ const char *rsk_diag_last_error(void);
  *   reply_dbg     TIMING ONLY (wrong replies and T): rp_tapply without its
  *                 folds (bit 0) / without its T stores (bit 1)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
- *   gpart_dbg     TIMING ONLY (wrong pool): hll_gpart1 writes each block's runs
- *                 block-major and the grouped add stops after it
  *   reset         every route back to automatic
- * Every route but reply_dbg gives bit-identical results; they differ in speed only. */
+ * Every route but sa_dbg and reply_dbg gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
 
 /* add()-with-replies counters of a context since it was created: key groups

@@ -393,7 +393,9 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
   const uint64_t region_probes = (uint64_t)W * nb1 * quota;
   if (q64 >= (1ull << 31) || (uint64_t)nb1 * quota >= (1ull << 32)) return false;  // u32 offsets -> exact-offset pipeline
   const uint32_t nbk = nb2 << SAH_SUB;  // sa2h buckets per coarse bin
-  const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / SA2_SLOTS + (uint64_t)W * nb1 + 64;  // bound on sa2 tiles
+  const int V2 = c->tune.sa_v == 6 || c->tune.sa_v == 8 ? c->tune.sa_v : SA2_V;  // sa2h: uint4 per lane per tile
+  const uint32_t slots2 = SA2_T * 4 * V2;
+  const uint64_t tt_max = (max_np + 3ull * nb1 * max_nst) / slots2 + (uint64_t)W * nb1 + 64;  // bound on sa2 tiles
   const uint64_t l2_slots = max_np + 3ull * nb1 * max_nst + 8 * tt_max + 8ull * ncp;  // sa2h output (u16), aligned tiles
   const uint64_t hp_bytes = al(16 * tt_max * (nb2 + 1));  // bucket-start rows: nb2 + 1 rows of tt_max uint4
   // apply's 32-bit uint4 indices of the records
@@ -449,15 +451,20 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
     {
       ProfScope ps(c, "bloom_st_mid");
       hipLaunchKernelGGL(sah_size_kernel, dim3((ncp + 255) / 256), dim3(256), 0, c->stream, used, Wc, nb1, P, ncp,
-                         tot, bud);
+                         tot, bud, slots2);
       RSK_CHECK_LAUNCH("bloom_sa_size");
       hipLaunchKernelGGL(st_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, tot, bud, ncp, reg_off, tile_off);
       RSK_CHECK_LAUNCH("bloom_st_offsets");
     }
     {
       ProfScope ps(c, "bloom_st2");
-      hipLaunchKernelGGL(bloom_sa2h_kernel<uint16_t>, dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, nb1, P,
-                         nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2);
+#define RSK_SA2H(V)                                                                                              \
+  hipLaunchKernelGGL((bloom_sa2h_kernel<uint16_t, V>), dim3(ncp), dim3(SA2_T), 0, c->stream, region, quota, used, Wc, \
+                     nb1, P, nbk, reg_off, tile_off, tiles, l2, hp, tt_max, tb2)
+      if (V2 == 8) RSK_SA2H(8);
+      else if (V2 == 6) RSK_SA2H(6);
+      else RSK_SA2H(SA2_V);
+#undef RSK_SA2H
       RSK_CHECK_LAUNCH("bloom_sa2");
     }
     {

@@ -119,19 +119,12 @@ __global__ __launch_bounds__(GP_T) void hll_gcount_kernel(const uint32_t* __rest
 __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict__ keys,
                                                         const uint32_t* __restrict__ groups, uint64_t n, uint64_t per,
                                                         uint64_t G, uint32_t nbins, const uint32_t* __restrict__ start,
-                                                        uint32_t* __restrict__ out, int dbg = 0) {
+                                                        uint32_t* __restrict__ out) {
   __shared__ SortLds<GP_TILE> L;
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
   L.hist[threadIdx.x] = 0;
   if (threadIdx.x < nbins) L.cur[threadIdx.x] = start[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
-  if (dbg) {  // TIMING ONLY (the host stops after this pass): block-major runs, inside the block's own window
-    const uint64_t ix = (uint64_t)threadIdx.x * gridDim.x + blockIdx.x;
-    const uint32_t cnt = threadIdx.x < nbins ? start[ix + 1] - start[ix] : 0u;
-    uint32_t total;
-    const uint32_t pre = block_excl_scan256(cnt, &total);
-    if (threadIdx.x < nbins) L.cur[threadIdx.x] = (uint32_t)(blockIdx.x * per) + pre;
-  }
   for (uint64_t k0 = begin; k0 < end; k0 += GP_TILE) {
     uint4 v[GP_E];
     uint32_t g[GP_E];
@@ -772,11 +765,9 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
     }
     {
       ProfScope ps(c, "hll_gpart1");
-      hipLaunchKernelGGL(hll_gpart1_kernel, dim3(G1), dim3(PT), 0, c->stream, kd, gd, m, per, G, nbins1, off1, buf_a,
-                         c->tune.gpart_dbg);
+      hipLaunchKernelGGL(hll_gpart1_kernel, dim3(G1), dim3(PT), 0, c->stream, kd, gd, m, per, G, nbins1, off1, buf_a);
       RSK_CHECK_LAUNCH("hll_gpart1");
     }
-    if (c->tune.gpart_dbg) continue;  // timing-only gpart1 form: its output is not the bin-major runs
     {
       ProfScope ps(c, "hll_gpart2");
       RSK_HIP(hipMemsetAsync(cnt2, 0, 4 * ncnt2, c->stream));

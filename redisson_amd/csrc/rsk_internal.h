@@ -51,6 +51,7 @@ struct Tuning {
   int bloom_part = 0;        // exact-offset insert (rsk_bloom_part.hip): 0 auto, 1 any size, -1 never
   uint64_t bloom_chunk = 0;  // probes per chunk of the slice-routed insert (0: 2^33)
   int sa_dbg = 0;            // TIMING ONLY: the insert's sa1 stores each tile contiguously and the insert stops there
+  int sa_v = 0;              // the insert's sa2h tile: uint4 per lane, 0 (= 3), 6 or 8
   int sa_tiny = 0;           // sub-regions of 32 probes: forces the overflow fallbacks
   uint32_t sa_parts = 0;     // sa2 / rp2 parts per coarse bin (0: 4 x CUs / bins)
   int reply = 0;             // add() replies: 0 auto, 1 group-tag pipeline at any size, -1 the sort path
@@ -60,7 +61,6 @@ struct Tuning {
   int reply_s = 0;           // rp_tapply: wave steps whose loads are in flight together, 0 (= 2), 1 or 4
   int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
-  int gpart_dbg = 0;         // TIMING ONLY: hll_gpart1 writes block-major runs and the grouped add stops there
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the
