@@ -167,11 +167,13 @@ def test_replies_match_sort_path_c3_filter(L, engine, route):
 
 
 @pytest.mark.gpu
-def test_c3_full_size_replies(L, engine, orc):
+def test_c3_full_size_replies(L, engine, orc, route):
     """BASELINE configs[2] with the reference's add() semantics at full size:
     1B keys in one add() call into the 9,585,058,377-bit filter (k = 7, one
-    chunk); 200,000 sampled replies equal the oracle's (exact minimum
-    sequence number over the whole stream for the sample's bits), and the bit string equals the reply-less insert's."""
+    chunk); all 1B replies equal the sort path's (an independent algorithm: a
+    stable radix sort of (bit, sequence)), 200,000 sampled replies equal the
+    oracle's (exact minimum sequence number over the whole stream for the
+    sample's bits), and the bit string equals the reply-less insert's."""
     import os
 
     from redisson_amd import _lib, devmem
@@ -182,8 +184,17 @@ def test_c3_full_size_replies(L, engine, orc):
     ks = ins.keys_fixed(n, 16).as_struct()
     b = _filter(L, engine, size, k)
     out = devmem.DeviceBuffer(engine, n)
+    pg0, fb0 = engine.reply_stats()
     _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), out.ptr))
     got = out.to_numpy()
+    pg1, fb1 = engine.reply_stats()
+    assert fb1 == fb0 and pg1 > pg0  # the group-tag pipeline answered, pending groups resolved in LDS
+    route(reply=-1)  # the sort path, into a fresh filter
+    srt = _filter(L, engine, size, k)
+    _lib.check(L.rsk_bloom_add(srt, ctypes.byref(ks), out.ptr))
+    assert np.array_equal(got, out.to_numpy())
+    L.rsk_bloom_destroy(srt)
+    route("reset=0")
     out.free()
     plain = _filter(L, engine, size, k)
     _lib.check(L.rsk_bloom_add(plain, ctypes.byref(ks), None))
