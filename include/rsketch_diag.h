@@ -25,6 +25,7 @@ const char *rsk_diag_last_error(void);
  *   bloom_part    exact-offset insert: 0 auto, 1 at any batch size, -1 never
  *   bloom_chunk   probes per chunk of the slice-routed insert (0 = default)
  *   sa_tiny       1: sub-regions of 32 probes (forces the overflow fallbacks)
+ *   sa_kc         -1: the insert's sa1 with the runtime k also at k = 7 (0: a k = 7 instance)
  *   sa_v          the insert's sa2h tile: uint4 loads per lane, 0 (= 3), 6 or 8
  *   sa_dbg        TIMING ONLY (wrong filter): the insert's sa1 stores each tile's image
  *                 contiguously and the insert stops after sa1

@@ -156,6 +156,7 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "bloom_part") t.bloom_part = (int)value;
     else if (k == "bloom_chunk") t.bloom_chunk = (uint64_t)value;
     else if (k == "sa_tiny") t.sa_tiny = (int)value;
+    else if (k == "sa_kc") t.sa_kc = (int)value;
     else if (k == "sa_v") t.sa_v = (int)value;
     else if (k == "sa_dbg") t.sa_dbg = (int)value;
     else if (k == "sa_parts") t.sa_parts = (uint32_t)value;

@@ -553,11 +553,13 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
     RSK_HIP(hipMemsetAsync(flags, 0, 12, c->stream));
     {
       ProfScope ps(c, "bloom_rp1");
-#define RSK_RP1(F16, KM, KPL)                                                                                       \
-  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint32_t, KPL, true>), dim3(Wl), dim3(T1), 0, c->stream,       \
+#define RSK_RP1(F16, KM, KPL, ...)                                                                                  \
+  hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint32_t, KPL, true, ##__VA_ARGS__>), dim3(Wl), dim3(T1), 0,    \
+                     c->stream,                                                                                       \
                      dk.data, dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit, used, \
                      flags, S, gs)
-      if (kpl4) RSK_RP1(true, 8, 4);
+      if (kpl4 && b->k == 7 && c->tune.sa_kc >= 0) RSK_RP1(true, 8, 4, 7);  // C3's k as a constant
+      else if (kpl4) RSK_RP1(true, 8, 4);
       else if (f16) RSK_RP1(true, 16, 1);
       else if (kmax == 8) RSK_RP1(false, 8, 2);
       else RSK_RP1(false, 16, 1);

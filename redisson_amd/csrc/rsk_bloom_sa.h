@@ -161,14 +161,14 @@ constexpr uint32_t SA2_SLOTS = SA2_T * SA2_V * 4;  // records per sa2h tile
 // 512-lane workgroups: at most 80 VGPRs, so 3 workgroups (6 waves per SIMD)
 // share a CU; with 4 keys per lane (73 KiB of LDS) 2.
 // KPL: keys per lane (default 16 / KMAX); more keys per super-tile make every
-// bin's run longer.
+// bin's run longer.  KC: the filter's k as a constant (0: the runtime k).
 //
 // TAGGED (the add()-with-replies pipeline, rsk_bloom_reply.hip): workgroup w
 // takes the CONTIGUOUS super-tiles [w S, (w + 1) S) instead of every
 // gridDim.x-th one, and each record carries in its top 6 bits the key group
 // g = (super-tile - w S) / gs of its key (offsets are < 2^26): along any
 // sub-region (w, c) g never decreases, so key order is known per group.
-template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX, bool TAGGED = false>
+template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX, bool TAGGED = false, int KC = 0>
 __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
     FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
@@ -176,6 +176,7 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
     int dbg = 0) {
   constexpr uint32_t KST = T1 * KPL;
   constexpr int NP = KPL * KMAX;
+  const int kk = KC ? KC : k;  // KC: k known at compile time (the probe loop without the t < k tests)
   constexpr int PER = 4;  // bins per wave-0 lane (<= 256 bins)
   static_assert(sizeof(R) == 4, "4-byte probe records");
   constexpr uint32_t RG = 16 / sizeof(R);  // records per 16-byte group
@@ -268,12 +269,12 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
         const int s = u * KMAX + t;
         tag[s] = INVALID;
         pay[s] = 0;
-        if (ok && t < k) {
+        if (ok && t < kk) {
           const uint64_t idx = ps.idx;
           const uint32_t bin = (uint32_t)(idx >> shift1);
           pay[s] = (R)((uint32_t)(idx & low) | gtag);
           tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
-          if (t + 1 < k) ps.next(t, fm);
+          if (t + 1 < kk) ps.next(t, fm);
         }
       }
     }
