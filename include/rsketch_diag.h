@@ -38,6 +38,9 @@ const char *rsk_diag_last_error(void);
  *   reply_dbg     TIMING ONLY (wrong replies and T): rp_tapply without its
  *                 folds (bit 0) / without its T stores (bit 1)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
+ *   gpart_tm      1 (default): its first pass tile-major (hll_gpart1t), 0: exact-offset runs (hll_gcount + hll_gpart1)
+ *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
+ *                 leaves unwritten then corrupts a register: the tests' hole check)
  *   reset         every route back to automatic
  * Every route but sa_dbg and reply_dbg gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);

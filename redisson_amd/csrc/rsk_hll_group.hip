@@ -156,6 +156,97 @@ __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict_
   }
 }
 
+// ---- tile-major first pass (the default): hll_gpart1t writes each tile's
+// bin-sorted image CONTIGUOUSLY at tile t's slot (t GP_TILE records) with a
+// u16 header of its bin starts; no count pass.  Scattered ~33-record runs
+// were the first pass's cost (DRAM row scatter on the write side: §4); the
+// fine-bin pass reads each coarse bin's per-tile segments instead, and
+// scattered segment reads run at the stream rate (6.5 TB/s for 256-byte
+// segments, scripts/fetch_calib.py).  Tile t = block b's tile j: t = b tpb + j.
+__global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict__ keys,
+                                                         const uint32_t* __restrict__ groups, uint64_t n, uint64_t per,
+                                                         uint64_t G, uint32_t nbins, uint32_t tpb,
+                                                         uint32_t* __restrict__ out, uint16_t* __restrict__ hdr) {
+  __shared__ SortLds<GP_TILE> L;
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  const uint32_t HS = nbins + 1;
+  L.hist[threadIdx.x] = 0;
+  uint32_t j = 0;
+  for (uint64_t k0 = begin; k0 < end; k0 += GP_TILE, ++j) {
+    uint4 v[GP_E];
+    uint32_t g[GP_E];
+#pragma unroll
+    for (int e = 0; e < GP_E; ++e) {
+      const uint64_t i = k0 + threadIdx.x + (uint64_t)e * PT;
+      const bool ok = i < end;
+      v[e] = ok ? ld_nt16(keys + i) : make_uint4(0, 0, 0, 0);
+      g[e] = ok ? __builtin_nontemporal_load(&groups[i]) : 0xFFFFFFFFu;
+    }
+    __syncthreads();  // the previous tile's image is written out, hist reset
+    uint32_t rec[GP_E], tag[GP_E];
+#pragma unroll
+    for (int e = 0; e < GP_E; ++e) {
+      tag[e] = 0xFFFFFFFFu;
+      if (g[e] < G) {
+        const uint64_t hsh = murmur64a_16(((uint64_t)v[e].y << 32) | v[e].x, ((uint64_t)v[e].w << 32) | v[e].z);
+        rec[e] = ((g[e] & ((1u << GP_BIN_SHIFT) - 1)) << 20) | (hll_index(hsh) << 6) | hll_rank(hsh);
+        const uint32_t b = g[e] >> GP_BIN_SHIFT;
+        tag[e] = (b << 16) | atomicAdd(&L.hist[b], 1u);
+      }
+    }
+    __syncthreads();
+    const uint32_t cnt = L.hist[threadIdx.x];
+    uint32_t np;
+    const uint32_t ls = block_excl_scan256(cnt, &np);
+    L.lstart[threadIdx.x] = ls;
+    const uint64_t t = (uint64_t)blockIdx.x * tpb + j;
+    if (threadIdx.x < nbins) hdr[t * HS + threadIdx.x] = (uint16_t)ls;
+    if (threadIdx.x == 0) hdr[t * HS + nbins] = (uint16_t)np;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < GP_E; ++e)
+      if (tag[e] != 0xFFFFFFFFu) L.srt[L.lstart[tag[e] >> 16] + (tag[e] & 0xFFFFu)] = rec[e];
+    __syncthreads();
+    uint32_t* o = out + t * GP_TILE;  // 16-byte aligned
+    const uint4* s4 = reinterpret_cast<const uint4*>(L.srt);
+    for (uint32_t q = threadIdx.x; q < (np + 3) / 4; q += PT) {  // the tail past np is never read
+      const uint4 x = s4[q];
+      u32x4 y = {x.x, x.y, x.z, x.w};
+      __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(o) + q);
+    }
+    L.hist[threadIdx.x] = 0;
+  }
+  for (; j < tpb; ++j) {  // the block's unused tile slots: empty headers
+    const uint64_t t = (uint64_t)blockIdx.x * tpb + j;
+    for (uint32_t c = threadIdx.x; c < HS; c += PT) hdr[t * HS + c] = 0;
+  }
+}
+
+// hdr [NT][HS] (u16, tile-major) -> hdrT [nbins][NT] (segment start of bin
+// c in tile t) and len [nbins][NT] (u32, its length), 64 x 64 tiles through
+// LDS.  One exclusive scan of len then gives every segment's global position
+// in bin-major order (the virtual run of bin c: its segments in tile order).
+__global__ __launch_bounds__(256) void hll_hdr_transpose_kernel(const uint16_t* __restrict__ in, uint32_t NT,
+                                                                uint32_t nbins, uint16_t* __restrict__ hdrT,
+                                                                uint32_t* __restrict__ len) {
+  __shared__ uint16_t tl[64][66];
+  const uint32_t t0 = blockIdx.x * 64, c0 = blockIdx.y * 64, HS = nbins + 1;
+  for (uint32_t i = threadIdx.x; i < 64 * 65; i += 256) {
+    const uint32_t rr = i / 65, cc = i % 65;  // 65 columns: bin c0 + 64's start ends bin c0 + 63's segment
+    tl[rr][cc] = (t0 + rr < NT && c0 + cc < HS) ? in[(uint64_t)(t0 + rr) * HS + c0 + cc] : 0;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += 256) {
+    const uint32_t cc = i >> 6, rr = i & 63;
+    if (t0 + rr < NT && c0 + cc < nbins) {
+      const uint64_t o = (uint64_t)(c0 + cc) * NT + t0 + rr;
+      hdrT[o] = tl[rr][cc];
+      len[o] = (uint32_t)tl[rr][cc + 1] - tl[rr][cc];
+    }
+  }
+}
+
 // ---- fine-bin pass: gpart1's coarse-bin runs re-sorted by fine bin (16
 // sketches, rec >> 24).  Each coarse bin c is cut into nq_c parts of about
 // `target` records (parts sized by records, so a heavy bin -- Zipf -- gets
@@ -364,6 +455,367 @@ __global__ __launch_bounds__(GQ_T) void hll_gpart2p_kernel(const uint32_t* __res
     if (threadIdx.x < PT) hist[threadIdx.x] = 0;
     for (uint32_t j = threadIdx.x; j < ntile; j += GQ_T) out[dlt[sbin[j]] + j] = img[j];
     __syncthreads();
+  }
+}
+
+
+// ---- tile-major fine-bin pass (route gpart_tm).  Bin c's records are its
+// segments in tiles 0..NT-1 (segment (c, t): seglen[c NT + t] records from
+// tile t's slot + hdrT[c NT + t]; goff = their exclusive scan, bin-major).
+// A TM part is bin c's segments in tiles [lo, hi).  Segments are read by the
+// lanes that own them when short (a sparse bin: a record or two per tile) and
+// by the whole wave, 64 records a load, when longer; either way many loads
+// are in flight per wave.
+constexpr uint32_t TM_PT = 16384;  // tiles per part at most
+constexpr uint32_t TM_SHORT = 8;   // a lane reads a segment of at most this many records alone
+constexpr int TM_MU = 16;          // medium segments (<= 64 records) loaded per wave step
+constexpr uint32_t TM_MED4 = 253;  // medium-long: one uint4 per lane covers the segment at any alignment
+constexpr int TM_LU = 4;           // uint4 loads per lane in flight per chunk of a long segment (gcount2t)
+constexpr int TM_LU2 = 2;          // (gpart2t)
+constexpr uint32_t TM_RT = 8192;   // records per gpart2t round
+constexpr uint32_t TM_W = 1024;    // tiles per gpart2t round window (one per lane)
+static_assert(TM_RT >= GP_TILE && TM_W == GQ_T, "a round holds any one tile's segment; one lane per window tile");
+
+// The segments i < ns of a window (LDS: first record index sa[i], length
+// sl[i], f's base sb[i]; sb may be null): f(x, sb[i] + r) for record r of
+// each.  Short, medium and medium-long segments are read with the lane that
+// owns them (segment i: wave i % 16, lane i / 16) -- the owner alone, the
+// wave one record per lane, the wave one uint4 per lane -- long ones
+// (> TM_MED4 records) in chunks of 64 LU uint4 dealt over all the waves, so a
+// window of one dense tile is read by every wave.  Called by the whole workgroup (uniform control flow).
+template <int LU, int M4, class F>
+RSK_DEV void tm_run(const uint32_t* __restrict__ recs, const uint32_t* sa, const uint32_t* sl, const uint32_t* sb,
+                    uint32_t ns, F&& f) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  {
+    const uint32_t i = w + 16 * lane;
+    uint32_t a = 0, l = 0, base = 0;
+    if (i < ns) {
+      a = sa[i];
+      l = sl[i];
+      base = sb ? sb[i] : 0u;
+    }
+    if (l > TM_MED4) l = 0;  // long: below
+    if (__ballot(l > 0 && l <= TM_SHORT)) {  // short: the owner alone (skipped by waves without any)
+      const bool sh = l <= TM_SHORT;
+      uint32_t x[TM_SHORT];
+#pragma unroll
+      for (uint32_t u = 0; u < TM_SHORT; ++u) x[u] = recs[a + (sh && u < l ? u : 0u)];  // unconditional: in flight together
+#pragma unroll
+      for (uint32_t u = 0; u < TM_SHORT; ++u)
+        if (sh && u < l) f(x[u], base + u);
+    }
+    uint64_t mm = __ballot(l > TM_SHORT && l <= 64);
+    while (mm) {  // medium: one load per lane each, TM_MU segments at a time
+      uint32_t y[TM_MU], lj[TM_MU], bj[TM_MU];
+#pragma unroll
+      for (int u = 0; u < TM_MU; ++u) {  // branch-free, loads unconditional (clamped): all in flight together
+        const bool ok = mm != 0;
+        const int j = ok ? __builtin_ctzll(mm) : 0;
+        mm &= mm - 1;
+        lj[u] = ok ? (uint32_t)__builtin_amdgcn_readlane((int)l, j) : 0u;
+        bj[u] = (uint32_t)__builtin_amdgcn_readlane((int)base, j);
+        const uint32_t aj = ok ? (uint32_t)__builtin_amdgcn_readlane((int)a, j) : 0u;
+        y[u] = recs[aj + (lane < lj[u] ? lane : 0u)];
+      }
+#pragma unroll
+      for (int u = 0; u < TM_MU; ++u)
+        if (lane < lj[u]) f(y[u], bj[u] + lane);
+    }
+    const uint4* r4 = reinterpret_cast<const uint4*>(recs);
+    uint64_t m4 = __ballot(l > 64);
+    while (m4) {  // medium-long: one uint4 per lane each (edges masked), M4 segments at a time
+      uint4 y[M4];
+      uint32_t aj[M4], lj[M4], bj[M4];
+#pragma unroll
+      for (int u = 0; u < M4; ++u) {
+        const bool ok = m4 != 0;
+        const int j = ok ? __builtin_ctzll(m4) : 0;
+        m4 &= m4 - 1;
+        lj[u] = ok ? (uint32_t)__builtin_amdgcn_readlane((int)l, j) : 0u;
+        bj[u] = (uint32_t)__builtin_amdgcn_readlane((int)base, j);
+        aj[u] = ok ? (uint32_t)__builtin_amdgcn_readlane((int)a, j) : 0u;
+        const bool in = 4 * ((aj[u] >> 2) + lane) < aj[u] + lj[u];
+        y[u] = r4[(aj[u] >> 2) + (in ? lane : 0u)];
+      }
+#pragma unroll
+      for (int u = 0; u < M4; ++u) {
+        const uint32_t r0 = 4 * ((aj[u] >> 2) + lane);
+        const uint32_t x[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          if (r0 + m >= aj[u] && r0 + m < aj[u] + lj[u]) f(x[m], bj[u] + (r0 + m - aj[u]));
+      }
+    }
+  }
+  // long: chunks of 64 LU uint4 (records 4 q .. 4 q + 3; the segment's edges
+  // masked) dealt over the waves, chunk g to wave g % 16
+  constexpr uint32_t CQ = 64 * LU;
+  const uint4* r4 = reinterpret_cast<const uint4*>(recs);
+  uint32_t g = 0;  // chunks dealt so far
+  for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t l = i < ns ? sl[i] : 0u;
+    uint64_t ml = __ballot(l > TM_MED4);
+    while (ml) {
+      const int j = __builtin_ctzll(ml);
+      ml &= ml - 1;
+      const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)l, j);
+      const uint32_t aj = (uint32_t)__builtin_amdgcn_readfirstlane((int)sa[i0 + j]);
+      const uint32_t bj = sb ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sb[i0 + j]) : 0u;
+      const uint32_t qa = aj >> 2, nq4 = ((aj + lj + 3) >> 2) - qa;
+      const uint32_t nch = (nq4 + CQ - 1) / CQ;
+      for (uint32_t ch = (w + 16 - g % 16) % 16; ch < nch; ch += 16) {
+        uint4 y[LU];
+#pragma unroll
+        for (int u = 0; u < LU; ++u) {
+          const uint32_t qq = ch * CQ + 64 * u + lane;
+          y[u] = r4[qa + (qq < nq4 ? qq : 0u)];
+        }
+#pragma unroll
+        for (int u = 0; u < LU; ++u) {
+          const uint32_t r0 = 4 * (qa + ch * CQ + 64 * u + lane);  // record index of y[u].x
+          const uint32_t x[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (r0 + m >= aj && r0 + m < aj + lj) f(x[m], bj + (r0 + m - aj));
+        }
+      }
+      g += nch;
+    }
+  }
+}
+
+// Thread per part q.  Each bin gets max(len / target + 1, ceil(NT / TM_PT))
+// parts cut at tile boundaries (the smaller of the record-balanced and the
+// tile-balanced cut, so both stay bounded for inputs in any order); every
+// block rebuilds the bins' part prefix.
+__global__ __launch_bounds__(PT) void hll_gparts_tm_kernel(const uint32_t* __restrict__ goff, uint32_t NT,
+                                                           uint32_t nbins1, uint32_t target, uint32_t qmax,
+                                                           GPart* __restrict__ parts, uint32_t* __restrict__ d_nq) {
+  __shared__ uint32_t q0s[PT + 1];
+  const uint32_t c = threadIdx.x;
+  uint32_t nq = 0;
+  if (c < nbins1) {
+    const uint32_t len = goff[(uint64_t)(c + 1) * NT] - goff[(uint64_t)c * NT];
+    const uint32_t a = len / target + 1, b = (NT + TM_PT - 1) / TM_PT;
+    nq = a > b ? a : b;
+  }
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan256(nq, &tot);
+  q0s[c] = ex;
+  if (c == 0) q0s[PT] = tot;
+  __syncthreads();
+  if (blockIdx.x == 0 && c == 0) *d_nq = tot < qmax ? tot : qmax;
+  const uint32_t q = blockIdx.x * PT + threadIdx.x;
+  if (q >= qmax || q >= tot) return;
+  uint32_t lo = 0, hi = nbins1 - 1;  // the bin of part q: the last with q0 <= q (every bin has a part)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (q0s[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint32_t cb = lo, q0 = q0s[cb], n = q0s[cb + 1] - q0, j = q - q0;
+  const uint32_t* so = goff + (uint64_t)cb * NT;
+  const uint32_t base = so[0], len = so[NT] - base;
+  auto cut = [&](uint32_t jj) -> uint32_t {
+    if (jj == 0) return 0;
+    if (jj >= n) return NT;
+    const uint32_t want = base + (uint32_t)((uint64_t)len * jj / n);
+    uint32_t a = 0, b = NT;  // the first tile with so[t] >= want
+    while (a < b) {
+      const uint32_t m = (a + b) >> 1;
+      if (so[m] < want) a = m + 1;
+      else b = m;
+    }
+    const uint32_t p = (uint32_t)((uint64_t)NT * jj / n);
+    return a < p ? a : p;
+  };
+  parts[q] = GPart{cb, q0, n, cut(j), cut(j + 1)};
+}
+
+// Fine-bin counts of a TM part (as hll_gcount2p), TM_W tiles at a time.
+__global__ __launch_bounds__(GQ_T) void hll_gcount2t_kernel(const uint32_t* __restrict__ recs,
+                                                            const GPart* __restrict__ parts,
+                                                            const uint32_t* __restrict__ d_nq,
+                                                            uint32_t* __restrict__ cnt, const uint16_t* __restrict__ hdrT,
+                                                            const uint32_t* __restrict__ seglen, uint32_t NT) {
+  constexpr int NH = 16;
+  __shared__ uint32_t h[NH][PT + 1];
+  __shared__ uint32_t sa[TM_W], sl[TM_W];
+  const uint32_t q = blockIdx.x;
+  if (q >= *d_nq) return;  // uniform
+  const GPart pt = parts[q];
+  for (uint32_t i = threadIdx.x; i < NH * (PT + 1); i += GQ_T) (&h[0][0])[i] = 0;
+  __syncthreads();
+  uint32_t* hw = h[(((threadIdx.x >> 6) & 3) << 2) | ((threadIdx.x & 63) >> 4)];
+  const uint16_t* hs = hdrT + (uint64_t)pt.c * NT;
+  const uint32_t* sg = seglen + (uint64_t)pt.c * NT;
+  // batches of TM_W tiles: headers staged in LDS (the next batch's loaded during this one)
+  auto hdr_load = [&](uint32_t t0, uint32_t& a, uint32_t& l) {
+    const uint32_t t = t0 + threadIdx.x;
+    a = 0, l = 0;
+    if (t < pt.hi) {
+      l = sg[t];
+      a = t * GP_TILE + hs[t];
+    }
+  };
+  uint32_t a, l;
+  hdr_load(pt.lo, a, l);
+  for (uint32_t t0 = pt.lo; t0 < pt.hi; t0 += TM_W) {
+    sa[threadIdx.x] = a;
+    sl[threadIdx.x] = l;
+    hdr_load(t0 + TM_W, a, l);
+    __syncthreads();
+    const uint32_t ns = pt.hi - t0 < TM_W ? pt.hi - t0 : TM_W;
+    tm_run<TM_LU, 4>(recs, sa, sl, nullptr, ns, [&](uint32_t x, uint32_t) { atomicAdd(&hw[x >> 24], 1u); });
+    __syncthreads();
+  }
+  __syncthreads();
+  if (threadIdx.x < PT) {
+    const uint32_t f = threadIdx.x;
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) t += h[k][f];
+    cnt[(uint64_t)pt.q0 * PT + (uint64_t)f * pt.nq + (q - pt.q0)] = t;
+  }
+}
+
+// Sorts a TM part by fine bin (as hll_gpart2p) in rounds of TM_RT records
+// (the last tile of a round may be cut and continue the next; at most TM_W
+// tiles): lane i of the window holds tile t + i, the count of lanes whose
+// segment starts before the round's end is the round's tile count (the next
+// window is loaded while the round runs).  Segments are staged in LDS at their round offsets
+// (phase A), counted by fine bin (C1), ranked and placed (C2), written out.
+__global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __restrict__ recs,
+                                                           const GPart* __restrict__ parts,
+                                                           const uint32_t* __restrict__ d_nq,
+                                                           const uint32_t* __restrict__ offf,
+                                                           uint32_t* __restrict__ out, const uint16_t* __restrict__ hdrT,
+                                                           const uint32_t* __restrict__ seglen,
+                                                           const uint32_t* __restrict__ goff, uint32_t NT) {
+  __shared__ uint32_t stage[TM_RT], img[TM_RT];
+  __shared__ uint32_t sa[TM_W], sl[TM_W], sr[TM_W];
+  __shared__ uint32_t hist[PT], dlt[PT], cur[PT], wsum[GQ_T / 64], wc[GQ_T / 64];
+  __shared__ uint32_t s_hot, s_e, s_cut;
+  const uint32_t q = blockIdx.x;
+  if (q >= *d_nq) return;  // uniform
+  const GPart pt = parts[q];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_hot = 0;
+  __syncthreads();
+  const uint16_t* hs = hdrT + (uint64_t)pt.c * NT;
+  const uint32_t* sg = seglen + (uint64_t)pt.c * NT;
+  const uint32_t* so = goff + (uint64_t)pt.c * NT;
+  if (threadIdx.x < PT) {
+    const uint64_t ix = (uint64_t)pt.q0 * PT + (uint64_t)threadIdx.x * pt.nq + (q - pt.q0);
+    cur[threadIdx.x] = offf[ix];
+    hist[threadIdx.x] = 0;
+    // a fine bin with more than an eighth of the part's records (as hll_gpart2p)
+    const uint32_t c = offf[ix + 1] - offf[ix];
+    if ((uint64_t)c * 8 > (uint64_t)(so[pt.hi] - so[pt.lo])) atomicMax(&s_hot, 0x100u | threadIdx.x);
+  }
+  // round state: tile t (partly consumed when v > so[t]), v = the round's first record (global position)
+  const uint32_t pe = so[pt.hi];
+  uint32_t t = pt.lo, v = so[pt.lo];
+  auto window = [&](uint32_t t0, uint32_t& e, uint32_t& l, uint32_t& h) {
+    const uint32_t tt = t0 + threadIdx.x;
+    e = 0xFFFFFFFFu, l = 0, h = 0;
+    if (tt < pt.hi) {
+      e = so[tt + 1];
+      l = sg[tt];
+      h = hs[tt];
+    }
+  };
+  uint32_t e, l, hv;
+  window(t, e, l, hv);
+  __syncthreads();
+  const bool hot_mode = s_hot != 0;  // uniform
+  const uint32_t hot = s_hot & 0xFFu;
+  while (v < pe) {
+    // the round: records [v, vend) from tiles t .. t + ntl - 1 (those starting before v + TM_RT, at
+    // most the window's TM_W; ntl >= 1), the last one possibly cut (it then starts the next round)
+    const uint32_t s0 = e - l;
+    const bool in = s0 < v + TM_RT;
+    const uint64_t bm = __ballot(in);
+    if (lane == 0) wc[w] = (uint32_t)__popcll(bm);
+    if (threadIdx.x == TM_W - 1) s_e = e;  // the window's last tile's end (all tiles in: the round ends there)
+    __syncthreads();
+    uint32_t ntl = 0;
+#pragma unroll
+    for (int i = 0; i < (int)(GQ_T / 64); ++i) ntl += wc[i];
+    uint32_t vend = pe - v < TM_RT ? pe : v + TM_RT;
+    if (ntl == TM_W && s_e < vend) vend = s_e;
+    if (in) {
+      const uint32_t a0 = s0 > v ? s0 : v, e0 = e < vend ? e : vend;
+      sa[threadIdx.x] = (t + threadIdx.x) * GP_TILE + hv + (a0 - s0);
+      sl[threadIdx.x] = e0 > a0 ? e0 - a0 : 0u;
+      sr[threadIdx.x] = a0 - v;
+      if (threadIdx.x == ntl - 1) s_cut = e > vend ? 1u : 0u;  // only the last tile in can be cut
+    }
+    __syncthreads();
+    const uint32_t tn = t + ntl - s_cut;
+    uint32_t e2, l2, h2;
+    window(tn, e2, l2, h2);  // the next round's window, in flight during this one
+    const uint32_t n = vend - v;
+    // A: stage the segments at their round offsets and count them by fine bin
+    // (a dominant bin's ranks once per wave: ballot + one atomic)
+    tm_run<TM_LU2, 4>(recs, sa, sl, sr, ntl, [&](uint32_t x, uint32_t p) {
+      stage[p] = x;
+      const uint32_t b = x >> 24;
+      const bool ish = hot_mode && b == hot;
+      if (hot_mode) {
+        const uint64_t mh = __ballot(ish);
+        if (mh && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(mh)) atomicAdd(&hist[hot], (uint32_t)__popcll(mh));
+      }
+      if (!ish) atomicAdd(&hist[b], 1u);
+    });
+    __syncthreads();
+    uint32_t hc = 0, incl = 0;
+    if (threadIdx.x < PT) {
+      hc = hist[threadIdx.x];
+      incl = gq_scan_incl(hc, lane);
+      if (lane == 63) wsum[w] = incl;
+    }
+    __syncthreads();
+    if (threadIdx.x < PT) {
+      uint32_t pre = 0;
+      for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
+      const uint32_t ls = pre + incl - hc;
+      dlt[threadIdx.x] = cur[threadIdx.x] - ls;
+      cur[threadIdx.x] += hc;
+      hist[threadIdx.x] = ls;  // now the bin's next free slot in img
+    }
+    __syncthreads();
+    // C2: rank and place
+#pragma unroll
+    for (int e8 = 0; e8 < (int)(TM_RT / GQ_T); ++e8) {
+      const uint32_t k = threadIdx.x + e8 * GQ_T;
+      const bool valid = k < n;
+      const uint32_t x = valid ? stage[k] : 0u, b = x >> 24;
+      const bool ish = hot_mode && valid && b == hot;
+      if (hot_mode) {
+        const uint64_t mh = __ballot(ish);
+        if (mh) {  // wave-uniform
+          const int leader = __builtin_ctzll(mh);
+          uint32_t base = 0;
+          if ((int)lane == leader) base = atomicAdd(&hist[hot], (uint32_t)__popcll(mh));
+          base = (uint32_t)__shfl((int)base, leader, 64);
+          if (ish) img[base + (uint32_t)__popcll(mh & ((1ull << lane) - 1))] = x;
+        }
+      }
+      if (valid && !ish) img[atomicAdd(&hist[b], 1u)] = x;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < n; j += GQ_T) {
+      const uint32_t x = img[j];
+      out[dlt[x >> 24] + j] = x;
+    }
+    if (threadIdx.x < PT) hist[threadIdx.x] = 0;
+    __syncthreads();
+    t = tn;
+    v = vend;
+    e = e2, l = l2, hv = h2;
   }
 }
 
@@ -722,7 +1174,11 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
   // fine-bin pass parts: about four per CU over the whole chunk, at least 16 tiles each
   const uint32_t target = (uint32_t)std::max<uint64_t>(16ull * GQ_TILE, max_np / (4ull * cus) + 1);
-  const uint32_t qmax = nbins1 + (uint32_t)(max_np / target) + 2;
+  const bool tm = c->tune.gpart_tm == 1;
+  const uint64_t per_max = ((max_np + G1 - 1) / G1 + 3) & ~3ull;
+  const uint64_t nt_max = (uint64_t)G1 * ((per_max + GP_TILE - 1) / GP_TILE);
+  // TM parts: also at most TM_PT tiles each
+  const uint32_t qmax = nbins1 + (uint32_t)(max_np / target) + 2 + (tm ? nbins1 * (uint32_t)((nt_max + TM_PT - 1) / TM_PT) : 0u);
   const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)qmax * PT + 1;
   size_t sb1 = 0, sb2 = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt1, c->stream);
@@ -731,7 +1187,17 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint32_t xcap = (uint32_t)(GP_NP * (chunk / GP_CH + 1) + 16);  // extra work items per chunk, at most
   const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1)) +
                         al(sizeof(GPart) * qmax) + al(4 * (nfine + 1)) + 256;
-  uint8_t* w = c->work(meta + 2 * al(4 * max_np) + 256);  // + slack: the uint4 record loads round their ends up
+  // tile-major first pass: NT tiles of GP_TILE record slots, a u16 header per tile and bin (and
+  // its transpose), the per-bin segment prefix
+  const uint32_t HS = nbins1 + 1;
+  const uint64_t bufa = tm ? al(4 * nt_max * GP_TILE) : al(4 * max_np);
+  size_t sb3 = 0;
+  if (tm)
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb3, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (int)(nbins1 * nt_max + 1), c->stream);
+  const uint64_t nseg = (uint64_t)nbins1 * nt_max + 1;
+  const uint64_t tm_bytes = tm ? al(2 * nt_max * HS) + al(2 * nseg) + 2 * al(4 * nseg) + al(sb3) : 0;
+  uint8_t* w = c->work(meta + tm_bytes + bufa + al(4 * max_np) + 256);  // + slack: the uint4 record loads round their ends up
   uint8_t* q = w;
   auto take = [&](uint64_t n) {
     uint8_t* r = q;
@@ -748,13 +1214,53 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   GPart* parts = reinterpret_cast<GPart*>(take(al(sizeof(GPart) * qmax)));
   uint32_t* off2 = reinterpret_cast<uint32_t*>(take(al(4 * (nfine + 1))));
   uint32_t* d_nq = reinterpret_cast<uint32_t*>(take(256));
-  uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta);
-  uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + al(4 * max_np));
+  uint16_t* hdr = reinterpret_cast<uint16_t*>(w + meta);
+  uint16_t* hdrT = reinterpret_cast<uint16_t*>(w + meta + al(2 * nt_max * HS));
+  uint32_t* seglen = reinterpret_cast<uint32_t*>(w + meta + al(2 * nt_max * HS) + al(2 * nseg));
+  uint32_t* segoff = reinterpret_cast<uint32_t*>(w + meta + al(2 * nt_max * HS) + al(2 * nseg) + al(4 * nseg));
+  void* scan_tmp3 = w + meta + al(2 * nt_max * HS) + al(2 * nseg) + 2 * al(4 * nseg);
+  uint32_t* buf_a = reinterpret_cast<uint32_t*>(w + meta + tm_bytes);
+  uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + tm_bytes + bufa);
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
     const uint64_t per = ((m + G1 - 1) / G1 + 3) & ~3ull;  // a multiple of 4: uint4 id loads in hll_gcount
     const uint4* kd = reinterpret_cast<const uint4*>(keys.data) + first;
     const uint32_t* gd = d_groups + first;
+    const uint32_t tpb = (uint32_t)((per + GP_TILE - 1) / GP_TILE), NT = G1 * tpb;
+    if (c->tune.gpart_poison) RSK_HIP(hipMemsetAsync(buf_b, 0xFF, 4 * max_np, c->stream));
+    if (tm) {
+      {
+        ProfScope ps(c, "hll_gpart1");
+        hipLaunchKernelGGL(hll_gpart1t_kernel, dim3(G1), dim3(PT), 0, c->stream, kd, gd, m, per, G, nbins1, tpb, buf_a,
+                           hdr);
+        RSK_CHECK_LAUNCH("hll_gpart1t");
+      }
+      {
+        ProfScope ps(c, "hll_gpart_count");
+        hipLaunchKernelGGL(hll_hdr_transpose_kernel, dim3((NT + 63) / 64, (nbins1 + 63) / 64), dim3(256), 0,
+                           c->stream, hdr, NT, nbins1, hdrT, seglen);
+        RSK_CHECK_LAUNCH("hll_hdr_transpose");
+        RSK_HIP(hipMemsetAsync(seglen + (uint64_t)nbins1 * NT, 0, 4, c->stream));
+        RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp3, sb3, seglen, segoff, (int)(nbins1 * NT + 1), c->stream));
+      }
+      {
+        ProfScope ps(c, "hll_gpart2");
+        RSK_HIP(hipMemsetAsync(cnt2, 0, 4 * ncnt2, c->stream));
+        hipLaunchKernelGGL(hll_gparts_tm_kernel, dim3((qmax + PT - 1) / PT), dim3(PT), 0, c->stream, segoff, NT, nbins1,
+                           target, qmax, parts, d_nq);
+        RSK_CHECK_LAUNCH("hll_gparts_tm");
+        hipLaunchKernelGGL(hll_gcount2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, cnt2, hdrT,
+                           seglen, NT);
+        RSK_CHECK_LAUNCH("hll_gcount2t");
+        RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, offf, (int)ncnt2, c->stream));
+        hipLaunchKernelGGL(hll_gfine_kernel, dim3(nfine / 256 + 1), dim3(256), 0, c->stream, offf, parts, d_nq, nbins1,
+                           off2);
+        RSK_CHECK_LAUNCH("hll_gfine");
+        hipLaunchKernelGGL(hll_gpart2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b,
+                           hdrT, seglen, segoff, NT);
+        RSK_CHECK_LAUNCH("hll_gpart2t");
+      }
+    } else {
     {
       ProfScope ps(c, "hll_gpart_count");
       RSK_HIP(hipMemsetAsync(cnt1 + ncnt1 - 1, 0, 4, c->stream));
@@ -782,6 +1288,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       RSK_CHECK_LAUNCH("hll_gfine");
       hipLaunchKernelGGL(hll_gpart2p_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b);
       RSK_CHECK_LAUNCH("hll_gpart2p");
+    }
     }
     {
       ProfScope ps(c, "hll_gapply");

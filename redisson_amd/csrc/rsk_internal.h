@@ -62,6 +62,8 @@ struct Tuning {
   int reply_s = 0;           // rp_tapply: wave steps whose loads are in flight together, 0 (= 2), 1 or 4
   int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
+  int gpart_poison = 0;      // timing-free check: fill the fine-bin output with 0xFF first (a hole then shows)
+  int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the

@@ -269,18 +269,20 @@ def _pool_regs(L, engine, h, G):
     return out
 
 
+@pytest.mark.parametrize("tm", [0, 1])
 @pytest.mark.parametrize("G,n", [(8205, 3_000_000), (1, 50_000), (4096 * 3, 2_000_001), (20, 4_500_003)])
-def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, route, G, n):
+def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, route, G, n, tm):
     """Grouped PFADD partitioned by sketch (coarse bins of 4096 sketches, fine
     bins of 16, LDS halves of 8; G not a multiple of any of them) equals the
-    direct random-CAS kernel and the oracle over the whole pool."""
+    direct random-CAS kernel and the oracle over the whole pool; tm=1 takes the
+    tile-major first pass (hll_gpart1t)."""
     from redisson_amd import _lib, devmem
 
     g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
     ks = k.keys_fixed(n, 16).as_struct()
     pools = {}
     for mode in ("1", "0"):
-        route(gpart=1 if mode == "1" else -1)
+        route(gpart=1 if mode == "1" else -1, gpart_tm=tm)
         h = _pool(L, engine, G)
         _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
         pools[mode] = h
@@ -295,7 +297,39 @@ def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, route, G,
         L.rsk_hll_destroy(h)
 
 
-def test_grouped_partitioned_unaligned_group_ids(L, engine, orc, route):
+@pytest.mark.parametrize("tm", [0, 1])
+@pytest.mark.parametrize("G,n,zipf", [(4096 * 10 + 16, 50_000_000, 0.0), (1_000_000, 60_000_000, 0.0),
+                                      (200_000, 40_000_000, 1.1)])
+def test_grouped_partitioned_leaves_no_holes(L, engine, route, G, n, zipf, tm):
+    """The fine-bin pass writes every slot the counts reserve: with its output
+    poisoned (0xFF records first: a slot left unwritten would raise a register
+    to 63) the partitioned add still equals the direct kernel.  Sizes where a
+    bin's segments are a few records per tile (the last, nearly empty coarse
+    bin; Zipf's cold bins) and rounds end at the window's tile count."""
+    from redisson_amd import _lib, devmem
+
+    if zipf:
+        g, k = devmem.gen_grouped_zipf(engine, 0x5EED0007, G, zipf, 0, n)
+    else:
+        g, k = devmem.gen_grouped(engine, 0x5EED0007, G, 0, n)
+    ks = k.keys_fixed(n, 16).as_struct()
+    pools = {}
+    for mode in ("1", "0"):
+        route(gpart=1 if mode == "1" else -1, gpart_tm=tm, gpart_poison=1)
+        h = _pool(L, engine, G)
+        _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+        pools[mode] = h
+    g.free()
+    k.free()
+    part, direct = (_pool_regs(L, engine, pools[m], G).reshape(G, 16384) for m in ("1", "0"))
+    bad = np.nonzero((part != direct).any(axis=1))[0]
+    assert bad.size == 0, (bad.size, bad[:8].tolist(), np.unique(bad >> 12)[:8].tolist())
+    for h in pools.values():
+        L.rsk_hll_destroy(h)
+
+
+@pytest.mark.parametrize("tm", [0, 1])
+def test_grouped_partitioned_unaligned_group_ids(L, engine, orc, route, tm):
     """Device-resident pairs from element 1 on: the group ids are then not
     16-byte aligned (hll_gcount's scalar path) while the keys are; the
     partitioned add equals the direct kernel and the oracle."""
@@ -306,7 +340,7 @@ def test_grouped_partitioned_unaligned_group_ids(L, engine, orc, route):
     ks = k.keys_fixed(n, 16, offset=16).as_struct()
     pools = {}
     for mode in ("1", "0"):
-        route(gpart=1 if mode == "1" else -1)
+        route(gpart=1 if mode == "1" else -1, gpart_tm=tm)
         h = _pool(L, engine, G)
         _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr + 4))
         pools[mode] = h
@@ -474,7 +508,8 @@ def _c5_stratified_sample(G: int, per_bin: int = 34, seed: int = 11) -> np.ndarr
     return np.unique(np.array(ids, np.uint64))
 
 
-def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
+@pytest.mark.parametrize("tm", [1, 0])
+def test_c5_full_size_group_sample_bit_exact(L, engine, orc, route, tm):
     """BASELINE configs[4] at its per-GPU size: 1M sketches, 500M (group, key)
     pairs through the grouped PFADD.  A stratified sample of >= 8192 sketches --
     ids from every coarse bin of the partitioned add and every slot of a fine
@@ -483,6 +518,7 @@ def test_c5_full_size_group_sample_bit_exact(L, engine, orc):
     on them."""
     from redisson_amd import _lib, devmem
 
+    route(gpart_tm=tm, gpart_poison=1)  # a fine-bin slot left unwritten would raise a register to 63
     G, n = 1_000_000, 500_000_000
     sample = _c5_stratified_sample(G)
     gs = sample.size
@@ -640,7 +676,8 @@ def test_count_estimator_branches(L, engine, orc, n, branch):
     L.rsk_hll_destroy(h)
 
 
-def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, route):
+@pytest.mark.parametrize("tm", [0, 1])
+def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, route, tm):
     """C5 Zipf(1.1) stress variant: the device generator equals the
     oracle's pair stream; the partitioned grouped add over it (one coarse bin
     holding most pairs, one fine bin a third of them) equals the direct kernel
@@ -655,7 +692,7 @@ def test_zipf_stream_matches_oracle_and_partitioned_add(L, engine, orc, route):
     ks = k.keys_fixed(n, 16).as_struct()
     pools = {}
     for mode in ("1", "0"):
-        route(gpart=1 if mode == "1" else -1)
+        route(gpart=1 if mode == "1" else -1, gpart_tm=tm)
         h = _pool(L, engine, G)
         _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
         pools[mode] = h
