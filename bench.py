@@ -489,14 +489,14 @@ def main():
     kern_label = kern + "_kernel"
     stage_ms = None
     if wl == "c5" and add_launches == 0:
-        # the partitioned grouped PFADD (rsk_bloom_part.hip): its stages together are the add
+        # the partitioned grouped PFADD (rsk_hll_group.hip): its stages together are the add
         stages = ("hll_gpart_count", "hll_gpart1", "hll_gpart2", "hll_gapply")
         reads = {st: engine.prof_read(st) for st in stages}
         add_launches = reads["hll_gapply"][1]
         add_ms = sum(v[0] for v in reads.values())
         stage_ms = {st: v[0] / max(1, v[1]) for st, v in reads.items()}
-        kern_label = ("hll_add_grouped (partitioned: hll_gcount + scan, hll_gpart1, hll_gparts + hll_gcount2p + "
-                      "scan + hll_gfine + hll_gpart2p, hll_gapply)")
+        kern_label = ("hll_add_grouped (partitioned, tile-major: hll_gpart1t, hll_hdr_transpose + scan, "
+                      "hll_gparts_tm + hll_gcount2t + scan + hll_gfine + hll_gpart2t, hll_gapply)")
     red_ms, red_launches = engine.prof_read("hll_reduce")
     side = {name: engine.prof_read(name) for name in ("hll_count", "hll_union_count", "hll_merge",
                                                        "hll_allreduce", "hll_allreduce_pool",
