@@ -84,12 +84,17 @@ def main():
             e["hbm_bytes_per_launch"] = (fe[k] + wr[k]) * 1024
             e["hbm_bytes_note"] = "raw FETCH_SIZE + WRITE_SIZE (uncalibrated for random 4 B access)"
         kern[k] = e
-    parts = ("hll_gcount_kernel", "hll_gpart1_kernel", "hll_gcount2p_kernel", "hll_gpart2p_kernel", "hll_gapply_kernel")
+    # tile-major form (default since late round 4) or the exact-offset form (route gpart_tm=0)
+    parts = ("hll_gpart1t_kernel", "hll_hdr_transpose_kernel", "hll_gcount2t_kernel", "hll_gpart2t_kernel",
+             "hll_gapply_kernel")
+    if not all(p in fe and p in wr for p in parts):
+        parts = ("hll_gcount_kernel", "hll_gpart1_kernel", "hll_gcount2p_kernel", "hll_gpart2p_kernel",
+                 "hll_gapply_kernel")
     extras = tuple(p for p in ("hll_gextra_list_kernel", "hll_gapply_extra_kernel") if p in fe and p in wr)
     if "hll_gapply_kernel" in kern and all(p in fe and p in wr for p in parts):
         parts = parts + extras
-        # the partitioned grouped PFADD as one unit (only in a C5-only run, where
-        # the fine-bin pass is hll_gcount2p + hll_gpart2p): raw counters summed over its stages
+        # the partitioned grouped PFADD as one unit (only in a C5-only run): raw
+        # counters summed over its stages
         kern["hll_add_grouped_partitioned"] = {
             "keys_per_launch": keys, "algorithmic_bytes_per_launch": 20 * keys,
             "hbm_bytes_per_launch": sum((fe[p] + wr[p]) * 1024 for p in parts),
