@@ -4,9 +4,14 @@ Step = RHyperLogLog.addAll(n synthetic 16-byte keys already resident in HBM)
        + (N > 1) RCCL MAX all-reduce of the 16384 registers + count().
 The keys are the SURVEY.md 8d C2 stream (splitmix64, seed 0x5EED0002), each
 rank taking its own contiguous range (weak scaling: n keys per GPU).
-Secondary fields (`bloom`) report the C3 Bloom filter per node (1B inserts at
-1% FPP, EXTENDED mode, sharded over the ranks and merged with the RCCL
-slice-OR, then 1B contains queries sharded over the replicated filter).
+Secondary fields of the same line:
+  `bloom`   the C3 Bloom filter per node (1B inserts at 1% FPP, EXTENDED mode,
+            sharded over the ranks and merged with the RCCL slice-OR, then 1B
+            contains queries sharded over the replicated filter);
+  `c4`      BASELINE configs[3] per GPU: 1B variable-length keys (+ RCCL MAX);
+  `c5`, `c5_zipf`  BASELINE configs[4] per GPU: 1M sketches, 500M pairs per
+            step, uniform and Zipf(1.1) groups, with count / countWith / mergeWith;
+each with its own ms_per_step, roofline and PMC traffic (--no-extra skips them).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--keys N_PER_GPU]
 """
@@ -45,7 +50,8 @@ def pmc_traffic(kernel: str, config: dict):
             continue
         k = d.get("kernels", {}).get(kernel)
         if k and k.get("hbm_bytes_per_launch"):
-            best = {"bytes": k["hbm_bytes_per_launch"], "source": os.path.relpath(p, ROOT)}
+            best = {"bytes": k["hbm_bytes_per_launch"], "source": os.path.relpath(p, ROOT),
+                    "note": k.get("hbm_bytes_note")}
     return best
 
 
@@ -324,73 +330,28 @@ def insert_roofline(n: int, k: int, size: int, secs: float):
             "pipeline_model_frac": model_b / secs / 1e9 / HBM_PEAK_GBS}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    # defaults: the kernel trace shows the first ~12 launches on a box running
-    # slower while the clock settles (profiles/r02_roofline_check.json)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
-                    help="c2: 16-byte keys (headline); c4: variable-length keys; c5: grouped sketches")
-    ap.add_argument("--keys", type=int, default=None,
-                    help="keys (pairs for c5) per GPU; default 1e9 (c2, c4), 5e8 for c5 (4e9 pairs over 8 GPUs)")
-    ap.add_argument("--groups", type=int, default=1_000_000)
-    ap.add_argument("--zipf", type=float, default=0.0,
-                    help="c5: draw groups Zipf(S) over the sketches (SURVEY 8d stress variant; 0 = uniform)")
-    ap.add_argument("--batch-ops", type=int, default=100_000)
-    ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
-    ap.add_argument("--no-bloom", action="store_true")
-    ap.add_argument("--no-bloom-replies", action="store_true")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=128 << 20)
-    ap.add_argument("--cpu-passes", type=int, default=8)
-    ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU figure (the GPU box's CPU share is 16)")
-    args = ap.parse_args()
+WORKLOADS = {
+    "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
+    "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
+    "c5": "Grouped HLL: %d sketches cleared each step, grouped add + count(all) + %d countWith + %d mergeWith "
+          "(BASELINE configs[4]), issued as one pipelined batch per step (the library's async calls, one wait); "
+          "N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
+          "own 1/N of the sketches and running countWith/mergeWith led by them against partners from "
+          "all G, fetched from their owners over RCCL",
+}
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
 
-    # librsketch (system ROCm runtime) is loaded before torch is imported, so
-    # the process has exactly one initialised HIP/HSA runtime (DESIGN.md).
-    from redisson_amd import _lib as _early
+def run_hll(ctx, wl: str, n: int, steps: int, warmup: int, zipf: float = 0.0, groups_n: int = 1_000_000,
+            batch_ops: int = 100_000, bloom_keys: int = 0):
+    """One HLL workload (c2 / c4 / c5) on this rank: inputs generated into HBM
+    (untimed), `warmup` untimed steps, then `steps` timed steps between
+    barriers; the max over ranks of the elapsed time.  Returns the bench
+    fields of that workload (value, ms_per_step, roofline, ...)."""
+    engine, client, rank, world = ctx["engine"], ctx["client"], ctx["rank"], ctx["world"]
+    from redisson_amd import devmem, shard
 
-    _early.load()
-    # The bench support library (generators) too: loaded after torch, its HIP
-    # calls bound to a runtime rocprofv3 had not hooked (a launch through a
-    # null dispatch entry under --kernel-trace).
-    _early.diag()
-    import torch
-    import torch.distributed as dist
-
-    if world > 1:
-        # gloo only ships the RCCL id and the timings; the data path is RCCL.
-        dist.init_process_group("gloo")
-
-    from redisson_amd import _lib, devmem, shard
-    from redisson_amd.client import Config, Redisson
-
-    L = _lib.load()
-    client = Redisson.create(Config(device=local))
-    engine = client.engine
-    if world > 1:
-        shard.init_comm(engine)
-    elif not args.no_bloom and args.workload == "c2":
-        shard.init_comm_single(engine)  # the node-level Bloom merge runs through the same call at N = 1
-    # what RCCL itself reports (ncclCommCount): every rank must have joined
-    rccl_nranks, rccl_rank = shard.comm_info(engine)
-    if world > 1 and (rccl_nranks, rccl_rank) != (world, rank):
-        raise SystemExit("RCCL reports %d ranks (this one %d), WORLD_SIZE is %d (RANK %d)"
-                         % (rccl_nranks, rccl_rank, world, rank))
-    wl = args.workload
-    n = args.keys if args.keys is not None else (500_000_000 if wl == "c5" else 1_000_000_000)
     extra = {}
-    hll = client.getHyperLogLog("bench")
-
-    # Inputs resident in HBM before the timed region (generation untimed).
+    hll = client.getHyperLogLog("bench-" + wl)
     if wl == "c2":
         keys = devmem.gen_keys16(engine, SEED_C2, rank * n, n)
         kb = keys.keys_fixed(n, 16)
@@ -406,10 +367,10 @@ def main():
         from redisson_amd.hyperloglog import GroupedHyperLogLog
         import numpy as np
 
-        G = args.groups
-        if args.zipf > 0:
-            groups, gkeys = devmem.gen_grouped_zipf(engine, SEED_C5, G, args.zipf, rank * n, n)
-            extra = {"group_distribution": "Zipf(%g) over the %d sketches (rank 1 = sketch 0)" % (args.zipf, G)}
+        G = groups_n
+        if zipf > 0:
+            groups, gkeys = devmem.gen_grouped_zipf(engine, SEED_C5, G, zipf, rank * n, n)
+            extra = {"group_distribution": "Zipf(%g) over the %d sketches (rank 1 = sketch 0)" % (zipf, G)}
         else:
             groups, gkeys = devmem.gen_grouped(engine, SEED_C5, G, rank * n, n)
         kb = gkeys.keys_fixed(n, 16)
@@ -421,15 +382,15 @@ def main():
         own_first, own_count = shard.owned_range(G, world, rank)
         own_ids = np.arange(own_first, own_first + own_count, dtype=np.uint64)
         rng = np.random.default_rng(5 + rank)
-        cw = np.stack([rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64),
-                       rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)], 1)
-        md = rng.integers(own_first, own_first + own_count, size=args.batch_ops, dtype=np.uint64)
-        ms_ = rng.integers(0, G, size=args.batch_ops, dtype=np.uint64)
+        cw = np.stack([rng.integers(own_first, own_first + own_count, size=batch_ops, dtype=np.uint64),
+                       rng.integers(0, G, size=batch_ops, dtype=np.uint64)], 1)
+        md = rng.integers(own_first, own_first + own_count, size=batch_ops, dtype=np.uint64)
+        ms_ = rng.integers(0, G, size=batch_ops, dtype=np.uint64)
         remote = np.concatenate([cw[:, 1], ms_])
         kern, unit_bytes = "hll_add_grouped16", 20.0 * n
         bufs = [groups, gkeys]
         counts_out = np.empty(max(G, own_count), np.uint64)  # the caller's reply buffers, reused across steps
-        cw_out = np.empty(args.batch_ops, np.uint64)
+        cw_out = np.empty(batch_ops, np.uint64)
 
     def step():
         if wl == "c5":
@@ -453,16 +414,18 @@ def main():
             return int(counts_out[0])
         hll.addAll(kb)
         if world > 1:
-            slot = client._hll_slot("bench", False)
+            slot = client._hll_slot("bench-" + wl, False)
             shard.hll_allreduce(slot.pool, slot.id)  # RCCL MAX over xGMI
         return hll.count()
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
 
     def barrier():
         engine.sync()
         if world > 1:
+            import torch.distributed as dist
+
             dist.barrier()
 
     engine.prof_reset()
@@ -470,15 +433,16 @@ def main():
     barrier()
     cards = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        card = step()
-        cards.append(card)
+    for _ in range(steps):
+        cards.append(step())
     barrier()
     elapsed = time.perf_counter() - t0
     cards_agree = None
     if world > 1 and wl != "c5":
         # after each step's RCCL MAX all-reduce every rank holds the same
         # registers, so every rank's count() of every step must agree
+        import torch.distributed as dist
+
         everyone = [None] * world
         dist.all_gather_object(everyone, cards)
         cards_agree = all(c == cards for c in everyone)
@@ -502,37 +466,24 @@ def main():
                                                        "hll_allreduce", "hll_allreduce_pool",
                                                        "hll_reducescatter_pool", "hll_fetch_rows", "hll_clear")}
     if world > 1:
+        import torch
+        import torch.distributed as dist
+
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_keys = n * world * args.steps
-    value = total_keys / elapsed
+    value = n * world * steps / elapsed
     avg_launch_s = (add_ms / 1e3) / max(1, add_launches)
     achieved = unit_bytes / avg_launch_s / 1e9  # algorithmic bytes per launch / launch time
-    workloads = {
-        "c2": "HLL addAll of 16-byte keys + count() (BASELINE configs[1])",
-        "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
-        "c5": "Grouped HLL: %d sketches cleared each step, grouped add + count(all) + %d countWith + %d mergeWith "
-              "(BASELINE configs[4]), issued as one pipelined batch per step (the library's async calls, one wait); "
-              "N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
-              "own 1/N of the sketches and running countWith/mergeWith led by them against partners from "
-              "all G, fetched from their owners over RCCL" % (args.groups, args.batch_ops, args.batch_ops),
-    }
-    result = {
-        "metric": "HLL adds/s + Bloom lookups/s (node), % HBM roofline, 1/2/4/8 MI355X",
+    res = {
         "value": value,
-        "unit": "keys/s",
+        "unit": "keys/s" if wl != "c5" else "pairs/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (splitmix64 %s stream generated on device, untimed)" % wl.upper(),
-        "config": dict({"workload": workloads[wl],
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
+        "config": dict({"workload": WORKLOADS[wl] % ((groups_n, batch_ops, batch_ops) if wl == "c5" else ()),
                         "keys_per_gpu": n, "global_keys_per_step": n * world,
                         "parallelism": "key-stream sharding, RCCL MAX all-reduce of the registers" if world > 1
                         else "single GPU", "redis_semantics": "3.2.0"}, **extra),
@@ -543,47 +494,151 @@ def main():
                      "reduce_avg_ms": red_ms / max(1, red_launches),
                      "algorithmic_bytes_per_launch": unit_bytes},
         "side_kernels_ms_per_launch": {k: (v[0] / v[1] if v[1] else None) for k, v in side.items()},
-        "count": int(card),
-        "rccl_nranks": rccl_nranks,
+        "count": int(cards[-1]),
     }
     if cards_agree is not None:
-        result["count_identical_across_ranks_every_step"] = cards_agree
-    pmc_cfg = {"workload": wl, "keys": n, "zipf": args.zipf,
-               "bloom_keys": args.bloom_keys if (wl == "c2" and not args.no_bloom) else 0}
+        res["count_identical_across_ranks_every_step"] = cards_agree
+    pmc_cfg = {"workload": wl, "keys": n, "zipf": zipf, "bloom_keys": bloom_keys}
     tr = pmc_traffic("hll_add_grouped_partitioned" if stage_ms else kern + "_kernel", pmc_cfg)
     if tr:
-        result["roofline"]["traffic"] = tr["bytes"]
-        result["roofline"]["traffic_source"] = tr["source"]
+        res["roofline"]["traffic"] = tr["bytes"]
+        res["roofline"]["traffic_source"] = tr["source"]
+        if tr.get("note"):
+            res["roofline"]["traffic_note"] = tr["note"]
     if wl == "c5":
         # The grouped add must also write every touched sketch once whatever
         # the update order (16 KiB per touched sketch; at 500 pairs/sketch all
         # G are touched; the pool was just cleared, so nothing need be read):
         # the state-inclusive floor.
-        touched = args.groups * -math.expm1(-n / args.groups)  # expected sketches hit by n uniform pairs
-        if args.zipf > 0:  # expected sketches hit by n Zipf pairs: sum over ranks of 1 - (1 - p_r)^n
+        touched = groups_n * -math.expm1(-n / groups_n)  # expected sketches hit by n uniform pairs
+        if zipf > 0:  # expected sketches hit by n Zipf pairs: sum over ranks of 1 - (1 - p_r)^n
             import numpy as np
 
-            w = np.arange(1, args.groups + 1, dtype=np.float64) ** -args.zipf
+            w = np.arange(1, groups_n + 1, dtype=np.float64) ** -zipf
             touched = float(-np.expm1(n * np.log1p(-w / w.sum())).sum())
         state = 1.0 * touched * 16384  # written once; the cleared pool need not be read
-        result["roofline"]["state_bytes_per_launch"] = state
-        result["roofline"]["frac_incl_state"] = (unit_bytes + state) / avg_launch_s / 1e9 / HBM_PEAK_GBS
+        res["roofline"]["state_bytes_per_launch"] = state
+        res["roofline"]["frac_incl_state"] = (unit_bytes + state) / avg_launch_s / 1e9 / HBM_PEAK_GBS
         if stage_ms:
-            result["roofline"]["stage_ms_per_launch"] = stage_ms
+            res["roofline"]["stage_ms_per_launch"] = stage_ms
+        res["add_ms_per_step"] = avg_launch_s * 1e3
     for b in bufs:
         b.free()
     if wl == "c5":
         pool.close()
-    if wl == "c2" and not args.no_bloom:  # every rank: the node-level Bloom is collective
+    else:
+        hll.delete()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    # defaults: the kernel trace shows the first ~12 launches on a box running
+    # slower while the clock settles (profiles/r02_roofline_check.json)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
+                    help="c2: 16-byte keys (headline); c4: variable-length keys; c5: grouped sketches")
+    ap.add_argument("--keys", type=int, default=None,
+                    help="keys (pairs for c5) per GPU; default 1e9 (c2, c4), 5e8 for c5 (4e9 pairs over 8 GPUs)")
+    ap.add_argument("--groups", type=int, default=1_000_000)
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="c5: draw groups Zipf(S) over the sketches (SURVEY 8d stress variant; 0 = uniform)")
+    ap.add_argument("--batch-ops", type=int, default=100_000)
+    ap.add_argument("--bloom-keys", type=int, default=1_000_000_000)
+    ap.add_argument("--no-bloom", action="store_true")
+    ap.add_argument("--no-bloom-replies", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="c2 only: skip the secondary C4 / C5 / C5-Zipf workloads (keys c4, c5, c5_zipf)")
+    ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--extra-warmup", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=128 << 20)
+    ap.add_argument("--cpu-passes", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU figure (the GPU box's CPU share is 16)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+
+    # librsketch (system ROCm runtime) is loaded before torch is imported, so
+    # the process has exactly one initialised HIP/HSA runtime (DESIGN.md).
+    from redisson_amd import _lib as _early
+
+    _early.load()
+    # The bench support library (generators) too: loaded after torch, its HIP
+    # calls bound to a runtime rocprofv3 had not hooked (a launch through a
+    # null dispatch entry under --kernel-trace).
+    _early.diag()
+    import torch.distributed as dist
+
+    if world > 1:
+        # gloo only ships the RCCL id and the timings; the data path is RCCL.
+        dist.init_process_group("gloo")
+
+    from redisson_amd import devmem, shard
+    from redisson_amd.client import Config, Redisson
+
+    client = Redisson.create(Config(device=local))
+    engine = client.engine
+    if world > 1:
+        shard.init_comm(engine)
+    elif not args.no_bloom and args.workload == "c2":
+        shard.init_comm_single(engine)  # the node-level Bloom merge runs through the same call at N = 1
+    # what RCCL itself reports (ncclCommCount): every rank must have joined
+    rccl_nranks, rccl_rank = shard.comm_info(engine)
+    if world > 1 and (rccl_nranks, rccl_rank) != (world, rank):
+        raise SystemExit("RCCL reports %d ranks (this one %d), WORLD_SIZE is %d (RANK %d)"
+                         % (rccl_nranks, rccl_rank, world, rank))
+    ctx = {"engine": engine, "client": client, "rank": rank, "world": world}
+    wl = args.workload
+    n = args.keys if args.keys is not None else (500_000_000 if wl == "c5" else 1_000_000_000)
+    bloom_on = wl == "c2" and not args.no_bloom
+    head = run_hll(ctx, wl, n, args.steps, args.warmup, zipf=args.zipf, groups_n=args.groups,
+                   batch_ops=args.batch_ops, bloom_keys=args.bloom_keys if bloom_on else 0)
+    result = {
+        "metric": "HLL adds/s + Bloom lookups/s (node), % HBM roofline, 1/2/4/8 MI355X",
+        "value": head.pop("value"),
+        "unit": head.pop("unit"),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": head.pop("ms_per_step"),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (splitmix64 %s stream generated on device, untimed)" % wl.upper(),
+    }
+    for k in ("n_gpus", "steps", "warmup"):
+        head.pop(k)
+    result.update(head)
+    result["rccl_nranks"] = rccl_nranks
+    if bloom_on:  # every rank: the node-level Bloom is collective
         bn = args.bloom_keys
         result["bloom"] = bloom_bench(engine, bn, bn, reps=2, rank=rank, world=world,
                                       with_replies=not args.no_bloom_replies)
-        tr = pmc_traffic("bloom_insert_supertile", pmc_cfg) if world == 1 else None
+        tr = pmc_traffic("bloom_insert_supertile", {"workload": wl, "keys": n, "zipf": args.zipf, "bloom_keys": bn}) \
+            if world == 1 else None
         if tr:
             ir = result["bloom"]["insert_roofline"]
             ir["traffic"] = tr["bytes"]
             ir["traffic_source"] = tr["source"]
             ir["traffic_GBps"] = tr["bytes"] * ir["achieved"] / ir["algorithmic_bytes"]  # traffic / insert time
+    if wl == "c2" and not args.no_extra:
+        # the other per-GPU BASELINE configs, each with its own timing and
+        # roofline: C4 (configs[3] per GPU: 1B variable-length keys), C5
+        # (configs[4] per GPU: 1M sketches, 500M pairs) uniform and Zipf(1.1)
+        for key, w2, n2, z in (("c4", "c4", 1_000_000_000, 0.0), ("c5", "c5", 500_000_000, 0.0),
+                               ("c5_zipf", "c5", 500_000_000, 1.1)):
+            t0 = time.perf_counter()
+            result[key] = run_hll(ctx, w2, n2, args.extra_steps, args.extra_warmup, zipf=z, groups_n=args.groups,
+                                  batch_ops=args.batch_ops)
+            log("%s: %.3f ms/step (%.1f s)" % (key, result[key]["ms_per_step"], time.perf_counter() - t0))
     if rank == 0 and world == 1 and wl == "c2" and not args.no_cpu:
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_passes, thr)

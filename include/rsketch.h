@@ -211,8 +211,14 @@ int rsk_hll_get_registers(rsk_hll *h, uint64_t id, uint8_t *out, uint32_t locati
  * this pool (each call re-derives the pool's cached state from that point). */
 void *rsk_hll_device_registers(rsk_hll *h);
 
-/* GET of the key as a Redis dense "HYLL" string (12304 bytes; card bytes as
- * Redis would hold them).  RBitSet.toByteArray-style export. */
+/* GET of the key as a Redis "HYLL" string, in the encoding Redis 3.2 would
+ * hold it in: SPARSE (16-byte header + canonical opcodes, at most
+ * hll-sparse-max-bytes = 3000 bytes) while the key never left the sparse
+ * encoding, else DENSE (12304 bytes; dense for good once promoted, after
+ * PFMERGE and after a multi-GPU merge); a string SET by rsk_hll_import_redis
+ * and not written since comes back byte for byte.  Card bytes as Redis would
+ * hold them.  cap must be >= 12304; *len = 0 for a missing key (nil).
+ * RBitSet.toByteArray-style export. */
 int rsk_hll_export_redis(rsk_hll *h, uint64_t id, uint8_t *buf, size_t cap, size_t *len);
 /* SET of a Redis HLL string (dense or sparse); validated like
  * isHLLObjectOrReply / hllMerge.  Replaces the key. */

@@ -51,6 +51,11 @@ int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
  * fallback (a group's pending probes overflowed its LDS tables). */
 int rsk_diag_reply_stats(rsk_ctx *ctx, uint64_t *pending_groups, uint64_t *fallbacks);
 
+/* Marks a context dead, as a device error on one of its streams does: every
+ * later call but rsk_shutdown fails with RSK_ERR_DEVICE (tests of the
+ * bindings' release paths). */
+int rsk_diag_mark_dead(rsk_ctx *ctx);
+
 /* --------------------------------------------------------- diagnostics */
 /* Memory-system microbenchmark on a device buffer (roofline denominators):
  * mode 0 stream read, 1 random 4 B gathers, 2 random 4 B atomicOr,
@@ -58,7 +63,9 @@ int rsk_diag_reply_stats(rsk_ctx *ctx, uint64_t *pending_groups, uint64_t *fallb
  * nontemporal stores, 6 scattered segment reads of n_ops (256, 512 or 1024)
  * bytes, one uint4 per lane, every byte of the largest power-of-two number
  * of segments that fits read once (FETCH_SIZE calibration), 7 stream copy
- * (buffer halves) with the loads and the stores in different waves.
+ * (buffer halves) with the loads and the stores in different waves, 8 stream
+ * read with 4 B per lane, 9 scattered segment reads of n_ops (128 or 256)
+ * bytes, one dword per lane (FETCH_SIZE calibration of 4-byte loads).
  * *ms = device time of the one launch. */
 int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
 /* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */

@@ -81,8 +81,13 @@ public final class GpuSketchContext {
         RSketchNative.sync(space);
     }
 
+    /* Releases the context even when it is dead (a device error: sync() then
+     * throws, and every later call fails): the native shutdown always runs. */
     public void shutdown() {
-        RSketchNative.sync(space);
-        RSketchNative.shutdown(space);
+        try {
+            RSketchNative.sync(space);
+        } finally {
+            RSketchNative.shutdown(space);
+        }
     }
 }

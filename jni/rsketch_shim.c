@@ -305,6 +305,11 @@ int rsk_shim_shutdown(int64_t h) {
   return rc;
 }
 
+rsk_ctx *rsk_shim_context(int64_t h) {
+  space *s = sp(h);
+  return s ? s->ctx : NULL;
+}
+
 int rsk_shim_sync(int64_t h) {
   ENTER();
   space *s = sp(h);

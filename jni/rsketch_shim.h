@@ -73,6 +73,9 @@ int rsk_shim_keys(rsk_shim_buf keys, rsk_shim_buf offsets, int64_t n, rsk_keys *
  * refused with IllegalArgumentException like the reference (:226-227). */
 int rsk_shim_init(int32_t device, int32_t extended_bloom, int64_t *space_out);
 int rsk_shim_shutdown(int64_t space);
+/* The library context of a space (for callers of the C ABI itself, e.g. the
+ * support library of include/rsketch_diag.h); NULL for a null space. */
+rsk_ctx *rsk_shim_context(int64_t space);
 /* Waits until every call issued so far has completed and its callback has
  * returned (rsk_sync).  Callbacks may call the shim again (rsketch.h,
  * rsk_done_fn): this wait does not hold the context. */

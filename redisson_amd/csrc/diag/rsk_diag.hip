@@ -8,6 +8,9 @@
 //   mode 5: streaming write (16 B/lane nontemporal stores) -> GB/s
 //   mode 6: scattered 256 B / 512 B / 1 KiB segment reads  -> GB/s (FETCH_SIZE calibration)
 //   mode 7: streaming copy, loads and stores in different waves -> GB/s (read+write)
+//   mode 8: streaming read, 4 B/lane (the grouped pass's id loads) -> GB/s (FETCH_SIZE calibration)
+//   mode 9: scattered 128 B / 256 B segment reads, one dword per lane (the
+//           fine-bin pass's medium segments)                    -> GB/s (FETCH_SIZE calibration)
 // Indices come from splitmix64(i), as uniform as the Bloom probe stream.
 // Also: the route overrides of a context (rsk_diag_set_route) and the timed
 // launches of the kernels' tuning variants (rsk_diag_kernels.hip).
@@ -42,6 +45,27 @@ __global__ __launch_bounds__(256) void diag_segment_read(const uint4* __restrict
     const uint64_t s = (g * 0x9E3779B97F4A7C15ull) & mask;
     const uint4 v = ld_nt16(p + s * L + lane);
     acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// Modes 8 / 9: the same with 4-byte loads (a dword per lane; L lanes per
+// segment in mode 9, L = 0 for a plain stream).
+template <int L>
+__global__ __launch_bounds__(256) void diag_read4(const uint32_t* __restrict__ p, uint64_t n4, uint64_t nseg_log,
+                                                  uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  if (L == 0) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x)
+      acc ^= p[i];
+  } else {
+    const uint64_t nseg = 1ull << nseg_log, mask = nseg - 1;
+    const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / (L ? L : 1), lane = threadIdx.x % (L ? L : 1);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x / (L ? L : 1);
+    for (uint64_t g = g0; g < nseg; g += gs) {
+      const uint64_t s = (g * 0x9E3779B97F4A7C15ull) & mask;
+      acc ^= p[s * L + lane];
+    }
   }
   if (acc == 0x9E3779B9u) sink[0] = acc;
 }
@@ -183,6 +207,14 @@ int rsk_diag_reply_stats(rsk_ctx* c, uint64_t* pending_groups, uint64_t* fallbac
   });
 }
 
+int rsk_diag_mark_dead(rsk_ctx* c) {
+  return diag::guarded([&] {
+    diag::need(c != nullptr, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    c->dead = true;
+  });
+}
+
 int rsk_diag_hll_variant(rsk_ctx* c, int variant, const void* dev_keys16, uint64_t n, double* ms) {
   return diag::guarded([&] {
     diag::need(c && dev_keys16 && ms && n, "bad arguments");
@@ -204,12 +236,13 @@ int rsk_diag_bloom_contains_variant(rsk_ctx* c, int variant, rsk_bloom* bf, cons
 
 int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t nops, double* ms) {
   return diag::guarded([&] {
-    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 7, "bad arguments");
+    diag::need(c && buf && ms && bytes >= 64 && mode >= 0 && mode <= 9, "bad arguments");
     // mode 6: segment reads of nops bytes (256, 512 or 1024) over the largest
-    // power-of-two number of segments that fits
+    // power-of-two number of segments that fits (mode 9: 128 or 256 B)
     diag::need(mode != 6 || nops == 256 || nops == 512 || nops == 1024, "segment bytes must be 256, 512 or 1024");
+    diag::need(mode != 9 || nops == 128 || nops == 256, "segment bytes must be 128 or 256");
     uint64_t nseg_log = 0;
-    if (mode == 6)
+    if (mode == 6 || mode == 9)
       while ((2ull << nseg_log) * nops <= bytes) ++nseg_log;
     diag::Lock l(c);
     uint32_t* sink = reinterpret_cast<uint32_t*>(c->d_small + 512);
@@ -252,6 +285,18 @@ int rsk_diag_membench(rsk_ctx* c, int mode, void* buf, uint64_t bytes, uint64_t 
             hipLaunchKernelGGL(diag_segment_read<64>, dim3(grid), dim3(256), 0, c->stream, p, nseg_log, sink);
           break;
         }
+        case 8:
+          hipLaunchKernelGGL(diag_read4<0>, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<const uint32_t*>(buf),
+                             bytes / 4, 0ull, sink);
+          break;
+        case 9:
+          if (nops == 128)
+            hipLaunchKernelGGL(diag_read4<32>, dim3(grid), dim3(256), 0, c->stream,
+                               reinterpret_cast<const uint32_t*>(buf), bytes / 4, nseg_log, sink);
+          else
+            hipLaunchKernelGGL(diag_read4<64>, dim3(grid), dim3(256), 0, c->stream,
+                               reinterpret_cast<const uint32_t*>(buf), bytes / 4, nseg_log, sink);
+          break;
         default: {
           const uint64_t half = bytes / 32;  // uint4 elements per half
           hipLaunchKernelGGL(diag_copy, dim3(grid), dim3(256), 0, c->stream, reinterpret_cast<const uint4*>(buf),

@@ -6,7 +6,10 @@ script gives FETCH per dispatch against the bytes read:
   python scripts/fetch_calib.py            (prints the dispatch order)
 
 dispatches: stream read 4 GiB; scattered segment reads of 256, 512 and 1024 B
-(one uint4 per lane: the Bloom apply / rp_apply / hll_gapply record loads)."""
+(one uint4 per lane: the Bloom apply / rp_apply / hll_gapply record loads);
+a 4 B/lane stream (hll_gpart1t's group ids, hll_gapply_extra's records) and
+scattered 128 / 256 B segments read one dword per lane (the C5 fine-bin
+pass's medium segments: hll_gcount2t / hll_gpart2t)."""
 import ctypes
 import os
 import sys
@@ -16,7 +19,8 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import _lib, devmem  # noqa: E402
 
-CASES = [("stream_read", 0, 0), ("segment_256B", 6, 256), ("segment_512B", 6, 512), ("segment_1KiB", 6, 1024)]
+CASES = [("stream_read", 0, 0), ("segment_256B", 6, 256), ("segment_512B", 6, 512), ("segment_1KiB", 6, 1024),
+         ("stream4_read", 8, 0), ("segment4_128B", 9, 128), ("segment4_256B", 9, 256)]
 
 
 def gathers():

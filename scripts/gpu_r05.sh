@@ -1,0 +1,75 @@
+#!/bin/bash
+# Round-5 GPU sessions (conventions of scripts/gpu_r03.sh: every GPU step under
+# its own time limit, the first failure ends the script, no retries).
+#   scripts/gpu_r05.sh PART[,PART...] [args]
+#     tests   : the -m gpu suite (or the given test paths), then smoke
+#     sel     : only the given test paths / -k expression
+#     bench   : the default bench line (C2 + Bloom + C4/C5/C5-Zipf extras + CPU baselines)
+#     benchq  : the same without the CPU baselines
+#     c4|c5|c5z : one workload alone
+#     calib   : FETCH_SIZE calibration per read pattern -> gpurun_out/r05_fetch_calib.json
+#     prof    : kernel trace of the headline bench + its FETCH/WRITE passes (r05_pmc*)
+#     prof4|prof5|prof5z : kernel trace + FETCH/WRITE passes of the C4 / C5 / C5-Zipf bench
+#     replies : add() with replies alone under rocprofv3 (trace, FETCH, WRITE)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+PART=${1:-tests}
+shift || true
+TAG=${TAG:-r05}
+step() { local name=$1 lim=$2; shift 2; echo "== $name"; timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "rc=$rc" >> "gpurun_out/$name.log"; tail -3 "gpurun_out/$name.log" | cut -c1-600; return $rc; }
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+# kernel trace + FETCH + WRITE passes of one command, summarised by pmc_summary.py
+profw() {  # name limit keys config_json cmd...
+  local name=$1 lim=$2 keys=$3 cfg=$4; shift 4
+  rm -rf gpurun_out/${name}_stats gpurun_out/${name}_fetch gpurun_out/${name}_write
+  step ${name}_stats $lim rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${name}_stats -o run -- "$@" || return 1
+  step ${name}_fetch $lim rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${name}_fetch -o run -- "$@" || return 1
+  step ${name}_write $lim rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${name}_write -o run -- "$@" || return 1
+  python3 scripts/pmc_summary.py gpurun_out/${name}_stats gpurun_out/${name}_fetch gpurun_out/${name}_write \
+    gpurun_out/${TAG}_${name} "$keys" "$cfg" > /dev/null || return 1
+  find gpurun_out/${name}_stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_${name}_kernel_stats.csv \;
+}
+for p in ${PART//,/ }; do
+  case $p in
+    tests)
+      step pytest_gpu 900 $PYT -m gpu ${@:-tests} || exit 1
+      step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    sel)
+      step pytest_sel 600 $PYT -m gpu "$@" || exit 1 ;;
+    bench)
+      step bench 500 python bench.py || exit 1 ;;
+    benchq)
+      step benchq 400 python bench.py --no-cpu || exit 1 ;;
+    c4)
+      step bench_c4 200 python bench.py --workload c4 || exit 1 ;;
+    c5)
+      step bench_c5 200 python bench.py --workload c5 || exit 1 ;;
+    c5z)
+      step bench_c5_zipf 200 python bench.py --workload c5 --zipf 1.1 || exit 1 ;;
+    calib)
+      rm -rf gpurun_out/calib_fetch
+      step calib 120 python3 scripts/fetch_calib.py || exit 1
+      step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- python3 scripts/fetch_calib.py || exit 1
+      python3 scripts/calib_summary.py gpurun_out/calib_fetch gpurun_out/${TAG}_fetch_calib.json > /dev/null || exit 1 ;;
+    prof)
+      profw pmc 300 1000000000 '{"workload": "c2", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
+        python3 bench.py --no-cpu --no-bloom-replies --no-extra || exit 1
+      python3 scripts/prof_agree.py gpurun_out/pmc_stats gpurun_out/pmc_stats.log gpurun_out/${TAG}_roofline_check.json || true ;;
+    prof4)
+      profw pmc_c4 200 1000000000 '{"workload": "c4", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 0}' \
+        python3 bench.py --workload c4 --steps 10 --warmup 3 || exit 1 ;;
+    prof5)
+      profw pmc_c5 200 500000000 '{"workload": "c5", "keys": 500000000, "zipf": 0.0, "bloom_keys": 0}' \
+        python3 bench.py --workload c5 --steps 10 --warmup 3 || exit 1 ;;
+    prof5z)
+      profw pmc_c5_zipf 200 500000000 '{"workload": "c5", "keys": 500000000, "zipf": 1.1, "bloom_keys": 0}' \
+        python3 bench.py --workload c5 --zipf 1.1 --steps 10 --warmup 3 || exit 1 ;;
+    replies)
+      profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
+        python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;
+    *) echo "unknown part $p"; exit 2 ;;
+  esac
+done
+exit 0

@@ -13,7 +13,8 @@ traffic only when its own configuration equals it.
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a wide (16 B/lane)
 coalesced streaming read, so the read side is doubled for the streaming
-hll_add16 kernel (the correction is recorded next to the raw value).
+hll_add16 kernel (the correction is recorded next to the raw value); every
+other kernel takes the factor calibrated for its read pattern (READS below).
 """
 import csv
 import glob
@@ -56,9 +57,54 @@ def counters(d, counter):
     return {k: sum(v) / len(v) for k, v in vals.items()}, p
 
 
+# Bytes per FETCH_SIZE byte by read pattern (MI355X_MICROARCH.md HBM: "calibrate
+# on a known byte count in your own access pattern"), from scripts/fetch_calib.py
+# under rocprofv3 (profiles/r05_fetch_calib.json; r03 for the uint4 patterns).
+def load_calib():
+    cal = {}
+    for name in ("r03_fetch_calib.json", "r05_fetch_calib.json"):
+        p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", name)
+        if os.path.exists(p):
+            for k, v in json.load(open(p)).get("patterns", {}).items():
+                cal[k] = v["bytes_over_fetch_bytes"]
+    cal.update(json.loads(os.environ.get("FETCH_CALIB", "{}")))
+    return cal
+
+
+# Read pattern of each kernel's dominant loads: a pattern name, or a list of
+# (pattern, share of the algorithmic read bytes) for kernels with two streams.
+READS = {
+    "hll_add16_kernel": "stream_read",                     # 16 B/lane nontemporal key stream
+    "hll_add_var_staged_kernel": "stream_read",            # C4: 16 B/lane coalesced tile staging (blob + offsets)
+    "hll_gpart1t_kernel": [("stream_read", 0.8), ("stream4_read", 0.2)],  # 16 B keys + 4 B group ids per pair
+    "hll_gpart1_kernel": [("stream_read", 0.8), ("stream4_read", 0.2)],
+    "hll_gcount_kernel": "stream_read",                    # uint4 id loads
+    "hll_gcount2t_kernel": "segment4_128B",                # ~33-record segments, one dword per lane
+    "hll_gpart2t_kernel": "segment4_128B",
+    "hll_gcount2p_kernel": "stream_read",                  # uint4 run loads
+    "hll_gpart2p_kernel": "stream_read",
+    "hll_gapply_kernel": "stream_read",                    # uint4 loads of each fine bin's contiguous run
+    "hll_gapply_extra_kernel": "stream4_read",             # 4 B/lane loads of a hot bin's extra chunks
+}
+
+
+def read_factor(kernel, cal):
+    pat = READS.get(kernel)
+    if pat is None:
+        return 1.0, "raw (uncalibrated pattern)"
+    if isinstance(pat, str):
+        pat = [(pat, 1.0)]
+    if not all(p in cal for p, _ in pat):
+        return 1.0, "raw (no calibration for %s)" % ", ".join(p for p, _ in pat if p not in cal)
+    # corrected = raw x (sum of shares) / (sum of share / factor): each stream's raw share scaled by its factor
+    f = sum(w for _, w in pat) / sum(w / cal[p] for p, w in pat)
+    return f, " + ".join("%s x%.3f (%.0f%%)" % (p, cal[p], 100 * w) for p, w in pat)
+
+
 def main():
     sdir, fdir, wdir, prefix, keys = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5])
     config = json.loads(sys.argv[6]) if len(sys.argv) > 6 else None
+    cal = load_calib()
     st, sp = stats(sdir)
     fe, fp = counters(fdir, "FETCH_SIZE")
     wr, wp = counters(wdir, "WRITE_SIZE")
@@ -67,15 +113,23 @@ def main():
         e = dict(st.get(k, {}))
         if k in fe:
             e["FETCH_SIZE_kib_raw"] = fe[k]
+            f, how = read_factor(k, cal)
+            e["fetch_bytes_corrected"] = fe[k] * 1024 * f
+            e["fetch_correction"] = how
         if k in wr:
             e["WRITE_SIZE_kib"] = wr[k]
         if k == "hll_add16_kernel":
             e["keys_per_launch"] = keys
             e["algorithmic_bytes_per_launch"] = 16 * keys
             if k in fe:
-                e["fetch_bytes_per_launch"] = fe[k] * 1024 * 2  # gfx950 wide-stream correction
+                e["fetch_bytes_per_launch"] = e["fetch_bytes_corrected"]  # gfx950 wide-stream correction
             if k in fe and k in wr:
                 e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + wr[k] * 1024
+        if k == "hll_add_var_staged_kernel" and k in fe and k in wr:
+            e["keys_per_launch"] = keys
+            e["hbm_bytes_per_launch"] = e["fetch_bytes_corrected"] + wr[k] * 1024
+            e["hbm_bytes_note"] = "FETCH_SIZE x %s + WRITE_SIZE" % e["fetch_correction"]
+            kern["hll_add_var_kernel"] = e  # bench.py's label of the C4 launch
         if k == "hll_add_grouped16_kernel" and k in fe and k in wr:
             # mixed access (16 B key stream + 4 B group ids + random 4 B register
             # words): no calibrated correction exists, so the raw counters are used
@@ -93,14 +147,19 @@ def main():
     extras = tuple(p for p in ("hll_gextra_list_kernel", "hll_gapply_extra_kernel") if p in fe and p in wr)
     if "hll_gapply_kernel" in kern and all(p in fe and p in wr for p in parts):
         parts = parts + extras
-        # the partitioned grouped PFADD as one unit (only in a C5-only run): raw
-        # counters summed over its stages
+        # the partitioned grouped PFADD as one unit (only in a C5-only run): per
+        # stage, FETCH corrected by its read pattern's calibration, plus WRITE
+        raw = sum((fe[p] + wr[p]) * 1024 for p in parts)
         kern["hll_add_grouped_partitioned"] = {
             "keys_per_launch": keys, "algorithmic_bytes_per_launch": 20 * keys,
-            "hbm_bytes_per_launch": sum((fe[p] + wr[p]) * 1024 for p in parts),
-            "stages": list(parts),
-            "hbm_bytes_note": "raw FETCH_SIZE + WRITE_SIZE of the stages per call (16 B key stream, 4 B records, "
-                              "16 KiB sketch rows; not corrected)"}
+            "hbm_bytes_per_launch": sum(kern[p]["fetch_bytes_corrected"] + wr[p] * 1024 for p in parts),
+            "hbm_bytes_raw": raw,
+            "stages": {p: {"fetch_bytes_corrected": kern[p]["fetch_bytes_corrected"],
+                           "write_bytes": wr[p] * 1024, "fetch_correction": kern[p]["fetch_correction"],
+                           "avg_ns": kern[p].get("avg_ns")} for p in parts},
+            "hbm_bytes_note": "per call: every stage's FETCH_SIZE corrected by the calibrated factor of its read "
+                              "pattern (scripts/fetch_calib.py) + WRITE_SIZE (exact for 16 B stores; raw for the "
+                              "fine-bin pass's 4 B scattered stores)"}
     # The Bloom insert at 1B keys, k = 7 (one chunk: one dispatch of each stage per insert call),
     # per stage and summed.  Append pipeline (default): sa1 reads the keys, sa2 its sub-regions and
     # apply its tiles with 16 B/lane loads, so FETCH is doubled per the guide; the header pipeline
@@ -108,7 +167,7 @@ def main():
     # Round 3: sa2 writes 16-bit records (bloom_sa2h_kernel) that bloom_sah_apply_kernel reads with
     # quarter-wave 256 B segment loads; the doubling is applied to it only as far as
     # scripts/fetch_calib.py shows it holds for that pattern (FETCH_CALIB, below).
-    calib = json.loads(os.environ.get("FETCH_CALIB", "{}"))
+    calib = cal
     for name, st, wide in (("bloom_insert_supertile",
                             ("bloom_sa1_kernel", "sah_size_kernel", "st_offsets_kernel", "bloom_sa2h_kernel",
                              "bloom_sah_apply_kernel"),
@@ -128,8 +187,9 @@ def main():
                       "wide_read_stages_doubled": list(wide),
                       "note": "per insert call = one dispatch of each stage"}
     doc = {"config": config, "sources": {"stats": sp, "fetch": fp, "write": wp}, "kernels": kern,
-           "note": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch (mean over dispatches); fetch doubled for "
-                   "hll_add16_kernel per MI355X_MICROARCH.md HBM section"}
+           "calibration": cal,
+           "note": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch (mean over dispatches); fetch_bytes_corrected = "
+                   "FETCH_SIZE x the calibrated factor of the kernel's read pattern (MI355X_MICROARCH.md HBM)"}
     with open(prefix + ".json", "w") as f:
         json.dump(doc, f, indent=1)
     lines = ["| kernel | calls | avg us | % time | FETCH_SIZE KiB (raw) | WRITE_SIZE KiB |", "|---|---|---|---|---|---|"]

@@ -31,6 +31,8 @@
 #include <unistd.h>
 
 #include "../../oracle/rsk_oracle.h"
+#include "rsketch_diag.h"
+#include "rsketch_shim.h"
 
 static int failures;
 #define CHECK(cond)                                                  \
@@ -487,6 +489,26 @@ int main(void) {
     CHECK(Java_org_redisson_gpu_RSketchNative_hllCount(env, CLS, SPACE, jstr("jbloom")) == 0 && m_ExceptionCheck(env));
     m_ExceptionClear(env);
     CHECK(Java_org_redisson_gpu_RSketchNative_type(env, CLS, SPACE, bs) == 3);
+  }
+
+  /* a context marked dead (as after a device error on its streams): every call
+   * and sync() throw RedisException, and the native shutdown that
+   * GpuSketchContext.shutdown() runs in its finally still releases it */
+  {
+    const jlong space3 = Java_org_redisson_gpu_RSketchNative_init(env, CLS, 0, JNI_FALSE);
+    CHECK(space3 != 0);
+    Java_org_redisson_gpu_RSketchNative_hllAddAsync(env, CLS, space3, nm, REB.keys, REB.offs, 1000, completion(70));
+    Java_org_redisson_gpu_RSketchNative_sync(env, CLS, space3);
+    CHECK(C[70].fired == 1 && C[70].status == 0);
+    CHECK(rsk_diag_mark_dead(rsk_shim_context((int64_t)space3)) == RSK_OK);
+    CHECK(Java_org_redisson_gpu_RSketchNative_hllCount(env, CLS, space3, nm) == 0 && m_ExceptionCheck(env) &&
+          strcmp(t_exc, "org/redisson/client/RedisException") == 0);
+    m_ExceptionClear(env);
+    Java_org_redisson_gpu_RSketchNative_sync(env, CLS, space3); /* try { sync } ... */
+    CHECK(m_ExceptionCheck(env) && strcmp(t_exc, "org/redisson/client/RedisException") == 0);
+    m_ExceptionClear(env);
+    Java_org_redisson_gpu_RSketchNative_shutdown(env, CLS, space3); /* ... finally { shutdown } */
+    CHECK(!m_ExceptionCheck(env));
   }
 
   Java_org_redisson_gpu_RSketchNative_shutdown(env, CLS, SPACE);
