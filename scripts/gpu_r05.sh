@@ -66,6 +66,12 @@ for p in ${PART//,/ }; do
     prof5z)
       profw pmc_c5_zipf 200 500000000 '{"workload": "c5", "keys": 500000000, "zipf": 1.1, "bloom_keys": 0}' \
         python3 bench.py --workload c5 --zipf 1.1 --steps 10 --warmup 3 || exit 1 ;;
+    gab)  # C5 grouped add, routes A/B interleaved: GAB="route=v,...;route=v,..." (uniform and Zipf 1.1)
+      IFS=';' read -ra FORMS <<< "${GAB:-gpart_xcd=0;gpart_xcd=1}"
+      for z in 0 1.1; do for rep in 1 2; do for f in "${FORMS[@]}"; do
+        step gab_$rep 120 python3 scripts/gpart_profile.py 5 $z "$f" || exit 1
+        grep '^{' gpurun_out/gab_$rep.log >> gpurun_out/gab.jsonl
+      done; done; done ;;
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;
