@@ -335,7 +335,8 @@ WORKLOADS = {
     "c4": "HLL addAll of variable-length string keys (8-64 B, blob+offsets) + count() (BASELINE configs[3])",
     "c5": "Grouped HLL: %d sketches cleared each step, grouped add + count(all) + %d countWith + %d mergeWith "
           "(BASELINE configs[4]), issued as one pipelined batch per step (the library's async calls, one wait); "
-          "N > 1: RCCL MAX reduce-scatter of the pool, each rank counting its "
+          "N > 1: each rank's pairs hashed locally and routed to the rank owning their sketch "
+          "(rsk_hll_add_grouped_routed: 8-byte records over RCCL send/recv), each rank counting its "
           "own 1/N of the sketches and running countWith/mergeWith led by them against partners from "
           "all G, fetched from their owners over RCCL",
 }
@@ -375,8 +376,8 @@ def run_hll(ctx, wl: str, n: int, steps: int, warmup: int, zipf: float = 0.0, gr
             groups, gkeys = devmem.gen_grouped(engine, SEED_C5, G, rank * n, n)
         kb = gkeys.keys_fixed(n, 16)
         pool = GroupedHyperLogLog(engine, G)
-        # N > 1: the pool is reduce-scattered, rank r owns a contiguous 1/N of
-        # the sketches and counts those; countWith(a, b) runs on a's owner and
+        # N > 1: the pairs are routed to their owners, rank r owns a contiguous 1/N
+        # of the sketches and counts those; countWith(a, b) runs on a's owner and
         # mergeWith(dst, src) on dst's owner, with b / src drawn from all G
         # sketches and fetched from their owners (rsk_hll_fetch_rows, RCCL).
         own_first, own_count = shard.owned_range(G, world, rank)
@@ -399,8 +400,9 @@ def run_hll(ctx, wl: str, n: int, steps: int, warmup: int, zipf: float = 0.0, gr
             # overlaps the GPU work queued before it, one wait at the end.
             pool.clear()  # every step builds the G sketches from empty (fresh PFADDs, not idempotent re-adds)
             if world > 1:
-                pool.add(kb, groups)
-                assert shard.hll_reducescatter_pool(pool.pool) == (own_first, own_count)  # RCCL MAX
+                # pairs hashed here, 8-byte records sent to the rank owning their
+                # sketch (grouped ncclSend/ncclRecv), applied to the owned rows only
+                assert shard.hll_add_grouped_routed(pool.pool, kb, groups) == (own_first, own_count)
                 ops = [pool.count_async(counts_out, own_ids)]
                 ops[0].wait()
                 shard.hll_fetch_rows(pool.pool, remote)  # partner / source rows from their owners
@@ -485,7 +487,9 @@ def run_hll(ctx, wl: str, n: int, steps: int, warmup: int, zipf: float = 0.0, gr
         "ms_per_step": elapsed / steps * 1e3,
         "config": dict({"workload": WORKLOADS[wl] % ((groups_n, batch_ops, batch_ops) if wl == "c5" else ()),
                         "keys_per_gpu": n, "global_keys_per_step": n * world,
-                        "parallelism": "key-stream sharding, RCCL MAX all-reduce of the registers" if world > 1
+                        "parallelism": ("pair-stream sharding, pairs routed to the sketch owners over RCCL"
+                                        if wl == "c5" else
+                                        "key-stream sharding, RCCL MAX all-reduce of the registers") if world > 1
                         else "single GPU", "redis_semantics": "3.2.0"}, **extra),
         "roofline": {"bound": "hbm", "kernel": kern_label, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -522,6 +526,8 @@ def run_hll(ctx, wl: str, n: int, steps: int, warmup: int, zipf: float = 0.0, gr
         if stage_ms:
             res["roofline"]["stage_ms_per_launch"] = stage_ms
         res["add_ms_per_step"] = avg_launch_s * 1e3
+        if world == 1 and zipf == 0:
+            res["checkpoint"] = checkpoint_bench(engine, pool)
     for b in bufs:
         b.free()
     if wl == "c5":
@@ -529,6 +535,38 @@ def run_hll(ctx, wl: str, n: int, steps: int, warmup: int, zipf: float = 0.0, gr
     else:
         hll.delete()
     return res
+
+
+def checkpoint_bench(engine, pool):
+    """The pool's checkpoint (the export path is the checkpoint): GET
+    of every sketch as its Redis string in one rsk_hll_export_redis_batch call
+    into host memory, then SET of all of them into a fresh pool in one
+    rsk_hll_import_redis_batch call; the restored pool re-exports to the same
+    bytes.  Host memory at both ends (PCIe inclusive)."""
+    import numpy as np
+
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    ids = np.arange(pool.n, dtype=np.uint64)
+    data, offs = pool.exportRedis(ids)  # warm-up: sizes the buffer
+    t0 = time.perf_counter()
+    data, offs = pool.exportRedis(ids, out=data)
+    t_exp = time.perf_counter() - t0
+    lens = np.diff(offs.astype(np.int64))
+    fresh = GroupedHyperLogLog(engine, pool.n)
+    fresh.importRedis(ids, data, offs)  # warm-up (scratch)
+    t0 = time.perf_counter()
+    fresh.importRedis(ids, data, offs)
+    t_imp = time.perf_counter() - t0
+    d2, o2 = fresh.exportRedis(ids, out=np.empty_like(data))
+    same = bool(np.array_equal(o2, offs) and np.array_equal(d2, data))
+    fresh.close()
+    return {"sketches": int(pool.n), "bytes": int(offs[-1]), "sparse_keys": int((lens < 12304).sum()),
+            "export_ms": t_exp * 1e3, "import_ms": t_imp * 1e3,
+            "export_sketches_per_s": pool.n / t_exp, "import_sketches_per_s": pool.n / t_imp,
+            "round_trip_identical": same,
+            "note": "rsk_hll_export_redis_batch / rsk_hll_import_redis_batch of every sketch after the timed "
+                    "steps, host buffers (PCIe inclusive), one call each"}
 
 
 def main():

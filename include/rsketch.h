@@ -224,6 +224,25 @@ int rsk_hll_export_redis(rsk_hll *h, uint64_t id, uint8_t *buf, size_t cap, size
  * isHLLObjectOrReply / hllMerge.  Replaces the key. */
 int rsk_hll_import_redis(rsk_hll *h, uint64_t id, const uint8_t *buf, size_t len);
 
+/* Batched GET: for each ids[i] the bytes rsk_hll_export_redis returns (empty
+ * for a missing key), packed back to back into out (host memory, cap bytes);
+ * key i occupies out[offsets[i] .. offsets[i+1]) (offsets: n + 1 entries).
+ * Same encoding decisions as the per-key call (sparse while the key fits,
+ * promoted for good otherwise; kept SET strings byte for byte); the sparse
+ * opcodes and the 6-bit dense packing are produced on the device, one wave
+ * per key, with one length pass and one copy per GiB of output -- the
+ * checkpoint of a pool.  cap too small: RSK_ERR_INVALID_ARG with
+ * offsets filled (offsets[n] = the bytes needed) and nothing written. */
+int rsk_hll_export_redis_batch(rsk_hll *h, const uint64_t *ids, uint64_t n, uint8_t *out, uint64_t cap,
+                               uint64_t *offsets);
+/* Batched SET: key ids[i] := the Redis HLL string data[offsets[i] .. offsets[i+1])
+ * (host memory; offsets: n + 1 non-decreasing entries), each validated like
+ * rsk_hll_import_redis.  All or nothing: one invalid string fails the call
+ * (RSK_ERR_WRONGTYPE / RSK_ERR_INVALID_HLL, its index in the message) before
+ * any key changes.  A key SET twice in one call keeps the later string. */
+int rsk_hll_import_redis_batch(rsk_hll *h, const uint64_t *ids, uint64_t n, const uint8_t *data,
+                               const uint64_t *offsets);
+
 /* ---------------------------------------------------------- Bloom filter */
 typedef enum rsk_bloom_mode {
   RSK_BLOOM_COMPAT = 0,  /* size <= 2*Integer.MAX_VALUE (RedissonBloomFilter.java:52,226-227) */
@@ -348,6 +367,22 @@ int rsk_hll_allreduce_pool(rsk_hll *h);
  * n mod nranks tail (which is all-reduced on every rank).  Sketches outside
  * the owned range keep this rank's partial registers.  Caches invalidated. */
 int rsk_hll_reducescatter_pool(rsk_hll *h, uint64_t *first, uint64_t *count);
+/* Grouped PFADD across ranks, routed to the owners (C5 across GPUs; the
+ * alternative to adding every pair locally and rsk_hll_reducescatter_pool).
+ * Collective: every rank passes its own pairs -- 16-byte keys (16-byte
+ * aligned) and uint32 group ids, both in device memory (n may be 0).  Each
+ * pair is hashed where it lives and its 8-byte record (sketch, register index
+ * and rank) shipped with grouped ncclSend/ncclRecv to the rank owning the
+ * sketch (ownership as in rsk_hll_reducescatter_pool); every rank applies the
+ * records it receives to its owned sketches [*first, *first + *count) only.
+ * Afterwards those hold the registers one process would hold after adding
+ * every rank's pairs (group ids >= the pool size are ignored); the rows
+ * outside are not written (fetch them with rsk_hll_fetch_rows).  A pending
+ * rsk_hll_clear is completed on the owned rows.  flags: RSK_FETCH_SELF also
+ * routes this rank's own records through RCCL (the exchange on one GPU).
+ * Argument errors on any rank are agreed on before anything moves. */
+int rsk_hll_add_grouped_routed(rsk_hll *h, const rsk_keys *keys, const uint32_t *groups, uint32_t flags,
+                               uint64_t *first, uint64_t *count);
 /* Collective (every rank calls it, n may be 0): after a reduce-scatter, make
  * the local rows ids[0..n) equal to their owners' rows, so that
  * rsk_hll_count_union_batch / rsk_hll_merge_batch can read sketches owned by

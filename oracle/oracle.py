@@ -70,6 +70,7 @@ def lib():
             "orc_hll_estimate": (ctypes.c_uint64, [ctypes.c_double, ctypes.c_int]),
             "orc_hll_count_raw": (ctypes.c_uint64, [ctypes.c_void_p]),
             "orc_hll_count_dense_regs": (ctypes.c_uint64, [ctypes.c_void_p]),
+            "orc_hll_records": (None, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]),
             "orc_hll_encode_dense": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
             "orc_hll_encode_sparse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
             "orc_hll_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
@@ -196,6 +197,13 @@ def hll_add(regs: np.ndarray, data: np.ndarray, offsets=None, fixed_len: int = 0
         n = (offsets.size - 1) if offsets is not None else data.size // fixed_len
     return int(lib().orc_hll_add_raw(_ptr(regs), _ptr(data),
                                      _ptr(offsets) if offsets is not None else None, fixed_len, n))
+
+
+def hll_records(data: np.ndarray, fixed_len: int, n: int) -> np.ndarray:
+    """index << 6 | rank of each key (Redis 3.2.0 hllPatLen)."""
+    out = np.empty(n, np.uint32)
+    lib().orc_hll_records(_ptr(np.ascontiguousarray(data, dtype=np.uint8)), fixed_len, n, _ptr(out))
+    return out
 
 
 def hll_add_fixed_mt(regs: np.ndarray, data: np.ndarray, fixed_len: int, n: int, nthreads: int):

@@ -81,6 +81,17 @@ int orc_hll_patlen(const uint8_t *ele, size_t len, long *regp) {
     return count;
 }
 
+/* The (register index, rank) of each fixed-length key as index << 6 | rank:
+ * the record the owner-routed grouped add ships (rsk_hll_add_grouped_routed),
+ * from hllPatLen above. */
+void orc_hll_records(const uint8_t *data, uint32_t fixed_len, uint64_t n, uint32_t *out) {
+    for (uint64_t i = 0; i < n; i++) {
+        long idx;
+        const int c = orc_hll_patlen(data + i * (uint64_t)fixed_len, fixed_len, &idx);
+        out[i] = ((uint32_t)idx << 6) | (uint32_t)c;
+    }
+}
+
 uint64_t orc_hll_add_raw(uint8_t *regs, const uint8_t *data, const uint64_t *offsets,
                          uint32_t fixed_len, uint64_t n) {
     uint64_t grown = 0;

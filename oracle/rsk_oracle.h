@@ -42,6 +42,7 @@ uint64_t orc_splitmix64(uint64_t x);
 int orc_hll_patlen(const uint8_t *ele, size_t len, long *regp);
 /* PFADD arithmetic on raw (one byte per register) registers; returns the
  * number of registers that grew. */
+void orc_hll_records(const uint8_t *data, uint32_t fixed_len, uint64_t n, uint32_t *out);
 uint64_t orc_hll_add_raw(uint8_t *regs, const uint8_t *data, const uint64_t *offsets,
                          uint32_t fixed_len, uint64_t n);
 /* Fixed-length keys on nthreads cores (OpenMP, private registers, max-merge). */

@@ -126,6 +126,8 @@ SIGNATURES = {
     "rsk_hll_device_registers": (_vp, [_vp]),
     "rsk_hll_export_redis": (ctypes.c_int, [_vp, _u64, _vp, _sz, _P(_sz)]),
     "rsk_hll_import_redis": (ctypes.c_int, [_vp, _u64, _vp, _sz]),
+    "rsk_hll_export_redis_batch": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
+    "rsk_hll_import_redis_batch": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
     "rsk_bloom_params": (ctypes.c_int, [_i64, ctypes.c_double, _u32, _P(_i64), _P(_i32)]),
     "rsk_bloom_create": (ctypes.c_int, [_vp, _i64, _i32, _P(_vp)]),
     "rsk_bloom_init": (ctypes.c_int, [_vp, _i64, ctypes.c_double, _u32, _P(_vp), _P(_i64), _P(_i32)]),
@@ -167,6 +169,7 @@ SIGNATURES = {
     "rsk_hll_allreduce_pool": (ctypes.c_int, [_vp]),
     "rsk_hll_reducescatter_pool": (ctypes.c_int, [_vp, _P(_u64), _P(_u64)]),
     "rsk_hll_fetch_rows": (ctypes.c_int, [_vp, _vp, _u64]),
+    "rsk_hll_add_grouped_routed": (ctypes.c_int, [_vp, _P(rsk_keys), _vp, _u32, _P(_u64), _P(_u64)]),
     "rsk_hll_fetch_rows_flags": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
     "rsk_plan_shard_range": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _P(_u64), _P(_u64)]),
     "rsk_plan_owned_range": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _P(_u64), _P(_u64)]),

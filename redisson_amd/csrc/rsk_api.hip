@@ -94,6 +94,21 @@ uint8_t* rsk_ctx::work(uint64_t bytes) {
   return d_work;
 }
 
+uint8_t* rsk_ctx::xbuf(uint64_t bytes) {
+  if (bytes > xbuf_bytes) {
+    if (d_xbuf) {
+      RSK_HIP(hipStreamSynchronize(stream));
+      RSK_HIP(hipFree(d_xbuf));
+      d_xbuf = nullptr;
+      xbuf_bytes = 0;
+    }
+    const uint64_t sz = std::max<uint64_t>(bytes, 16ull << 20);
+    RSK_HIP(hipMalloc(&d_xbuf, sz));
+    xbuf_bytes = sz;
+  }
+  return d_xbuf;
+}
+
 uint8_t* rsk_ctx::pinned(uint64_t bytes) {
   // every call that fills this buffer waits for its DMA before returning
   if (bytes > h_batch_bytes) {
@@ -567,6 +582,7 @@ int rsk_shutdown(rsk_ctx* c) {
     if (c->h_batch) (void)hipHostFree(c->h_batch);
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_out);
+    (void)hipFree(c->d_xbuf);
     (void)hipFree(c->d_lc);
     for (rsk::AsyncOp* op : c->async_all) {  // stream and completion queue drained: every op is idle
       if (op->h_buf) (void)hipHostFree(op->h_buf);
@@ -598,8 +614,9 @@ int rsk_trim(rsk_ctx* c) {
     RSK_HIP(hipStreamSynchronize(c->xout));
     RSK_HIP(hipFree(c->d_work));
     RSK_HIP(hipFree(c->d_out));
-    c->d_work = c->d_out = nullptr;
-    c->work_bytes = c->out_bytes = 0;
+    RSK_HIP(hipFree(c->d_xbuf));
+    c->d_work = c->d_out = c->d_xbuf = nullptr;
+    c->work_bytes = c->out_bytes = c->xbuf_bytes = 0;
     if (c->h_batch) RSK_HIP(hipHostFree(c->h_batch));
     c->h_batch = nullptr;
     c->h_batch_bytes = 0;
@@ -1278,6 +1295,187 @@ int rsk_hll_import_redis(rsk_hll* h, uint64_t id, const uint8_t* buf, size_t len
     }
     if (canonical) hll_forget_import(h, id);
     else h->imported[id].assign(buf, buf + len);
+  });
+}
+
+// Batched GET / SET of the Redis strings (rsk_hll_io.hip): the checkpoint of
+// a pool, one length pass and one copy per GiB of output (export), one upload
+// and two kernels (import) instead of a synchronous round trip per key.
+int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint8_t* out, uint64_t cap,
+                               uint64_t* offsets) {
+  return guarded([&] {
+    need(h != nullptr, "hll handle is NULL");
+    need(offsets != nullptr && (ids != nullptr || n == 0), "NULL argument");
+    need(n < (1ull << 31), "at most 2^31 - 1 keys per call");
+    offsets[0] = 0;
+    if (n == 0) return;
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < n; ++i) bad |= ids[i] >= h->n;
+    need(!bad, "sketch id out of range");
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    rsk::hll_materialize(h);  // a pending lazy clear: GET reads zero registers (export writes none)
+    // keys the device encodes (present, not a kept SET string), in call order
+    std::vector<uint64_t> dev_i, dev_id;
+    std::vector<uint8_t> want;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t id = ids[i];
+      if (!h->exists[id] || h->imported.count(id)) continue;
+      dev_i.push_back(i);
+      dev_id.push_back(id);
+      want.push_back(h->dense[id] ? 0 : 1);
+    }
+    const uint64_t nd = dev_i.size();
+    auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+    constexpr uint64_t CHUNK = 1ull << 30;  // output bytes staged per copy
+    uint64_t stage_cap = 0;
+    std::vector<uint32_t> len(nd);
+    uint8_t* w = nullptr;
+    if (nd) {
+      stage_cap = std::min<uint64_t>(CHUNK, nd * (uint64_t)RSK_HLL_DENSE_BYTES);
+      w = c->work(al(8 * nd) * 2 + al(nd) + al(4 * nd) + stage_cap + 256);
+      uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
+      uint64_t* d_pos = reinterpret_cast<uint64_t*>(w + al(8 * nd));
+      uint8_t* d_want = w + 2 * al(8 * nd);
+      uint32_t* d_len = reinterpret_cast<uint32_t*>(w + 2 * al(8 * nd) + al(nd));
+      RSK_HIP(hipMemcpyAsync(d_ids, dev_id.data(), 8 * nd, hipMemcpyHostToDevice, c->stream));
+      RSK_HIP(hipMemcpyAsync(d_want, want.data(), nd, hipMemcpyHostToDevice, c->stream));
+      hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)nd, d_len, nullptr, nullptr);
+      RSK_HIP(hipMemcpyAsync(len.data(), d_len, 4 * nd, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      (void)d_pos;
+    }
+    // offsets: device keys by their length pass, kept SET strings as stored, missing keys empty
+    {
+      uint64_t o = 0, d = 0;
+      for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t id = ids[i];
+        uint64_t L = 0;
+        if (d < nd && dev_i[d] == i) {
+          L = len[d++] & 0x7FFFFFFFu;
+        } else if (h->exists[id]) {
+          L = h->imported.find(id)->second.size();
+        }
+        o += L;
+        offsets[i + 1] = o;
+      }
+      if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
+      need(out != nullptr || o == 0, "out is NULL");
+    }
+    // the write pass, chunk by chunk of output: [offsets[a], offsets[b]) staged whole and copied
+    if (nd) {
+      uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
+      uint64_t* d_pos = reinterpret_cast<uint64_t*>(w + al(8 * nd));
+      uint32_t* d_len = reinterpret_cast<uint32_t*>(w + 2 * al(8 * nd) + al(nd));
+      uint8_t* d_stage = w + 2 * al(8 * nd) + al(nd) + al(4 * nd);
+      std::vector<uint64_t> pos(nd);
+      uint64_t d0 = 0;
+      while (d0 < nd) {
+        const uint64_t base = offsets[dev_i[d0]];
+        uint64_t d1 = d0;
+        while (d1 < nd && offsets[dev_i[d1] + 1] - base <= stage_cap) {
+          pos[d1] = offsets[dev_i[d1]] - base;
+          ++d1;
+        }
+        const uint64_t end = offsets[dev_i[d1 - 1] + 1];
+        RSK_HIP(hipMemcpyAsync(d_pos + d0, pos.data() + d0, 8 * (d1 - d0), hipMemcpyHostToDevice, c->stream));
+        hll_export_launch(c, h->d_regs, h->d_card, d_ids + d0, nullptr, (uint32_t)(d1 - d0), d_len + d0, d_pos + d0,
+                          d_stage);
+        RSK_HIP(hipMemcpyAsync(out + base, d_stage, end - base, hipMemcpyDeviceToHost, c->stream));
+        RSK_HIP(hipStreamSynchronize(c->stream));  // the stage is reused by the next chunk
+        d0 = d1;
+      }
+      // promoted for good (hllSparseSet -> hllSparseToDense), as the per-key GET
+      for (uint64_t d = 0; d < nd; ++d)
+        if (want[d] && !(len[d] >> 31)) h->dense[dev_id[d]] = 1;
+    }
+    // kept SET strings: their bytes, card bytes as PFCOUNT last left them (rare: copied one by one)
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t id = ids[i];
+      if (!h->exists[id]) continue;
+      const auto imp = h->imported.find(id);
+      if (imp == h->imported.end()) continue;
+      uint64_t card = 0;
+      RSK_HIP(hipMemcpy(&card, h->d_card + id, 8, hipMemcpyDeviceToHost));
+      uint8_t* d = out + offsets[i];
+      std::memcpy(d, imp->second.data(), imp->second.size());
+      for (int b = 0; b < 8; ++b) d[8 + b] = (uint8_t)(card >> (8 * b));
+    }
+  });
+}
+
+int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, const uint8_t* data,
+                               const uint64_t* offsets) {
+  return guarded([&] {
+    need(h != nullptr, "hll handle is NULL");
+    need(n == 0 || (ids != nullptr && offsets != nullptr && data != nullptr), "NULL argument");
+    need(n < (1ull << 31), "at most 2^31 - 1 keys per call");
+    if (n == 0) return;
+    for (uint64_t i = 0; i < n; ++i) need(offsets[i + 1] >= offsets[i], "offsets must be non-decreasing");
+    check_hll_ids(h, ids, n);
+    // isHLLObjectOrReply per string (as rsk_hll_import_redis), on the host: header, magic,
+    // encoding, exact dense length; the sparse opcodes are checked on the device
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint8_t* s = data + offsets[i];
+      const uint64_t len = offsets[i + 1] - offsets[i];
+      if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1 || (s[4] == 0 && len != RSK_HLL_DENSE_BYTES))
+        fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value. (string " + std::to_string(i) + ")");
+      need(len <= (1ull << 31), "string too long");
+    }
+    // SETs of one key in one call: the last wins
+    std::vector<uint8_t> apply(n, 1);
+    {
+      std::unordered_map<uint64_t, uint64_t> last;
+      last.reserve(n);
+      for (uint64_t i = 0; i < n; ++i) {
+        auto r = last.emplace(ids[i], i);
+        if (!r.second) {
+          apply[r.first->second] = 0;
+          r.first->second = i;
+        }
+      }
+    }
+    rsk_ctx* c = h->ctx;
+    CtxLock l(c);
+    const uint64_t base = offsets[0], total = offsets[n] - base;
+    auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+    uint8_t* w = c->work(al(8 * n) + al(8 * (n + 1)) + 2 * al(n) + 256 + al(total) + 256);
+    uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(w + al(8 * n));
+    uint8_t* d_apply = w + al(8 * n) + al(8 * (n + 1));
+    uint8_t* d_canon = d_apply + al(n);
+    auto* d_err = reinterpret_cast<unsigned long long*>(d_canon + al(n));
+    uint8_t* d_data = d_canon + al(n) + 256;
+    std::vector<uint64_t> off(n + 1);
+    for (uint64_t i = 0; i <= n; ++i) off[i] = offsets[i] - base;
+    RSK_HIP(hipMemcpyAsync(d_ids, ids, 8 * n, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemcpyAsync(d_apply, apply.data(), n, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemcpyAsync(d_data, data + base, total, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipMemsetAsync(d_err, 0xFF, 8, c->stream));
+    RSK_HIP(hipMemsetAsync(d_canon, 1, n, c->stream));
+    hll_import_launch(c, d_data, d_off, d_ids, nullptr, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
+    hll_import_launch(c, d_data, d_off, d_ids, d_apply, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
+    std::vector<uint8_t> canon(n);
+    unsigned long long err = 0;
+    RSK_HIP(hipMemcpyAsync(canon.data(), d_canon, n, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipMemcpyAsync(&err, d_err, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    if (err != ~0ull)
+      fail(RSK_ERR_INVALID_HLL, "INVALIDOBJ Corrupted HLL object detected (string " + std::to_string(err) + ")");
+    for (uint64_t i = 0; i < n; ++i) {
+      if (!apply[i]) continue;
+      const uint64_t id = ids[i];
+      const uint8_t* s = data + offsets[i];
+      const uint64_t len = offsets[i + 1] - offsets[i];
+      h->exists[id] = 1;
+      h->dense[id] = s[4] == 0;
+      // a copy only where the canonical re-encoding would differ (as rsk_hll_import_redis)
+      bool canonical = s[5] == 0 && s[6] == 0 && s[7] == 0;
+      if (canonical && s[4] == 1) canonical = canon[i] && len <= HLL_SPARSE_MAX_BYTES;
+      if (canonical) hll_forget_import(h, id);
+      else h->imported[id].assign(s, s + len);
+    }
   });
 }
 

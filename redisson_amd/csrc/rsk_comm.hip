@@ -278,6 +278,140 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
   });
 }
 
+// The owner-routed grouped add (C5 across GPUs): pairs hashed
+// where they live, 8-byte records shipped to the rank owning their sketch,
+// applied there to the owned rows only.  Against building every sketch on
+// every rank and reduce-scattering the pool, per rank at N = 8 and the C5
+// size (500M pairs, 10^6 sketches): 7/8 x 4 GB of records over xGMI instead
+// of 7/8 x 16 GiB of rows, and 2 GiB of rows written instead of 16 GiB.
+int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups, uint32_t flags,
+                               uint64_t* first_out, uint64_t* count_out) {
+  return guarded([&] {
+    need(h && first_out && count_out, "NULL argument");
+    rsk_ctx* c = h->ctx;
+    Lock l(c);
+    ncclComm_t comm = comm_of(c);
+    const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank;
+    auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+    auto on_gpu = [&](const void* p) {
+      hipPointerAttribute_t a{};
+      if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+      }
+      return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+    };
+    // local argument errors are agreed on by every rank before anything moves
+    const uint64_t n = keys ? keys->n : 0;
+    const bool args_ok =
+        keys != nullptr && (flags & ~RSK_FETCH_SELF) == 0 && N <= 64 && h->n <= 0xFFFFFFFFull &&
+        (n == 0 || (keys->location == RSK_MEM_DEVICE && keys->offsets == nullptr && keys->fixed_len == 16 &&
+                    (reinterpret_cast<uintptr_t>(keys->data) & 15) == 0 && groups != nullptr && on_gpu(keys->data) &&
+                    on_gpu(groups)));
+    const uint32_t B = rsk::route_blocks(c);
+    uint8_t* w = c->work(al(8 * 3) + al(4 * N * B) + al(8 * N * B) + 2 * al(8 * N) + al(8 * std::max<uint64_t>(n, 1)));
+    uint64_t* d_meta = reinterpret_cast<uint64_t*>(w);
+    uint32_t* d_cnt = reinterpret_cast<uint32_t*>(w + al(24));
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(w + al(24) + al(4 * N * B));
+    uint64_t* d_scnt = reinterpret_cast<uint64_t*>(w + al(24) + al(4 * N * B) + al(8 * N * B));
+    uint64_t* d_rcnt = d_scnt + al(8 * N) / 8;
+    uint2* d_send = reinterpret_cast<uint2*>(w + al(24) + al(4 * N * B) + al(8 * N * B) + 2 * al(8 * N));
+    uint64_t* h_meta = reinterpret_cast<uint64_t*>(c->h_small + 8192);
+    h_meta[0] = args_ok ? 0 : 1;
+    h_meta[1] = h->n;
+    h_meta[2] = ~h->n;
+    RSK_HIP(hipMemcpyAsync(d_meta, h_meta, 24, hipMemcpyHostToDevice, c->stream));
+    RSK_NCCL(ncclAllReduce(d_meta, d_meta, 3, ncclUint64, ncclMax, comm, c->stream));
+    RSK_HIP(hipMemcpyAsync(h_meta, d_meta, 24, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    need(args_ok, "rsk_hll_add_grouped_routed: keys must be 16-byte aligned fixed 16-byte keys and groups, both in "
+                  "device memory; flags RSK_FETCH_SELF or 0; at most 64 ranks");
+    need(h_meta[0] == 0, "rsk_hll_add_grouped_routed: another rank passed an invalid argument");
+    need(h_meta[1] == ~h_meta[2], "rsk_hll_add_grouped_routed: pool sizes differ across ranks");
+    uint64_t first, count;
+    rsk::plan_owned_range(h->n, N, r, &first, &count);
+    *first_out = first;
+    *count_out = count;
+    const uint64_t G = h->n;
+    // 1. owner counts per block, their offsets in the send buffer (owner-major)
+    std::vector<uint32_t> cnt(N * B, 0);
+    std::vector<uint64_t> off(N * B), scnt(2 * N, 0);
+    if (n) {
+      rsk::hll_route_count_launch(c, groups, n, G, (uint32_t)N, d_cnt);
+      RSK_HIP(hipMemcpyAsync(cnt.data(), d_cnt, 4 * N * B, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+    }
+    uint64_t at = 0;
+    for (uint64_t o = 0; o < N; ++o) {
+      const uint64_t o0 = at;
+      for (uint64_t b = 0; b < B; ++b) {
+        off[o * B + b] = at;
+        at += cnt[o * B + b];
+      }
+      scnt[o] = at - o0;  // records for rank o
+    }
+    // own records stay in place unless they are routed through RCCL (RSK_FETCH_SELF)
+    const bool self = (flags & RSK_FETCH_SELF) != 0;
+    if (n) {
+      RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * N * B, hipMemcpyHostToDevice, c->stream));
+      rsk::hll_route_scatter_launch(c, reinterpret_cast<const uint8_t*>(keys->data), groups, n, G, (uint32_t)N, d_off,
+                                    d_send);
+    }
+    // 2. record counts both ways
+    RSK_HIP(hipMemcpyAsync(d_scnt, scnt.data(), 8 * N, hipMemcpyHostToDevice, c->stream));
+    {
+      rsk::ProfScope ps(c, "hll_route_counts");
+      RSK_NCCL(ncclGroupStart());
+      for (uint64_t j = 0; j < N; ++j) {
+        if (j == r && !self) continue;
+        RSK_NCCL(ncclSend(d_scnt + j, 1, ncclUint64, (int)j, comm, c->stream));
+        RSK_NCCL(ncclRecv(d_rcnt + j, 1, ncclUint64, (int)j, comm, c->stream));
+      }
+      RSK_NCCL(ncclGroupEnd());
+    }
+    RSK_HIP(hipMemcpyAsync(scnt.data() + N, d_rcnt, 8 * N, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    if (!self) scnt[N + r] = scnt[r];
+    uint64_t n_in = 0;
+    for (uint64_t j = 0; j < N; ++j) n_in += scnt[N + j];
+    // 3. the records: my run for rank j to j, j's run for me into the receive buffer (in rank order)
+    uint64_t s0 = 0;
+    for (uint64_t j = 0; j < r; ++j) s0 += scnt[j];
+    uint2* d_recv = reinterpret_cast<uint2*>(c->xbuf(8 * std::max<uint64_t>(n_in, 1)));
+    {
+      rsk::ProfScope ps(c, "hll_route_exchange");
+      RSK_NCCL(ncclGroupStart());
+      for (uint64_t j = 0, so = 0, ro = 0; j < N; so += scnt[j], ro += scnt[N + j], ++j) {
+        if (j == r && !self) continue;
+        if (scnt[j]) RSK_NCCL(ncclSend(d_send + so, scnt[j] * 8, ncclUint8, (int)j, comm, c->stream));
+        if (scnt[N + j]) RSK_NCCL(ncclRecv(d_recv + ro, scnt[N + j] * 8, ncclUint8, (int)j, comm, c->stream));
+      }
+      RSK_NCCL(ncclGroupEnd());
+    }
+    if (!self && scnt[r]) {
+      uint64_t ro = 0;
+      for (uint64_t j = 0; j < r; ++j) ro += scnt[N + j];
+      RSK_HIP(hipMemcpyAsync(d_recv + ro, d_send + s0, scnt[r] * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    // 4. the owned rows [first, first + count): a pending lazy clear is completed on them by
+    // the add (every owned row written); rows outside stay as they were
+    rsk::hll_forget_imports(h);
+    const bool pool_zero = h->zero;
+    const bool write_all = h->pending_clear;
+    rsk::hll_touch(h);
+    h->pending_clear = false;
+    rsk::hll_add_grouped_recs_launch(c, d_recv, n_in, h->d_regs + first * (uint64_t)rsk::HLL_REGS, count, pool_zero,
+                                     write_all,
+                                     rsk::PCount{h->d_pcount + first, h->d_pepoch + first, h->pc_epoch});
+    if (count) {
+      hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card + first, count);
+      RSK_CHECK_LAUNCH("invalidate");
+    }
+    std::fill(h->exists.begin() + first, h->exists.begin() + first + count, 1);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
 int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32_t flags) {
   return guarded([&] {
     need(h != nullptr, "NULL handle");  // no communicator to agree through without one

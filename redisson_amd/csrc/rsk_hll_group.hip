@@ -163,8 +163,12 @@ __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict_
 // fine-bin pass reads each coarse bin's per-tile segments instead, and
 // scattered segment reads run at the stream rate (6.5 TB/s for 256-byte
 // segments, scripts/fetch_calib.py).  Tile t = block b's tile j: t = b tpb + j.
+// REC: the input is already hashed -- 8-byte records {group, index << 6 | rank}
+// (the owner-routed add, rsk_hll_add_grouped_routed) read instead of keys + ids.
+template <bool REC>
 __global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict__ keys,
-                                                         const uint32_t* __restrict__ groups, uint64_t n, uint64_t per,
+                                                         const uint32_t* __restrict__ groups,
+                                                         const uint2* __restrict__ recs, uint64_t n, uint64_t per,
                                                          uint64_t G, uint32_t nbins, uint32_t tpb,
                                                          uint32_t* __restrict__ out, uint16_t* __restrict__ hdr) {
   __shared__ SortLds<GP_TILE> L;
@@ -180,8 +184,14 @@ __global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict
     for (int e = 0; e < GP_E; ++e) {
       const uint64_t i = k0 + threadIdx.x + (uint64_t)e * PT;
       const bool ok = i < end;
-      v[e] = ok ? ld_nt16(keys + i) : make_uint4(0, 0, 0, 0);
-      g[e] = ok ? __builtin_nontemporal_load(&groups[i]) : 0xFFFFFFFFu;
+      if constexpr (REC) {
+        const uint2 r = ok ? recs[i] : make_uint2(0xFFFFFFFFu, 0);
+        g[e] = r.x;
+        v[e].x = r.y;
+      } else {
+        v[e] = ok ? ld_nt16(keys + i) : make_uint4(0, 0, 0, 0);
+        g[e] = ok ? __builtin_nontemporal_load(&groups[i]) : 0xFFFFFFFFu;
+      }
     }
     __syncthreads();  // the previous tile's image is written out, hist reset
     uint32_t rec[GP_E], tag[GP_E];
@@ -189,8 +199,14 @@ __global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict
     for (int e = 0; e < GP_E; ++e) {
       tag[e] = 0xFFFFFFFFu;
       if (g[e] < G) {
-        const uint64_t hsh = murmur64a_16(((uint64_t)v[e].y << 32) | v[e].x, ((uint64_t)v[e].w << 32) | v[e].z);
-        rec[e] = ((g[e] & ((1u << GP_BIN_SHIFT) - 1)) << 20) | (hll_index(hsh) << 6) | hll_rank(hsh);
+        uint32_t ir;
+        if constexpr (REC) {
+          ir = v[e].x;
+        } else {
+          const uint64_t hsh = murmur64a_16(((uint64_t)v[e].y << 32) | v[e].x, ((uint64_t)v[e].w << 32) | v[e].z);
+          ir = (hll_index(hsh) << 6) | hll_rank(hsh);
+        }
+        rec[e] = ((g[e] & ((1u << GP_BIN_SHIFT) - 1)) << 20) | ir;
         const uint32_t b = g[e] >> GP_BIN_SHIFT;
         tag[e] = (b << 16) | atomicAdd(&L.hist[b], 1u);
       }
@@ -1147,10 +1163,10 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_extra_kernel(const uint32_t* 
   }
 }
 
-bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& keys, uint64_t G) {
+bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& keys, uint64_t G, bool recs) {
   const int mode = c->tune.gpart;  // 0 auto, 1 always, -1 never
-  const bool f16 =
-      keys.offsets == nullptr && keys.fixed_len == 16 && (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0;
+  const bool f16 = recs || (keys.offsets == nullptr && keys.fixed_len == 16 &&
+                            (reinterpret_cast<uintptr_t>(keys.data) & 15) == 0);
   if (mode < 0 || !f16 || keys.n == 0 || G == 0 || G > (1ull << (GP_BIN_SHIFT + 8))) return false;
   // auto: large batches dense enough that reading + writing each touched sketch once pays
   if (mode == 0 && (keys.n < (1ull << 22) || keys.n < 16 * G)) return false;
@@ -1160,8 +1176,8 @@ bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& keys, uint64
 // write_all (a pending lazy clear, pool_zero too): hll_gapply writes every
 // row of the pool, zero rows for sketches without records.
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t* d_groups, uint8_t* d_regs,
-                                 uint64_t G, bool pool_zero, bool write_all, PCount pc) {
-  if (!hll_grouped_partition_applies(c, keys, G)) return false;
+                                 uint64_t G, bool pool_zero, bool write_all, PCount pc, const uint2* d_recs) {
+  if (!hll_grouped_partition_applies(c, keys, G, d_recs != nullptr)) return false;
   const uint32_t nbins1 = (uint32_t)(((G - 1) >> GP_BIN_SHIFT) + 1);
   const uint32_t nfine = nbins1 * PT;
   const uint32_t cus = (uint32_t)c->num_cus;
@@ -1174,7 +1190,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   const uint64_t max_np = std::min<uint64_t>(keys.n, chunk);
   // fine-bin pass parts: about four per CU over the whole chunk, at least 16 tiles each
   const uint32_t target = (uint32_t)std::max<uint64_t>(16ull * GQ_TILE, max_np / (4ull * cus) + 1);
-  const bool tm = c->tune.gpart_tm == 1;
+  const bool tm = d_recs || c->tune.gpart_tm == 1;  // records: the tile-major form only
   const uint64_t per_max = ((max_np + G1 - 1) / G1 + 3) & ~3ull;
   const uint64_t nt_max = (uint64_t)G1 * ((per_max + GP_TILE - 1) / GP_TILE);
   // TM parts: also at most TM_PT tiles each
@@ -1224,15 +1240,20 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
     const uint64_t per = ((m + G1 - 1) / G1 + 3) & ~3ull;  // a multiple of 4: uint4 id loads in hll_gcount
-    const uint4* kd = reinterpret_cast<const uint4*>(keys.data) + first;
-    const uint32_t* gd = d_groups + first;
+    const uint4* kd = d_recs ? nullptr : reinterpret_cast<const uint4*>(keys.data) + first;
+    const uint32_t* gd = d_recs ? nullptr : d_groups + first;
+    const uint2* rd = d_recs ? d_recs + first : nullptr;
     const uint32_t tpb = (uint32_t)((per + GP_TILE - 1) / GP_TILE), NT = G1 * tpb;
     if (c->tune.gpart_poison) RSK_HIP(hipMemsetAsync(buf_b, 0xFF, 4 * max_np, c->stream));
     if (tm) {
       {
         ProfScope ps(c, "hll_gpart1");
-        hipLaunchKernelGGL(hll_gpart1t_kernel, dim3(G1), dim3(PT), 0, c->stream, kd, gd, m, per, G, nbins1, tpb, buf_a,
-                           hdr);
+        if (rd)
+          hipLaunchKernelGGL(hll_gpart1t_kernel<true>, dim3(G1), dim3(PT), 0, c->stream, kd, gd, rd, m, per, G, nbins1,
+                             tpb, buf_a, hdr);
+        else
+          hipLaunchKernelGGL(hll_gpart1t_kernel<false>, dim3(G1), dim3(PT), 0, c->stream, kd, gd, rd, m, per, G, nbins1,
+                             tpb, buf_a, hdr);
         RSK_CHECK_LAUNCH("hll_gpart1t");
       }
       {
@@ -1307,6 +1328,144 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
     }
   }
   return true;
+}
+
+
+// ===================================================== owner-routed grouped add
+// (rsk_hll_add_grouped_routed, C5 across GPUs): each rank hashes its own pairs
+// and ships 8-byte records {group - owner's first, index << 6 | rank} to the
+// rank that owns the group (contiguous ranges, rsk_plan.hip plan_owned_range),
+// instead of building all G sketches and reduce-scattering the pool.
+//   route_count   : cnt[o * B + b] = pairs of block b owned by rank o
+//   route_scatter : block b hashes its pairs again and appends each to owner
+//                   o's run at off[o * B + b] (one LDS cursor per owner; wave-
+//                   aggregated: one atomic per owner present in the wave)
+constexpr uint32_t RT_T = 256;
+constexpr uint32_t RT_MAXN = 64;  // ranks
+
+RSK_DEV uint32_t route_owner(uint32_t g, uint64_t q, uint32_t N) {
+  return q ? (uint32_t)min<uint64_t>(g / q, N - 1) : N - 1;
+}
+
+__global__ __launch_bounds__(RT_T) void hll_route_count_kernel(const uint32_t* __restrict__ groups, uint64_t n,
+                                                               uint64_t per, uint64_t G, uint32_t N,
+                                                               uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[RT_MAXN];
+  if (threadIdx.x < RT_MAXN) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  const uint64_t q = G / N;
+  uint32_t mine[RT_MAXN > 8 ? 8 : RT_MAXN] = {};  // lane-private counts for the first 8 owners
+  for (uint64_t i = begin + threadIdx.x; i < end; i += RT_T) {
+    const uint32_t g = __builtin_nontemporal_load(&groups[i]);
+    if (g >= G) continue;
+    const uint32_t o = route_owner(g, q, N);
+    if (o < 8) {
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) mine[k] += o == k;
+    } else {
+      atomicAdd(&h[o], 1u);
+    }
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k)
+    if (k < N && mine[k]) atomicAdd(&h[k], mine[k]);
+  __syncthreads();
+  if (threadIdx.x < N) cnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __restrict__ keys,
+                                                                 const uint32_t* __restrict__ groups, uint64_t n,
+                                                                 uint64_t per, uint64_t G, uint32_t N,
+                                                                 const uint64_t* __restrict__ off,
+                                                                 uint2* __restrict__ out) {
+  __shared__ unsigned long long cur[RT_MAXN];
+  if (threadIdx.x < N) cur[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  const uint64_t q = G / N;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  for (uint64_t i0 = begin; i0 < end; i0 += RT_T) {  // block-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    const bool in = i < end;
+    const uint32_t g = in ? __builtin_nontemporal_load(&groups[i]) : 0xFFFFFFFFu;
+    const bool valid = g < G;
+    uint32_t o = 0, gl = 0, ir = 0;
+    if (valid) {
+      const uint4 v = ld_nt16(keys + i);
+      const uint64_t hsh = murmur64a_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
+      ir = (hll_index(hsh) << 6) | hll_rank(hsh);
+      o = route_owner(g, q, N);
+      gl = (uint32_t)(g - (uint64_t)o * q);
+    }
+    uint64_t pending = __ballot(valid);
+    while (pending) {  // one atomic per owner present in the wave
+      const uint32_t oo = (uint32_t)__builtin_amdgcn_readlane((int)o, __builtin_ctzll(pending));
+      const uint64_t m = __ballot(valid && o == oo) & pending;
+      const int leader = __builtin_ctzll(m);
+      unsigned long long base = 0;
+      if ((int)lane == leader) base = atomicAdd(&cur[oo], (unsigned long long)__popcll(m));
+      base = __shfl(base, leader, 64);
+      if (valid && o == oo) out[base + (uint64_t)__popcll(m & lt)] = make_uint2(gl, ir);
+      pending &= ~m;
+    }
+  }
+}
+
+// Records into the pool directly (small batches): a memory-side byte-max CAS each.
+__global__ __launch_bounds__(256) void hll_add_grouped_rec_kernel(const uint2* __restrict__ recs, uint64_t n,
+                                                                  uint8_t* __restrict__ regs, uint64_t G) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint2 r = recs[i];
+    if (r.x >= G) continue;
+    const uint32_t idx = r.y >> 6, rank = r.y & 63u;
+    uint32_t* word = reinterpret_cast<uint32_t*>(regs + (uint64_t)r.x * HLL_REGS + (idx & ~3u));
+    const uint32_t sh = (idx & 3u) * 8;
+    uint32_t old = *word;
+    while (((old >> sh) & 0xFFu) < rank) {
+      const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+      if (prev == old) break;
+      old = prev;
+    }
+  }
+}
+
+uint32_t route_blocks(const rsk_ctx* c) { return (uint32_t)c->num_cus * 4; }
+
+void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N,
+                            uint32_t* d_cnt) {
+  const uint32_t B = route_blocks(c);
+  const uint64_t per = (n + B - 1) / B;
+  ProfScope ps(c, "hll_route");
+  hipLaunchKernelGGL(hll_route_count_kernel, dim3(B), dim3(RT_T), 0, c->stream, d_groups, n, per, G, N, d_cnt);
+  RSK_CHECK_LAUNCH("hll_route_count");
+}
+
+void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
+                              uint32_t N, const uint64_t* d_off, uint2* d_out) {
+  const uint32_t B = route_blocks(c);
+  const uint64_t per = (n + B - 1) / B;
+  ProfScope ps(c, "hll_route");
+  hipLaunchKernelGGL(hll_route_scatter_kernel, dim3(B), dim3(RT_T), 0, c->stream,
+                     reinterpret_cast<const uint4*>(d_keys16), d_groups, n, per, G, N, d_off, d_out);
+  RSK_CHECK_LAUNCH("hll_route_scatter");
+}
+
+void hll_add_grouped_recs_launch(rsk_ctx* c, const uint2* d_recs, uint64_t n, uint8_t* d_regs, uint64_t G,
+                                 bool pool_zero, bool write_all, PCount pc) {
+  if (n == 0 && !write_all) return;
+  const DevKeys none{nullptr, nullptr, n, 16};
+  if (n && hll_add_grouped_partitioned(c, none, nullptr, d_regs, G, pool_zero, write_all, pc, d_recs)) return;
+  if (write_all) RSK_HIP(hipMemsetAsync(d_regs, 0, G * (uint64_t)HLL_REGS, c->stream));
+  if (!n) return;
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+  ProfScope ps(c, "hll_add_grouped_rec");
+  hipLaunchKernelGGL(hll_add_grouped_rec_kernel, dim3((uint32_t)blocks), dim3(256), 0, c->stream, d_recs, n, d_regs,
+                     G);
+  RSK_CHECK_LAUNCH("hll_add_grouped_rec");
 }
 
 }  // namespace rsk

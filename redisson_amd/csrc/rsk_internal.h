@@ -193,8 +193,14 @@ struct rsk_ctx {
   // the context fails with it (its streams cannot be trusted any more).
   std::atomic<bool> dead{false};
 
+  // grow-on-demand device scratch for collectives' receive buffers (the
+  // routed grouped add), distinct from d_work, which the add itself uses
+  uint8_t* d_xbuf = nullptr;
+  uint64_t xbuf_bytes = 0;
+
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);
+  uint8_t* xbuf(uint64_t bytes);
 };
 
 struct rsk_hll {
@@ -306,6 +312,21 @@ void hll_merge_launch(rsk_ctx* c, uint8_t* const* d_dst_ptrs, const uint8_t* con
 void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_sketch, uint8_t* d_out);
 void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag);
 
+// ---- Redis strings of many keys (rsk_hll_io.hip)
+// Export: d_pos null -> d_len[i] = the string length of key d_ids[i] (bit 31:
+// sparse; d_want_sparse[i]: the key is still in the sparse encoding); d_pos
+// given -> its string at d_out + d_pos[i] in the encoding d_len[i] names.
+void hll_export_launch(rsk_ctx* c, const uint8_t* d_regs, const uint64_t* d_card, const uint64_t* d_ids,
+                       const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, const uint64_t* d_pos,
+                       uint8_t* d_out);
+// Import: d_apply null -> check the sparse strings (atomicMin(d_err, i) on a
+// corrupt one; d_canon[i] = 0 where the payload is not the canonical
+// encoding); d_apply given -> decode strings with d_apply[i] set into rows
+// d_ids[i] (and their card bytes), unless *d_err was set.
+void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_ids,
+                       const uint8_t* d_apply, uint32_t n, uint8_t* d_regs, uint64_t* d_card, uint8_t* d_canon,
+                       unsigned long long* d_err);
+
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Slice-partitioned add (rsk_bloom_part.hip); false when the direct kernel is used
@@ -317,8 +338,20 @@ bool bloom_add_supertile(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 void bloom_add_direct_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);
 // Grouped PFADD partitioned by sketch (rsk_bloom_part.hip); false when the
 // batch is not worth it (or not 16-byte keys): use the direct kernel.
-bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& k, uint64_t G);
+bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& k, uint64_t G, bool recs = false);
+// d_recs: the input is already hashed (8-byte records {group, index << 6 | rank}, k.n of them)
 bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d_groups, uint8_t* d_regs, uint64_t G,
+                                 bool pool_zero, bool write_all, PCount pc, const uint2* d_recs = nullptr);
+// Owner-routed grouped add (rsk_hll_group.hip; the exchange in rsk_comm.hip):
+// per-block owner counts cnt[o * B + b] (B = route_blocks), then the pairs
+// hashed into 8-byte records appended to owner o's run at off[o * B + b].
+uint32_t route_blocks(const rsk_ctx* c);
+void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N, uint32_t* d_cnt);
+void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
+                              uint32_t N, const uint64_t* d_off, uint2* d_out);
+// Records into a pool of G rows (partitioned for large batches, else a CAS each);
+// write_all: every row written (zero rows for sketches without records).
+void hll_add_grouped_recs_launch(rsk_ctx* c, const uint2* d_recs, uint64_t n, uint8_t* d_regs, uint64_t G,
                                  bool pool_zero, bool write_all, PCount pc);
 // Performs a pending lazy clear (rsk_api.hip).
 void hll_materialize(const rsk_hll* h);

@@ -206,6 +206,40 @@ class GroupedHyperLogLog:
         _lib.check(_lib.load().rsk_hll_get_registers(self.pool, gid, out.ctypes.data, _lib.RSK_MEM_HOST))
         return out
 
+    # -- the pool's Redis strings (checkpoint / restore)
+    def exportRedis(self, ids=None, out=None):
+        """GET of many keys (rsk_hll_export_redis_batch): returns (data, offsets)
+        with key i's "HYLL" string in data[offsets[i]:offsets[i+1]] (empty for
+        a missing key).  `out` (a uint8 array) is used when large enough;
+        otherwise the call is repeated with an exact buffer."""
+        ids = np.arange(self.n, dtype=np.uint64) if ids is None else np.ascontiguousarray(ids, dtype=np.uint64)
+        offs = np.zeros(ids.size + 1, dtype=np.uint64)
+        L = _lib.load()
+        if out is None or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            out = np.empty(0, np.uint8)
+        rc = L.rsk_hll_export_redis_batch(self.pool, ids.ctypes.data, ids.size, out.ctypes.data if out.size else None,
+                                          out.size, offs.ctypes.data)
+        if rc == _lib.RSK_ERR_INVALID_ARG and int(offs[-1]) > out.size:
+            out = np.empty(int(offs[-1]), np.uint8)
+            rc = L.rsk_hll_export_redis_batch(self.pool, ids.ctypes.data, ids.size, out.ctypes.data, out.size,
+                                              offs.ctypes.data)
+        _lib.check(rc)
+        return out[: int(offs[-1])], offs
+
+    def importRedis(self, ids, data, offsets) -> None:
+        """SET of many keys (rsk_hll_import_redis_batch): key ids[i] := the string
+        data[offsets[i]:offsets[i+1]]; all or nothing."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        data = np.ascontiguousarray(np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                                    dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        if offs.size != ids.size + 1 or (ids.size and int(offs[-1]) > data.size):
+            raise ValueError("offsets must hold n + 1 entries inside data")
+        _lib.check(_lib.load().rsk_hll_import_redis_batch(self.pool, ids.ctypes.data, ids.size,
+                                                          data.ctypes.data, offs.ctypes.data))
+
     # -- pipelined forms (the library's async calls, ordered on the context
     # stream like the synchronous ones; each returns a NativeOp to wait on)
     def add_async(self, keys: KeyBatch, groups) -> "_lib.NativeOp":

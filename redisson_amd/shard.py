@@ -5,6 +5,8 @@ RCCL layer of librsketch (rsk_comm.hip):
   HLL   : rsk_hll_allreduce        ncclAllReduce(uint8, MAX), 16 KiB
   pools : rsk_hll_allreduce_pool   the same over [n][16384]
           rsk_hll_reducescatter_pool  MAX reduce-scatter: rank r owns 1/N of the sketches (C5)
+          rsk_hll_add_grouped_routed  pairs hashed where they live, 8-byte records
+                                      sent to the rank owning their sketch (C5)
   Bloom : rsk_bloom_allreduce_or   slices to their owners, local OR, merged slices back
 
 torch.distributed is used only as the out-of-band channel that ships the
@@ -98,6 +100,63 @@ def owner_of(ids, n: int, world: int) -> np.ndarray:
     if q == 0:
         return np.full(ids.shape, world - 1, dtype=np.int64)
     return np.minimum(ids // np.uint64(q), np.uint64(world - 1)).astype(np.int64)
+
+
+def hll_add_grouped_routed(pool, keys, groups, flags: int = 0):
+    """Collective grouped PFADD routed to the owners (rsk_hll_add_grouped_routed):
+    every rank passes its own device-resident 16-byte keys (a KeyBatch) and
+    uint32 group ids (a DeviceBuffer); returns (first, count) of the sketches
+    this rank owns, which then hold every rank's pairs."""
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    ks = keys.as_struct()
+    _lib.check(_lib.load().rsk_hll_add_grouped_routed(pool, ctypes.byref(ks), groups.ptr if keys.n else None, flags,
+                                                      ctypes.byref(first), ctypes.byref(count)),
+               "rsk_hll_add_grouped_routed")
+    return first.value, count.value
+
+
+def route_plan(groups, n: int, world: int):
+    """The routing plan of rsk_hll_add_grouped_routed restated: for each pair
+    its owner (ids >= n dropped: -1) and its id local to the owner's range,
+    and the pairs sent to each rank (records[o] in the send buffer are the
+    pairs with owner o, in any order: MAX does not care)."""
+    g = np.asarray(groups, dtype=np.uint64)
+    valid = g < np.uint64(n)
+    owner = np.where(valid, owner_of(np.where(valid, g, 0), n, world), -1)
+    q = n // world
+    local = np.where(valid, g - owner.clip(0).astype(np.uint64) * np.uint64(q), 0).astype(np.uint64)
+    counts = np.bincount(owner[valid], minlength=world).astype(np.uint64)
+    return owner, local, counts
+
+
+def hll_add_grouped_routed_cpu(records, groups, n: int, group=None):
+    """The routed grouped add on CPU tensors, same plan as the GPU path:
+    `records` (uint32 index << 6 | rank per pair, the hash taken where the
+    pair lives) and `groups` of this rank's pairs; pairs sorted by owner, the
+    per-owner counts then the 8-byte records {local id, record} exchanged
+    all-to-all, each rank maxing what it receives into its owned rows.
+    Returns (first, count, owned rows [count][16384])."""
+    import torch
+    import torch.distributed as dist
+
+    N, r = dist.get_world_size(group), dist.get_rank(group)
+    owner, local, counts = route_plan(groups, n, N)
+    order = np.argsort(owner, kind="stable")
+    order = order[owner[order] >= 0]
+    send = np.stack([local[order].astype(np.int64), np.asarray(records, np.uint32)[order].astype(np.int64)], 1)
+    cin = torch.zeros(N, dtype=torch.int64)
+    dist.all_to_all_single(cin, torch.from_numpy(counts.astype(np.int64)), group=group)
+    si, so = [int(x) for x in cin], [int(x) for x in counts]
+    recv = torch.zeros(sum(si) * 2, dtype=torch.int64)
+    dist.all_to_all_single(recv, torch.from_numpy(send.reshape(-1).copy()), output_split_sizes=[2 * x for x in si],
+                           input_split_sizes=[2 * x for x in so], group=group)
+    rec = recv.numpy().reshape(-1, 2)
+    first, count = owned_range(n, N, r)
+    rows = np.zeros((count, 16384), np.uint8)
+    if rec.size:
+        idx, rank = (rec[:, 1] >> 6).astype(np.int64), (rec[:, 1] & 63).astype(np.uint8)
+        np.maximum.at(rows, (rec[:, 0], idx), rank)
+    return first, count, rows
 
 
 def hll_fetch_rows(pool, ids, flags: int = 0) -> None:

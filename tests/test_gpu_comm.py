@@ -166,3 +166,103 @@ def test_device_memory_roundtrip(engine):
     b.zero()
     assert not b.to_numpy().any()
     b.free()
+
+
+def _rows_equal(L, engine, a, b, G):
+    """Every row of two pools equal (device copies compared in chunks)."""
+    from redisson_amd import _lib
+
+    pa, pb = L.rsk_hll_device_registers(a), L.rsk_hll_device_registers(b)
+    chunk = 16384
+    for lo in range(0, G, chunk):
+        m = min(chunk, G - lo)
+        x = np.zeros(m * 16384, np.uint8)
+        y = np.zeros(m * 16384, np.uint8)
+        _lib.check(L.rsk_memcpy(engine.ctx, x.ctypes.data, ctypes.c_void_p(pa + lo * 16384), x.size, 1))
+        _lib.check(L.rsk_memcpy(engine.ctx, y.ctypes.data, ctypes.c_void_p(pb + lo * 16384), y.size, 1))
+        if not np.array_equal(x, y):
+            bad = np.nonzero((x != y).reshape(m, 16384).any(1))[0]
+            return lo + int(bad[0])
+    return None
+
+
+@pytest.mark.parametrize("G,n", [(5000, 10_000), (100_000, 5_000_000)])
+def test_routed_add_self_exchange(engine, orc, G, n):
+    """rsk_hll_add_grouped_routed on a 1-rank communicator with RSK_FETCH_SELF:
+    the route count and scatter kernels, the record exchange through RCCL to
+    itself and the record-input grouped add (the direct CAS kernel for the
+    small batch, the partitioned pipeline for the large one, onto a pending
+    clear) give the registers of the plain grouped add; ids >= G are ignored."""
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    engine.prof_enable(True)
+    engine.prof_reset()
+    try:
+        groups, keys = orc.gen_grouped(0x5EED0006, G, 0, n)
+        groups[::101] = G + 7
+        kd = devmem.DeviceBuffer.from_numpy(engine, keys)
+        gd = devmem.DeviceBuffer.from_numpy(engine, groups)
+        kb = kd.keys_fixed(n, 16)
+        a = GroupedHyperLogLog(engine, G)
+        b = GroupedHyperLogLog(engine, G)
+        a.add(kb, gd)
+        a.add(kb, gd)  # (rows to clear below)
+        b.clear()
+        b.add(kb, gd)  # reference: the plain grouped add from a cleared pool
+        a.clear()      # the routed add completes the lazy clear on the owned rows
+        assert shard.hll_add_grouped_routed(a.pool, kb, gd, flags=_lib.RSK_FETCH_SELF) == (0, G)
+        assert _prof(engine, "hll_route_exchange") == 1
+        assert _rows_equal(L, engine, a.pool, b.pool, G) is None
+        for gid in (0, 1, G // 2, G - 1):
+            ref = np.zeros(16384, np.uint8)
+            sel = groups == gid
+            orc.hll_add(ref, keys.reshape(-1, 16)[sel].reshape(-1), None, 16, int(sel.sum()))
+            assert np.array_equal(a.registers(gid), ref), gid
+        assert list(a.count(ids=[0, 1])) == list(b.count(ids=[0, 1]))
+        shard.hll_add_grouped_routed(a.pool, kb, gd)  # without the flag: own records stay local; re-adds change nothing
+        assert _rows_equal(L, engine, a.pool, b.pool, G) is None
+        a.close()
+        b.close()
+        kd.free()
+        gd.free()
+    finally:
+        engine.prof_enable(False)
+        _lib.check(L.rsk_comm_destroy(engine.ctx))
+
+
+def test_routed_add_c5_full_size_self_exchange(engine, orc):
+    """BASELINE configs[4] at its per-GPU size through the routed form at N = 1
+    (every record through RCCL to itself): the stratified sample of sketches is
+    bit-exact against the oracle over the whole pair stream."""
+    import os
+
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+    from test_gpu_hll import _c5_stratified_sample
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    try:
+        G, n = 1_000_000, 500_000_000
+        g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+        pool = GroupedHyperLogLog(engine, G)
+        pool.clear()
+        assert shard.hll_add_grouped_routed(pool.pool, k.keys_fixed(n, 16), g, flags=_lib.RSK_FETCH_SELF) == (0, G)
+        g.free()
+        k.free()
+        sample = _c5_stratified_sample(G)
+        ref = np.zeros((sample.size, 16384), np.uint8)
+        orc.hll_add_gen_grouped_ids(ref, G, sample, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
+        bad = [gid for s, gid in enumerate(sample.tolist()) if not np.array_equal(pool.registers(gid), ref[s])]
+        assert not bad, (len(bad), bad[:10])
+        pool.close()
+        _lib.check(L.rsk_trim(engine.ctx))
+    finally:
+        _lib.check(L.rsk_comm_destroy(engine.ctx))

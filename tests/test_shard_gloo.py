@@ -127,6 +127,66 @@ def test_grouped_reducescatter_owned_slices(world, G, orc):
     assert covered == G
 
 
+def _worker_routed(rank, world, port, G, n, q):
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from redisson_amd.shard import ShardPlan, hll_add_grouped_routed_cpu
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = ShardPlan(n, world).range(rank)
+        groups, keys = O.gen_grouped(0x5EED0006, G, lo, hi - lo)
+        groups[::97] = G + 3  # ids outside the pool are dropped, as by the grouped add
+        recs = O.hll_records(keys, 16, hi - lo)  # hashed where the pair lives
+        first, count, owned = hll_add_grouped_routed_cpu(recs, groups, G)
+        q.put((rank, first, count, owned.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,G", [(2, 7), (3, 1000), (3, 2)])
+def test_grouped_routed_owned_slices(world, G, orc):
+    """C5 across GPUs, routed form (rsk_hll_add_grouped_routed's plan): each
+    rank's pairs hashed locally, records sorted by owner and exchanged
+    all-to-all, each owner maxing its own rows; every rank's owned sketches
+    equal the single-process sketches (ids outside the pool dropped), the
+    owned ranges tile [0, G) (tail and G < N included)."""
+    n = 40_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_routed, args=(r, world, port, G, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process: every pair of the stream but the dropped ones (every 97th of each shard)
+    from redisson_amd.shard import ShardPlan
+
+    ref = np.zeros((G, orc.REGISTERS), np.uint8)
+    for r in range(world):
+        lo, hi = ShardPlan(n, world).range(r)
+        g, k = orc.gen_grouped(0x5EED0006, G, lo, hi - lo)
+        keep = np.ones(hi - lo, bool)
+        keep[::97] = False
+        for gid in np.unique(g[keep]):
+            sel = keep & (g == gid)
+            orc.hll_add(ref[gid], k.reshape(-1, 16)[sel].reshape(-1), None, 16, int(sel.sum()))
+    full = np.zeros((G, orc.REGISTERS), np.uint8)
+    orc.hll_add_gen_grouped(full, G, 0x5EED0006, 0, n)
+    assert (ref <= full).all()  # (pinned: dropping pairs only lowers registers)
+    covered = 0
+    for rank, first, count, owned in results:
+        assert first == covered
+        covered += count
+        assert owned == ref[first:first + count].tobytes(), rank
+    assert covered == G
+
+
 def _worker_fetch(rank, world, port, G, n, q):
     import torch.distributed as dist
 
