@@ -59,6 +59,20 @@ ncclComm_t comm_of(rsk_ctx* c) {
   return reinterpret_cast<ncclComm_t>(c->comm);
 }
 
+// One point-to-point transfer as pieces of at most 1 GiB (a 4 GB self
+// send/recv of the routed add's records came back wrong in one piece, 1 GiB
+// pieces right; the pieces to one peer are matched in issue order on both
+// sides).  Every row / slice / record exchange below goes through it.
+constexpr uint64_t P2P_PIECE = 1ull << 30;
+void p2p_pieces(const void* buf, uint64_t bytes, int peer, ncclComm_t comm, hipStream_t s, bool send) {
+  for (uint64_t o = 0; o < bytes; o += P2P_PIECE) {
+    const uint64_t m = std::min(P2P_PIECE, bytes - o);
+    const uint8_t* p = static_cast<const uint8_t*>(buf) + o;
+    if (send) RSK_NCCL(ncclSend(p, m, ncclUint8, peer, comm, s));
+    else RSK_NCCL(ncclRecv(const_cast<uint8_t*>(p), m, ncclUint8, peer, comm, s));
+  }
+}
+
 __global__ void invalidate_card_kernel(uint64_t* card, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     card[i] |= (1ull << 63);
@@ -383,8 +397,8 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
       RSK_NCCL(ncclGroupStart());
       for (uint64_t j = 0, so = 0, ro = 0; j < N; so += scnt[j], ro += scnt[N + j], ++j) {
         if (j == r && !self) continue;
-        if (scnt[j]) RSK_NCCL(ncclSend(d_send + so, scnt[j] * 8, ncclUint8, (int)j, comm, c->stream));
-        if (scnt[N + j]) RSK_NCCL(ncclRecv(d_recv + ro, scnt[N + j] * 8, ncclUint8, (int)j, comm, c->stream));
+        p2p_pieces(d_send + so, scnt[j] * 8, (int)j, comm, c->stream, true);
+        p2p_pieces(d_recv + ro, scnt[N + j] * 8, (int)j, comm, c->stream, false);
       }
       RSK_NCCL(ncclGroupEnd());
     }
@@ -493,8 +507,8 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
     }
     RSK_NCCL(ncclGroupStart());  // the rows, in request order
     for (uint64_t j = 0, so = 0, ro = 0; j < N; so += cnt[N + j], ro += cnt[j], ++j) {
-      if (cnt[N + j]) RSK_NCCL(ncclSend(rows_send + so * R, cnt[N + j] * R, ncclUint8, (int)j, comm, c->stream));
-      if (cnt[j]) RSK_NCCL(ncclRecv(rows_recv + ro * R, cnt[j] * R, ncclUint8, (int)j, comm, c->stream));
+      p2p_pieces(rows_send + so * R, cnt[N + j] * R, (int)j, comm, c->stream, true);
+      p2p_pieces(rows_recv + ro * R, cnt[j] * R, (int)j, comm, c->stream, false);
     }
     RSK_NCCL(ncclGroupEnd());
     if (n_out) {
@@ -544,8 +558,8 @@ int rsk_bloom_allreduce_or_flags(rsk_bloom* b, uint32_t flags) {
         RSK_NCCL(ncclGroupStart());
         for (size_t r = 0; r < peers.size(); ++r) {
           const uint64_t j = peers[r];
-          if (sz(j)) RSK_NCCL(ncclSend(b->d_bits + j * S, sz(j) * 4, ncclUint8, (int)j, comm, c->stream));
-          if (mine) RSK_NCCL(ncclRecv(recv + r * row, mine * 4, ncclUint8, (int)j, comm, c->stream));
+          p2p_pieces(b->d_bits + j * S, sz(j) * 4, (int)j, comm, c->stream, true);
+          p2p_pieces(recv + r * row, mine * 4, (int)j, comm, c->stream, false);
         }
         RSK_NCCL(ncclGroupEnd());
       }
@@ -556,8 +570,8 @@ int rsk_bloom_allreduce_or_flags(rsk_bloom* b, uint32_t flags) {
         for (uint64_t j : peers) {
           // my own slice coming back (self exchange) lands in the consumed recv rows
           uint32_t* into = j == me ? recv : b->d_bits + j * S;
-          if (mine) RSK_NCCL(ncclSend(b->d_bits + me * S, mine * 4, ncclUint8, (int)j, comm, c->stream));
-          if (sz(j)) RSK_NCCL(ncclRecv(into, sz(j) * 4, ncclUint8, (int)j, comm, c->stream));
+          p2p_pieces(b->d_bits + me * S, mine * 4, (int)j, comm, c->stream, true);
+          p2p_pieces(into, sz(j) * 4, (int)j, comm, c->stream, false);
         }
         RSK_NCCL(ncclGroupEnd());
       }

@@ -86,6 +86,12 @@ def _mixed_pool(L, engine, orc):
         ks_ = KeyBatch.from_numpy(ks).as_struct()
         _lib.check(L.rsk_hll_add(h, i, ctypes.byref(ks_), ctypes.byref(ch)))
 
+    # ids 30 .. 63: grouped adds of a few keys each (the C5 shape; first: a grouped add
+    # drops every kept SET string of the pool)
+    gk = orc.gen_keys16(SEED_C2, 100000, 34 * 300).reshape(-1, 16)
+    grp = (30 + np.arange(gk.shape[0]) % 34).astype(np.uint32)
+    ks_ = KeyBatch.from_numpy(gk).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks_), grp.ctypes.data))
     add(1, keys[:0])                     # created, all-zero: one XZERO
     sizes = [1, 2, 5, 17, 64, 100, 300, 700, 1200, 2000, 5000, 20000]
     at = 0
@@ -122,11 +128,6 @@ def _mixed_pool(L, engine, orc):
     d2[6] = 7
     b = (ctypes.c_uint8 * len(d2)).from_buffer_copy(bytes(d2))
     _lib.check(L.rsk_hll_import_redis(h, 24, b, len(d2)))
-    # ids 30 .. 63: grouped adds of a few keys each (the C5 shape)
-    gk = orc.gen_keys16(SEED_C2, 100000, 34 * 300).reshape(-1, 16)
-    grp = (30 + np.arange(gk.shape[0]) % 34).astype(np.uint32)
-    ks_ = KeyBatch.from_numpy(gk).as_struct()
-    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks_), grp.ctypes.data))
     return h, G
 
 
