@@ -1083,10 +1083,16 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
 }
 
 // List the extra work items: entry (s << 13) | (part << 12) | j for chunk
-// j >= 1 of fine bin s, part `part` (records [a + j GP_CH, min(e, a + (j+1) GP_CH))).
+// j >= 1 of fine bin s, part `part` (records [a + j GP_CH, min(e, a + (j+1) GP_CH))),
+// and per heavy fine bin one hot entry {s, first list index, chunks}: the
+// slabs the extra items leave are reduced into that bin's rows afterwards.
+struct GHot {
+  uint32_t s, at, extra;
+};
 __global__ __launch_bounds__(256) void hll_gextra_list_kernel(const uint32_t* __restrict__ off2, uint32_t G1,
                                                               uint32_t nfine, uint32_t cap,
-                                                              uint32_t* __restrict__ list, uint32_t* __restrict__ nlist) {
+                                                              uint32_t* __restrict__ list, uint32_t* __restrict__ nlist,
+                                                              GHot* __restrict__ hot, uint32_t* __restrict__ nhot) {
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nfine; s += gridDim.x * blockDim.x) {
     const uint32_t n = off2[(uint64_t)(s + 1) * G1] - off2[(uint64_t)s * G1];
     if (n <= GP_CH) continue;
@@ -1097,70 +1103,135 @@ __global__ __launch_bounds__(256) void hll_gextra_list_kernel(const uint32_t* __
         const uint32_t q = at + (j - 1) * GP_NP + h;
         if (q < cap) list[q] = (s << 13) | (h << 12) | j;
       }
+    hot[atomicAdd(nhot, 1u)] = GHot{s, at, extra};
   }
 }
 
-// Extra chunks of heavy fine bins, after hll_gapply wrote every row: the
-// chunk's records are maxed into zeroed LDS registers, then each non-zero
-// word is folded into the pool row by a bytewise-max CAS (only the few
-// workgroups of one heavy bin contend for its words).
+// Extra chunks of heavy fine bins (skewed groups: under Zipf(1.1) the first
+// fine bin holds 40 % of the pairs): each chunk's records are maxed into a
+// zeroed LDS file, which is stored whole as the chunk's private slab
+// (nontemporal: read once by hll_gextra_reduce).  Earlier, each chunk folded
+// its file into the pool rows by bytewise-max CAS: ~170 chunks of one bin
+// serialised on the same 128 KiB of words.
 __global__ __launch_bounds__(GP_T) void hll_gapply_extra_kernel(const uint32_t* __restrict__ recs,
                                                                 const uint32_t* __restrict__ off2, uint32_t G1,
                                                                 uint64_t G, const uint32_t* __restrict__ list,
                                                                 const uint32_t* __restrict__ nlist, uint32_t cap,
-                                                                uint8_t* __restrict__ regs) {
+                                                                uint8_t* __restrict__ slabs) {
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
   const uint32_t nl = min(*nlist, cap);
+  // (consecutive entries -- the two halves of a chunk -- placed on one XCD by
+  // xcd_slot measured slower: 0.93 against 0.70 ms at C5 Zipf(1.1), the
+  // second round of items then falls on two XCDs)
   for (uint32_t w = blockIdx.x; w < nl; w += gridDim.x) {
     const uint32_t ent = list[w], s = ent >> 13, half = (ent >> 12) & 1u, j = ent & 4095u;
     const uint32_t a0 = off2[(uint64_t)s * G1], e0 = off2[(uint64_t)(s + 1) * G1];
     const uint32_t a = a0 + j * GP_CH, e = e0 - a > GP_CH ? a + GP_CH : e0;
     const uint64_t g0 = (uint64_t)(s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(s & 255) * 16 + half * GP_SK;
     if (g0 >= G) continue;
-    const uint32_t nsk = (uint32_t)(G - g0 < GP_SK ? G - g0 : GP_SK);
     for (uint32_t q = threadIdx.x; q < GP_SK * HLL_REGS / 4; q += GP_T) r32[q] = 0;
     __syncthreads();
-    for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += GP_T * GP_U) {
-      uint32_t rv[GP_U];
+    // uint4 record loads, XR per lane issued together (clamped, unconditional:
+    // every load in flight at once), the next round's issued before this
+    // round's records are applied (the chunk is latency-bound otherwise: a
+    // saturated hot sketch changes almost no register, so each record costs
+    // only its load and one LDS read)
+    constexpr int XR = 4;
+    const uint4* r4 = reinterpret_cast<const uint4*>(recs);
+    const uint32_t q0 = a >> 2, q1 = (e + 3) >> 2;
+    auto xload = [&](uint32_t qb, uint4 (&v)[XR]) {
 #pragma unroll
-      for (int u = 0; u < GP_U; ++u) {
-        const uint32_t i = i0 + u * GP_T;
-        rv[u] = i < e ? __builtin_nontemporal_load(&recs[i]) : 0xFFFFFFFFu;
+      for (int u = 0; u < XR; ++u) {
+        const uint32_t q = qb + threadIdx.x + u * GP_T;
+        v[u] = ld_nt16(r4 + (q < q1 ? q : q0));
       }
+    };
+    uint4 cur[XR], nxt[XR];
+    xload(q0, cur);
+    for (uint32_t qb = q0; qb < q1; qb += XR * GP_T) {
+      xload(qb + XR * GP_T, nxt);
 #pragma unroll
-      for (int u = 0; u < GP_U; ++u) {
-        const uint32_t r = rv[u];
-        const uint32_t sk = (r >> 20) & 15u;
-        if (r == 0xFFFFFFFFu || sk / GP_SK != half) continue;
-        const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
-        const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
-        uint32_t* word = &r32[byte >> 2];
-        uint32_t old = *word;
-        while (((old >> sh) & 0xFFu) < rank) {
-          const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
-          if (prev == old) break;
-          old = prev;
+      for (int u = 0; u < XR; ++u) {
+        const uint32_t q = qb + threadIdx.x + u * GP_T;
+        const uint32_t x[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t i = 4 * q + m, r = x[m];
+          const uint32_t sk = (r >> 20) & 15u;
+          if (q >= q1 || i < a || i >= e || sk / GP_SK != half) continue;
+          const uint32_t byte = (sk % GP_SK) * HLL_REGS + ((r >> 6) & (HLL_REGS - 1));
+          const uint32_t rank = r & 63u, sh = (byte & 3u) * 8;
+          uint32_t* word = &r32[byte >> 2];
+          uint32_t old = *word;
+          while (((old >> sh) & 0xFFu) < rank) {
+            const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+            if (prev == old) break;
+            old = prev;
+          }
         }
       }
+#pragma unroll
+      for (int u = 0; u < XR; ++u) cur[u] = nxt[u];
     }
     __syncthreads();
-    uint32_t* gw = reinterpret_cast<uint32_t*>(regs + g0 * HLL_REGS);
-    for (uint32_t q = threadIdx.x; q < nsk * (HLL_REGS / 4); q += GP_T) {
-      const uint32_t v = r32[q];
-      if (!v) continue;
-      uint32_t old = gw[q];
-      for (;;) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) m |= max((old >> (8 * b)) & 0xFFu, (v >> (8 * b)) & 0xFFu) << (8 * b);
-        if (m == old) break;
-        const uint32_t prev = atomicCAS(&gw[q], old, m);
-        if (prev == old) break;
-        old = prev;
-      }
+    const uint4* l4 = reinterpret_cast<const uint4*>(r32);
+    u32x4* sl = reinterpret_cast<u32x4*>(slabs + (uint64_t)w * GP_SK * HLL_REGS);
+    for (uint32_t q = threadIdx.x; q < GP_SK * HLL_REGS / 16; q += GP_T) {
+      const uint4 v = l4[q];
+      const u32x4 x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, sl + q);
     }
     __syncthreads();
   }
+}
+
+// Byte-wise max of four register bytes (values <= 63, so bit 7 is free).
+RSK_DEV uint32_t gmax4(uint32_t a, uint32_t b) {
+  const uint32_t d = (a | 0x80808080u) - b;
+  const uint32_t m = ((d & 0x80808080u) >> 7) * 0xFFu;
+  return (a & m) | (b & ~m);
+}
+
+// The rows of every heavy fine bin := their max with the bin's extra slabs.
+// Block (k, t): hot entry k, piece t of its 16 rows (16 sketches x 16 KiB in
+// GX_PC pieces of 2 KiB); each lane one uint4 of the piece, the slabs of its
+// half read one after another (4 loads in flight).
+constexpr uint32_t GX_PIECE = 2048;                       // bytes of a row per block
+constexpr uint32_t GX_PC = 16 * HLL_REGS / GX_PIECE;      // pieces per fine bin (128)
+__global__ __launch_bounds__(128) void hll_gextra_reduce_kernel(const GHot* __restrict__ hot,
+                                                                const uint32_t* __restrict__ nhot, uint32_t cap,
+                                                                const uint8_t* __restrict__ slabs, uint64_t G,
+                                                                uint8_t* __restrict__ regs) {
+  const uint32_t k = blockIdx.x / GX_PC, t = blockIdx.x % GX_PC;
+  if (k >= *nhot) return;
+  const GHot hk = hot[k];
+  const uint32_t byte0 = t * GX_PIECE + threadIdx.x * 16;   // byte of the fine bin's 16 rows (256 KiB)
+  const uint32_t sk = byte0 / HLL_REGS, half = sk / GP_SK;  // sketch in the fine bin, its half
+  const uint64_t g = (uint64_t)(hk.s >> 8) * (1u << GP_BIN_SHIFT) + (uint64_t)(hk.s & 255) * 16 + sk;
+  if (g >= G) return;
+  uint4* row = reinterpret_cast<uint4*>(regs + g * HLL_REGS + (byte0 % HLL_REGS));
+  uint4 m = *row;
+  const uint64_t in_slab = (uint64_t)(sk % GP_SK) * HLL_REGS + (byte0 % HLL_REGS);
+  uint32_t j = 1;
+  for (; j + 3 <= hk.extra; j += 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t q = hk.at + (j + u - 1) * GP_NP + half;
+      v[u] = q < cap ? ld_nt16(reinterpret_cast<const uint4*>(slabs + (uint64_t)q * GP_SK * HLL_REGS + in_slab))
+                     : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      m = make_uint4(gmax4(m.x, v[u].x), gmax4(m.y, v[u].y), gmax4(m.z, v[u].z), gmax4(m.w, v[u].w));
+  }
+  for (; j <= hk.extra; ++j) {
+    const uint32_t q = hk.at + (j - 1) * GP_NP + half;
+    if (q >= cap) continue;
+    const uint4 v = ld_nt16(reinterpret_cast<const uint4*>(slabs + (uint64_t)q * GP_SK * HLL_REGS + in_slab));
+    m = make_uint4(gmax4(m.x, v.x), gmax4(m.y, v.y), gmax4(m.z, v.z), gmax4(m.w, v.w));
+  }
+  *row = m;
 }
 
 bool hll_grouped_partition_applies(const rsk_ctx* c, const DevKeys& keys, uint64_t G, bool recs) {
@@ -1200,9 +1271,11 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt1, c->stream);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)ncnt2, c->stream);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  const uint32_t xcap = (uint32_t)(GP_NP * (chunk / GP_CH + 1) + 16);  // extra work items per chunk, at most
+  const uint32_t xcap = (uint32_t)(GP_NP * (max_np / GP_CH + 1) + 16);  // extra work items per chunk, at most
+  const uint32_t hcap = (uint32_t)(max_np / GP_CH + 2);                 // heavy fine bins per chunk, at most
   const uint64_t meta = 2 * al(4 * ncnt1) + 2 * al(4 * ncnt2) + al(std::max(sb1, sb2)) + al(4 * (xcap + 1)) +
-                        al(sizeof(GPart) * qmax) + al(4 * (nfine + 1)) + 256;
+                        al(sizeof(GPart) * qmax) + al(4 * (nfine + 1)) + 256 + al(sizeof(GHot) * hcap) + 256 +
+                        al((uint64_t)xcap * GP_SK * HLL_REGS);
   // tile-major first pass: NT tiles of GP_TILE record slots, a u16 header per tile and bin (and
   // its transpose), the per-bin segment prefix
   const uint32_t HS = nbins1 + 1;
@@ -1230,6 +1303,9 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   GPart* parts = reinterpret_cast<GPart*>(take(al(sizeof(GPart) * qmax)));
   uint32_t* off2 = reinterpret_cast<uint32_t*>(take(al(4 * (nfine + 1))));
   uint32_t* d_nq = reinterpret_cast<uint32_t*>(take(256));
+  GHot* xhot = reinterpret_cast<GHot*>(take(al(sizeof(GHot) * hcap)));
+  uint32_t* xnhot = reinterpret_cast<uint32_t*>(take(256));
+  uint8_t* xslabs = take(al((uint64_t)xcap * GP_SK * HLL_REGS));
   uint16_t* hdr = reinterpret_cast<uint16_t*>(w + meta);
   uint16_t* hdrT = reinterpret_cast<uint16_t*>(w + meta + al(2 * nt_max * HS));
   uint32_t* seglen = reinterpret_cast<uint32_t*>(w + meta + al(2 * nt_max * HS) + al(2 * nseg));
@@ -1319,12 +1395,16 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
                          (write_all && first == 0) ? 1 : 0, d_regs, pc, c->d_lc);
       RSK_CHECK_LAUNCH("hll_gapply");
       RSK_HIP(hipMemsetAsync(xcount, 0, 4, c->stream));
+      RSK_HIP(hipMemsetAsync(xnhot, 0, 4, c->stream));
       hipLaunchKernelGGL(hll_gextra_list_kernel, dim3((nfine + 255) / 256), dim3(256), 0, c->stream, off2, 1u, nfine,
-                         xcap, xlist, xcount);
+                         xcap, xlist, xcount, xhot, xnhot);
       RSK_CHECK_LAUNCH("hll_gextra_list");
       hipLaunchKernelGGL(hll_gapply_extra_kernel, dim3(2 * cus), dim3(GP_T), 0, c->stream, buf_b, off2, 1u, G, xlist,
-                         xcount, xcap, d_regs);
+                         xcount, xcap, xslabs);
       RSK_CHECK_LAUNCH("hll_gapply_extra");
+      hipLaunchKernelGGL(hll_gextra_reduce_kernel, dim3(hcap * GX_PC), dim3(GX_PIECE / 16), 0, c->stream, xhot, xnhot,
+                         xcap, xslabs, G, d_regs);
+      RSK_CHECK_LAUNCH("hll_gextra_reduce");
     }
   }
   return true;

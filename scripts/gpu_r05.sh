@@ -72,6 +72,11 @@ for p in ${PART//,/ }; do
         step gab_$rep 120 python3 scripts/gpart_profile.py 5 $z "$f" || exit 1
         grep '^{' gpurun_out/gab_$rep.log >> gpurun_out/gab.jsonl
       done; done; done ;;
+    gtrace)  # kernel trace of the C5 grouped add alone (uniform and Zipf 1.1)
+      for z in 0 1.1; do
+        rm -rf gpurun_out/gtrace_$z
+        step gtrace_$z 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gtrace_$z -o run -- python3 scripts/gpart_profile.py 5 $z || exit 1
+      done ;;
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;
