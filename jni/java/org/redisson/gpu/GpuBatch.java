@@ -180,19 +180,38 @@ public final class GpuBatch {
         }
     }
 
+    /* Largest SETBIT offset Redis accepts (512 MB strings: 2^32 - 1 bits), as
+     * the shim's check (rsketch_shim.c offsets_ok). */
+    private static final long MAX_BIT_OFFSET = 4294967295L;
+
+    /* A pipeline fails only the SETBITs Redis rejects (offset out of range, each
+     * with Redis's error) and applies the others: they go in one native call. */
     private void runSetBits(List<Op> run) {
         SetBitOp first = (SetBitOp) run.get(0);
-        long[] indexes = new long[run.size()];
-        for (int q = 0; q < run.size(); q++) {
-            indexes[q] = ((SetBitOp) run.get(q)).index;
+        List<Op> good = new ArrayList<Op>(run.size());
+        for (Op op : run) {
+            long index = ((SetBitOp) op).index;
+            if (index < 0 || index > MAX_BIT_OFFSET) {
+                op.promise.setFailure(new org.redisson.client.RedisException(
+                        "ERR bit offset is not an integer or out of range"));
+            } else {
+                good.add(op);
+            }
+        }
+        if (good.isEmpty()) {
+            return;
+        }
+        long[] indexes = new long[good.size()];
+        for (int q = 0; q < good.size(); q++) {
+            indexes[q] = ((SetBitOp) good.get(q)).index;
         }
         try {
             RSketchNative.bitsetSetBits(gpu.space, first.name, indexes, first.value);
-            for (Op op : run) {
+            for (Op op : good) {
                 op.promise.setSuccess(null);
             }
         } catch (RuntimeException e) {
-            for (Op op : run) {
+            for (Op op : good) {
                 op.promise.setFailure(e);
             }
         }

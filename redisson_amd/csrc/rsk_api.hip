@@ -793,7 +793,6 @@ int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out
     bool created;
     check_keys(c, keys);
     check_out(c, keys, out);
-    hll_forget_import(h, id);
     create_if_missing(h, id, &created);
     // Sub-chunks bounded for the 32-bit sort; replies compose sequentially.
     const uint64_t max_chunk = 1ull << 26;
@@ -825,10 +824,12 @@ int rsk_hll_add_each(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* out
         bool any = created;
         for (uint64_t i = 0; i < keys->n && !any; ++i) any = out[i] != 0;
         if (any) invalidate(h, id, nullptr, true);
+        if (any) hll_forget_import(h, id);  // a kept SET string survives PFADDs that change nothing (as rsk_hll_add)
         if (created) out[0] = 1;
       } else {
         // Device replies: cheap on-device OR via the flag word.
         invalidate(h, id, nullptr, true);  // conservative: a no-op PFADD keeps the old card bytes valid in Redis
+        hll_forget_import(h, id);          // conservative too (device replies are not read back)
         if (created) RSK_HIP(hipMemsetAsync(out, 1, 1, c->stream));
       }
     } else if (created) {
@@ -1554,6 +1555,7 @@ int rsk_bloom_add(rsk_bloom* b, const rsk_keys* keys, uint8_t* added_out) {
     CtxLock l(c);
     check_keys(c, keys);
     check_out(c, keys, added_out);
+    ++b->wgen;
     if (!added_out) {
       for_each_chunk(c, keys, [&](const DevKeys& dk, uint64_t, uint64_t) { bloom_add_launch(c, b, dk); });
       return;
@@ -1657,6 +1659,9 @@ int rsk_bloom_import_bits(rsk_bloom* b, const uint8_t* buf, size_t len) {
     RSK_HIP(hipMemsetAsync(b->d_bits, 0, b->nwords * 4, b->ctx->stream));
     if (len) RSK_HIP(hipMemcpyAsync(b->d_bits, buf, len, hipMemcpyHostToDevice, b->ctx->stream));
     RSK_HIP(hipStreamSynchronize(b->ctx->stream));
+    ++b->wgen;  // SET of the whole string: its views take STRLEN = len
+    ++b->rgen;
+    b->set_len = len;
   });
 }
 
@@ -1667,6 +1672,7 @@ int rsk_bloom_or_bits(rsk_bloom* b, const uint8_t* bits, size_t len, uint32_t lo
     rsk_ctx* c = b->ctx;
     CtxLock l(c);
     if (len == 0) return;
+    ++b->wgen;
     const uint8_t* src = bits;
     if (location == RSK_MEM_HOST) {
       uint8_t* s = out_scratch(c, len);
@@ -1678,7 +1684,12 @@ int rsk_bloom_or_bits(rsk_bloom* b, const uint8_t* bits, size_t len, uint32_t lo
   });
 }
 
-void* rsk_bloom_device_bits(rsk_bloom* b) { return b ? b->d_bits : nullptr; }
+void* rsk_bloom_device_bits(rsk_bloom* b) {
+  if (!b) return nullptr;
+  std::lock_guard<std::recursive_mutex> g(b->ctx->mu);
+  ++b->wgen;  // the caller may write through the pointer: views rescan their STRLEN
+  return b->d_bits;
+}
 
 }  // extern "C"
 
@@ -1795,6 +1806,7 @@ AsyncOp* op_get(rsk_ctx* c, uint64_t host_bytes, uint64_t dev_bytes) {
   op->user = nullptr;
   op->kind = K_PRESET;
   op->value = 0;
+  op->failed = false;
   op->user_out = op->h_out = nullptr;
   op->n_out = 0;
   op->created = false;
@@ -1835,7 +1847,12 @@ bool streams_failed(rsk_ctx* c) {
 void done_loop(rsk_ctx* c) {
   (void)hipSetDevice(c->device);
   std::unique_lock<std::mutex> lk(c->done_mu);
-  auto ready = [c] { return !c->done_arrived.empty() && c->done_arrived.begin()->first == c->done_delivered + 1; };
+  // entries of ops the watchdog already failed (filed before it took them) are dropped
+  auto ready = [c] {
+    while (!c->done_arrived.empty() && c->done_arrived.begin()->first <= c->done_delivered)
+      c->done_arrived.erase(c->done_arrived.begin());
+    return !c->done_arrived.empty() && c->done_arrived.begin()->first == c->done_delivered + 1;
+  };
   for (;;) {
     const bool woke = c->done_cv.wait_for(lk, std::chrono::milliseconds(500), [&] {
       return ready() || (c->done_stop && c->done_delivered == c->done_submitted);
@@ -1851,6 +1868,9 @@ void done_loop(rsk_ctx* c) {
         AsyncOp* op = it->second;
         c->done_pending.erase(it);
         c->done_arrived.erase(op->seq);
+        // marked while done_mu is held: a host function of this op firing while the
+        // callback below runs (lock released) must not file it again (op_reached)
+        op->failed = true;
         lk.unlock();
         if (op->cb) op->cb(op->user, RSK_ERR_DEVICE, 0);  // the op is not recycled: its copies may still be queued
         lk.lock();
@@ -1877,7 +1897,7 @@ void op_reached(void* p) {
   rsk_ctx* c = op->c;
   {
     std::lock_guard<std::mutex> g(c->done_mu);
-    if (op->seq <= c->done_delivered) return;  // already failed by the watchdog
+    if (op->failed || op->seq <= c->done_delivered) return;  // already failed by the watchdog
     c->done_arrived.emplace(op->seq, op);
   }
   c->done_cv.notify_all();
@@ -2004,7 +2024,7 @@ int rsk_hll_add_async(rsk_hll* h, uint64_t id, const rsk_keys* keys, rsk_done_fn
     bool created = false;
     try {
       create_if_missing(h, id, &created);
-      hll_forget_import(h, id);
+      const bool had_import = h->imported.count(id) != 0;
       uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->d_small);
       if (++c->epoch == 0) {
         RSK_HIP(hipMemsetAsync(d_flag, 0, 4, c->stream));
@@ -2017,6 +2037,13 @@ int rsk_hll_add_async(rsk_hll* h, uint64_t id, const rsk_keys* keys, rsk_done_fn
       if (dk.n) hll_add_launch(c, dk, regs_of(h, id), h->d_card + id, d_flag, op->epoch, created);
       else if (created) invalidate(h, id, nullptr, true);
       RSK_HIP(hipMemcpyAsync(op->h_res, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
+      if (had_import) {
+        // A kept SET string survives a PFADD that changes nothing (as rsk_hll_add): the
+        // decision needs the flag before any later call reads the key, so this (rare)
+        // call waits for it here instead of in the completion.
+        RSK_HIP(hipStreamSynchronize(c->stream));
+        if ((uint32_t)op->h_res[0] == op->epoch || created) hll_forget_import(h, id);
+      }
       op_submit(op, cb, user);
     } catch (...) {
       (void)hipStreamSynchronize(c->stream);
@@ -2271,6 +2298,7 @@ int bloom_async(rsk_bloom* b, const rsk_keys* keys, uint8_t* out, bool out_requi
     const bool host = keys->location == RSK_MEM_HOST;
     const uint64_t kb = host ? al256(host_key_bytes(keys)) : 0;
     const uint64_t ob = (host && out) ? keys->n : 0;
+    if (!out_required) ++b->wgen;  // an add (contains writes no bit)
     AsyncOp* op = op_get(c, kb + ob, kb + ob);
     try {
       const DevKeys dk = stage_keys(c, keys, op, 0);

@@ -31,6 +31,8 @@ struct rsk_bitset {
   // (clears, SET, BITOP) fixed beyond that.
   rsk_bloom* alias = nullptr;
   uint64_t floor = 0;
+  // the filter's write / SET generations this view's len reflects (rsk_bloom::wgen, rgen)
+  uint64_t seen = 0, rseen = 0;
 };
 
 namespace {
@@ -71,6 +73,7 @@ __global__ void length_kernel(const uint4* __restrict__ d, uint64_t len, unsigne
 // to 16 bytes and zero past len.  Under the context lock.
 uint64_t length_bits(rsk_ctx* c, const uint8_t* d, uint64_t len) {
   if (len == 0) return 0;
+  rsk::ProfScope ps(c, "bitset_length");
   auto* dl = reinterpret_cast<unsigned long long*>(c->d_small + 320);
   RSK_HIP(hipMemsetAsync(dl, 0, 8, c->stream));
   hipLaunchKernelGGL(length_kernel, dim3(grid_of(c, (len + 15) / 16)), dim3(256), 0, c->stream,
@@ -85,13 +88,38 @@ uint64_t length_bits(rsk_ctx* c, const uint8_t* d, uint64_t len) {
 
 // A view's STRLEN as it stands now (Bloom adds may have grown it since the
 // last call): refreshes b->d / cap / len.  Plain strings are left alone.
+// The scan runs only when the filter was written since this view last looked
+// (a GETBIT / GET through the view does not rescan a 1.2 GB filter).
 void sync_view(rsk_bitset* b) {
   if (!b->alias) return;
-  b->d = reinterpret_cast<uint8_t*>(b->alias->d_bits);
-  b->cap = b->alias->nwords * 4;
-  const uint64_t bits = length_bits(b->ctx, b->d, b->alias->nbytes);
+  rsk_bloom* f = b->alias;
+  b->d = reinterpret_cast<uint8_t*>(f->d_bits);
+  b->cap = f->nwords * 4;
+  if (b->rseen != f->rgen) {  // the string was SET (rsk_bloom_import_bits, a SET / DEL / BITOP through a view)
+    b->floor = f->set_len;
+    b->rseen = f->rgen;
+    b->seen = 0;
+  }
+  if (b->seen == f->wgen) return;
+  const uint64_t bits = length_bits(b->ctx, b->d, f->nbytes);
   const uint64_t used = bits ? ((bits - 1) >> 3) + 1 : 0;
   b->len = std::max(b->floor, used);
+  b->seen = f->wgen;
+}
+
+// After a write through view b (its len already maintained by grow): other
+// views of the filter rescan; set: the write replaced the whole string
+// (STRLEN = b->len for every view).
+void view_written(rsk_bitset* b, bool set = false) {
+  if (!b->alias) return;
+  rsk_bloom* f = b->alias;
+  ++f->wgen;
+  b->seen = f->wgen;
+  if (set) {
+    ++f->rgen;
+    f->set_len = b->len;
+    b->rseen = f->rgen;
+  }
 }
 
 // Grow the string to `newlen` bytes (zero filled), keeping 16-byte padding.
@@ -312,6 +340,7 @@ int rsk_bitset_setbits(rsk_bitset* b, const uint64_t* offs, uint64_t n, int valu
     hipLaunchKernelGGL(setbits_kernel, dim3(grid_of(c, n)), dim3(256), 0, c->stream, b->d, d_offs, n, value);
     RSK_CHECK_LAUNCH("bitset_setbits");
     RSK_HIP(hipStreamSynchronize(c->stream));
+    view_written(b);
   });
 }
 
@@ -363,6 +392,7 @@ int rsk_bitset_set_range(rsk_bitset* b, uint64_t from, uint64_t to, int value) {
     }
     RSK_CHECK_LAUNCH("bitset_range");
     RSK_HIP(hipStreamSynchronize(c->stream));
+    view_written(b);
   });
 }
 
@@ -418,6 +448,7 @@ int rsk_bitset_bitop(int op, rsk_bitset* dst, rsk_bitset* const* srcs, uint32_t 
       dst->floor = 0;
       if (dst->d) RSK_HIP(hipMemsetAsync(dst->d, 0, dst->cap, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
+      view_written(dst, true);
       return;
     }
     if (dst->alias)
@@ -436,6 +467,7 @@ int rsk_bitset_bitop(int op, rsk_bitset* dst, rsk_bitset* const* srcs, uint32_t 
       RSK_HIP(hipStreamSynchronize(c->stream));
       RSK_HIP(hipFree(nd));
       dst->floor = dst->len = maxlen;
+      view_written(dst, true);
       return;
     }
     RSK_HIP(hipStreamSynchronize(c->stream));
@@ -474,6 +506,7 @@ int rsk_bitset_set_bytes(rsk_bitset* b, const uint8_t* buf, size_t len) {
     grow(b, len);
     if (len) RSK_HIP(hipMemcpyAsync(b->d, buf, len, hipMemcpyHostToDevice, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
+    view_written(b, true);
   });
 }
 
@@ -486,6 +519,7 @@ int rsk_bitset_clear(rsk_bitset* b) {
     RSK_HIP(hipStreamSynchronize(b->ctx->stream));
     b->len = 0;
     b->floor = 0;
+    view_written(b, true);
   });
 }
 

@@ -533,6 +533,7 @@ int rsk_bloom_allreduce_or_flags(rsk_bloom* b, uint32_t flags) {
     rsk_ctx* c = b->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
+    ++b->wgen;
     const uint64_t N = (uint64_t)c->nranks, me = (uint64_t)c->rank;
     // Rank j owns words [j*S, j*S + sz(j)) of the filter: S is a multiple of 4
     // (16-byte vector OR) with N*S >= nwords, so the last slices may be short

@@ -165,24 +165,58 @@ __global__ __launch_bounds__(PT) void hll_gpart1_kernel(const uint4* __restrict_
 // segments, scripts/fetch_calib.py).  Tile t = block b's tile j: t = b tpb + j.
 // REC: the input is already hashed -- 8-byte records {group, index << 6 | rank}
 // (the owner-routed add, rsk_hll_add_grouped_routed) read instead of keys + ids.
-template <bool REC>
-__global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict__ keys,
+// P1 lanes, TILE records per tile: 256 x 8192 (two workgroups per CU) or
+// 512 x 16384 (route gpart_tile: one per CU, segments twice as long for the
+// fine-bin pass); 32 pairs per lane either way.
+template <uint32_t TILE>
+struct TmLds {
+  uint32_t hist[PT], lstart[PT];
+  uint32_t srt[TILE];
+};
+// Exclusive scan of the 256 bin counts held by lanes 0..255 of a workgroup of
+// any size >= 256 (every lane calls it; the others pass and get nothing useful).
+RSK_DEV uint32_t bins_excl_scan(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t ws[PT / 64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (w < PT / 64 && lane == 63) ws[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PT / 64; ++q) {
+    pre += q < w ? ws[q] : 0;
+    tot += ws[q];
+  }
+  *total = tot;
+  __syncthreads();
+  return pre + x - v;
+}
+
+template <bool REC, uint32_t P1, uint32_t TILE>
+__global__ __launch_bounds__(P1) void hll_gpart1t_kernel(const uint4* __restrict__ keys,
                                                          const uint32_t* __restrict__ groups,
                                                          const uint2* __restrict__ recs, uint64_t n, uint64_t per,
                                                          uint64_t G, uint32_t nbins, uint32_t tpb,
                                                          uint32_t* __restrict__ out, uint16_t* __restrict__ hdr) {
-  __shared__ SortLds<GP_TILE> L;
+  constexpr int E = TILE / P1;
+  static_assert(P1 >= PT && TILE % P1 == 0 && TILE <= 65535, "bins held by lanes 0..255; u16 starts");
+  __shared__ TmLds<TILE> L;
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
   const uint32_t HS = nbins + 1;
-  L.hist[threadIdx.x] = 0;
+  if (threadIdx.x < PT) L.hist[threadIdx.x] = 0;
   uint32_t j = 0;
-  for (uint64_t k0 = begin; k0 < end; k0 += GP_TILE, ++j) {
-    uint4 v[GP_E];
-    uint32_t g[GP_E];
+  for (uint64_t k0 = begin; k0 < end; k0 += TILE, ++j) {
+    uint4 v[E];
+    uint32_t g[E];
 #pragma unroll
-    for (int e = 0; e < GP_E; ++e) {
-      const uint64_t i = k0 + threadIdx.x + (uint64_t)e * PT;
+    for (int e = 0; e < E; ++e) {
+      const uint64_t i = k0 + threadIdx.x + (uint64_t)e * P1;
       const bool ok = i < end;
       if constexpr (REC) {
         const uint2 r = ok ? recs[i] : make_uint2(0xFFFFFFFFu, 0);
@@ -194,9 +228,9 @@ __global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict
       }
     }
     __syncthreads();  // the previous tile's image is written out, hist reset
-    uint32_t rec[GP_E], tag[GP_E];
+    uint32_t rec[E], tag[E];
 #pragma unroll
-    for (int e = 0; e < GP_E; ++e) {
+    for (int e = 0; e < E; ++e) {
       tag[e] = 0xFFFFFFFFu;
       if (g[e] < G) {
         uint32_t ir;
@@ -212,30 +246,30 @@ __global__ __launch_bounds__(PT) void hll_gpart1t_kernel(const uint4* __restrict
       }
     }
     __syncthreads();
-    const uint32_t cnt = L.hist[threadIdx.x];
+    const uint32_t cnt = threadIdx.x < PT ? L.hist[threadIdx.x] : 0u;
     uint32_t np;
-    const uint32_t ls = block_excl_scan256(cnt, &np);
-    L.lstart[threadIdx.x] = ls;
+    const uint32_t ls = bins_excl_scan(cnt, &np);
+    if (threadIdx.x < PT) L.lstart[threadIdx.x] = ls;
     const uint64_t t = (uint64_t)blockIdx.x * tpb + j;
     if (threadIdx.x < nbins) hdr[t * HS + threadIdx.x] = (uint16_t)ls;
     if (threadIdx.x == 0) hdr[t * HS + nbins] = (uint16_t)np;
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < GP_E; ++e)
+    for (int e = 0; e < E; ++e)
       if (tag[e] != 0xFFFFFFFFu) L.srt[L.lstart[tag[e] >> 16] + (tag[e] & 0xFFFFu)] = rec[e];
     __syncthreads();
-    uint32_t* o = out + t * GP_TILE;  // 16-byte aligned
+    uint32_t* o = out + t * TILE;  // 16-byte aligned
     const uint4* s4 = reinterpret_cast<const uint4*>(L.srt);
-    for (uint32_t q = threadIdx.x; q < (np + 3) / 4; q += PT) {  // the tail past np is never read
+    for (uint32_t q = threadIdx.x; q < (np + 3) / 4; q += P1) {  // the tail past np is never read
       const uint4 x = s4[q];
       u32x4 y = {x.x, x.y, x.z, x.w};
       __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(o) + q);
     }
-    L.hist[threadIdx.x] = 0;
+    if (threadIdx.x < PT) L.hist[threadIdx.x] = 0;
   }
   for (; j < tpb; ++j) {  // the block's unused tile slots: empty headers
     const uint64_t t = (uint64_t)blockIdx.x * tpb + j;
-    for (uint32_t c = threadIdx.x; c < HS; c += PT) hdr[t * HS + c] = 0;
+    for (uint32_t c = threadIdx.x; c < HS; c += P1) hdr[t * HS + c] = 0;
   }
 }
 
@@ -490,7 +524,7 @@ constexpr int TM_LU = 4;           // uint4 loads per lane in flight per chunk o
 constexpr int TM_LU2 = 2;          // (gpart2t)
 constexpr uint32_t TM_RT = 8192;   // records per gpart2t round
 constexpr uint32_t TM_W = 1024;    // tiles per gpart2t round window (one per lane)
-static_assert(TM_RT >= GP_TILE && TM_W == GQ_T, "a round holds any one tile's segment; one lane per window tile");
+static_assert(TM_W == GQ_T, "one lane per window tile");  // (a segment longer than a round is cut across rounds)
 
 // The segments i < ns of a window (LDS: first record index sa[i], length
 // sl[i], f's base sb[i]; sb may be null): f(x, sb[i] + r) for record r of
@@ -655,7 +689,8 @@ __global__ __launch_bounds__(GQ_T) void hll_gcount2t_kernel(const uint32_t* __re
                                                             const GPart* __restrict__ parts,
                                                             const uint32_t* __restrict__ d_nq,
                                                             uint32_t* __restrict__ cnt, const uint16_t* __restrict__ hdrT,
-                                                            const uint32_t* __restrict__ seglen, uint32_t NT) {
+                                                            const uint32_t* __restrict__ seglen, uint32_t NT,
+                                                            uint32_t tile) {
   constexpr int NH = 16;
   __shared__ uint32_t h[NH][PT + 1];
   __shared__ uint32_t sa[TM_W], sl[TM_W];
@@ -673,7 +708,7 @@ __global__ __launch_bounds__(GQ_T) void hll_gcount2t_kernel(const uint32_t* __re
     a = 0, l = 0;
     if (t < pt.hi) {
       l = sg[t];
-      a = t * GP_TILE + hs[t];
+      a = t * tile + hs[t];
     }
   };
   uint32_t a, l;
@@ -709,7 +744,8 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
                                                            const uint32_t* __restrict__ offf,
                                                            uint32_t* __restrict__ out, const uint16_t* __restrict__ hdrT,
                                                            const uint32_t* __restrict__ seglen,
-                                                           const uint32_t* __restrict__ goff, uint32_t NT) {
+                                                           const uint32_t* __restrict__ goff, uint32_t NT,
+                                                           uint32_t tile) {
   __shared__ uint32_t stage[TM_RT], img[TM_RT];
   __shared__ uint32_t sa[TM_W], sl[TM_W], sr[TM_W];
   __shared__ uint32_t hist[PT], dlt[PT], cur[PT], wsum[GQ_T / 64], wc[GQ_T / 64];
@@ -764,7 +800,7 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
     if (ntl == TM_W && s_e < vend) vend = s_e;
     if (in) {
       const uint32_t a0 = s0 > v ? s0 : v, e0 = e < vend ? e : vend;
-      sa[threadIdx.x] = (t + threadIdx.x) * GP_TILE + hv + (a0 - s0);
+      sa[threadIdx.x] = (t + threadIdx.x) * tile + hv + (a0 - s0);
       sl[threadIdx.x] = e0 > a0 ? e0 - a0 : 0u;
       sr[threadIdx.x] = a0 - v;
       if (threadIdx.x == ntl - 1) s_cut = e > vend ? 1u : 0u;  // only the last tile in can be cut
@@ -1262,8 +1298,12 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   // fine-bin pass parts: about four per CU over the whole chunk, at least 16 tiles each
   const uint32_t target = (uint32_t)std::max<uint64_t>(16ull * GQ_TILE, max_np / (4ull * cus) + 1);
   const bool tm = d_recs || c->tune.gpart_tm == 1;  // records: the tile-major form only
-  const uint64_t per_max = ((max_np + G1 - 1) / G1 + 3) & ~3ull;
-  const uint64_t nt_max = (uint64_t)G1 * ((per_max + GP_TILE - 1) / GP_TILE);
+  // tile-major first pass: 2 x 256-lane blocks per CU with 8192-record tiles, or
+  // (route gpart_tile) one 512-lane block per CU with 16384-record tiles
+  const bool big = tm && c->tune.gpart_tile == 1;
+  const uint32_t tile = big ? 16384u : GP_TILE, G1t = tm ? (big ? cus : G1) : G1;
+  const uint64_t per_max = ((max_np + G1t - 1) / G1t + 3) & ~3ull;
+  const uint64_t nt_max = (uint64_t)G1t * ((per_max + tile - 1) / tile);
   // TM parts: also at most TM_PT tiles each
   const uint32_t qmax = nbins1 + (uint32_t)(max_np / target) + 2 + (tm ? nbins1 * (uint32_t)((nt_max + TM_PT - 1) / TM_PT) : 0u);
   const uint64_t ncnt1 = (uint64_t)nbins1 * G1 + 1, ncnt2 = (uint64_t)qmax * PT + 1;
@@ -1279,7 +1319,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   // tile-major first pass: NT tiles of GP_TILE record slots, a u16 header per tile and bin (and
   // its transpose), the per-bin segment prefix
   const uint32_t HS = nbins1 + 1;
-  const uint64_t bufa = tm ? al(4 * nt_max * GP_TILE) : al(4 * max_np);
+  const uint64_t bufa = tm ? al(4 * nt_max * tile) : al(4 * max_np);
   size_t sb3 = 0;
   if (tm)
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb3, (uint32_t*)nullptr, (uint32_t*)nullptr,
@@ -1315,21 +1355,26 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
   uint32_t* buf_b = reinterpret_cast<uint32_t*>(w + meta + tm_bytes + bufa);
   for (uint64_t first = 0; first < keys.n; first += chunk) {
     const uint64_t m = std::min<uint64_t>(chunk, keys.n - first);
-    const uint64_t per = ((m + G1 - 1) / G1 + 3) & ~3ull;  // a multiple of 4: uint4 id loads in hll_gcount
+    const uint64_t per = ((m + G1t - 1) / G1t + 3) & ~3ull;  // a multiple of 4: uint4 id loads in hll_gcount
     const uint4* kd = d_recs ? nullptr : reinterpret_cast<const uint4*>(keys.data) + first;
     const uint32_t* gd = d_recs ? nullptr : d_groups + first;
     const uint2* rd = d_recs ? d_recs + first : nullptr;
-    const uint32_t tpb = (uint32_t)((per + GP_TILE - 1) / GP_TILE), NT = G1 * tpb;
+    const uint32_t tpb = (uint32_t)((per + tile - 1) / tile), NT = G1t * tpb;
     if (c->tune.gpart_poison) RSK_HIP(hipMemsetAsync(buf_b, 0xFF, 4 * max_np, c->stream));
     if (tm) {
       {
         ProfScope ps(c, "hll_gpart1");
-        if (rd)
-          hipLaunchKernelGGL(hll_gpart1t_kernel<true>, dim3(G1), dim3(PT), 0, c->stream, kd, gd, rd, m, per, G, nbins1,
-                             tpb, buf_a, hdr);
-        else
-          hipLaunchKernelGGL(hll_gpart1t_kernel<false>, dim3(G1), dim3(PT), 0, c->stream, kd, gd, rd, m, per, G, nbins1,
-                             tpb, buf_a, hdr);
+#define RSK_GP1T(R, P1, TL)                                                                                    \
+  hipLaunchKernelGGL((hll_gpart1t_kernel<R, P1, TL>), dim3(G1t), dim3(P1), 0, c->stream, kd, gd, rd, m, per, G,      \
+                     nbins1, tpb, buf_a, hdr)
+        if (big) {
+          if (rd) RSK_GP1T(true, 512, 16384);
+          else RSK_GP1T(false, 512, 16384);
+        } else {
+          if (rd) RSK_GP1T(true, PT, GP_TILE);
+          else RSK_GP1T(false, PT, GP_TILE);
+        }
+#undef RSK_GP1T
         RSK_CHECK_LAUNCH("hll_gpart1t");
       }
       {
@@ -1347,14 +1392,14 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
                            target, qmax, parts, d_nq);
         RSK_CHECK_LAUNCH("hll_gparts_tm");
         hipLaunchKernelGGL(hll_gcount2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, cnt2, hdrT,
-                           seglen, NT);
+                           seglen, NT, tile);
         RSK_CHECK_LAUNCH("hll_gcount2t");
         RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, offf, (int)ncnt2, c->stream));
         hipLaunchKernelGGL(hll_gfine_kernel, dim3(nfine / 256 + 1), dim3(256), 0, c->stream, offf, parts, d_nq, nbins1,
                            off2);
         RSK_CHECK_LAUNCH("hll_gfine");
         hipLaunchKernelGGL(hll_gpart2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b,
-                           hdrT, seglen, segoff, NT);
+                           hdrT, seglen, segoff, NT, tile);
         RSK_CHECK_LAUNCH("hll_gpart2t");
       }
     } else {

@@ -64,6 +64,7 @@ struct Tuning {
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
   int gpart_poison = 0;      // timing-free check: fill the fine-bin output with 0xFF first (a hole then shows)
   int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no
+  int gpart_tile = 0;        // its tile-major first pass: 0 8192-record tiles (2 x 256 lanes per CU), 1 16384 (512 lanes)
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the
@@ -94,6 +95,7 @@ struct AsyncOp {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool on_xfer = false;
   uint64_t seq = 0;         // submission number: callbacks run in this order
+  bool failed = false;      // failed by the completion watchdog (its host function may still fire)
 };
 
 struct ProfEntry {
@@ -255,6 +257,11 @@ struct rsk_bloom {
   uint64_t nwords = 0;         // u32 words allocated (>= nbytes/4)
   uint32_t* d_bits = nullptr;  // MSB-first bytes, addressed as LE u32 words
   rsk::FastMod63 fm{};
+  // for the RBitSet views of the filter (rsk_bloom_bitset): wgen counts the
+  // calls that may have set bits (a view rescans its STRLEN only when it
+  // changed), rgen the calls that replaced the whole string (SET: STRLEN =
+  // set_len from then on, whatever a view had fixed before)
+  uint64_t wgen = 1, rgen = 1, set_len = 0;
 };
 
 namespace rsk {

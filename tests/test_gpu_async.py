@@ -385,3 +385,68 @@ def test_async_reads_back_state_at_call_time(engine):
     finally:
         ref.close()
         got.close()
+
+
+def _noncanonical(canon: bytes) -> bytes:
+    """The same registers as a canonical sparse string, re-encoded with its first
+    long zero run (XZERO of 130+) cut into XZERO + ZERO 64: two zero opcodes in
+    a row, which the canonical encoder never writes."""
+    body, out, i = canon[16:], bytearray(), 0
+    done = False
+    while i < len(body):
+        b = body[i]
+        if (b & 0xC0) == 0x40:
+            run = (((b & 0x3F) << 8) | body[i + 1]) + 1
+            if not done and run >= 130:
+                r = run - 64
+                out += bytes([0x40 | ((r - 1) >> 8), (r - 1) & 0xFF, 63])
+                done = True
+            else:
+                out += body[i:i + 2]
+            i += 2
+        else:
+            out.append(b)
+            i += 1
+    assert done
+    return canon[:16] + bytes(out)
+
+
+def test_async_add_keeps_set_string_when_nothing_changes(L, engine, orc):
+    """a PFADD that changes no register leaves a kept SET string in
+    place -- rsk_hll_add, rsk_hll_add_async and rsk_hll_add_each (host replies)
+    alike; one that changes a register re-encodes it (async too)."""
+    from redisson_amd import KeyBatch, _lib
+
+    keys = orc.gen_keys16(0x5EED0002, 0, 40)
+    regs = np.zeros(16384, np.uint8)
+    orc.hll_add(regs, keys, None, 16, 40)
+    s = _noncanonical(orc.hll_encode_sparse(regs))
+    h = _pool(L, engine)
+    ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+    buf = (ctypes.c_uint8 * 12304)()
+    n = ctypes.c_size_t()
+
+    def get():
+        _lib.check(L.rsk_hll_export_redis(h, 0, buf, 12304, ctypes.byref(n)))
+        return bytes(buf[: n.value])
+
+    b = (ctypes.c_uint8 * len(s)).from_buffer_copy(s)
+    _lib.check(L.rsk_hll_import_redis(h, 0, b, len(s)))
+    assert get() == s
+    op = _lib.NativeOp(ks)
+    op.issued(L.rsk_hll_add_async(h, 0, ctypes.byref(ks), op.fn, None))
+    assert op.wait(30) == 0 and get() == s  # nothing changed: still the SET bytes
+    ch = ctypes.c_uint8()
+    _lib.check(L.rsk_hll_add(h, 0, ctypes.byref(ks), ctypes.byref(ch)))
+    assert ch.value == 0 and get() == s
+    out = np.zeros(40, np.uint8)
+    _lib.check(L.rsk_hll_add_each(h, 0, ctypes.byref(ks), out.ctypes.data))
+    assert not out.any() and get() == s
+    more = orc.gen_keys16(0x5EED0002, 1000, 50)
+    km = KeyBatch.from_numpy(more.reshape(-1, 16)).as_struct()
+    op = _lib.NativeOp(km)
+    op.issued(L.rsk_hll_add_async(h, 0, ctypes.byref(km), op.fn, None))
+    assert op.wait(30) == 1
+    orc.hll_add(regs, more, None, 16, 50)
+    assert get()[16:] == orc.hll_encode_sparse(regs)[16:]  # re-encoded canonically
+    L.rsk_hll_destroy(h)

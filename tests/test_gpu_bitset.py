@@ -1,6 +1,7 @@
 """RBitSet on the GPU: the reference's JUnit tests (T/RedissonBitSetTest.java)
 replayed through the mirror, plus batched SETBIT/GETBIT/BITOP/BITCOUNT parity
 against the oracle's Redis model."""
+import ctypes
 import numpy as np
 import pytest
 
@@ -278,3 +279,57 @@ def test_getBitSet_of_bloom_filter_is_its_bit_string(client, orc):
 
     with pytest.raises(_lib.IllegalArgumentException):
         bs.set((size + 7) // 8 * 8 + 100)
+
+
+def test_bloom_view_rescans_only_after_writes(engine, orc):
+    """the RBitSet view of a Bloom filter recomputes STRLEN (a scan of
+    the whole filter) only when the filter was written since it last looked --
+    GETBIT / GET / STRLEN repeated cost no scan -- and SET of the filter's
+    string (rsk_bloom_import_bits) gives STRLEN = the SET length, trailing
+    zero bytes included (Redis SET semantics), not a length left over from
+    earlier writes through the view."""
+    from redisson_amd import KeyBatch, _lib
+
+    L = _lib.load()
+    b = ctypes.c_void_p()
+    _lib.check(L.rsk_bloom_create(engine.ctx, 1_000_003, 5, ctypes.byref(b)))
+    v = ctypes.c_void_p()
+    _lib.check(L.rsk_bloom_bitset(b, ctypes.byref(v)))
+
+    def strlen():
+        n = ctypes.c_uint64()
+        _lib.check(L.rsk_bitset_strlen(v, ctypes.byref(n)))
+        return n.value
+
+    def scans():
+        return engine.prof_read("bitset_length")[1]
+
+    keys = orc.gen_keys16(0x5EED0003, 0, 2000)
+    ks = KeyBatch.from_numpy(keys.reshape(-1, 16)).as_struct()
+    engine.prof_enable(True)
+    engine.prof_reset()
+    try:
+        _lib.check(L.rsk_bloom_add(b, ctypes.byref(ks), None))
+        n0 = strlen()
+        assert n0 > 0 and scans() == 1
+        offs = np.arange(0, 1_000_000, 997, dtype=np.uint64)
+        out = np.zeros(offs.size, np.uint8)
+        for _ in range(5):
+            _lib.check(L.rsk_bitset_getbits(v, offs.ctypes.data, offs.size, _lib.RSK_MEM_HOST, out.ctypes.data))
+            assert strlen() == n0
+        assert scans() == 1  # reads never rescan
+        more = orc.gen_keys16(0x5EED0003, 2000, 2000)
+        km = KeyBatch.from_numpy(more.reshape(-1, 16)).as_struct()
+        _lib.check(L.rsk_bloom_add(b, ctypes.byref(km), None))
+        assert strlen() >= n0 and scans() == 2  # one rescan after the write
+        set_off = np.array([999_000], np.uint64)
+        _lib.check(L.rsk_bitset_setbits(v, set_off.ctypes.data, 1, 1, _lib.RSK_MEM_HOST))
+        assert strlen() == 999_000 // 8 + 1 and scans() == 2  # the view's own write keeps its length
+        s = bytes([0x80]) + bytes(99)  # SET of 100 bytes: bit 0 and 99 zero bytes
+        buf = (ctypes.c_uint8 * len(s)).from_buffer_copy(s)
+        _lib.check(L.rsk_bloom_import_bits(b, buf, len(s)))
+        assert strlen() == 100
+    finally:
+        engine.prof_enable(False)
+        L.rsk_bitset_destroy(v)
+        L.rsk_bloom_destroy(b)

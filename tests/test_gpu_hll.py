@@ -297,7 +297,7 @@ def test_grouped_partitioned_matches_direct_and_oracle(L, engine, orc, route, G,
         L.rsk_hll_destroy(h)
 
 
-@pytest.mark.parametrize("tm", [0, 1])
+@pytest.mark.parametrize("tm", [0, 1, 2])  # 2: tile-major with 16384-record tiles (route gpart_tile)
 @pytest.mark.parametrize("G,n,zipf", [(4096 * 10 + 16, 50_000_000, 0.0), (1_000_000, 60_000_000, 0.0),
                                       (200_000, 40_000_000, 1.1)])
 def test_grouped_partitioned_leaves_no_holes(L, engine, route, G, n, zipf, tm):
@@ -315,7 +315,7 @@ def test_grouped_partitioned_leaves_no_holes(L, engine, route, G, n, zipf, tm):
     ks = k.keys_fixed(n, 16).as_struct()
     pools = {}
     for mode in ("1", "0"):
-        route(gpart=1 if mode == "1" else -1, gpart_tm=tm, gpart_poison=1)
+        route(gpart=1 if mode == "1" else -1, gpart_tm=min(tm, 1), gpart_tile=int(tm == 2), gpart_poison=1)
         h = _pool(L, engine, G)
         _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
         pools[mode] = h
@@ -508,7 +508,7 @@ def _c5_stratified_sample(G: int, per_bin: int = 34, seed: int = 11) -> np.ndarr
     return np.unique(np.array(ids, np.uint64))
 
 
-@pytest.mark.parametrize("tm", [1, 0])
+@pytest.mark.parametrize("tm", [1, 0, 2])  # 2: tile-major with 16384-record tiles (route gpart_tile)
 def test_c5_full_size_group_sample_bit_exact(L, engine, orc, route, tm):
     """BASELINE configs[4] at its per-GPU size: 1M sketches, 500M (group, key)
     pairs through the grouped PFADD.  A stratified sample of >= 8192 sketches --
@@ -518,7 +518,7 @@ def test_c5_full_size_group_sample_bit_exact(L, engine, orc, route, tm):
     on them."""
     from redisson_amd import _lib, devmem
 
-    route(gpart_tm=tm, gpart_poison=1)  # a fine-bin slot left unwritten would raise a register to 63
+    route(gpart_tm=min(tm, 1), gpart_tile=int(tm == 2), gpart_poison=1)  # an unwritten fine-bin slot would raise a register to 63
     G, n = 1_000_000, 500_000_000
     sample = _c5_stratified_sample(G)
     gs = sample.size
