@@ -67,6 +67,12 @@ def load_calib():
         if os.path.exists(p):
             for k, v in json.load(open(p)).get("patterns", {}).items():
                 cal[k] = v["bytes_over_fetch_bytes"]
+    # random 4-byte gathers: FETCH_SIZE counts 64 B per gather (profiles/r04_gather_fetch_calib.json,
+    # 63.98 B raw per gather); the line fetched is taken as those 64 B (factor 1)
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                     "r04_gather_fetch_calib.json")
+    if os.path.exists(p):
+        cal["gather_64B"] = 1.0
     cal.update(json.loads(os.environ.get("FETCH_CALIB", "{}")))
     return cal
 
@@ -84,7 +90,14 @@ READS = {
     "hll_gcount2p_kernel": "stream_read",                  # uint4 run loads
     "hll_gpart2p_kernel": "stream_read",
     "hll_gapply_kernel": "stream_read",                    # uint4 loads of each fine bin's contiguous run
-    "hll_gapply_extra_kernel": "stream4_read",             # 4 B/lane loads of a hot bin's extra chunks
+    "hll_gapply_extra_kernel": "stream_read",              # uint4 loads of a hot bin's extra chunks (round 5)
+    # the Bloom add() with replies (rsk_bloom_reply.hip): rp1 = bloom_sa1 (16 B/lane keys), rp2 =
+    # bloom_sa2h (uint4 sub-region reads), rp_tapply (uint4 segment loads), rp_treply (16 B/lane
+    # keys + ~1.34 random 2-byte gathers of T per key, 64 B of FETCH each: gather_64B, r04 calibration)
+    "bloom_sa1_kernel": "stream_read",
+    "bloom_sa2h_kernel": "stream_read",
+    "rp_tapply_kernel": "segment_256B",
+    "rp_treply_kernel": [("stream_read", 0.16), ("gather_64B", 0.84)],
 }
 
 
@@ -160,6 +173,20 @@ def main():
             "hbm_bytes_note": "per call: every stage's FETCH_SIZE corrected by the calibrated factor of its read "
                               "pattern (scripts/fetch_calib.py) + WRITE_SIZE (exact for 16 B stores; raw for the "
                               "fine-bin pass's 4 B scattered stores)"}
+    # add() with replies as one unit (a reply_profile.py run: one call per dispatch of each stage)
+    rp = ("bloom_sa1_kernel", "sah_size_kernel", "st_offsets_kernel", "bloom_sa2h_kernel", "rp_tapply_kernel",
+          "rp_treply_kernel")
+    if "rp_treply_kernel" in kern and all(x in fe and x in wr for x in rp if x.startswith(("bloom_", "rp_"))):
+        kern["bloom_add_replies"] = {
+            "keys_per_launch": keys,
+            "hbm_bytes_per_launch": sum(kern[x].get("fetch_bytes_corrected", 0.0) + wr.get(x, 0.0) * 1024
+                                        for x in rp if x in kern),
+            "hbm_bytes_raw": sum((fe.get(x, 0.0) + wr.get(x, 0.0)) * 1024 for x in rp),
+            "stages": {x: {"fetch_bytes_corrected": kern[x].get("fetch_bytes_corrected"),
+                           "write_bytes": wr.get(x, 0.0) * 1024, "fetch_correction": kern[x].get("fetch_correction"),
+                           "avg_ns": kern[x].get("avg_ns")} for x in rp if x in kern},
+            "hbm_bytes_note": "per add() call: FETCH_SIZE of each stage corrected by its read pattern's calibration "
+                              "(rp_treply: keys x2, T gathers at 64 B each) + WRITE_SIZE"}
     # The Bloom insert at 1B keys, k = 7 (one chunk: one dispatch of each stage per insert call),
     # per stage and summed.  Append pipeline (default): sa1 reads the keys, sa2 its sub-regions and
     # apply its tiles with 16 B/lane loads, so FETCH is doubled per the guide; the header pipeline
