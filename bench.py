@@ -278,6 +278,12 @@ def bloom_bench(engine, n_ins: int, n_q: int, reps: int, rank: int = 0, world: i
                    "note": "rsk_bloom_add with added_out (sequential SETBIT-reply semantics), fresh filter, "
                            "partitioned group-tag pipeline (rsk_bloom_reply.hip); model excludes the reply "
                            "pass's random gathers"}
+        tr = pmc_traffic("bloom_add_replies", {"workload": "bloom_add_replies", "keys": n_ins, "zipf": 0.0,
+                                               "bloom_keys": n_ins})
+        if tr:  # the same pipeline alone under rocprofv3 (scripts/reply_profile.py)
+            replies["traffic"] = tr["bytes"]
+            replies["traffic_source"] = tr["source"]
+            replies["traffic_GBps"] = tr["bytes"] / dt / 1e9
         rout.free()
     for buf in (ins, qs, out):
         buf.free()

@@ -252,6 +252,25 @@ void hll_var_variant_launch(rsk_ctx* c, int variant, const uint8_t* data, const 
                            n, rpb, c->d_slab);
       break;
     }
+    case 11:  // form 2 with a 20 KiB stage, 4 workgroups per CU (<= 64 VGPRs, <= 40 KiB of LDS)
+    case 12: {  // the same without MurmurHash64A (its stream floor at that occupancy)
+      uint64_t b4, pb4;
+      var_grid(c, n, &b4, &pb4, 4);
+      if (variant == 11)
+        hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 0, 2, 20480, 4>), dim3((uint32_t)b4), dim3(VAR_TILE), 0,
+                           c->stream, data, offsets, n, pb4, c->d_slab);
+      else
+        hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 1, 2, 20480, 4>), dim3((uint32_t)b4), dim3(VAR_TILE), 0,
+                           c->stream, data, offsets, n, pb4, c->d_slab);
+      break;
+    }
+    case 13: {  // form 2 with a 20 KiB stage at the production 3 workgroups per CU
+      uint64_t b3, pb3;
+      var_grid(c, n, &b3, &pb3, 3);
+      hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 0, 2, 20480, 3>), dim3((uint32_t)b3), dim3(VAR_TILE), 0,
+                         c->stream, data, offsets, n, pb3, c->d_slab);
+      break;
+    }
     case 7:  // the round-3 form (ceil(len/8) classes, branch on the last step, 64-bit rank, long update)
       hipLaunchKernelGGL((hll_add_var_staged_kernel<1, 0, 0>), g, dim3(VAR_TILE), 0, c->stream, data, offsets, n,
                          per_block, c->d_slab); break;

@@ -241,6 +241,59 @@ void ensure_pinned(rsk_ctx* c) {
   }
 }
 
+// Bulk copies between device memory and a pageable host buffer through the
+// two pinned stages: host threads copy one stage while the DMA of the other
+// runs (the export / import of a pool's Redis strings: GBs at a time).
+void d2h_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+  ensure_pinned(c);
+  if (c->pin_off) {
+    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    return;
+  }
+  const uint64_t S = c->stage_bytes;
+  int prev = -1;
+  uint64_t prev_off = 0, prev_n = 0;
+  for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
+    const int slot = (int)(k & 1);  // its previous contents were copied out in the last round
+    const uint64_t n = std::min<uint64_t>(S, bytes - o);
+    RSK_HIP(hipMemcpyAsync(c->h_pin[slot], src + o, n, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipEventRecord(c->pin_ev[slot], c->stream));
+    if (prev >= 0) {
+      RSK_HIP(hipEventSynchronize(c->pin_ev[prev]));
+      par_copy(dst + prev_off, c->h_pin[prev], prev_n, c->stage_threads);
+    }
+    prev = slot;
+    prev_off = o;
+    prev_n = n;
+  }
+  if (prev >= 0) {
+    RSK_HIP(hipEventSynchronize(c->pin_ev[prev]));
+    par_copy(dst + prev_off, c->h_pin[prev], prev_n, c->stage_threads);
+  }
+  RSK_HIP(hipStreamSynchronize(c->stream));
+}
+// The other way; returns with the copies queued on the stream (ordered
+// before the caller's next launch).
+void h2d_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+  ensure_pinned(c);
+  if (c->pin_off) {
+    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return;
+  }
+  const uint64_t S = c->stage_bytes;
+  bool used[2] = {false, false};
+  for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
+    const int slot = (int)(k & 1);
+    const uint64_t n = std::min<uint64_t>(S, bytes - o);
+    if (used[slot]) RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));  // the DMA that last read it is done
+    par_copy(c->h_pin[slot], src + o, n, c->stage_threads);
+    RSK_HIP(hipMemcpyAsync(dst + o, c->h_pin[slot], n, hipMemcpyHostToDevice, c->stream));
+    RSK_HIP(hipEventRecord(c->pin_ev[slot], c->stream));
+    used[slot] = true;
+  }
+}
+
 // Calls fn(dev_keys, first_index, count) over the batch; host batches are
 // copied through the staging buffers in whole-key chunks.  On return every
 // chunk's work has completed.
@@ -1382,8 +1435,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
         RSK_HIP(hipMemcpyAsync(d_pos + d0, pos.data() + d0, 8 * (d1 - d0), hipMemcpyHostToDevice, c->stream));
         hll_export_launch(c, h->d_regs, h->d_card, d_ids + d0, nullptr, (uint32_t)(d1 - d0), d_len + d0, d_pos + d0,
                           d_stage);
-        RSK_HIP(hipMemcpyAsync(out + base, d_stage, end - base, hipMemcpyDeviceToHost, c->stream));
-        RSK_HIP(hipStreamSynchronize(c->stream));  // the stage is reused by the next chunk
+        d2h_staged(c, out + base, d_stage, end - base);  // (returns synchronised: the stage is reused next)
         d0 = d1;
       }
       // promoted for good (hllSparseSet -> hllSparseToDense), as the per-key GET
@@ -1452,7 +1504,7 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     RSK_HIP(hipMemcpyAsync(d_ids, ids, 8 * n, hipMemcpyHostToDevice, c->stream));
     RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, c->stream));
     RSK_HIP(hipMemcpyAsync(d_apply, apply.data(), n, hipMemcpyHostToDevice, c->stream));
-    RSK_HIP(hipMemcpyAsync(d_data, data + base, total, hipMemcpyHostToDevice, c->stream));
+    h2d_staged(c, d_data, data + base, total);
     RSK_HIP(hipMemsetAsync(d_err, 0xFF, 8, c->stream));
     RSK_HIP(hipMemsetAsync(d_canon, 1, n, c->stream));
     hll_import_launch(c, d_data, d_off, d_ids, nullptr, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);

@@ -269,15 +269,18 @@ RSK_DEV uint64_t var_hash(bool staged, const uint64_t* st, uint32_t off, const u
 // F (form): 2 = production (full-block classes, select tail, h0 table,
 // short register update, dword-aligned LDS reads); 1 = the same with 8-byte
 // reads at byte offsets; 0 = the round-3 form (support library A/B only).
-template <int KPL, int DIAG = 0, int F = 2>
-__global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_add_var_staged_kernel(
+// STAGE: stage bytes per tile; OCC: workgroups per CU the launch bounds ask
+// for (3 with the 32 KiB stage; 4 fit with 20 KiB -- 512 C4 keys span
+// 18.4 KiB +- 0.4 -- and 64 VGPRs).
+template <int KPL, int DIAG = 0, int F = 2, int STAGE = VAR_STAGE, int OCC = 3>
+__global__ __launch_bounds__(VAR_TILE / KPL, OCC * VAR_TILE / KPL / 256) void hll_add_var_staged_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint64_t n, uint64_t per_block,
     uint8_t* __restrict__ slabs) {
   constexpr int T = VAR_TILE / KPL;
-  constexpr int PF = VAR_STAGE / 16 / T;  // 16-byte stage chunks per lane
+  constexpr int PF = (STAGE / 16 + T - 1) / T;  // 16-byte stage chunks per lane
   constexpr bool FULL = F >= 1 && KPL == 1;  // F 1: unaligned 8-byte reads; F 2: aligned dwords
   __shared__ __attribute__((aligned(16))) uint32_t regs32[HLL_REGS / 4];
-  __shared__ __attribute__((aligned(16))) uint64_t stage[VAR_STAGE / 8 + 4];
+  __shared__ __attribute__((aligned(16))) uint64_t stage[STAGE / 8 + 4];
   __shared__ uint32_t perm[VAR_TILE];  // sorted keys: stage offset | len << 16
   __shared__ uint32_t cnt[VAR_NCLS_PAD], cbase[VAR_NCLS_PAD];
   __shared__ uint64_t h0tab[FULL ? 65 : 1];  // HLL_SEED ^ len * m, len <= 64
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(VAR_TILE / KPL, 3 * VAR_TILE / KPL / 256) void hll_
     last = b + VAR_TILE < end ? b + VAR_TILE : end;
     a0 = (dbase + lo) & ~uintptr_t(15);
     const uint64_t span = dbase + hi - a0;
-    staged = span <= (uint64_t)VAR_STAGE;
+    staged = span <= (uint64_t)STAGE;
     nchunk = staged ? (uint32_t)((span + 15) >> 4) : 0;
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -628,9 +631,9 @@ __global__ __launch_bounds__(VAR_TILE, 2) void hll_add_var_ring_kernel(const uin
   lds8_to_slab(regs32, slabs + (uint64_t)blockIdx.x * HLL_REGS);
 }
 
-inline void var_grid(rsk_ctx* c, uint64_t n, uint64_t* blocks, uint64_t* per_block) {
-  // LDS-staged tiles: ~50 KiB of LDS per workgroup -> 3 workgroups per CU.
-  uint64_t b = std::min<uint64_t>((n + VAR_TILE - 1) / VAR_TILE, std::min<uint64_t>(3ull * c->num_cus, c->slab_count));
+inline void var_grid(rsk_ctx* c, uint64_t n, uint64_t* blocks, uint64_t* per_block, uint32_t occ = 3) {
+  // LDS-staged tiles: ~50 KiB of LDS per workgroup -> 3 workgroups per CU (occ).
+  uint64_t b = std::min<uint64_t>((n + VAR_TILE - 1) / VAR_TILE, std::min<uint64_t>(occ * (uint64_t)c->num_cus, c->slab_count));
   if (b == 0) b = 1;
   uint64_t pb = (n + b - 1) / b;
   pb = (pb + VAR_TILE - 1) / VAR_TILE * VAR_TILE;

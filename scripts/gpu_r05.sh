@@ -77,6 +77,8 @@ for p in ${PART//,/ }; do
         rm -rf gpurun_out/gtrace_$z
         step gtrace_$z 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gtrace_$z -o run -- python3 scripts/gpart_profile.py 5 $z || exit 1
       done ;;
+    c4var)  # C4 kernel variants interleaved (VARIANTS=..., scripts/var_variants.py)
+      step c4var 300 python3 scripts/var_variants.py gpurun_out/c4var.json || exit 1 ;;
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;

@@ -17,7 +17,8 @@ from redisson_amd import _lib, devmem  # noqa: E402
 
 NAMES = {0: "production_form2", 1: "sorted_2_per_lane", 2: "round1_simple", 3: "sorted_4_per_lane",
          4: "diag_trivial_hash", 5: "diag_no_update", 6: "diag_trivial_hash_no_update", 7: "round3_form",
-         8: "ring_lds_dma", 9: "diag_ring_trivial_hash", 10: "staged_form1_unaligned_lds"}
+         8: "ring_lds_dma", 9: "diag_ring_trivial_hash", 10: "staged_form1_unaligned_lds",
+         11: "form2_stage20k_4wg", 12: "diag_stage20k_4wg_trivial_hash", 13: "form2_stage20k_3wg"}
 if os.environ.get("VARIANTS"):
     NAMES = {int(v): NAMES[int(v)] for v in os.environ["VARIANTS"].split(",")}
 
