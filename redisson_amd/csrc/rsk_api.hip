@@ -1372,9 +1372,13 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     // keys the device encodes (present, not a kept SET string), in call order
     std::vector<uint64_t> dev_i, dev_id;
     std::vector<uint8_t> want;
+    dev_i.reserve(n);
+    dev_id.reserve(n);
+    want.reserve(n);
+    const bool any_imp = !h->imported.empty();
     for (uint64_t i = 0; i < n; ++i) {
       const uint64_t id = ids[i];
-      if (!h->exists[id] || h->imported.count(id)) continue;
+      if (!h->exists[id] || (any_imp && h->imported.count(id))) continue;
       dev_i.push_back(i);
       dev_id.push_back(id);
       want.push_back(h->dense[id] ? 0 : 1);
@@ -1475,18 +1479,15 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
         fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value. (string " + std::to_string(i) + ")");
       need(len <= (1ull << 31), "string too long");
     }
-    // SETs of one key in one call: the last wins
-    std::vector<uint8_t> apply(n, 1);
+    // SETs of one key in one call: the last wins (a pass from the end marks each id once)
+    std::vector<uint8_t> apply(n, 0);
     {
-      std::unordered_map<uint64_t, uint64_t> last;
-      last.reserve(n);
-      for (uint64_t i = 0; i < n; ++i) {
-        auto r = last.emplace(ids[i], i);
-        if (!r.second) {
-          apply[r.first->second] = 0;
-          r.first->second = i;
+      std::vector<uint8_t> seen(h->n, 0);
+      for (uint64_t i = n; i-- > 0;)
+        if (!seen[ids[i]]) {
+          seen[ids[i]] = 1;
+          apply[i] = 1;
         }
-      }
     }
     rsk_ctx* c = h->ctx;
     CtxLock l(c);

@@ -79,6 +79,8 @@ for p in ${PART//,/ }; do
       done ;;
     c4var)  # C4 kernel variants interleaved (VARIANTS=..., scripts/var_variants.py)
       step c4var 300 python3 scripts/var_variants.py gpurun_out/c4var.json || exit 1 ;;
+    io)  # batched Redis export / import of the C5 pool alone
+      step io 200 python3 scripts/io_profile.py 3 || exit 1 ;;
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;

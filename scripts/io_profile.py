@@ -1,0 +1,53 @@
+"""Batched Redis export / import of the C5 pool (1M sketches after 500M
+grouped pairs) alone in a process: wall time of each call and the device time
+of its kernels (rsk_hll_export_redis_batch / rsk_hll_import_redis_batch).
+
+  python scripts/io_profile.py [reps]   -> one JSON line"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from redisson_amd import _lib, devmem  # noqa: E402
+from redisson_amd.hyperloglog import GroupedHyperLogLog  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    _lib.load()
+    _lib.diag()
+    eng = _lib.Engine(0)
+    G, n = 1_000_000, 500_000_000
+    g, k = devmem.gen_grouped(eng, 0x5EED0006, G, 0, n)
+    pool = GroupedHyperLogLog(eng, G)
+    pool.add(k.keys_fixed(n, 16), g)
+    g.free()
+    k.free()
+    ids = np.arange(G, dtype=np.uint64)
+    data, offs = pool.exportRedis(ids)
+    fresh = GroupedHyperLogLog(eng, G)
+    fresh.importRedis(ids, data, offs)
+    eng.prof_reset()
+    eng.prof_enable(True)
+    te, ti = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        pool.exportRedis(ids, out=data)
+        te.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        fresh.importRedis(ids, data, offs)
+        ti.append(time.perf_counter() - t0)
+    eng.prof_enable(False)
+    dev = {s: eng.prof_read(s)[0] / reps for s in ("hll_export_len", "hll_export_write", "hll_import_check",
+                                                    "hll_import_write")}
+    print(json.dumps({"sketches": G, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
+                      "device_ms": dev}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
