@@ -29,6 +29,10 @@ const char *rsk_diag_last_error(void);
  *   sa_v          the insert's sa2h tile: uint4 loads per lane, 0 (= 3), 6 or 8
  *   sa_dbg        TIMING ONLY (wrong filter): the insert's sa1 stores each tile's image
  *                 contiguously and the insert stops after sa1
+ *   sa_full       -1: the insert's sa1 and the replies' rp1 without their branch-free path for
+ *                 full super-tiles at k = 7
+ *   sa_hash       TIMING ONLY (wrong filter): the insert's sa1 at k = 7 with the key words as
+ *                 its hashes (1), also without the two mods (2)
  *   sa_parts      sa2 / rp2 parts per coarse bin (0 = default)
  *   reply         add() replies: 0 auto, 1 group-tag pipeline at any size, -1 sort path
  *   reply_chunk   probes per chunk of the group-tag pipeline (0 = default)
@@ -43,7 +47,7 @@ const char *rsk_diag_last_error(void);
  *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
  *                 leaves unwritten then corrupts a register: the tests' hole check)
  *   reset         every route back to automatic
- * Every route but sa_dbg and reply_dbg gives bit-identical results; they differ in speed only. */
+ * Every route but sa_dbg, sa_hash and reply_dbg gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
 
 /* add()-with-replies counters of a context since it was created: key groups

@@ -5,6 +5,8 @@
 // namespace: each translation unit instantiates its own kernels.  See
 // rsk_bloom_st.hip for the pipeline.
 #pragma once
+#include <type_traits>
+
 #include "rsk_internal.h"
 
 namespace rsk {
@@ -168,7 +170,9 @@ constexpr uint32_t SA2_SLOTS = SA2_T * SA2_V * 4;  // records per sa2h tile
 // gridDim.x-th one, and each record carries in its top 6 bits the key group
 // g = (super-tile - w S) / gs of its key (offsets are < 2^26): along any
 // sub-region (w, c) g never decreases, so key order is known per group.
-template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX, bool TAGGED = false, int KC = 0>
+// HX (timing only, diag route sa_hash): 1 = the key words as h1 / h2 (no
+// hashes), 2 = also no mods (idx_0 = h1 mod 2^32) -- wrong filters.
+template <bool FIXED16, int KMAX, int T1, class R, int KPL = 16 / KMAX, bool TAGGED = false, int KC = 0, int HX = 0>
 __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void bloom_sa1_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets, uint32_t fixed_len, uint64_t n,
     FastMod63 fm, int k, uint32_t shift1, uint32_t nb1, uint64_t nst, R* __restrict__ region, uint32_t quota,
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
   uint64_t wst = 0;  // dbg: the super-tile being written out
   auto write_out = [&](uint32_t total4) {
     const uint4* img4 = reinterpret_cast<const uint4*>(img);
-    if (dbg) {  // TIMING ONLY (the host stops after this pass): each tile's image stored contiguously
+    if (dbg & 1) {  // TIMING ONLY (the host stops after this pass): each tile's image stored contiguously
       u32x4* o4 = reinterpret_cast<u32x4*>(region + wst * IMG);
       for (uint32_t g = threadIdx.x; g < total4; g += T1) {
         const uint4 v = img4[g];
@@ -248,36 +252,52 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
     if (FIXED16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keys t here, before the loads of t + 1 issue
     R pay[NP];
     uint32_t tag[NP];
+    // A full super-tile (every one but a chunk's last) with k a constant takes
+    // its hashes and ranks without a per-key or per-probe test: no exec-mask
+    // branches around the 4 x 7 probes (FULL = std::true_type).
+    const bool full = nk == KST && !(dbg & 2);  // dbg bit 1: the general path only (A/B)
+    auto hash_rank = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
 #pragma unroll
-    for (int u = 0; u < KPL; ++u) {
-      const uint32_t q = threadIdx.x + u * T1;
-      const bool ok = q < nk;
-      uint64_t h1 = 0, h2 = 0;
-      if (ok) {
-        if (FIXED16) {
-          uint64_t w0, w1;
-          key_words(cur[u], &w0, &w1);
-          h1 = xxh64_16(w0, w1);
-          h2 = farm_16(w0, w1);
+      for (int u = 0; u < KPL; ++u) {
+        const uint32_t q = threadIdx.x + u * T1;
+        const bool ok = FULL || q < nk;
+        uint64_t h1 = 0, h2 = 0;
+        if (ok) {
+          if (FIXED16) {
+            uint64_t w0, w1;
+            key_words(cur[u], &w0, &w1);
+            h1 = HX ? w0 : xxh64_16(w0, w1);
+            h2 = HX ? w1 : farm_16(w0, w1);
+          } else {
+            bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
+          }
+        }
+        ProbeSeq ps;
+        if (HX == 2) {
+          ps.v1 = h1 & JAVA_LONG_MAX;
+          ps.v2 = h2 & JAVA_LONG_MAX;
+          ps.init((uint32_t)h1, (uint32_t)h2, fm);
         } else {
-          bloom_key_hashes<false>(data, offsets, fixed_len, k0 + q, h1, h2);
+          ps = ProbeSeq(h1, h2, fm);
         }
-      }
-      ProbeSeq ps(h1, h2, fm);
 #pragma unroll
-      for (int t = 0; t < KMAX; ++t) {
-        const int s = u * KMAX + t;
-        tag[s] = INVALID;
-        pay[s] = 0;
-        if (ok && t < kk) {
-          const uint64_t idx = ps.idx;
-          const uint32_t bin = (uint32_t)(idx >> shift1);
-          pay[s] = (R)((uint32_t)(idx & low) | gtag);
-          tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
-          if (t + 1 < kk) ps.next(t, fm);
+        for (int t = 0; t < KMAX; ++t) {
+          const int s = u * KMAX + t;
+          tag[s] = INVALID;
+          pay[s] = 0;
+          if (ok && t < kk) {
+            const uint64_t idx = ps.idx;
+            const uint32_t bin = (uint32_t)(idx >> shift1);
+            pay[s] = (R)((uint32_t)(idx & low) | gtag);
+            tag[s] = (bin << 16) | atomicAdd(&hist[bin], 1u);
+            if (t + 1 < kk) ps.next(t, fm);
+          }
         }
       }
-    }
+    };
+    if (KC && full) hash_rank(std::true_type{});
+    else hash_rank(std::false_type{});
     if (FIXED16) fetch(st + s_step);
     write_out(pend4);  // tile t - 1
     wst = st;
@@ -317,13 +337,18 @@ __global__ __launch_bounds__(T1, KPL * KMAX > 16 ? 4 : (T1 == 512 ? 6 : 4)) void
       if (lane == 63) s_total = incl;
     }
     lds_barrier();  // (B) lstart / dst / total ready
+    auto scatter = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;  // every tag valid
 #pragma unroll
-    for (int s = 0; s < NP; ++s)
-      if (tag[s] != INVALID) {
-        const uint32_t b = tag[s] >> 16, r = tag[s] & 0xFFFFu, j = lstart[b] + r;
-        img[j] = pay[s];
-        if ((r & (RG - 1)) == 0) ibin[j / RG] = (uint8_t)b;  // the group's first slot always holds a probe
-      }
+      for (int s = 0; s < NP; ++s)
+        if (FULL || tag[s] != INVALID) {
+          const uint32_t b = tag[s] >> 16, r = tag[s] & 0xFFFFu, j = lstart[b] + r;
+          img[j] = pay[s];
+          if ((r & (RG - 1)) == 0) ibin[j / RG] = (uint8_t)b;  // the group's first slot always holds a probe
+        }
+    };
+    if (KC && KC == KMAX && full) scatter(std::true_type{});
+    else scatter(std::false_type{});
     pend4 = s_total / RG;
     lds_barrier();  // (C) image complete
   }

@@ -438,8 +438,10 @@ bool bloom_add_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, bool f16, u
 #define RSK_SA1(F16, KM, ...)                                                                                   \
   hipLaunchKernelGGL((bloom_sa1_kernel<F16, KM, T1, uint32_t, ##__VA_ARGS__>), dim3(Wc), dim3(T1), 0, c->stream, \
                      dk.data, dk.offsets, dk.fixed_len, m, b->fm, b->k, shift1, nb1, nst, region, quota, limit,  \
-                     used, overflow, 0u, 1u, sa_dbg)
-      if (kpl4 && b->k == 7 && c->tune.sa_kc >= 0) RSK_SA1(true, 8, 4, false, 7);  // C3's k (1 % FPP)
+                     used, overflow, 0u, 1u, sa_dbg | (c->tune.sa_full < 0 ? 2 : 0))
+      if (kpl4 && b->k == 7 && c->tune.sa_hash == 1) RSK_SA1(true, 8, 4, false, 7, 1);  // timing only
+      else if (kpl4 && b->k == 7 && c->tune.sa_hash == 2) RSK_SA1(true, 8, 4, false, 7, 2);  // timing only
+      else if (kpl4 && b->k == 7 && c->tune.sa_kc >= 0) RSK_SA1(true, 8, 4, false, 7);  // C3's k (1 % FPP)
       else if (kpl4) RSK_SA1(true, 8, 4);
       else if (f16 && kmax == 8) RSK_SA1(true, 8);
       else if (f16) RSK_SA1(true, 16);

@@ -393,33 +393,41 @@ RSK_DEV uint64_t fastmod63(uint64_t x, const FastMod63& f) {
   uint64_t q = __umul64hi(x, f.M) >> (f.l - 1);
   return x - q * f.d;
 }
-
 // Bloom probe indices idx_t = (h_t & Long.MAX_VALUE) % size, h_0 = h1,
 // h_{t+1} = h_t + (t even ? h2 : h1) mod 2^64 (RedissonBloomFilter.java:116-131),
 // with two divisions per key instead of k.  With v_t = h_t mod 2^63 and
 // b = (step addend) mod 2^63:  v_{t+1} = v_t + b - c*2^63, c = bit 63 of
-// v_t + b, so  idx_{t+1} = idx_t + (b mod size) - c*(2^63 mod size)  (mod size),
-// every term already reduced: one conditional subtract and one conditional add.
+// v_t + b, so  idx_{t+1} = idx_t + (b mod size) - c*(2^63 mod size)  (mod size).
+// Both addends, b mod size and (b - 2^63) mod size, are reduced once per key
+// (r1 / r1c for h1, r2 / r2c for h2), so a step is one add of the addend c
+// selects and one conditional subtract.
 struct ProbeSeq {
-  uint64_t v = 0, idx = 0, v1 = 0, v2 = 0, r1 = 0, r2 = 0;
+  uint64_t v = 0, idx = 0, v1 = 0, v2 = 0, r1 = 0, r2 = 0, r1c = 0, r2c = 0;
   ProbeSeq() = default;
   RSK_DEV ProbeSeq(uint64_t h1, uint64_t h2, const FastMod63& f) {
     v1 = h1 & 0x7FFFFFFFFFFFFFFFULL;
     v2 = h2 & 0x7FFFFFFFFFFFFFFFULL;
-    r1 = fastmod63(v1, f);
-    r2 = fastmod63(v2, f);
+    init(fastmod63(v1, f), fastmod63(v2, f), f);
+  }
+  // residues r1 = v1 mod d, r2 = v2 mod d given (timing variants)
+  RSK_DEV void init(uint64_t m1, uint64_t m2, const FastMod63& f) {
+    r1 = m1;
+    r2 = m2;
+    r1c = r1 >= f.r63 ? r1 - f.r63 : r1 + (f.d - f.r63);
+    r2c = r2 >= f.r63 ? r2 - f.r63 : r2 + (f.d - f.r63);
     v = v1;
     idx = r1;
   }
   // idx_t -> idx_{t+1}
+  // (values selected, never member lvalues: a conditional over members with a
+  // run-time t puts the whole struct in scratch memory)
   RSK_DEV void next(int t, const FastMod63& f) {
-    const uint64_t b = (t & 1) ? v1 : v2, rb = (t & 1) ? r1 : r2;
+    const bool odd = t & 1;
+    const uint64_t b = odd ? v1 : v2, ra = odd ? r1 : r2, rc = odd ? r1c : r2c;
     const uint64_t s = v + b;  // < 2^64
-    uint64_t x = idx + rb;     // < 2 * size
-    x = x >= f.d ? x - f.d : x;
-    if (s >> 63) x = x >= f.r63 ? x - f.r63 : x + (f.d - f.r63);
+    const uint64_t x = idx + ((s >> 63) ? rc : ra);  // < 2 * size
+    idx = x >= f.d ? x - f.d : x;
     v = s & 0x7FFFFFFFFFFFFFFFULL;
-    idx = x;
   }
 };
 

@@ -32,7 +32,6 @@ constexpr uint32_t GP_BIN_SHIFT = 12;  // sketches per coarse bin = 4096 (rec ke
 #endif
 constexpr uint32_t GP_SK = RSK_GP_SK;  // sketches per gapply workgroup (GP_SK x 16 KiB of LDS)
 constexpr uint32_t GP_NP = 16 / GP_SK; // gapply parts per fine bin (each reads the bin's records)
-constexpr int GP_U = 4;                // record loads in flight per gapply lane
 constexpr uint32_t GP_T = 1024;        // gcount / gapply workgroup
 #ifndef RSK_GP_TILE
 #define RSK_GP_TILE 8192

@@ -52,6 +52,8 @@ struct Tuning {
   uint64_t bloom_chunk = 0;  // probes per chunk of the slice-routed insert (0: 2^33)
   int sa_dbg = 0;            // TIMING ONLY: the insert's sa1 stores each tile contiguously and the insert stops there
   int sa_v = 0;              // the insert's sa2h tile: uint4 per lane, 0 (= 3), 6 or 8
+  int sa_hash = 0;           // TIMING ONLY: sa1 without the hashes (1) or hashes and mods (2); wrong filters
+  int sa_full = 0;           // -1: sa1 / rp1 without their full-super-tile path (A/B)
   int sa_kc = 0;             // the insert's sa1 for k = 7 with k as a constant: 0 yes, -1 no
   int sa_tiny = 0;           // sub-regions of 32 probes: forces the overflow fallbacks
   uint32_t sa_parts = 0;     // sa2 / rp2 parts per coarse bin (0: 4 x CUs / bins)

@@ -81,6 +81,39 @@ for p in ${PART//,/ }; do
       step c4var 300 python3 scripts/var_variants.py gpurun_out/c4var.json || exit 1 ;;
     io)  # batched Redis export / import of the C5 pool alone
       step io 200 python3 scripts/io_profile.py 3 || exit 1 ;;
+    chain)  # the C3 per-key arithmetic alone, in registers, at C3's size and boundary sizes
+      for d in 9585058378 2147483648 2147483649 4294967297 8589934592 8589934593 17179869189 1099511627773 9007199254740993 4611686018427387909; do
+        step chain_$d 60 scripts/bloom_chain_bench $d 7 || exit 1
+        grep '^{' gpurun_out/chain_$d.log >> gpurun_out/${TAG}_bloom_chain.jsonl
+      done ;;
+    insroutes)  # the C3 insert under diag routes, interleaved (INS="spec spec ...")
+      step insroutes 300 python3 scripts/insert_routes.py gpurun_out/${TAG}_insert_routes.json ${INS:-default sa_hash=1 sa_hash=2} || exit 1 ;;
+    sqacct)  # SQ / LDS counters (3 passes) of the C3 insert, the insert without hashes, add() with replies
+      export ROUNDS=1
+      PA="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"
+      PB="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_LDS_ADDR_CONFLICT"
+      PC="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_ATOMIC_RETURN SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SMEM"
+      for run in ${SQRUNS:-ins ins_h1 rp}; do
+        case $run in
+          ins) R="python3 scripts/insert_routes.py gpurun_out/sq_ins.json default" ;;
+          ins_h1) R="python3 scripts/insert_routes.py gpurun_out/sq_ins_h1.json sa_hash=1" ;;
+          rp) R="python3 scripts/reply_profile.py 1000000000 1" ;;
+        esac
+        for pass in a b c; do
+          case $pass in a) C=$PA ;; b) C=$PB ;; c) C=$PC ;; esac
+          rm -rf gpurun_out/sq_${run}_$pass
+          step sq_${run}_$pass 150 rocprofv3 --pmc $C --output-format csv -d gpurun_out/sq_${run}_$pass -o run -- $R || exit 1
+        done
+      done ;;
+    rpab)  # add() with replies, routes A/B interleaved, one process each: RPAB="route=v,...;route=v,..."
+      IFS=';' read -ra FORMS <<< "${RPAB:-reply_dbg=0;reply_dbg=4}"
+      for rep in 1 2 3; do for f in "${FORMS[@]}"; do
+        step rpab_$rep 120 python3 scripts/reply_profile.py 1000000000 2 "$f" || exit 1
+        grep '^{' gpurun_out/rpab_$rep.log >> gpurun_out/${TAG}_rpab.jsonl
+      done; done ;;
+    chain1)
+      step chain1 60 scripts/bloom_chain_bench || exit 1
+      grep '^{' gpurun_out/chain1.log >> gpurun_out/${TAG}_bloom_chain.jsonl ;;
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;
