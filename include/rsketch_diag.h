@@ -46,8 +46,10 @@ const char *rsk_diag_last_error(void);
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
  *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
  *                 leaves unwritten then corrupts a register: the tests' hole check)
+ *   gpart_dbg     TIMING ONLY (the grouped add stops before its apply): bit 0 the fine-bin pass
+ *                 stores each round's image contiguously, bit 1 no fine-bin count pass
  *   reset         every route back to automatic
- * Every route but sa_dbg, sa_hash and reply_dbg gives bit-identical results; they differ in speed only. */
+ * Every route but sa_dbg, sa_hash, gpart_dbg and reply_dbg gives bit-identical results; they differ in speed only. */
 int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
 
 /* add()-with-replies counters of a context since it was created: key groups

@@ -184,6 +184,7 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "sa_v") t.sa_v = (int)value;
     else if (k == "sa_dbg") t.sa_dbg = (int)value;
     else if (k == "sa_hash") t.sa_hash = (int)value;
+    else if (k == "gpart_dbg") t.gpart_dbg = (int)value;
     else if (k == "sa_full") t.sa_full = (int)value;
     else if (k == "sa_parts") t.sa_parts = (uint32_t)value;
     else if (k == "reply") t.reply = (int)value;

@@ -229,6 +229,17 @@ RSK_DEV void sah_prep(uint32_t p0, uint32_t beg, uint32_t end, const uint32_t* h
 }
 constexpr int SAH_NR = 2;  // segments per quarter in flight (64 VGPRs at 8 waves per SIMD)
 
+// Redis bit i of a 32-bit word (byte i>>3, MSB first) <-> natural bit i
+// (1 << i): the bits of every byte reversed, an involution.
+RSK_DEV uint32_t byte_bitrev(uint32_t x) { return __builtin_bswap32(__builtin_bitreverse32(x)); }
+RSK_DEV uint4 byte_bitrev4(const uint4& v) {
+  return make_uint4(byte_bitrev(v.x), byte_bitrev(v.y), byte_bitrev(v.z), byte_bitrev(v.w));
+}
+
+// The slice is held in LDS in natural bit order (converted on load and
+// write-back), so a record's mask is one shift: 6.07 -> 5.46 ms at C3 (the
+// kernel is VALU-bound, profiles/r05_c3_sq.json).  No branch per record (a
+// slot outside the segment ORs 0 into its word) measured 8.9 ms: more LDS ops.
 __global__ __launch_bounds__(TA, 8) void bloom_sah_apply_kernel(const uint16_t* __restrict__ recs,
                                                              const uint4* __restrict__ hp, uint64_t hp_stride,
                                                              uint32_t f2, const uint32_t* __restrict__ tb,
@@ -247,7 +258,7 @@ __global__ __launch_bounds__(TA, 8) void bloom_sah_apply_kernel(const uint16_t* 
     for (int e = 0; e < 8; ++e)
       if (vm & (1u << e)) {
         const uint32_t off = (((S >> (4 * e)) & 15u) << 16) | ((wv[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
-        atomicOr(&sl[off >> 5], bloom_bit_mask(off));
+        atomicOr(&sl[off >> 5], 1u << (off & 31u));
       }
   };
   for (uint32_t s = xcd_slot(blockIdx.x, gridDim.x); s < nslices; s += gridDim.x) {  // neighbours share segment edges
@@ -255,7 +266,7 @@ __global__ __launch_bounds__(TA, 8) void bloom_sah_apply_kernel(const uint16_t* 
     const uint32_t nw4 = (uint32_t)((nwords - w0 < SL_WORDS ? nwords - w0 : SL_WORDS) / 4);
     uint4* g4 = reinterpret_cast<uint4*>(bits + w0);
     uint4* l4 = reinterpret_cast<uint4*>(sl);
-    for (uint32_t q = threadIdx.x; q < nw4; q += TA) l4[q] = g4[q];
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) l4[q] = byte_bitrev4(g4[q]);
     lds_barrier();  // LDS only: the previous slice's write-back stays in flight
     const uint32_t c = s >> f2, f = s & ((1u << f2) - 1);
     const uint4* hrow = hp + (uint64_t)f * hp_stride;
@@ -326,7 +337,7 @@ __global__ __launch_bounds__(TA, 8) void bloom_sah_apply_kernel(const uint16_t* 
       }
     }
     lds_barrier();
-    for (uint32_t q = threadIdx.x; q < nw4; q += TA) g4[q] = l4[q];
+    for (uint32_t q = threadIdx.x; q < nw4; q += TA) g4[q] = byte_bitrev4(l4[q]);
     lds_barrier();
   }
 }

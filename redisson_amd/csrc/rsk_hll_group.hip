@@ -744,7 +744,7 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
                                                            uint32_t* __restrict__ out, const uint16_t* __restrict__ hdrT,
                                                            const uint32_t* __restrict__ seglen,
                                                            const uint32_t* __restrict__ goff, uint32_t NT,
-                                                           uint32_t tile) {
+                                                           uint32_t tile, int dbg = 0) {
   __shared__ uint32_t stage[TM_RT], img[TM_RT];
   __shared__ uint32_t sa[TM_W], sl[TM_W], sr[TM_W];
   __shared__ uint32_t hist[PT], dlt[PT], cur[PT], wsum[GQ_T / 64], wc[GQ_T / 64];
@@ -860,7 +860,7 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < n; j += GQ_T) {
       const uint32_t x = img[j];
-      out[dlt[x >> 24] + j] = x;
+      out[dbg ? v + j : dlt[x >> 24] + j] = x;  // dbg (timing only): the round's image contiguously
     }
     if (threadIdx.x < PT) hist[threadIdx.x] = 0;
     __syncthreads();
@@ -1390,17 +1390,20 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
         hipLaunchKernelGGL(hll_gparts_tm_kernel, dim3((qmax + PT - 1) / PT), dim3(PT), 0, c->stream, segoff, NT, nbins1,
                            target, qmax, parts, d_nq);
         RSK_CHECK_LAUNCH("hll_gparts_tm");
-        hipLaunchKernelGGL(hll_gcount2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, cnt2, hdrT,
-                           seglen, NT, tile);
-        RSK_CHECK_LAUNCH("hll_gcount2t");
+        if (!(c->tune.gpart_dbg & 2)) {  // timing only: without the count pass
+          hipLaunchKernelGGL(hll_gcount2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, cnt2, hdrT,
+                             seglen, NT, tile);
+          RSK_CHECK_LAUNCH("hll_gcount2t");
+        }
         RSK_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp, sb2, cnt2, offf, (int)ncnt2, c->stream));
         hipLaunchKernelGGL(hll_gfine_kernel, dim3(nfine / 256 + 1), dim3(256), 0, c->stream, offf, parts, d_nq, nbins1,
                            off2);
         RSK_CHECK_LAUNCH("hll_gfine");
         hipLaunchKernelGGL(hll_gpart2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b,
-                           hdrT, seglen, segoff, NT, tile);
+                           hdrT, seglen, segoff, NT, tile, c->tune.gpart_dbg & 1);
         RSK_CHECK_LAUNCH("hll_gpart2t");
       }
+      if (c->tune.gpart_dbg) continue;  // TIMING ONLY: the fine-bin output is not the apply's layout
     } else {
     {
       ProfScope ps(c, "hll_gpart_count");

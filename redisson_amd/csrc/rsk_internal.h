@@ -54,6 +54,7 @@ struct Tuning {
   int sa_v = 0;              // the insert's sa2h tile: uint4 per lane, 0 (= 3), 6 or 8
   int sa_hash = 0;           // TIMING ONLY: sa1 without the hashes (1) or hashes and mods (2); wrong filters
   int sa_full = 0;           // -1: sa1 / rp1 without their full-super-tile path (A/B)
+  int gpart_dbg = 0;         // TIMING ONLY (C5 rows not written): bit 0 fine-bin rounds stored contiguously, bit 1 no count pass
   int sa_kc = 0;             // the insert's sa1 for k = 7 with k as a constant: 0 yes, -1 no
   int sa_tiny = 0;           // sub-regions of 32 probes: forces the overflow fallbacks
   uint32_t sa_parts = 0;     // sa2 / rp2 parts per coarse bin (0: 4 x CUs / bins)
