@@ -952,7 +952,7 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
                                                           const uint32_t* __restrict__ off2, uint32_t G1,
                                                           uint32_t nfine, uint64_t G, int pool_zero,
                                                           int write_all, uint8_t* __restrict__ regs, PCount pc,
-                                                          const double* __restrict__ lc) {
+                                                          const double* __restrict__ lc, int plain_st = 0) {
   static_assert(GP_T == 1024 && GP_SK == 8, "8 writer waves, one sketch each");
   __shared__ __attribute__((aligned(16))) uint32_t r32[GP_SK * HLL_REGS / 4];
   __shared__ SumD part[GP_SK];
@@ -1058,7 +1058,8 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
 #pragma unroll
           for (int u = 0; u < GP_Q; ++u) {  // streaming stores: rows are written once, read back by later calls only
             const u32x4 x = {keep[u].x, keep[u].y, keep[u].z, keep[u].w};
-            __builtin_nontemporal_store(x, gp + u * 64 + lane);
+            if (plain_st) gp[u * 64 + lane] = x;  // (A/B: route gapply_st)
+            else __builtin_nontemporal_store(x, gp + u * 64 + lane);
           }
           if (est) {
             if (__any(kq.big != 0)) {  // a register >= 15 (rare here): the FP64 sum (uniform per wave = per sketch)
@@ -1439,7 +1440,7 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
       // persistent: one resident workgroup per CU (128 KiB of LDS), items strided
       hipLaunchKernelGGL(hll_gapply_kernel, dim3(std::min<uint32_t>(GP_NP * nfine, cus)), dim3(GP_T), 0,
                          c->stream, buf_b, off2, 1u, nfine, G, (pool_zero && first == 0) ? 1 : 0,
-                         (write_all && first == 0) ? 1 : 0, d_regs, pc, c->d_lc);
+                         (write_all && first == 0) ? 1 : 0, d_regs, pc, c->d_lc, c->tune.gapply_st);
       RSK_CHECK_LAUNCH("hll_gapply");
       RSK_HIP(hipMemsetAsync(xcount, 0, 4, c->stream));
       RSK_HIP(hipMemsetAsync(xnhot, 0, 4, c->stream));
