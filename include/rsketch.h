@@ -230,9 +230,10 @@ int rsk_hll_import_redis(rsk_hll *h, uint64_t id, const uint8_t *buf, size_t len
  * Same encoding decisions as the per-key call (sparse while the key fits,
  * promoted for good otherwise; kept SET strings byte for byte); the sparse
  * opcodes and the 6-bit dense packing are produced on the device, one wave
- * per key, with one length pass and one copy per GiB of output -- the
- * checkpoint of a pool.  cap too small: RSK_ERR_INVALID_ARG with
- * offsets filled (offsets[n] = the bytes needed) and nothing written. */
+ * per key, each key encoded once, one copy per 65536 keys -- the checkpoint
+ * of a pool.  cap too small: RSK_ERR_INVALID_ARG with offsets
+ * filled (offsets[n] = the bytes needed); out holds at most the strings of
+ * the whole chunks of 65536 keys that fit before the first that does not. */
 int rsk_hll_export_redis_batch(rsk_hll *h, const uint64_t *ids, uint64_t n, uint8_t *out, uint64_t cap,
                                uint64_t *offsets);
 /* Batched SET: key ids[i] := the Redis HLL string data[offsets[i] .. offsets[i+1])

@@ -1353,8 +1353,8 @@ int rsk_hll_import_redis(rsk_hll* h, uint64_t id, const uint8_t* buf, size_t len
 }
 
 // Batched GET / SET of the Redis strings (rsk_hll_io.hip): the checkpoint of
-// a pool, one length pass and one copy per GiB of output (export), one upload
-// and two kernels (import) instead of a synchronous round trip per key.
+// a pool, one encode pass and one copy per 65536 keys (export), one upload and
+// two kernels (import) instead of a synchronous round trip per key.
 int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint8_t* out, uint64_t cap,
                                uint64_t* offsets) {
   return guarded([&] {
@@ -1385,67 +1385,62 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     }
     const uint64_t nd = dev_i.size();
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-    constexpr uint64_t CHUNK = 1ull << 30;  // output bytes staged per copy
-    uint64_t stage_cap = 0;
+    // Chunks of KC device keys: each encoded once into its slot (12304 bytes
+    // apart), the lengths copied back, the offsets advanced to the chunk's last
+    // key (kept SET strings and missing keys in between from the host), then
+    // the chunk's strings packed into a stage and copied to `out` -- unless the
+    // strings no longer fit in cap: then only the lengths go on, for
+    // offsets[n], and the call fails.
+    constexpr uint64_t KC = 1ull << 16;
+    const uint64_t kc = std::min<uint64_t>(KC, std::max<uint64_t>(nd, 1));
+    uint8_t* w = c->work(al(8 * kc) * 2 + al(kc) + al(4 * kc) + 2 * al(kc * (uint64_t)RSK_HLL_DENSE_BYTES) + 256);
+    uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
+    uint64_t* d_pos = reinterpret_cast<uint64_t*>(w + al(8 * kc));
+    uint8_t* d_want = w + 2 * al(8 * kc);
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(w + 2 * al(8 * kc) + al(kc));
+    uint8_t* d_slots = w + 2 * al(8 * kc) + al(kc) + al(4 * kc);
+    uint8_t* d_stage = d_slots + al(kc * (uint64_t)RSK_HLL_DENSE_BYTES);
     std::vector<uint32_t> len(nd);
-    uint8_t* w = nullptr;
-    if (nd) {
-      stage_cap = std::min<uint64_t>(CHUNK, nd * (uint64_t)RSK_HLL_DENSE_BYTES);
-      w = c->work(al(8 * nd) * 2 + al(nd) + al(4 * nd) + stage_cap + 256);
-      uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
-      uint64_t* d_pos = reinterpret_cast<uint64_t*>(w + al(8 * nd));
-      uint8_t* d_want = w + 2 * al(8 * nd);
-      uint32_t* d_len = reinterpret_cast<uint32_t*>(w + 2 * al(8 * nd) + al(nd));
-      RSK_HIP(hipMemcpyAsync(d_ids, dev_id.data(), 8 * nd, hipMemcpyHostToDevice, c->stream));
-      RSK_HIP(hipMemcpyAsync(d_want, want.data(), nd, hipMemcpyHostToDevice, c->stream));
-      hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)nd, d_len, nullptr, nullptr);
-      RSK_HIP(hipMemcpyAsync(len.data(), d_len, 4 * nd, hipMemcpyDeviceToHost, c->stream));
-      RSK_HIP(hipStreamSynchronize(c->stream));
-      (void)d_pos;
-    }
-    // offsets: device keys by their length pass, kept SET strings as stored, missing keys empty
-    {
-      uint64_t o = 0, d = 0;
-      for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t id = ids[i];
+    std::vector<uint64_t> pos(kc);
+    uint64_t o = 0, next_i = 0;  // offsets[0 .. next_i] are final
+    bool fits = true;
+    auto advance = [&](uint64_t upto, uint64_t d) {  // offsets of keys [next_i, upto); d: the next device key
+      for (; next_i < upto; ++next_i) {
+        const uint64_t id = ids[next_i];
         uint64_t L = 0;
-        if (d < nd && dev_i[d] == i) {
+        if (d < nd && dev_i[d] == next_i) {
           L = len[d++] & 0x7FFFFFFFu;
         } else if (h->exists[id]) {
           L = h->imported.find(id)->second.size();
         }
         o += L;
-        offsets[i + 1] = o;
+        offsets[next_i + 1] = o;
       }
-      if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
-      need(out != nullptr || o == 0, "out is NULL");
+      return d;
+    };
+    uint64_t dcur = 0;  // device keys whose offsets are final
+    for (uint64_t d0 = 0; d0 < nd; d0 += kc) {
+      const uint64_t m = std::min<uint64_t>(kc, nd - d0);
+      RSK_HIP(hipMemcpyAsync(d_ids, dev_id.data() + d0, 8 * m, hipMemcpyHostToDevice, c->stream));
+      RSK_HIP(hipMemcpyAsync(d_want, want.data() + d0, m, hipMemcpyHostToDevice, c->stream));
+      hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)m, d_len, d_slots);
+      RSK_HIP(hipMemcpyAsync(len.data() + d0, d_len, 4 * m, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+      dcur = advance(dev_i[d0 + m - 1] + 1, dcur);
+      fits = fits && o <= cap && out != nullptr;
+      if (!fits) continue;
+      const uint64_t base = offsets[dev_i[d0]], end = offsets[dev_i[d0 + m - 1] + 1];
+      for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
+      RSK_HIP(hipMemcpyAsync(d_pos, pos.data(), 8 * m, hipMemcpyHostToDevice, c->stream));
+      hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, d_stage);
+      d2h_staged(c, out + base, d_stage, end - base);  // (returns synchronised: the stage is reused next)
     }
-    // the write pass, chunk by chunk of output: [offsets[a], offsets[b]) staged whole and copied
-    if (nd) {
-      uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
-      uint64_t* d_pos = reinterpret_cast<uint64_t*>(w + al(8 * nd));
-      uint32_t* d_len = reinterpret_cast<uint32_t*>(w + 2 * al(8 * nd) + al(nd));
-      uint8_t* d_stage = w + 2 * al(8 * nd) + al(nd) + al(4 * nd);
-      std::vector<uint64_t> pos(nd);
-      uint64_t d0 = 0;
-      while (d0 < nd) {
-        const uint64_t base = offsets[dev_i[d0]];
-        uint64_t d1 = d0;
-        while (d1 < nd && offsets[dev_i[d1] + 1] - base <= stage_cap) {
-          pos[d1] = offsets[dev_i[d1]] - base;
-          ++d1;
-        }
-        const uint64_t end = offsets[dev_i[d1 - 1] + 1];
-        RSK_HIP(hipMemcpyAsync(d_pos + d0, pos.data() + d0, 8 * (d1 - d0), hipMemcpyHostToDevice, c->stream));
-        hll_export_launch(c, h->d_regs, h->d_card, d_ids + d0, nullptr, (uint32_t)(d1 - d0), d_len + d0, d_pos + d0,
-                          d_stage);
-        d2h_staged(c, out + base, d_stage, end - base);  // (returns synchronised: the stage is reused next)
-        d0 = d1;
-      }
-      // promoted for good (hllSparseSet -> hllSparseToDense), as the per-key GET
-      for (uint64_t d = 0; d < nd; ++d)
-        if (want[d] && !(len[d] >> 31)) h->dense[dev_id[d]] = 1;
-    }
+    advance(n, dcur);  // the keys after the last device key
+    if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
+    need(out != nullptr || o == 0, "out is NULL");
+    // promoted for good (hllSparseSet -> hllSparseToDense), as the per-key GET
+    for (uint64_t d = 0; d < nd; ++d)
+      if (want[d] && !(len[d] >> 31)) h->dense[dev_id[d]] = 1;
     // kept SET strings: their bytes, card bytes as PFCOUNT last left them (rare: copied one by one)
     for (uint64_t i = 0; i < n; ++i) {
       const uint64_t id = ids[i];

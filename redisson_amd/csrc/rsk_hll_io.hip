@@ -2,7 +2,8 @@
 // GET / SET of the "HYLL" strings (rsk_hll_export_redis_batch /
 // rsk_hll_import_redis_batch), the checkpoint of a grouped pool (SURVEY 5,
 // 8f-1).  One wave per key, its 16384 registers staged in LDS:
-//   export : the key's run structure (a start mask per 64 registers, the last
+//   export : (encoded once into a fixed slot per key, then packed to its
+//            offset) the key's run structure (a start mask per 64 registers, the last
 //            / first run start around each chunk), then either the canonical
 //            sparse opcodes (Redis hyperloglog.c: ZERO 00xxxxxx run 1..64,
 //            XZERO 01xxxxxx yyyyyyyy run 1..16384, VAL 1vvvvvxx value 1..32
@@ -93,8 +94,8 @@ RSK_DEV bool row_runs(IoWave& S, uint32_t lane) {
 // non-zero run, ZERO or the first XZERO byte at a zero run's start, the
 // second XZERO byte at the 65th register of a zero run longer than 64 -- so
 // register j's byte lands at the number of contributions before it.  dst
-// null: the payload length only.
-RSK_DEV uint32_t row_sparse(const IoWave& S, uint32_t lane, uint8_t* __restrict__ dst) {
+// null: the payload length only; bytes at or past dcap are not written.
+RSK_DEV uint32_t row_sparse(const IoWave& S, uint32_t lane, uint8_t* __restrict__ dst, uint32_t dcap = 0xFFFFFFFFu) {
   uint32_t o = 0;
   const uint64_t lt = (1ull << lane) - 1, le = lane == 63 ? ~0ull : (2ull << lane) - 1;
   for (uint32_t k = 0; k < IO_NCH; ++k) {
@@ -115,54 +116,47 @@ RSK_DEV uint32_t row_sparse(const IoWave& S, uint32_t lane, uint8_t* __restrict_
       byte = 0x80u | ((v - 1) << 2) | (r - 1);
     }
     const uint64_t em = __ballot(emit);
-    if (dst && emit) dst[o + (uint32_t)__popcll(em & lt)] = (uint8_t)byte;
+    const uint32_t at = o + (uint32_t)__popcll(em & lt);
+    if (dst && emit && at < dcap) dst[at] = (uint8_t)byte;
     o += (uint32_t)__popcll(em);
   }
   return o;
 }
 
-// Export (rsk_hll_export_redis_batch).  pos null: the length pass -- len[i] =
-// 16 + payload | 1 << 31 for a key that stays sparse (want_sparse and it fits:
-// registers <= 32, string <= 3000 bytes), else 12304.  pos given: the write
-// pass, key i's string at out + pos[i] in the encoding the length pass chose.
+// Export (rsk_hll_export_redis_batch): key i encoded once, into its slot
+// slots + i IO_DENSE (16-byte aligned), its length in len[i] (| 1 << 31 for a
+// key that stays sparse: want_sparse and it fits -- registers <= 32, string
+// <= 3000 bytes -- else the dense 12304 bytes).  The sparse payload is written
+// while it is counted; a payload that turns out too long is overwritten by the
+// dense form.  hll_export_pack then moves the strings to their offsets.
 __global__ __launch_bounds__(IO_T) void hll_export_kernel(const uint8_t* __restrict__ regs,
                                                           const uint64_t* __restrict__ card,
                                                           const uint64_t* __restrict__ ids,
                                                           const uint8_t* __restrict__ want_sparse, uint32_t n,
-                                                          uint32_t* __restrict__ len, const uint64_t* __restrict__ pos,
-                                                          uint8_t* __restrict__ out) {
+                                                          uint32_t* __restrict__ len, uint8_t* __restrict__ slots) {
   __shared__ IoWave SW[IO_W];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   IoWave& S = SW[wv];
   for (uint32_t i = blockIdx.x * IO_W + wv; i < n; i += gridDim.x * IO_W) {  // wave-uniform
     const uint64_t id = ids[i];
+    uint8_t* d = slots + (uint64_t)i * IO_DENSE;
     row_load(S, regs + id * HLL_REGS, lane);
-    bool sparse;
-    if (!pos) {
-      sparse = want_sparse[i] != 0;
-      uint32_t pl = 0;
+    bool sparse = want_sparse[i] != 0;
+    uint32_t pl = 0;
+    if (sparse) {
+      sparse = !row_runs(S, lane);
       if (sparse) {
-        sparse = !row_runs(S, lane);
-        if (sparse) {
-          pl = row_sparse(S, lane, nullptr);
-          sparse = 16 + pl <= IO_SPARSE_MAX;
-        }
+        pl = row_sparse(S, lane, d + 16, IO_SPARSE_MAX - 16);  // (a longer one is dense: the slot stays in bounds)
+        sparse = 16 + pl <= IO_SPARSE_MAX;
       }
-      if (lane == 0) len[i] = sparse ? (0x80000000u | (16 + pl)) : IO_DENSE;
-      continue;
     }
-    sparse = (len[i] >> 31) != 0;
-    uint8_t* d = out + pos[i];
     if (lane < 16) {
       const uint64_t cv = card[id];
       const uint8_t hdr = lane < 4 ? (uint8_t)"HYLL"[lane] : lane == 4 ? (uint8_t)(sparse ? 1 : 0)
                           : lane < 8 ? (uint8_t)0 : (uint8_t)(cv >> (8 * (lane - 8)));
       d[lane] = hdr;
     }
-    if (sparse) {
-      (void)row_runs(S, lane);
-      (void)row_sparse(S, lane, d + 16);
-    } else {
+    if (!sparse) {
       // payload byte b = bits 8b .. 8b + 7 of the register stream (6 bits each, LSB first)
       for (uint32_t b = lane; b < IO_DENSE - 16; b += 64) {
         const uint32_t bit = 8 * b, j = bit / 6, fb = bit % 6;
@@ -170,7 +164,22 @@ __global__ __launch_bounds__(IO_T) void hll_export_kernel(const uint8_t* __restr
         d[16 + b] = (uint8_t)(w >> fb);
       }
     }
+    if (lane == 0) len[i] = sparse ? (0x80000000u | (16 + pl)) : IO_DENSE;
     wave_lds_sync();  // the row is read by every lane before the next key's load
+  }
+}
+
+// String i (slot i, len[i] bytes) to out + pos[i]: one workgroup per string
+// at a time, bytes in order across the lanes (the stores of a wave fill lines).
+__global__ __launch_bounds__(256) void hll_export_pack_kernel(const uint8_t* __restrict__ slots,
+                                                              const uint32_t* __restrict__ len,
+                                                              const uint64_t* __restrict__ pos, uint32_t n,
+                                                              uint8_t* __restrict__ out) {
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t L = len[i] & 0x7FFFFFFFu;
+    const uint8_t* src = slots + (uint64_t)i * IO_DENSE;
+    uint8_t* dst = out + pos[i];
+    for (uint32_t b = threadIdx.x; b < L; b += 256) dst[b] = src[b];
   }
 }
 
@@ -311,14 +320,22 @@ __global__ __launch_bounds__(IO_T) void hll_import_kernel(const uint8_t* __restr
 }
 
 void hll_export_launch(rsk_ctx* c, const uint8_t* d_regs, const uint64_t* d_card, const uint64_t* d_ids,
-                       const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, const uint64_t* d_pos,
-                       uint8_t* d_out) {
+                       const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, uint8_t* d_slots) {
   if (!n) return;
-  ProfScope ps(c, d_pos ? "hll_export_write" : "hll_export_len");
+  ProfScope ps(c, "hll_export_encode");
   const uint32_t blocks = std::min<uint32_t>((n + IO_W - 1) / IO_W, (uint32_t)c->num_cus * 4);
   hipLaunchKernelGGL(hll_export_kernel, dim3(blocks), dim3(IO_T), 0, c->stream, d_regs, d_card, d_ids, d_want_sparse,
-                     n, d_len, d_pos, d_out);
+                     n, d_len, d_slots);
   RSK_CHECK_LAUNCH("hll_export");
+}
+
+void hll_export_pack_launch(rsk_ctx* c, const uint8_t* d_slots, const uint32_t* d_len, const uint64_t* d_pos,
+                            uint32_t n, uint8_t* d_out) {
+  if (!n) return;
+  ProfScope ps(c, "hll_export_pack");
+  const uint32_t blocks = std::min<uint32_t>(n, (uint32_t)c->num_cus * 8);
+  hipLaunchKernelGGL(hll_export_pack_kernel, dim3(blocks), dim3(256), 0, c->stream, d_slots, d_len, d_pos, n, d_out);
+  RSK_CHECK_LAUNCH("hll_export_pack");
 }
 
 void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_ids,

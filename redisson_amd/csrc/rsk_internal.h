@@ -324,12 +324,13 @@ void hll_add_each_launch(rsk_ctx* c, const DevKeys& k, const uint8_t* d_regs_ske
 void hll_max_into_launch(rsk_ctx* c, uint8_t* d_dst, const uint8_t* d_src, uint32_t* d_flag);
 
 // ---- Redis strings of many keys (rsk_hll_io.hip)
-// Export: d_pos null -> d_len[i] = the string length of key d_ids[i] (bit 31:
-// sparse; d_want_sparse[i]: the key is still in the sparse encoding); d_pos
-// given -> its string at d_out + d_pos[i] in the encoding d_len[i] names.
+// Export: key d_ids[i]'s string encoded into d_slots + i * 12304 and its
+// length in d_len[i] (bit 31: sparse; d_want_sparse[i]: the key is still in
+// the sparse encoding); pack: string i from its slot to d_out + d_pos[i].
 void hll_export_launch(rsk_ctx* c, const uint8_t* d_regs, const uint64_t* d_card, const uint64_t* d_ids,
-                       const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, const uint64_t* d_pos,
-                       uint8_t* d_out);
+                       const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, uint8_t* d_slots);
+void hll_export_pack_launch(rsk_ctx* c, const uint8_t* d_slots, const uint32_t* d_len, const uint64_t* d_pos,
+                            uint32_t n, uint8_t* d_out);
 // Import: d_apply null -> check the sparse strings (atomicMin(d_err, i) on a
 // corrupt one; d_canon[i] = 0 where the payload is not the canonical
 // encoding); d_apply given -> decode strings with d_apply[i] set into rows

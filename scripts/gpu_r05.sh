@@ -114,6 +114,9 @@ for p in ${PART//,/ }; do
     chain1)
       step chain1 60 scripts/bloom_chain_bench || exit 1
       grep '^{' gpurun_out/chain1.log >> gpurun_out/${TAG}_bloom_chain.jsonl ;;
+    c5tl)  # C5 bench step timeline: kernel + memory-copy trace
+      rm -rf gpurun_out/c5tl
+      step c5tl 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/c5tl -o run -- python3 bench.py --workload c5 --steps 5 --warmup 2 || exit 1 ;;
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;

@@ -43,7 +43,7 @@ def main():
         fresh.importRedis(ids, data, offs)
         ti.append(time.perf_counter() - t0)
     eng.prof_enable(False)
-    dev = {s: eng.prof_read(s)[0] / reps for s in ("hll_export_len", "hll_export_write", "hll_import_check",
+    dev = {s: eng.prof_read(s)[0] / reps for s in ("hll_export_encode", "hll_export_pack", "hll_import_check",
                                                     "hll_import_write")}
     print(json.dumps({"sketches": G, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
                       "device_ms": dev}), flush=True)

@@ -188,6 +188,36 @@ def test_export_batch_small_buffer(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
+def test_export_batch_chunks_and_late_overflow(L, engine, orc):
+    """More keys than one encode chunk (65536): the chunked export equals the
+    per-key GET at the chunk edges, and a cap one byte short of the total
+    fails with offsets[n] = the bytes needed, the first chunk's strings
+    written."""
+    from redisson_amd import KeyBatch, _lib
+
+    G = 70000
+    h = _pool(L, engine, G)
+    gk = orc.gen_keys16(SEED_C2, 0, 4 * G).reshape(-1, 16)
+    grp = (np.arange(gk.shape[0]) % G).astype(np.uint32)
+    grp[:40000] = 0  # one key with many pairs (dense by size); every key keeps a pair
+    assert np.unique(grp).size == G
+    ks_ = KeyBatch.from_numpy(gk).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks_), grp.ctypes.data))
+    ids = np.arange(G, dtype=np.uint64)
+    rc, out, offs = _export_batch(L, h, ids, cap=G * 300)
+    assert rc == 0
+    need = int(offs[-1])
+    got = _strings(out, offs)
+    for i in (0, 1, 65535, 65536, 65537, G - 1):
+        assert got[i] == _export1(L, h, i), i
+    rc2, out2, offs2 = _export_batch(L, h, ids, cap=need - 1)
+    assert rc2 == _lib.RSK_ERR_INVALID_ARG and int(offs2[-1]) == need
+    assert np.array_equal(offs2, offs)
+    first = int(offs[65536])
+    assert np.array_equal(out2[:first], out[:first])
+    L.rsk_hll_destroy(h)
+
+
 def test_import_batch_round_trip(L, engine, orc):
     """Export every key of the mixed pool, import the strings into a fresh pool
     in one call: same registers, same GET bytes (kept SET strings included),
