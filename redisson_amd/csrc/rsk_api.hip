@@ -244,11 +244,14 @@ void ensure_pinned(rsk_ctx* c) {
 // Bulk copies between device memory and a pageable host buffer through the
 // two pinned stages: host threads copy one stage while the DMA of the other
 // runs (the export / import of a pool's Redis strings: GBs at a time).
-void d2h_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+// On stream `s`, after event `after` (when not null): the context stream
+// stays free for the next kernels meanwhile.  Returns synchronised.
+void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
   ensure_pinned(c);
+  if (after) RSK_HIP(hipStreamWaitEvent(s, after, 0));
   if (c->pin_off) {
-    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    RSK_HIP(hipStreamSynchronize(c->stream));
+    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    RSK_HIP(hipStreamSynchronize(s));
     return;
   }
   const uint64_t S = c->stage_bytes;
@@ -257,8 +260,8 @@ void d2h_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
   for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
     const int slot = (int)(k & 1);  // its previous contents were copied out in the last round
     const uint64_t n = std::min<uint64_t>(S, bytes - o);
-    RSK_HIP(hipMemcpyAsync(c->h_pin[slot], src + o, n, hipMemcpyDeviceToHost, c->stream));
-    RSK_HIP(hipEventRecord(c->pin_ev[slot], c->stream));
+    RSK_HIP(hipMemcpyAsync(c->h_pin[slot], src + o, n, hipMemcpyDeviceToHost, s));
+    RSK_HIP(hipEventRecord(c->pin_ev[slot], s));
     if (prev >= 0) {
       RSK_HIP(hipEventSynchronize(c->pin_ev[prev]));
       par_copy(dst + prev_off, c->h_pin[prev], prev_n, c->stage_threads);
@@ -271,7 +274,7 @@ void d2h_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
     RSK_HIP(hipEventSynchronize(c->pin_ev[prev]));
     par_copy(dst + prev_off, c->h_pin[prev], prev_n, c->stage_threads);
   }
-  RSK_HIP(hipStreamSynchronize(c->stream));
+  RSK_HIP(hipStreamSynchronize(s));
 }
 // The other way; returns with the copies queued on the stream (ordered
 // before the caller's next launch).
@@ -1419,21 +1422,41 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       return d;
     };
     uint64_t dcur = 0;  // device keys whose offsets are final
-    for (uint64_t d0 = 0; d0 < nd; d0 += kc) {
+    auto encode = [&](uint64_t d0) {  // chunk d0's encode and its lengths, queued on the context stream
       const uint64_t m = std::min<uint64_t>(kc, nd - d0);
       RSK_HIP(hipMemcpyAsync(d_ids, dev_id.data() + d0, 8 * m, hipMemcpyHostToDevice, c->stream));
       RSK_HIP(hipMemcpyAsync(d_want, want.data() + d0, m, hipMemcpyHostToDevice, c->stream));
       hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)m, d_len, d_slots);
       RSK_HIP(hipMemcpyAsync(len.data() + d0, d_len, 4 * m, hipMemcpyDeviceToHost, c->stream));
-      RSK_HIP(hipStreamSynchronize(c->stream));
+    };
+    hipEvent_t packed = nullptr;
+    if (nd) {
+      RSK_HIP(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
+      encode(0);
+    }
+    struct EvGuard {
+      hipEvent_t e;
+      ~EvGuard() {
+        if (e) (void)hipEventDestroy(e);
+      }
+    } eg{packed};
+    // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes
+    for (uint64_t d0 = 0; d0 < nd; d0 += kc) {
+      const uint64_t m = std::min<uint64_t>(kc, nd - d0);
+      RSK_HIP(hipStreamSynchronize(c->stream));  // chunk d0's lengths (and the previous pack) done
       dcur = advance(dev_i[d0 + m - 1] + 1, dcur);
       fits = fits && o <= cap && out != nullptr;
-      if (!fits) continue;
-      const uint64_t base = offsets[dev_i[d0]], end = offsets[dev_i[d0 + m - 1] + 1];
-      for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
-      RSK_HIP(hipMemcpyAsync(d_pos, pos.data(), 8 * m, hipMemcpyHostToDevice, c->stream));
-      hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, d_stage);
-      d2h_staged(c, out + base, d_stage, end - base);  // (returns synchronised: the stage is reused next)
+      uint64_t base = 0, end = 0;
+      if (fits) {
+        base = offsets[dev_i[d0]];
+        end = offsets[dev_i[d0 + m - 1] + 1];
+        for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
+        RSK_HIP(hipMemcpyAsync(d_pos, pos.data(), 8 * m, hipMemcpyHostToDevice, c->stream));
+        hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, d_stage);
+        RSK_HIP(hipEventRecord(packed, c->stream));
+      }
+      if (d0 + kc < nd) encode(d0 + kc);  // (after the pack on the same stream: the slots are free)
+      if (fits) d2h_staged_on(c, c->xout, packed, out + base, d_stage, end - base);  // returns synchronised
     }
     advance(n, dcur);  // the keys after the last device key
     if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
