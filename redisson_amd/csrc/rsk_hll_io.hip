@@ -3,13 +3,14 @@
 // rsk_hll_import_redis_batch), the checkpoint of a grouped pool (SURVEY 5,
 // 8f-1).  One wave per key, its 16384 registers staged in LDS:
 //   export : (encoded once into a fixed slot per key, then packed to its
-//            offset) the key's run structure (a start mask per 64 registers, the last
-//            / first run start around each chunk), then either the canonical
+//            offset) the row's run starts compacted in order (four registers
+//            per lane per step, slots from ballots), then either the canonical
 //            sparse opcodes (Redis hyperloglog.c: ZERO 00xxxxxx run 1..64,
 //            XZERO 01xxxxxx yyyyyyyy run 1..16384, VAL 1vvvvvxx value 1..32
 //            run 1..4; maximal runs cut into the longest opcodes, as
-//            encode_sparse in rsk_api.hip) or the 6-bit LSB-first dense
-//            packing (HLL_DENSE_SET_REGISTER), one byte per lane at a time;
+//            encode_sparse in rsk_api.hip) one run per lane, or the 6-bit
+//            LSB-first dense packing (HLL_DENSE_SET_REGISTER), four registers
+//            per lane at a time;
 //   import : the sparse opcode stream parsed 64 bytes per step (which bytes
 //            are XZERO second bytes follows from the last non-XZERO byte
 //            before each lane; run lengths prefix-summed across the wave),
@@ -17,108 +18,104 @@
 //            exactly once), then written into the pool row.
 #include "rsk_internal.h"
 
+#include <utility>
+
 namespace rsk {
 
 constexpr uint32_t IO_T = 256;              // 4 waves: one key each
 constexpr uint32_t IO_W = IO_T / 64;
-constexpr uint32_t IO_NCH = HLL_REGS / 64;  // 64-register chunks of a row
 constexpr uint32_t IO_DENSE = 12304;        // HLL_DENSE_SIZE: 16-byte header + 12288
 constexpr uint32_t IO_SPARSE_MAX = 3000;    // server.hll_sparse_max_bytes (whole string)
 
 struct IoWave {
   uint8_t row[HLL_REGS];
-  uint64_t mask[IO_NCH];             // run starts of chunk k (bit l: register 64k + l)
-  uint16_t lastw[IO_NCH];            // last run start at or before the end of chunk k
-  uint16_t firstw[IO_NCH + 1];       // first run start at or after the beginning of chunk k (HLL_REGS: none)
 };
 
 // This wave's LDS writes are visible to its other lanes (one wave: in order).
 RSK_DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-RSK_DEV void row_load(IoWave& S, const uint8_t* __restrict__ src, uint32_t lane) {
-  const uint4* s4 = reinterpret_cast<const uint4*>(src);
-  uint4 v[HLL_REGS / 16 / 64];
-#pragma unroll
-  for (int u = 0; u < HLL_REGS / 16 / 64; ++u) v[u] = s4[lane + 64 * u];
-  uint4* d4 = reinterpret_cast<uint4*>(S.row);
-#pragma unroll
-  for (int u = 0; u < HLL_REGS / 16 / 64; ++u) d4[lane + 64 * u] = v[u];
-  wave_lds_sync();
+// Lane l gets lane l - 1's x, lane 0 gets lane0 (DPP wave_shr:1, no LDS trip).
+RSK_DEV uint32_t wave_shr1(uint32_t x, uint32_t lane0) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)x, 0x138, 0xF, 0xF, false);
+}
+// Set bits of b in lanes below this one, plus acc.
+RSK_DEV uint32_t lanes_below(uint64_t b, uint32_t acc) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, acc));
 }
 
-// Run starts of the row and their neighbours per chunk; true if any register
-// exceeds 32 (no sparse form: VAL holds 1..32).
-RSK_DEV bool row_runs(IoWave& S, uint32_t lane) {
-  bool big = false;
-  for (uint32_t k = 0; k < IO_NCH; ++k) {
-    const uint32_t j = 64 * k + lane;
-    const uint32_t v = S.row[j], p = j ? S.row[j - 1] : 0x100u;  // register 0 starts a run
-    big |= v > 32;
-    const uint64_t m = __ballot(v != p);
-    if (lane == 0) S.mask[k] = m;
-  }
-  wave_lds_sync();
-  // lane l: chunks 4l .. 4l + 3; prefix max of the last starts, suffix min of the first
-  uint32_t last[4], first[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t k = 4 * lane + i;
-    const uint64_t m = S.mask[k];
-    last[i] = m ? 64 * k + 63 - (uint32_t)__clzll(m) : 0u;  // chunk 0 has register 0: the max is defined
-    first[i] = m ? 64 * k + (uint32_t)__ffsll((long long)m) - 1 : (uint32_t)HLL_REGS;
-  }
-#pragma unroll
-  for (int i = 1; i < 4; ++i) last[i] = max(last[i], last[i - 1]);
-#pragma unroll
-  for (int i = 2; i >= 0; --i) first[i] = min(first[i], first[i + 1]);
-  uint32_t lx = last[3], fx = first[0];  // inclusive scans over lanes: max upward, min downward
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t a = __shfl_up(lx, o, 64), b = __shfl_down(fx, o, 64);
-    if (lane >= (uint32_t)o) lx = max(lx, a);
-    if (lane + o < 64) fx = min(fx, b);
-  }
-  const uint32_t lprev = __shfl_up(lx, 1, 64), fnext = __shfl_down(fx, 1, 64);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    S.lastw[4 * lane + i] = (uint16_t)max(last[i], lane ? lprev : 0u);
-    S.firstw[4 * lane + i] = (uint16_t)min(first[i], lane < 63 ? fnext : (uint32_t)HLL_REGS);
-  }
-  if (lane == 0) S.firstw[IO_NCH] = (uint16_t)HLL_REGS;
-  wave_lds_sync();
-  return __ballot(big) != 0;
-}
+// The export's wave: the row and its run starts in order.  Every run is at
+// least one payload byte, so a row of more runs than IO_RUNS is dense.
+constexpr uint32_t IO_RUNS = IO_SPARSE_MAX - 16;
+struct ExWave {
+  uint8_t row[HLL_REGS];
+  uint16_t start[IO_RUNS];
+};
 
-// The canonical sparse payload of the row (after row_runs).  Every register
-// contributes at most one byte -- a VAL opcode at every 4th register of a
-// non-zero run, ZERO or the first XZERO byte at a zero run's start, the
-// second XZERO byte at the 65th register of a zero run longer than 64 -- so
-// register j's byte lands at the number of contributions before it.  dst
-// null: the payload length only; bytes at or past dcap are not written.
-RSK_DEV uint32_t row_sparse(const IoWave& S, uint32_t lane, uint8_t* __restrict__ dst, uint32_t dcap = 0xFFFFFFFFu) {
-  uint32_t o = 0;
-  const uint64_t lt = (1ull << lane) - 1, le = lane == 63 ? ~0ull : (2ull << lane) - 1;
-  for (uint32_t k = 0; k < IO_NCH; ++k) {
-    const uint32_t j = 64 * k + lane;
-    const uint32_t v = S.row[j];
-    const uint64_t m = S.mask[k], below = m & le, above = m & ~le;
-    const uint32_t s = below ? 64 * k + 63 - (uint32_t)__clzll(below) : S.lastw[k ? k - 1 : 0];
-    const uint32_t e = above ? 64 * k + (uint32_t)__ffsll((long long)above) - 1 : S.firstw[k + 1];
-    const uint32_t L = e - s, p = j - s;
-    bool emit;
-    uint32_t byte;
-    if (v == 0) {
-      emit = p == 0 || (p == 64 && L > 64);
-      byte = p == 0 ? (L <= 64 ? L - 1 : 0x40u | ((L - 1) >> 8)) : ((L - 1) & 0xFFu);
-    } else {
-      emit = (p & 3u) == 0;
-      const uint32_t r = L - p < 4 ? L - p : 4u;
-      byte = 0x80u | ((v - 1) << 2) | (r - 1);
+// Pass 1: the run starts of the row, compacted in order into S.start (a
+// register starts a run when it differs from the one before; register 0
+// always does).  Four registers per lane per step (one dword of the row, the
+// next step's read issued ahead): lane l of step t holds registers 256 t + 4 l
+// .. + 3; a start's slot is the starts in the step's four ballots below this
+// lane (mbcnt) plus the lane's own earlier ones.  Returns the number of runs
+// (stops counting past IO_RUNS: dense); *big: a register exceeds 32 (VAL
+// holds 1..32: no sparse form), valid when the count is at most IO_RUNS.
+RSK_DEV uint32_t row_starts(ExWave& S, uint32_t lane, bool* big) {
+  const uint32_t* r32 = reinterpret_cast<const uint32_t*>(S.row);
+  uint32_t carry = 0x100u, o = 0, wn = r32[lane];
+  bool b = false;
+  for (uint32_t t = 0; t < HLL_REGS / 256; ++t) {
+    const uint32_t w = wn;
+    wn = r32[64 * ((t + 1) & 63) + lane];
+    const uint32_t r0 = w & 0xFFu, r1 = (w >> 8) & 0xFFu, r2 = (w >> 16) & 0xFFu, r3 = w >> 24;
+    const uint32_t prev = wave_shr1(r3, carry);
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)r3, 63);
+    b |= ((w + 0x5F5F5F5Fu) & 0x80808080u) != 0;  // a byte of 33 .. 63 (registers are at most 63)
+    const bool n[4] = {r0 != prev, r1 != r0, r2 != r1, r3 != r2};
+    const uint64_t b0 = __ballot(n[0]), b1 = __ballot(n[1]), b2 = __ballot(n[2]), b3 = __ballot(n[3]);
+    uint32_t at = lanes_below(b3, lanes_below(b2, lanes_below(b1, lanes_below(b0, o))));
+    const uint32_t j0 = 256 * t + 4 * lane;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (n[i] && at < IO_RUNS) S.start[at] = (uint16_t)(j0 + i);
+      at += n[i] ? 1u : 0u;
     }
-    const uint64_t em = __ballot(emit);
-    const uint32_t at = o + (uint32_t)__popcll(em & lt);
-    if (dst && emit && at < dcap) dst[at] = (uint8_t)byte;
-    o += (uint32_t)__popcll(em);
+    o += (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+    if (o > IO_RUNS) break;  // (uniform)
+  }
+  *big = __ballot(b) != 0;
+  return o;
+}
+
+// Pass 2: the canonical sparse payload (Redis hyperloglog.c), one run per
+// lane, 64 runs per step: a zero run of L registers is ZERO (L - 1) when L <=
+// 64, else XZERO's two bytes; a run of value v is ceil(L / 4) VAL opcodes of
+// 4 registers, the last one of the remainder.  Each run's bytes land at the
+// exclusive scan of the bytes per run.  Returns the payload length, or a
+// count past IO_RUNS (stopped early) when it does not fit a sparse string.
+RSK_DEV uint32_t runs_encode(const ExWave& S, uint32_t lane, uint32_t R, uint8_t* __restrict__ dst) {
+  uint32_t o = 0;
+  for (uint32_t rb = 0; rb < R; rb += 64) {
+    const uint32_t r = rb + lane;
+    const bool in = r < R;
+    const uint32_t s = in ? S.start[r] : 0u, e = r + 1 < R ? S.start[r + 1] : (uint32_t)HLL_REGS;
+    const uint32_t v = S.row[s], L = e - s;
+    const uint32_t nb = !in ? 0u : v ? (L + 3) >> 2 : (L > 64 ? 2u : 1u);
+    uint32_t x = nb;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    const uint32_t tot = (uint32_t)__shfl((int)x, 63, 64);
+    if (o + tot > IO_RUNS) return o + tot;  // (uniform)
+    const uint32_t at = o + x - nb;
+    const uint32_t zb0 = L <= 64 ? L - 1 : 0x40u | ((L - 1) >> 8);
+    for (uint32_t q = 0; __ballot(q < nb) != 0; ++q)
+      if (q < nb) {
+        const uint32_t rl = min(L - 4 * q, 4u);
+        dst[at + q] = (uint8_t)(v ? 0x80u | ((v - 1) << 2) | (rl - 1) : q == 0 ? zb0 : ((L - 1) & 0xFFu));
+      }
+    o += tot;
   }
   return o;
 }
@@ -129,25 +126,50 @@ RSK_DEV uint32_t row_sparse(const IoWave& S, uint32_t lane, uint8_t* __restrict_
 // <= 3000 bytes -- else the dense 12304 bytes).  The sparse payload is written
 // while it is counted; a payload that turns out too long is overwritten by the
 // dense form.  hll_export_pack then moves the strings to their offsets.
-__global__ __launch_bounds__(IO_T) void hll_export_kernel(const uint8_t* __restrict__ regs,
-                                                          const uint64_t* __restrict__ card,
-                                                          const uint64_t* __restrict__ ids,
-                                                          const uint8_t* __restrict__ want_sparse, uint32_t n,
-                                                          uint32_t* __restrict__ len, uint8_t* __restrict__ slots) {
-  __shared__ IoWave SW[IO_W];
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  IoWave& S = SW[wv];
-  for (uint32_t i = blockIdx.x * IO_W + wv; i < n; i += gridDim.x * IO_W) {  // wave-uniform
+// A row in registers, 16 bytes x 16 per lane (a native vector type and
+// constant indices from the start: the array stays in VGPRs across the key
+// loop, where uint4's struct copies kept it in scratch).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <size_t... U>
+RSK_DEV void row_regs_load(u32x4 (&nx)[sizeof...(U)], const uint8_t* __restrict__ src, uint32_t lane,
+                           std::index_sequence<U...>) {
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+  ((nx[U] = s4[lane + 64 * U]), ...);
+}
+template <size_t... U>
+RSK_DEV void row_regs_store(const u32x4 (&nx)[sizeof...(U)], ExWave& S, uint32_t lane, std::index_sequence<U...>) {
+  u32x4* d4 = reinterpret_cast<u32x4*>(S.row);
+  ((d4[lane + 64 * U] = nx[U]), ...);
+}
+
+__global__ __launch_bounds__(64) void hll_export_kernel(const uint8_t* __restrict__ regs,
+                                                        const uint64_t* __restrict__ card,
+                                                        const uint64_t* __restrict__ ids,
+                                                        const uint8_t* __restrict__ want_sparse, uint32_t n,
+                                                        uint32_t* __restrict__ len, uint8_t* __restrict__ slots) {
+  __shared__ ExWave S;  // one wave per workgroup: LDS is what bounds the waves per CU
+  const uint32_t lane = threadIdx.x;
+  constexpr int NV = HLL_REGS / 16 / 64;
+  u32x4 nx[NV];  // the next key's row, loaded while this key is encoded
+  const auto U = std::make_index_sequence<NV>{};
+  uint32_t i = blockIdx.x;
+  row_regs_load(nx, regs + ids[i < n ? i : 0] * HLL_REGS, lane, U);
+  for (; i < n; i += gridDim.x) {  // wave-uniform
     const uint64_t id = ids[i];
     uint8_t* d = slots + (uint64_t)i * IO_DENSE;
-    row_load(S, regs + id * HLL_REGS, lane);
+    row_regs_store(nx, S, lane, U);
+    wave_lds_sync();
+    row_regs_load(nx, regs + ids[i + gridDim.x < n ? i + gridDim.x : i] * HLL_REGS, lane, U);
     bool sparse = want_sparse[i] != 0;
     uint32_t pl = 0;
     if (sparse) {
-      sparse = !row_runs(S, lane);
+      bool big;
+      const uint32_t R = row_starts(S, lane, &big);
+      sparse = !big && R <= IO_RUNS;
       if (sparse) {
-        pl = row_sparse(S, lane, d + 16, IO_SPARSE_MAX - 16);  // (a longer one is dense: the slot stays in bounds)
-        sparse = 16 + pl <= IO_SPARSE_MAX;
+        wave_lds_sync();
+        pl = runs_encode(S, lane, R, d + 16);  // (a longer one is dense: the slot stays in bounds)
+        sparse = pl <= IO_RUNS;
       }
     }
     if (lane < 16) {
@@ -157,11 +179,15 @@ __global__ __launch_bounds__(IO_T) void hll_export_kernel(const uint8_t* __restr
       d[lane] = hdr;
     }
     if (!sparse) {
-      // payload byte b = bits 8b .. 8b + 7 of the register stream (6 bits each, LSB first)
-      for (uint32_t b = lane; b < IO_DENSE - 16; b += 64) {
-        const uint32_t bit = 8 * b, j = bit / 6, fb = bit % 6;
-        const uint32_t w = (S.row[j] & 63u) | (j + 1 < (uint32_t)HLL_REGS ? (uint32_t)(S.row[j + 1] & 63u) << 6 : 0u);
-        d[16 + b] = (uint8_t)(w >> fb);
+      // the register stream, 6 bits each, LSB first: registers 4g .. 4g + 3 are payload bytes 3g .. 3g + 2
+      const uint32_t* r32 = reinterpret_cast<const uint32_t*>(S.row);
+      for (uint32_t g = lane; g < HLL_REGS / 4; g += 64) {
+        const uint32_t w = r32[g];
+        const uint32_t bits = (w & 63u) | ((w >> 8) & 63u) << 6 | ((w >> 16) & 63u) << 12 | ((w >> 24) & 63u) << 18;
+        uint8_t* q = d + 16 + 3 * g;
+        q[0] = (uint8_t)bits;
+        q[1] = (uint8_t)(bits >> 8);
+        q[2] = (uint8_t)(bits >> 16);
       }
     }
     if (lane == 0) len[i] = sparse ? (0x80000000u | (16 + pl)) : IO_DENSE;
@@ -323,8 +349,8 @@ void hll_export_launch(rsk_ctx* c, const uint8_t* d_regs, const uint64_t* d_card
                        const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, uint8_t* d_slots) {
   if (!n) return;
   ProfScope ps(c, "hll_export_encode");
-  const uint32_t blocks = std::min<uint32_t>((n + IO_W - 1) / IO_W, (uint32_t)c->num_cus * 4);
-  hipLaunchKernelGGL(hll_export_kernel, dim3(blocks), dim3(IO_T), 0, c->stream, d_regs, d_card, d_ids, d_want_sparse,
+  const uint32_t blocks = std::min<uint32_t>(n, (uint32_t)c->num_cus * 7);  // 22 KB LDS per wave: 7 waves per CU
+  hipLaunchKernelGGL(hll_export_kernel, dim3(blocks), dim3(64), 0, c->stream, d_regs, d_card, d_ids, d_want_sparse,
                      n, d_len, d_slots);
   RSK_CHECK_LAUNCH("hll_export");
 }

@@ -172,6 +172,58 @@ def test_export_batch_matches_oracle_encoders(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
+def _row_with_sparse_len(orc, target):
+    """Registers whose canonical sparse string is exactly target bytes: N
+    single-register VALs with a ZERO of 4 between each two, one of them a run
+    of 5 (VAL 4 + VAL 1) for an even target, and an XZERO tail."""
+    extra = (target - 17) % 2  # header 16 + N VALs + (N - 1) ZEROs + the XZERO tail's 2
+    n = (target - 17 - extra) // 2
+    r = np.zeros(16384, np.uint8)
+    j = 0
+    for k in range(n):
+        run = 5 if (extra and k == 0) else 1
+        r[j:j + run] = 1 + k % 32
+        j += run + 4
+    assert len(orc.hll_encode_sparse(r)) == target
+    return r
+
+
+def test_export_sparse_length_boundary(L, engine, orc):
+    """The encoder's sparse-or-dense decision at the 3000-byte limit
+    (server.hll_sparse_max_bytes): rows of 2996 .. 3000 sparse bytes come back
+    sparse; single PFADDs then grow them across the limit -- each GET equals
+    the per-key GET and the oracle's encoder for the encoding it chose, sparse
+    exactly while the canonical sparse string fits (promotion is for good)."""
+    from redisson_amd import KeyBatch, _lib
+
+    targets = [2996, 2997, 2999, 3000]
+    rows = [_row_with_sparse_len(orc, t) for t in targets]
+    strs = [orc.hll_encode_sparse(r) for r in rows]
+    h = _pool(L, engine, len(rows))
+    ids = np.arange(len(rows), dtype=np.uint64)
+    assert _import_batch(L, h, ids, strs) == 0
+    rc, out, offs = _export_batch(L, h, ids)
+    assert rc == 0 and _strings(out, offs) == strs
+    keys = orc.gen_keys16(SEED_C2, 500000, 16 * len(rows)).reshape(len(rows), 16, 16)
+    promoted = [False] * len(rows)
+    for step in range(16):
+        for i in range(len(rows)):
+            ch = ctypes.c_uint8()
+            ks_ = KeyBatch.from_numpy(np.ascontiguousarray(keys[i, step:step + 1])).as_struct()
+            _lib.check(L.rsk_hll_add(h, i, ctypes.byref(ks_), ctypes.byref(ch)))
+        rc, out, offs = _export_batch(L, h, ids)
+        assert rc == 0
+        for i, s in enumerate(_strings(out, offs)):
+            regs = _regs(L, h, i)
+            sp = orc.hll_encode_sparse(regs, s[8:16])
+            promoted[i] = promoted[i] or len(sp) > 3000
+            assert s[4] == (0 if promoted[i] else 1), (step, i, len(sp))
+            assert s == (orc.hll_encode_dense(regs, s[8:16]) if promoted[i] else sp), (step, i)
+            assert s == _export1(L, h, i), (step, i)
+    assert all(promoted)
+    L.rsk_hll_destroy(h)
+
+
 def test_export_batch_small_buffer(L, engine, orc):
     """cap below the total: RSK_ERR_INVALID_ARG, offsets[n] = the bytes needed,
     nothing written; then the exact size succeeds."""
