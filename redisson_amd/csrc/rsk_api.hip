@@ -243,7 +243,13 @@ void ensure_pinned(rsk_ctx* c) {
 
 // Bulk copies between device memory and a pageable host buffer through the
 // two pinned stages: host threads copy one stage while the DMA of the other
-// runs (the export / import of a pool's Redis strings: GBs at a time).
+// runs (the export / import of a pool's Redis strings: GBs at a time), in
+// about 8 pieces per call (at least 32 MiB each: par_copy starts its threads
+// per piece), so the first copy and the last DMA, which nothing overlaps,
+// stay short.
+uint64_t staged_piece(const rsk_ctx* c, uint64_t bytes) {
+  return std::min<uint64_t>(c->stage_bytes, std::max<uint64_t>(32ull << 20, ((bytes / 8) + 4095) & ~uint64_t(4095)));
+}
 // On stream `s`, after event `after` (when not null): the context stream
 // stays free for the next kernels meanwhile.  Returns synchronised.
 void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
@@ -254,7 +260,7 @@ void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, co
     RSK_HIP(hipStreamSynchronize(s));
     return;
   }
-  const uint64_t S = c->stage_bytes;
+  const uint64_t S = staged_piece(c, bytes);
   int prev = -1;
   uint64_t prev_off = 0, prev_n = 0;
   for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
@@ -284,7 +290,7 @@ void h2d_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
     if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     return;
   }
-  const uint64_t S = c->stage_bytes;
+  const uint64_t S = staged_piece(c, bytes);
   bool used[2] = {false, false};
   for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
     const int slot = (int)(k & 1);
