@@ -44,6 +44,8 @@ const char *rsk_diag_last_error(void);
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
  *   gpart_tm      1 (default): its first pass tile-major (hll_gpart1t), 0: exact-offset runs (hll_gcount + hll_gpart1)
  *   gapply_st     the grouped apply's row stores: 0 nontemporal (default), 1 plain
+ *   gpart_rt      the fine-bin sort's round: 0 8192 records (default), 1 16384 (one
+ *                 workgroup per CU)
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
  *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
  *                 leaves unwritten then corrupts a register: the tests' hole check)

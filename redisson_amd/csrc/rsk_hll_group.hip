@@ -737,7 +737,8 @@ __global__ __launch_bounds__(GQ_T) void hll_gcount2t_kernel(const uint32_t* __re
 // segment starts before the round's end is the round's tile count (the next
 // window is loaded while the round runs).  Segments are staged in LDS at their round offsets
 // (phase A), counted by fine bin (C1), ranked and placed (C2), written out.
-__global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __restrict__ recs,
+template <uint32_t RT = TM_RT>
+__global__ __launch_bounds__(GQ_T, RT > 8192 ? 4 : 8) void hll_gpart2t_kernel(const uint32_t* __restrict__ recs,
                                                            const GPart* __restrict__ parts,
                                                            const uint32_t* __restrict__ d_nq,
                                                            const uint32_t* __restrict__ offf,
@@ -745,7 +746,7 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
                                                            const uint32_t* __restrict__ seglen,
                                                            const uint32_t* __restrict__ goff, uint32_t NT,
                                                            uint32_t tile, int dbg = 0) {
-  __shared__ uint32_t stage[TM_RT], img[TM_RT];
+  __shared__ uint32_t stage[RT], img[RT];
   __shared__ uint32_t sa[TM_W], sl[TM_W], sr[TM_W];
   __shared__ uint32_t hist[PT], dlt[PT], cur[PT], wsum[GQ_T / 64], wc[GQ_T / 64];
   __shared__ uint32_t s_hot, s_e, s_cut;
@@ -784,10 +785,10 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
   const bool hot_mode = s_hot != 0;  // uniform
   const uint32_t hot = s_hot & 0xFFu;
   while (v < pe) {
-    // the round: records [v, vend) from tiles t .. t + ntl - 1 (those starting before v + TM_RT, at
+    // the round: records [v, vend) from tiles t .. t + ntl - 1 (those starting before v + RT, at
     // most the window's TM_W; ntl >= 1), the last one possibly cut (it then starts the next round)
     const uint32_t s0 = e - l;
-    const bool in = s0 < v + TM_RT;
+    const bool in = s0 < v + RT;
     const uint64_t bm = __ballot(in);
     if (lane == 0) wc[w] = (uint32_t)__popcll(bm);
     if (threadIdx.x == TM_W - 1) s_e = e;  // the window's last tile's end (all tiles in: the round ends there)
@@ -795,7 +796,7 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
     uint32_t ntl = 0;
 #pragma unroll
     for (int i = 0; i < (int)(GQ_T / 64); ++i) ntl += wc[i];
-    uint32_t vend = pe - v < TM_RT ? pe : v + TM_RT;
+    uint32_t vend = pe - v < RT ? pe : v + RT;
     if (ntl == TM_W && s_e < vend) vend = s_e;
     if (in) {
       const uint32_t a0 = s0 > v ? s0 : v, e0 = e < vend ? e : vend;
@@ -840,7 +841,7 @@ __global__ __launch_bounds__(GQ_T, 8) void hll_gpart2t_kernel(const uint32_t* __
     __syncthreads();
     // C2: rank and place
 #pragma unroll
-    for (int e8 = 0; e8 < (int)(TM_RT / GQ_T); ++e8) {
+    for (int e8 = 0; e8 < (int)(RT / GQ_T); ++e8) {
       const uint32_t k = threadIdx.x + e8 * GQ_T;
       const bool valid = k < n;
       const uint32_t x = valid ? stage[k] : 0u, b = x >> 24;
@@ -1400,8 +1401,12 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
         hipLaunchKernelGGL(hll_gfine_kernel, dim3(nfine / 256 + 1), dim3(256), 0, c->stream, offf, parts, d_nq, nbins1,
                            off2);
         RSK_CHECK_LAUNCH("hll_gfine");
-        hipLaunchKernelGGL(hll_gpart2t_kernel, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b,
-                           hdrT, seglen, segoff, NT, tile, c->tune.gpart_dbg & 1);
+        if (c->tune.gpart_rt == 1)  // (A/B: route gpart_rt, rounds of 16384 records, one workgroup per CU)
+          hipLaunchKernelGGL(hll_gpart2t_kernel<16384>, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf,
+                             buf_b, hdrT, seglen, segoff, NT, tile, c->tune.gpart_dbg & 1);
+        else
+          hipLaunchKernelGGL(hll_gpart2t_kernel<>, dim3(qmax), dim3(GQ_T), 0, c->stream, buf_a, parts, d_nq, offf, buf_b,
+                             hdrT, seglen, segoff, NT, tile, c->tune.gpart_dbg & 1);
         RSK_CHECK_LAUNCH("hll_gpart2t");
       }
       if (c->tune.gpart_dbg) continue;  // TIMING ONLY: the fine-bin output is not the apply's layout
