@@ -6,10 +6,15 @@
 // mapping.  All arithmetic on keys runs in the HIP kernels of rsk_hll.hip /
 // rsk_bloom.hip; nothing here hashes a key.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -200,6 +205,68 @@ void check_out(const rsk_ctx* c, const rsk_keys* k, const void* out) {
 // read at memcpy speed and the link carries pinned transfers.  Each stage has
 // its own device twin, so chunk i+1's DMA may queue behind chunk i's kernels
 // without a host wait.  rsk_options.stage_threads (default 8) sets the copy threads.
+// The copy threads persist (one pool per process, grown on demand, one job
+// at a time): a staged copy is cut into ~8 pieces per call, and starting and
+// joining the threads per piece cost more than a 32 MiB piece's memcpy.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();  // never destroyed: its threads may be waiting at exit
+    return *p;
+  }
+  // slices 1 .. nt-1 on the workers, slice 0 on the caller
+  void run(uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t piece, unsigned nt) {
+    std::lock_guard<std::mutex> job(job_mu_);
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      while (workers_ + 1 < nt) {
+        const unsigned t = workers_++;
+        const uint64_t g0 = gen_;  // the generation before this job: the new worker takes part in it
+        std::thread([this, t, g0] { loop(t, g0); }).detach();
+      }
+      dst_ = dst;
+      src_ = src;
+      n_ = n;
+      piece_ = piece;
+      nt_ = nt;
+      pending_ = nt - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    std::memcpy(dst, src, std::min<uint64_t>(n, piece));
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void loop(unsigned t, uint64_t seen) {
+    while (true) {
+      uint8_t* dst;
+      const uint8_t* src;
+      uint64_t lo, hi;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (t + 1 >= nt_) continue;  // not part of this job
+        dst = dst_;
+        src = src_;
+        lo = std::min<uint64_t>(n_, (uint64_t)(t + 1) * piece_);
+        hi = std::min<uint64_t>(n_, lo + piece_);
+      }
+      if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  unsigned workers_ = 0, nt_ = 0, pending_ = 0;
+  uint64_t gen_ = 0, n_ = 0, piece_ = 0;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+};
+
 void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n, unsigned threads) {
   const uint64_t min_piece = 2ull << 20;
   const unsigned nt = (unsigned)std::min<uint64_t>(threads, n / min_piece);
@@ -208,13 +275,23 @@ void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n, unsigned threads) {
     return;
   }
   const uint64_t piece = ((n + nt - 1) / nt + 4095) & ~uint64_t(4095);
+  CopyPool::get().run(dst, src, n, piece, nt);
+}
+
+// f(lo, hi) over [0, n) on up to `threads` threads (slices of at least 64Ki
+// items): the batched import's per-string header pass.
+template <class F>
+void par_for(uint64_t n, unsigned threads, F&& f) {
+  const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads, n >> 16));
+  if (nt <= 1) {
+    f(uint64_t(0), n);
+    return;
+  }
+  const uint64_t per = (n + nt - 1) / nt;
   std::vector<std::thread> th;
   th.reserve(nt - 1);
-  for (unsigned t = 1; t < nt; ++t) {
-    const uint64_t lo = std::min<uint64_t>(n, (uint64_t)t * piece), hi = std::min<uint64_t>(n, lo + piece);
-    if (hi > lo) th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
-  }
-  std::memcpy(dst, src, std::min<uint64_t>(n, piece));
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back([&, t] { f(std::min(n, t * per), std::min(n, (t + 1) * per)); });
+  f(uint64_t(0), std::min(n, per));
   for (auto& x : th) x.join();
 }
 
@@ -244,16 +321,21 @@ void ensure_pinned(rsk_ctx* c) {
 // Bulk copies between device memory and a pageable host buffer through the
 // two pinned stages: host threads copy one stage while the DMA of the other
 // runs (the export / import of a pool's Redis strings: GBs at a time), in
-// about 8 pieces per call (at least 32 MiB each: par_copy starts its threads
-// per piece), so the first copy and the last DMA, which nothing overlaps,
-// stay short.
+// about 8 pieces per call (at least 8 MiB each), so the first copy and the
+// last DMA, which nothing overlaps, stay short.
 uint64_t staged_piece(const rsk_ctx* c, uint64_t bytes) {
-  return std::min<uint64_t>(c->stage_bytes, std::max<uint64_t>(32ull << 20, ((bytes / 8) + 4095) & ~uint64_t(4095)));
+  return std::min<uint64_t>(c->stage_bytes, std::max<uint64_t>(8ull << 20, ((bytes / 8) + 4095) & ~uint64_t(4095)));
 }
 // On stream `s`, after event `after` (when not null): the context stream
 // stays free for the next kernels meanwhile.  Returns synchronised.
+// A stage may still feed a DMA an earlier h2d_staged queued (it returns with
+// its copies in flight): both stages' last events are waited for first.
+void pinned_idle(rsk_ctx* c) {
+  for (int b = 0; b < 2; ++b) RSK_HIP(hipEventSynchronize(c->pin_ev[b]));
+}
 void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
   ensure_pinned(c);
+  if (!c->pin_off) pinned_idle(c);
   if (after) RSK_HIP(hipStreamWaitEvent(s, after, 0));
   if (c->pin_off) {
     if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
@@ -290,6 +372,7 @@ void h2d_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
     if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     return;
   }
+  pinned_idle(c);
   const uint64_t S = staged_piece(c, bytes);
   bool used[2] = {false, false};
   for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
@@ -641,6 +724,7 @@ int rsk_shutdown(rsk_ctx* c) {
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_small);
     (void)hipHostFree(c->h_small);
+    if (c->h_io) (void)hipHostFree(c->h_io);
     if (c->h_batch) (void)hipHostFree(c->h_batch);
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_out);
@@ -1410,7 +1494,14 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     uint8_t* d_slots = w + 2 * al(8 * kc) + al(kc) + al(4 * kc);
     uint8_t* d_stage = d_slots + al(kc * (uint64_t)RSK_HLL_DENSE_BYTES);
     std::vector<uint32_t> len(nd);
-    std::vector<uint64_t> pos(kc);
+    // the chunk's ids, flags, lengths and string offsets cross the link from pinned memory: a
+    // pageable copy would hold the host until the stream reaches it (the next chunk's encode
+    // queued behind this chunk's pack would then delay this chunk's copy-out by a whole encode)
+    if (!c->h_io) RSK_HIP(hipHostMalloc(&c->h_io, 21 * KC, hipHostMallocDefault));
+    uint64_t* h_ids = reinterpret_cast<uint64_t*>(c->h_io);
+    uint64_t* pos = h_ids + KC;
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(pos + KC);
+    uint8_t* h_want = reinterpret_cast<uint8_t*>(h_len + KC);
     uint64_t o = 0, next_i = 0;  // offsets[0 .. next_i] are final
     bool fits = true;
     auto advance = [&](uint64_t upto, uint64_t d) {  // offsets of keys [next_i, upto); d: the next device key
@@ -1430,10 +1521,12 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     uint64_t dcur = 0;  // device keys whose offsets are final
     auto encode = [&](uint64_t d0) {  // chunk d0's encode and its lengths, queued on the context stream
       const uint64_t m = std::min<uint64_t>(kc, nd - d0);
-      RSK_HIP(hipMemcpyAsync(d_ids, dev_id.data() + d0, 8 * m, hipMemcpyHostToDevice, c->stream));
-      RSK_HIP(hipMemcpyAsync(d_want, want.data() + d0, m, hipMemcpyHostToDevice, c->stream));
+      std::memcpy(h_ids, dev_id.data() + d0, 8 * m);  // (the previous chunk's copies are done: synchronised)
+      std::memcpy(h_want, want.data() + d0, m);
+      RSK_HIP(hipMemcpyAsync(d_ids, h_ids, 8 * m, hipMemcpyHostToDevice, c->stream));
+      RSK_HIP(hipMemcpyAsync(d_want, h_want, m, hipMemcpyHostToDevice, c->stream));
       hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)m, d_len, d_slots);
-      RSK_HIP(hipMemcpyAsync(len.data() + d0, d_len, 4 * m, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipMemcpyAsync(h_len, d_len, 4 * m, hipMemcpyDeviceToHost, c->stream));
     };
     hipEvent_t packed = nullptr;
     if (nd) {
@@ -1447,23 +1540,42 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       }
     } eg{packed};
     // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes
+    static const bool trace = std::getenv("RSK_IO_TRACE") != nullptr;  // (phase times to stderr)
+    double t_sync = 0, t_adv = 0, t_pack = 0, t_enc = 0, t_d2h = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto t00 = now();
     for (uint64_t d0 = 0; d0 < nd; d0 += kc) {
       const uint64_t m = std::min<uint64_t>(kc, nd - d0);
+      auto t0 = now();
       RSK_HIP(hipStreamSynchronize(c->stream));  // chunk d0's lengths (and the previous pack) done
+      std::memcpy(len.data() + d0, h_len, 4 * m);
+      auto t1 = now();
+      t_sync += ms(t0, t1);
       dcur = advance(dev_i[d0 + m - 1] + 1, dcur);
+      t0 = now();
+      t_adv += ms(t1, t0);
       fits = fits && o <= cap && out != nullptr;
       uint64_t base = 0, end = 0;
       if (fits) {
         base = offsets[dev_i[d0]];
         end = offsets[dev_i[d0 + m - 1] + 1];
         for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
-        RSK_HIP(hipMemcpyAsync(d_pos, pos.data(), 8 * m, hipMemcpyHostToDevice, c->stream));
+        RSK_HIP(hipMemcpyAsync(d_pos, pos, 8 * m, hipMemcpyHostToDevice, c->stream));
         hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, d_stage);
         RSK_HIP(hipEventRecord(packed, c->stream));
       }
+      t1 = now();
+      t_pack += ms(t0, t1);
       if (d0 + kc < nd) encode(d0 + kc);  // (after the pack on the same stream: the slots are free)
+      t0 = now();
+      t_enc += ms(t1, t0);
       if (fits) d2h_staged_on(c, c->xout, packed, out + base, d_stage, end - base);  // returns synchronised
+      t_d2h += ms(t0, now());
     }
+    if (trace)
+      std::fprintf(stderr, "export: loop %.2f ms: sync %.2f advance %.2f pack %.2f encode %.2f d2h %.2f\n",
+                   ms(t00, now()), t_sync, t_adv, t_pack, t_enc, t_d2h);
     advance(n, dcur);  // the keys after the last device key
     if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
     need(out != nullptr || o == 0, "out is NULL");
@@ -1492,16 +1604,50 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     need(n == 0 || (ids != nullptr && offsets != nullptr && data != nullptr), "NULL argument");
     need(n < (1ull << 31), "at most 2^31 - 1 keys per call");
     if (n == 0) return;
-    for (uint64_t i = 0; i < n; ++i) need(offsets[i + 1] >= offsets[i], "offsets must be non-decreasing");
+    static const bool trace = std::getenv("RSK_IO_TRACE") != nullptr;  // (phase times to stderr)
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto tA = now();
+    const unsigned nth = std::max(1u, h->ctx->stage_threads);
+    std::atomic<uint64_t> bad_off{~0ull};
+    par_for(n, nth, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i)
+        if (offsets[i + 1] < offsets[i]) {
+          bad_off.store(i);
+          return;
+        }
+    });
+    need(bad_off.load() == ~0ull, "offsets must be non-decreasing");
     check_hll_ids(h, ids, n);
     // isHLLObjectOrReply per string (as rsk_hll_import_redis), on the host: header, magic,
-    // encoding, exact dense length; the sparse opcodes are checked on the device
-    for (uint64_t i = 0; i < n; ++i) {
+    // encoding, exact dense length; the sparse opcodes are checked on the device.  One pass
+    // over the headers (threads), leaving per string: bit 0 sparse, bit 1 a non-zero unused
+    // header byte (kept as SET), bit 7 not an HLL string / too long (the first one fails).
+    std::vector<uint8_t> hf(n);
+    std::atomic<uint64_t> first_bad{~0ull};
+    par_for(n, nth, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) {
+        const uint8_t* s = data + offsets[i];
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        uint8_t f = 0;
+        if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1 || (s[4] == 0 && len != RSK_HLL_DENSE_BYTES) ||
+            len > (1ull << 31)) {
+          f = 0x80;
+          uint64_t cur = first_bad.load();
+          while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {
+          }
+        } else {
+          f = (uint8_t)(s[4] | ((s[5] | s[6] | s[7]) ? 2 : 0));
+        }
+        hf[i] = f;
+      }
+    });
+    if (first_bad.load() != ~0ull) {
+      const uint64_t i = first_bad.load(), len = offsets[i + 1] - offsets[i];
       const uint8_t* s = data + offsets[i];
-      const uint64_t len = offsets[i + 1] - offsets[i];
-      if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1 || (s[4] == 0 && len != RSK_HLL_DENSE_BYTES))
-        fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value. (string " + std::to_string(i) + ")");
-      need(len <= (1ull << 31), "string too long");
+      if (len >= 16 && std::memcmp(s, "HYLL", 4) == 0 && s[4] <= 1 && !(s[4] == 0 && len != RSK_HLL_DENSE_BYTES))
+        need(false, "string too long");
+      fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value. (string " + std::to_string(i) + ")");
     }
     // SETs of one key in one call: the last wins (a pass from the end marks each id once)
     std::vector<uint8_t> apply(n, 0);
@@ -1526,10 +1672,12 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     uint8_t* d_data = d_canon + al(n) + 256;
     std::vector<uint64_t> off(n + 1);
     for (uint64_t i = 0; i <= n; ++i) off[i] = offsets[i] - base;
-    RSK_HIP(hipMemcpyAsync(d_ids, ids, 8 * n, hipMemcpyHostToDevice, c->stream));
-    RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, c->stream));
-    RSK_HIP(hipMemcpyAsync(d_apply, apply.data(), n, hipMemcpyHostToDevice, c->stream));
+    h2d_staged(c, reinterpret_cast<uint8_t*>(d_ids), reinterpret_cast<const uint8_t*>(ids), 8 * n);
+    h2d_staged(c, reinterpret_cast<uint8_t*>(d_off), reinterpret_cast<const uint8_t*>(off.data()), 8 * (n + 1));
+    h2d_staged(c, d_apply, apply.data(), n);
+    const auto t0 = now();
     h2d_staged(c, d_data, data + base, total);
+    const auto t1 = now();
     RSK_HIP(hipMemsetAsync(d_err, 0xFF, 8, c->stream));
     RSK_HIP(hipMemsetAsync(d_canon, 1, n, c->stream));
     hll_import_launch(c, d_data, d_off, d_ids, nullptr, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
@@ -1539,21 +1687,29 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     RSK_HIP(hipMemcpyAsync(canon.data(), d_canon, n, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipMemcpyAsync(&err, d_err, 8, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
+    const auto t2 = now();
     if (err != ~0ull)
       fail(RSK_ERR_INVALID_HLL, "INVALIDOBJ Corrupted HLL object detected (string " + std::to_string(err) + ")");
     for (uint64_t i = 0; i < n; ++i) {
       if (!apply[i]) continue;
       const uint64_t id = ids[i];
-      const uint8_t* s = data + offsets[i];
       const uint64_t len = offsets[i + 1] - offsets[i];
+      const bool sparse = hf[i] & 1;
       h->exists[id] = 1;
-      h->dense[id] = s[4] == 0;
+      h->dense[id] = !sparse;
       // a copy only where the canonical re-encoding would differ (as rsk_hll_import_redis)
-      bool canonical = s[5] == 0 && s[6] == 0 && s[7] == 0;
-      if (canonical && s[4] == 1) canonical = canon[i] && len <= HLL_SPARSE_MAX_BYTES;
-      if (canonical) hll_forget_import(h, id);
-      else h->imported[id].assign(s, s + len);
+      bool canonical = !(hf[i] & 2);
+      if (canonical && sparse) canonical = canon[i] && len <= HLL_SPARSE_MAX_BYTES;
+      if (canonical) {
+        hll_forget_import(h, id);
+      } else {
+        const uint8_t* s = data + offsets[i];
+        h->imported[id].assign(s, s + len);
+      }
     }
+    if (trace)
+      std::fprintf(stderr, "import: host checks + metadata %.2f ms, h2d %.2f, kernels + sync %.2f, post %.2f\n",
+                   ms(tA, t0), ms(t0, t1), ms(t1, t2), ms(t2, now()));
   });
 }
 

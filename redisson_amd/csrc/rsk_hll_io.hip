@@ -22,14 +22,8 @@
 
 namespace rsk {
 
-constexpr uint32_t IO_T = 256;              // 4 waves: one key each
-constexpr uint32_t IO_W = IO_T / 64;
 constexpr uint32_t IO_DENSE = 12304;        // HLL_DENSE_SIZE: 16-byte header + 12288
 constexpr uint32_t IO_SPARSE_MAX = 3000;    // server.hll_sparse_max_bytes (whole string)
-
-struct IoWave {
-  uint8_t row[HLL_REGS];
-};
 
 // This wave's LDS writes are visible to its other lanes (one wave: in order).
 RSK_DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -225,70 +219,118 @@ RSK_DEV uint32_t sp_op(uint32_t b, uint32_t b1, uint32_t* val, bool* two) {
   return (b & 3u) + 1;
 }
 
+// Inclusive sum over the wave on the DPP path: within each 16-lane row
+// (row_shr 1, 2, 4, 8, zeros shifted in), then row 0's total into row 1 and
+// row 2's into row 3 (row_bcast:15), rows 0-1's into rows 2-3 (row_bcast:31).
+RSK_DEV uint32_t wave_incl_add(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return x;
+}
+
 // Import (rsk_hll_import_redis_batch): string i = data[off[i] .. off[i+1]),
-// its 16-byte header already checked on the host.  apply null: the check
+// its 16-byte header already checked on the host.  APPLY false: the check
 // pass over sparse strings -- every register covered exactly once (else
 // atomicMin(err, i)), canon[i] = the payload is what the export would write
 // (no two zero opcodes in a row, no XZERO of 64 or fewer, a VAL shorter than
-// 4 never followed by a VAL of its value).  apply given (and no error): every
+// 4 never followed by a VAL of its value).  APPLY (and no error): every
 // string with apply[i] set is decoded into row ids[i] and its card bytes.
-__global__ __launch_bounds__(IO_T) void hll_import_kernel(const uint8_t* __restrict__ data,
-                                                          const uint64_t* __restrict__ off,
-                                                          const uint64_t* __restrict__ ids,
-                                                          const uint8_t* __restrict__ apply, uint32_t n,
-                                                          uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
-                                                          uint8_t* __restrict__ canon,
-                                                          unsigned long long* __restrict__ err) {
-  __shared__ IoWave SW[IO_W];
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  IoWave& S = SW[wv];
-  if (apply && *err != ~0ull) return;  // a string failed the check: nothing is written
-  for (uint32_t i = blockIdx.x * IO_W + wv; i < n; i += gridDim.x * IO_W) {  // wave-uniform
-    if (apply && !apply[i]) continue;
+// A sparse payload of at most IO_SB bytes is first copied into LDS with
+// 16-byte loads all in flight together, then parsed from there (parsing
+// from global memory waited a full load latency per 64-byte step); a longer
+// one is parsed from global memory.  One wave per workgroup.
+constexpr uint32_t IO_SB = 4096;
+template <bool APPLY>
+struct ImWave;
+template <>
+struct ImWave<false> {
+  uint8_t sb[IO_SB + 32];
+};
+template <>
+struct ImWave<true> {
+  uint8_t row[HLL_REGS];
+  uint8_t sb[IO_SB + 32];
+};
+template <bool APPLY>
+__global__ __launch_bounds__(64) void hll_import_kernel(const uint8_t* __restrict__ data,
+                                                        const uint64_t* __restrict__ off,
+                                                        const uint64_t* __restrict__ ids,
+                                                        const uint8_t* __restrict__ apply, uint32_t n,
+                                                        uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
+                                                        uint8_t* __restrict__ canon,
+                                                        unsigned long long* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) ImWave<APPLY> S;
+  const uint32_t lane = threadIdx.x;
+  if (APPLY && *err != ~0ull) return;  // a string failed the check: nothing is written
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {  // wave-uniform
+    if (APPLY && !apply[i]) continue;
     const uint8_t* s = data + off[i];
     const uint32_t slen = (uint32_t)(off[i + 1] - off[i]);
     const bool dense = s[4] == 0;
-    if (!apply && dense) continue;  // nothing to check (exact length checked on the host)
-    uint8_t* row = regs + ids[i] * HLL_REGS;
+    if (!APPLY && dense) continue;  // nothing to check (exact length checked on the host)
     const uint8_t* p = s + 16;
     const uint32_t plen = slen - 16;
-    if (dense) {
-      // registers 16q .. 16q + 15 = payload bytes 12q .. 12q + 11
+    if constexpr (APPLY) {
+      if (dense) {
+        uint8_t* row = regs + ids[i] * HLL_REGS;
+        // registers 16q .. 16q + 15 = payload bytes 12q .. 12q + 11
 #pragma unroll 4
-      for (uint32_t q = lane; q < HLL_REGS / 16; q += 64) {
-        const uint8_t* b = p + 12 * q;
-        const uint64_t lo = (uint64_t)ld_u32(b) | (uint64_t)ld_u32(b + 4) << 32;
-        const uint32_t hi = ld_u32(b + 8);
-        uint32_t w[4];
+        for (uint32_t q = lane; q < HLL_REGS / 16; q += 64) {
+          const uint8_t* b = p + 12 * q;
+          const uint64_t lo = (uint64_t)ld_u32(b) | (uint64_t)ld_u32(b + 4) << 32;
+          const uint32_t hi = ld_u32(b + 8);
+          uint32_t w[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          uint32_t x = 0;
+          for (int r = 0; r < 4; ++r) {
+            uint32_t x = 0;
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const uint32_t bit = 6 * (4 * r + t);
-            const uint32_t v = bit + 6 <= 64 ? (uint32_t)(lo >> bit) & 63u
-                               : bit >= 64 ? (hi >> (bit - 64)) & 63u
-                                           : (uint32_t)((lo >> bit) | ((uint64_t)hi << (64 - bit))) & 63u;
-            x |= v << (8 * t);
+            for (int t = 0; t < 4; ++t) {
+              const uint32_t bit = 6 * (4 * r + t);
+              const uint32_t v = bit + 6 <= 64 ? (uint32_t)(lo >> bit) & 63u
+                                 : bit >= 64 ? (hi >> (bit - 64)) & 63u
+                                             : (uint32_t)((lo >> bit) | ((uint64_t)hi << (64 - bit))) & 63u;
+              x |= v << (8 * t);
+            }
+            w[r] = x;
           }
-          w[r] = x;
+          reinterpret_cast<uint4*>(row)[q] = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        reinterpret_cast<uint4*>(row)[q] = make_uint4(w[0], w[1], w[2], w[3]);
+        if (lane == 0) card[ids[i]] = ld_u64(s + 8);
+        continue;
       }
-      if (lane == 0) card[ids[i]] = ld_u64(s + 8);
-      continue;
-    }
-    if (apply) {
       uint4* d4 = reinterpret_cast<uint4*>(S.row);
       for (uint32_t u = lane; u < HLL_REGS / 16; u += 64) d4[u] = make_uint4(0, 0, 0, 0);
-      wave_lds_sync();
     }
+    // the payload into LDS (16-byte aligned loads around it: d_data has slack past the end)
+    const bool staged = plen <= IO_SB;
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    if (staged) {
+      const uint4* g4 = reinterpret_cast<const uint4*>(p - sh);
+      const uint32_t n4 = (sh + plen + 15) / 16;
+      uint4 v[IO_SB / 16 / 64 + 1];
+#pragma unroll
+      for (uint32_t u = 0; u < IO_SB / 16 / 64 + 1; ++u) {
+        const uint32_t c = lane + 64 * u;
+        v[u] = c < n4 ? g4[c] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < IO_SB / 16 / 64 + 1; ++u) {
+        const uint32_t c = lane + 64 * u;
+        if (c < n4 && 16 * c < IO_SB + 32) reinterpret_cast<uint4*>(S.sb)[c] = v[u];
+      }
+    }
+    wave_lds_sync();
+    auto byte_at = [&](uint32_t q) -> uint32_t { return staged ? S.sb[sh + q] : p[q]; };
     uint32_t at = 0, cin = 0;  // registers covered so far; byte 0 of the step is an XZERO second byte
     bool ok = true, can = true;
     for (uint32_t c0 = 0; c0 < plen; c0 += 64) {
       const uint32_t q = c0 + lane;
       const bool in = q < plen;
-      const uint32_t b = in ? p[q] : 0u;
+      const uint32_t b = in ? byte_at(q) : 0u;
       const bool isx = in && (b & 0xC0u) == 0x40u;
       // byte l is a second byte iff an odd number of XZERO first bytes precede it back to the
       // last byte that cannot start one (or to the step's start, whose state is cin)
@@ -299,49 +341,46 @@ __global__ __launch_bounds__(IO_T) void hll_import_kernel(const uint8_t* __restr
       uint32_t val = 0, run = 0;
       bool two = false;
       if (st) {
-        const uint32_t b1 = q + 1 < plen ? p[q + 1] : 0u;
+        const uint32_t b1 = q + 1 < plen ? byte_at(q + 1) : 0u;
         run = sp_op(b, b1, &val, &two);
         if (two && q + 1 >= plen) ok = false;  // XZERO cut by the end of the string
-        if (!apply) {
+        if constexpr (!APPLY) {
           // canonical form: the export's encoder would emit exactly this opcode here
           if (two && run <= 64) can = false;
           const uint32_t qn = q + (two ? 2 : 1);
           if (qn < plen) {
             uint32_t nv = 0;
             bool ntwo = false;
-            (void)sp_op(p[qn], qn + 1 < plen ? p[qn + 1] : 0u, &nv, &ntwo);
+            (void)sp_op(byte_at(qn), qn + 1 < plen ? byte_at(qn + 1) : 0u, &nv, &ntwo);
             if (val == 0 && nv == 0) can = false;                  // two zero runs in a row
             if (val != 0 && nv == val && run < 4) can = false;     // a VAL run cut short
           }
         }
       }
       // register position of each opcode: exclusive prefix of the run lengths
-      uint32_t x = run;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-      }
+      const uint32_t x = wave_incl_add(run);
       const uint32_t first = at + x - run;
-      if (apply && st && val != 0 && first + run <= (uint32_t)HLL_REGS)
-        for (uint32_t r = 0; r < run; ++r) S.row[first + r] = (uint8_t)val;
-      at += __shfl(x, 63, 64);
+      if constexpr (APPLY)
+        if (st && val != 0 && first + run <= (uint32_t)HLL_REGS)
+          for (uint32_t r = 0; r < run; ++r) S.row[first + r] = (uint8_t)val;
+      at += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
       if (at > (uint32_t)HLL_REGS) at = HLL_REGS + 1;  // (no wrap on adversarial input)
     }
     ok = __ballot(!ok) == 0 && at == (uint32_t)HLL_REGS;
     can = __ballot(!can) == 0;
-    if (!apply) {
+    if constexpr (!APPLY) {
       if (lane == 0) {
         canon[i] = can ? 1 : 0;
         if (!ok) atomicMin(err, (unsigned long long)i);
       }
-      continue;
+    } else {
+      wave_lds_sync();
+      uint8_t* row = regs + ids[i] * HLL_REGS;
+      const uint4* s4 = reinterpret_cast<const uint4*>(S.row);
+      for (uint32_t u = lane; u < HLL_REGS / 16; u += 64) reinterpret_cast<uint4*>(row)[u] = s4[u];
+      if (lane == 0) card[ids[i]] = ld_u64(s + 8);
     }
-    wave_lds_sync();
-    const uint4* s4 = reinterpret_cast<const uint4*>(S.row);
-    for (uint32_t u = lane; u < HLL_REGS / 16; u += 64) reinterpret_cast<uint4*>(row)[u] = s4[u];
-    if (lane == 0) card[ids[i]] = ld_u64(s + 8);
-    wave_lds_sync();
+    wave_lds_sync();  // this string's LDS reads are done before the next string's writes
   }
 }
 
@@ -369,9 +408,13 @@ void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
                        unsigned long long* d_err) {
   if (!n) return;
   ProfScope ps(c, d_apply ? "hll_import_write" : "hll_import_check");
-  const uint32_t blocks = std::min<uint32_t>((n + IO_W - 1) / IO_W, (uint32_t)c->num_cus * 4);
-  hipLaunchKernelGGL(hll_import_kernel, dim3(blocks), dim3(IO_T), 0, c->stream, d_data, d_off, d_ids, d_apply, n,
-                     d_regs, d_card, d_canon, d_err);
+  // one wave per workgroup: the check pass holds 4 KiB of LDS (24 waves per CU), the decode 20 KiB (7 per CU)
+  if (d_apply)
+    hipLaunchKernelGGL(hll_import_kernel<true>, dim3(std::min<uint32_t>(n, (uint32_t)c->num_cus * 7)), dim3(64), 0,
+                       c->stream, d_data, d_off, d_ids, d_apply, n, d_regs, d_card, d_canon, d_err);
+  else
+    hipLaunchKernelGGL(hll_import_kernel<false>, dim3(std::min<uint32_t>(n, (uint32_t)c->num_cus * 24)), dim3(64), 0,
+                       c->stream, d_data, d_off, d_ids, d_apply, n, d_regs, d_card, d_canon, d_err);
   RSK_CHECK_LAUNCH("hll_import");
 }
 

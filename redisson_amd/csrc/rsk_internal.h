@@ -149,6 +149,7 @@ struct rsk_ctx {
   // small scratch: flags / counters / ids (device) and pinned host mirror
   uint8_t* d_small = nullptr;
   uint8_t* h_small = nullptr;
+  uint8_t* h_io = nullptr;  // pinned per-chunk ids / lengths / offsets of the batched export (lazy)
   uint64_t small_bytes = 0;
   // grow-on-demand device scratch for batched calls (released by rsk_trim)
   uint8_t* d_work = nullptr;

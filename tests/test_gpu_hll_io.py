@@ -357,6 +357,45 @@ def test_import_batch_every_sparse_shape(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
+def test_import_batch_long_sparse(L, engine, orc):
+    """Sparse strings longer than the decoder's 4 KiB LDS stage (parsed from
+    global memory) next to staged ones: 16384 single-register VALs (16400
+    bytes), a 5000-byte one, a 4096-byte payload (the stage's edge, staged)
+    and 4097 (not) -- decoded exactly and kept as SET; one covering a
+    register too many fails the whole batch with nothing written."""
+    from redisson_amd import _lib
+
+    def hdr():
+        return bytearray(b"HYLL\x01" + bytes(11))
+
+    rows, strs = [], []
+    r = (1 + np.arange(16384) % 2).astype(np.uint8)  # 1, 2, 1, 2, ...: one VAL per register
+    rows.append(r)
+    for plen in (5000, 4096, 4097, 3001):
+        # plen - 1 single-register VALs alternating 3 / 4, then one XZERO... sized to plen bytes
+        nv = plen - 2
+        rr = np.zeros(16384, np.uint8)
+        rr[:nv] = 3 + np.arange(nv) % 2
+        rows.append(rr)
+    for rr in rows:
+        sp = orc.hll_encode_sparse(rr)
+        strs.append(bytes(sp))
+    assert [len(x) - 16 for x in strs] == [16384, 5000, 4096, 4097, 3001]
+    h = _pool(L, engine, len(strs) + 1)
+    ids = np.arange(len(strs))
+    assert _import_batch(L, h, ids, strs) == 0
+    for i, rr in enumerate(rows):
+        assert np.array_equal(_regs(L, h, i), rr), i
+    rc, out, offs = _export_batch(L, h, ids)
+    assert rc == 0 and _strings(out, offs) == strs  # kept as SET (over 3000 bytes)
+    # one register too many (a trailing ZERO 1) on the long, unstaged form: nothing is written
+    bad = strs[0] + bytes([0x00])
+    before = _regs(L, h, 5).copy()
+    assert _import_batch(L, h, np.array([5, 0]), [strs[1], bad]) == _lib.RSK_ERR_INVALID_HLL
+    assert np.array_equal(_regs(L, h, 5), before)
+    L.rsk_hll_destroy(h)
+
+
 def test_c5_pool_checkpoint_round_trip(L, engine, orc):
     """BASELINE configs[4] per GPU: 1M sketches after 500M grouped pairs,
     exported in one call and imported into a fresh pool in one call.  The
