@@ -305,6 +305,7 @@ void ensure_pinned(rsk_ctx* c) {
             hipMalloc(&c->d_pin[1], bytes) == hipSuccess &&
             hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess;
+  for (int r = 0; r < 8 && ok; ++r) ok = hipEventCreateWithFlags(&c->ring_ev[r], hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     (void)hipGetLastError();
     for (int b = 0; b < 2; ++b) {
@@ -313,6 +314,10 @@ void ensure_pinned(rsk_ctx* c) {
       if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
       c->h_pin[b] = c->d_pin[b] = nullptr;
       c->pin_ev[b] = nullptr;
+    }
+    for (auto& e : c->ring_ev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
     }
     c->pin_off = true;
   }
@@ -333,6 +338,7 @@ uint64_t staged_piece(const rsk_ctx* c, uint64_t bytes) {
 void pinned_idle(rsk_ctx* c) {
   for (int b = 0; b < 2; ++b) RSK_HIP(hipEventSynchronize(c->pin_ev[b]));
 }
+// (d2h_staged_on returns synchronised: its ring events are idle between calls)
 void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
   ensure_pinned(c);
   if (!c->pin_off) pinned_idle(c);
@@ -342,26 +348,26 @@ void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, co
     RSK_HIP(hipStreamSynchronize(s));
     return;
   }
-  const uint64_t S = staged_piece(c, bytes);
-  int prev = -1;
-  uint64_t prev_off = 0, prev_n = 0;
-  for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
-    const int slot = (int)(k & 1);  // its previous contents were copied out in the last round
-    const uint64_t n = std::min<uint64_t>(S, bytes - o);
-    RSK_HIP(hipMemcpyAsync(c->h_pin[slot], src + o, n, hipMemcpyDeviceToHost, s));
-    RSK_HIP(hipEventRecord(c->pin_ev[slot], s));
-    if (prev >= 0) {
-      RSK_HIP(hipEventSynchronize(c->pin_ev[prev]));
-      par_copy(dst + prev_off, c->h_pin[prev], prev_n, c->stage_threads);
-    }
-    prev = slot;
-    prev_off = o;
-    prev_n = n;
+  // a ring of NS slots over the two stages (2, 4 or 8: as many pieces of S as they hold), the
+  // DMAs of up to NS - 1 pieces queued ahead of the host copy (the copy engine never waits for
+  // the host between pieces)
+  const uint64_t S = staged_piece(c, bytes), B = c->stage_bytes + c->stage_bytes / 4;
+  const uint32_t per = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, B / S));
+  const uint32_t NS = 2 * (per >= 4 ? 4 : per >= 2 ? 2 : 1);
+  auto slot_ptr = [&](uint32_t j) { return c->h_pin[j & 1] + (uint64_t)(j >> 1) * S; };
+  const uint64_t np = (bytes + S - 1) / S;
+  auto copy_out = [&](uint64_t k) {
+    const uint32_t j = (uint32_t)(k % NS);
+    RSK_HIP(hipEventSynchronize(c->ring_ev[j]));
+    par_copy(dst + k * S, slot_ptr(j), std::min<uint64_t>(S, bytes - k * S), c->stage_threads);
+  };
+  for (uint64_t k = 0; k < np; ++k) {
+    const uint32_t j = (uint32_t)(k % NS);  // piece k - NS, its last user, was copied out at k - 1
+    RSK_HIP(hipMemcpyAsync(slot_ptr(j), src + k * S, std::min<uint64_t>(S, bytes - k * S), hipMemcpyDeviceToHost, s));
+    RSK_HIP(hipEventRecord(c->ring_ev[j], s));
+    if (k + 1 >= NS) copy_out(k + 1 - NS);
   }
-  if (prev >= 0) {
-    RSK_HIP(hipEventSynchronize(c->pin_ev[prev]));
-    par_copy(dst + prev_off, c->h_pin[prev], prev_n, c->stage_threads);
-  }
+  for (uint64_t k = np >= NS - 1 ? np - (NS - 1) : 0; k < np; ++k) copy_out(k);
   RSK_HIP(hipStreamSynchronize(s));
 }
 // The other way; returns with the copies queued on the stream (ordered
@@ -721,6 +727,8 @@ int rsk_shutdown(rsk_ctx* c) {
       (void)hipFree(c->d_pin[b]);
       if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
     }
+    for (hipEvent_t e : c->ring_ev)
+      if (e) (void)hipEventDestroy(e);
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_small);
     (void)hipHostFree(c->h_small);

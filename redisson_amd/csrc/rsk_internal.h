@@ -142,6 +142,7 @@ struct rsk_ctx {
   uint8_t* h_pin[2] = {nullptr, nullptr};
   uint8_t* d_pin[2] = {nullptr, nullptr};
   hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  hipEvent_t ring_ev[8] = {};  // d2h_staged_on: up to 8 pieces of the two stages in flight
   bool pin_off = false;
   // per-workgroup partial register files [slabs][16384] u8
   uint8_t* d_slab = nullptr;
