@@ -20,6 +20,8 @@
 #include <vector>
 #include <unordered_map>
 
+#include <pthread.h>
+
 #include "rsk_internal.h"
 
 using rsk::DevKeys;
@@ -211,8 +213,14 @@ void check_out(const rsk_ctx* c, const rsk_keys* k, const void* out) {
 class CopyPool {
  public:
   static CopyPool& get() {
-    static CopyPool* p = new CopyPool();  // never destroyed: its threads may be waiting at exit
-    return *p;
+    // never destroyed (its threads may be waiting at exit); a forked child, which has none of
+    // the threads, starts a fresh pool
+    static std::once_flag once;
+    std::call_once(once, [] {
+      inst_ = new CopyPool();
+      pthread_atfork(nullptr, nullptr, [] { inst_ = new CopyPool(); });
+    });
+    return *inst_;
   }
   // slices 1 .. nt-1 on the workers, slice 0 on the caller
   void run(uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t piece, unsigned nt) {
@@ -259,6 +267,7 @@ class CopyPool {
       if (--pending_ == 0) done_cv_.notify_all();
     }
   }
+  static inline CopyPool* inst_ = nullptr;
   std::mutex job_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   unsigned workers_ = 0, nt_ = 0, pending_ = 0;
