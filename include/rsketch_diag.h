@@ -46,6 +46,7 @@ const char *rsk_diag_last_error(void);
  *   gapply_st     the grouped apply's row stores: 0 nontemporal (default), 1 plain
  *   gpart_rt      the fine-bin sort's round: 0 8192 records (default), 1 16384 (one
  *                 workgroup per CU)
+ *   io_trace      1: the batched export / import print their host phase times to stderr
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
  *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
  *                 leaves unwritten then corrupts a register: the tests' hole check)

@@ -1557,7 +1557,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       }
     } eg{packed};
     // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes
-    static const bool trace = std::getenv("RSK_IO_TRACE") != nullptr;  // (phase times to stderr)
+    const bool trace = c->tune.io_trace != 0;  // (route io_trace: phase times to stderr)
     double t_sync = 0, t_adv = 0, t_pack = 0, t_enc = 0, t_d2h = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1621,7 +1621,7 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     need(n == 0 || (ids != nullptr && offsets != nullptr && data != nullptr), "NULL argument");
     need(n < (1ull << 31), "at most 2^31 - 1 keys per call");
     if (n == 0) return;
-    static const bool trace = std::getenv("RSK_IO_TRACE") != nullptr;  // (phase times to stderr)
+    const bool trace = h->ctx->tune.io_trace != 0;  // (route io_trace: phase times to stderr)
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto tA = now();

@@ -66,6 +66,7 @@ struct Tuning {
   int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
   int gpart_poison = 0;      // timing-free check: fill the fine-bin output with 0xFF first (a hole then shows)
+  int io_trace = 0;          // batched export / import: host phase times to stderr
   int gpart_rt = 0;          // hll_gpart2t's round: 0 8192 records, 1 16384 (A/B)
   int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B)
   int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no

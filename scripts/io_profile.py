@@ -22,6 +22,8 @@ def main():
     _lib.load()
     _lib.diag()
     eng = _lib.Engine(0)
+    if os.environ.get("IO_TRACE"):
+        eng.set_route("io_trace", 1)  # host phase times of each call to stderr
     G, n = 1_000_000, 500_000_000
     g, k = devmem.gen_grouped(eng, 0x5EED0006, G, 0, n)
     pool = GroupedHyperLogLog(eng, G)
