@@ -396,6 +396,30 @@ def test_import_batch_long_sparse(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
+def test_dense_pool_round_trip_many_pieces(L, engine, orc):
+    """70000 dense keys (861 MB of strings): one export chunk is ~806 MB, so
+    the staged copy-out cycles its ring of pinned slots several times, and the
+    import stages ~861 MB in pieces; SET then GET returns the same bytes, and
+    the registers equal the oracle's decode."""
+    rng = np.random.default_rng(29)
+    G = 70000
+    rows = rng.integers(0, 25, size=(64, 16384), dtype=np.uint8)
+    strs64 = [bytes(orc.hll_encode_dense(r)) for r in rows]
+    assert all(len(x) == 12304 for x in strs64)
+    pick = rng.integers(0, 64, G)
+    strs = [strs64[j] for j in pick]
+    h = _pool(L, engine, G)
+    ids = np.arange(G)
+    assert _import_batch(L, h, ids, strs) == 0
+    rc, out, offs = _export_batch(L, h, ids)
+    assert rc == 0
+    assert int(offs[-1]) == 12304 * G
+    assert np.array_equal(out[: 12304 * G].reshape(G, 12304), np.frombuffer(b"".join(strs), np.uint8).reshape(G, 12304))
+    for i in (0, 1, 65535, 65536, G - 1):
+        assert np.array_equal(_regs(L, h, i), rows[pick[i]]), i
+    L.rsk_hll_destroy(h)
+
+
 def test_c5_pool_checkpoint_round_trip(L, engine, orc):
     """BASELINE configs[4] per GPU: 1M sketches after 500M grouped pairs,
     exported in one call and imported into a fresh pool in one call.  The
