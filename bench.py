@@ -575,9 +575,90 @@ def checkpoint_bench(engine, pool):
                     "steps, host buffers (PCIe inclusive), one call each"}
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher around it (no WORLD_SIZE in the
+    environment): start N fresh worker processes of this same command, one per
+    GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as
+    torch.distributed.run would set them, forward rank 0's JSON line, and fail
+    if any worker fails.  This process makes no HIP, RCCL or torch call (it
+    never touched the GPU, and it execs nothing): the workers own the devices.
+    After the first worker fails the others are stopped (they would wait in a
+    collective for the dead rank), by their own pids."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+    # rank 0's stdout is drained by a thread so a full pipe never stalls it
+    import threading
+
+    out = []
+    t = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    t.start()
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log("launcher: rank %d exited with %d; stopping the other ranks" % (r, code))
+                for q in sorted(live):
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGTERM)  # the worker's own session, started above
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.05)
+    t.join(timeout=30)
+    text = out[0].decode() if out and out[0] else ""
+    lines = [ln for ln in text.splitlines() if ln.startswith("{")]
+    if rc == 0 and not lines:
+        log("launcher: rank 0 printed no JSON line")
+        rc = 1
+    if lines:
+        print(lines[-1], flush=True)
+    return rc
+
+
+def launcher_selftest(rank: int, world: int) -> None:
+    """--launcher-selftest: the launch plumbing alone, stopped before
+    librsketch is loaded -- every rank joins one gloo group and rank 0 prints
+    the ranks that joined (tests/test_bench_launcher.py, on the CPU)."""
+    if world == 1:
+        print(json.dumps({"launcher_selftest": True, "n_gpus": 1, "ranks": [{"rank": 0, "local_rank": 0,
+                                                                             "pid": os.getpid()}]}), flush=True)
+        return
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if os.environ.get("RSK_SELFTEST_FAIL_RANK") == str(rank):
+        raise SystemExit(3)  # the test of a failing rank: the others then wait in all_gather until stopped
+    everyone = [None] * world
+    dist.all_gather_object(everyone, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                      "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"launcher_selftest": True, "n_gpus": world, "ranks": everyone}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; without a launcher (no WORLD_SIZE) bench.py starts them itself")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="test the multi-rank launch only: ranks join a gloo group and stop (no GPU)")
     # defaults: the kernel trace shows the first ~12 launches on a box running
     # slower while the clock settles (profiles/r02_roofline_check.json)
     ap.add_argument("--steps", type=int, default=50)
@@ -602,12 +683,21 @@ def main():
     ap.add_argument("--cpu-passes", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU figure (the GPU box's CPU share is 16)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start the ranks here, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+        # a silent N = 1 run reported as N GPUs (or the reverse) would corrupt the scaling curve
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus=%d; refusing to run" % (world, args.gpus))
+    if args.launcher_selftest:
+        launcher_selftest(rank, world)
+        return
 
     # librsketch (system ROCm runtime) is loaded before torch is imported, so
     # the process has exactly one initialised HIP/HSA runtime.
