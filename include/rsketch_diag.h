@@ -48,6 +48,8 @@ const char *rsk_diag_last_error(void);
  *                 workgroup per CU)
  *   io_trace      1: the batched export / import print their host phase times to stderr
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
+ *   route_vranks  TEST ONLY, 1-rank communicator: rsk_hll_add_grouped_routed plans as rank route_vrank of
+ *   route_vrank   route_vranks (its owned sub-range; records for the other owners are dropped)
  *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
  *                 leaves unwritten then corrupts a register: the tests' hole check)
  *   gpart_dbg     TIMING ONLY (the grouped add stops before its apply): bit 0 the fine-bin pass
@@ -79,6 +81,13 @@ int rsk_diag_mark_dead(rsk_ctx *ctx);
  * bytes, one dword per lane (FETCH_SIZE calibration of 4-byte loads).
  * *ms = device time of the one launch. */
 int rsk_diag_membench(rsk_ctx *ctx, int mode, void *dev_buf, uint64_t bytes, uint64_t n_ops, double *ms);
+
+/* Self send/recv of `bytes` (a multiple of 8) of a known pattern through the context's 1-rank
+ * communicator, then a device compare (rsk_diag_p2p.hip): mode 0 one ncclSend/ncclRecv of bytes
+ * ncclUint8 elements, mode 1 one of bytes/8 ncclUint64 elements, mode 2 pieces of <= 1 GiB
+ * (the library's p2p_pieces).  bad_words: 4-byte words that differ; first_bad: the lowest one
+ * (~0 if none). */
+int rsk_diag_p2p_probe(rsk_ctx *ctx, uint64_t bytes, int mode, uint64_t *bad_words, uint64_t *first_bad);
 /* Time one launch of a tuning variant of the 16-byte PFADD kernel (slabs only). */
 int rsk_diag_hll_variant(rsk_ctx *ctx, int variant, const void *dev_keys16, uint64_t n, double *ms);
 /* Time one launch of a variant of the blob+offsets PFADD kernel (slabs only):

@@ -186,6 +186,7 @@ DIAG_SIGNATURES = {
     "rsk_diag_reply_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "rsk_diag_mark_dead": (ctypes.c_int, [_vp]),
     "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
+    "rsk_diag_p2p_probe": (ctypes.c_int, [_vp, _u64, ctypes.c_int, _P(_u64), _P(_u64)]),
     "rsk_diag_hll_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _P(ctypes.c_double)]),
     "rsk_diag_bloom_contains_variant": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _u64, _vp,
                                                        _P(ctypes.c_double)]),

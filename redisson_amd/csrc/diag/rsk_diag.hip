@@ -197,6 +197,8 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "gpart_tm") t.gpart_tm = (int)value;
     else if (k == "gpart_poison") t.gpart_poison = (int)value;
     else if (k == "gpart_tile") t.gpart_tile = (int)value;
+    else if (k == "route_vranks") t.route_vranks = (int)value;
+    else if (k == "route_vrank") t.route_vrank = (int)value;
     else if (k == "gapply_st") t.gapply_st = (int)value;
     else if (k == "gpart_rt") t.gpart_rt = (int)value;
     else if (k == "io_trace") t.io_trace = (int)value;

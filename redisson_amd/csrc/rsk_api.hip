@@ -484,8 +484,8 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
 void check_hll(const rsk_hll* h, uint64_t id) {
   need(h != nullptr, "hll handle is NULL");
   need(id < h->n, "sketch id out of range");
-  CtxLock l(h->ctx);         // the pool's host state is the context's
-  rsk::hll_materialize(h);  // every caller reads or writes registers
+  CtxLock l(h->ctx);                   // the pool's host state is the context's
+  rsk::hll_materialize_ids(h, &id, 1);  // every caller reads or writes this row's registers
   rsk::hll_touch(h);        // conservatively: every caller may write them
 }
 
@@ -498,7 +498,8 @@ void check_hll_ids(const rsk_hll* h, const uint64_t* a, uint64_t na, const uint6
   for (uint64_t i = 0; i < nb; ++i) bad |= b[i] >= h->n;
   need(!bad, "sketch id out of range");
   CtxLock l(h->ctx);
-  rsk::hll_materialize(h);
+  rsk::hll_materialize_ids(h, a, na);  // the rows these calls read or write (a partial lazy clear)
+  if (nb) rsk::hll_materialize_ids(h, b, nb);
   rsk::hll_touch(h);
 }
 
@@ -647,14 +648,107 @@ void stop_done(rsk_ctx* c) {
 
 }  // namespace
 
+namespace {
+// Rows of a partial lazy clear, zeroed by id: one workgroup per row, 16-byte stores.
+__global__ __launch_bounds__(256) void zero_rows_kernel(uint4* __restrict__ pool, const uint64_t* __restrict__ ids,
+                                                        uint64_t n) {
+  constexpr uint32_t ROW_U4 = rsk::HLL_REGS / 16;
+  for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    uint4* dst = pool + ids[r] * ROW_U4;
+    for (uint32_t q = threadIdx.x; q < ROW_U4; q += 256) dst[q] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// Zero the given pending rows (ascending), clear their flags, and wait: runs
+// of consecutive rows by memset when there are few, a row list otherwise (in a
+// buffer of its own: the caller may hold the context's scratch).
+void zero_pending_rows(const rsk_hll* h, const std::vector<uint64_t>& rows) {
+  if (rows.empty()) return;
+  rsk_ctx* c = h->ctx;
+  rsk::ProfScope ps(c, "hll_clear");
+  std::vector<std::pair<uint64_t, uint64_t>> runs;
+  for (uint64_t id : rows) {
+    if (!runs.empty() && runs.back().first + runs.back().second == id) ++runs.back().second;
+    else runs.push_back({id, 1});
+  }
+  if (runs.size() <= 64) {
+    for (const auto& r : runs)
+      RSK_HIP(hipMemsetAsync(h->d_regs + r.first * (uint64_t)rsk::HLL_REGS, 0, r.second * (uint64_t)rsk::HLL_REGS,
+                             c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  } else {
+    uint64_t* d_ids = nullptr;
+    RSK_HIP(hipMalloc(&d_ids, 8 * rows.size()));
+    struct Free {
+      uint64_t* p;
+      ~Free() { (void)hipFree(p); }
+    } fr{d_ids};
+    RSK_HIP(hipMemcpyAsync(d_ids, rows.data(), 8 * rows.size(), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((uint32_t)std::min<uint64_t>(rows.size(), 1u << 16)), dim3(256), 0,
+                       c->stream, reinterpret_cast<uint4*>(h->d_regs), d_ids, (uint64_t)rows.size());
+    RSK_CHECK_LAUNCH("zero_rows");
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  }
+  for (uint64_t id : rows) h->pend[id] = 0;
+  h->pend_n -= rows.size();
+  rsk::hll_touch(h);
+}
+}  // namespace
+
 namespace rsk {
 void hll_materialize(const rsk_hll* h) {
+  if (h->pend_n) {
+    CtxLock l(h->ctx);
+    std::vector<uint64_t> rows;
+    rows.reserve(h->pend_n);
+    for (uint64_t g = 0; g < h->n; ++g)
+      if (h->pend[g]) rows.push_back(g);
+    zero_pending_rows(h, rows);
+    return;
+  }
   if (!h->pending_clear) return;
   CtxLock l(h->ctx);
   ProfScope ps(h->ctx, "hll_clear");
   RSK_HIP(hipMemsetAsync(h->d_regs, 0, h->n * (uint64_t)HLL_REGS, h->ctx->stream));
   h->pending_clear = false;
   hll_touch(h);
+}
+
+void hll_materialize_ids(const rsk_hll* h, const uint64_t* ids, uint64_t n) {
+  if (h->pending_clear) return hll_materialize(h);
+  if (!h->pend_n) return;
+  CtxLock l(h->ctx);
+  std::vector<uint64_t> rows;
+  for (uint64_t i = 0; i < n; ++i)
+    if (ids[i] < h->n && h->pend[ids[i]]) rows.push_back(ids[i]);
+  std::sort(rows.begin(), rows.end());
+  rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+  zero_pending_rows(h, rows);
+}
+
+void hll_materialize_range(const rsk_hll* h, uint64_t first, uint64_t count) {
+  if (h->pending_clear) return hll_materialize(h);
+  if (!h->pend_n) return;
+  CtxLock l(h->ctx);
+  std::vector<uint64_t> rows;
+  for (uint64_t g = first; g < first + count && g < h->n; ++g)
+    if (h->pend[g]) rows.push_back(g);
+  zero_pending_rows(h, rows);
+}
+
+void hll_pend_outside(const rsk_hll* h, uint64_t first, uint64_t count) {
+  h->pend.assign(h->n, 1);
+  std::fill(h->pend.begin() + first, h->pend.begin() + first + count, 0);
+  h->pend_n = h->n - count;
+}
+
+void hll_unpend(const rsk_hll* h, const uint64_t* ids, uint64_t n) {
+  if (!h->pend_n) return;
+  for (uint64_t i = 0; i < n; ++i)
+    if (h->pend[ids[i]]) {
+      h->pend[ids[i]] = 0;
+      --h->pend_n;
+    }
 }
 
 void hll_touch(const rsk_hll* h) {
@@ -905,7 +999,9 @@ int rsk_hll_clear(rsk_hll* h) {
     }
     std::fill(h->exists.begin(), h->exists.end(), 0);
     std::fill(h->dense.begin(), h->dense.end(), 0);
-    h->pending_clear = true;
+    h->pending_clear = true;  // the whole pool: supersedes any partially pending rows
+    h->pend.clear();
+    h->pend_n = 0;
     h->zero = true;
   });
 }
@@ -1081,7 +1177,8 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
     need(h != nullptr && out != nullptr, "NULL argument");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    hll_materialize(h);
+    if (ids) hll_materialize_ids(h, ids, n);
+    else hll_materialize(h);
     if (n == 0) return;
     uint64_t* d_ids = nullptr;
     SmallIds small{};
@@ -1635,6 +1732,10 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
         }
     });
     need(bad_off.load() == ~0ull, "offsets must be non-decreasing");
+    rsk_ctx* c = h->ctx;
+    // held from the pending-clear completion through the kernels: an rsk_hll_clear
+    // from another thread in between would otherwise zero the imported rows later
+    CtxLock l(c);
     check_hll_ids(h, ids, n);
     // isHLLObjectOrReply per string (as rsk_hll_import_redis), on the host: header, magic,
     // encoding, exact dense length; the sparse opcodes are checked on the device.  One pass
@@ -1676,8 +1777,6 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
           apply[i] = 1;
         }
     }
-    rsk_ctx* c = h->ctx;
-    CtxLock l(c);
     const uint64_t base = offsets[0], total = offsets[n] - base;
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
     uint8_t* w = c->work(al(8 * n) + al(8 * (n + 1)) + 2 * al(n) + 256 + al(total) + 256);
@@ -2459,7 +2558,7 @@ int rsk_hll_count_ids_async(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_
     const uint64_t ib = ids ? al256(8 * n) : 0, ob = al256(8 * n);
     AsyncOp* op = op_get(c, ib + ob, ib + ob);
     try {
-      hll_materialize(h);
+      if (!ids) hll_materialize(h);  // (listed ids: check_hll_ids above)
       if (n) {
         uint64_t* d_ids = nullptr;
         if (ids) {

@@ -305,7 +305,14 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     rsk_ctx* c = h->ctx;
     Lock l(c);
     ncclComm_t comm = comm_of(c);
-    const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank;
+    // TEST ONLY (route route_vranks, 1-rank communicator): plan as rank route_vrank of
+    // route_vranks -- its owned sub-range, records for other owners dropped, as if every
+    // other rank held no pairs -- so one GPU exercises the sub-range offsets
+    const bool virt = c->nranks == 1 && c->tune.route_vranks > 1;
+    const uint64_t N = virt ? (uint64_t)c->tune.route_vranks : (uint64_t)c->nranks;
+    const uint64_t r = virt ? (uint64_t)c->tune.route_vrank : (uint64_t)c->rank;
+    need(r < N, "route_vrank outside route_vranks");
+    auto peer = [&](uint64_t j) { return virt ? 0 : (int)j; };  // the communicator rank of plan rank j
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
     auto on_gpu = [&](const void* p) {
       hipPointerAttribute_t a{};
@@ -377,28 +384,50 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
       rsk::ProfScope ps(c, "hll_route_counts");
       RSK_NCCL(ncclGroupStart());
       for (uint64_t j = 0; j < N; ++j) {
-        if (j == r && !self) continue;
-        RSK_NCCL(ncclSend(d_scnt + j, 1, ncclUint64, (int)j, comm, c->stream));
-        RSK_NCCL(ncclRecv(d_rcnt + j, 1, ncclUint64, (int)j, comm, c->stream));
+        if ((j == r && !self) || (virt && j != r)) continue;
+        RSK_NCCL(ncclSend(d_scnt + j, 1, ncclUint64, peer(j), comm, c->stream));
+        RSK_NCCL(ncclRecv(d_rcnt + j, 1, ncclUint64, peer(j), comm, c->stream));
       }
       RSK_NCCL(ncclGroupEnd());
     }
     RSK_HIP(hipMemcpyAsync(scnt.data() + N, d_rcnt, 8 * N, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
+    if (virt)
+      for (uint64_t j = 0; j < N; ++j)
+        if (j != r) scnt[N + j] = 0;
     if (!self) scnt[N + r] = scnt[r];
     uint64_t n_in = 0;
     for (uint64_t j = 0; j < N; ++j) n_in += scnt[N + j];
     // 3. the records: my run for rank j to j, j's run for me into the receive buffer (in rank order)
     uint64_t s0 = 0;
     for (uint64_t j = 0; j < r; ++j) s0 += scnt[j];
-    uint2* d_recv = reinterpret_cast<uint2*>(c->xbuf(8 * std::max<uint64_t>(n_in, 1)));
+    // The receive buffer may fail to allocate on one rank only: every rank learns of it
+    // (one more MAX all-reduce) before any record moves, so none waits in the exchange.
+    uint2* d_recv = nullptr;
+    int alloc_code = RSK_OK;
+    std::string alloc_msg;
+    try {
+      d_recv = reinterpret_cast<uint2*>(c->xbuf(8 * std::max<uint64_t>(n_in, 1)));
+    } catch (const RskError& e) {
+      alloc_code = e.code;
+      alloc_msg = e.msg;
+    }
+    h_meta[0] = alloc_code == RSK_OK ? 0 : 1;
+    RSK_HIP(hipMemcpyAsync(d_meta, h_meta, 8, hipMemcpyHostToDevice, c->stream));
+    RSK_NCCL(ncclAllReduce(d_meta, d_meta, 1, ncclUint64, ncclMax, comm, c->stream));
+    RSK_HIP(hipMemcpyAsync(h_meta, d_meta, 8, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    if (alloc_code != RSK_OK) throw RskError{alloc_code, "rsk_hll_add_grouped_routed: receive buffer: " + alloc_msg};
+    if (h_meta[0] != 0)
+      throw RskError{RSK_ERR_OUT_OF_MEMORY, "rsk_hll_add_grouped_routed: another rank could not allocate its receive "
+                                            "buffer"};
     {
       rsk::ProfScope ps(c, "hll_route_exchange");
       RSK_NCCL(ncclGroupStart());
       for (uint64_t j = 0, so = 0, ro = 0; j < N; so += scnt[j], ro += scnt[N + j], ++j) {
-        if (j == r && !self) continue;
-        p2p_pieces(d_send + so, scnt[j] * 8, (int)j, comm, c->stream, true);
-        p2p_pieces(d_recv + ro, scnt[N + j] * 8, (int)j, comm, c->stream, false);
+        if ((j == r && !self) || (virt && j != r)) continue;
+        p2p_pieces(d_send + so, scnt[j] * 8, peer(j), comm, c->stream, true);
+        p2p_pieces(d_recv + ro, scnt[N + j] * 8, peer(j), comm, c->stream, false);
       }
       RSK_NCCL(ncclGroupEnd());
     }
@@ -407,13 +436,17 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
       for (uint64_t j = 0; j < r; ++j) ro += scnt[N + j];
       RSK_HIP(hipMemcpyAsync(d_recv + ro, d_send + s0, scnt[r] * 8, hipMemcpyDeviceToDevice, c->stream));
     }
-    // 4. the owned rows [first, first + count): a pending lazy clear is completed on them by
-    // the add (every owned row written); rows outside stay as they were
+    // 4. the owned rows [first, first + count): a pending lazy clear of the whole pool is
+    // completed on them by the add (every owned row written) and stays pending on every
+    // other row (hll_pend_outside: they read as cleared and are zeroed before any other
+    // access); owned rows a partial clear left pending are zeroed first
     rsk::hll_forget_imports(h);
-    const bool pool_zero = h->zero;
     const bool write_all = h->pending_clear;
+    if (!write_all) rsk::hll_materialize_range(h, first, count);
+    const bool pool_zero = h->zero;
     rsk::hll_touch(h);
     h->pending_clear = false;
+    if (write_all && count < h->n) rsk::hll_pend_outside(h, first, count);
     rsk::hll_add_grouped_recs_launch(c, d_recv, n_in, h->d_regs + first * (uint64_t)rsk::HLL_REGS, count, pool_zero,
                                      write_all,
                                      rsk::PCount{h->d_pcount + first, h->d_pepoch + first, h->pc_epoch});
@@ -431,11 +464,15 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
     need(h != nullptr, "NULL handle");  // no communicator to agree through without one
     rsk_ctx* c = h->ctx;
     Lock l(c);
-    rsk::hll_materialize(h);
-    rsk::hll_touch(h);
-    rsk::hll_forget_imports(h);
     ncclComm_t comm = comm_of(c);
     const uint64_t N = (uint64_t)c->nranks, r = (uint64_t)c->rank, R = rsk::HLL_REGS;
+    {  // peers ask only for owned rows (the shared plan); fetched rows are overwritten whole
+      uint64_t f0, fc;
+      rsk::plan_owned_range(h->n, N, r, &f0, &fc);
+      rsk::hll_materialize_range(h, f0, fc);
+    }
+    rsk::hll_touch(h);
+    rsk::hll_forget_imports(h);
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
     // Local argument errors (NULL ids, unknown flags, an id outside the pool)
     // are not thrown here: they go into the agreed "bad" word below, so no
@@ -495,8 +532,8 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
     rsk::ProfScope ps(c, "hll_fetch_rows");
     RSK_NCCL(ncclGroupStart());  // the ids each owner must ship
     for (uint64_t j = 0, so = 0, ro = 0; j < N; so += cnt[j], ro += cnt[N + j], ++j) {
-      if (cnt[j]) RSK_NCCL(ncclSend(d_want + so, cnt[j], ncclUint64, (int)j, comm, c->stream));
-      if (cnt[N + j]) RSK_NCCL(ncclRecv(d_in + ro, cnt[N + j], ncclUint64, (int)j, comm, c->stream));
+      p2p_pieces(d_want + so, cnt[j] * 8, (int)j, comm, c->stream, true);
+      p2p_pieces(d_in + ro, cnt[N + j] * 8, (int)j, comm, c->stream, false);
     }
     RSK_NCCL(ncclGroupEnd());
     if (n_in) {
@@ -517,6 +554,7 @@ int rsk_hll_fetch_rows_flags(rsk_hll* h, const uint64_t* ids, uint64_t n, uint32
                          reinterpret_cast<const uint4*>(rows_recv));
       RSK_CHECK_LAUNCH("scatter_rows");
       for (uint64_t id : want) h->exists[id] = h->dense[id] = 1;
+      rsk::hll_unpend(h, want.data(), want.size());  // written whole: no longer pending clear
     }
     RSK_HIP(hipStreamSynchronize(c->stream));
   });

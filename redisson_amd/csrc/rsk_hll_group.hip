@@ -1473,6 +1473,12 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& keys, const uint32_t
 //   route_scatter : block b hashes its pairs again and appends each to owner
 //                   o's run at off[o * B + b] (one LDS cursor per owner; wave-
 //                   aggregated: one atomic per owner present in the wave)
+// Heavy groups (skew, VERDICT r05: at Zipf(1.1) the lowest 1/8 of the ids hold
+// 93 % of the pairs, all owned by rank 0) are pre-combined where the pairs are:
+// with slot_of (slot of each heavy group, ~0 for the others) their pairs go to
+// an extra run o = N as records {slot, index << 6 | rank}, which the rank folds
+// into one local 16 KiB row per heavy group; the rows, not the records, go to
+// the owners (rsk_comm.hip).
 constexpr uint32_t RT_T = 256;
 constexpr uint32_t RT_MAXN = 64;  // ranks
 
@@ -1482,18 +1488,21 @@ RSK_DEV uint32_t route_owner(uint32_t g, uint64_t q, uint32_t N) {
 
 __global__ __launch_bounds__(RT_T) void hll_route_count_kernel(const uint32_t* __restrict__ groups, uint64_t n,
                                                                uint64_t per, uint64_t G, uint32_t N,
+                                                               const uint32_t* __restrict__ slot_of,
                                                                uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t h[RT_MAXN];
-  if (threadIdx.x < RT_MAXN) h[threadIdx.x] = 0;
+  __shared__ uint32_t h[RT_MAXN + 1];
+  const uint32_t NO = N + (slot_of ? 1u : 0u);  // owners + the heavy run
+  if (threadIdx.x < NO) h[threadIdx.x] = 0;
   __syncthreads();
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
   const uint64_t q = G / N;
-  uint32_t mine[RT_MAXN > 8 ? 8 : RT_MAXN] = {};  // lane-private counts for the first 8 owners
+  uint32_t mine[8] = {};  // lane-private counts for the first 8 owners
   for (uint64_t i = begin + threadIdx.x; i < end; i += RT_T) {
     const uint32_t g = __builtin_nontemporal_load(&groups[i]);
     if (g >= G) continue;
-    const uint32_t o = route_owner(g, q, N);
+    uint32_t o = route_owner(g, q, N);
+    if (slot_of && slot_of[g] != 0xFFFFFFFFu) o = N;
     if (o < 8) {
 #pragma unroll
       for (uint32_t k = 0; k < 8; ++k) mine[k] += o == k;
@@ -1503,18 +1512,20 @@ __global__ __launch_bounds__(RT_T) void hll_route_count_kernel(const uint32_t* _
   }
 #pragma unroll
   for (uint32_t k = 0; k < 8; ++k)
-    if (k < N && mine[k]) atomicAdd(&h[k], mine[k]);
+    if (k < NO && mine[k]) atomicAdd(&h[k], mine[k]);
   __syncthreads();
-  if (threadIdx.x < N) cnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+  if (threadIdx.x < NO) cnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
 __global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __restrict__ keys,
                                                                  const uint32_t* __restrict__ groups, uint64_t n,
                                                                  uint64_t per, uint64_t G, uint32_t N,
+                                                                 const uint32_t* __restrict__ slot_of,
                                                                  const uint64_t* __restrict__ off,
                                                                  uint2* __restrict__ out) {
-  __shared__ unsigned long long cur[RT_MAXN];
-  if (threadIdx.x < N) cur[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  __shared__ unsigned long long cur[RT_MAXN + 1];
+  const uint32_t NO = N + (slot_of ? 1u : 0u);
+  if (threadIdx.x < NO) cur[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
@@ -1533,6 +1544,13 @@ __global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __
       ir = (hll_index(hsh) << 6) | hll_rank(hsh);
       o = route_owner(g, q, N);
       gl = (uint32_t)(g - (uint64_t)o * q);
+      if (slot_of) {
+        const uint32_t sl = slot_of[g];
+        if (sl != 0xFFFFFFFFu) {
+          o = N;
+          gl = sl;
+        }
+      }
     }
     uint64_t pending = __ballot(valid);
     while (pending) {  // one atomic per owner present in the wave
@@ -1545,6 +1563,48 @@ __global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __
       if (valid && o == oo) out[base + (uint64_t)__popcll(m & lt)] = make_uint2(gl, ir);
       pending &= ~m;
     }
+  }
+}
+
+// Heavy-group detection: a sampled count per group (every stride-th pair of each
+// block's range; one atomic per distinct group in a wave, so a hot group costs
+// one atomic per wave, not one per pair), then flags, an exclusive scan (slots in
+// group order, so each owner's heavy rows are one contiguous range) and the slots.
+__global__ __launch_bounds__(RT_T) void hll_route_sample_kernel(const uint32_t* __restrict__ groups, uint64_t n,
+                                                                uint64_t per, uint64_t G, uint32_t stride,
+                                                                uint32_t* __restrict__ hist) {
+  uint64_t begin, end;
+  key_range(n, per, &begin, &end);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t i0 = begin; i0 < end; i0 += (uint64_t)RT_T * stride) {  // block-uniform trip count
+    const uint64_t i = i0 + (uint64_t)threadIdx.x * stride;
+    const uint32_t g = i < end ? groups[i] : 0xFFFFFFFFu;
+    const bool valid = g < G;
+    uint64_t pending = __ballot(valid);
+    while (pending) {
+      const uint32_t gg = (uint32_t)__builtin_amdgcn_readlane((int)g, __builtin_ctzll(pending));
+      const uint64_t m = __ballot(valid && g == gg) & pending;
+      if ((int)lane == __builtin_ctzll(m)) atomicAdd(&hist[gg], (uint32_t)__popcll(m));
+      pending &= ~m;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void hll_heavy_flag_kernel(const uint32_t* __restrict__ hist, uint64_t G,
+                                                             uint32_t thr, uint32_t* __restrict__ flag) {
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += (uint64_t)gridDim.x * blockDim.x)
+    flag[g] = g < G && hist[g] >= thr ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void hll_heavy_slot_kernel(const uint32_t* __restrict__ hist,
+                                                             const uint32_t* __restrict__ pos, uint64_t G, uint32_t thr,
+                                                             uint32_t cap, uint32_t* __restrict__ slot_of,
+                                                             uint32_t* __restrict__ heavy_ids) {
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = pos[g];
+    const bool hv = hist[g] >= thr && p < cap;
+    slot_of[g] = hv ? p : 0xFFFFFFFFu;
+    if (hv) heavy_ids[p] = (uint32_t)g;
   }
 }
 
@@ -1569,22 +1629,69 @@ __global__ __launch_bounds__(256) void hll_add_grouped_rec_kernel(const uint2* _
 uint32_t route_blocks(const rsk_ctx* c) { return (uint32_t)c->num_cus * 4; }
 
 void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N,
-                            uint32_t* d_cnt) {
+                            const uint32_t* d_slot_of, uint32_t* d_cnt) {
   const uint32_t B = route_blocks(c);
   const uint64_t per = (n + B - 1) / B;
   ProfScope ps(c, "hll_route");
-  hipLaunchKernelGGL(hll_route_count_kernel, dim3(B), dim3(RT_T), 0, c->stream, d_groups, n, per, G, N, d_cnt);
+  hipLaunchKernelGGL(hll_route_count_kernel, dim3(B), dim3(RT_T), 0, c->stream, d_groups, n, per, G, N, d_slot_of,
+                     d_cnt);
   RSK_CHECK_LAUNCH("hll_route_count");
 }
 
 void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
-                              uint32_t N, const uint64_t* d_off, uint2* d_out) {
+                              uint32_t N, const uint32_t* d_slot_of, const uint64_t* d_off, uint2* d_out) {
   const uint32_t B = route_blocks(c);
   const uint64_t per = (n + B - 1) / B;
   ProfScope ps(c, "hll_route");
   hipLaunchKernelGGL(hll_route_scatter_kernel, dim3(B), dim3(RT_T), 0, c->stream,
-                     reinterpret_cast<const uint4*>(d_keys16), d_groups, n, per, G, N, d_off, d_out);
+                     reinterpret_cast<const uint4*>(d_keys16), d_groups, n, per, G, N, d_slot_of, d_off, d_out);
   RSK_CHECK_LAUNCH("hll_route_scatter");
+}
+
+uint64_t hll_heavy_scratch_bytes(uint64_t G, uint32_t cap) {
+  size_t sb = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(G + 1),
+                                         (hipStream_t)0);
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  return al(4 * G) + 2 * al(4 * (G + 1)) + al(4ull * cap) + al(sb);
+}
+
+uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t stride, uint32_t thr,
+                          uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of, std::vector<uint32_t>* heavy_ids) {
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* pos = reinterpret_cast<uint32_t*>(scratch + al(4 * G));
+  uint32_t* slot = reinterpret_cast<uint32_t*>(scratch + al(4 * G) + al(4 * (G + 1)));
+  uint32_t* ids = reinterpret_cast<uint32_t*>(scratch + al(4 * G) + 2 * al(4 * (G + 1)));
+  uint8_t* tmp = scratch + al(4 * G) + 2 * al(4 * (G + 1)) + al(4ull * cap);
+  size_t sb = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(G + 1),
+                                         c->stream);
+  const uint32_t B = route_blocks(c);
+  const uint64_t per = (n + B - 1) / B;
+  const uint32_t gb = (uint32_t)std::min<uint64_t>((G + 256) / 256, 4096);
+  {
+    ProfScope ps(c, "hll_route_heavy");
+    RSK_HIP(hipMemsetAsync(hist, 0, 4 * G, c->stream));
+    hipLaunchKernelGGL(hll_route_sample_kernel, dim3(B), dim3(RT_T), 0, c->stream, d_groups, n, per, G, stride, hist);
+    RSK_CHECK_LAUNCH("hll_route_sample");
+    hipLaunchKernelGGL(hll_heavy_flag_kernel, dim3(gb), dim3(256), 0, c->stream, hist, G, thr, pos);
+    RSK_CHECK_LAUNCH("hll_heavy_flag");
+    RSK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, sb, pos, pos, (int)(G + 1), c->stream));
+    hipLaunchKernelGGL(hll_heavy_slot_kernel, dim3(gb), dim3(256), 0, c->stream, hist, pos, G, thr, cap, slot, ids);
+    RSK_CHECK_LAUNCH("hll_heavy_slot");
+  }
+  uint32_t total = 0;
+  RSK_HIP(hipMemcpyAsync(&total, pos + G, 4, hipMemcpyDeviceToHost, c->stream));
+  RSK_HIP(hipStreamSynchronize(c->stream));
+  const uint64_t H = std::min<uint64_t>(total, cap);
+  heavy_ids->resize(H);
+  if (H) {
+    RSK_HIP(hipMemcpyAsync(heavy_ids->data(), ids, 4 * H, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipStreamSynchronize(c->stream));
+  }
+  *d_slot_of = slot;
+  return H;
 }
 
 void hll_add_grouped_recs_launch(rsk_ctx* c, const uint2* d_recs, uint64_t n, uint8_t* d_regs, uint64_t G,

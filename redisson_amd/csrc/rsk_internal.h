@@ -71,6 +71,8 @@ struct Tuning {
   int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B)
   int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no
   int gpart_tile = 0;        // its tile-major first pass: 0 8192-record tiles (2 x 256 lanes per CU), 1 16384 (512 lanes)
+  int route_vranks = 0;      // TEST ONLY, 1-rank communicator: the routed grouped add plans as rank route_vrank of
+  int route_vrank = 0;       // route_vranks (its owned sub-range; records of other owners dropped)
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the
@@ -233,6 +235,15 @@ struct rsk_hll {
   // that rewrites every row anyway (hll_gapply with write_all), or by
   // hll_materialize before any other access.
   mutable bool pending_clear = false;
+  // Part of a lazy clear still pending, per row: after a clear, the routed
+  // grouped add (rsk_comm.hip) writes only the rank's owned rows, so every
+  // other row keeps its old registers until it is zeroed here (pend[g] = 1:
+  // row g reads as cleared; zeroed by hll_materialize, or by
+  // hll_materialize_ids / _range for the rows a call touches, or dropped when
+  // a row is overwritten whole, as rsk_hll_fetch_rows does).  pending_clear
+  // (the whole pool) and pend_n > 0 are never both set.
+  mutable std::vector<uint8_t> pend;
+  mutable uint64_t pend_n = 0;
   // PFCOUNT precomputed by the partitioned grouped add (hll_gapply estimates
   // every row it writes, from LDS): d_pcount[g] is valid while d_pepoch[g] ==
   // pc_epoch.  Every entry point that may write registers bumps pc_epoch
@@ -362,15 +373,33 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d
 // per-block owner counts cnt[o * B + b] (B = route_blocks), then the pairs
 // hashed into 8-byte records appended to owner o's run at off[o * B + b].
 uint32_t route_blocks(const rsk_ctx* c);
-void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N, uint32_t* d_cnt);
+void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N,
+                            const uint32_t* d_slot_of, uint32_t* d_cnt);
 void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
-                              uint32_t N, const uint64_t* d_off, uint2* d_out);
+                              uint32_t N, const uint32_t* d_slot_of, const uint64_t* d_off, uint2* d_out);
+// Heavy groups of a routed add (skew): sampled counts (every stride-th pair), a
+// group is heavy when its sample count reaches thr; at most cap, by group id.
+// scratch: hll_heavy_scratch_bytes(G, cap) of device memory; *d_slot_of points
+// into it (a group's slot, ~0 if light), heavy_ids gets the heavy groups
+// ascending (slot order).  Returns their number; synchronises the stream.
+uint64_t hll_heavy_scratch_bytes(uint64_t G, uint32_t cap);
+uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t stride, uint32_t thr,
+                          uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of, std::vector<uint32_t>* heavy_ids);
 // Records into a pool of G rows (partitioned for large batches, else a CAS each);
 // write_all: every row written (zero rows for sketches without records).
 void hll_add_grouped_recs_launch(rsk_ctx* c, const uint2* d_recs, uint64_t n, uint8_t* d_regs, uint64_t G,
                                  bool pool_zero, bool write_all, PCount pc);
 // Performs a pending lazy clear (rsk_api.hip).
 void hll_materialize(const rsk_hll* h);
+// The rows among ids[0..n) / [first, first + count) that a partial lazy clear
+// left pending are zeroed (and the stream synchronised); a whole-pool pending
+// clear is completed as by hll_materialize.
+void hll_materialize_ids(const rsk_hll* h, const uint64_t* ids, uint64_t n);
+void hll_materialize_range(const rsk_hll* h, uint64_t first, uint64_t count);
+// Rows [first, first + count) hold data, every other row is pending clear.
+void hll_pend_outside(const rsk_hll* h, uint64_t first, uint64_t count);
+// Rows overwritten whole (no longer pending).
+void hll_unpend(const rsk_hll* h, const uint64_t* ids, uint64_t n);
 void bloom_add_each_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k, uint8_t* d_out);
 // add() replies (RedissonBloomFilter.java:100-107) + the insert, any batch size:
 // the partitioned first-probe pipeline (rsk_bloom_reply.hip) when it applies,

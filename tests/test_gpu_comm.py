@@ -266,3 +266,85 @@ def test_routed_add_c5_full_size_self_exchange(engine, orc):
         _lib.check(L.rsk_trim(engine.ctx))
     finally:
         _lib.check(L.rsk_comm_destroy(engine.ctx))
+
+
+def _all_rows(L, engine, pool, G):
+    """The whole pool as a [G][16384] host array (rsk_hll_device_registers first
+    completes any pending clear)."""
+    from redisson_amd import _lib
+
+    p = L.rsk_hll_device_registers(pool)
+    assert p
+    out = np.zeros((G, 16384), np.uint8)
+    _lib.check(L.rsk_memcpy(engine.ctx, out.ctypes.data, ctypes.c_void_p(p), out.size, 1))
+    return out
+
+
+@pytest.mark.parametrize("G,n,vrank", [(5000, 10_000, 1), (100_003, 5_000_000, 1), (100_003, 5_000_000, 2)])
+def test_routed_add_owned_subrange(engine, orc, route, G, n, vrank):
+    """the routed add on an owned SUB-range (rank vrank of 3, planned
+    on the 1-rank communicator by the route_vranks test route: records of the
+    other owners dropped): the owned rows equal the plain grouped add's (the
+    d_regs + first * 16384 and PCount offsets), and after a clear every row
+    outside the owned range reads as cleared -- per row (registers, PFCOUNT,
+    exists), through countWith / mergeWith members, through a fetch, and for the
+    whole pool -- never the registers it held before the clear."""
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    try:
+        groups, keys = orc.gen_grouped(0x5EED0006, G, 0, n)
+        kd = devmem.DeviceBuffer.from_numpy(engine, keys)
+        gd = devmem.DeviceBuffer.from_numpy(engine, groups)
+        kb = kd.keys_fixed(n, 16)
+        first, count = shard.owned_range(G, 3, vrank)
+        assert count > 0 and first > 0
+        a = GroupedHyperLogLog(engine, G)
+        b = GroupedHyperLogLog(engine, G)
+        b.clear()
+        b.add(kb, gd)  # reference: every row from the plain grouped add
+        ref = _all_rows(L, engine, b.pool, G)
+        a.add(kb, gd)  # a's rows all hold registers before the clear
+        a.clear()
+        route(route_vranks=3, route_vrank=vrank)
+        assert shard.hll_add_grouped_routed(a.pool, kb, gd, flags=_lib.RSK_FETCH_SELF) == (first, count)
+        out_lo, out_hi = first - 1, (first + count) % G  # rows just outside the owned range
+        for gid in (first, first + count - 1, first + count // 2):
+            assert np.array_equal(a.registers(gid), ref[gid]), gid
+        for gid in (0, out_lo, out_hi):
+            assert not a.registers(gid).any(), gid  # cleared, not the pre-clear registers
+            ex = ctypes.c_int()
+            _lib.check(L.rsk_hll_exists(a.pool, gid, ctypes.byref(ex)))
+            assert ex.value == 0
+        assert list(a.count(ids=[out_lo, first])) == [0, int(b.count(ids=[first])[0])]
+        # countWith of an owned row with a pending one = the owned row alone
+        cw = a.countWith(np.array([[first, out_hi]], np.uint64))
+        assert int(cw[0]) == int(b.count(ids=[first])[0])
+        # a second routed add onto the owned rows (pending rows elsewhere): re-adds change nothing
+        shard.hll_add_grouped_routed(a.pool, kb, gd)
+        assert np.array_equal(a.registers(first), ref[first])
+        # mergeWith into a pending row: the source's registers, not a max with stale ones
+        a.mergeWith(np.array([out_lo], np.uint64), np.array([first], np.uint64))
+        assert np.array_equal(a.registers(out_lo), ref[first])
+        route(route_vranks=0)
+        # a fetch (N = 1: every row owned) leaves the pending rows cleared too
+        shard.hll_fetch_rows(a.pool, [out_hi, first], flags=_lib.RSK_FETCH_SELF)
+        assert not a.registers(out_hi).any()
+        whole = _all_rows(L, engine, a.pool, G)
+        owned = np.zeros(G, bool)
+        owned[first:first + count] = True
+        assert np.array_equal(whole[owned], ref[owned])
+        rest = ~owned
+        rest[out_lo] = False  # the mergeWith destination
+        assert not whole[rest].any()
+        a.close()
+        b.close()
+        kd.free()
+        gd.free()
+    finally:
+        route(route_vranks=0)
+        _lib.check(L.rsk_comm_destroy(engine.ctx))
