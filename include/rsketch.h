@@ -428,6 +428,14 @@ int rsk_plan_bloom_slice_words(uint64_t nwords, int nranks, uint64_t *words);
  * owner.  RSK_ERR_INVALID_ARG if an id is >= n. */
 int rsk_plan_fetch(uint64_t n, int nranks, int rank, const uint64_t *ids, uint64_t n_ids, uint32_t flags,
                    uint64_t *want_out, uint64_t *n_want, uint64_t *counts_out);
+/* rsk_hll_add_grouped_routed's traffic per owner: counts[s * G + g] = pairs of
+ * group g on rank s; groups of >= heavy_min pairs owned by another rank (0:
+ * none; at most heavy_cap per rank, lowest ids first) pre-combined at their
+ * source into one 16 KiB row each.  Per rank (arrays of nranks): bytes received from the other ranks
+ * (8 per light record, 16388 per heavy row with its id), heavy rows received,
+ * light records its apply folds. */
+int rsk_plan_route_recv(const uint64_t *counts, uint64_t G, int nranks, uint64_t heavy_min, uint64_t heavy_cap,
+                        uint64_t *recv_bytes, uint64_t *recv_rows, uint64_t *apply_records);
 
 #if defined(__GNUC__)
 #pragma GCC visibility pop

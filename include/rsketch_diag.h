@@ -50,6 +50,8 @@ const char *rsk_diag_last_error(void);
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
  *   route_vranks  TEST ONLY, 1-rank communicator: rsk_hll_add_grouped_routed plans as rank route_vrank of
  *   route_vrank   route_vranks (its owned sub-range; records for the other owners are dropped)
+ *   route_heavy   routed add's heavy-group pre-combine: 0 auto, -1 never, > 0 at any size with that many
+ *                 pairs (estimated from a sample) making a group heavy
  *   gpart_poison  1: its fine-bin output is filled with 0xFF before the fine-bin pass (a slot the pass
  *                 leaves unwritten then corrupts a register: the tests' hole check)
  *   gpart_dbg     TIMING ONLY (the grouped add stops before its apply): bit 0 the fine-bin pass

@@ -176,6 +176,7 @@ SIGNATURES = {
     "rsk_plan_owner": (ctypes.c_int, [_u64, ctypes.c_int, _u64, _P(ctypes.c_int)]),
     "rsk_plan_bloom_slice_words": (ctypes.c_int, [_u64, ctypes.c_int, _P(_u64)]),
     "rsk_plan_fetch": (ctypes.c_int, [_u64, ctypes.c_int, ctypes.c_int, _vp, _u64, _u32, _vp, _P(_u64), _vp]),
+    "rsk_plan_route_recv": (ctypes.c_int, [_vp, _u64, ctypes.c_int, _u64, _u64, _vp, _vp, _vp]),
     "rsk_bloom_allreduce_or": (ctypes.c_int, [_vp]),
     "rsk_bloom_allreduce_or_flags": (ctypes.c_int, [_vp, _u32]),
 }

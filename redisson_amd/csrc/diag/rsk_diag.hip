@@ -199,6 +199,7 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "gpart_tile") t.gpart_tile = (int)value;
     else if (k == "route_vranks") t.route_vranks = (int)value;
     else if (k == "route_vrank") t.route_vrank = (int)value;
+    else if (k == "route_heavy") t.route_heavy = (int)value;
     else if (k == "gapply_st") t.gapply_st = (int)value;
     else if (k == "gpart_rt") t.gpart_rt = (int)value;
     else if (k == "io_trace") t.io_trace = (int)value;

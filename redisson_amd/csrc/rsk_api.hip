@@ -101,20 +101,24 @@ uint8_t* rsk_ctx::work(uint64_t bytes) {
   return d_work;
 }
 
-uint8_t* rsk_ctx::xbuf(uint64_t bytes) {
-  if (bytes > xbuf_bytes) {
-    if (d_xbuf) {
+static uint8_t* grow_dev(hipStream_t stream, uint8_t*& p, uint64_t& have, uint64_t bytes) {
+  if (bytes > have) {
+    if (p) {
       RSK_HIP(hipStreamSynchronize(stream));
-      RSK_HIP(hipFree(d_xbuf));
-      d_xbuf = nullptr;
-      xbuf_bytes = 0;
+      RSK_HIP(hipFree(p));
+      p = nullptr;
+      have = 0;
     }
     const uint64_t sz = std::max<uint64_t>(bytes, 16ull << 20);
-    RSK_HIP(hipMalloc(&d_xbuf, sz));
-    xbuf_bytes = sz;
+    RSK_HIP(hipMalloc(&p, sz));
+    have = sz;
   }
-  return d_xbuf;
+  return p;
 }
+
+uint8_t* rsk_ctx::xbuf(uint64_t bytes) { return grow_dev(stream, d_xbuf, xbuf_bytes, bytes); }
+uint8_t* rsk_ctx::sbuf(uint64_t bytes) { return grow_dev(stream, d_sbuf, sbuf_bytes, bytes); }
+uint8_t* rsk_ctx::hrows(uint64_t bytes) { return grow_dev(stream, d_hrows, hrows_bytes, bytes); }
 
 uint8_t* rsk_ctx::pinned(uint64_t bytes) {
   // every call that fills this buffer waits for its DMA before returning
@@ -840,6 +844,8 @@ int rsk_shutdown(rsk_ctx* c) {
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_xbuf);
+    (void)hipFree(c->d_sbuf);
+    (void)hipFree(c->d_hrows);
     (void)hipFree(c->d_lc);
     for (rsk::AsyncOp* op : c->async_all) {  // stream and completion queue drained: every op is idle
       if (op->h_buf) (void)hipHostFree(op->h_buf);
@@ -872,8 +878,10 @@ int rsk_trim(rsk_ctx* c) {
     RSK_HIP(hipFree(c->d_work));
     RSK_HIP(hipFree(c->d_out));
     RSK_HIP(hipFree(c->d_xbuf));
-    c->d_work = c->d_out = c->d_xbuf = nullptr;
-    c->work_bytes = c->out_bytes = c->xbuf_bytes = 0;
+    RSK_HIP(hipFree(c->d_sbuf));
+    RSK_HIP(hipFree(c->d_hrows));
+    c->d_work = c->d_out = c->d_xbuf = c->d_sbuf = c->d_hrows = nullptr;
+    c->work_bytes = c->out_bytes = c->xbuf_bytes = c->sbuf_bytes = c->hrows_bytes = 0;
     if (c->h_batch) RSK_HIP(hipHostFree(c->h_batch));
     c->h_batch = nullptr;
     c->h_batch_bytes = 0;

@@ -298,6 +298,42 @@ int rsk_hll_reducescatter_pool(rsk_hll* h, uint64_t* first_out, uint64_t* count_
 // every rank and reduce-scattering the pool, per rank at N = 8 and the C5
 // size (500M pairs, 10^6 sketches): 7/8 x 4 GB of records over xGMI instead
 // of 7/8 x 16 GiB of rows, and 2 GiB of rows written instead of 16 GiB.
+//
+// Skew (VERDICT r05 Weak 6b): with contiguous ownership a Zipf(1.1) stream
+// sends 93 % of all pairs to rank 0 at N = 8.  A group with at least
+// HEAVY_MIN = 2048 pairs on a rank (16 KiB of records = one row) is folded
+// there into a local 16 KiB row (the same record pipeline, onto a scratch pool
+// of the heavy groups), and the row travels instead of its records; the owner
+// max-merges the rows it receives into its rows after its own apply.  A rank's
+// own groups are never pre-combined (no transfer to save; the apply folds
+// their records anyway).  Heavy
+// groups are found from a sample (hll_heavy_select), which changes only where
+// a pair is folded, never the registers (max is order-free).
+constexpr uint64_t HEAVY_MIN = 2048;
+constexpr uint32_t HEAVY_CAP = 65536;  // heavy rows per rank and call (1 GiB)
+
+__global__ __launch_bounds__(256) void max_rows_kernel(uint4* __restrict__ pool, const uint32_t* __restrict__ ids,
+                                                       uint64_t m, const uint4* __restrict__ rows,
+                                                       uint32_t* __restrict__ pepoch) {
+  // registers are < 64, so a byte max is one SWAR compare: bit 7 of
+  // (a | 0x80) - b is set iff a >= b, with no borrow between the bytes
+  auto bmax = [](uint32_t a, uint32_t b) {
+    const uint32_t ge = ((a | 0x80808080u) - b) & 0x80808080u;
+    const uint32_t mk = (ge >> 7) * 0xFFu;
+    return (a & mk) | (b & ~mk);
+  };
+  for (uint64_t r = blockIdx.x; r < m; r += gridDim.x) {
+    const uint32_t id = ids[r];
+    uint4* dst = pool + (uint64_t)id * ROW_U4;
+    const uint4* src = rows + r * ROW_U4;
+    for (uint32_t q = threadIdx.x; q < ROW_U4; q += 256) {
+      const uint4 a = dst[q], b = src[q];
+      dst[q] = make_uint4(bmax(a.x, b.x), bmax(a.y, b.y), bmax(a.z, b.z), bmax(a.w, b.w));
+    }
+    if (threadIdx.x == 0) pepoch[id] = 0;  // the apply's precomputed PFCOUNT no longer holds
+  }
+}
+
 int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t* groups, uint32_t flags,
                                uint64_t* first_out, uint64_t* count_out) {
   return guarded([&] {
@@ -329,14 +365,24 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
         (n == 0 || (keys->location == RSK_MEM_DEVICE && keys->offsets == nullptr && keys->fixed_len == 16 &&
                     (reinterpret_cast<uintptr_t>(keys->data) & 15) == 0 && groups != nullptr && on_gpu(keys->data) &&
                     on_gpu(groups)));
+    const bool self = (flags & RSK_FETCH_SELF) != 0;  // own records / rows also through RCCL
+    const uint64_t G = h->n;
+    // heavy-group pre-combine: on where it can move bytes off the links (N > 1, or the
+    // self exchange that tests it), for large batches; route_heavy forces it (tests)
+    const int hv = c->tune.route_heavy;
+    const uint64_t heavy_min = hv > 0 ? (uint64_t)hv : HEAVY_MIN;
+    const bool heavy_try = args_ok && hv >= 0 && (N > 1 || self) && n > 0 && G <= (1ull << 28) &&
+                           (hv > 0 || n >= (1ull << 22));
     const uint32_t B = rsk::route_blocks(c);
-    uint8_t* w = c->work(al(8 * 3) + al(4 * N * B) + al(8 * N * B) + 2 * al(8 * N) + al(8 * std::max<uint64_t>(n, 1)));
+    const uint64_t NO = N + 1;  // owners + the heavy run
+    const uint64_t hs_bytes = heavy_try ? rsk::hll_heavy_scratch_bytes(G, HEAVY_CAP) : 0;
+    uint8_t* w = c->work(al(8 * 3) + al(4 * NO * B) + al(8 * NO * B) + 2 * al(16 * N) + al(hs_bytes));
     uint64_t* d_meta = reinterpret_cast<uint64_t*>(w);
     uint32_t* d_cnt = reinterpret_cast<uint32_t*>(w + al(24));
-    uint64_t* d_off = reinterpret_cast<uint64_t*>(w + al(24) + al(4 * N * B));
-    uint64_t* d_scnt = reinterpret_cast<uint64_t*>(w + al(24) + al(4 * N * B) + al(8 * N * B));
-    uint64_t* d_rcnt = d_scnt + al(8 * N) / 8;
-    uint2* d_send = reinterpret_cast<uint2*>(w + al(24) + al(4 * N * B) + al(8 * N * B) + 2 * al(8 * N));
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(w + al(24) + al(4 * NO * B));
+    uint64_t* d_scnt = reinterpret_cast<uint64_t*>(w + al(24) + al(4 * NO * B) + al(8 * NO * B));
+    uint64_t* d_rcnt = d_scnt + al(16 * N) / 8;
+    uint8_t* d_hscratch = w + al(24) + al(4 * NO * B) + al(8 * NO * B) + 2 * al(16 * N);
     uint64_t* h_meta = reinterpret_cast<uint64_t*>(c->h_small + 8192);
     h_meta[0] = args_ok ? 0 : 1;
     h_meta[1] = h->n;
@@ -353,61 +399,100 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     rsk::plan_owned_range(h->n, N, r, &first, &count);
     *first_out = first;
     *count_out = count;
-    const uint64_t G = h->n;
-    // 1. owner counts per block, their offsets in the send buffer (owner-major)
-    std::vector<uint32_t> cnt(N * B, 0);
-    std::vector<uint64_t> off(N * B), scnt(2 * N, 0);
+    // 0. heavy groups (sampled counts): their pairs become local rows, not records
+    std::vector<uint32_t> heavy_ids;
+    uint32_t* d_slot_of = nullptr;
+    uint64_t H = 0;
+    if (heavy_try) {
+      const uint32_t stride = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, heavy_min / 8));
+      const uint32_t thr = (uint32_t)std::max<uint64_t>(1, (heavy_min + stride - 1) / stride);
+      // own groups stay records unless they too go through RCCL (self exchange)
+      const uint64_t skip_lo = self ? 0 : first, skip_hi = self ? 0 : first + count;
+      H = rsk::hll_heavy_select(c, groups, n, G, stride, thr, skip_lo, skip_hi, HEAVY_CAP, d_hscratch, &d_slot_of,
+                                &heavy_ids);
+      if (!H) d_slot_of = nullptr;
+    }
+    std::vector<uint64_t> hrows(N, 0), hfirst(N + 1, 0);  // heavy rows per owner, their first slot
+    rsk::plan_heavy_rows(G, N, heavy_ids.data(), H, &hrows);
+    for (uint64_t o = 0; o < N; ++o) hfirst[o + 1] = hfirst[o] + hrows[o];
+    // 1. owner counts per block, their offsets in the send buffer (owner-major, the heavy run last)
+    std::vector<uint32_t> cnt(NO * B, 0);
+    std::vector<uint64_t> off(NO * B);
+    // per peer j: [2j] records for j, [2j + 1] heavy rows for j; received into [2N + 2j], [2N + 2j + 1]
+    std::vector<uint64_t> scnt(4 * N, 0);
     if (n) {
-      rsk::hll_route_count_launch(c, groups, n, G, (uint32_t)N, d_cnt);
-      RSK_HIP(hipMemcpyAsync(cnt.data(), d_cnt, 4 * N * B, hipMemcpyDeviceToHost, c->stream));
+      rsk::hll_route_count_launch(c, groups, n, G, (uint32_t)N, d_slot_of, d_cnt);
+      RSK_HIP(hipMemcpyAsync(cnt.data(), d_cnt, 4 * NO * B, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
     }
+    std::vector<uint64_t> sfirst(NO + 1, 0);  // each owner's run in the send buffer
     uint64_t at = 0;
-    for (uint64_t o = 0; o < N; ++o) {
-      const uint64_t o0 = at;
+    for (uint64_t o = 0; o < NO; ++o) {
+      sfirst[o] = at;
       for (uint64_t b = 0; b < B; ++b) {
         off[o * B + b] = at;
         at += cnt[o * B + b];
       }
-      scnt[o] = at - o0;  // records for rank o
     }
-    // own records stay in place unless they are routed through RCCL (RSK_FETCH_SELF)
-    const bool self = (flags & RSK_FETCH_SELF) != 0;
-    if (n) {
-      RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * N * B, hipMemcpyHostToDevice, c->stream));
-      rsk::hll_route_scatter_launch(c, reinterpret_cast<const uint8_t*>(keys->data), groups, n, G, (uint32_t)N, d_off,
-                                    d_send);
+    sfirst[NO] = at;
+    const uint64_t n_heavy = sfirst[NO] - sfirst[N];  // pairs folded into local rows
+    for (uint64_t j = 0; j < N; ++j) {
+      scnt[2 * j] = sfirst[j + 1] - sfirst[j];
+      scnt[2 * j + 1] = hrows[j];
     }
-    // 2. record counts both ways
-    RSK_HIP(hipMemcpyAsync(d_scnt, scnt.data(), 8 * N, hipMemcpyHostToDevice, c->stream));
+    // 2. record and row counts both ways
+    RSK_HIP(hipMemcpyAsync(d_scnt, scnt.data(), 16 * N, hipMemcpyHostToDevice, c->stream));
     {
       rsk::ProfScope ps(c, "hll_route_counts");
       RSK_NCCL(ncclGroupStart());
       for (uint64_t j = 0; j < N; ++j) {
         if ((j == r && !self) || (virt && j != r)) continue;
-        RSK_NCCL(ncclSend(d_scnt + j, 1, ncclUint64, peer(j), comm, c->stream));
-        RSK_NCCL(ncclRecv(d_rcnt + j, 1, ncclUint64, peer(j), comm, c->stream));
+        RSK_NCCL(ncclSend(d_scnt + 2 * j, 2, ncclUint64, peer(j), comm, c->stream));
+        RSK_NCCL(ncclRecv(d_rcnt + 2 * j, 2, ncclUint64, peer(j), comm, c->stream));
       }
       RSK_NCCL(ncclGroupEnd());
     }
-    RSK_HIP(hipMemcpyAsync(scnt.data() + N, d_rcnt, 8 * N, hipMemcpyDeviceToHost, c->stream));
+    RSK_HIP(hipMemcpyAsync(scnt.data() + 2 * N, d_rcnt, 16 * N, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
-    if (virt)
-      for (uint64_t j = 0; j < N; ++j)
-        if (j != r) scnt[N + j] = 0;
-    if (!self) scnt[N + r] = scnt[r];
-    uint64_t n_in = 0;
-    for (uint64_t j = 0; j < N; ++j) n_in += scnt[N + j];
-    // 3. the records: my run for rank j to j, j's run for me into the receive buffer (in rank order)
-    uint64_t s0 = 0;
-    for (uint64_t j = 0; j < r; ++j) s0 += scnt[j];
-    // The receive buffer may fail to allocate on one rank only: every rank learns of it
-    // (one more MAX all-reduce) before any record moves, so none waits in the exchange.
+    auto rrec = [&](uint64_t j) -> uint64_t& { return scnt[2 * N + 2 * j]; };
+    auto rrow = [&](uint64_t j) -> uint64_t& { return scnt[2 * N + 2 * j + 1]; };
+    for (uint64_t j = 0; j < N; ++j)
+      if (virt && j != r) rrec(j) = rrow(j) = 0;
+    if (!self) {  // my own run and rows stay here (used in place)
+      rrec(r) = scnt[2 * r];
+      rrow(r) = 0;
+    }
+    uint64_t n_in = 0, rows_in = 0;
+    std::vector<uint64_t> rofs(N + 1, 0), rrofs(N + 1, 0);  // each peer's records / rows in the receive buffers
+    for (uint64_t j = 0; j < N; ++j) {
+      rofs[j + 1] = rofs[j] + rrec(j);
+      rrofs[j + 1] = rrofs[j] + rrow(j);
+    }
+    n_in = rofs[N];
+    rows_in = rrofs[N];
+    // 3. buffers: records received (+ heavy row ids received), the send side (records +
+    // heavy ids), the heavy rows (local + received).  An allocation may fail on one rank
+    // only: every rank learns of it (one more MAX all-reduce) before anything moves.
+    const uint64_t R = rsk::HLL_REGS;
     uint2* d_recv = nullptr;
+    uint32_t* d_rids = nullptr;
+    uint2* d_send = nullptr;
+    uint32_t* d_hids = nullptr;
+    uint8_t* d_lrows = nullptr;
+    uint8_t* d_rrows = nullptr;
     int alloc_code = RSK_OK;
     std::string alloc_msg;
     try {
-      d_recv = reinterpret_cast<uint2*>(c->xbuf(8 * std::max<uint64_t>(n_in, 1)));
+      uint8_t* x = c->xbuf(al(8 * std::max<uint64_t>(n_in, 1)) + al(4 * rows_in));
+      d_recv = reinterpret_cast<uint2*>(x);
+      d_rids = reinterpret_cast<uint32_t*>(x + al(8 * std::max<uint64_t>(n_in, 1)));
+      uint8_t* sb = c->sbuf(al(8 * std::max<uint64_t>(n, 1)) + al(4 * H));
+      d_send = reinterpret_cast<uint2*>(sb);
+      d_hids = reinterpret_cast<uint32_t*>(sb + al(8 * std::max<uint64_t>(n, 1)));
+      if (H + rows_in) {
+        d_lrows = c->hrows((H + rows_in) * R);
+        d_rrows = d_lrows + H * R;
+      }
     } catch (const RskError& e) {
       alloc_code = e.code;
       alloc_msg = e.msg;
@@ -417,26 +502,44 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     RSK_NCCL(ncclAllReduce(d_meta, d_meta, 1, ncclUint64, ncclMax, comm, c->stream));
     RSK_HIP(hipMemcpyAsync(h_meta, d_meta, 8, hipMemcpyDeviceToHost, c->stream));
     RSK_HIP(hipStreamSynchronize(c->stream));
-    if (alloc_code != RSK_OK) throw RskError{alloc_code, "rsk_hll_add_grouped_routed: receive buffer: " + alloc_msg};
+    if (alloc_code != RSK_OK) throw RskError{alloc_code, "rsk_hll_add_grouped_routed: exchange buffers: " + alloc_msg};
     if (h_meta[0] != 0)
-      throw RskError{RSK_ERR_OUT_OF_MEMORY, "rsk_hll_add_grouped_routed: another rank could not allocate its receive "
-                                            "buffer"};
+      throw RskError{RSK_ERR_OUT_OF_MEMORY, "rsk_hll_add_grouped_routed: another rank could not allocate its exchange "
+                                            "buffers"};
+    // 4. the records (light pairs to their owners' runs, heavy pairs to the last run)
+    if (n) {
+      RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * NO * B, hipMemcpyHostToDevice, c->stream));
+      rsk::hll_route_scatter_launch(c, reinterpret_cast<const uint8_t*>(keys->data), groups, n, G, (uint32_t)N,
+                                    d_slot_of, d_off, d_send);
+    }
+    // 5. heavy pairs folded into local rows (the record pipeline onto a pool of the H heavy
+    // groups; it reuses the context's work buffer, which holds nothing live from here on)
+    if (H) {
+      RSK_HIP(hipMemcpyAsync(d_hids, heavy_ids.data(), 4 * H, hipMemcpyHostToDevice, c->stream));
+      rsk::ProfScope ps(c, "hll_route_heavy_rows");
+      rsk::hll_add_grouped_recs_launch(c, d_send + sfirst[N], n_heavy, d_lrows, H, true, true,
+                                       rsk::PCount{nullptr, nullptr, 0});
+    }
+    // 6. exchange: per peer its record run, then its heavy row ids and rows (matched in
+    // issue order on both sides), every transfer in pieces of <= 1 GiB
     {
       rsk::ProfScope ps(c, "hll_route_exchange");
       RSK_NCCL(ncclGroupStart());
-      for (uint64_t j = 0, so = 0, ro = 0; j < N; so += scnt[j], ro += scnt[N + j], ++j) {
+      for (uint64_t j = 0; j < N; ++j) {
         if ((j == r && !self) || (virt && j != r)) continue;
-        p2p_pieces(d_send + so, scnt[j] * 8, peer(j), comm, c->stream, true);
-        p2p_pieces(d_recv + ro, scnt[N + j] * 8, peer(j), comm, c->stream, false);
+        p2p_pieces(d_send + sfirst[j], scnt[2 * j] * 8, peer(j), comm, c->stream, true);
+        p2p_pieces(d_recv + rofs[j], rrec(j) * 8, peer(j), comm, c->stream, false);
+        p2p_pieces(d_hids + hfirst[j], hrows[j] * 4, peer(j), comm, c->stream, true);
+        p2p_pieces(d_rids + rrofs[j], rrow(j) * 4, peer(j), comm, c->stream, false);
+        p2p_pieces(d_lrows + hfirst[j] * R, hrows[j] * R, peer(j), comm, c->stream, true);
+        p2p_pieces(d_rrows + rrofs[j] * R, rrow(j) * R, peer(j), comm, c->stream, false);
       }
       RSK_NCCL(ncclGroupEnd());
     }
-    if (!self && scnt[r]) {
-      uint64_t ro = 0;
-      for (uint64_t j = 0; j < r; ++j) ro += scnt[N + j];
-      RSK_HIP(hipMemcpyAsync(d_recv + ro, d_send + s0, scnt[r] * 8, hipMemcpyDeviceToDevice, c->stream));
-    }
-    // 4. the owned rows [first, first + count): a pending lazy clear of the whole pool is
+    if (!self && scnt[2 * r])
+      RSK_HIP(hipMemcpyAsync(d_recv + rofs[r], d_send + sfirst[r], scnt[2 * r] * 8, hipMemcpyDeviceToDevice,
+                             c->stream));
+    // 7. the owned rows [first, first + count): a pending lazy clear of the whole pool is
     // completed on them by the add (every owned row written) and stays pending on every
     // other row (hll_pend_outside: they read as cleared and are zeroed before any other
     // access); owned rows a partial clear left pending are zeroed first
@@ -447,9 +550,23 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     rsk::hll_touch(h);
     h->pending_clear = false;
     if (write_all && count < h->n) rsk::hll_pend_outside(h, first, count);
-    rsk::hll_add_grouped_recs_launch(c, d_recv, n_in, h->d_regs + first * (uint64_t)rsk::HLL_REGS, count, pool_zero,
-                                     write_all,
+    rsk::hll_add_grouped_recs_launch(c, d_recv, n_in, h->d_regs + first * R, count, pool_zero, write_all,
                                      rsk::PCount{h->d_pcount + first, h->d_pepoch + first, h->pc_epoch});
+    // 8. heavy rows into the owned rows, one launch per source (ids distinct within one)
+    {
+      rsk::ProfScope ps(c, "hll_route_rows_merge");
+      for (uint64_t j = 0; j < N; ++j) {
+        const bool local = j == r && !self;
+        const uint64_t m = local ? hrows[r] : rrow(j);
+        if (!m) continue;
+        const uint32_t* ids = local ? d_hids + hfirst[r] : d_rids + rrofs[j];
+        const uint8_t* rows = local ? d_lrows + hfirst[r] * R : d_rrows + rrofs[j] * R;
+        hipLaunchKernelGGL(max_rows_kernel, dim3((uint32_t)std::min<uint64_t>(m, 1u << 16)), dim3(256), 0, c->stream,
+                           reinterpret_cast<uint4*>(h->d_regs), ids, m, reinterpret_cast<const uint4*>(rows),
+                           h->d_pepoch);
+        RSK_CHECK_LAUNCH("max_rows");
+      }
+    }
     if (count) {
       hipLaunchKernelGGL(invalidate_card_kernel, dim3(256), dim3(256), 0, c->stream, h->d_card + first, count);
       RSK_CHECK_LAUNCH("invalidate");

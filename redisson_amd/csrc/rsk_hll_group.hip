@@ -1590,10 +1590,15 @@ __global__ __launch_bounds__(RT_T) void hll_route_sample_kernel(const uint32_t* 
   }
 }
 
-__global__ __launch_bounds__(256) void hll_heavy_flag_kernel(const uint32_t* __restrict__ hist, uint64_t G,
-                                                             uint32_t thr, uint32_t* __restrict__ flag) {
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += (uint64_t)gridDim.x * blockDim.x)
-    flag[g] = g < G && hist[g] >= thr ? 1u : 0u;
+// groups in [skip_lo, skip_hi) (the rank's own: no transfer to save) are never heavy
+__global__ __launch_bounds__(256) void hll_heavy_flag_kernel(uint32_t* __restrict__ hist, uint64_t G, uint32_t thr,
+                                                             uint64_t skip_lo, uint64_t skip_hi,
+                                                             uint32_t* __restrict__ flag) {
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += (uint64_t)gridDim.x * blockDim.x) {
+    const bool hv = g < G && hist[g] >= thr && !(g >= skip_lo && g < skip_hi);
+    if (g < G && !hv) hist[g] = 0;  // (the slot pass reads the flag from hist)
+    flag[g] = hv ? 1u : 0u;
+  }
 }
 
 __global__ __launch_bounds__(256) void hll_heavy_slot_kernel(const uint32_t* __restrict__ hist,
@@ -1657,7 +1662,8 @@ uint64_t hll_heavy_scratch_bytes(uint64_t G, uint32_t cap) {
 }
 
 uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t stride, uint32_t thr,
-                          uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of, std::vector<uint32_t>* heavy_ids) {
+                          uint64_t skip_lo, uint64_t skip_hi, uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of,
+                          std::vector<uint32_t>* heavy_ids) {
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* pos = reinterpret_cast<uint32_t*>(scratch + al(4 * G));
@@ -1675,7 +1681,7 @@ uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint
     RSK_HIP(hipMemsetAsync(hist, 0, 4 * G, c->stream));
     hipLaunchKernelGGL(hll_route_sample_kernel, dim3(B), dim3(RT_T), 0, c->stream, d_groups, n, per, G, stride, hist);
     RSK_CHECK_LAUNCH("hll_route_sample");
-    hipLaunchKernelGGL(hll_heavy_flag_kernel, dim3(gb), dim3(256), 0, c->stream, hist, G, thr, pos);
+    hipLaunchKernelGGL(hll_heavy_flag_kernel, dim3(gb), dim3(256), 0, c->stream, hist, G, thr, skip_lo, skip_hi, pos);
     RSK_CHECK_LAUNCH("hll_heavy_flag");
     RSK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, sb, pos, pos, (int)(G + 1), c->stream));
     hipLaunchKernelGGL(hll_heavy_slot_kernel, dim3(gb), dim3(256), 0, c->stream, hist, pos, G, thr, cap, slot, ids);

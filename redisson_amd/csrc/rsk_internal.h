@@ -73,6 +73,8 @@ struct Tuning {
   int gpart_tile = 0;        // its tile-major first pass: 0 8192-record tiles (2 x 256 lanes per CU), 1 16384 (512 lanes)
   int route_vranks = 0;      // TEST ONLY, 1-rank communicator: the routed grouped add plans as rank route_vrank of
   int route_vrank = 0;       // route_vranks (its owned sub-range; records of other owners dropped)
+  int route_heavy = 0;       // routed add's heavy-group pre-combine: 0 auto (>= 2048 pairs, N > 1 or self exchange,
+                             // >= 2^22 pairs), -1 never, > 0 on at any size with that many pairs per heavy group
 };
 
 // An asynchronous call (rsk_*_async): its host inputs are copied into the
@@ -209,10 +211,18 @@ struct rsk_ctx {
   // routed grouped add), distinct from d_work, which the add itself uses
   uint8_t* d_xbuf = nullptr;
   uint64_t xbuf_bytes = 0;
+  // the routed grouped add's send side (records, heavy ids) and its heavy
+  // rows (built locally and received), grow-on-demand like d_xbuf
+  uint8_t* d_sbuf = nullptr;
+  uint64_t sbuf_bytes = 0;
+  uint8_t* d_hrows = nullptr;
+  uint64_t hrows_bytes = 0;
 
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);
   uint8_t* xbuf(uint64_t bytes);
+  uint8_t* sbuf(uint64_t bytes);
+  uint8_t* hrows(uint64_t bytes);
 };
 
 struct rsk_hll {
@@ -378,13 +388,15 @@ void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, ui
 void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
                               uint32_t N, const uint32_t* d_slot_of, const uint64_t* d_off, uint2* d_out);
 // Heavy groups of a routed add (skew): sampled counts (every stride-th pair), a
-// group is heavy when its sample count reaches thr; at most cap, by group id.
+// group is heavy when its sample count reaches thr and it lies outside
+// [skip_lo, skip_hi); at most cap, by group id.
 // scratch: hll_heavy_scratch_bytes(G, cap) of device memory; *d_slot_of points
 // into it (a group's slot, ~0 if light), heavy_ids gets the heavy groups
 // ascending (slot order).  Returns their number; synchronises the stream.
 uint64_t hll_heavy_scratch_bytes(uint64_t G, uint32_t cap);
 uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t stride, uint32_t thr,
-                          uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of, std::vector<uint32_t>* heavy_ids);
+                          uint64_t skip_lo, uint64_t skip_hi, uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of,
+                          std::vector<uint32_t>* heavy_ids);
 // Records into a pool of G rows (partitioned for large batches, else a CAS each);
 // write_all: every row written (zero rows for sketches without records).
 void hll_add_grouped_recs_launch(rsk_ctx* c, const uint2* d_recs, uint64_t n, uint8_t* d_regs, uint64_t G,
@@ -423,5 +435,6 @@ uint64_t plan_owner(uint64_t n, uint64_t N, uint64_t id);
 uint64_t plan_bloom_slice_words(uint64_t nwords, uint64_t N);
 bool plan_fetch(uint64_t n, uint64_t N, uint64_t r, const uint64_t* ids, uint64_t n_ids, uint32_t flags,
                 std::vector<uint64_t>* want, std::vector<uint64_t>* counts);
+void plan_heavy_rows(uint64_t G, uint64_t N, const uint32_t* heavy_ids, uint64_t H, std::vector<uint64_t>* rows);
 
 }  // namespace rsk

@@ -65,6 +65,45 @@ bool plan_fetch(uint64_t n, uint64_t N, uint64_t r, const uint64_t* ids, uint64_
   return true;
 }
 
+// Heavy rows of a routed add per owner: heavy_ids ascending (the slot order),
+// so owner o's rows are the slots [sum of rows[< o], + rows[o]).
+void plan_heavy_rows(uint64_t G, uint64_t N, const uint32_t* heavy_ids, uint64_t H, std::vector<uint64_t>* rows) {
+  rows->assign(N, 0);
+  for (uint64_t i = 0; i < H; ++i) ++(*rows)[plan_owner(G, N, heavy_ids[i])];
+}
+
+// The routed grouped add's traffic per owner (rsk_hll_add_grouped_routed): from
+// counts[s * G + g] = pairs of group g on source rank s, with the groups of at
+// least heavy_min pairs owned by another rank (0: none; at most heavy_cap per
+// source, lowest ids first) pre-combined at the source into one 16 KiB row each.  Per rank o:
+// bytes received from the other ranks (8 B per light record, 16384 + 4 B per
+// heavy row and its id), heavy rows received, and light records its apply
+// folds (its own included).  The device takes the heavy set from a sampled
+// count (every stride-th pair) instead of the exact one.
+void plan_route_recv(const uint64_t* counts, uint64_t G, uint64_t N, uint64_t heavy_min, uint64_t heavy_cap,
+                     uint64_t* recv_bytes, uint64_t* recv_rows, uint64_t* apply_records) {
+  for (uint64_t o = 0; o < N; ++o) recv_bytes[o] = recv_rows[o] = apply_records[o] = 0;
+  for (uint64_t s = 0; s < N; ++s) {
+    const uint64_t* cs = counts + s * G;
+    uint64_t heavy = 0;
+    for (uint64_t g = 0; g < G; ++g) {
+      const uint64_t k = cs[g];
+      if (!k) continue;
+      const uint64_t o = plan_owner(G, N, g);
+      if (heavy_min && k >= heavy_min && o != s && heavy < heavy_cap) {
+        ++heavy;
+        if (o != s) {
+          recv_bytes[o] += 16384 + 4;
+          ++recv_rows[o];
+        }
+      } else {
+        apply_records[o] += k;
+        if (o != s) recv_bytes[o] += 8 * k;
+      }
+    }
+  }
+}
+
 }  // namespace rsk
 
 extern "C" {
@@ -104,6 +143,13 @@ int rsk_plan_fetch(uint64_t n, int nranks, int rank, const uint64_t* ids, uint64
   std::copy(want.begin(), want.end(), want_out);
   std::copy(counts.begin(), counts.end(), counts_out);
   *n_want = want.size();
+  return RSK_OK;
+}
+
+int rsk_plan_route_recv(const uint64_t* counts, uint64_t G, int nranks, uint64_t heavy_min, uint64_t heavy_cap,
+                        uint64_t* recv_bytes, uint64_t* recv_rows, uint64_t* apply_records) {
+  if (nranks < 1 || (!counts && G) || !recv_bytes || !recv_rows || !apply_records) return RSK_ERR_INVALID_ARG;
+  rsk::plan_route_recv(counts, G, (uint64_t)nranks, heavy_min, heavy_cap, recv_bytes, recv_rows, apply_records);
   return RSK_OK;
 }
 

@@ -121,8 +121,8 @@ for p in ${PART//,/ }; do
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;
     p2p)  # >2 GB self send/recv probe (rsk_diag_p2p_probe): one uint8 / one uint64 transfer / 1 GiB pieces
-      step p2p 300 python3 scripts/p2p_probe.py || exit 1
-      grep '^{' gpurun_out/p2p.log > gpurun_out/${TAG}_p2p_probe.jsonl ;;
+      step p2p 300 python3 scripts/p2p_probe.py $P2P_SIZES || exit 1
+      grep '^{' gpurun_out/p2p.log >> gpurun_out/${TAG}_p2p_probe.jsonl ;;
     *) echo "unknown part $p"; exit 2 ;;
   esac
 done

@@ -4,7 +4,7 @@ known pattern through a 1-rank RCCL communicator at sizes around 2^31 and
 elements) and in the library's 1 GiB pieces (rsk_diag_p2p_probe).  One JSON
 line per case to stdout.
 
-    python scripts/p2p_probe.py > gpurun_out/p2p_probe.jsonl
+    python scripts/p2p_probe.py [BYTES ...] > gpurun_out/p2p_probe.jsonl
 """
 import ctypes
 import json
@@ -27,7 +27,8 @@ def main():
     uid = (ctypes.c_uint8 * 128)()
     _lib.check(L.rsk_comm_unique_id(uid))
     _lib.check(L.rsk_comm_init(eng.ctx, 1, 0, uid))
-    sizes = [1 << 30, (1 << 31) - 8, (1 << 31) + 8, 3 << 30, 4_000_000_000, (1 << 32) + 8]
+    sizes = [int(a) for a in sys.argv[1:]] or [1 << 30, (1 << 31) - 8, (1 << 31) + 8, 3 << 30, 4_000_000_000,
+                                              (1 << 32) + 8]
     for b in sizes:
         for mode in (2, 1, 0):
             bad, first = ctypes.c_uint64(), ctypes.c_uint64()

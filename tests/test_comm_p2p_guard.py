@@ -1,7 +1,9 @@
 """Every point-to-point transfer of data in the RCCL layer goes through the one
 guarded path, p2p_pieces (pieces of at most P2P_PIECE = 1 GiB), VERDICT r05
-Weak 7: a 4.0 GB self send/recv in one piece came back wrong.  Only the
-one-word count exchanges may call ncclSend / ncclRecv directly.  A recorder
+Weak 7: a self send/recv of more than 1 GiB in one piece delivers only its
+first half with RCCL 2.27.7 (profiles/r06_p2p_probe.jsonl).  Only the count
+exchanges (one or two u64 words per peer) may call ncclSend / ncclRecv
+directly.  A recorder
 restatement of p2p_pieces checks the piece arithmetic: contiguous, in order,
 covering every byte, none above the cap (zero bytes issue nothing)."""
 import os
@@ -34,7 +36,7 @@ def test_only_count_words_bypass_p2p_pieces():
     assert calls, "expected the count exchanges"
     for kind, args in calls:
         parts = [a.strip() for a in args.split(",")]
-        assert parts[1] == "1" and parts[2] == "ncclUint64", (kind, args)  # one u64 count per peer
+        assert parts[1] in ("1", "2") and parts[2] == "ncclUint64", (kind, args)  # one or two u64 counts per peer
 
 
 def _pieces(nbytes, cap=1 << 30):

@@ -348,3 +348,65 @@ def test_routed_add_owned_subrange(engine, orc, route, G, n, vrank):
     finally:
         route(route_vranks=0)
         _lib.check(L.rsk_comm_destroy(engine.ctx))
+
+
+@pytest.mark.parametrize("G,n,heavy,vranks,vrank,self_", [
+    (100_003, 5_000_000, 64, 0, 0, True),     # every heavy row through RCCL to itself
+    (100_003, 5_000_000, 64, 3, 1, False),    # owner 1 of 3: heavy groups of ranks 0 / 2 are rows (dropped with
+                                              # their records), its own groups stay records
+    (100_003, 5_000_000, 300, 3, 0, True),    # owner 0 of 3, rows through RCCL (the Zipf-hot range)
+    (20_000, 8_000_000, 0, 0, 0, True),       # auto: >= 2048 pairs per heavy group at >= 2^22 pairs
+])
+def test_routed_add_heavy_precombine(engine, orc, route, G, n, heavy, vranks, vrank, self_):
+    """VERDICT r05 Next 2: under Zipf(1.1) the groups with many pairs are folded
+    into 16 KiB rows where the pairs are, the rows (not the records) go to the
+    owner, which max-merges them after its own apply.  The owned rows must equal
+    the plain grouped add's, bit for bit, whichever groups the sample makes heavy;
+    the pre-combine ran (its stages were timed)."""
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    engine.prof_enable(True)
+    engine.prof_reset()
+    try:
+        if heavy:
+            groups, keys = orc.gen_grouped_zipf(0x5EED0006, G, 1.1, 0, n)
+        else:
+            groups, keys = orc.gen_grouped(0x5EED0006, G, 0, n)  # 400 pairs per group: none heavy ...
+            groups[: n // 4] = np.arange(n // 4, dtype=np.uint32) % 64  # ... but 64 groups of ~31k pairs
+        kd = devmem.DeviceBuffer.from_numpy(engine, keys)
+        gd = devmem.DeviceBuffer.from_numpy(engine, groups)
+        kb = kd.keys_fixed(n, 16)
+        first, count = shard.owned_range(G, vranks or 1, vrank)
+        b = GroupedHyperLogLog(engine, G)
+        b.clear()
+        b.add(kb, gd)
+        ref = _all_rows(L, engine, b.pool, G)
+        a = GroupedHyperLogLog(engine, G)
+        a.add(kb, gd)  # stale rows under the clear
+        a.clear()
+        route(route_heavy=heavy, route_vranks=vranks, route_vrank=vrank)
+        flags = _lib.RSK_FETCH_SELF if self_ else 0
+        assert shard.hll_add_grouped_routed(a.pool, kb, gd, flags=flags) == (first, count)
+        assert _prof(engine, "hll_route_heavy") == 1
+        assert _prof(engine, "hll_route_heavy_rows") == 1  # some group was heavy
+        assert _prof(engine, "hll_route_rows_merge") == 1
+        got = _all_rows(L, engine, a.pool, G)
+        bad = np.nonzero((got[first:first + count] != ref[first:first + count]).any(1))[0]
+        assert bad.size == 0, (bad.size, (bad[:10] + first).tolist())
+        assert not got[:first].any() and not got[first + count:].any()  # outside: cleared
+        # PFCOUNT of owned rows: merged rows' precomputed estimates were retired
+        ids = np.array([first, first + 1, first + 2, first + count - 1], np.uint64)
+        assert list(a.count(ids=ids)) == list(b.count(ids=ids))
+        a.close()
+        b.close()
+        kd.free()
+        gd.free()
+    finally:
+        route(route_vranks=0, route_heavy=0)
+        engine.prof_enable(False)
+        _lib.check(L.rsk_comm_destroy(engine.ctx))

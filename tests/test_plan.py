@@ -147,3 +147,46 @@ def test_plan_argument_checks():
     assert L.rsk_plan_owned_range(10, 2, 2, ctypes.byref(f), ctypes.byref(c)) == _lib.RSK_ERR_INVALID_ARG
     o = ctypes.c_int()
     assert L.rsk_plan_owner(10, 2, 10, ctypes.byref(o)) == _lib.RSK_ERR_INVALID_ARG
+
+
+def _route_recv(counts, G, N, heavy_min, cap=65536):
+    rb, rr, ap = (np.zeros(N, np.uint64) for _ in range(3))
+    c = np.ascontiguousarray(counts, np.uint64)
+    _ck(plan_lib().rsk_plan_route_recv(c.ctypes.data, G, N, heavy_min, cap, rb.ctypes.data, rr.ctypes.data,
+                                       ap.ctypes.data))
+    return rb, rr, ap
+
+
+def test_route_plan_small_by_hand():
+    # G = 6, N = 2 (rank 0 owns 0..2, rank 1 owns 3..5); heavy at >= 4 pairs
+    counts = np.array([[5, 1, 0, 4, 2, 0],
+                       [0, 4, 0, 9, 3, 1]], np.uint64)
+    rb, rr, ap = _route_recv(counts, 6, 2, 4)
+    # rank 0 receives from rank 1: group 1 (4 pairs, heavy: a row); rank 1 from rank 0: group 3 (a row), group 4 (2)
+    assert rr.tolist() == [1, 1]
+    assert rb.tolist() == [16388, 16388 + 16]
+    # applied light records: rank 0 its own 5 + 1 (groups 0, 1 own), rank 1 own 9 + 3 + 1 and rank 0's 2 of group 4
+    assert ap.tolist() == [6, 15]
+    rb0, rr0, ap0 = _route_recv(counts, 6, 2, 0)  # no pre-combine
+    assert rr0.tolist() == [0, 0] and rb0.tolist() == [8 * 4, 8 * 6] and ap0.tolist() == [10, 19]
+
+
+def test_route_plan_zipf_balance_at_8_ranks():
+    """VERDICT r05 Next 2 at the C5 configuration: N = 8, G = 1M, 5e8 pairs per
+    rank drawn Zipf(1.1) (expected counts).  Contiguous ownership sends rank 0
+    ~26 GB (7.4x a uniform rank's 3.5 GB); with groups of >= 2048 pairs owned
+    elsewhere pre-combined into rows, rank 0 receives <= 1.25x the uniform
+    per-rank bytes, and no rank more.  (The other ranks receive far less than
+    uniform, so max/mean bytes stays ~5: the Zipf traffic itself lands in rank
+    0's range; what bounds the step is the max.)"""
+    G, N, n = 1_000_000, 8, 500_000_000
+    w = np.arange(1, G + 1, dtype=np.float64) ** -1.1
+    cz = np.rint(n * w / w.sum()).astype(np.uint64)
+    cu = np.full(G, n // G, np.uint64)
+    uni, _, uni_ap = _route_recv(np.tile(cu, (N, 1)), G, N, 2048)
+    raw, _, raw_ap = _route_recv(np.tile(cz, (N, 1)), G, N, 0)
+    pre, rows, pre_ap = _route_recv(np.tile(cz, (N, 1)), G, N, 2048)
+    assert raw[0] > 7 * uni[0]
+    assert pre[0] <= 1.25 * uni[0] and pre.max() == pre[0]
+    assert rows[0] > 0 and rows[1:].sum() == 0
+    assert int(pre_ap.sum()) < int(raw_ap.sum())  # heavy pairs folded at the source, not applied at the owner
