@@ -43,7 +43,7 @@ const char *rsk_diag_last_error(void);
  *                 folds (bit 0) / without its T stores (bit 1)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never
  *   gpart_tm      1 (default): its first pass tile-major (hll_gpart1t), 0: exact-offset runs (hll_gcount + hll_gpart1)
- *   gapply_st     the grouped apply's row stores: 0 nontemporal (default), 1 plain
+ *   gapply_st     the grouped apply's row stores: 0 nontemporal (default), 1 plain, 2 none (TIMING ONLY)
  *   gpart_rt      the fine-bin sort's round: 0 8192 records (default), 1 16384 (one
  *                 workgroup per CU)
  *   io_trace      1: the batched export / import print their host phase times to stderr

@@ -344,65 +344,96 @@ void ensure_pinned(rsk_ctx* c) {
 uint64_t staged_piece(const rsk_ctx* c, uint64_t bytes) {
   return std::min<uint64_t>(c->stage_bytes, std::max<uint64_t>(8ull << 20, ((bytes / 8) + 4095) & ~uint64_t(4095)));
 }
-// On stream `s`, after event `after` (when not null): the context stream
-// stays free for the next kernels meanwhile.  Returns synchronised.
 // A stage may still feed a DMA an earlier h2d_staged queued (it returns with
 // its copies in flight): both stages' last events are waited for first.
 void pinned_idle(rsk_ctx* c) {
   for (int b = 0; b < 2; ++b) RSK_HIP(hipEventSynchronize(c->pin_ev[b]));
 }
-// (d2h_staged_on returns synchronised: its ring events are idle between calls)
-void d2h_staged_on(rsk_ctx* c, hipStream_t s, hipEvent_t after, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
-  ensure_pinned(c);
-  if (!c->pin_off) pinned_idle(c);
-  if (after) RSK_HIP(hipStreamWaitEvent(s, after, 0));
-  if (c->pin_off) {
-    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
-    RSK_HIP(hipStreamSynchronize(s));
-    return;
+// Device -> pageable host through the two pinned stages, as a stream of
+// pieces that may span several calls of put(): a ring of NS slots over the two
+// stages (2, 4 or 8: as many pieces of S as they hold), the DMAs of up to
+// NS - 1 pieces queued on stream `s` ahead of the host copy-out, so the copy
+// engine never waits for the host between pieces -- nor between the chunks of
+// a batched export, whose pieces go through one stream (drain() at the end).
+class D2HStream {
+ public:
+  D2HStream(rsk_ctx* c, hipStream_t s, uint64_t piece) : c_(c), s_(s) {
+    ensure_pinned(c);
+    if (c->pin_off) return;
+    pinned_idle(c);  // a stage may still feed a DMA an earlier h2d_staged queued
+    S_ = piece;
+    const uint64_t B = c->stage_bytes + c->stage_bytes / 4;
+    const uint32_t per = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, B / S_));
+    NS_ = 2 * (per >= 4 ? 4 : per >= 2 ? 2 : 1);
   }
-  // a ring of NS slots over the two stages (2, 4 or 8: as many pieces of S as they hold), the
-  // DMAs of up to NS - 1 pieces queued ahead of the host copy (the copy engine never waits for
-  // the host between pieces)
-  const uint64_t S = staged_piece(c, bytes), B = c->stage_bytes + c->stage_bytes / 4;
-  const uint32_t per = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, B / S));
-  const uint32_t NS = 2 * (per >= 4 ? 4 : per >= 2 ? 2 : 1);
-  auto slot_ptr = [&](uint32_t j) { return c->h_pin[j & 1] + (uint64_t)(j >> 1) * S; };
-  const uint64_t np = (bytes + S - 1) / S;
-  auto copy_out = [&](uint64_t k) {
-    const uint32_t j = (uint32_t)(k % NS);
-    RSK_HIP(hipEventSynchronize(c->ring_ev[j]));
-    par_copy(dst + k * S, slot_ptr(j), std::min<uint64_t>(S, bytes - k * S), c->stage_threads);
+  // bytes from device src to host dst, on the stream after event `after` (when not null)
+  void put(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipEvent_t after) {
+    if (after) RSK_HIP(hipStreamWaitEvent(s_, after, 0));
+    if (c_->pin_off) {
+      if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_));
+      return;
+    }
+    for (uint64_t o = 0; o < bytes; o += S_) {
+      const uint64_t m = std::min<uint64_t>(S_, bytes - o);
+      if (fifo_n_ == NS_ - 1) pop();  // the slot this piece takes was copied out by then
+      const uint32_t j = (uint32_t)(issued_++ % NS_);
+      RSK_HIP(hipMemcpyAsync(slot(j), src + o, m, hipMemcpyDeviceToHost, s_));
+      RSK_HIP(hipEventRecord(c_->ring_ev[j], s_));
+      fifo_[(head_ + fifo_n_++) % 8] = Piece{dst + o, m, j};
+    }
+  }
+  ~D2HStream() {  // unwound by an error: no DMA may still fill a stage the next call refills
+    if (fifo_n_) (void)hipStreamSynchronize(s_);
+  }
+  // every piece copied out, the stream synchronised
+  void drain() {
+    while (fifo_n_) pop();
+    RSK_HIP(hipStreamSynchronize(s_));
+  }
+
+ private:
+  struct Piece {
+    uint8_t* dst;
+    uint64_t bytes;
+    uint32_t slot;
   };
-  for (uint64_t k = 0; k < np; ++k) {
-    const uint32_t j = (uint32_t)(k % NS);  // piece k - NS, its last user, was copied out at k - 1
-    RSK_HIP(hipMemcpyAsync(slot_ptr(j), src + k * S, std::min<uint64_t>(S, bytes - k * S), hipMemcpyDeviceToHost, s));
-    RSK_HIP(hipEventRecord(c->ring_ev[j], s));
-    if (k + 1 >= NS) copy_out(k + 1 - NS);
+  uint8_t* slot(uint32_t j) const { return c_->h_pin[j & 1] + (uint64_t)(j >> 1) * S_; }
+  void pop() {
+    const Piece p = fifo_[head_];
+    head_ = (head_ + 1) % 8;
+    --fifo_n_;
+    RSK_HIP(hipEventSynchronize(c_->ring_ev[p.slot]));
+    par_copy(p.dst, slot(p.slot), p.bytes, c_->stage_threads);
   }
-  for (uint64_t k = np >= NS - 1 ? np - (NS - 1) : 0; k < np; ++k) copy_out(k);
-  RSK_HIP(hipStreamSynchronize(s));
-}
+  rsk_ctx* c_;
+  hipStream_t s_;
+  uint64_t S_ = 0, issued_ = 0;
+  uint32_t NS_ = 2, head_ = 0, fifo_n_ = 0;
+  Piece fifo_[8] = {};
+};
+
 // The other way; returns with the copies queued on the stream (ordered
 // before the caller's next launch).
-void h2d_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+// On stream s; consecutive calls keep the link busy (a stage is refilled as
+// soon as the DMA that last read it is done, whichever call issued it).
+void h2d_staged_on(rsk_ctx* c, hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
   ensure_pinned(c);
   if (c->pin_off) {
-    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     return;
   }
-  pinned_idle(c);
   const uint64_t S = staged_piece(c, bytes);
-  bool used[2] = {false, false};
   for (uint64_t o = 0, k = 0; o < bytes; o += S, ++k) {
     const int slot = (int)(k & 1);
     const uint64_t n = std::min<uint64_t>(S, bytes - o);
-    if (used[slot]) RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));  // the DMA that last read it is done
+    RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));  // the DMA that last read this stage is done
     par_copy(c->h_pin[slot], src + o, n, c->stage_threads);
-    RSK_HIP(hipMemcpyAsync(dst + o, c->h_pin[slot], n, hipMemcpyHostToDevice, c->stream));
-    RSK_HIP(hipEventRecord(c->pin_ev[slot], c->stream));
-    used[slot] = true;
+    RSK_HIP(hipMemcpyAsync(dst + o, c->h_pin[slot], n, hipMemcpyHostToDevice, s));
+    RSK_HIP(hipEventRecord(c->pin_ev[slot], s));
   }
+}
+void h2d_staged(rsk_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+  h2d_staged_on(c, c->stream, dst, src, bytes);
 }
 
 // Calls fn(dev_keys, first_index, count) over the batch; host batches are
@@ -1608,13 +1639,15 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     // offsets[n], and the call fails.
     constexpr uint64_t KC = 1ull << 16;
     const uint64_t kc = std::min<uint64_t>(KC, std::max<uint64_t>(nd, 1));
-    uint8_t* w = c->work(al(8 * kc) * 2 + al(kc) + al(4 * kc) + 2 * al(kc * (uint64_t)RSK_HLL_DENSE_BYTES) + 256);
+    uint8_t* w = c->work(al(8 * kc) * 2 + al(kc) + al(4 * kc) + 3 * al(kc * (uint64_t)RSK_HLL_DENSE_BYTES) + 256);
     uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
     uint64_t* d_pos = reinterpret_cast<uint64_t*>(w + al(8 * kc));
     uint8_t* d_want = w + 2 * al(8 * kc);
     uint32_t* d_len = reinterpret_cast<uint32_t*>(w + 2 * al(8 * kc) + al(kc));
     uint8_t* d_slots = w + 2 * al(8 * kc) + al(kc) + al(4 * kc);
-    uint8_t* d_stage = d_slots + al(kc * (uint64_t)RSK_HLL_DENSE_BYTES);
+    // two packed stages: chunk k + 1 packs into one while chunk k's strings leave the other
+    uint8_t* d_stage[2] = {d_slots + al(kc * (uint64_t)RSK_HLL_DENSE_BYTES),
+                           d_slots + 2 * al(kc * (uint64_t)RSK_HLL_DENSE_BYTES)};
     std::vector<uint32_t> len(nd);
     // the chunk's ids, flags, lengths and string offsets cross the link from pinned memory: a
     // pageable copy would hold the host until the stream reaches it (the next chunk's encode
@@ -1650,25 +1683,34 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)m, d_len, d_slots);
       RSK_HIP(hipMemcpyAsync(h_len, d_len, 4 * m, hipMemcpyDeviceToHost, c->stream));
     };
-    hipEvent_t packed = nullptr;
+    // packed: chunk k's strings are in their stage; out_done[s]: the copy-out of stage s was queued
+    // (chunk k + 2 packs into it after that, on the device)
+    hipEvent_t packed = nullptr, out_done[2] = {nullptr, nullptr};
+    struct EvGuard {
+      hipEvent_t* e[3];
+      ~EvGuard() {
+        for (hipEvent_t* p : e)
+          if (*p) (void)hipEventDestroy(*p);
+      }
+    } eg{{&packed, &out_done[0], &out_done[1]}};
     if (nd) {
       RSK_HIP(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
+      RSK_HIP(hipEventCreateWithFlags(&out_done[0], hipEventDisableTiming));
+      RSK_HIP(hipEventCreateWithFlags(&out_done[1], hipEventDisableTiming));
       encode(0);
     }
-    struct EvGuard {
-      hipEvent_t e;
-      ~EvGuard() {
-        if (e) (void)hipEventDestroy(e);
-      }
-    } eg{packed};
-    // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes
+    // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes and
+    // packs; the pieces of every chunk go through one D2H stream (16 MiB pieces, up to 7 in
+    // flight), so the copy engine runs on across chunk boundaries
+    D2HStream xo(c, c->xout, 16ull << 20);
     const bool trace = c->tune.io_trace != 0;  // (route io_trace: phase times to stderr)
     double t_sync = 0, t_adv = 0, t_pack = 0, t_enc = 0, t_d2h = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto t00 = now();
-    for (uint64_t d0 = 0; d0 < nd; d0 += kc) {
+    for (uint64_t d0 = 0, ck = 0; d0 < nd; d0 += kc, ++ck) {
       const uint64_t m = std::min<uint64_t>(kc, nd - d0);
+      uint8_t* stage = d_stage[ck & 1];
       auto t0 = now();
       RSK_HIP(hipStreamSynchronize(c->stream));  // chunk d0's lengths (and the previous pack) done
       std::memcpy(len.data() + d0, h_len, 4 * m);
@@ -1684,7 +1726,8 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
         end = offsets[dev_i[d0 + m - 1] + 1];
         for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
         RSK_HIP(hipMemcpyAsync(d_pos, pos, 8 * m, hipMemcpyHostToDevice, c->stream));
-        hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, d_stage);
+        if (ck >= 2) RSK_HIP(hipStreamWaitEvent(c->stream, out_done[ck & 1], 0));  // chunk k - 2 left this stage
+        hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, stage);
         RSK_HIP(hipEventRecord(packed, c->stream));
       }
       t1 = now();
@@ -1692,7 +1735,15 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       if (d0 + kc < nd) encode(d0 + kc);  // (after the pack on the same stream: the slots are free)
       t0 = now();
       t_enc += ms(t1, t0);
-      if (fits) d2h_staged_on(c, c->xout, packed, out + base, d_stage, end - base);  // returns synchronised
+      if (fits) {
+        xo.put(out + base, stage, end - base, packed);  // returns with up to 7 pieces in flight
+        RSK_HIP(hipEventRecord(out_done[ck & 1], c->xout));
+      }
+      t_d2h += ms(t0, now());
+    }
+    {
+      const auto t0 = now();
+      xo.drain();
       t_d2h += ms(t0, now());
     }
     if (trace)
@@ -1749,42 +1800,59 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     // encoding, exact dense length; the sparse opcodes are checked on the device.  One pass
     // over the headers (threads), leaving per string: bit 0 sparse, bit 1 a non-zero unused
     // header byte (kept as SET), bit 7 not an HLL string / too long (the first one fails).
-    std::vector<uint8_t> hf(n);
+    // Then the SETs of one key in one call: the last wins (a pass from the end marks each id
+    // once).  Both run on a helper thread while the strings go up (below); no string is
+    // checked on the device before its header passed.
+    std::vector<uint8_t> hf(n), apply(n, 0);
     std::atomic<uint64_t> first_bad{~0ull};
-    par_for(n, nth, [&](uint64_t lo, uint64_t hi) {
-      for (uint64_t i = lo; i < hi; ++i) {
-        const uint8_t* s = data + offsets[i];
-        const uint64_t len = offsets[i + 1] - offsets[i];
-        uint8_t f = 0;
-        if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1 || (s[4] == 0 && len != RSK_HLL_DENSE_BYTES) ||
-            len > (1ull << 31)) {
-          f = 0x80;
-          uint64_t cur = first_bad.load();
-          while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {
+    bool hdr_oom = false;
+    std::thread hdr([&] {
+      try {
+        par_for(n, nth, [&](uint64_t lo, uint64_t hi) {
+          for (uint64_t i = lo; i < hi; ++i) {
+            const uint8_t* s = data + offsets[i];
+            const uint64_t len = offsets[i + 1] - offsets[i];
+            uint8_t f = 0;
+            if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1 || (s[4] == 0 && len != RSK_HLL_DENSE_BYTES) ||
+                len > (1ull << 31)) {
+              f = 0x80;
+              uint64_t cur = first_bad.load();
+              while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {
+              }
+            } else {
+              f = (uint8_t)(s[4] | ((s[5] | s[6] | s[7]) ? 2 : 0));
+            }
+            hf[i] = f;
           }
-        } else {
-          f = (uint8_t)(s[4] | ((s[5] | s[6] | s[7]) ? 2 : 0));
-        }
-        hf[i] = f;
+        });
+        std::vector<uint8_t> seen(h->n, 0);
+        for (uint64_t i = n; i-- > 0;)
+          if (!seen[ids[i]]) {
+            seen[ids[i]] = 1;
+            apply[i] = 1;
+          }
+      } catch (const std::bad_alloc&) {
+        hdr_oom = true;
       }
     });
-    if (first_bad.load() != ~0ull) {
-      const uint64_t i = first_bad.load(), len = offsets[i + 1] - offsets[i];
-      const uint8_t* s = data + offsets[i];
-      if (len >= 16 && std::memcmp(s, "HYLL", 4) == 0 && s[4] <= 1 && !(s[4] == 0 && len != RSK_HLL_DENSE_BYTES))
-        need(false, "string too long");
-      fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value. (string " + std::to_string(i) + ")");
-    }
-    // SETs of one key in one call: the last wins (a pass from the end marks each id once)
-    std::vector<uint8_t> apply(n, 0);
-    {
-      std::vector<uint8_t> seen(h->n, 0);
-      for (uint64_t i = n; i-- > 0;)
-        if (!seen[ids[i]]) {
-          seen[ids[i]] = 1;
-          apply[i] = 1;
-        }
-    }
+    struct Join {
+      std::thread& t;
+      ~Join() {
+        if (t.joinable()) t.join();
+      }
+    } hj{hdr};
+    auto headers = [&] {  // the helper's verdict (the first bad header fails the call)
+      hdr.join();
+      if (hdr_oom) fail(RSK_ERR_OUT_OF_MEMORY, "host memory for the import's bookkeeping");
+      if (first_bad.load() != ~0ull) {
+        const uint64_t i = first_bad.load(), len = offsets[i + 1] - offsets[i];
+        const uint8_t* s = data + offsets[i];
+        if (len >= 16 && std::memcmp(s, "HYLL", 4) == 0 && s[4] <= 1 && !(s[4] == 0 && len != RSK_HLL_DENSE_BYTES))
+          need(false, "string too long");
+        fail(RSK_ERR_WRONGTYPE, "WRONGTYPE Key is not a valid HyperLogLog string value. (string " + std::to_string(i) +
+                                    ")");
+      }
+    };
     const uint64_t base = offsets[0], total = offsets[n] - base;
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
     uint8_t* w = c->work(al(8 * n) + al(8 * (n + 1)) + 2 * al(n) + 256 + al(total) + 256);
@@ -1798,13 +1866,48 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     for (uint64_t i = 0; i <= n; ++i) off[i] = offsets[i] - base;
     h2d_staged(c, reinterpret_cast<uint8_t*>(d_ids), reinterpret_cast<const uint8_t*>(ids), 8 * n);
     h2d_staged(c, reinterpret_cast<uint8_t*>(d_off), reinterpret_cast<const uint8_t*>(off.data()), 8 * (n + 1));
-    h2d_staged(c, d_apply, apply.data(), n);
-    const auto t0 = now();
-    h2d_staged(c, d_data, data + base, total);
-    const auto t1 = now();
     RSK_HIP(hipMemsetAsync(d_err, 0xFF, 8, c->stream));
     RSK_HIP(hipMemsetAsync(d_canon, 1, n, c->stream));
-    hll_import_launch(c, d_data, d_off, d_ids, nullptr, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
+    // The strings in 8 chunks of about equal bytes, each checked on the device as soon as it is
+    // there (the check of chunk q runs while chunk q + 1 crosses the link); the headers are in
+    // by the end of the first chunk.  The decode waits for every check (all or nothing).
+    // (the strings go up on the input copy stream, c->xin: a check kernel on the context
+    // stream would otherwise hold the next chunk's copies behind it)
+    constexpr uint64_t NCH = 8;
+    uint64_t cut[NCH + 1];
+    hipEvent_t up = nullptr;
+    RSK_HIP(hipEventCreateWithFlags(&up, hipEventDisableTiming));
+    struct EvFree {
+      hipEvent_t e;
+      ~EvFree() { (void)hipEventDestroy(e); }
+    } uf{up};
+    RSK_HIP(hipEventRecord(up, c->stream));  // ids / offsets staged first (same stages)
+    RSK_HIP(hipStreamWaitEvent(c->xin, up, 0));
+    cut[0] = 0;
+    cut[NCH] = n;
+    for (uint64_t q = 1; q < NCH; ++q)
+      cut[q] = std::max<uint64_t>(cut[q - 1], (uint64_t)(std::lower_bound(offsets, offsets + n, base + q * (total / NCH)) -
+                                                         offsets));
+    const auto t0 = now();
+    uint64_t checked = 0;  // chunks [0, checked) have their check queued
+    bool hdr_ok = false;
+    for (uint64_t q = 0; q < NCH; ++q) {
+      const uint64_t i0 = cut[q], i1 = cut[q + 1];
+      h2d_staged_on(c, c->xin, d_data + off[i0], data + offsets[i0], off[i1] - off[i0]);
+      RSK_HIP(hipEventRecord(up, c->xin));
+      RSK_HIP(hipStreamWaitEvent(c->stream, up, 0));  // chunk q's check after its strings
+      if (!hdr_ok) {
+        headers();
+        hdr_ok = true;
+      }
+      for (; checked <= q; ++checked) {
+        const uint64_t a = cut[checked], b = cut[checked + 1];
+        hll_import_launch(c, d_data, d_off + a, d_ids + a, nullptr, (uint32_t)(b - a), h->d_regs, h->d_card,
+                          d_canon + a, d_err, (uint32_t)a);
+      }
+    }
+    const auto t1 = now();
+    h2d_staged(c, d_apply, apply.data(), n);
     hll_import_launch(c, d_data, d_off, d_ids, d_apply, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
     std::vector<uint8_t> canon(n);
     unsigned long long err = 0;
@@ -1832,7 +1935,7 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
       }
     }
     if (trace)
-      std::fprintf(stderr, "import: host checks + metadata %.2f ms, h2d %.2f, kernels + sync %.2f, post %.2f\n",
+      std::fprintf(stderr, "import: metadata %.2f ms, strings up + checks %.2f, decode + sync %.2f, post %.2f\n",
                    ms(tA, t0), ms(t0, t1), ms(t1, t2), ms(t2, now()));
   });
 }

@@ -1059,8 +1059,13 @@ __global__ __launch_bounds__(GP_T) void hll_gapply_kernel(const uint32_t* __rest
 #pragma unroll
           for (int u = 0; u < GP_Q; ++u) {  // streaming stores: rows are written once, read back by later calls only
             const u32x4 x = {keep[u].x, keep[u].y, keep[u].z, keep[u].w};
-            if (plain_st) gp[u * 64 + lane] = x;  // (A/B: route gapply_st)
-            else __builtin_nontemporal_store(x, gp + u * 64 + lane);
+            if (plain_st == 2) {  // TIMING ONLY (route gapply_st = 2): no row stores (registers < 64: never true)
+              if (x[0] == 0xFFFFFFFFu) gp[u * 64 + lane] = x;
+            } else if (plain_st) {
+              gp[u * 64 + lane] = x;  // (A/B: route gapply_st)
+            } else {
+              __builtin_nontemporal_store(x, gp + u * 64 + lane);
+            }
           }
           if (est) {
             if (__any(kq.big != 0)) {  // a register >= 15 (rare here): the FP64 sum (uniform per wave = per sketch)

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(64) void hll_import_kernel(const uint8_t* __restric
                                                         const uint8_t* __restrict__ apply, uint32_t n,
                                                         uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
                                                         uint8_t* __restrict__ canon,
-                                                        unsigned long long* __restrict__ err) {
+                                                        unsigned long long* __restrict__ err, uint32_t i0) {
   __shared__ __attribute__((aligned(16))) ImWave<APPLY> S;
   const uint32_t lane = threadIdx.x;
   if (APPLY && *err != ~0ull) return;  // a string failed the check: nothing is written
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(64) void hll_import_kernel(const uint8_t* __restric
     if constexpr (!APPLY) {
       if (lane == 0) {
         canon[i] = can ? 1 : 0;
-        if (!ok) atomicMin(err, (unsigned long long)i);
+        if (!ok) atomicMin(err, (unsigned long long)(i0 + i));  // (i0: the chunk's first string in the call)
       }
     } else {
       wave_lds_sync();
@@ -405,16 +405,16 @@ void hll_export_pack_launch(rsk_ctx* c, const uint8_t* d_slots, const uint32_t* 
 
 void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_ids,
                        const uint8_t* d_apply, uint32_t n, uint8_t* d_regs, uint64_t* d_card, uint8_t* d_canon,
-                       unsigned long long* d_err) {
+                       unsigned long long* d_err, uint32_t i0) {
   if (!n) return;
   ProfScope ps(c, d_apply ? "hll_import_write" : "hll_import_check");
   // one wave per workgroup: the check pass holds 4 KiB of LDS (24 waves per CU), the decode 20 KiB (7 per CU)
   if (d_apply)
     hipLaunchKernelGGL(hll_import_kernel<true>, dim3(std::min<uint32_t>(n, (uint32_t)c->num_cus * 7)), dim3(64), 0,
-                       c->stream, d_data, d_off, d_ids, d_apply, n, d_regs, d_card, d_canon, d_err);
+                       c->stream, d_data, d_off, d_ids, d_apply, n, d_regs, d_card, d_canon, d_err, i0);
   else
     hipLaunchKernelGGL(hll_import_kernel<false>, dim3(std::min<uint32_t>(n, (uint32_t)c->num_cus * 24)), dim3(64), 0,
-                       c->stream, d_data, d_off, d_ids, d_apply, n, d_regs, d_card, d_canon, d_err);
+                       c->stream, d_data, d_off, d_ids, d_apply, n, d_regs, d_card, d_canon, d_err, i0);
   RSK_CHECK_LAUNCH("hll_import");
 }
 

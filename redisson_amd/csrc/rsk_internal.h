@@ -68,7 +68,7 @@ struct Tuning {
   int gpart_poison = 0;      // timing-free check: fill the fine-bin output with 0xFF first (a hole then shows)
   int io_trace = 0;          // batched export / import: host phase times to stderr
   int gpart_rt = 0;          // hll_gpart2t's round: 0 8192 records, 1 16384 (A/B)
-  int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B)
+  int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B), 2 none (TIMING ONLY)
   int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no
   int gpart_tile = 0;        // its tile-major first pass: 0 8192-record tiles (2 x 256 lanes per CU), 1 16384 (512 lanes)
   int route_vranks = 0;      // TEST ONLY, 1-rank communicator: the routed grouped add plans as rank route_vrank of
@@ -356,13 +356,14 @@ void hll_export_launch(rsk_ctx* c, const uint8_t* d_regs, const uint64_t* d_card
                        const uint8_t* d_want_sparse, uint32_t n, uint32_t* d_len, uint8_t* d_slots);
 void hll_export_pack_launch(rsk_ctx* c, const uint8_t* d_slots, const uint32_t* d_len, const uint64_t* d_pos,
                             uint32_t n, uint8_t* d_out);
-// Import: d_apply null -> check the sparse strings (atomicMin(d_err, i) on a
-// corrupt one; d_canon[i] = 0 where the payload is not the canonical
+// Import: d_apply null -> check the sparse strings (atomicMin(d_err, i0 + i)
+// on a corrupt one; d_canon[i] = 0 where the payload is not the canonical
 // encoding); d_apply given -> decode strings with d_apply[i] set into rows
-// d_ids[i] (and their card bytes), unless *d_err was set.
+// d_ids[i] (and their card bytes), unless *d_err was set.  A call may check
+// its strings in chunks (pointers advanced by the chunk's first string i0).
 void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_ids,
                        const uint8_t* d_apply, uint32_t n, uint8_t* d_regs, uint64_t* d_card, uint8_t* d_canon,
-                       unsigned long long* d_err);
+                       unsigned long long* d_err, uint32_t i0 = 0);
 
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);

@@ -80,7 +80,8 @@ for p in ${PART//,/ }; do
     c4var)  # C4 kernel variants interleaved (VARIANTS=..., scripts/var_variants.py)
       step c4var 300 python3 scripts/var_variants.py gpurun_out/c4var.json || exit 1 ;;
     io)  # batched Redis export / import of the C5 pool alone
-      step io 200 python3 scripts/io_profile.py 3 || exit 1 ;;
+      step io 200 python3 scripts/io_profile.py 3 ${IO_MERGES:-0} || exit 1
+      grep '^{' gpurun_out/io.log >> gpurun_out/${TAG}_io_profile.jsonl ;;
     chain)  # the C3 per-key arithmetic alone, in registers, at C3's size and boundary sizes
       for d in 9585058378 2147483648 2147483649 4294967297 8589934592 8589934593 17179869189 1099511627773 9007199254740993 4611686018427387909; do
         step chain_$d 60 scripts/bloom_chain_bench $d 7 || exit 1

@@ -2,7 +2,10 @@
 grouped pairs) alone in a process: wall time of each call and the device time
 of its kernels (rsk_hll_export_redis_batch / rsk_hll_import_redis_batch).
 
-  python scripts/io_profile.py [reps]   -> one JSON line"""
+  python scripts/io_profile.py [reps] [merges]   -> one JSON line
+
+merges: that many random mergeWith pairs after the add (the bench's C5 pool:
+10^5, which leaves ~95k destinations dense -- half the checkpoint's bytes)."""
 import json
 import os
 import sys
@@ -19,6 +22,7 @@ from redisson_amd.hyperloglog import GroupedHyperLogLog  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    merges = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     _lib.load()
     _lib.diag()
     eng = _lib.Engine(0)
@@ -30,6 +34,9 @@ def main():
     pool.add(k.keys_fixed(n, 16), g)
     g.free()
     k.free()
+    if merges:
+        rng = np.random.default_rng(5)
+        pool.mergeWith(rng.integers(0, G, size=merges, dtype=np.uint64), rng.integers(0, G, size=merges, dtype=np.uint64))
     ids = np.arange(G, dtype=np.uint64)
     data, offs = pool.exportRedis(ids)
     fresh = GroupedHyperLogLog(eng, G)
@@ -47,7 +54,7 @@ def main():
     eng.prof_enable(False)
     dev = {s: eng.prof_read(s)[0] / reps for s in ("hll_export_encode", "hll_export_pack", "hll_import_check",
                                                     "hll_import_write")}
-    print(json.dumps({"sketches": G, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
+    print(json.dumps({"sketches": G, "merges": merges, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
                       "device_ms": dev}), flush=True)
 
 
