@@ -47,6 +47,8 @@ const char *rsk_diag_last_error(void);
  *   gpart_rt      the fine-bin sort's round: 0 8192 records (default), 1 16384 (one
  *                 workgroup per CU)
  *   io_trace      1: the batched export / import print their host phase times to stderr
+ *   io_piece      batched export's copy-out pieces in MiB (0: 16)
+ *   io_drain      batched export: 1 = each chunk's copy-out finished before the next chunk (A/B)
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
  *   route_vranks  TEST ONLY, 1-rank communicator: rsk_hll_add_grouped_routed plans as rank route_vrank of
  *   route_vrank   route_vranks (its owned sub-range; records for the other owners are dropped)

@@ -203,6 +203,8 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "gapply_st") t.gapply_st = (int)value;
     else if (k == "gpart_rt") t.gpart_rt = (int)value;
     else if (k == "io_trace") t.io_trace = (int)value;
+    else if (k == "io_piece") t.io_piece = (int)value;
+    else if (k == "io_drain") t.io_drain = (int)value;
     else if (k == "reset") t = Tuning{};
     else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};
   });

@@ -382,6 +382,16 @@ class D2HStream {
       fifo_[(head_ + fifo_n_++) % 8] = Piece{dst + o, m, j};
     }
   }
+  // wait for event e, copying out the pieces whose DMA is done meanwhile (the ring keeps moving)
+  void service_until(hipEvent_t e) {
+    while (true) {
+      const hipError_t q = hipEventQuery(e);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) RSK_HIP(q);
+      if (fifo_n_ && hipEventQuery(c_->ring_ev[fifo_[head_].slot]) == hipSuccess) pop();
+      else std::this_thread::yield();
+    }
+  }
   ~D2HStream() {  // unwound by an error: no DMA may still fill a stage the next call refills
     if (fifo_n_) (void)hipStreamSynchronize(s_);
   }
@@ -684,6 +694,29 @@ void stop_done(rsk_ctx* c) {
 }  // namespace
 
 namespace {
+// Small host <-> device transfers by a kernel that reads or writes pinned host
+// memory directly (mapped into the device's address space): queued on the
+// context stream between kernels without going through a copy engine, so they
+// never wait behind a bulk DMA queued on the copy streams (the batched export's
+// per-chunk ids, flags, offsets and lengths).
+__global__ __launch_bounds__(256) void xfer_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   uint64_t n) {
+  const uint64_t n4 = n / 4;
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x)
+    d4[i] = s4[i];
+  const uint64_t t = 4 * n4 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) dst[t] = src[t];
+}
+void xfer(rsk_ctx* c, void* dst, const void* src, uint64_t n) {  // both 4-byte aligned
+  if (!n) return;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(512, (n / 4 + 255) / 256 + 1);
+  hipLaunchKernelGGL(xfer_kernel, dim3(blocks), dim3(256), 0, c->stream, static_cast<const uint8_t*>(src),
+                     static_cast<uint8_t*>(dst), n);
+  RSK_CHECK_LAUNCH("xfer");
+}
+
 // Rows of a partial lazy clear, zeroed by id: one workgroup per row, 16-byte stores.
 __global__ __launch_bounds__(256) void zero_rows_kernel(uint4* __restrict__ pool, const uint64_t* __restrict__ ids,
                                                         uint64_t n) {
@@ -1649,9 +1682,9 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     uint8_t* d_stage[2] = {d_slots + al(kc * (uint64_t)RSK_HLL_DENSE_BYTES),
                            d_slots + 2 * al(kc * (uint64_t)RSK_HLL_DENSE_BYTES)};
     std::vector<uint32_t> len(nd);
-    // the chunk's ids, flags, lengths and string offsets cross the link from pinned memory: a
-    // pageable copy would hold the host until the stream reaches it (the next chunk's encode
-    // queued behind this chunk's pack would then delay this chunk's copy-out by a whole encode)
+    // the chunk's ids, flags, lengths and string offsets live in pinned memory, moved by small
+    // kernels on the context stream (xfer): a pageable copy would hold the host until the stream
+    // reaches it, and a DMA would queue behind the bulk copy-out on the copy engine
     if (!c->h_io) RSK_HIP(hipHostMalloc(&c->h_io, 21 * KC, hipHostMallocDefault));
     uint64_t* h_ids = reinterpret_cast<uint64_t*>(c->h_io);
     uint64_t* pos = h_ids + KC;
@@ -1674,27 +1707,29 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       return d;
     };
     uint64_t dcur = 0;  // device keys whose offsets are final
-    auto encode = [&](uint64_t d0) {  // chunk d0's encode and its lengths, queued on the context stream
-      const uint64_t m = std::min<uint64_t>(kc, nd - d0);
-      std::memcpy(h_ids, dev_id.data() + d0, 8 * m);  // (the previous chunk's copies are done: synchronised)
-      std::memcpy(h_want, want.data() + d0, m);
-      RSK_HIP(hipMemcpyAsync(d_ids, h_ids, 8 * m, hipMemcpyHostToDevice, c->stream));
-      RSK_HIP(hipMemcpyAsync(d_want, h_want, m, hipMemcpyHostToDevice, c->stream));
-      hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)m, d_len, d_slots);
-      RSK_HIP(hipMemcpyAsync(h_len, d_len, 4 * m, hipMemcpyDeviceToHost, c->stream));
-    };
     // packed: chunk k's strings are in their stage; out_done[s]: the copy-out of stage s was queued
     // (chunk k + 2 packs into it after that, on the device)
-    hipEvent_t packed = nullptr, out_done[2] = {nullptr, nullptr};
+    hipEvent_t packed = nullptr, lens = nullptr, out_done[2] = {nullptr, nullptr};
     struct EvGuard {
-      hipEvent_t* e[3];
+      hipEvent_t* e[4];
       ~EvGuard() {
         for (hipEvent_t* p : e)
           if (*p) (void)hipEventDestroy(*p);
       }
-    } eg{{&packed, &out_done[0], &out_done[1]}};
+    } eg{{&packed, &lens, &out_done[0], &out_done[1]}};
+    auto encode = [&](uint64_t d0) {  // chunk d0's encode and its lengths, queued on the context stream
+      const uint64_t m = std::min<uint64_t>(kc, nd - d0);
+      std::memcpy(h_ids, dev_id.data() + d0, 8 * m);  // (the previous chunk's copies are done: synchronised)
+      std::memcpy(h_want, want.data() + d0, m);
+      xfer(c, d_ids, h_ids, 8 * m);  // (kernels, not copies: a copy here would queue behind the bulk D2H)
+      xfer(c, d_want, h_want, m);
+      hll_export_launch(c, h->d_regs, h->d_card, d_ids, d_want, (uint32_t)m, d_len, d_slots);
+      xfer(c, h_len, d_len, 4 * m);
+      RSK_HIP(hipEventRecord(lens, c->stream));
+    };
     if (nd) {
       RSK_HIP(hipEventCreateWithFlags(&packed, hipEventDisableTiming));
+      RSK_HIP(hipEventCreateWithFlags(&lens, hipEventDisableTiming));
       RSK_HIP(hipEventCreateWithFlags(&out_done[0], hipEventDisableTiming));
       RSK_HIP(hipEventCreateWithFlags(&out_done[1], hipEventDisableTiming));
       encode(0);
@@ -1702,7 +1737,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes and
     // packs; the pieces of every chunk go through one D2H stream (16 MiB pieces, up to 7 in
     // flight), so the copy engine runs on across chunk boundaries
-    D2HStream xo(c, c->xout, 16ull << 20);
+    D2HStream xo(c, c->xout, (c->tune.io_piece ? (uint64_t)c->tune.io_piece : 16ull) << 20);  // (A/B: io_piece MiB)
     const bool trace = c->tune.io_trace != 0;  // (route io_trace: phase times to stderr)
     double t_sync = 0, t_adv = 0, t_pack = 0, t_enc = 0, t_d2h = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -1712,7 +1747,8 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       const uint64_t m = std::min<uint64_t>(kc, nd - d0);
       uint8_t* stage = d_stage[ck & 1];
       auto t0 = now();
-      RSK_HIP(hipStreamSynchronize(c->stream));  // chunk d0's lengths (and the previous pack) done
+      if (c->tune.io_drain) RSK_HIP(hipEventSynchronize(lens));  // (A/B: route io_drain)
+      else xo.service_until(lens);  // chunk d0's lengths (and the previous pack) done; copy-outs meanwhile
       std::memcpy(len.data() + d0, h_len, 4 * m);
       auto t1 = now();
       t_sync += ms(t0, t1);
@@ -1725,7 +1761,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
         base = offsets[dev_i[d0]];
         end = offsets[dev_i[d0 + m - 1] + 1];
         for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
-        RSK_HIP(hipMemcpyAsync(d_pos, pos, 8 * m, hipMemcpyHostToDevice, c->stream));
+        xfer(c, d_pos, pos, 8 * m);
         if (ck >= 2) RSK_HIP(hipStreamWaitEvent(c->stream, out_done[ck & 1], 0));  // chunk k - 2 left this stage
         hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, stage);
         RSK_HIP(hipEventRecord(packed, c->stream));
@@ -1738,6 +1774,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       if (fits) {
         xo.put(out + base, stage, end - base, packed);  // returns with up to 7 pieces in flight
         RSK_HIP(hipEventRecord(out_done[ck & 1], c->xout));
+        if (c->tune.io_drain) xo.drain();  // (A/B: each chunk's copy-out finished before the next chunk)
       }
       t_d2h += ms(t0, now());
     }

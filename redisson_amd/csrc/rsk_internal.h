@@ -67,6 +67,8 @@ struct Tuning {
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
   int gpart_poison = 0;      // timing-free check: fill the fine-bin output with 0xFF first (a hole then shows)
   int io_trace = 0;          // batched export / import: host phase times to stderr
+  int io_piece = 0;          // batched export's copy-out pieces, MiB (0: 16)
+  int io_drain = 0;          // batched export: 1 = each chunk's copy-out drained before the next chunk (A/B)
   int gpart_rt = 0;          // hll_gpart2t's round: 0 8192 records, 1 16384 (A/B)
   int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B), 2 none (TIMING ONLY)
   int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no

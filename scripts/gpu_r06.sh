@@ -82,6 +82,12 @@ for p in ${PART//,/ }; do
     io)  # batched Redis export / import of the C5 pool alone
       step io 200 python3 scripts/io_profile.py 3 ${IO_MERGES:-0} || exit 1
       grep '^{' gpurun_out/io.log >> gpurun_out/${TAG}_io_profile.jsonl ;;
+    ioab)  # export / import routes A/B interleaved, one process each: IOAB="route=v,...;route=v,..."
+      IFS=';' read -ra FORMS <<< "${IOAB:-io_drain=0;io_drain=1}"
+      for m in ${IO_MERGES:-0 100000}; do for rep in 1 2; do for f in "${FORMS[@]}"; do
+        step ioab_$rep 200 python3 scripts/io_profile.py 3 $m "$f" || exit 1
+        grep '^{' gpurun_out/ioab_$rep.log >> gpurun_out/${TAG}_ioab.jsonl
+      done; done; done ;;
     chain)  # the C3 per-key arithmetic alone, in registers, at C3's size and boundary sizes
       for d in 9585058378 2147483648 2147483649 4294967297 8589934592 8589934593 17179869189 1099511627773 9007199254740993 4611686018427387909; do
         step chain_$d 60 scripts/bloom_chain_bench $d 7 || exit 1

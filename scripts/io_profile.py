@@ -2,7 +2,7 @@
 grouped pairs) alone in a process: wall time of each call and the device time
 of its kernels (rsk_hll_export_redis_batch / rsk_hll_import_redis_batch).
 
-  python scripts/io_profile.py [reps] [merges]   -> one JSON line
+  python scripts/io_profile.py [reps] [merges] [route=value,...]   -> one JSON line
 
 merges: that many random mergeWith pairs after the add (the bench's C5 pool:
 10^5, which leaves ~95k destinations dense -- half the checkpoint's bytes)."""
@@ -23,9 +23,12 @@ from redisson_amd.hyperloglog import GroupedHyperLogLog  # noqa: E402
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     merges = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    routes = dict(kv.split("=") for kv in sys.argv[3].split(",")) if len(sys.argv) > 3 and sys.argv[3] else {}
     _lib.load()
     _lib.diag()
     eng = _lib.Engine(0)
+    for k_, v_ in routes.items():
+        eng.set_route(k_, int(v_))
     if os.environ.get("IO_TRACE"):
         eng.set_route("io_trace", 1)  # host phase times of each call to stderr
     G, n = 1_000_000, 500_000_000
@@ -54,7 +57,7 @@ def main():
     eng.prof_enable(False)
     dev = {s: eng.prof_read(s)[0] / reps for s in ("hll_export_encode", "hll_export_pack", "hll_import_check",
                                                     "hll_import_write")}
-    print(json.dumps({"sketches": G, "merges": merges, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
+    print(json.dumps({"routes": routes, "sketches": G, "merges": merges, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
                       "device_ms": dev}), flush=True)
 
 
