@@ -129,33 +129,71 @@ def route_plan(groups, n: int, world: int):
     return owner, local, counts
 
 
-def hll_add_grouped_routed_cpu(records, groups, n: int, group=None):
+def hll_add_grouped_routed_cpu(records, groups, n: int, group=None, heavy_min: int = 0, stats=None):
     """The routed grouped add on CPU tensors, same plan as the GPU path:
     `records` (uint32 index << 6 | rank per pair, the hash taken where the
     pair lives) and `groups` of this rank's pairs; pairs sorted by owner, the
     per-owner counts then the 8-byte records {local id, record} exchanged
     all-to-all, each rank maxing what it receives into its owned rows.
-    Returns (first, count, owned rows [count][16384])."""
+    heavy_min > 0: groups with at least that many pairs here that another rank
+    owns are first folded into one local row each, and the rows (16384 bytes +
+    a 4-byte id) travel instead of their records (rsk_comm.hip; the device
+    takes the counts from a sample, this restatement the exact ones); the owner
+    maxes them into its rows.  stats (a dict) gets the bytes this rank
+    received.  Returns (first, count, owned rows [count][16384])."""
     import torch
     import torch.distributed as dist
 
     N, r = dist.get_world_size(group), dist.get_rank(group)
     owner, local, counts = route_plan(groups, n, N)
+    g = np.asarray(groups, dtype=np.uint64)
+    recs = np.asarray(records, np.uint32)
+    heavy = np.zeros(g.shape, bool)
+    hids = np.zeros(0, np.uint64)
+    if heavy_min > 0:
+        valid = owner >= 0
+        ids, cnt = np.unique(g[valid], return_counts=True)
+        hids = ids[(cnt >= heavy_min) & (owner_of(ids, n, N) != r)]  # ascending: each owner's rows contiguous
+        heavy = valid & np.isin(g, hids)
+    light = (owner >= 0) & ~heavy
+    lcounts = np.bincount(owner[light], minlength=N).astype(np.int64)
     order = np.argsort(owner, kind="stable")
-    order = order[owner[order] >= 0]
-    send = np.stack([local[order].astype(np.int64), np.asarray(records, np.uint32)[order].astype(np.int64)], 1)
-    cin = torch.zeros(N, dtype=torch.int64)
-    dist.all_to_all_single(cin, torch.from_numpy(counts.astype(np.int64)), group=group)
-    si, so = [int(x) for x in cin], [int(x) for x in counts]
+    order = order[light[order]]
+    send = np.stack([local[order].astype(np.int64), recs[order].astype(np.int64)], 1)
+    # heavy rows, folded here, and their ids (global), grouped by owner
+    hrows = np.zeros((hids.size, 16384), np.uint8)
+    if hids.size:
+        slot = np.searchsorted(hids, g[heavy])
+        rc = recs[heavy]
+        np.maximum.at(hrows, (slot, (rc >> 6).astype(np.int64)), (rc & 63).astype(np.uint8))
+    hcounts = np.bincount(owner_of(hids, n, N), minlength=N).astype(np.int64) if hids.size else np.zeros(N, np.int64)
+    cin = torch.zeros(2 * N, dtype=torch.int64)
+    dist.all_to_all_single(cin, torch.from_numpy(np.stack([lcounts, hcounts], 1).reshape(-1).copy()), group=group)
+    cin = cin.numpy().reshape(N, 2)
+    si, so = [int(x) for x in cin[:, 0]], [int(x) for x in lcounts]
     recv = torch.zeros(sum(si) * 2, dtype=torch.int64)
     dist.all_to_all_single(recv, torch.from_numpy(send.reshape(-1).copy()), output_split_sizes=[2 * x for x in si],
                            input_split_sizes=[2 * x for x in so], group=group)
     rec = recv.numpy().reshape(-1, 2)
+    hi_, ho = [int(x) for x in cin[:, 1]], [int(x) for x in hcounts]
+    rid = torch.zeros(sum(hi_), dtype=torch.int64)
+    dist.all_to_all_single(rid, torch.from_numpy(hids.astype(np.int64)), output_split_sizes=hi_,
+                           input_split_sizes=ho, group=group)
+    rrows = torch.zeros(sum(hi_) * 16384, dtype=torch.uint8)
+    dist.all_to_all_single(rrows, torch.from_numpy(hrows.reshape(-1).copy()), output_split_sizes=[16384 * x for x in hi_],
+                           input_split_sizes=[16384 * x for x in ho], group=group)
     first, count = owned_range(n, N, r)
     rows = np.zeros((count, 16384), np.uint8)
     if rec.size:
         idx, rank = (rec[:, 1] >> 6).astype(np.int64), (rec[:, 1] & 63).astype(np.uint8)
         np.maximum.at(rows, (rec[:, 0], idx), rank)
+    rr = rrows.numpy().reshape(-1, 16384)
+    for gid, row in zip(rid.numpy(), rr):
+        np.maximum(rows[int(gid) - first], row, out=rows[int(gid) - first])
+    if stats is not None:
+        own_light = int(lcounts[r])
+        stats["recv_bytes"] = 8 * (int(sum(si)) - own_light) + (16384 + 4) * int(sum(hi_))
+        stats["recv_rows"] = int(sum(hi_))
     return first, count, rows
 
 

@@ -187,6 +187,63 @@ def test_grouped_routed_owned_slices(world, G, orc):
     assert covered == G
 
 
+def _worker_routed_zipf(rank, world, port, G, n, heavy_min, q):
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from redisson_amd.shard import ShardPlan, hll_add_grouped_routed_cpu
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = ShardPlan(n, world).range(rank)
+        groups, keys = O.gen_grouped_zipf(0x5EED0006, G, 1.1, lo, hi - lo)
+        recs = O.hll_records(keys, 16, hi - lo)
+        st = {}
+        first, count, owned = hll_add_grouped_routed_cpu(recs, groups, G, heavy_min=heavy_min, stats=st)
+        q.put((rank, first, count, owned.tobytes(), st["recv_bytes"], st["recv_rows"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grouped_routed_zipf_heavy_rows_world3(orc):
+    """VERDICT r05 Next 2 on gloo: Zipf(1.1) groups at world 3, the routed add
+    with heavy groups pre-combined into rows at their source (groups owned
+    elsewhere with >= 64 pairs -- many rows -- or >= 2048, the library's
+    threshold) and without; all bit-exact against the single-process sketches,
+    and at the library's threshold rank 0 (the owner of the hot ids) receives
+    fewer bytes than with records only (at 64 pairs a 16 KiB row costs more
+    than its records: why the threshold is one row's worth of records)."""
+    world, G, n = 3, 3000, 300_000
+    ctx = mp.get_context("spawn")
+    out = {}
+    for hm in (0, 64, 2048):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker_routed_zipf, args=(r, world, port, G, n, hm, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out[hm] = sorted(q.get(timeout=240) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    groups, keys = orc.gen_grouped_zipf(0x5EED0006, G, 1.1, 0, n)
+    ref = np.zeros((G, orc.REGISTERS), np.uint8)
+    for gid in np.unique(groups):
+        sel = groups == gid
+        orc.hll_add(ref[gid], keys.reshape(-1, 16)[sel].reshape(-1), None, 16, int(sel.sum()))
+    for hm in (0, 64, 2048):
+        covered = 0
+        for rank, first, count, owned, _, _ in out[hm]:
+            assert first == covered
+            covered += count
+            assert owned == ref[first:first + count].tobytes(), (hm, rank)
+        assert covered == G
+    raw0, pre0 = out[0][0][4], out[2048][0][4]
+    assert out[64][0][5] > out[2048][0][5] > 0 and out[0][0][5] == 0  # rank 0 received rows only with the pre-combine
+    assert pre0 < 0.8 * raw0, (pre0, raw0)
+
+
 def _worker_fetch(rank, world, port, G, n, q):
     import torch.distributed as dist
 
