@@ -21,6 +21,9 @@
 #include <unordered_map>
 
 #include <pthread.h>
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <emmintrin.h>
+#endif
 
 #include "rsk_internal.h"
 
@@ -214,6 +217,38 @@ void check_out(const rsk_ctx* c, const rsk_keys* k, const void* out) {
 // The copy threads persist (one pool per process, grown on demand, one job
 // at a time): a staged copy is cut into ~8 pieces per call, and starting and
 // joining the threads per piece cost more than a 32 MiB piece's memcpy.
+// Host copies of the staged paths with streaming (non-temporal) 16-byte stores:
+// the destination is not read back soon (a user buffer filled from a stage, or
+// a stage the DMA reads next), and ordinary stores would first read every line
+// they write (read-for-ownership) -- a quarter of the host DRAM traffic of a
+// staged copy (DMA write + copy read + write + that read).
+void host_copy(uint8_t* dst, const uint8_t* src, uint64_t n, bool nt) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  if (nt && n >= 4096) {
+    uint64_t h = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+    std::memcpy(dst, src, h);
+    dst += h;
+    src += h;
+    n -= h;
+    const uint64_t m = n & ~uint64_t(63);
+    for (uint64_t i = 0; i < m; i += 64) {
+      const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+      const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+      const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+      const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    std::memcpy(dst + m, src + m, n - m);
+    _mm_sfence();  // the streamed lines are globally visible before the copy counts as done
+    return;
+  }
+#endif
+  std::memcpy(dst, src, n);
+}
+
 class CopyPool {
  public:
   static CopyPool& get() {
@@ -227,7 +262,7 @@ class CopyPool {
     return *inst_;
   }
   // slices 1 .. nt-1 on the workers, slice 0 on the caller
-  void run(uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t piece, unsigned nt) {
+  void run(uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t piece, unsigned nt, bool stream_st) {
     std::lock_guard<std::mutex> job(job_mu_);
     {
       std::unique_lock<std::mutex> lk(mu_);
@@ -241,11 +276,12 @@ class CopyPool {
       n_ = n;
       piece_ = piece;
       nt_ = nt;
+      stream_st_ = stream_st;
       pending_ = nt - 1;
       ++gen_;
     }
     cv_.notify_all();
-    std::memcpy(dst, src, std::min<uint64_t>(n, piece));
+    host_copy(dst, src, std::min<uint64_t>(n, piece), stream_st);
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [&] { return pending_ == 0; });
   }
@@ -256,6 +292,7 @@ class CopyPool {
       uint8_t* dst;
       const uint8_t* src;
       uint64_t lo, hi;
+      bool st;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
@@ -263,10 +300,11 @@ class CopyPool {
         if (t + 1 >= nt_) continue;  // not part of this job
         dst = dst_;
         src = src_;
+        st = stream_st_;
         lo = std::min<uint64_t>(n_, (uint64_t)(t + 1) * piece_);
         hi = std::min<uint64_t>(n_, lo + piece_);
       }
-      if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
+      if (hi > lo) host_copy(dst + lo, src + lo, hi - lo, st);
       std::lock_guard<std::mutex> lk(mu_);
       if (--pending_ == 0) done_cv_.notify_all();
     }
@@ -275,20 +313,22 @@ class CopyPool {
   std::mutex job_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   unsigned workers_ = 0, nt_ = 0, pending_ = 0;
+  bool stream_st_ = true;
   uint64_t gen_ = 0, n_ = 0, piece_ = 0;
   uint8_t* dst_ = nullptr;
   const uint8_t* src_ = nullptr;
 };
 
-void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n, unsigned threads) {
+// stream_st: streaming stores (host_copy); off only for A/B (route copy_nt = -1)
+void par_copy(uint8_t* dst, const uint8_t* src, uint64_t n, unsigned threads, bool stream_st = true) {
   const uint64_t min_piece = 2ull << 20;
   const unsigned nt = (unsigned)std::min<uint64_t>(threads, n / min_piece);
   if (nt <= 1) {
-    if (n) std::memcpy(dst, src, n);
+    if (n) host_copy(dst, src, n, stream_st);
     return;
   }
   const uint64_t piece = ((n + nt - 1) / nt + 4095) & ~uint64_t(4095);
-  CopyPool::get().run(dst, src, n, piece, nt);
+  CopyPool::get().run(dst, src, n, piece, nt, stream_st);
 }
 
 // f(lo, hi) over [0, n) on up to `threads` threads (slices of at least 64Ki
@@ -413,7 +453,7 @@ class D2HStream {
     head_ = (head_ + 1) % 8;
     --fifo_n_;
     RSK_HIP(hipEventSynchronize(c_->ring_ev[p.slot]));
-    par_copy(p.dst, slot(p.slot), p.bytes, c_->stage_threads);
+    par_copy(p.dst, slot(p.slot), p.bytes, c_->stage_threads, c_->tune.copy_nt >= 0);
   }
   rsk_ctx* c_;
   hipStream_t s_;
@@ -437,7 +477,7 @@ void h2d_staged_on(rsk_ctx* c, hipStream_t s, uint8_t* dst, const uint8_t* src, 
     const int slot = (int)(k & 1);
     const uint64_t n = std::min<uint64_t>(S, bytes - o);
     RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));  // the DMA that last read this stage is done
-    par_copy(c->h_pin[slot], src + o, n, c->stage_threads);
+    par_copy(c->h_pin[slot], src + o, n, c->stage_threads, c->tune.copy_nt >= 0);
     RSK_HIP(hipMemcpyAsync(dst + o, c->h_pin[slot], n, hipMemcpyHostToDevice, s));
     RSK_HIP(hipEventRecord(c->pin_ev[slot], s));
   }
