@@ -1932,7 +1932,32 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     };
     const uint64_t base = offsets[0], total = offsets[n] - base;
     auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-    uint8_t* w = c->work(al(8 * n) + al(8 * (n + 1)) + 2 * al(n) + 256 + al(total) + 256);
+    // Decode each chunk as soon as it is checked (overlapped with the next chunk's upload), with
+    // the rows it replaces copied aside first and copied back if a later string fails its check
+    // (all or nothing): when the copy (16 KiB + 8 B per string) fits in a quarter of the free
+    // device memory; otherwise every string is decoded after the last check.
+    const uint64_t base_bytes = al(8 * n) + al(8 * (n + 1)) + 2 * al(n) + 256 + al(total) + 256;
+    const uint64_t bak_bytes = al(n * (uint64_t)HLL_REGS) + al(8 * n);
+    bool early = false;
+    {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+        early = (double)bak_bytes < 0.25 * (double)(fr + (c->work_bytes >= base_bytes ? c->work_bytes - base_bytes : 0));
+      (void)hipGetLastError();
+    }
+    uint8_t* w = nullptr;
+    if (early) {
+      try {
+        w = c->work(base_bytes + bak_bytes);
+      } catch (const RskError& e) {
+        if (e.code != RSK_ERR_OUT_OF_MEMORY) throw;
+        (void)hipGetLastError();
+        early = false;
+      }
+    }
+    if (!early) w = c->work(base_bytes);
+    uint8_t* d_bak = w + base_bytes;
+    uint64_t* d_bak_card = reinterpret_cast<uint64_t*>(d_bak + al(n * (uint64_t)HLL_REGS));
     uint64_t* d_ids = reinterpret_cast<uint64_t*>(w);
     uint64_t* d_off = reinterpret_cast<uint64_t*>(w + al(8 * n));
     uint8_t* d_apply = w + al(8 * n) + al(8 * (n + 1));
@@ -1947,7 +1972,8 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     RSK_HIP(hipMemsetAsync(d_canon, 1, n, c->stream));
     // The strings in 8 chunks of about equal bytes, each checked on the device as soon as it is
     // there (the check of chunk q runs while chunk q + 1 crosses the link); the headers are in
-    // by the end of the first chunk.  The decode waits for every check (all or nothing).
+    // by the end of the first chunk.  Early: each chunk then decoded behind its check (its rows
+    // copied aside first); otherwise the decode waits for every check.
     // (the strings go up on the input copy stream, c->xin: a check kernel on the context
     // stream would otherwise hold the next chunk's copies behind it)
     constexpr uint64_t NCH = 8;
@@ -1976,16 +2002,27 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
       if (!hdr_ok) {
         headers();
         hdr_ok = true;
+        if (early) h2d_staged(c, d_apply, apply.data(), n);  // (the dedup is in with the headers)
       }
       for (; checked <= q; ++checked) {
         const uint64_t a = cut[checked], b = cut[checked + 1];
         hll_import_launch(c, d_data, d_off + a, d_ids + a, nullptr, (uint32_t)(b - a), h->d_regs, h->d_card,
                           d_canon + a, d_err, (uint32_t)a);
+        if (early) {
+          hll_rows_bak_launch(c, false, h->d_regs, h->d_card, d_ids + a, d_apply + a, (uint32_t)(b - a),
+                              d_bak + a * (uint64_t)HLL_REGS, d_bak_card + a, d_err);
+          hll_import_launch(c, d_data, d_off + a, d_ids + a, d_apply + a, (uint32_t)(b - a), h->d_regs, h->d_card,
+                            d_canon + a, d_err, (uint32_t)a);
+        }
       }
     }
     const auto t1 = now();
-    h2d_staged(c, d_apply, apply.data(), n);
-    hll_import_launch(c, d_data, d_off, d_ids, d_apply, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
+    if (early) {  // a failed check anywhere: every replaced row back as it was
+      hll_rows_bak_launch(c, true, h->d_regs, h->d_card, d_ids, d_apply, (uint32_t)n, d_bak, d_bak_card, d_err);
+    } else {
+      h2d_staged(c, d_apply, apply.data(), n);
+      hll_import_launch(c, d_data, d_off, d_ids, d_apply, (uint32_t)n, h->d_regs, h->d_card, d_canon, d_err);
+    }
     std::vector<uint8_t> canon(n);
     unsigned long long err = 0;
     RSK_HIP(hipMemcpyAsync(canon.data(), d_canon, n, hipMemcpyDeviceToHost, c->stream));

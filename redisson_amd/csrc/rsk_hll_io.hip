@@ -403,6 +403,49 @@ void hll_export_pack_launch(rsk_ctx* c, const uint8_t* d_slots, const uint32_t* 
   RSK_CHECK_LAUNCH("hll_export_pack");
 }
 
+// The import's decode per chunk (overlapped with the next chunk's upload) stays
+// all-or-nothing: before a chunk is decoded, the rows (and card words) its
+// strings will replace are copied aside (bak row i for string i), and if any
+// string of the call fails its check they are copied back.  One workgroup per
+// string with apply[i] set, 16-byte lanes.
+template <bool RESTORE>
+__global__ __launch_bounds__(256) void hll_rows_bak_kernel(uint4* __restrict__ regs, uint64_t* __restrict__ card,
+                                                           const uint64_t* __restrict__ ids,
+                                                           const uint8_t* __restrict__ apply, uint32_t n,
+                                                           uint4* __restrict__ bak, uint64_t* __restrict__ bak_card,
+                                                           const unsigned long long* __restrict__ err) {
+  constexpr uint32_t ROW_U4 = HLL_REGS / 16;
+  if (RESTORE && *err == ~0ull) return;  // every string passed: nothing to undo
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    if (!apply[i]) continue;
+    uint4* row = regs + ids[i] * ROW_U4;
+    uint4* b = bak + (uint64_t)i * ROW_U4;
+    for (uint32_t q = threadIdx.x; q < ROW_U4; q += 256) {
+      if (RESTORE) row[q] = b[q];
+      else b[q] = row[q];
+    }
+    if (threadIdx.x == 0) {
+      if (RESTORE) card[ids[i]] = bak_card[i];
+      else bak_card[i] = card[ids[i]];
+    }
+  }
+}
+
+void hll_rows_bak_launch(rsk_ctx* c, bool restore, uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
+                         const uint8_t* d_apply, uint32_t n, uint8_t* d_bak, uint64_t* d_bak_card,
+                         const unsigned long long* d_err) {
+  if (!n) return;
+  ProfScope ps(c, restore ? "hll_import_restore" : "hll_import_backup");
+  const dim3 g(std::min<uint32_t>(n, (uint32_t)c->num_cus * 8)), b(256);
+  if (restore)
+    hipLaunchKernelGGL(hll_rows_bak_kernel<true>, g, b, 0, c->stream, reinterpret_cast<uint4*>(d_regs), d_card, d_ids,
+                       d_apply, n, reinterpret_cast<uint4*>(d_bak), d_bak_card, d_err);
+  else
+    hipLaunchKernelGGL(hll_rows_bak_kernel<false>, g, b, 0, c->stream, reinterpret_cast<uint4*>(d_regs), d_card, d_ids,
+                       d_apply, n, reinterpret_cast<uint4*>(d_bak), d_bak_card, d_err);
+  RSK_CHECK_LAUNCH("hll_rows_bak");
+}
+
 void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_ids,
                        const uint8_t* d_apply, uint32_t n, uint8_t* d_regs, uint64_t* d_card, uint8_t* d_canon,
                        unsigned long long* d_err, uint32_t i0) {

@@ -367,6 +367,11 @@ void hll_export_pack_launch(rsk_ctx* c, const uint8_t* d_slots, const uint32_t* 
 void hll_import_launch(rsk_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_ids,
                        const uint8_t* d_apply, uint32_t n, uint8_t* d_regs, uint64_t* d_card, uint8_t* d_canon,
                        unsigned long long* d_err, uint32_t i0 = 0);
+// The rows (and card words) strings i with d_apply[i] will replace, copied to
+// d_bak row i (restore = false), or copied back if *d_err is set (restore).
+void hll_rows_bak_launch(rsk_ctx* c, bool restore, uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
+                         const uint8_t* d_apply, uint32_t n, uint8_t* d_bak, uint64_t* d_bak_card,
+                         const unsigned long long* d_err);
 
 // ---- Bloom launchers (rsk_bloom.hip)
 void bloom_add_launch(rsk_ctx* c, rsk_bloom* b, const DevKeys& k);

@@ -328,6 +328,46 @@ def test_import_batch_rejects_with_nothing_changed(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
+def test_import_batch_late_failure_restores_every_row(L, engine, orc):
+    """The batched SET decodes each upload chunk as soon as it is checked, with
+    the rows it replaces copied aside: a corrupt string in the LAST chunk must
+    still leave every key as it was -- registers, card bytes and GET bytes of
+    all 20000 keys equal to before the call -- and the same batch without the
+    corrupt string then lands whole."""
+    from redisson_amd import _lib
+
+    rng = np.random.default_rng(41)
+    n = 20000
+
+    def strings(seed_shift):
+        out = []
+        for i in range(n):
+            r = np.zeros(16384, np.uint8)
+            idx = rng.integers(0, 16384, size=int(rng.integers(1, 40)))
+            r[idx] = rng.integers(1, 20, size=idx.size)
+            out.append(bytes(orc.hll_encode_sparse(r)))
+        return out
+
+    first = strings(0)
+    h = _pool(L, engine, n)
+    ids = np.arange(n)
+    assert _import_batch(L, h, ids, first) == 0
+    rc, out0, offs0 = _export_batch(L, h, ids)
+    assert rc == 0
+    before = [_regs(L, h, i).copy() for i in (0, 1, n // 2, n - 2)]
+    second = strings(1)
+    bad = second[-1] + bytes([0x00])  # one register too many, at the very end of the batch
+    assert _import_batch(L, h, ids, second[:-1] + [bad]) == _lib.RSK_ERR_INVALID_HLL
+    rc, out1, offs1 = _export_batch(L, h, ids)
+    assert rc == 0 and np.array_equal(offs1, offs0) and np.array_equal(out1, out0)  # every key as it was
+    for j, i in enumerate((0, 1, n // 2, n - 2)):
+        assert np.array_equal(_regs(L, h, i), before[j]), i
+    assert _import_batch(L, h, ids, second) == 0
+    rc, out2, offs2 = _export_batch(L, h, ids)
+    assert rc == 0 and _strings(out2, offs2) == second
+    L.rsk_hll_destroy(h)
+
+
 def test_import_batch_every_sparse_shape(L, engine, orc):
     """Registers with runs of every opcode length at 64-byte step boundaries:
     XZERO second bytes in lane 63 and lane 0, runs of 1..4 VALs, zero runs of
