@@ -410,3 +410,47 @@ def test_routed_add_heavy_precombine(engine, orc, route, G, n, heavy, vranks, vr
         route(route_vranks=0, route_heavy=0)
         engine.prof_enable(False)
         _lib.check(L.rsk_comm_destroy(engine.ctx))
+
+
+def test_routed_add_c5_zipf_full_size_heavy_rows(engine, orc):
+    """BASELINE configs[4]'s Zipf(1.1) stress variant at its per-GPU size (1M
+    sketches, 500M pairs) through the routed add on one GPU with the self
+    exchange: the automatic heavy-group pre-combine folds the ~12k sketches of
+    >= 2048 pairs into rows (which then travel through RCCL to the owner and are
+    max-merged), the rest go as records.  The 1024 hottest sketches (~60 % of
+    the pairs, all of them heavy rows) are bit-exact against the oracle over the
+    whole stream, and their PFCOUNTs (the merged rows' precomputed estimates
+    retired)."""
+    import os
+
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    engine.prof_enable(True)
+    engine.prof_reset()
+    try:
+        G, n, gs = 1_000_000, 500_000_000, 1024
+        g, k = devmem.gen_grouped_zipf(engine, 0x5EED0006, G, 1.1, 0, n)
+        pool = GroupedHyperLogLog(engine, G)
+        pool.clear()
+        assert shard.hll_add_grouped_routed(pool.pool, k.keys_fixed(n, 16), g, flags=_lib.RSK_FETCH_SELF) == (0, G)
+        assert _prof(engine, "hll_route_heavy_rows") == 1
+        g.free()
+        k.free()
+        ref = np.zeros((gs, 16384), np.uint8)
+        orc.hll_add_gen_grouped_zipf_subset(ref, G, gs, 1.1, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
+        got = np.zeros((gs, 16384), np.uint8)
+        _lib.check(L.rsk_memcpy(engine.ctx, got.ctypes.data, L.rsk_hll_device_registers(pool.pool), got.nbytes, 1))
+        bad = np.nonzero((got != ref).any(1))[0]
+        assert bad.size == 0, (bad.size, bad[:10].tolist())
+        cnt = pool.count(ids=list(range(64)))
+        assert [int(c) for c in cnt] == [orc.hll_count_dense(ref[i]) for i in range(64)]
+        pool.close()
+        _lib.check(L.rsk_trim(engine.ctx))
+    finally:
+        engine.prof_enable(False)
+        _lib.check(L.rsk_comm_destroy(engine.ctx))
