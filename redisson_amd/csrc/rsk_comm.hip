@@ -402,15 +402,18 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     // 0. heavy groups (sampled counts): their pairs become local rows, not records
     std::vector<uint32_t> heavy_ids;
     uint32_t* d_slot_of = nullptr;
+    uint32_t* d_hbits = nullptr;
     uint64_t H = 0;
     if (heavy_try) {
-      const uint32_t stride = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, heavy_min / 8));
+      // ~32 samples at the threshold: a group of a quarter of it (Poisson 8) is almost never
+      // taken for heavy (1 group in 10^6 at Poisson 2 with 8 samples was ~1000 at C5 uniform)
+      const uint32_t stride = (uint32_t)std::max<uint64_t>(1, heavy_min / 32);
       const uint32_t thr = (uint32_t)std::max<uint64_t>(1, (heavy_min + stride - 1) / stride);
       // own groups stay records unless they too go through RCCL (self exchange)
       const uint64_t skip_lo = self ? 0 : first, skip_hi = self ? 0 : first + count;
       H = rsk::hll_heavy_select(c, groups, n, G, stride, thr, skip_lo, skip_hi, HEAVY_CAP, d_hscratch, &d_slot_of,
-                                &heavy_ids);
-      if (!H) d_slot_of = nullptr;
+                                &d_hbits, &heavy_ids);
+      if (!H) d_slot_of = d_hbits = nullptr;
     }
     std::vector<uint64_t> hrows(N, 0), hfirst(N + 1, 0);  // heavy rows per owner, their first slot
     rsk::plan_heavy_rows(G, N, heavy_ids.data(), H, &hrows);
@@ -421,7 +424,7 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     // per peer j: [2j] records for j, [2j + 1] heavy rows for j; received into [2N + 2j], [2N + 2j + 1]
     std::vector<uint64_t> scnt(4 * N, 0);
     if (n) {
-      rsk::hll_route_count_launch(c, groups, n, G, (uint32_t)N, d_slot_of, d_cnt);
+      rsk::hll_route_count_launch(c, groups, n, G, (uint32_t)N, d_slot_of, d_hbits, d_cnt);
       RSK_HIP(hipMemcpyAsync(cnt.data(), d_cnt, 4 * NO * B, hipMemcpyDeviceToHost, c->stream));
       RSK_HIP(hipStreamSynchronize(c->stream));
     }
@@ -510,7 +513,7 @@ int rsk_hll_add_grouped_routed(rsk_hll* h, const rsk_keys* keys, const uint32_t*
     if (n) {
       RSK_HIP(hipMemcpyAsync(d_off, off.data(), 8 * NO * B, hipMemcpyHostToDevice, c->stream));
       rsk::hll_route_scatter_launch(c, reinterpret_cast<const uint8_t*>(keys->data), groups, n, G, (uint32_t)N,
-                                    d_slot_of, d_off, d_send);
+                                    d_slot_of, d_hbits, d_off, d_send);
     }
     // 5. heavy pairs folded into local rows (the record pipeline onto a pool of the H heavy
     // groups; it reuses the context's work buffer, which holds nothing live from here on)

@@ -1494,6 +1494,7 @@ RSK_DEV uint32_t route_owner(uint32_t g, uint64_t q, uint32_t N) {
 __global__ __launch_bounds__(RT_T) void hll_route_count_kernel(const uint32_t* __restrict__ groups, uint64_t n,
                                                                uint64_t per, uint64_t G, uint32_t N,
                                                                const uint32_t* __restrict__ slot_of,
+                                                               const uint32_t* __restrict__ hbits,
                                                                uint32_t* __restrict__ cnt) {
   __shared__ uint32_t h[RT_MAXN + 1];
   const uint32_t NO = N + (slot_of ? 1u : 0u);  // owners + the heavy run
@@ -1507,7 +1508,7 @@ __global__ __launch_bounds__(RT_T) void hll_route_count_kernel(const uint32_t* _
     const uint32_t g = __builtin_nontemporal_load(&groups[i]);
     if (g >= G) continue;
     uint32_t o = route_owner(g, q, N);
-    if (slot_of && slot_of[g] != 0xFFFFFFFFu) o = N;
+    if (slot_of && ((hbits[g >> 5] >> (g & 31)) & 1u)) o = N;  // (a 128 KiB bitmap at 1M groups: stays in L2)
     if (o < 8) {
 #pragma unroll
       for (uint32_t k = 0; k < 8; ++k) mine[k] += o == k;
@@ -1526,6 +1527,7 @@ __global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __
                                                                  const uint32_t* __restrict__ groups, uint64_t n,
                                                                  uint64_t per, uint64_t G, uint32_t N,
                                                                  const uint32_t* __restrict__ slot_of,
+                                                                 const uint32_t* __restrict__ hbits,
                                                                  const uint64_t* __restrict__ off,
                                                                  uint2* __restrict__ out) {
   __shared__ unsigned long long cur[RT_MAXN + 1];
@@ -1549,12 +1551,9 @@ __global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __
       ir = (hll_index(hsh) << 6) | hll_rank(hsh);
       o = route_owner(g, q, N);
       gl = (uint32_t)(g - (uint64_t)o * q);
-      if (slot_of) {
-        const uint32_t sl = slot_of[g];
-        if (sl != 0xFFFFFFFFu) {
-          o = N;
-          gl = sl;
-        }
+      if (slot_of && ((hbits[g >> 5] >> (g & 31)) & 1u)) {  // heavy: the slot table only for its pairs
+        o = N;
+        gl = slot_of[g];
       }
     }
     uint64_t pending = __ballot(valid);
@@ -1572,12 +1571,24 @@ __global__ __launch_bounds__(RT_T) void hll_route_scatter_kernel(const uint4* __
 }
 
 // Heavy-group detection: a sampled count per group (every stride-th pair of each
-// block's range; one atomic per distinct group in a wave, so a hot group costs
-// one atomic per wave, not one per pair), then flags, an exclusive scan (slots in
-// group order, so each owner's heavy rows are one contiguous range) and the slots.
+// block's range), then flags, an exclusive scan (slots in group order, so each
+// owner's heavy rows are one contiguous range), the slots and a bitmap of the
+// heavy groups.  A wave folds its samples of one group into one count; a block
+// keeps its counts in a small LDS table (keyed by group, first come first
+// served; a sample whose slot another group holds goes to HBM directly) and
+// flushes it once, so a Zipf-hot group costs one global atomic per block, not
+// one per wave (under Zipf(1.1) one group is 12 % of all pairs: the per-wave
+// atomics on its counter took 3.5 ms).
+constexpr uint32_t RS_SLOTS = 1024;
 __global__ __launch_bounds__(RT_T) void hll_route_sample_kernel(const uint32_t* __restrict__ groups, uint64_t n,
                                                                 uint64_t per, uint64_t G, uint32_t stride,
                                                                 uint32_t* __restrict__ hist) {
+  __shared__ uint32_t skey[RS_SLOTS], scnt[RS_SLOTS];
+  for (uint32_t q = threadIdx.x; q < RS_SLOTS; q += RT_T) {
+    skey[q] = 0xFFFFFFFFu;
+    scnt[q] = 0;
+  }
+  __syncthreads();
   uint64_t begin, end;
   key_range(n, per, &begin, &end);
   const uint32_t lane = threadIdx.x & 63;
@@ -1589,10 +1600,22 @@ __global__ __launch_bounds__(RT_T) void hll_route_sample_kernel(const uint32_t* 
     while (pending) {
       const uint32_t gg = (uint32_t)__builtin_amdgcn_readlane((int)g, __builtin_ctzll(pending));
       const uint64_t m = __ballot(valid && g == gg) & pending;
-      if ((int)lane == __builtin_ctzll(m)) atomicAdd(&hist[gg], (uint32_t)__popcll(m));
+      if ((int)lane == __builtin_ctzll(m)) {
+        const uint32_t sl = (gg * 2654435761u) >> 22;  // 10 bits
+        uint32_t k = skey[sl];
+        if (k == 0xFFFFFFFFu) {
+          k = atomicCAS(&skey[sl], 0xFFFFFFFFu, gg);  // the slot's previous key: empty means it is ours now
+          if (k == 0xFFFFFFFFu) k = gg;
+        }
+        if (k == gg) atomicAdd(&scnt[sl], (uint32_t)__popcll(m));
+        else atomicAdd(&hist[gg], (uint32_t)__popcll(m));
+      }
       pending &= ~m;
     }
   }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < RS_SLOTS; q += RT_T)
+    if (scnt[q]) atomicAdd(&hist[skey[q]], scnt[q]);
 }
 
 // groups in [skip_lo, skip_hi) (the rank's own: no transfer to save) are never heavy
@@ -1609,12 +1632,24 @@ __global__ __launch_bounds__(256) void hll_heavy_flag_kernel(uint32_t* __restric
 __global__ __launch_bounds__(256) void hll_heavy_slot_kernel(const uint32_t* __restrict__ hist,
                                                              const uint32_t* __restrict__ pos, uint64_t G, uint32_t thr,
                                                              uint32_t cap, uint32_t* __restrict__ slot_of,
-                                                             uint32_t* __restrict__ heavy_ids) {
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = pos[g];
-    const bool hv = hist[g] >= thr && p < cap;
-    slot_of[g] = hv ? p : 0xFFFFFFFFu;
-    if (hv) heavy_ids[p] = (uint32_t)g;
+                                                             uint32_t* __restrict__ heavy_ids,
+                                                             uint32_t* __restrict__ hbits) {
+  // grid-stride in whole waves: a wave's 64 groups are two bitmap words
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < G; g0 += stride) {
+    const uint64_t g = g0 + (threadIdx.x & 63u);
+    bool hv = false;
+    if (g < G) {
+      const uint32_t p = pos[g];
+      hv = hist[g] >= thr && p < cap;
+      slot_of[g] = hv ? p : 0xFFFFFFFFu;
+      if (hv) heavy_ids[p] = (uint32_t)g;
+    }
+    const uint64_t b = __ballot(hv);
+    if ((threadIdx.x & 63u) == 0) {
+      hbits[g0 >> 5] = (uint32_t)b;
+      if (g0 + 32 < G) hbits[(g0 >> 5) + 1] = (uint32_t)(b >> 32);
+    }
   }
 }
 
@@ -1639,22 +1674,23 @@ __global__ __launch_bounds__(256) void hll_add_grouped_rec_kernel(const uint2* _
 uint32_t route_blocks(const rsk_ctx* c) { return (uint32_t)c->num_cus * 4; }
 
 void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N,
-                            const uint32_t* d_slot_of, uint32_t* d_cnt) {
+                            const uint32_t* d_slot_of, const uint32_t* d_hbits, uint32_t* d_cnt) {
   const uint32_t B = route_blocks(c);
   const uint64_t per = (n + B - 1) / B;
   ProfScope ps(c, "hll_route");
   hipLaunchKernelGGL(hll_route_count_kernel, dim3(B), dim3(RT_T), 0, c->stream, d_groups, n, per, G, N, d_slot_of,
-                     d_cnt);
+                     d_hbits, d_cnt);
   RSK_CHECK_LAUNCH("hll_route_count");
 }
 
 void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
-                              uint32_t N, const uint32_t* d_slot_of, const uint64_t* d_off, uint2* d_out) {
+                              uint32_t N, const uint32_t* d_slot_of, const uint32_t* d_hbits, const uint64_t* d_off,
+                              uint2* d_out) {
   const uint32_t B = route_blocks(c);
   const uint64_t per = (n + B - 1) / B;
   ProfScope ps(c, "hll_route");
   hipLaunchKernelGGL(hll_route_scatter_kernel, dim3(B), dim3(RT_T), 0, c->stream,
-                     reinterpret_cast<const uint4*>(d_keys16), d_groups, n, per, G, N, d_slot_of, d_off, d_out);
+                     reinterpret_cast<const uint4*>(d_keys16), d_groups, n, per, G, N, d_slot_of, d_hbits, d_off, d_out);
   RSK_CHECK_LAUNCH("hll_route_scatter");
 }
 
@@ -1663,12 +1699,12 @@ uint64_t hll_heavy_scratch_bytes(uint64_t G, uint32_t cap) {
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(G + 1),
                                          (hipStream_t)0);
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  return al(4 * G) + 2 * al(4 * (G + 1)) + al(4ull * cap) + al(sb);
+  return al(4 * G) + 2 * al(4 * (G + 1)) + al(4ull * cap) + al(sb) + al(4 * ((G + 63) / 64 * 2));
 }
 
 uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t stride, uint32_t thr,
                           uint64_t skip_lo, uint64_t skip_hi, uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of,
-                          std::vector<uint32_t>* heavy_ids) {
+                          uint32_t** d_hbits, std::vector<uint32_t>* heavy_ids) {
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* pos = reinterpret_cast<uint32_t*>(scratch + al(4 * G));
@@ -1678,6 +1714,7 @@ uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint
   size_t sb = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(G + 1),
                                          c->stream);
+  uint32_t* hb = reinterpret_cast<uint32_t*>(tmp + al(sb));
   const uint32_t B = route_blocks(c);
   const uint64_t per = (n + B - 1) / B;
   const uint32_t gb = (uint32_t)std::min<uint64_t>((G + 256) / 256, 4096);
@@ -1689,7 +1726,7 @@ uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint
     hipLaunchKernelGGL(hll_heavy_flag_kernel, dim3(gb), dim3(256), 0, c->stream, hist, G, thr, skip_lo, skip_hi, pos);
     RSK_CHECK_LAUNCH("hll_heavy_flag");
     RSK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, sb, pos, pos, (int)(G + 1), c->stream));
-    hipLaunchKernelGGL(hll_heavy_slot_kernel, dim3(gb), dim3(256), 0, c->stream, hist, pos, G, thr, cap, slot, ids);
+    hipLaunchKernelGGL(hll_heavy_slot_kernel, dim3(gb), dim3(256), 0, c->stream, hist, pos, G, thr, cap, slot, ids, hb);
     RSK_CHECK_LAUNCH("hll_heavy_slot");
   }
   uint32_t total = 0;
@@ -1702,6 +1739,7 @@ uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint
     RSK_HIP(hipStreamSynchronize(c->stream));
   }
   *d_slot_of = slot;
+  *d_hbits = hb;
   return H;
 }
 

@@ -393,19 +393,21 @@ bool hll_add_grouped_partitioned(rsk_ctx* c, const DevKeys& k, const uint32_t* d
 // hashed into 8-byte records appended to owner o's run at off[o * B + b].
 uint32_t route_blocks(const rsk_ctx* c);
 void hll_route_count_launch(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t N,
-                            const uint32_t* d_slot_of, uint32_t* d_cnt);
+                            const uint32_t* d_slot_of, const uint32_t* d_hbits, uint32_t* d_cnt);
 void hll_route_scatter_launch(rsk_ctx* c, const uint8_t* d_keys16, const uint32_t* d_groups, uint64_t n, uint64_t G,
-                              uint32_t N, const uint32_t* d_slot_of, const uint64_t* d_off, uint2* d_out);
+                              uint32_t N, const uint32_t* d_slot_of, const uint32_t* d_hbits, const uint64_t* d_off,
+                              uint2* d_out);
 // Heavy groups of a routed add (skew): sampled counts (every stride-th pair), a
 // group is heavy when its sample count reaches thr and it lies outside
 // [skip_lo, skip_hi); at most cap, by group id.
 // scratch: hll_heavy_scratch_bytes(G, cap) of device memory; *d_slot_of points
-// into it (a group's slot, ~0 if light), heavy_ids gets the heavy groups
-// ascending (slot order).  Returns their number; synchronises the stream.
+// into it (a group's slot, ~0 if light), *d_hbits to the bitmap of the heavy
+// groups, heavy_ids gets the heavy groups ascending (slot order).  Returns
+// their number; synchronises the stream.
 uint64_t hll_heavy_scratch_bytes(uint64_t G, uint32_t cap);
 uint64_t hll_heavy_select(rsk_ctx* c, const uint32_t* d_groups, uint64_t n, uint64_t G, uint32_t stride, uint32_t thr,
                           uint64_t skip_lo, uint64_t skip_hi, uint32_t cap, uint8_t* scratch, uint32_t** d_slot_of,
-                          std::vector<uint32_t>* heavy_ids);
+                          uint32_t** d_hbits, std::vector<uint32_t>* heavy_ids);
 // Records into a pool of G rows (partitioned for large batches, else a CAS each);
 // write_all: every row written (zero rows for sketches without records).
 void hll_add_grouped_recs_launch(rsk_ctx* c, const uint2* d_recs, uint64_t n, uint8_t* d_regs, uint64_t G,

@@ -127,6 +127,16 @@ for p in ${PART//,/ }; do
     replies)
       profw pmc_replies 200 1000000000 '{"workload": "bloom_add_replies", "keys": 1000000000, "zipf": 0.0, "bloom_keys": 1000000000}' \
         python3 scripts/reply_profile.py 1000000000 1 || exit 1 ;;
+    routed)  # the routed add at C5 size through the self exchange, heavy pre-combine on / off, uniform and Zipf
+      for z in 0 1.1; do for rep in 1 2; do for f in "" "route_heavy=-1"; do
+        step routed_$rep 150 python3 scripts/routed_profile.py 3 $z "$f" || exit 1
+        grep '^{' gpurun_out/routed_$rep.log >> gpurun_out/${TAG}_routed.jsonl
+      done; done; done ;;
+    d2hx)  # the link / host-copy probe in two successive processes, then the export twice (process-order effects)
+      for rep in 1 2; do
+        step d2h_$rep 120 python3 scripts/d2h_probe.py || exit 1
+        grep '^{' gpurun_out/d2h_$rep.log >> gpurun_out/${TAG}_d2h_probe.jsonl
+      done ;;
     p2p)  # >2 GB self send/recv probe (rsk_diag_p2p_probe): one uint8 / one uint64 transfer / 1 GiB pieces
       step p2p 300 python3 scripts/p2p_probe.py $P2P_SIZES || exit 1
       grep '^{' gpurun_out/p2p.log >> gpurun_out/${TAG}_p2p_probe.jsonl ;;
