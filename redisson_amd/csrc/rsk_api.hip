@@ -2031,21 +2031,35 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     const auto t2 = now();
     if (err != ~0ull)
       fail(RSK_ERR_INVALID_HLL, "INVALIDOBJ Corrupted HLL object detected (string " + std::to_string(err) + ")");
-    for (uint64_t i = 0; i < n; ++i) {
-      if (!apply[i]) continue;
-      const uint64_t id = ids[i];
-      const uint64_t len = offsets[i + 1] - offsets[i];
-      const bool sparse = hf[i] & 1;
-      h->exists[id] = 1;
-      h->dense[id] = !sparse;
-      // a copy only where the canonical re-encoding would differ (as rsk_hll_import_redis)
-      bool canonical = !(hf[i] & 2);
-      if (canonical && sparse) canonical = canon[i] && len <= HLL_SPARSE_MAX_BYTES;
-      if (canonical) {
-        hll_forget_import(h, id);
-      } else {
-        const uint8_t* s = data + offsets[i];
-        h->imported[id].assign(s, s + len);
+    // host state per SET (the ids with apply[i] are distinct): exists / dense on threads; the
+    // kept strings (a copy only where the canonical re-encoding would differ, as
+    // rsk_hll_import_redis) and the forgotten ones in one serial pass over those only
+    std::atomic<uint64_t> n_keep{0};
+    par_for(n, nth, [&](uint64_t lo, uint64_t hi) {
+      uint64_t k = 0;
+      for (uint64_t i = lo; i < hi; ++i) {
+        if (!apply[i]) continue;
+        const uint64_t id = ids[i];
+        const bool sparse = hf[i] & 1;
+        h->exists[id] = 1;
+        h->dense[id] = !sparse;
+        bool canonical = !(hf[i] & 2);
+        if (canonical && sparse) canonical = canon[i] && offsets[i + 1] - offsets[i] <= HLL_SPARSE_MAX_BYTES;
+        canon[i] = canonical ? 1 : 0;  // (from here: 1 = re-encode, 0 = keep the SET string)
+        k += !canonical;
+      }
+      n_keep += k;
+    });
+    if (n_keep.load() || !h->imported.empty()) {
+      for (uint64_t i = 0; i < n; ++i) {
+        if (!apply[i]) continue;
+        const uint64_t id = ids[i];
+        if (canon[i]) {
+          hll_forget_import(h, id);
+        } else {
+          const uint8_t* s = data + offsets[i];
+          h->imported[id].assign(s, s + (offsets[i + 1] - offsets[i]));
+        }
       }
     }
     if (trace)
