@@ -119,6 +119,17 @@ int rsk_sync(rsk_ctx *ctx);
  * replies pipeline up to ~165 GB at 1B keys); it is kept for the next call
  * otherwise.  Waits for the context's queued work. */
 int rsk_trim(rsk_ctx *ctx);
+/* Pin a caller's pageable host buffer in place (hipHostRegister) for as long
+ * as the caller keeps it registered -- a long-lived buffer reused across calls,
+ * like a Java direct ByteBuffer holding checkpoints.  The batched export /
+ * import (rsk_hll_export_redis_batch / import_redis_batch) and staged key
+ * batches then move data between HBM and a registered range by DMA straight
+ * to / from it, instead of through the library's pinned stages and a host
+ * copy.  A range may not overlap one already registered; rsk_host_unregister
+ * takes the pointer given to rsk_host_register; rsk_shutdown unregisters what
+ * is left. */
+int rsk_host_register(rsk_ctx *ctx, void *ptr, uint64_t bytes);
+int rsk_host_unregister(rsk_ctx *ctx, void *ptr);
 /* Per-kernel device-time accounting with HIP events on the context stream
  * (used by bench.py for the roofline; off by default). */
 int rsk_prof_enable(rsk_ctx *ctx, int on);

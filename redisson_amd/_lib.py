@@ -96,6 +96,8 @@ SIGNATURES = {
     "rsk_ctx_stream": (_vp, [_vp]),
     "rsk_sync": (ctypes.c_int, [_vp]),
     "rsk_trim": (ctypes.c_int, [_vp]),
+    "rsk_host_register": (ctypes.c_int, [_vp, _vp, _u64]),
+    "rsk_host_unregister": (ctypes.c_int, [_vp, _vp]),
     "rsk_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rsk_prof_reset": (ctypes.c_int, [_vp]),
     "rsk_prof_read": (ctypes.c_int, [_vp, ctypes.c_char_p, _P(ctypes.c_double), _P(_u64)]),
@@ -357,6 +359,15 @@ class Engine:
 
     def sync(self):
         check(self.lib.rsk_sync(self.ctx))
+
+    def host_register(self, arr):
+        """Pin a numpy array's memory in place (rsk_host_register): transfers
+        to / from it skip the library's pinned stages.  Keep `arr` alive until
+        host_unregister(arr)."""
+        check(self.lib.rsk_host_register(self.ctx, arr.ctypes.data, arr.nbytes))
+
+    def host_unregister(self, arr):
+        check(self.lib.rsk_host_unregister(self.ctx, arr.ctypes.data))
 
     def prof_enable(self, on=True):
         check(self.lib.rsk_prof_enable(self.ctx, 1 if on else 0))

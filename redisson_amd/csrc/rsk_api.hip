@@ -409,7 +409,7 @@ class D2HStream {
   // bytes from device src to host dst, on the stream after event `after` (when not null)
   void put(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipEvent_t after) {
     if (after) RSK_HIP(hipStreamWaitEvent(s_, after, 0));
-    if (c_->pin_off) {
+    if (c_->pin_off || c_->host_registered(dst, bytes)) {  // (a registered range: DMA straight into it)
       if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_));
       return;
     }
@@ -468,7 +468,7 @@ class D2HStream {
 // soon as the DMA that last read it is done, whichever call issued it).
 void h2d_staged_on(rsk_ctx* c, hipStream_t s, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
   ensure_pinned(c);
-  if (c->pin_off) {
+  if (c->pin_off || c->host_registered(src, bytes)) {  // (a registered range: DMA straight from it)
     if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     return;
   }
@@ -962,6 +962,8 @@ int rsk_shutdown(rsk_ctx* c) {
     c->async_all.clear();
     c->async_free.clear();
     if (c->comm) (void)rsk_comm_destroy(c);
+    for (const auto& r : c->host_regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+    c->host_regs.clear();
     (void)hipStreamDestroy(c->stream);
     if (c->xin) (void)hipStreamDestroy(c->xin);
     if (c->xout) (void)hipStreamDestroy(c->xout);
@@ -971,6 +973,34 @@ int rsk_shutdown(rsk_ctx* c) {
 }
 
 void* rsk_ctx_stream(rsk_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int rsk_host_register(rsk_ctx* c, void* p, uint64_t bytes) {
+  return guarded([&] {
+    need(c && p && bytes, "NULL argument or empty range");
+    CtxLock l(c);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (const auto& r : c->host_regs)
+      need(a + bytes <= r.first || a >= r.first + r.second, "range overlaps a registered one");
+    RSK_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    c->host_regs.push_back({a, bytes});
+  });
+}
+
+int rsk_host_unregister(rsk_ctx* c, void* p) {
+  return guarded([&] {
+    need(c && p, "NULL argument");
+    CtxLock l(c);
+    // no queued transfer may still use the range
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    RSK_HIP(hipStreamSynchronize(c->xin));
+    RSK_HIP(hipStreamSynchronize(c->xout));
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = std::find_if(c->host_regs.begin(), c->host_regs.end(), [&](const auto& r) { return r.first == a; });
+    need(it != c->host_regs.end(), "not a registered range");
+    c->host_regs.erase(it);
+    RSK_HIP(hipHostUnregister(p));
+  });
+}
 
 int rsk_trim(rsk_ctx* c) {
   return guarded([&] {

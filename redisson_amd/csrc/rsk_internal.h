@@ -223,6 +223,15 @@ struct rsk_ctx {
 
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);
+  // host ranges the caller registered (rsk_host_register): [start, start + bytes)
+  std::vector<std::pair<uintptr_t, uint64_t>> host_regs;
+  bool host_registered(const void* p, uint64_t bytes) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (const auto& r : host_regs)
+      if (a >= r.first && a + bytes <= r.first + r.second) return true;
+    return false;
+  }
+
   uint8_t* xbuf(uint64_t bytes);
   uint8_t* sbuf(uint64_t bytes);
   uint8_t* hrows(uint64_t bytes);

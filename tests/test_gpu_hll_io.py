@@ -506,3 +506,41 @@ def test_c5_pool_checkpoint_round_trip(L, engine, orc):
     assert np.array_equal(offs2, offs) and np.array_equal(data2, data)
     pool.close()
     pool2.close()
+
+
+def test_export_import_through_registered_host_buffers(L, engine, orc):
+    """rsk_host_register: the batched export / import DMA straight into / out of
+    a caller-registered buffer (no pinned stage, no host copy) and give the same
+    bytes and registers as the staged path; overlapping registrations and
+    unregistering an unknown pointer are refused."""
+    from redisson_amd import _lib, devmem
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    G, n = 3000, 3_000_000
+    g, k = devmem.gen_grouped(engine, 0x5EED0006, G, 0, n)
+    pool = GroupedHyperLogLog(engine, G)
+    pool.add(k.keys_fixed(n, 16), g)
+    pool.mergeWith(np.arange(0, 300, dtype=np.uint64), np.arange(300, 600, dtype=np.uint64))  # some dense keys
+    g.free()
+    k.free()
+    ids = np.arange(G, dtype=np.uint64)
+    staged, offs = pool.exportRedis(ids)
+    reg = np.zeros(staged.size + 4096, np.uint8)  # registered, larger than needed
+    engine.host_register(reg)
+    try:
+        with pytest.raises(_lib.IllegalArgumentException):
+            _lib.check(L.rsk_host_register(engine.ctx, reg.ctypes.data + 4096, 4096))  # overlaps
+        data, offs2 = pool.exportRedis(ids, out=reg)
+        assert np.array_equal(offs2, offs) and np.array_equal(reg[:staged.size], staged)
+        fresh = GroupedHyperLogLog(engine, G)
+        fresh.importRedis(ids, reg[:staged.size], offs)
+        back, offs3 = fresh.exportRedis(ids)
+        assert np.array_equal(offs3, offs) and np.array_equal(back, staged)
+        for gid in (0, 299, 300, G - 1):
+            assert np.array_equal(fresh.registers(gid), pool.registers(gid))
+        fresh.close()
+    finally:
+        engine.host_unregister(reg)
+    with pytest.raises(_lib.IllegalArgumentException):
+        engine.host_unregister(reg)
+    pool.close()
