@@ -576,7 +576,10 @@ void check_hll(const rsk_hll* h, uint64_t id) {
 
 // check_hll for a batch of ids of one pool: ranges checked in one pass, the
 // pool materialised and touched once (10^5-pair countWith / mergeWith batches).
-void check_hll_ids(const rsk_hll* h, const uint64_t* a, uint64_t na, const uint64_t* b = nullptr, uint64_t nb = 0) {
+// writes: the caller may write registers (its precomputed PFCOUNTs are retired); read-only
+// callers (count, countWith) keep them.
+void check_hll_ids(const rsk_hll* h, const uint64_t* a, uint64_t na, const uint64_t* b = nullptr, uint64_t nb = 0,
+                   bool writes = true) {
   need(h != nullptr, "hll handle is NULL");
   uint64_t bad = 0;
   for (uint64_t i = 0; i < na; ++i) bad |= a[i] >= h->n;
@@ -585,7 +588,7 @@ void check_hll_ids(const rsk_hll* h, const uint64_t* a, uint64_t na, const uint6
   CtxLock l(h->ctx);
   rsk::hll_materialize_ids(h, a, na);  // the rows these calls read or write (a partial lazy clear)
   if (nb) rsk::hll_materialize_ids(h, b, nb);
-  rsk::hll_touch(h);
+  if (writes) rsk::hll_touch(h);
 }
 
 uint8_t* regs_of(rsk_hll* h, uint64_t id) { return h->d_regs + id * (uint64_t)HLL_REGS; }
@@ -1478,7 +1481,7 @@ int rsk_hll_count_union_batch(rsk_hll* h, const uint64_t* member_ids, uint32_t a
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     if (n == 0) return;
-    check_hll_ids(h, member_ids, n * arity);
+    check_hll_ids(h, member_ids, n * arity, nullptr, 0, false);
     auto* ptrs = reinterpret_cast<const uint8_t**>(c->pinned(8ull * n * arity + 8ull * n));
     const uint8_t* e = h->exists.data();
     for (uint64_t i = 0; i < n * arity; ++i) {
@@ -2822,7 +2825,7 @@ int rsk_hll_count_ids_async(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_
     need(h != nullptr && out != nullptr, "NULL argument");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    if (ids) check_hll_ids(h, ids, n);
+    if (ids) check_hll_ids(h, ids, n, nullptr, 0, false);
     else need(n <= h->n, "n exceeds pool size");
     const uint64_t ib = ids ? al256(8 * n) : 0, ob = al256(8 * n);
     AsyncOp* op = op_get(c, ib + ob, ib + ob);
@@ -2860,7 +2863,7 @@ int rsk_hll_count_union_batch_async(rsk_hll* h, const uint64_t* member_ids, uint
     need(h && member_ids && out && arity >= 1, "bad arguments");
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
-    check_hll_ids(h, member_ids, n * arity);
+    check_hll_ids(h, member_ids, n * arity, nullptr, 0, false);
     const uint64_t pb = al256(8 * n * arity), ob = al256(8 * n);
     AsyncOp* op = op_get(c, pb + ob, pb + ob);
     try {
