@@ -105,6 +105,12 @@ def lib():
             "orc_hll_add_gen_grouped_zipf_subset": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                            ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64,
                                                            ctypes.c_uint64, ctypes.c_int]),
+            "orc_gen_grouped_groups": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_void_p, ctypes.c_int]),
+            "orc_gen_grouped_zipf_groups": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, ctypes.c_uint64,
+                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]),
+            "orc_hll_add_keys_by_groups": (None, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
             "orc_gen_grouped": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_void_p]),
             "orc_gen_queries16": (None, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -236,6 +242,27 @@ def hll_add_gen_grouped_zipf_subset(regs: np.ndarray, G: int, gsub: int, s: floa
                                     nthreads: int = 1):
     assert regs.dtype == np.uint8 and regs.size == gsub * REGISTERS
     lib().orc_hll_add_gen_grouped_zipf_subset(_ptr(regs), G, gsub, s, seed, start, n, nthreads)
+
+
+def gen_grouped_groups(seed: int, G: int, start: int, n: int, nthreads: int = 1) -> np.ndarray:
+    """The groups of the uniform pair stream (orc_gen_grouped without the keys)."""
+    groups = np.zeros(n, np.uint32)
+    lib().orc_gen_grouped_groups(seed, G, start, n, _ptr(groups), nthreads)
+    return groups
+
+
+def gen_grouped_zipf_groups(seed: int, G: int, s: float, start: int, n: int, nthreads: int = 1) -> np.ndarray:
+    """The groups of the Zipf pair stream (orc_gen_grouped_zipf without the keys)."""
+    groups = np.zeros(n, np.uint32)
+    lib().orc_gen_grouped_zipf_groups(seed, G, s, start, n, _ptr(groups), nthreads)
+    return groups
+
+
+def hll_add_keys_by_groups(regs: np.ndarray, G: int, groups: np.ndarray, seed: int, start: int, nthreads: int = 1):
+    """A whole pool [G][16384] from the pairs whose groups are given and whose
+    keys are the grouped streams' (rsk_oracle.c orc_hll_add_keys_by_groups)."""
+    assert regs.dtype == np.uint8 and regs.size == G * REGISTERS and groups.dtype == np.uint32
+    lib().orc_hll_add_keys_by_groups(_ptr(regs), G, _ptr(groups), seed, start, groups.size, nthreads)
 
 
 def hll_add_gen_grouped(regs: np.ndarray, G: int, seed: int, start: int, n: int):

@@ -293,6 +293,64 @@ void orc_hll_add_gen_grouped_zipf_subset(uint8_t *regs, uint64_t G, uint64_t gsu
     free(cdf);
 }
 
+/* The groups of the uniform pair stream for pairs [start, start + n) (as
+ * orc_gen_grouped, without the keys), on nthreads cores. */
+void orc_gen_grouped_groups(uint64_t seed, uint64_t G, uint64_t start, uint64_t n, uint32_t *groups, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+    for (uint64_t j = 0; j < n; j++) groups[j] = (uint32_t)(orc_splitmix64(seed + 3 * (start + j)) % G);
+}
+
+/* The groups of the Zipf pair stream for pairs [start, start + n) (as
+ * orc_gen_grouped_zipf, without the keys), on nthreads cores. */
+void orc_gen_grouped_zipf_groups(uint64_t seed, uint64_t G, double s, uint64_t start, uint64_t n, uint32_t *groups,
+                                 int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    uint64_t *cdf = malloc(8 * G);
+    orc_zipf_cdf(G, s, cdf);
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+    for (uint64_t j = 0; j < n; j++) groups[j] = zipf_rank(cdf, G, orc_splitmix64(seed + 3 * (start + j)) >> 1);
+    free(cdf);
+}
+
+/* A whole pool [G][16384] from pairs [start, start + n) whose groups are
+ * given (groups[j]: ids >= G dropped) and whose keys are the grouped streams'
+ * (splitmix64 of seed + 3i + 1, seed + 3i + 2): each of nthreads cores owns a
+ * contiguous range of the groups and hashes only its pairs, so no two threads
+ * write one row (a full-pool check of the grouped add, uniform or Zipf). */
+void orc_hll_add_keys_by_groups(uint8_t *regs, uint64_t G, const uint32_t *groups, uint64_t seed, uint64_t start,
+                                uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+#ifdef _OPENMP
+        const uint64_t t = (uint64_t)omp_get_thread_num(), nt = (uint64_t)omp_get_num_threads();
+#else
+        const uint64_t t = 0, nt = 1;
+#endif
+        const uint64_t g0 = G * t / nt, g1 = G * (t + 1) / nt;
+        for (uint64_t j = 0; j < n; j++) {
+            const uint32_t g = groups[j];
+            if (g < g0 || g >= g1) continue;
+            const uint64_t i = start + j;
+            uint8_t key[16];
+            uint64_t lo = orc_splitmix64(seed + 3 * i + 1), hi = orc_splitmix64(seed + 3 * i + 2);
+            memcpy(key, &lo, 8);
+            memcpy(key + 8, &hi, 8);
+            long idx;
+            int c = orc_hll_patlen(key, 16, &idx);
+            uint8_t *r = regs + (uint64_t)g * ORC_HLL_REGISTERS;
+            if (c > r[idx]) r[idx] = (uint8_t)c;
+        }
+    }
+}
+
 /* Bloom query stream (C3): query q is an inserted key (index r>>1 mod n_ins
  * of the insert stream iseed) when r&1, else a fresh key. */
 void orc_gen_queries16(uint64_t qseed, uint64_t iseed, uint64_t n_ins, uint64_t start, uint64_t n, uint8_t *out) {

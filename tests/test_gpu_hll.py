@@ -846,3 +846,44 @@ def test_export_follows_redis_encoding(L, engine, orc):
     _add(L, h, KeyBatch.from_numpy(keys[:3]), 3)
     assert _export(L, h, 3)[4] == 1
     L.rsk_hll_destroy(h)
+
+
+@pytest.mark.parametrize("zipf", [0.0, 1.1])
+def test_c5_full_size_every_sketch_bit_exact(L, engine, orc, zipf):
+    """BASELINE configs[4] at its per-GPU size (1M sketches, 500M pairs; uniform
+    and the Zipf(1.1) stress variant): EVERY sketch of the pool bit-exact
+    against the oracle over the whole pair stream -- 16 GB of registers
+    compared row by row (the oracle on up to 16 cores, each owning a range of
+    the groups) -- and PFCOUNT of an evenly spread sample of 1024 sketches."""
+    from redisson_amd import _lib, devmem
+
+    G, n, seed = 1_000_000, 500_000_000, 0x5EED0006
+    thr = max(1, min(16, os.cpu_count() or 1))
+    if zipf:
+        g, k = devmem.gen_grouped_zipf(engine, seed, G, zipf, 0, n)
+    else:
+        g, k = devmem.gen_grouped(engine, seed, G, 0, n)
+    h = _pool(L, engine, G)
+    ks = k.keys_fixed(n, 16).as_struct()
+    _lib.check(L.rsk_hll_add_grouped(h, ctypes.byref(ks), g.ptr))
+    g.free()
+    k.free()
+    groups = orc.gen_grouped_zipf_groups(seed, G, zipf, 0, n, thr) if zipf else orc.gen_grouped_groups(seed, G, 0, n, thr)
+    ref = np.zeros((G, 16384), np.uint8)
+    orc.hll_add_keys_by_groups(ref, G, groups, seed, 0, thr)
+    del groups
+    base = L.rsk_hll_device_registers(h)
+    chunk = 65536
+    buf = np.empty((chunk, 16384), np.uint8)
+    bad = []
+    for lo in range(0, G, chunk):
+        m = min(chunk, G - lo)
+        _lib.check(L.rsk_memcpy(engine.ctx, buf.ctypes.data, ctypes.c_void_p(base + lo * 16384), m * 16384, 1))
+        diff = np.nonzero((buf[:m] != ref[lo:lo + m]).any(1))[0]
+        bad.extend((diff + lo)[:16].tolist())
+    assert not bad, (len(bad), bad[:16])
+    sample = np.linspace(0, G - 1, 1024).astype(np.int64)
+    cnt = _count(L, h, sample.tolist())
+    assert [int(c) for c in cnt] == [orc.hll_count_dense(ref[i]) for i in sample]
+    L.rsk_hll_destroy(h)
+    _lib.check(L.rsk_trim(engine.ctx))

@@ -325,3 +325,25 @@ def test_zipf_stream_shape_and_subset_oracle(orc):
         sub = np.zeros(gs * orc.REGISTERS, np.uint8)
         orc.hll_add_gen_grouped_zipf_subset(sub, G, gs, s, 0x5EED0006, 0, n, threads)
         assert np.array_equal(sub, ref), threads
+
+
+def test_full_pool_oracle_forms_match_the_sequential_ones(orc):
+    """The multi-threaded full-pool oracle forms used by the every-sketch C5
+    checks (groups generated alone, then each thread hashing the pairs of its
+    own range of groups) give the same pools as the sequential generators."""
+    G, n = 97, 40_000
+    for zipf in (0.0, 1.1):
+        if zipf:
+            g_ref, k_ref = orc.gen_grouped_zipf(0x5EED0006, G, zipf, 123, n)
+            groups = orc.gen_grouped_zipf_groups(0x5EED0006, G, zipf, 123, n, 4)
+        else:
+            g_ref, k_ref = orc.gen_grouped(0x5EED0006, G, 123, n)
+            groups = orc.gen_grouped_groups(0x5EED0006, G, 123, n, 4)
+        assert np.array_equal(groups, g_ref)
+        ref = np.zeros((G, orc.REGISTERS), np.uint8)
+        for gid in np.unique(g_ref):
+            sel = g_ref == gid
+            orc.hll_add(ref[gid], k_ref.reshape(-1, 16)[sel].reshape(-1), None, 16, int(sel.sum()))
+        full = np.zeros((G, orc.REGISTERS), np.uint8)
+        orc.hll_add_keys_by_groups(full, G, groups, 0x5EED0006, 123, 4)
+        assert np.array_equal(full, ref), zipf
