@@ -235,15 +235,36 @@ def test_routed_add_self_exchange(engine, orc, G, n):
         _lib.check(L.rsk_comm_destroy(engine.ctx))
 
 
-def test_routed_add_c5_full_size_self_exchange(engine, orc):
-    """BASELINE configs[4] at its per-GPU size through the routed form at N = 1
-    (every record through RCCL to itself): the stratified sample of sketches is
-    bit-exact against the oracle over the whole pair stream."""
+def _assert_pool_equals_oracle(L, engine, orc, pool, G, n, zipf, seed=0x5EED0006):
+    """Every row of a full-size pool against the oracle over the whole pair
+    stream (16 GB at 1M sketches, compared in 1 GiB chunks)."""
     import os
 
+    from redisson_amd import _lib
+
+    thr = max(1, min(16, os.cpu_count() or 1))
+    groups = orc.gen_grouped_zipf_groups(seed, G, zipf, 0, n, thr) if zipf else orc.gen_grouped_groups(seed, G, 0, n, thr)
+    ref = np.zeros((G, 16384), np.uint8)
+    orc.hll_add_keys_by_groups(ref, G, groups, seed, 0, thr)
+    del groups
+    base = L.rsk_hll_device_registers(pool)
+    chunk = 65536
+    buf = np.empty((chunk, 16384), np.uint8)
+    bad = []
+    for lo in range(0, G, chunk):
+        m = min(chunk, G - lo)
+        _lib.check(L.rsk_memcpy(engine.ctx, buf.ctypes.data, ctypes.c_void_p(base + lo * 16384), m * 16384, 1))
+        bad.extend((np.nonzero((buf[:m] != ref[lo:lo + m]).any(1))[0] + lo)[:16].tolist())
+    assert not bad, (len(bad), bad[:16])
+    return ref
+
+
+def test_routed_add_c5_full_size_self_exchange(engine, orc):
+    """BASELINE configs[4] at its per-GPU size through the routed form at N = 1
+    (every record through RCCL to itself): every sketch is bit-exact against
+    the oracle over the whole pair stream."""
     from redisson_amd import _lib, devmem, shard
     from redisson_amd.hyperloglog import GroupedHyperLogLog
-    from test_gpu_hll import _c5_stratified_sample
 
     L = _lib.load()
     uid = (ctypes.c_uint8 * 128)()
@@ -257,11 +278,7 @@ def test_routed_add_c5_full_size_self_exchange(engine, orc):
         assert shard.hll_add_grouped_routed(pool.pool, k.keys_fixed(n, 16), g, flags=_lib.RSK_FETCH_SELF) == (0, G)
         g.free()
         k.free()
-        sample = _c5_stratified_sample(G)
-        ref = np.zeros((sample.size, 16384), np.uint8)
-        orc.hll_add_gen_grouped_ids(ref, G, sample, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
-        bad = [gid for s, gid in enumerate(sample.tolist()) if not np.array_equal(pool.registers(gid), ref[s])]
-        assert not bad, (len(bad), bad[:10])
+        _assert_pool_equals_oracle(L, engine, orc, pool.pool, G, n, 0.0)  # every sketch
         pool.close()
         _lib.check(L.rsk_trim(engine.ctx))
     finally:
@@ -417,11 +434,9 @@ def test_routed_add_c5_zipf_full_size_heavy_rows(engine, orc):
     sketches, 500M pairs) through the routed add on one GPU with the self
     exchange: the automatic heavy-group pre-combine folds the ~12k sketches of
     >= 2048 pairs into rows (which then travel through RCCL to the owner and are
-    max-merged), the rest go as records.  The 1024 hottest sketches (~60 % of
-    the pairs, all of them heavy rows) are bit-exact against the oracle over the
-    whole stream, and their PFCOUNTs (the merged rows' precomputed estimates
-    retired)."""
-    import os
+    max-merged), the rest go as records.  Every sketch is bit-exact against
+    the oracle over the whole stream, and the PFCOUNTs of the 64 hottest (heavy
+    rows: the merged rows' precomputed estimates retired)."""
 
     from redisson_amd import _lib, devmem, shard
     from redisson_amd.hyperloglog import GroupedHyperLogLog
@@ -433,7 +448,7 @@ def test_routed_add_c5_zipf_full_size_heavy_rows(engine, orc):
     engine.prof_enable(True)
     engine.prof_reset()
     try:
-        G, n, gs = 1_000_000, 500_000_000, 1024
+        G, n = 1_000_000, 500_000_000
         g, k = devmem.gen_grouped_zipf(engine, 0x5EED0006, G, 1.1, 0, n)
         pool = GroupedHyperLogLog(engine, G)
         pool.clear()
@@ -441,12 +456,7 @@ def test_routed_add_c5_zipf_full_size_heavy_rows(engine, orc):
         assert _prof(engine, "hll_route_heavy_rows") == 1
         g.free()
         k.free()
-        ref = np.zeros((gs, 16384), np.uint8)
-        orc.hll_add_gen_grouped_zipf_subset(ref, G, gs, 1.1, 0x5EED0006, 0, n, max(1, min(16, os.cpu_count() or 1)))
-        got = np.zeros((gs, 16384), np.uint8)
-        _lib.check(L.rsk_memcpy(engine.ctx, got.ctypes.data, L.rsk_hll_device_registers(pool.pool), got.nbytes, 1))
-        bad = np.nonzero((got != ref).any(1))[0]
-        assert bad.size == 0, (bad.size, bad[:10].tolist())
+        ref = _assert_pool_equals_oracle(L, engine, orc, pool.pool, G, n, 1.1)  # every sketch
         cnt = pool.count(ids=list(range(64)))
         assert [int(c) for c in cnt] == [orc.hll_count_dense(ref[i]) for i in range(64)]
         pool.close()
