@@ -436,11 +436,15 @@ def test_import_batch_long_sparse(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
-def test_dense_pool_round_trip_many_pieces(L, engine, orc):
+@pytest.mark.parametrize("pin", [0, -1])
+def test_dense_pool_round_trip_many_pieces(L, engine, orc, route, pin):
     """70000 dense keys (861 MB of strings): one export chunk is ~806 MB, so
-    the staged copy-out cycles its ring of pinned slots several times, and the
-    import stages ~861 MB in pieces; SET then GET returns the same bytes, and
-    the registers equal the oracle's decode."""
+    the staged copy-out (route io_pin = -1) cycles its ring of pinned slots
+    several times, or the output buffer is pinned for the call and takes the
+    DMA (the default for a buffer >= 256 MiB); the import stages ~861 MB in
+    pieces; SET then GET returns the same bytes, and the registers equal the
+    oracle's decode."""
+    route(io_pin=pin)
     rng = np.random.default_rng(29)
     G = 70000
     rows = rng.integers(0, 25, size=(64, 16384), dtype=np.uint8)
