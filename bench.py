@@ -603,7 +603,8 @@ def checkpoint_bench(engine, pool):
                                        "note": "the host buffer pinned once with rsk_host_register (not timed in "
                                                "export_ms / import_ms; register_ms is its one-time cost)"},
             "note": "rsk_hll_export_redis_batch / rsk_hll_import_redis_batch of every sketch after the timed "
-                    "steps, pageable host buffers (PCIe inclusive), one call each, best of 2 (both listed)"}
+                    "steps, pageable host buffers (PCIe inclusive; the export pins its >= 256 MiB output buffer "
+                    "for the call, inside export_ms), one call each, best of 2 (both listed)"}
 
 
 def launch_ranks(n: int, argv) -> int:
