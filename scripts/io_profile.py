@@ -26,6 +26,8 @@ def main():
     routes = dict(kv.split("=") for kv in sys.argv[3].split(",")) if len(sys.argv) > 3 and sys.argv[3] else {}
     _lib.load()
     _lib.diag()
+    if os.environ.get("IO_TORCH"):  # (as bench.py: torch imported after the library)
+        import torch.distributed  # noqa: F401
     eng = _lib.Engine(0)
     for k_, v_ in routes.items():
         eng.set_route(k_, int(v_))
@@ -42,22 +44,37 @@ def main():
         pool.mergeWith(rng.integers(0, G, size=merges, dtype=np.uint64), rng.integers(0, G, size=merges, dtype=np.uint64))
     ids = np.arange(G, dtype=np.uint64)
     data, offs = pool.exportRedis(ids)
+    thp = os.environ.get("IO_THP")
+    if thp is not None:  # the output buffer from an anonymous mapping with (1) or without (0) MADV_HUGEPAGE
+        import mmap
+
+        mm = mmap.mmap(-1, (data.size + (2 << 20) - 1) // (2 << 20) * (2 << 20))
+        mm.madvise(mmap.MADV_HUGEPAGE if thp == "1" else mmap.MADV_NOHUGEPAGE)
+        buf = np.frombuffer(mm, np.uint8)
+        buf[:] = 0  # touch (faults the pages in, huge where granted)
+        data, offs = pool.exportRedis(ids, out=buf)
     fresh = GroupedHyperLogLog(eng, G)
     fresh.importRedis(ids, data, offs)
     eng.prof_reset()
     eng.prof_enable(True)
     te, ti = [], []
+    no_import = bool(os.environ.get("IO_NOIMPORT"))  # (exports back to back)
     for _ in range(reps):
         t0 = time.perf_counter()
         pool.exportRedis(ids, out=data)
         te.append(time.perf_counter() - t0)
+        if no_import:
+            continue
         t0 = time.perf_counter()
         fresh.importRedis(ids, data, offs)
         ti.append(time.perf_counter() - t0)
+    ti = ti or [float("nan")]
     eng.prof_enable(False)
     dev = {s: eng.prof_read(s)[0] / reps for s in ("hll_export_encode", "hll_export_pack", "hll_import_check",
                                                     "hll_import_write")}
     print(json.dumps({"routes": routes, "sketches": G, "merges": merges, "bytes": int(offs[-1]), "export_ms": min(te) * 1e3, "import_ms": min(ti) * 1e3,
+                      "export_ms_each": [round(t * 1e3, 2) for t in te], "no_import": no_import,
+                      "thp": os.environ.get("IO_THP"), "torch": bool(os.environ.get("IO_TORCH")),
                       "device_ms": dev}), flush=True)
 
 
