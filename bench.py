@@ -556,7 +556,7 @@ def checkpoint_bench(engine, pool):
     ids = np.arange(pool.n, dtype=np.uint64)
     data, offs = pool.exportRedis(ids)  # warm-up: sizes the buffer (and touches its pages)
     t_exp = []
-    for _ in range(2):
+    for _ in range(3):
         t0 = time.perf_counter()
         data, offs = pool.exportRedis(ids, out=data)
         t_exp.append(time.perf_counter() - t0)
@@ -564,7 +564,7 @@ def checkpoint_bench(engine, pool):
     fresh = GroupedHyperLogLog(engine, pool.n)
     fresh.importRedis(ids, data, offs)  # warm-up (scratch)
     t_imp = []
-    for _ in range(2):
+    for _ in range(3):
         t0 = time.perf_counter()
         fresh.importRedis(ids, data, offs)
         t_imp.append(time.perf_counter() - t0)
@@ -604,7 +604,7 @@ def checkpoint_bench(engine, pool):
                                                "export_ms / import_ms; register_ms is its one-time cost)"},
             "note": "rsk_hll_export_redis_batch / rsk_hll_import_redis_batch of every sketch after the timed "
                     "steps, pageable host buffers (PCIe inclusive; the export pins its >= 256 MiB output buffer "
-                    "for the call, inside export_ms), one call each, best of 2 (both listed)"}
+                    "for the call, inside export_ms), one call each, best of 3 (all listed)"}
 
 
 def launch_ranks(n: int, argv) -> int:

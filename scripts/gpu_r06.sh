@@ -85,7 +85,7 @@ for p in ${PART//,/ }; do
     ioab)  # export / import routes A/B interleaved, one process each: IOAB="route=v,...;route=v,..."
       IFS=';' read -ra FORMS <<< "${IOAB:-io_drain=0;io_drain=1}"
       for m in ${IO_MERGES:-0 100000}; do for rep in 1 2; do for f in "${FORMS[@]}"; do
-        step ioab_$rep 200 python3 scripts/io_profile.py 3 $m "$f" || exit 1
+        step ioab_$rep 200 python3 scripts/io_profile.py ${IO_REPS:-3} $m "$f" || exit 1
         grep '^{' gpurun_out/ioab_$rep.log >> gpurun_out/${TAG}_ioab.jsonl
       done; done; done ;;
     chain)  # the C3 per-key arithmetic alone, in registers, at C3's size and boundary sizes
