@@ -51,7 +51,6 @@ const char *rsk_diag_last_error(void);
  *   io_drain      batched export: 1 = each chunk's copy-out finished before the next chunk (A/B)
  *   copy_nt       staged host copies (host keys, export / import strings): 0 streaming stores, -1 memcpy (A/B)
  *   io_pin        batched export: 0 pin a pageable output buffer >= 256 MiB for the call, -1 never (staged)
- *   sync_poll     per-call reply waits (PFADD flag, small PFCOUNT): 0 hipStreamSynchronize, 1 poll (A/B)
  *   gpart_tile    tile-major first pass: 0 (default) 8192-record tiles, 1 16384 (one 512-lane block per CU)
  *   route_vranks  TEST ONLY, 1-rank communicator: rsk_hll_add_grouped_routed plans as rank route_vrank of
  *   route_vrank   route_vranks (its owned sub-range; records for the other owners are dropped)

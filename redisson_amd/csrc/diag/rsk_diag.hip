@@ -207,7 +207,6 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "io_drain") t.io_drain = (int)value;
     else if (k == "copy_nt") t.copy_nt = (int)value;
     else if (k == "io_pin") t.io_pin = (int)value;
-    else if (k == "sync_poll") t.sync_poll = (int)value;
     else if (k == "reset") t = Tuning{};
     else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};
   });

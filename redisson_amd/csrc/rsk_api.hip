@@ -566,21 +566,6 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
   RSK_HIP(hipStreamSynchronize(c->stream));
 }
 
-// Wait for the context stream: hipStreamSynchronize, or (route sync_poll = 1,
-// A/B) a poll of hipStreamQuery that yields between polls.
-void stream_wait(rsk_ctx* c) {
-  if (c->tune.sync_poll <= 0) {
-    RSK_HIP(hipStreamSynchronize(c->stream));
-    return;
-  }
-  while (true) {
-    const hipError_t e = hipStreamQuery(c->stream);
-    if (e == hipSuccess) return;
-    if (e != hipErrorNotReady) RSK_HIP(e);
-    std::this_thread::yield();
-  }
-}
-
 void check_hll(const rsk_hll* h, uint64_t id) {
   need(h != nullptr, "hll handle is NULL");
   need(id < h->n, "sketch id out of range");
@@ -1193,7 +1178,7 @@ int rsk_hll_add(rsk_hll* h, uint64_t id, const rsk_keys* keys, uint8_t* changed_
     if (!any_chunk && created) invalidate(h, id, nullptr, true);  // PFADD key (no elements) creates it
     if (changed_out || had_import) {
       RSK_HIP(hipMemcpyAsync(c->h_small, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
-      stream_wait(c);  // (the per-call reply: route sync_poll)
+      RSK_HIP(hipStreamSynchronize(c->stream));
       uint32_t f;
       std::memcpy(&f, c->h_small, 4);
       const bool changed = (f == epoch) || created;
@@ -1360,7 +1345,7 @@ int rsk_hll_count(rsk_hll* h, const uint64_t* ids, uint64_t n, uint64_t* out) {
     hll_count_launch(c, h->d_regs, h->d_card, d_ids, small, n, d_out, PCount{h->d_pcount, h->d_pepoch, h->pc_epoch});
     if (n * 8 <= 4096) {  // small results come back through the pinned buffer
       RSK_HIP(hipMemcpyAsync(c->h_small + 4096, d_out, n * 8, hipMemcpyDeviceToHost, c->stream));
-      stream_wait(c);  // (the per-call reply: route sync_poll)
+      RSK_HIP(hipStreamSynchronize(c->stream));
       std::memcpy(out, c->h_small + 4096, n * 8);
     } else {  // large ones (count of a whole pool: 8 MB at 10^6 sketches) through the
               // pinned per-call buffer: one full-speed DMA, then host threads copy out

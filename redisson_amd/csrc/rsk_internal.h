@@ -70,7 +70,6 @@ struct Tuning {
   int io_piece = 0;          // batched export's copy-out pieces, MiB (0: 16)
   int io_drain = 0;          // batched export: 1 = each chunk's copy-out drained before the next chunk (A/B)
   int copy_nt = 0;           // staged host copies: 0 streaming stores, -1 memcpy (A/B)
-  int sync_poll = 0;         // per-call reply waits (PFADD flag, small PFCOUNT): 0 hipStreamSynchronize, 1 poll (A/B)
   int io_pin = 0;            // batched export: a pageable output buffer >= 256 MiB pinned for the call (0), never (-1)
   int gpart_rt = 0;          // hll_gpart2t's round: 0 8192 records, 1 16384 (A/B)
   int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B), 2 none (TIMING ONLY)
