@@ -464,3 +464,47 @@ def test_routed_add_c5_zipf_full_size_heavy_rows(engine, orc):
     finally:
         engine.prof_enable(False)
         _lib.check(L.rsk_comm_destroy(engine.ctx))
+
+
+@pytest.mark.parametrize("G,n,heavy,vranks,vrank", [
+    (200_003, 6_000_000, 2, 0, 0),   # nearly every group heavy: the 65536-row cap cuts the heavy set (by id)
+    (10, 300_000, 64, 3, 2),         # the tail owner (10 = 3 + 3 + 4), every group heavy
+    (2, 50_000, 64, 3, 0),           # G < N: ranks 0, 1 own nothing; rank 2 owns both
+])
+def test_routed_add_heavy_edges(engine, orc, route, G, n, heavy, vranks, vrank):
+    """The heavy pre-combine at its edges: the per-call cap on heavy rows (the
+    groups past it stay records), the tail owner, and a rank that owns no
+    sketch (its pairs all go elsewhere as rows or records).  Owned rows equal
+    the plain grouped add's."""
+    from redisson_amd import _lib, devmem, shard
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    _lib.check(L.rsk_comm_unique_id(uid))
+    _lib.check(L.rsk_comm_init(engine.ctx, 1, 0, uid))
+    try:
+        groups, keys = orc.gen_grouped(0x5EED0016, G, 0, n)
+        kd = devmem.DeviceBuffer.from_numpy(engine, keys)
+        gd = devmem.DeviceBuffer.from_numpy(engine, groups)
+        kb = kd.keys_fixed(n, 16)
+        b = GroupedHyperLogLog(engine, G)
+        b.clear()
+        b.add(kb, gd)
+        ref = _all_rows(L, engine, b.pool, G)
+        a = GroupedHyperLogLog(engine, G)
+        a.clear()
+        route(route_heavy=heavy, route_vranks=vranks, route_vrank=vrank)
+        first, count = shard.owned_range(G, vranks or 1, vrank)
+        assert shard.hll_add_grouped_routed(a.pool, kb, gd, flags=_lib.RSK_FETCH_SELF) == (first, count)
+        route(route_vranks=0, route_heavy=0)
+        got = _all_rows(L, engine, a.pool, G)
+        assert np.array_equal(got[first:first + count], ref[first:first + count])
+        assert not got[:first].any() and not got[first + count:].any()
+        a.close()
+        b.close()
+        kd.free()
+        gd.free()
+    finally:
+        route(route_vranks=0, route_heavy=0)
+        _lib.check(L.rsk_comm_destroy(engine.ctx))
