@@ -39,6 +39,7 @@ const char *rsk_diag_last_error(void);
  *   reply_u       rp_treply keys (gather chains) per lane: 0 (= 2), 1, 2, 4
  *   reply_v       rp2 tile: uint4 loads per lane, 0 (= 8), 3 or 6
  *   reply_s       rp_tapply: wave steps whose segment loads are issued together, 0 (= 2), 1, 4
+ *   reply_bal     rp_tapply: 0 an equal slice of the bucket's tiles per wave, -1 strided (A/B)
  *   reply_dbg     TIMING ONLY (wrong replies and T): rp_tapply without its
  *                 folds (bit 0) / without its T stores (bit 1)
  *   gpart         partitioned grouped PFADD: 0 auto, 1 any size, -1 never

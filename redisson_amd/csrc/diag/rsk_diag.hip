@@ -193,6 +193,7 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "reply_v") t.reply_v = (int)value;
     else if (k == "reply_dbg") t.reply_dbg = (int)value;
     else if (k == "reply_s") t.reply_s = (int)value;
+    else if (k == "reply_bal") t.reply_bal = (int)value;
     else if (k == "gpart") t.gpart = (int)value;
     else if (k == "gpart_tm") t.gpart_tm = (int)value;
     else if (k == "gpart_poison") t.gpart_poison = (int)value;

@@ -112,7 +112,8 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
                                                          const uint32_t* __restrict__ tile_off,
                                                          const uint32_t* __restrict__ ntiles, uint32_t P,
                                                          uint64_t nbuckets, uint32_t* __restrict__ bits,
-                                                         uint64_t nwords, uint16_t* __restrict__ T, int dbg) {
+                                                         uint64_t nwords, uint16_t* __restrict__ T, int dbg,
+                                                         int strided) {
   __shared__ __attribute__((aligned(16))) uint32_t tt[BK_BITS / 2];
   __shared__ __attribute__((aligned(16))) uint32_t f0[BK_BITS / 32];
   constexpr uint32_t FW = BK_BITS / 32 / TA_T;  // filter words per lane (2)
@@ -139,11 +140,22 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
     k.te = tile_off[(uint64_t)c * P + P - 1] + ntiles[(uint64_t)c * P + P - 1];
     return k;
   };
-  // lane's tile g + lane: segment bounds of the bucket and the tile's first uint4
-  auto hload = [&](const Bk& k, uint32_t g, uint32_t& beg, uint32_t& end, uint32_t& tbl) {
+  // the wave's share of the bucket's tiles: an equal slice each (a wave of 64
+  // lanes loads 64 tiles' bounds at a time), so no wave runs a round more than
+  // another -- at C3 a bucket has ~1500 tiles: waves striding by 1024 tiles
+  // left half of them with two full rounds of 64 tiles, the rest with one
+  // (strided, A/B: route reply_bal = -1 -- wave w takes tiles w*64.. then every 1024th)
+  const uint32_t gstep = strided ? 64 * NW : 64;
+  auto wrange = [&](const Bk& k, uint32_t& a, uint32_t& b) {
+    const uint64_t T = k.te - k.ta;
+    a = strided ? k.ta + 64 * w : k.ta + (uint32_t)(T * w / NW);
+    b = strided ? k.te : k.ta + (uint32_t)(T * (w + 1) / NW);
+  };
+  // lane's tile g + lane (below lim): segment bounds of the bucket and the tile's first uint4
+  auto hload = [&](const Bk& k, uint32_t g, uint32_t lim, uint32_t& beg, uint32_t& end, uint32_t& tbl) {
     const uint32_t t = g + lane;
     beg = end = tbl = 0;
-    if (t < k.te) {
+    if (t < lim) {
       const uint4 v = k.hrow[t];
       const uint32_t hw[4] = {v.x, v.y, v.z, v.w};
       beg = (hw[k.e >> 1] >> (16 * (k.e & 1))) & 0xFFFFu;
@@ -155,14 +167,16 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
   // prefetched for bucket u: its filter words and this wave's first tile bounds
   uint32_t pfw[FW], pbeg = 0, pend = 0, ptb = 0;
   Bk k{};
+  uint32_t wa = 0, wb = 0;  // this wave's tiles of the current bucket
   if (u < nbuckets) {
     k = bucket(u);
+    wrange(k, wa, wb);
 #pragma unroll
     for (uint32_t i = 0; i < FW; ++i) {
       const uint64_t q = u * (BK_BITS / 32) + threadIdx.x + i * TA_T;
       pfw[i] = q < nwords ? bits[q] : 0u;
     }
-    hload(k, k.ta + 64 * w, pbeg, pend, ptb);
+    hload(k, wa, wb, pbeg, pend, ptb);
   }
   for (; u < nbuckets; u += gridDim.x) {
     uint4* t4 = reinterpret_cast<uint4*>(tt);
@@ -170,16 +184,16 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
 #pragma unroll
     for (uint32_t i = 0; i < FW; ++i) f0[threadIdx.x + i * TA_T] = pfw[i];
     lds_barrier();
-    for (uint32_t g = k.ta + 64 * w; g < k.te; g += 64 * NW) {
+    for (uint32_t g = wa; g < wb; g += gstep) {
       uint32_t beg, end, tbl;
-      if (g == k.ta + 64 * w) {
+      if (g == wa) {
         beg = pbeg;
         end = pend;
         tbl = ptb;
       } else {
-        hload(k, g, beg, end, tbl);
+        hload(k, g, wb, beg, end, tbl);
       }
-      const uint32_t ng = k.te - g < 64 ? k.te - g : 64;
+      const uint32_t ng = wb - g < 64 ? wb - g : 64;
       for (uint32_t j0 = 0; j0 < ng; j0 += 16 * S) {
         uint4 v[S][SU];
         uint32_t sb[S], se[S], st[S], p0[S];
@@ -227,8 +241,12 @@ __global__ __launch_bounds__(TA_T) void rp_tapply_kernel(const uint32_t* __restr
         const uint64_t q = un * (BK_BITS / 32) + threadIdx.x + i * TA_T;
         pfw[i] = q < nwords ? bits[q] : 0u;
       }
-      hload(kn, kn.ta + 64 * w, pbeg, pend, ptb);
+      uint32_t na, nb;
+      wrange(kn, na, nb);
+      hload(kn, na, nb, pbeg, pend, ptb);
       k = kn;
+      wa = na;
+      wb = nb;
     }
     lds_barrier();
     // T and the filter, one byte of the Redis string (8 bits, MSB first) per lane step
@@ -605,10 +623,10 @@ bool bloom_add_replies_append(rsk_ctx* c, rsk_bloom* b, const DevKeys& keys, uin
       const uint32_t ga = (uint32_t)std::min<uint64_t>(nbuckets, cus);
 #define RSK_TAP(S)                                                                                                \
   hipLaunchKernelGGL(rp_tapply_kernel<S>, dim3(ga), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2, tile_off, \
-                     tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg)
+                     tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg, c->tune.reply_bal < 0)
 #define RSK_TAP2(S, SU)                                                                                              \
   hipLaunchKernelGGL((rp_tapply_kernel<S, SU>), dim3(ga), dim3(TA_T), 0, c->stream, l2, hp, tt_max, f2, tb2,     \
-                     tile_off, tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg)
+                     tile_off, tiles, P, nbuckets, b->d_bits, b->nwords, T, c->tune.reply_dbg, c->tune.reply_bal < 0)
       if (V2 == 8) RSK_TAP2(2, 3);  // segments of ~32 records: 48 slots per four lanes
       else if (c->tune.reply_s == 1) RSK_TAP(1);
       else if (c->tune.reply_s == 4) RSK_TAP(4);

@@ -64,6 +64,7 @@ struct Tuning {
   int reply_v = 0;           // rp2 tile: uint4 per lane, 0 (= 8), 3 or 6
   int reply_s = 0;           // rp_tapply: wave steps whose loads are in flight together, 0 (= 2), 1 or 4
   int reply_dbg = 0;         // timing-only rp_tapply forms (bit 0: no folds, bit 1: no T stores); wrong results
+  int reply_bal = 0;         // rp_tapply: 0 an equal slice of the bucket's tiles per wave, -1 strided by 1024 (A/B)
   int gpart = 0;             // partitioned grouped PFADD: 0 auto, 1 any size, -1 never
   int gpart_poison = 0;      // timing-free check: fill the fine-bin output with 0xFF first (a hole then shows)
   int io_trace = 0;          // batched export / import: host phase times to stderr
