@@ -30,7 +30,7 @@ build/diag/%.o: redisson_amd/csrc/diag/%.hip $(DHDR)
 	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -fvisibility-inlines-hidden -c $< -o $@
 
 $(DLIB): $(DOBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DOBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-z,now
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DOBJ) -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib -Wl,-z,now
 
 # -z now: every HIP/RCCL symbol is bound when the library loads.  Lazily bound
 # calls made after `import torch` (which brings its own libamdhip64 into the
@@ -38,7 +38,7 @@ $(DLIB): $(DOBJ)
 # does not know these kernels (hipOccupancyMaxActiveBlocksPerMultiprocessor
 # answered 1 there: persistent grids a third of their size).
 $(LIB): $(OBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-z,now
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib -Wl,-z,now
 
 oracle:
 	$(MAKE) -s -C oracle

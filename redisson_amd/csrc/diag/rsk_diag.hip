@@ -208,8 +208,18 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
     else if (k == "io_drain") t.io_drain = (int)value;
     else if (k == "copy_nt") t.copy_nt = (int)value;
     else if (k == "io_pin") t.io_pin = (int)value;
+    else if (k == "io_engine") t.io_engine = (int)value;
     else if (k == "reset") t = Tuning{};
     else throw RskError{RSK_ERR_INVALID_ARG, "unknown route: " + k};
+  });
+}
+
+int rsk_diag_copy_engine(rsk_ctx* c, int* engine, float* rates) {
+  return diag::guarded([&] {
+    diag::need(c && engine && rates, "NULL argument");
+    diag::Lock l(c);
+    *engine = c->d2h_engine;
+    for (int e = 0; e < 8; ++e) rates[e] = c->d2h_rate[e];
   });
 }
 

@@ -54,6 +54,16 @@ static int guarded(F&& fn) {
 
 [[noreturn]] static void fail(int code, const std::string& msg) { throw RskError{code, msg}; }
 
+// The address the copy engines use for a registered host range (0: the runtime has none).
+static uintptr_t reg_dptr(void* p) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return reinterpret_cast<uintptr_t>(d);
+}
+
 void prof_begin(rsk_ctx* c, const char*, hipEvent_t* a, hipEvent_t* b) {
   if (!c->prof.on) return;
   for (hipEvent_t* e : {a, b}) {
@@ -389,27 +399,130 @@ uint64_t staged_piece(const rsk_ctx* c, uint64_t bytes) {
 void pinned_idle(rsk_ctx* c) {
   for (int b = 0; b < 2; ++b) RSK_HIP(hipEventSynchronize(c->pin_ev[b]));
 }
+// The SDMA engine of the batched export's device->host copies (rsk_ctx::d2h_engine).  The
+// engine the runtime picks for device->host copies is not the fastest on every box: round 6
+// measured one engine at 26-30 GB/s and its neighbours at 57 on some boxes
+// (profiles/r06_sdma_engines.jsonl), so each of the first 8 engines the runtime reports free
+// moves a 4 MiB warm-up and then 32 MiB from a device scratch into a pinned stage, once per
+// context (~10 ms), and the fastest is kept.  Anything the runtime refuses: HIP's copies (-1).
+static hsa_status_t first_cpu_agent(hsa_agent_t a, void* out) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(out) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// one device->host copy of `bytes` on engine e, signal g (1 while in flight)
+static bool engine_copy(rsk_ctx* c, int e, hsa_signal_t g, void* to, const void* from, uint64_t bytes) {
+  hsa_signal_store_relaxed(g, 1);
+  return hsa_amd_memory_async_copy_on_engine(to, c->cpu_agent, from, c->gpu_agent, bytes, 0, nullptr, g,
+                                             (hsa_amd_sdma_engine_id_t)(1u << e), false) == HSA_STATUS_SUCCESS;
+}
+static hsa_signal_value_t engine_wait(hsa_signal_t g) {
+  hsa_signal_value_t v;
+  while ((v = hsa_signal_wait_scacquire(g, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE)) >= 1) {
+  }
+  return v;
+}
+
+void measure_d2h_engines(rsk_ctx* c) {
+  c->d2h_engine = -1;
+  if (hsa_init() != HSA_STATUS_SUCCESS) return;  // (the runtime HIP runs on: a reference, never shut down)
+  const uint64_t B = c->stage_bytes + c->stage_bytes / 4;
+  const uint64_t warm = std::min<uint64_t>(4ull << 20, B), big = std::min<uint64_t>(32ull << 20, B);
+  uint8_t* d = nullptr;
+  if (hipMalloc(&d, big) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  hsa_amd_pointer_info_t info{};
+  info.size = sizeof(info);
+  hsa_agent_t cpu{};
+  bool ok = hsa_amd_pointer_info(d, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+            info.type == HSA_EXT_POINTER_TYPE_HSA && hsa_iterate_agents(first_cpu_agent, &cpu) == HSA_STATUS_INFO_BREAK;
+  for (int j = 0; j < 8 && ok; ++j)
+    if (!c->eng_sig[j].handle) ok = hsa_signal_create(0, 0, nullptr, &c->eng_sig[j]) == HSA_STATUS_SUCCESS;
+  if (ok) {
+    c->gpu_agent = info.agentOwner;
+    c->cpu_agent = cpu;
+    uint32_t mask = 0;
+    if (hsa_amd_memory_copy_engine_status(cpu, c->gpu_agent, &mask) != HSA_STATUS_SUCCESS) mask = 0xFF;
+    float best = 0;
+    for (int e = 0; e < 8; ++e) {
+      if (!(mask >> e & 1)) continue;
+      const hsa_signal_t g = c->eng_sig[0];
+      if (!engine_copy(c, e, g, c->h_pin[0], d, warm) || engine_wait(g) < 0) continue;
+      const auto t0 = std::chrono::steady_clock::now();
+      if (!engine_copy(c, e, g, c->h_pin[0], d, big) || engine_wait(g) < 0) continue;
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      c->d2h_rate[e] = (float)(big / s / 1e9);
+      if (c->d2h_rate[e] > best) {
+        best = c->d2h_rate[e];
+        c->d2h_engine = e;
+      }
+    }
+  }
+  (void)hipFree(d);
+}
+
+// The engine of this export's copies: route io_engine, else the measured fastest (-1: HIP's copies).
+int export_engine(rsk_ctx* c) {
+  if (c->tune.io_engine < 0) return -1;
+  ensure_pinned(c);
+  if (c->pin_off) return -1;
+  if (c->d2h_engine == -2) {
+    pinned_idle(c);  // (the measurement writes a stage)
+    measure_d2h_engines(c);
+  }
+  if (!c->gpu_agent.handle) return -1;
+  return c->tune.io_engine > 0 ? std::min(c->tune.io_engine - 1, 15) : c->d2h_engine;
+}
+
 // Device -> pageable host through the two pinned stages, as a stream of
 // pieces that may span several calls of put(): a ring of NS slots over the two
 // stages (2, 4 or 8: as many pieces of S as they hold), the DMAs of up to
-// NS - 1 pieces queued on stream `s` ahead of the host copy-out, so the copy
-// engine never waits for the host between pieces -- nor between the chunks of
-// a batched export, whose pieces go through one stream (drain() at the end).
+// NS - 1 pieces queued ahead of the host copy-out, so the copy engine never
+// waits for the host between pieces -- nor between the chunks of a batched
+// export, whose pieces go through one stream (drain() at the end).  The DMAs
+// go on stream `s`, or with engine >= 0 straight to that SDMA engine (HSA
+// copies, each piece's completion a signal; the host orders them after the
+// device work that wrote their source, and order_after() orders the device
+// work that overwrites it after them).  Pieces for a registered range go
+// straight into it (on an engine: in ring pieces, with no copy-out).
 class D2HStream {
  public:
-  D2HStream(rsk_ctx* c, hipStream_t s, uint64_t piece) : c_(c), s_(s) {
+  D2HStream(rsk_ctx* c, hipStream_t s, uint64_t piece, int engine = -1) : c_(c), s_(s) {
     ensure_pinned(c);
     if (c->pin_off) return;
     pinned_idle(c);  // a stage may still feed a DMA an earlier h2d_staged queued
+    eng_ = engine;
     S_ = piece;
     const uint64_t B = c->stage_bytes + c->stage_bytes / 4;
     const uint32_t per = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, B / S_));
     NS_ = 2 * (per >= 4 ? 4 : per >= 2 ? 2 : 1);
   }
-  // bytes from device src to host dst, on the stream after event `after` (when not null)
+  // bytes from device src to host dst, after event `after` (when not null)
   void put(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipEvent_t after) {
+    const rsk_ctx::HostReg* reg = c_->pin_off ? nullptr : c_->host_reg(dst, bytes);
+    if (eng_ >= 0 && (!reg || reg->dptr)) {
+      if (after) service_until(after);  // the source is written (copy-outs meanwhile)
+      for (uint64_t o = 0; o < bytes; o += S_) {
+        const uint64_t m = std::min<uint64_t>(S_, bytes - o);
+        if (fifo_n_ == NS_ - 1) pop();
+        const uint32_t j = (uint32_t)(issued_++ % NS_);
+        void* to = reg ? reinterpret_cast<void*>(reg->dptr + (reinterpret_cast<uintptr_t>(dst + o) - reg->base)) : slot(j);
+        fifo_[(head_ + fifo_n_++) % 8] = Piece{dst + o, m, j, reg != nullptr};
+        if (!engine_copy(c_, eng_, c_->eng_sig[j], to, src + o, m)) {
+          hsa_signal_store_relaxed(c_->eng_sig[j], 0);  // (never issued)
+          fail(RSK_ERR_DEVICE, "device->host copy on SDMA engine " + std::to_string(eng_) + " refused");
+        }
+      }
+      return;
+    }
     if (after) RSK_HIP(hipStreamWaitEvent(s_, after, 0));
-    if (c_->pin_off || c_->host_registered(dst, bytes)) {  // (a registered range: DMA straight into it)
+    if (c_->pin_off || reg) {  // (a registered range: DMA straight into it)
       if (bytes) RSK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_));
       return;
     }
@@ -419,7 +532,7 @@ class D2HStream {
       const uint32_t j = (uint32_t)(issued_++ % NS_);
       RSK_HIP(hipMemcpyAsync(slot(j), src + o, m, hipMemcpyDeviceToHost, s_));
       RSK_HIP(hipEventRecord(c_->ring_ev[j], s_));
-      fifo_[(head_ + fifo_n_++) % 8] = Piece{dst + o, m, j};
+      fifo_[(head_ + fifo_n_++) % 8] = Piece{dst + o, m, j, false};
     }
   }
   // wait for event e, copying out the pieces whose DMA is done meanwhile (the ring keeps moving)
@@ -428,12 +541,27 @@ class D2HStream {
       const hipError_t q = hipEventQuery(e);
       if (q == hipSuccess) return;
       if (q != hipErrorNotReady) RSK_HIP(q);
-      if (fifo_n_ && hipEventQuery(c_->ring_ev[fifo_[head_].slot]) == hipSuccess) pop();
+      if (fifo_n_ && done(fifo_[head_].slot)) pop();
       else std::this_thread::yield();
     }
   }
+  // pieces put so far (a mark for order_after)
+  uint64_t issued() const { return issued_; }
+  // the device work queued on stream s next may overwrite the sources of the pieces put before
+  // `mark`: after event ev (recorded on this stream behind them) and, on an engine, once they are done
+  void order_after(uint64_t mark, hipEvent_t ev, hipStream_t s) {
+    RSK_HIP(hipStreamWaitEvent(s, ev, 0));
+    if (eng_ >= 0)
+      while (issued_ - fifo_n_ < mark) pop();
+  }
   ~D2HStream() {  // unwound by an error: no DMA may still fill a stage the next call refills
-    if (fifo_n_) (void)hipStreamSynchronize(s_);
+    if (!fifo_n_) return;
+    if (eng_ < 0) {
+      (void)hipStreamSynchronize(s_);
+      return;
+    }
+    for (uint32_t i = 0; i < fifo_n_; ++i) (void)engine_wait(c_->eng_sig[fifo_[(head_ + i) % 8].slot]);
+    (void)hipStreamSynchronize(s_);
   }
   // every piece copied out, the stream synchronised
   void drain() {
@@ -446,17 +574,26 @@ class D2HStream {
     uint8_t* dst;
     uint64_t bytes;
     uint32_t slot;
+    bool direct;  // DMA'd into its destination: nothing to copy out
   };
   uint8_t* slot(uint32_t j) const { return c_->h_pin[j & 1] + (uint64_t)(j >> 1) * S_; }
+  bool done(uint32_t j) const {
+    return eng_ >= 0 ? hsa_signal_load_scacquire(c_->eng_sig[j]) < 1 : hipEventQuery(c_->ring_ev[j]) == hipSuccess;
+  }
   void pop() {
     const Piece p = fifo_[head_];
     head_ = (head_ + 1) % 8;
     --fifo_n_;
-    RSK_HIP(hipEventSynchronize(c_->ring_ev[p.slot]));
-    par_copy(p.dst, slot(p.slot), p.bytes, c_->stage_threads, c_->tune.copy_nt >= 0);
+    if (eng_ >= 0) {
+      if (engine_wait(c_->eng_sig[p.slot]) < 0) fail(RSK_ERR_DEVICE, "device->host copy on an SDMA engine failed");
+    } else {
+      RSK_HIP(hipEventSynchronize(c_->ring_ev[p.slot]));
+    }
+    if (!p.direct) par_copy(p.dst, slot(p.slot), p.bytes, c_->stage_threads, c_->tune.copy_nt >= 0);
   }
   rsk_ctx* c_;
   hipStream_t s_;
+  int eng_ = -1;
   uint64_t S_ = 0, issued_ = 0;
   uint32_t NS_ = 2, head_ = 0, fifo_n_ = 0;
   Piece fifo_[8] = {};
@@ -965,8 +1102,10 @@ int rsk_shutdown(rsk_ctx* c) {
     c->async_all.clear();
     c->async_free.clear();
     if (c->comm) (void)rsk_comm_destroy(c);
-    for (const auto& r : c->host_regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+    for (const auto& r : c->host_regs) (void)hipHostUnregister(reinterpret_cast<void*>(r.base));
     c->host_regs.clear();
+    for (hsa_signal_t& g : c->eng_sig)
+      if (g.handle) (void)hsa_signal_destroy(g);
     (void)hipStreamDestroy(c->stream);
     if (c->xin) (void)hipStreamDestroy(c->xin);
     if (c->xout) (void)hipStreamDestroy(c->xout);
@@ -983,9 +1122,9 @@ int rsk_host_register(rsk_ctx* c, void* p, uint64_t bytes) {
     CtxLock l(c);
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     for (const auto& r : c->host_regs)
-      need(a + bytes <= r.first || a >= r.first + r.second, "range overlaps a registered one");
+      need(a + bytes <= r.base || a >= r.base + r.bytes, "range overlaps a registered one");
     RSK_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
-    c->host_regs.push_back({a, bytes});
+    c->host_regs.push_back({a, bytes, rsk::reg_dptr(p)});
   });
 }
 
@@ -998,7 +1137,7 @@ int rsk_host_unregister(rsk_ctx* c, void* p) {
     RSK_HIP(hipStreamSynchronize(c->xin));
     RSK_HIP(hipStreamSynchronize(c->xout));
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    auto it = std::find_if(c->host_regs.begin(), c->host_regs.end(), [&](const auto& r) { return r.first == a; });
+    auto it = std::find_if(c->host_regs.begin(), c->host_regs.end(), [&](const auto& r) { return r.base == a; });
     need(it != c->host_regs.end(), "not a registered range");
     c->host_regs.erase(it);
     RSK_HIP(hipHostUnregister(p));
@@ -1735,7 +1874,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
         (void)hipStreamSynchronize(c->stream);
         auto& v = c->host_regs;
         for (size_t i = 0; i < v.size(); ++i)
-          if (v[i].first == reinterpret_cast<uintptr_t>(p)) {
+          if (v[i].base == reinterpret_cast<uintptr_t>(p)) {
             v.erase(v.begin() + (long)i);
             break;
           }
@@ -1746,11 +1885,12 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       if (hipHostRegister(out, cap, hipHostRegisterDefault) == hipSuccess) {
         treg.c = c;
         treg.p = out;
-        c->host_regs.push_back({reinterpret_cast<uintptr_t>(out), cap});
+        c->host_regs.push_back({reinterpret_cast<uintptr_t>(out), cap, rsk::reg_dptr(out)});
       } else {
         (void)hipGetLastError();
       }
     }
+    const int eng = export_engine(c);  // (before any of this call's work is queued)
     // keys the device encodes (present, not a kept SET string), in call order
     std::vector<uint64_t> dev_i, dev_id;
     std::vector<uint8_t> want;
@@ -1840,7 +1980,8 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     // chunk k's strings leave through the copy stream (c->xout) while chunk k + 1 encodes and
     // packs; the pieces of every chunk go through one D2H stream (16 MiB pieces, up to 7 in
     // flight), so the copy engine runs on across chunk boundaries
-    D2HStream xo(c, c->xout, (c->tune.io_piece ? (uint64_t)c->tune.io_piece : 16ull) << 20);  // (A/B: io_piece MiB)
+    D2HStream xo(c, c->xout, (c->tune.io_piece ? (uint64_t)c->tune.io_piece : 16ull) << 20, eng);  // (A/B: io_piece MiB)
+    uint64_t left[2] = {0, 0};  // xo.issued() after each stage's last put
     const bool trace = c->tune.io_trace != 0;  // (route io_trace: phase times to stderr)
     double t_sync = 0, t_adv = 0, t_pack = 0, t_enc = 0, t_d2h = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -1865,7 +2006,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
         end = offsets[dev_i[d0 + m - 1] + 1];
         for (uint64_t d = 0; d < m; ++d) pos[d] = offsets[dev_i[d0 + d]] - base;
         xfer(c, d_pos, pos, 8 * m);
-        if (ck >= 2) RSK_HIP(hipStreamWaitEvent(c->stream, out_done[ck & 1], 0));  // chunk k - 2 left this stage
+        if (ck >= 2) xo.order_after(left[ck & 1], out_done[ck & 1], c->stream);  // chunk k - 2 left this stage
         hll_export_pack_launch(c, d_slots, d_len, d_pos, (uint32_t)m, stage);
         RSK_HIP(hipEventRecord(packed, c->stream));
       }
@@ -1877,6 +2018,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       if (fits) {
         xo.put(out + base, stage, end - base, packed);  // returns with up to 7 pieces in flight
         RSK_HIP(hipEventRecord(out_done[ck & 1], c->xout));
+        left[ck & 1] = xo.issued();
         if (c->tune.io_drain) xo.drain();  // (A/B: each chunk's copy-out finished before the next chunk)
       }
       t_d2h += ms(t0, now());
@@ -1887,8 +2029,8 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       t_d2h += ms(t0, now());
     }
     if (trace)
-      std::fprintf(stderr, "export: loop %.2f ms: sync %.2f advance %.2f pack %.2f encode %.2f d2h %.2f\n",
-                   ms(t00, now()), t_sync, t_adv, t_pack, t_enc, t_d2h);
+      std::fprintf(stderr, "export: loop %.2f ms: sync %.2f advance %.2f pack %.2f encode %.2f d2h %.2f (engine %d)\n",
+                   ms(t00, now()), t_sync, t_adv, t_pack, t_enc, t_d2h, eng);
     advance(n, dcur);  // the keys after the last device key
     if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
     need(out != nullptr || o == 0, "out is NULL");

@@ -76,6 +76,12 @@ def main():
                       "export_ms_each": [round(t * 1e3, 2) for t in te], "no_import": no_import,
                       "thp": os.environ.get("IO_THP"), "torch": bool(os.environ.get("IO_TORCH")),
                       "device_ms": dev}), flush=True)
+    if os.environ.get("IO_SDMA"):  # per-engine copy rates in this same process (scripts/sdma_probe.cpp)
+        import ctypes
+
+        lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libsdma_probe.so"))
+        lib.sdma_probe_run.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        lib.sdma_probe_run(64, 1, 4)
 
 
 if __name__ == "__main__":

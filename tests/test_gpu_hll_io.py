@@ -436,15 +436,16 @@ def test_import_batch_long_sparse(L, engine, orc):
     L.rsk_hll_destroy(h)
 
 
-@pytest.mark.parametrize("pin", [0, -1])
-def test_dense_pool_round_trip_many_pieces(L, engine, orc, route, pin):
+@pytest.mark.parametrize("pin,copy", [(0, 0), (-1, 0), (0, -1), (-1, -1)])
+def test_dense_pool_round_trip_many_pieces(L, engine, orc, route, pin, copy):
     """70000 dense keys (861 MB of strings): one export chunk is ~806 MB, so
     the staged copy-out (route io_pin = -1) cycles its ring of pinned slots
     several times, or the output buffer is pinned for the call and takes the
-    DMA (the default for a buffer >= 256 MiB); the import stages ~861 MB in
-    pieces; SET then GET returns the same bytes, and the registers equal the
-    oracle's decode."""
-    route(io_pin=pin)
+    DMA (the default for a buffer >= 256 MiB), the DMAs on the measured SDMA
+    engine (route io_engine = 0) or HIP's copies (-1); the import stages
+    ~861 MB in pieces; SET then GET returns the same bytes, and the registers
+    equal the oracle's decode."""
+    route(io_pin=pin, io_engine=copy)
     rng = np.random.default_rng(29)
     G = 70000
     rows = rng.integers(0, 25, size=(64, 16384), dtype=np.uint8)
@@ -548,3 +549,48 @@ def test_export_import_through_registered_host_buffers(L, engine, orc):
     with pytest.raises(_lib.IllegalArgumentException):
         engine.host_unregister(reg)
     pool.close()
+
+
+def test_export_on_every_copy_engine_gives_the_same_bytes(L, engine, orc, route):
+    """The batched export's device->host copies on an SDMA engine chosen by
+    measurement (route io_engine = 0), on each engine forced (io_engine = k:
+    engine k - 1), and on HIP's copies (-1) give the same strings, staged
+    through the pinned ring (io_pin = -1), into a buffer the call pins, and
+    into a caller-registered buffer; the measured engine is the fastest."""
+    from redisson_amd import _lib
+
+    rng = np.random.default_rng(31)
+    G = 4000  # 49 MB of dense strings: several 16 MiB pieces
+    rows = rng.integers(0, 25, size=(16, 16384), dtype=np.uint8)
+    strs16 = [bytes(orc.hll_encode_dense(r)) for r in rows]
+    pick = rng.integers(0, 16, G)
+    strs = [strs16[j] for j in pick]
+    want = np.frombuffer(b"".join(strs), np.uint8)
+    h = _pool(L, engine, G)
+    ids = np.arange(G)
+    assert _import_batch(L, h, ids, strs) == 0
+    route(io_engine=-1, io_pin=-1)
+    rc, out, offs = _export_batch(L, h, ids)
+    assert rc == 0 and np.array_equal(out[: want.size], want)
+    route(io_engine=0, io_pin=-1)
+    rc, out, offs = _export_batch(L, h, ids)
+    assert rc == 0 and np.array_equal(out[: want.size], want)
+    eng, rates = engine.copy_engine()
+    assert eng >= 0, (eng, rates)
+    assert rates[eng] == max(rates) > 0, rates
+    for k in [e + 1 for e in range(8) if rates[e] > 0]:
+        for pin in (-1, 0):  # (0 with a 256 MiB buffer: the call pins it)
+            route(io_engine=k, io_pin=pin)
+            rc, out, offs = _export_batch(L, h, ids, cap=None if pin else 256 << 20)
+            assert rc == 0 and np.array_equal(out[: want.size], want), (k, pin)
+    route(io_engine=0, io_pin=0)
+    reg = np.zeros(want.size + 8192, np.uint8)
+    engine.host_register(reg)
+    try:
+        offs = np.zeros(G + 1, np.uint64)
+        uids = ids.astype(np.uint64)
+        _lib.check(L.rsk_hll_export_redis_batch(h, uids.ctypes.data, G, reg.ctypes.data, reg.size, offs.ctypes.data))
+        assert int(offs[-1]) == want.size and np.array_equal(reg[: want.size], want)
+    finally:
+        engine.host_unregister(reg)
+    L.rsk_hll_destroy(h)
