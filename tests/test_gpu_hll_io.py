@@ -241,10 +241,10 @@ def test_export_batch_small_buffer(L, engine, orc):
 
 
 def test_export_batch_chunks_and_late_overflow(L, engine, orc):
-    """More keys than one encode chunk (65536): the chunked export equals the
-    per-key GET at the chunk edges, and a cap one byte short of the total
-    fails with offsets[n] = the bytes needed, the first chunk's strings
-    written."""
+    """More keys than one encode chunk (16384 keys, then 65536 per chunk): the
+    chunked export equals the per-key GET at the chunk edges, and a cap one
+    byte short of the total fails with offsets[n] = the bytes needed, the
+    first chunk's strings written."""
     from redisson_amd import KeyBatch, _lib
 
     G = 70000
@@ -260,12 +260,12 @@ def test_export_batch_chunks_and_late_overflow(L, engine, orc):
     assert rc == 0
     need = int(offs[-1])
     got = _strings(out, offs)
-    for i in (0, 1, 65535, 65536, 65537, G - 1):
+    for i in (0, 1, 16383, 16384, 65535, 65536, 65537, G - 1):
         assert got[i] == _export1(L, h, i), i
     rc2, out2, offs2 = _export_batch(L, h, ids, cap=need - 1)
     assert rc2 == _lib.RSK_ERR_INVALID_ARG and int(offs2[-1]) == need
     assert np.array_equal(offs2, offs)
-    first = int(offs[65536])
+    first = int(offs[16384])
     assert np.array_equal(out2[:first], out[:first])
     L.rsk_hll_destroy(h)
 
