@@ -2470,9 +2470,26 @@ int rsk_bloom_export_bits(rsk_bloom* b, uint8_t* buf, size_t cap, size_t* len) {
   return guarded([&] {
     need(b && len, "NULL argument");
     need(buf != nullptr && cap >= b->nbytes, "buffer smaller than ceil(size/8)");
-    CtxLock l(b->ctx);
-    RSK_HIP(hipMemcpyAsync(buf, b->d_bits, b->nbytes, hipMemcpyDeviceToHost, b->ctx->stream));
-    RSK_HIP(hipStreamSynchronize(b->ctx->stream));
+    rsk_ctx* c = b->ctx;
+    CtxLock l(c);
+    if (b->nbytes < (64ull << 20)) {
+      RSK_HIP(hipMemcpyAsync(buf, b->d_bits, b->nbytes, hipMemcpyDeviceToHost, c->stream));
+      RSK_HIP(hipStreamSynchronize(c->stream));
+    } else {
+      // a large filter (C3: 1.2 GB) goes out as the batched HLL export's strings do: 16 MiB pieces
+      // on the fastest SDMA engine through the pinned ring (or straight into a registered buffer)
+      const int eng = export_engine(c);
+      hipEvent_t written = nullptr;
+      RSK_HIP(hipEventCreateWithFlags(&written, hipEventDisableTiming));
+      struct EvGuard {
+        hipEvent_t e;
+        ~EvGuard() { (void)hipEventDestroy(e); }
+      } eg{written};
+      RSK_HIP(hipEventRecord(written, c->stream));
+      D2HStream xo(c, c->xout, 16ull << 20, eng);
+      xo.put(buf, reinterpret_cast<const uint8_t*>(b->d_bits), b->nbytes, written);
+      xo.drain();
+    }
     *len = b->nbytes;
   });
 }
@@ -2484,7 +2501,8 @@ int rsk_bloom_import_bits(rsk_bloom* b, const uint8_t* buf, size_t len) {
     need(buf != nullptr || len == 0, "buf is NULL");
     CtxLock l(b->ctx);
     RSK_HIP(hipMemsetAsync(b->d_bits, 0, b->nwords * 4, b->ctx->stream));
-    if (len) RSK_HIP(hipMemcpyAsync(b->d_bits, buf, len, hipMemcpyHostToDevice, b->ctx->stream));
+    if (len >= (64ull << 20)) h2d_staged(b->ctx, reinterpret_cast<uint8_t*>(b->d_bits), buf, len);  // (pinned stages)
+    else if (len) RSK_HIP(hipMemcpyAsync(b->d_bits, buf, len, hipMemcpyHostToDevice, b->ctx->stream));
     RSK_HIP(hipStreamSynchronize(b->ctx->stream));
     ++b->wgen;  // SET of the whole string: its views take STRLEN = len
     ++b->rgen;

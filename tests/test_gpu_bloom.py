@@ -325,3 +325,36 @@ def test_c3_full_size_bit_exact(L, engine, orc):
     trues = orc.bloom_contains_gen_queries_mt(ref_bits, size, k, 0x5EED0004, 0x5EED0003, n, 0, n, want, threads)
     assert np.array_equal(got, want)
     assert 0.50 < trues / n < 0.52  # half members + ~1% false positives on the fresh half
+
+
+@pytest.mark.parametrize("copy", [0, -1])
+def test_large_filter_bits_round_trip(L, engine, route, copy):
+    """A filter of 2^30 + 12345 bits (128 MiB, not a whole number of 16 MiB
+    pieces): SET of a random bit string (rsk_bloom_import_bits, through the
+    pinned stages) then GET (rsk_bloom_export_bits, through the D2H ring on
+    the measured SDMA engine -- route io_engine = 0 -- or HIP's copies, -1;
+    and straight into a caller-registered buffer) returns the same bytes, and
+    BITCOUNT equals the host popcount."""
+    from redisson_amd import _lib
+
+    route(io_engine=copy)
+    size = (1 << 30) + 12345
+    nb = (size + 7) // 8
+    rng = np.random.default_rng(33)
+    src = rng.integers(0, 256, nb, dtype=np.uint8)
+    src[-1] &= 0xFF << (8 - size % 8) & 0xFF  # (bits past size stay clear)
+    b = _filter(L, engine, size, 3)
+    _lib.check(L.rsk_bloom_import_bits(b, src.ctypes.data, src.size))
+    assert np.array_equal(_bits(L, b, size), src)
+    bc = ctypes.c_uint64()
+    _lib.check(L.rsk_bloom_bitcount(b, ctypes.byref(bc)))
+    assert bc.value == int(np.unpackbits(src).sum())
+    reg = np.zeros(nb + 4096, np.uint8)
+    engine.host_register(reg)
+    try:
+        n = ctypes.c_size_t()
+        _lib.check(L.rsk_bloom_export_bits(b, reg.ctypes.data, reg.size, ctypes.byref(n)))
+        assert n.value == nb and np.array_equal(reg[:nb], src)
+    finally:
+        engine.host_unregister(reg)
+    L.rsk_bloom_destroy(b)
