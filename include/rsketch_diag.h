@@ -71,11 +71,12 @@ int rsk_diag_set_route(rsk_ctx *ctx, const char *name, int64_t value);
  * fallback (a group's pending probes overflowed its LDS tables). */
 int rsk_diag_reply_stats(rsk_ctx *ctx, uint64_t *pending_groups, uint64_t *fallbacks);
 
-/* The SDMA engine the batched export's device->host copies use on this
- * context (-2: not measured yet, no export so far; -1: HIP's own copies) and
- * the device->host rate measured on each of engines 0..7 (GB/s; 0: not
+/* The SDMA engine the batched export's device->host copies (to_host = 1) or
+ * the batched import's host->device copies (to_host = 0) use on this context
+ * (-2: not measured yet, no export / import so far; -1: HIP's own copies) and
+ * the rate measured in that direction on each of engines 0..7 (GB/s; 0: not
  * measured or not available). */
-int rsk_diag_copy_engine(rsk_ctx *ctx, int *engine, float *rates);
+int rsk_diag_copy_engine(rsk_ctx *ctx, int to_host, int *engine, float *rates);
 
 /* Marks a context dead, as a device error on one of its streams does: every
  * later call but rsk_shutdown fails with RSK_ERR_DEVICE (tests of the

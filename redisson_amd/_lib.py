@@ -187,7 +187,7 @@ DIAG_SIGNATURES = {
     "rsk_diag_last_error": (ctypes.c_char_p, []),
     "rsk_diag_set_route": (ctypes.c_int, [_vp, ctypes.c_char_p, _i64]),
     "rsk_diag_reply_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
-    "rsk_diag_copy_engine": (ctypes.c_int, [_vp, _P(ctypes.c_int), _P(ctypes.c_float)]),
+    "rsk_diag_copy_engine": (ctypes.c_int, [_vp, ctypes.c_int, _P(ctypes.c_int), _P(ctypes.c_float)]),
     "rsk_diag_mark_dead": (ctypes.c_int, [_vp]),
     "rsk_diag_membench": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _u64, _u64, _P(ctypes.c_double)]),
     "rsk_diag_p2p_probe": (ctypes.c_int, [_vp, _u64, ctypes.c_int, _P(_u64), _P(_u64)]),
@@ -394,12 +394,14 @@ class Engine:
         check_diag(diag().rsk_diag_reply_stats(self.ctx, ctypes.byref(pg), ctypes.byref(fb)), "rsk_diag_reply_stats")
         return pg.value, fb.value
 
-    def copy_engine(self):
-        """(engine, rates): the SDMA engine of this context's batched-export copies (-2 not
-        measured yet, -1 HIP's copies) and the GB/s measured on engines 0..7 (rsk_diag_copy_engine)."""
+    def copy_engine(self, to_host=True):
+        """(engine, rates): the SDMA engine of this context's batched-export (to_host) or
+        batched-import copies (-2 not measured yet, -1 HIP's copies) and the GB/s measured in
+        that direction on engines 0..7 (rsk_diag_copy_engine)."""
         e = ctypes.c_int()
         r = (ctypes.c_float * 8)()
-        check_diag(diag().rsk_diag_copy_engine(self.ctx, ctypes.byref(e), r), "rsk_diag_copy_engine")
+        check_diag(diag().rsk_diag_copy_engine(self.ctx, int(bool(to_host)), ctypes.byref(e), r),
+                   "rsk_diag_copy_engine")
         return e.value, [round(float(x), 2) for x in r]
 
     def routes(self, **kw):

@@ -214,12 +214,12 @@ int rsk_diag_set_route(rsk_ctx* c, const char* name, int64_t value) {
   });
 }
 
-int rsk_diag_copy_engine(rsk_ctx* c, int* engine, float* rates) {
+int rsk_diag_copy_engine(rsk_ctx* c, int to_host, int* engine, float* rates) {
   return diag::guarded([&] {
     diag::need(c && engine && rates, "NULL argument");
     diag::Lock l(c);
-    *engine = c->d2h_engine;
-    for (int e = 0; e < 8; ++e) rates[e] = c->d2h_rate[e];
+    *engine = to_host ? c->d2h_engine : c->h2d_engine;
+    for (int e = 0; e < 8; ++e) rates[e] = to_host ? c->d2h_rate[e] : c->h2d_rate[e];
   });
 }
 

@@ -399,12 +399,13 @@ uint64_t staged_piece(const rsk_ctx* c, uint64_t bytes) {
 void pinned_idle(rsk_ctx* c) {
   for (int b = 0; b < 2; ++b) RSK_HIP(hipEventSynchronize(c->pin_ev[b]));
 }
-// The SDMA engine of the batched export's device->host copies (rsk_ctx::d2h_engine).  The
-// engine the runtime picks for device->host copies is not the fastest on every box: round 6
-// measured one engine at 26-30 GB/s and its neighbours at 57 on some boxes
-// (profiles/r06_sdma_engines.jsonl), so each of the first 8 engines the runtime reports free
-// moves a 4 MiB warm-up and then 32 MiB from a device scratch into a pinned stage, once per
-// context (~10 ms), and the fastest is kept.  Anything the runtime refuses: HIP's copies (-1).
+// The SDMA engines of the batched export's device->host copies and the batched import's
+// host->device ones (rsk_ctx::d2h_engine / h2d_engine).  The engine the runtime picks is not
+// the fastest on every box: round 6 measured one engine at 26-30 GB/s both ways and its
+// neighbours at 57 on some boxes (profiles/r06_sdma_engines.jsonl), so each of the first 8
+// engines the runtime reports free moves a 4 MiB warm-up and then 32 MiB between a device
+// scratch and a pinned stage in each direction, once per context (~15 ms), and the fastest per
+// direction is kept.  Anything the runtime refuses: HIP's copies (-1).
 static hsa_status_t first_cpu_agent(hsa_agent_t a, void* out) {
   hsa_device_type_t t;
   if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
@@ -414,10 +415,12 @@ static hsa_status_t first_cpu_agent(hsa_agent_t a, void* out) {
   return HSA_STATUS_SUCCESS;
 }
 
-// one device->host copy of `bytes` on engine e, signal g (1 while in flight)
-static bool engine_copy(rsk_ctx* c, int e, hsa_signal_t g, void* to, const void* from, uint64_t bytes) {
+// one copy of `bytes` on engine e, signal g (1 while in flight): device->host, or host->device
+static bool engine_copy(rsk_ctx* c, int e, hsa_signal_t g, void* to, const void* from, uint64_t bytes,
+                        bool to_host = true) {
   hsa_signal_store_relaxed(g, 1);
-  return hsa_amd_memory_async_copy_on_engine(to, c->cpu_agent, from, c->gpu_agent, bytes, 0, nullptr, g,
+  return hsa_amd_memory_async_copy_on_engine(to, to_host ? c->cpu_agent : c->gpu_agent, from,
+                                             to_host ? c->gpu_agent : c->cpu_agent, bytes, 0, nullptr, g,
                                              (hsa_amd_sdma_engine_id_t)(1u << e), false) == HSA_STATUS_SUCCESS;
 }
 static hsa_signal_value_t engine_wait(hsa_signal_t g) {
@@ -427,8 +430,8 @@ static hsa_signal_value_t engine_wait(hsa_signal_t g) {
   return v;
 }
 
-void measure_d2h_engines(rsk_ctx* c) {
-  c->d2h_engine = -1;
+void measure_copy_engines(rsk_ctx* c) {
+  c->d2h_engine = c->h2d_engine = -1;
   if (hsa_init() != HSA_STATUS_SUCCESS) return;  // (the runtime HIP runs on: a reference, never shut down)
   const uint64_t B = c->stage_bytes + c->stage_bytes / 4;
   const uint64_t warm = std::min<uint64_t>(4ull << 20, B), big = std::min<uint64_t>(32ull << 20, B);
@@ -447,38 +450,103 @@ void measure_d2h_engines(rsk_ctx* c) {
   if (ok) {
     c->gpu_agent = info.agentOwner;
     c->cpu_agent = cpu;
-    uint32_t mask = 0;
-    if (hsa_amd_memory_copy_engine_status(cpu, c->gpu_agent, &mask) != HSA_STATUS_SUCCESS) mask = 0xFF;
-    float best = 0;
-    for (int e = 0; e < 8; ++e) {
-      if (!(mask >> e & 1)) continue;
-      const hsa_signal_t g = c->eng_sig[0];
-      if (!engine_copy(c, e, g, c->h_pin[0], d, warm) || engine_wait(g) < 0) continue;
-      const auto t0 = std::chrono::steady_clock::now();
-      if (!engine_copy(c, e, g, c->h_pin[0], d, big) || engine_wait(g) < 0) continue;
-      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      c->d2h_rate[e] = (float)(big / s / 1e9);
-      if (c->d2h_rate[e] > best) {
-        best = c->d2h_rate[e];
-        c->d2h_engine = e;
+    for (int dir = 0; dir < 2; ++dir) {  // 0: device -> host, 1: host -> device
+      const bool to_host = dir == 0;
+      uint32_t mask = 0;
+      if ((to_host ? hsa_amd_memory_copy_engine_status(cpu, c->gpu_agent, &mask)
+                   : hsa_amd_memory_copy_engine_status(c->gpu_agent, cpu, &mask)) != HSA_STATUS_SUCCESS)
+        mask = 0xFF;
+      float* rate = to_host ? c->d2h_rate : c->h2d_rate;
+      int& pick = to_host ? c->d2h_engine : c->h2d_engine;
+      float best = 0;
+      void* to = to_host ? (void*)c->h_pin[0] : (void*)d;
+      const void* from = to_host ? (const void*)d : (const void*)c->h_pin[0];
+      for (int e = 0; e < 8; ++e) {
+        if (!(mask >> e & 1)) continue;
+        const hsa_signal_t g = c->eng_sig[0];
+        if (!engine_copy(c, e, g, to, from, warm, to_host) || engine_wait(g) < 0) continue;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (!engine_copy(c, e, g, to, from, big, to_host) || engine_wait(g) < 0) continue;
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        rate[e] = (float)(big / sec / 1e9);
+        if (rate[e] > best) {
+          best = rate[e];
+          pick = e;
+        }
       }
     }
   }
   (void)hipFree(d);
 }
 
-// The engine of this export's copies: route io_engine, else the measured fastest (-1: HIP's copies).
-int export_engine(rsk_ctx* c) {
+// The engine of this call's copies in one direction: route io_engine, else the measured
+// fastest (-1: HIP's copies).
+int copy_engine(rsk_ctx* c, bool to_host) {
   if (c->tune.io_engine < 0) return -1;
   ensure_pinned(c);
   if (c->pin_off) return -1;
   if (c->d2h_engine == -2) {
-    pinned_idle(c);  // (the measurement writes a stage)
-    measure_d2h_engines(c);
+    pinned_idle(c);  // (the measurement uses a stage)
+    measure_copy_engines(c);
   }
   if (!c->gpu_agent.handle) return -1;
-  return c->tune.io_engine > 0 ? std::min(c->tune.io_engine - 1, 15) : c->d2h_engine;
+  return c->tune.io_engine > 0 ? std::min(c->tune.io_engine - 1, 15) : to_host ? c->d2h_engine : c->h2d_engine;
 }
+int export_engine(rsk_ctx* c) { return copy_engine(c, true); }
+
+// Pageable (or registered) host -> device on SDMA engine `engine` through the two pinned stages:
+// a ring of NS slots of S bytes, a host copy into each slot while the engine moves the previous
+// one, each piece's completion a signal; a registered range is copied straight from (no slot).
+// put() returns with the pieces issued (their host copies done); wait_upto(mark) waits for the
+// pieces issued before mark -- the device work that reads them is launched after that.
+class H2DStream {
+ public:
+  H2DStream(rsk_ctx* c, int engine, uint64_t piece) : c_(c), eng_(engine), S_(piece) {
+    pinned_idle(c);  // (a stage may still feed an earlier HIP copy)
+    const uint64_t B = c->stage_bytes + c->stage_bytes / 4;
+    const uint32_t per = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, B / S_));
+    NS_ = 2 * (per >= 4 ? 4 : per >= 2 ? 2 : 1);
+  }
+  void put(uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+    const rsk_ctx::HostReg* reg = c_->host_reg(src, bytes);
+    if (reg && !reg->dptr) reg = nullptr;
+    for (uint64_t o = 0; o < bytes; o += S_) {
+      const uint64_t m = std::min<uint64_t>(S_, bytes - o);
+      if (issued_ - done_ == NS_) wait_upto(done_ + 1);  // the slot (and signal) this piece takes is free
+      const uint32_t j = (uint32_t)(issued_ % NS_);
+      const void* from;
+      if (reg) {
+        from = reinterpret_cast<const void*>(reg->dptr + (reinterpret_cast<uintptr_t>(src + o) - reg->base));
+      } else {
+        par_copy(slot(j), src + o, m, c_->stage_threads, c_->tune.copy_nt >= 0);
+        from = slot(j);
+      }
+      if (!engine_copy(c_, eng_, c_->eng_sig[j], dst + o, from, m, false)) {
+        hsa_signal_store_relaxed(c_->eng_sig[j], 0);  // (never issued)
+        fail(RSK_ERR_DEVICE, "host->device copy on SDMA engine " + std::to_string(eng_) + " refused");
+      }
+      ++issued_;
+    }
+  }
+  uint64_t issued() const { return issued_; }
+  void wait_upto(uint64_t mark) {
+    for (; done_ < mark; ++done_)
+      if (engine_wait(c_->eng_sig[done_ % NS_]) < 0) {
+        ++done_;
+        fail(RSK_ERR_DEVICE, "host->device copy on an SDMA engine failed");
+      }
+  }
+  ~H2DStream() {  // unwound by an error: no DMA may still read a stage or write the device
+    for (; done_ < issued_; ++done_) (void)engine_wait(c_->eng_sig[done_ % NS_]);
+  }
+
+ private:
+  uint8_t* slot(uint32_t j) const { return c_->h_pin[j & 1] + (uint64_t)(j >> 1) * S_; }
+  rsk_ctx* c_;
+  int eng_;
+  uint64_t S_, issued_ = 0, done_ = 0;
+  uint32_t NS_ = 2;
+};
 
 // Device -> pageable host through the two pinned stages, as a stream of
 // pieces that may span several calls of put(): a ring of NS slots over the two
@@ -2233,27 +2301,57 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     const auto t0 = now();
     uint64_t checked = 0;  // chunks [0, checked) have their check queued
     bool hdr_ok = false;
+    // On an SDMA engine (the fastest measured, copy_engine) the strings go up as engine copies
+    // instead, and chunk q's check is launched once its pieces are in, after chunk q + 1's first
+    // pieces are on their way (so the engine is not idle while the host launches it).
+    auto launch_chunk = [&](uint64_t qq) {  // chunk qq's check (and, early, its rows aside and its decode)
+      const uint64_t a = cut[qq], b = cut[qq + 1];
+      hll_import_launch(c, d_data, d_off + a, d_ids + a, nullptr, (uint32_t)(b - a), h->d_regs, h->d_card,
+                        d_canon + a, d_err, (uint32_t)a);
+      if (early) {
+        hll_rows_bak_launch(c, false, h->d_regs, h->d_card, d_ids + a, d_apply + a, (uint32_t)(b - a),
+                            d_bak + a * (uint64_t)HLL_REGS, d_bak_card + a, d_err);
+        hll_import_launch(c, d_data, d_off + a, d_ids + a, d_apply + a, (uint32_t)(b - a), h->d_regs, h->d_card,
+                          d_canon + a, d_err, (uint32_t)a);
+      }
+    };
+    const int ein = copy_engine(c, false);
+    std::unique_ptr<H2DStream> xi;
+    if (ein >= 0) {
+      RSK_HIP(hipEventSynchronize(up));  // the device work queued before (it may use this scratch) is done
+      xi.reset(new H2DStream(c, ein, 16ull << 20));
+    }
+    uint64_t in_mark[NCH] = {}, apply_mark = 0;  // xi->issued() after each chunk / after d_apply
     for (uint64_t q = 0; q < NCH; ++q) {
       const uint64_t i0 = cut[q], i1 = cut[q + 1];
-      h2d_staged_on(c, c->xin, d_data + off[i0], data + offsets[i0], off[i1] - off[i0]);
-      RSK_HIP(hipEventRecord(up, c->xin));
-      RSK_HIP(hipStreamWaitEvent(c->stream, up, 0));  // chunk q's check after its strings
+      if (xi) {
+        xi->put(d_data + off[i0], data + offsets[i0], off[i1] - off[i0]);
+        in_mark[q] = xi->issued();
+      } else {
+        h2d_staged_on(c, c->xin, d_data + off[i0], data + offsets[i0], off[i1] - off[i0]);
+        RSK_HIP(hipEventRecord(up, c->xin));
+        RSK_HIP(hipStreamWaitEvent(c->stream, up, 0));  // chunk q's check after its strings
+      }
       if (!hdr_ok) {
         headers();
         hdr_ok = true;
-        if (early) h2d_staged(c, d_apply, apply.data(), n);  // (the dedup is in with the headers)
-      }
-      for (; checked <= q; ++checked) {
-        const uint64_t a = cut[checked], b = cut[checked + 1];
-        hll_import_launch(c, d_data, d_off + a, d_ids + a, nullptr, (uint32_t)(b - a), h->d_regs, h->d_card,
-                          d_canon + a, d_err, (uint32_t)a);
-        if (early) {
-          hll_rows_bak_launch(c, false, h->d_regs, h->d_card, d_ids + a, d_apply + a, (uint32_t)(b - a),
-                              d_bak + a * (uint64_t)HLL_REGS, d_bak_card + a, d_err);
-          hll_import_launch(c, d_data, d_off + a, d_ids + a, d_apply + a, (uint32_t)(b - a), h->d_regs, h->d_card,
-                            d_canon + a, d_err, (uint32_t)a);
+        if (early && xi) {
+          xi->put(d_apply, apply.data(), n);  // (the dedup is in with the headers)
+          apply_mark = xi->issued();
+        } else if (early) {
+          h2d_staged(c, d_apply, apply.data(), n);
         }
       }
+      if (xi) {
+        if (q == 0) continue;
+        xi->wait_upto(std::max(in_mark[q - 1], apply_mark));  // chunk q - 1 (and the dedup flags) in
+      }
+      for (; checked < (xi ? q : q + 1); ++checked) launch_chunk(checked);
+    }
+    if (xi) {  // the last chunk
+      xi->wait_upto(std::max(in_mark[NCH - 1], apply_mark));
+      for (; checked < NCH; ++checked) launch_chunk(checked);
+      xi.reset();  // (every piece is in: the stages are free for the HIP copies below)
     }
     const auto t1 = now();
     if (early) {  // a failed check anywhere: every replaced row back as it was
@@ -2500,10 +2598,20 @@ int rsk_bloom_import_bits(rsk_bloom* b, const uint8_t* buf, size_t len) {
     need(len <= b->nbytes, "bit string longer than the filter");
     need(buf != nullptr || len == 0, "buf is NULL");
     CtxLock l(b->ctx);
-    RSK_HIP(hipMemsetAsync(b->d_bits, 0, b->nwords * 4, b->ctx->stream));
-    if (len >= (64ull << 20)) h2d_staged(b->ctx, reinterpret_cast<uint8_t*>(b->d_bits), buf, len);  // (pinned stages)
-    else if (len) RSK_HIP(hipMemcpyAsync(b->d_bits, buf, len, hipMemcpyHostToDevice, b->ctx->stream));
-    RSK_HIP(hipStreamSynchronize(b->ctx->stream));
+    rsk_ctx* c = b->ctx;
+    RSK_HIP(hipMemsetAsync(b->d_bits, 0, b->nwords * 4, c->stream));
+    const int ein = len >= (64ull << 20) ? copy_engine(c, false) : -1;
+    if (ein >= 0) {  // a large string: on the measured SDMA engine through the pinned stages
+      RSK_HIP(hipStreamSynchronize(c->stream));  // (the zeroing first)
+      H2DStream xi(c, ein, 16ull << 20);
+      xi.put(reinterpret_cast<uint8_t*>(b->d_bits), buf, len);
+      xi.wait_upto(xi.issued());
+    } else if (len >= (64ull << 20)) {
+      h2d_staged(c, reinterpret_cast<uint8_t*>(b->d_bits), buf, len);
+    } else if (len) {
+      RSK_HIP(hipMemcpyAsync(b->d_bits, buf, len, hipMemcpyHostToDevice, c->stream));
+    }
+    RSK_HIP(hipStreamSynchronize(c->stream));
     ++b->wgen;  // SET of the whole string: its views take STRLEN = len
     ++b->rgen;
     b->set_len = len;

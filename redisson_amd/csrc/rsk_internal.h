@@ -74,8 +74,8 @@ struct Tuning {
   int io_drain = 0;          // batched export: 1 = each chunk's copy-out drained before the next chunk (A/B)
   int copy_nt = 0;           // staged host copies: 0 streaming stores, -1 memcpy (A/B)
   int io_pin = 0;            // batched export: a pageable output buffer >= 256 MiB pinned for the call (0), never (-1)
-  int io_engine = 0;         // batched export's device->host copies: 0 the fastest SDMA engine (measured once per
-                             // context), -1 HIP's copies (A/B), k > 0 SDMA engine k - 1
+  int io_engine = 0;         // batched export / import (and large Bloom GET / SET) copies: 0 the fastest SDMA engine
+                             // per direction (measured once per context), -1 HIP's copies (A/B), k > 0 engine k - 1
   int gpart_rt = 0;          // hll_gpart2t's round: 0 8192 records, 1 16384 (A/B)
   int gapply_st = 0;         // hll_gapply's row stores: 0 nontemporal, 1 plain (A/B), 2 none (TIMING ONLY)
   int gpart_tm = 1;          // its first pass tile-major (hll_gpart1t, no count pass): 1 yes, 0 no
@@ -244,12 +244,12 @@ struct rsk_ctx {
     return nullptr;
   }
   bool host_registered(const void* p, uint64_t bytes) const { return host_reg(p, bytes) != nullptr; }
-  // The batched export's device->host copies go to one SDMA engine, the fastest of those
-  // measured once per context (round 6: the engine the runtime picks for device->host moved
-  // 26-30 GB/s on some boxes, 57 on others and on the engines beside it):
-  // -2 not measured yet, -1 HIP's copies, else the engine's index; d2h_rate: GB/s measured
-  int d2h_engine = -2;
-  float d2h_rate[8] = {};
+  // The batched export's device->host copies (and the batched import's host->device ones) go
+  // to one SDMA engine per direction, the fastest of those measured once per context (round 6:
+  // the engine the runtime picks moved 26-30 GB/s on some boxes, 57 on others and on the engines
+  // beside it): -2 not measured yet, -1 HIP's copies, else the engine's index; *_rate: GB/s measured
+  int d2h_engine = -2, h2d_engine = -2;
+  float d2h_rate[8] = {}, h2d_rate[8] = {};
   hsa_agent_t gpu_agent{}, cpu_agent{};
   hsa_signal_t eng_sig[8] = {};
 

@@ -556,7 +556,9 @@ def test_export_on_every_copy_engine_gives_the_same_bytes(L, engine, orc, route)
     measurement (route io_engine = 0), on each engine forced (io_engine = k:
     engine k - 1), and on HIP's copies (-1) give the same strings, staged
     through the pinned ring (io_pin = -1), into a buffer the call pins, and
-    into a caller-registered buffer; the measured engine is the fastest."""
+    into a caller-registered buffer; the batched import's host->device copies
+    on each of the same choices (and straight from a registered buffer) give
+    the same registers; the measured engine is the fastest each way."""
     from redisson_amd import _lib
 
     rng = np.random.default_rng(31)
@@ -583,6 +585,19 @@ def test_export_on_every_copy_engine_gives_the_same_bytes(L, engine, orc, route)
             route(io_engine=k, io_pin=pin)
             rc, out, offs = _export_batch(L, h, ids, cap=None if pin else 256 << 20)
             assert rc == 0 and np.array_equal(out[: want.size], want), (k, pin)
+    # the import's host->device copies: measured engine, each engine forced, HIP's copies
+    ein, irates = engine.copy_engine(to_host=False)
+    assert ein >= 0 and irates[ein] == max(irates) > 0, (ein, irates)
+    for k in [0, -1] + [e + 1 for e in range(8) if irates[e] > 0]:
+        route(io_engine=k)
+        h2 = _pool(L, engine, G)
+        assert _import_batch(L, h2, ids, strs) == 0, k
+        route(io_engine=-1)
+        rc, out, offs = _export_batch(L, h2, ids)
+        assert rc == 0 and np.array_equal(out[: want.size], want), k
+        for i in (0, 1, G // 2, G - 1):
+            assert np.array_equal(_regs(L, h2, i), rows[pick[i]]), (k, i)
+        L.rsk_hll_destroy(h2)
     route(io_engine=0, io_pin=0)
     reg = np.zeros(want.size + 8192, np.uint8)
     engine.host_register(reg)
@@ -591,6 +606,12 @@ def test_export_on_every_copy_engine_gives_the_same_bytes(L, engine, orc, route)
         uids = ids.astype(np.uint64)
         _lib.check(L.rsk_hll_export_redis_batch(h, uids.ctypes.data, G, reg.ctypes.data, reg.size, offs.ctypes.data))
         assert int(offs[-1]) == want.size and np.array_equal(reg[: want.size], want)
+        # and SET straight from the registered buffer (the engine reads it at its device address)
+        h3 = _pool(L, engine, G)
+        _lib.check(L.rsk_hll_import_redis_batch(h3, uids.ctypes.data, G, reg.ctypes.data, offs.ctypes.data))
+        for i in (0, 1, G // 2, G - 1):
+            assert np.array_equal(_regs(L, h3, i), rows[pick[i]]), i
+        L.rsk_hll_destroy(h3)
     finally:
         engine.host_unregister(reg)
     L.rsk_hll_destroy(h)
