@@ -733,6 +733,91 @@ void for_each_chunk(rsk_ctx* c, const rsk_keys* k, F&& fn) {
   uint64_t first = 0;
   int slot = 0;
   bool recorded[2] = {false, false};  // earlier calls ended with a stream sync
+  // A large batch (>= 64 MiB) goes up on the SDMA engine measured fastest (copy_engine): chunk
+  // k's copies are issued, then chunk k - 1's work is launched once its copies are in (so the
+  // engine moves chunk k while the host launches k - 1); pin_ev[slot], recorded behind a chunk's
+  // work, frees its stage for chunk k + 2.
+  const uint64_t total = k->offsets ? k->offsets[k->n] - k->offsets[0] + 8 * (k->n + 1) : k->n * k->fixed_len;
+  const int eng = pinned && total >= (64ull << 20) ? copy_engine(c, false) : -1;
+  if (eng >= 0) {
+    RSK_HIP(hipStreamSynchronize(c->stream));  // (no earlier work may still use a device stage)
+    struct Chunk {
+      bool on = false;
+      int slot = 0;
+      uint64_t first = 0, m = 0, base = 0;
+      bool copies[2] = {false, false};  // data, offsets: their signals are eng_sig[2 * slot + i]
+    } pend;
+    struct WaitCopies {  // unwound by an error: no engine copy may still write a stage
+      rsk_ctx* c;
+      Chunk* p;
+      Chunk* q;
+      ~WaitCopies() {
+        for (Chunk* x : {p, q})
+          for (int i = 0; i < 2; ++i)
+            if (x->on && x->copies[i]) (void)engine_wait(c->eng_sig[2 * x->slot + i]);
+      }
+    };
+    Chunk cur;
+    WaitCopies wc{c, &pend, &cur};
+    auto issue = [&](int sl, int i, uint64_t at, const void* from, uint64_t bytes) {
+      if (!bytes) return;
+      par_copy(c->h_pin[sl] + at, reinterpret_cast<const uint8_t*>(from), bytes, c->stage_threads);
+      cur.copies[i] = true;
+      if (!engine_copy(c, eng, c->eng_sig[2 * sl + i], dbuf[sl] + at, c->h_pin[sl] + at, bytes, false)) {
+        cur.copies[i] = false;
+        fail(RSK_ERR_DEVICE, "host->device copy on SDMA engine " + std::to_string(eng) + " refused");
+      }
+    };
+    auto launch = [&](Chunk& ch) {  // its copies in, then its work on the context stream
+      for (int i = 0; i < 2; ++i)
+        if (ch.copies[i]) {
+          ch.copies[i] = false;
+          if (engine_wait(c->eng_sig[2 * ch.slot + i]) < 0) fail(RSK_ERR_DEVICE, "host->device copy on an SDMA engine failed");
+        }
+      uint8_t* d_data = dbuf[ch.slot];
+      if (k->offsets == nullptr) {
+        fn(DevKeys{d_data, nullptr, ch.m, k->fixed_len}, ch.first, ch.m);
+      } else {
+        fn(DevKeys{d_data - ch.base, reinterpret_cast<uint64_t*>(d_data + c->stage_bytes), ch.m, 0}, ch.first, ch.m);
+      }
+      RSK_HIP(hipEventRecord(c->pin_ev[ch.slot], c->stream));
+      recorded[ch.slot] = true;
+      ch.on = false;
+    };
+    while (first < k->n) {
+      if (recorded[slot]) RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));  // chunk k - 2's work is done with it
+      cur = Chunk{};
+      cur.on = true;
+      cur.slot = slot;
+      cur.first = first;
+      if (k->offsets == nullptr) {
+        uint64_t m = k->fixed_len ? c->stage_bytes / k->fixed_len : k->n;
+        m = std::min<uint64_t>(m, k->n - first);
+        need(m > 0, "key longer than the staging buffer");
+        cur.m = m;
+        issue(slot, 0, 0, src + first * k->fixed_len, m * k->fixed_len);
+      } else {
+        const uint64_t base = k->offsets[first];
+        const uint64_t lim = std::min<uint64_t>(k->n - first, off_cap);
+        const uint64_t* o = k->offsets + first;
+        const uint64_t m = (uint64_t)(std::upper_bound(o + 1, o + lim + 1, base + c->stage_bytes) - (o + 1));
+        need(m > 0, "key longer than the staging buffer");
+        need(k->offsets[first + m] >= base, "offsets must be non-decreasing");
+        cur.m = m;
+        cur.base = base;
+        issue(slot, 1, c->stage_bytes, k->offsets + first, (m + 1) * 8);
+        issue(slot, 0, 0, src + base, k->offsets[first + m] - base);
+      }
+      if (pend.on) launch(pend);
+      pend = cur;
+      cur.on = false;
+      first += pend.m;
+      slot ^= 1;
+    }
+    if (pend.on) launch(pend);
+    RSK_HIP(hipStreamSynchronize(c->stream));
+    return;
+  }
   while (first < k->n) {
     // The pinned stage is free once the DMA that last read it has finished.
     if (pinned && recorded[slot]) RSK_HIP(hipEventSynchronize(c->pin_ev[slot]));

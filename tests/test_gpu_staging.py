@@ -2,7 +2,8 @@
 pinned stages (par_copy by host threads while the other stage's DMA runs)
 must give the same registers / bits / replies as the oracle and as one-chunk
 batches.  A 32 MiB stage makes every batch here 3-6 chunks, each copied by
-several threads."""
+several threads; batches of 64 MiB or more go up on the SDMA engine measured
+fastest (route io_engine = 0) or on HIP's copies (-1), both run."""
 import ctypes
 
 import numpy as np
@@ -22,12 +23,19 @@ def L():
 
 
 @pytest.fixture(scope="module")
-def small_engine():
+def small_engine_ctx():
     from redisson_amd import _lib
 
     e = _lib.Engine(0, staging_bytes=STAGE)
     yield e
     e.close()
+
+
+@pytest.fixture(params=[0, -1], ids=["engine", "hip"])
+def small_engine(request, small_engine_ctx):
+    small_engine_ctx.set_route("io_engine", request.param)
+    yield small_engine_ctx
+    small_engine_ctx.set_route("reset", 0)
 
 
 def _regs_after_add(L, engine, kb):
