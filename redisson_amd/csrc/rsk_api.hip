@@ -132,6 +132,7 @@ static uint8_t* grow_dev(hipStream_t stream, uint8_t*& p, uint64_t& have, uint64
 uint8_t* rsk_ctx::xbuf(uint64_t bytes) { return grow_dev(stream, d_xbuf, xbuf_bytes, bytes); }
 uint8_t* rsk_ctx::sbuf(uint64_t bytes) { return grow_dev(stream, d_sbuf, sbuf_bytes, bytes); }
 uint8_t* rsk_ctx::hrows(uint64_t bytes) { return grow_dev(stream, d_hrows, hrows_bytes, bytes); }
+uint8_t* rsk_ctx::cslow(uint64_t bytes) { return grow_dev(stream, d_cslow, cslow_bytes, bytes); }
 
 uint8_t* rsk_ctx::pinned(uint64_t bytes) {
   // every call that fills this buffer waits for its DMA before returning
@@ -1243,6 +1244,7 @@ int rsk_shutdown(rsk_ctx* c) {
     (void)hipFree(c->d_xbuf);
     (void)hipFree(c->d_sbuf);
     (void)hipFree(c->d_hrows);
+    (void)hipFree(c->d_cslow);
     (void)hipFree(c->d_lc);
     for (rsk::AsyncOp* op : c->async_all) {  // stream and completion queue drained: every op is idle
       if (op->h_buf) (void)hipHostFree(op->h_buf);
@@ -1309,8 +1311,9 @@ int rsk_trim(rsk_ctx* c) {
     RSK_HIP(hipFree(c->d_xbuf));
     RSK_HIP(hipFree(c->d_sbuf));
     RSK_HIP(hipFree(c->d_hrows));
-    c->d_work = c->d_out = c->d_xbuf = c->d_sbuf = c->d_hrows = nullptr;
-    c->work_bytes = c->out_bytes = c->xbuf_bytes = c->sbuf_bytes = c->hrows_bytes = 0;
+    RSK_HIP(hipFree(c->d_cslow));
+    c->d_work = c->d_out = c->d_xbuf = c->d_sbuf = c->d_hrows = c->d_cslow = nullptr;
+    c->work_bytes = c->out_bytes = c->xbuf_bytes = c->sbuf_bytes = c->hrows_bytes = c->cslow_bytes = 0;
     if (c->h_batch) RSK_HIP(hipHostFree(c->h_batch));
     c->h_batch = nullptr;
     c->h_batch_bytes = 0;

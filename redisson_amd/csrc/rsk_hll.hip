@@ -289,9 +289,86 @@ __global__ __launch_bounds__(256) void hll_count_kernel(const uint8_t* __restric
   }
 }
 
+// Large counts (a pool's 10^6 sketches after a grouped add): a sketch per lane answers from
+// the card cache or the add's precomputed estimate and lists the others (wave-aggregated
+// append); then a wave per listed sketch, as hll_count_kernel.  One wave per sketch for the
+// whole batch spent ~0.2 ms dispatching 10^6 waves that each read three words.
+__global__ __launch_bounds__(256) void hll_count_fast_kernel(uint64_t* __restrict__ card, const uint64_t* __restrict__ ids,
+                                                             SmallIds small, uint64_t n, uint64_t* __restrict__ out,
+                                                             PCount pc, uint32_t* __restrict__ slow_n,
+                                                             uint32_t* __restrict__ slow) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t w = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); w < n; w += (uint64_t)gridDim.x * 256) {
+    const uint64_t b = w + lane;
+    bool rest = false;
+    if (b < n) {
+      const uint64_t id = ids ? ids[b] : (small.n ? small.v[b] : b);
+      const uint64_t cached = card[id];
+      if ((cached >> 63) == 0) {  // HLL_VALID_CACHE
+        out[b] = cached;
+      } else if (pc.pcount && pc.pepoch[id] == pc.epoch) {
+        const uint64_t est = pc.pcount[id];
+        out[b] = est;
+        card[id] = est;
+      } else {
+        rest = true;
+      }
+    }
+    const uint64_t m = __ballot(rest);
+    if (m) {
+      const int leader = __ffsll((long long)m) - 1;
+      uint32_t at = 0;
+      if ((int)lane == leader) at = atomicAdd(slow_n, (uint32_t)__popcll(m));
+      at = __shfl(at, leader);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (rest) slow[at + below] = (uint32_t)b;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void hll_count_slow_kernel(const uint8_t* __restrict__ regs, uint64_t* __restrict__ card,
+                                                             const uint64_t* __restrict__ ids, SmallIds small,
+                                                             const uint32_t* __restrict__ slow_n,
+                                                             const uint32_t* __restrict__ slow,
+                                                             const double* __restrict__ lc, uint64_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4, cnt = *slow_n;
+  for (uint64_t s = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; s < cnt; s += nwaves) {
+    const uint64_t b = slow[s];
+    const uint64_t id = ids ? ids[b] : (small.n ? small.v[b] : b);
+    const uint8_t* r = regs + id * HLL_REGS;
+    const uint4* r4 = reinterpret_cast<const uint4*>(r) + lane;
+    uint4 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = r4[64 * q];
+    const SumD sm = wave_sum(v);
+    if (lane == 0) {
+      int ez = (int)sm.ez;
+      const double E = exact_total(sm) ? sm.t : dense_order_sum(r, &ez);
+      const uint64_t est = hll_estimate(E, ez, lc);
+      out[b] = est;
+      card[id] = est;
+    }
+  }
+}
+
 void hll_count_launch(rsk_ctx* c, const uint8_t* d_regs, uint64_t* d_card, const uint64_t* d_ids,
                       const SmallIds& small, uint64_t n, uint64_t* d_out, PCount pc) {
   if (n == 0) return;
+  if (n >= 4096 && n < (1ull << 32)) {
+    ProfScope ps(c, "hll_count");
+    uint32_t* slow = reinterpret_cast<uint32_t*>(c->cslow(4 * (n + 64)));  // [0]: count; the list from [64]
+    RSK_HIP(hipMemsetAsync(slow, 0, 4, c->stream));
+    const uint64_t g1 = std::min<uint64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(hll_count_fast_kernel, dim3((uint32_t)g1), dim3(256), 0, c->stream, d_card, d_ids, small, n,
+                       d_out, pc, slow, slow + 64);
+    RSK_CHECK_LAUNCH("hll_count_fast");
+    const uint64_t g2 = std::min<uint64_t>((n + 3) / 4, (uint64_t)c->num_cus * 16);
+    hipLaunchKernelGGL(hll_count_slow_kernel, dim3((uint32_t)g2), dim3(256), 0, c->stream, d_regs, d_card, d_ids, small,
+                       slow, slow + 64, c->d_lc, d_out);
+    RSK_CHECK_LAUNCH("hll_count_slow");
+    return;
+  }
   uint64_t grid = (n + 3) / 4;  // 4 waves (sketches) per workgroup
   if (grid > (1u << 20)) grid = 1u << 20;
   ProfScope ps(c, "hll_count");

@@ -226,6 +226,9 @@ struct rsk_ctx {
   uint64_t sbuf_bytes = 0;
   uint8_t* d_hrows = nullptr;
   uint64_t hrows_bytes = 0;
+  // large PFCOUNT batches: the list of sketches the cache / precomputed estimate does not answer
+  uint8_t* d_cslow = nullptr;
+  uint64_t cslow_bytes = 0;
 
   uint8_t* work(uint64_t bytes);
   uint8_t* pinned(uint64_t bytes);
@@ -256,6 +259,7 @@ struct rsk_ctx {
   uint8_t* xbuf(uint64_t bytes);
   uint8_t* sbuf(uint64_t bytes);
   uint8_t* hrows(uint64_t bytes);
+  uint8_t* cslow(uint64_t bytes);
 };
 
 struct rsk_hll {

@@ -887,3 +887,50 @@ def test_c5_full_size_every_sketch_bit_exact(L, engine, orc, zipf):
     assert [int(c) for c in cnt] == [orc.hll_count_dense(ref[i]) for i in sample]
     L.rsk_hll_destroy(h)
     _lib.check(L.rsk_trim(engine.ctx))
+
+
+def test_large_count_mixes_cache_precomputed_and_recomputed(L, engine, orc, route):
+    """A PFCOUNT batch of >= 4096 ids takes the two-phase count (a lane per
+    sketch answers from the card cache or the grouped add's precomputed
+    estimate and lists the rest, then a wave per listed sketch): on a pool
+    holding all three states -- cached by an earlier count, stamped by the
+    partitioned add, invalidated by a merge, a raw register write and a
+    per-key add -- and with duplicate ids, it equals the one-wave-per-sketch
+    count (batches under 4096) on an identical pool and the oracle's count of
+    the registers."""
+    from redisson_amd import KeyBatch, devmem
+    from redisson_amd.hyperloglog import GroupedHyperLogLog
+
+    route(gpart=1)
+    G, n = 20000, 4_000_000
+    rng = np.random.default_rng(41)
+    regs = rng.integers(0, 9, 16384).astype(np.uint8)
+    extra = orc.gen_keys16(SEED_C2 + 77, 0, 3000).reshape(3000, 16)
+    pools = []
+    for _ in range(2):
+        g, k = devmem.gen_grouped(engine, 0x5EED0041, G, 0, n)
+        p = GroupedHyperLogLog(engine, G)
+        p.add(k.keys_fixed(n, 16), g)
+        g.free()
+        k.free()
+        p.count(np.arange(0, 1000, dtype=np.uint64))  # cached
+        p.mergeWith(np.arange(1000, 2000, dtype=np.uint64), np.arange(5000, 6000, dtype=np.uint64))
+        _lib_merge_raw(L, p.pool, 2500, regs)
+        _add(L, p.pool, KeyBatch.from_numpy(extra), 3000)
+        pools.append(p)
+    ids = np.concatenate([np.arange(G, dtype=np.uint64), np.array([7, 1500, 2500, 3000, 19999], np.uint64)])
+    every = pools[0].count().copy()  # (no id list: the whole pool, two-phase)
+    big = pools[0].count(ids)  # (now from the cache, duplicates included)
+    small = np.concatenate([pools[1].count(ids[i:i + 4000]) for i in range(0, ids.size, 4000)])
+    assert np.array_equal(every, small[:G])
+    assert np.array_equal(big, small)
+    for gid in (0, 999, 1000, 1999, 2500, 3000, 5000, 19999):
+        assert int(big[gid]) == orc.hll_count_dense(pools[0].registers(gid)), gid
+    for p in pools:
+        p.close()
+
+
+def _lib_merge_raw(L, h, i, regs):
+    from redisson_amd import _lib
+
+    _lib.check(L.rsk_hll_merge_raw(h, i, regs.ctypes.data, _lib.RSK_MEM_HOST))
