@@ -2107,7 +2107,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     // two packed stages: chunk k + 1 packs into one while chunk k's strings leave the other
     uint8_t* d_stage[2] = {d_slots + al(kc * (uint64_t)RSK_HLL_DENSE_BYTES),
                            d_slots + 2 * al(kc * (uint64_t)RSK_HLL_DENSE_BYTES)};
-    std::vector<uint32_t> len(nd);
+    std::unique_ptr<uint32_t[]> len(new uint32_t[nd ? nd : 1]);  // (every chunk's lengths copied in before use)
     // the chunk's ids, flags, lengths and string offsets live in pinned memory, moved by small
     // kernels on the context stream (xfer): a pageable copy would hold the host until the stream
     // reaches it, and a DMA would queue behind the bulk copy-out on the copy engine
@@ -2178,7 +2178,7 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
       auto t0 = now();
       if (c->tune.io_drain) RSK_HIP(hipEventSynchronize(lens));  // (A/B: route io_drain)
       else xo.service_until(lens);  // chunk d0's lengths (and the previous pack) done; copy-outs meanwhile
-      std::memcpy(len.data() + d0, h_len, 4 * m);
+      std::memcpy(len.get() + d0, h_len, 4 * m);
       auto t1 = now();
       t_sync += ms(t0, t1);
       dcur = advance(dev_i[d0 + m - 1] + 1, dcur);
@@ -2218,8 +2218,10 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     if (o > cap) fail(RSK_ERR_INVALID_ARG, "output buffer smaller than the strings (offsets[n] holds the bytes needed)");
     need(out != nullptr || o == 0, "out is NULL");
     // promoted for good (hllSparseSet -> hllSparseToDense), as the per-key GET
-    for (uint64_t d = 0; d < nd; ++d)
-      if (want[d] && !(len[d] >> 31)) h->dense[dev_id[d]] = 1;
+    par_for(nd, std::max(1u, c->stage_threads), [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t d = lo; d < hi; ++d)
+        if (want[d] && !(len[d] >> 31)) h->dense[dev_id[d]] = 1;  // (a repeated id: the same byte, the same 1)
+    });
     // kept SET strings: their bytes, card bytes as PFCOUNT last left them (rare: copied one by one)
     for (uint64_t i = 0; i < (any_imp ? n : 0); ++i) {
       const uint64_t id = ids[i];

@@ -213,7 +213,8 @@ class GroupedHyperLogLog:
         a missing key).  `out` (a uint8 array) is used when large enough;
         otherwise the call is repeated with an exact buffer."""
         ids = np.arange(self.n, dtype=np.uint64) if ids is None else np.ascontiguousarray(ids, dtype=np.uint64)
-        offs = np.zeros(ids.size + 1, dtype=np.uint64)
+        offs = np.empty(ids.size + 1, dtype=np.uint64)  # (every entry written by a call that succeeds or
+        offs[-1] = 0                                    # overflows; offs[-1] read only then)
         L = _lib.load()
         if out is None or out.dtype != np.uint8 or not out.flags.c_contiguous:
             out = np.empty(0, np.uint8)
