@@ -2361,10 +2361,25 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     uint8_t* d_canon = d_apply + al(n);
     auto* d_err = reinterpret_cast<unsigned long long*>(d_canon + al(n));
     uint8_t* d_data = d_canon + al(n) + 256;
-    std::vector<uint64_t> off(n + 1);
-    for (uint64_t i = 0; i <= n; ++i) off[i] = offsets[i] - base;
-    h2d_staged(c, reinterpret_cast<uint8_t*>(d_ids), reinterpret_cast<const uint8_t*>(ids), 8 * n);
-    h2d_staged(c, reinterpret_cast<uint8_t*>(d_off), reinterpret_cast<const uint8_t*>(off.data()), 8 * (n + 1));
+    std::unique_ptr<uint64_t[]> off(new uint64_t[n + 1]);
+    par_for(n + 1, nth, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) off[i] = offsets[i] - base;
+    });
+    // On an SDMA engine (the fastest measured, copy_engine) the ids, offsets and strings go up as
+    // engine copies through the pinned ring, and chunk q's check is launched once its pieces are
+    // in, after chunk q + 1's first pieces are on their way (so the engine is not idle while the
+    // host launches it); otherwise HIP's copies, the strings on the input copy stream.
+    const int ein = copy_engine(c, false);
+    std::unique_ptr<H2DStream> xi;
+    if (ein >= 0) {
+      RSK_HIP(hipStreamSynchronize(c->stream));  // the device work queued before (it may use this scratch) is done
+      xi.reset(new H2DStream(c, ein, 16ull << 20));
+      xi->put(reinterpret_cast<uint8_t*>(d_ids), reinterpret_cast<const uint8_t*>(ids), 8 * n);
+      xi->put(reinterpret_cast<uint8_t*>(d_off), reinterpret_cast<const uint8_t*>(off.get()), 8 * (n + 1));
+    } else {
+      h2d_staged(c, reinterpret_cast<uint8_t*>(d_ids), reinterpret_cast<const uint8_t*>(ids), 8 * n);
+      h2d_staged(c, reinterpret_cast<uint8_t*>(d_off), reinterpret_cast<const uint8_t*>(off.get()), 8 * (n + 1));
+    }
     RSK_HIP(hipMemsetAsync(d_err, 0xFF, 8, c->stream));
     RSK_HIP(hipMemsetAsync(d_canon, 1, n, c->stream));
     // The strings in 8 chunks of about equal bytes, each checked on the device as soon as it is
@@ -2391,9 +2406,6 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     const auto t0 = now();
     uint64_t checked = 0;  // chunks [0, checked) have their check queued
     bool hdr_ok = false;
-    // On an SDMA engine (the fastest measured, copy_engine) the strings go up as engine copies
-    // instead, and chunk q's check is launched once its pieces are in, after chunk q + 1's first
-    // pieces are on their way (so the engine is not idle while the host launches it).
     auto launch_chunk = [&](uint64_t qq) {  // chunk qq's check (and, early, its rows aside and its decode)
       const uint64_t a = cut[qq], b = cut[qq + 1];
       hll_import_launch(c, d_data, d_off + a, d_ids + a, nullptr, (uint32_t)(b - a), h->d_regs, h->d_card,
@@ -2405,12 +2417,6 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
                           d_canon + a, d_err, (uint32_t)a);
       }
     };
-    const int ein = copy_engine(c, false);
-    std::unique_ptr<H2DStream> xi;
-    if (ein >= 0) {
-      RSK_HIP(hipEventSynchronize(up));  // the device work queued before (it may use this scratch) is done
-      xi.reset(new H2DStream(c, ein, 16ull << 20));
-    }
     uint64_t in_mark[NCH] = {}, apply_mark = 0;  // xi->issued() after each chunk / after d_apply
     for (uint64_t q = 0; q < NCH; ++q) {
       const uint64_t i0 = cut[q], i1 = cut[q + 1];
