@@ -495,6 +495,41 @@ int copy_engine(rsk_ctx* c, bool to_host) {
 }
 int export_engine(rsk_ctx* c) { return copy_engine(c, true); }
 
+// A large pageable host buffer (>= 256 MiB: a checkpoint's strings) pinned in place for one call
+// (hipHostRegister, a few ms for 2 GB) so the call's copies go to / from it by DMA instead of
+// through the pinned stages and a host copy, which is bound by the box's host memory (round 6:
+// the C5 export 80-85 ms staged against 44-48 registered on such a box); unpinned when the call
+// ends.  Not possible (pinned by someone else, too little lockable memory, route io_pin = -1):
+// the staged copies.
+struct CallPin {
+  rsk_ctx* c = nullptr;
+  void* p = nullptr;
+  void pin(rsk_ctx* cc, const void* ptr, uint64_t bytes) {
+    if (!ptr || bytes < (256ull << 20) || cc->tune.io_pin < 0 || cc->host_registered(ptr, bytes)) return;
+    void* q = const_cast<void*>(ptr);  // (registering does not write the range)
+    if (hipHostRegister(q, bytes, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    c = cc;
+    p = q;
+    c->host_regs.push_back({reinterpret_cast<uintptr_t>(q), bytes, reg_dptr(q)});
+  }
+  ~CallPin() {
+    if (!p) return;
+    (void)hipStreamSynchronize(c->xin);  // no DMA may still use it
+    (void)hipStreamSynchronize(c->xout);
+    (void)hipStreamSynchronize(c->stream);
+    auto& v = c->host_regs;
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].base == reinterpret_cast<uintptr_t>(p)) {
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+    (void)hipHostUnregister(p);
+  }
+};
+
 // Pageable (or registered) host -> device on SDMA engine `engine` through the two pinned stages:
 // a ring of NS slots of S bytes, a host copy into each slot while the engine moves the previous
 // one, each piece's completion a signal; a registered range is copied straight from (no slot).
@@ -2017,37 +2052,11 @@ int rsk_hll_export_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, uint
     rsk_ctx* c = h->ctx;
     CtxLock l(c);
     rsk::hll_materialize(h);  // a pending lazy clear: GET reads zero registers (export writes none)
-    // A large pageable output buffer is pinned in place for the call (hipHostRegister: ~4 ms
-    // for 2 GB) so the strings go to it by DMA, not through the stages and a host copy, which
-    // is bound by the box's host memory (round 6: 80-85 ms staged against 44-48 registered for
-    // the C5 pool's 2.12 GB on such a box).  Not possible (already pinned by someone else,
-    // too little lockable memory): the staged copy-out.
-    struct TempReg {
-      rsk_ctx* c = nullptr;
-      void* p = nullptr;
-      ~TempReg() {
-        if (!p) return;
-        (void)hipStreamSynchronize(c->xout);  // no DMA may still target it
-        (void)hipStreamSynchronize(c->stream);
-        auto& v = c->host_regs;
-        for (size_t i = 0; i < v.size(); ++i)
-          if (v[i].base == reinterpret_cast<uintptr_t>(p)) {
-            v.erase(v.begin() + (long)i);
-            break;
-          }
-        (void)hipHostUnregister(p);
-      }
-    } treg;
+    // A large pageable output buffer is pinned in place for the call (CallPin) so the strings
+    // go to it by DMA, not through the stages and a host copy.
     const auto tR = std::chrono::steady_clock::now();
-    if (out && cap >= (256ull << 20) && c->tune.io_pin >= 0 && !c->host_registered(out, cap)) {
-      if (hipHostRegister(out, cap, hipHostRegisterDefault) == hipSuccess) {
-        treg.c = c;
-        treg.p = out;
-        c->host_regs.push_back({reinterpret_cast<uintptr_t>(out), cap, rsk::reg_dptr(out)});
-      } else {
-        (void)hipGetLastError();
-      }
-    }
+    CallPin treg;
+    treg.pin(c, out, cap);
     const auto tG = std::chrono::steady_clock::now();
     const int eng = export_engine(c);  // (before any of this call's work is queued)
     const auto tI0 = std::chrono::steady_clock::now();
@@ -2361,6 +2370,8 @@ int rsk_hll_import_redis_batch(rsk_hll* h, const uint64_t* ids, uint64_t n, cons
     uint8_t* d_canon = d_apply + al(n);
     auto* d_err = reinterpret_cast<unsigned long long*>(d_canon + al(n));
     uint8_t* d_data = d_canon + al(n) + 256;
+    CallPin in_pin;  // the strings DMA'd straight from the caller's buffer (>= 256 MiB)
+    in_pin.pin(c, data + base, total);
     std::unique_ptr<uint64_t[]> off(new uint64_t[n + 1]);
     par_for(n + 1, nth, [&](uint64_t lo, uint64_t hi) {
       for (uint64_t i = lo; i < hi; ++i) off[i] = offsets[i] - base;

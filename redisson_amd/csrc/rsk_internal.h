@@ -73,7 +73,7 @@ struct Tuning {
   int io_piece = 0;          // batched export's copy-out pieces, MiB (0: 16)
   int io_drain = 0;          // batched export: 1 = each chunk's copy-out drained before the next chunk (A/B)
   int copy_nt = 0;           // staged host copies: 0 streaming stores, -1 memcpy (A/B)
-  int io_pin = 0;            // batched export: a pageable output buffer >= 256 MiB pinned for the call (0), never (-1)
+  int io_pin = 0;            // batched export / import: a pageable buffer >= 256 MiB pinned for the call (0), never (-1)
   int io_engine = 0;         // batched export / import (and large Bloom GET / SET) copies: 0 the fastest SDMA engine
                              // per direction (measured once per context), -1 HIP's copies (A/B), k > 0 engine k - 1
   int gpart_rt = 0;          // hll_gpart2t's round: 0 8192 records, 1 16384 (A/B)
